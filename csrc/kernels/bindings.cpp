@@ -1,0 +1,114 @@
+// pybind11 launcher table for the HIP kernels (module llm_consensus_amd._lib._llmc_hip).
+//
+// Every entry takes raw device pointers (uintptr_t from torch.Tensor.data_ptr()) and the HIP
+// stream handle (torch.cuda.current_stream().cuda_stream), launches asynchronously and raises
+// on a launch error. No torch headers: the module builds in seconds and is graph-capturable
+// (launches land on whatever stream torch is capturing).
+#include <hip/hip_runtime_api.h>
+#include <pybind11/pybind11.h>
+
+#include <stdexcept>
+#include <string>
+
+namespace py = pybind11;
+typedef uintptr_t ptr;
+
+extern "C" {
+int llmc_rmsnorm(const void*, const void*, void*, int, int, int, int, float, hipStream_t);
+int llmc_embedding(const void*, const void*, void*, int, int, int, hipStream_t);
+int llmc_silu_mul_interleaved(const void*, void*, int, int, hipStream_t);
+int llmc_gemv(int, const void*, int, const void*, float, const void*, void*, int, int, int, int, hipStream_t);
+int llmc_gemm(const void*, int, const void*, int, void*, int, int, int, int, int, hipStream_t);
+int llmc_rope_kv_write(void*, int, const void*, const void*, const void*, void*, void*, const void*, int, int, int,
+                       int, int, hipStream_t);
+int llmc_attn_decode(const void*, int, const void*, const void*, const void*, int, const void*, void*, void*, void*,
+                     int, int, int, int, int, int, int, int, float, hipStream_t);
+int llmc_attn_prefill(const void*, int, const void*, const void*, const void*, int, const void*, const void*,
+                      const void*, void*, int, int, int, int, int, int, int, float, hipStream_t);
+int llmc_sample(const void*, int64_t, int, int, const void*, const void*, const void*, const void*, const void*, void*,
+                void*, void*, void*, void*, void*, const void*, int, int, void*, void*, int, int, hipStream_t);
+int llmc_sample_parts();
+int llmc_moe_route(const void*, int, int, int, void*, void*, hipStream_t);
+int llmc_moe_align(const void*, int, int, int, int, void*, void*, void*, void*, hipStream_t);
+int llmc_moe_gemm(const void*, int, const void*, const void*, const void*, const void*, void*, int, int, int, int, int,
+                  int, hipStream_t);
+int llmc_moe_combine(const void*, const void*, const void*, void*, int, int, int, hipStream_t);
+int llmc_moe_gemv(int, const void*, int, const void*, float, const void*, const void*, int, void*, int, int, int, int,
+                  hipStream_t);
+}
+
+static inline void check(int rc, const char* what) {
+  if (rc != 0) {
+    std::string msg = std::string("llmc HIP launch failed: ") + what + " rc=" + std::to_string(rc);
+    if (rc > 0) msg += std::string(" (") + hipGetErrorString(static_cast<hipError_t>(rc)) + ")";
+    throw std::runtime_error(msg);
+  }
+}
+#define P(x) reinterpret_cast<void*>(x)
+#define S(x) reinterpret_cast<hipStream_t>(x)
+
+PYBIND11_MODULE(_llmc_hip, m) {
+  m.doc() = "llm_consensus_amd gfx950 HIP kernels (raw-pointer launchers)";
+  m.def("rmsnorm", [](ptr x, ptr w, ptr y, int T, int H, int xs, int ys, float eps, ptr s) {
+    check(llmc_rmsnorm(P(x), P(w), P(y), T, H, xs, ys, eps, S(s)), "rmsnorm");
+  });
+  m.def("embedding", [](ptr ids, ptr table, ptr out, int T, int H, int V, ptr s) {
+    check(llmc_embedding(P(ids), P(table), P(out), T, H, V, S(s)), "embedding");
+  });
+  m.def("silu_mul_interleaved", [](ptr gu, ptr y, int T, int I, ptr s) {
+    check(llmc_silu_mul_interleaved(P(gu), P(y), T, I, S(s)), "silu_mul");
+  });
+  m.def("gemv", [](int M, ptr x, int xs, ptr nw, float eps, ptr W, ptr out, int os, int N, int K, int epi, ptr s) {
+    check(llmc_gemv(M, P(x), xs, P(nw), eps, P(W), P(out), os, N, K, epi, S(s)), "gemv");
+  });
+  m.def("gemm", [](ptr A, int lda, ptr W, int ldw, ptr C, int ldc, int M, int N, int K, int epi, ptr s) {
+    check(llmc_gemm(P(A), lda, P(W), ldw, P(C), ldc, M, N, K, epi, S(s)), "gemm");
+  });
+  m.def("rope_kv_write", [](ptr qkv, int qs, ptr pos, ptr cos_t, ptr sin_t, ptr kc, ptr vc, ptr slots, int T, int nh,
+                            int nkv, int D, int bs, ptr s) {
+    check(llmc_rope_kv_write(P(qkv), qs, P(pos), P(cos_t), P(sin_t), P(kc), P(vc), P(slots), T, nh, nkv, D, bs, S(s)),
+          "rope_kv_write");
+  });
+  m.def("attn_decode", [](ptr q, int qs, ptr kc, ptr vc, ptr bt, int bts, ptr sl, ptr po, ptr pml, ptr out, int os,
+                          int B, int nh, int nkv, int D, int bs, int chunk, int max_chunks, float scale, ptr s) {
+    check(llmc_attn_decode(P(q), qs, P(kc), P(vc), P(bt), bts, P(sl), P(po), P(pml), P(out), os, B, nh, nkv, D, bs,
+                           chunk, max_chunks, scale, S(s)),
+          "attn_decode");
+  });
+  m.def("attn_prefill", [](ptr q, int qs, ptr kc, ptr vc, ptr bt, int bts, ptr qst, ptr ql, ptr cl, ptr out, int os,
+                           int B, int max_qlen, int nh, int nkv, int D, int bs, float scale, ptr s) {
+    check(llmc_attn_prefill(P(q), qs, P(kc), P(vc), P(bt), bts, P(qst), P(ql), P(cl), P(out), os, B, max_qlen, nh, nkv,
+                            D, bs, scale, S(s)),
+          "attn_prefill");
+  });
+  m.def("sample", [](ptr logits, int64_t rs, int B, int V, ptr it, ptr tk, ptr tp, ptr seeds, ptr pos, ptr wv, ptr wi,
+                     ptr next, ptr tin, ptr sl, ptr slots, ptr bt, int bts, int bs, ptr ot, ptr oc, int cap,
+                     int use_topkp, ptr s) {
+    check(llmc_sample(P(logits), rs, B, V, P(it), P(tk), P(tp), P(seeds), P(pos), P(wv), P(wi), P(next), P(tin), P(sl),
+                      P(slots), P(bt), bts, bs, P(ot), P(oc), cap, use_topkp, S(s)),
+          "sample");
+  });
+  m.def("sample_parts", []() { return llmc_sample_parts(); });
+  m.def("moe_route", [](ptr logits, int T, int E, int k, ptr w, ptr ids, ptr s) {
+    check(llmc_moe_route(P(logits), T, E, k, P(w), P(ids), S(s)), "moe_route");
+  });
+  m.def("moe_align", [](ptr ids, int T, int k, int E, int tile, ptr sorted_rows, ptr tile_expert, ptr tile_count,
+                        ptr counts, ptr s) {
+    check(llmc_moe_align(P(ids), T, k, E, tile, P(sorted_rows), P(tile_expert), P(tile_count), P(counts), S(s)),
+          "moe_align");
+  });
+  m.def("moe_gemm", [](ptr A, int lda, ptr W, ptr sorted_rows, ptr tile_expert, ptr tile_count, ptr C, int ldc,
+                       int N, int K, int max_tiles, int a_row_div, int epi, ptr s) {
+    check(llmc_moe_gemm(P(A), lda, P(W), P(sorted_rows), P(tile_expert), P(tile_count), P(C), ldc, N, K, max_tiles,
+                        a_row_div, epi, S(s)),
+          "moe_gemm");
+  });
+  m.def("moe_combine", [](ptr y, ptr w, ptr ids, ptr out, int T, int k, int H, ptr s) {
+    check(llmc_moe_combine(P(y), P(w), P(ids), P(out), T, k, H, S(s)), "moe_combine");
+  });
+  m.def("moe_gemv", [](int k, ptr x, int xs, ptr nw, float eps, ptr W, ptr ids, int ids_stride, ptr out, int os,
+                       int N, int K, int epi, ptr s) {
+    check(llmc_moe_gemv(k, P(x), xs, P(nw), eps, P(W), P(ids), ids_stride, P(out), os, N, K, epi, S(s)), "moe_gemv");
+  });
+  m.def("device_synchronize", []() { check(static_cast<int>(hipDeviceSynchronize()), "hipDeviceSynchronize"); });
+}

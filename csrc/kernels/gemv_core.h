@@ -1,0 +1,176 @@
+// K6 (decode class): skinny GEMM  y[m, n] = sum_k x[m, k] * W[n, k]   for M = 1..4 rows.
+//
+// Batch-1 decode is HBM-bound weight streaming (8B = 15 GB/token), so this is
+// THE hot kernel. Design (cdna_hip_programming.md §5 row "GEMV / M <= 16"; MI355X_MICROARCH
+// rows nt-weights, launches-baseline):
+//  * W [N, K] bf16, K contiguous. A wave owns RPW output rows; lane l streams chunks
+//    c = l + 64 i (16 B = 8 bf16 each) of all RPW rows -> RPW*UNROLL independent 16 B loads in
+//    flight per lane, straight to VGPRs (no LDS round trip for W), non-temporal (read once).
+//  * x is staged ONCE per block in LDS (M*K bf16); every lane reads the same chunk index it
+//    loads from W, so ds_read_b128 addresses are lane-consecutive (conflict-free).
+//  * v_dot2_f32_bf16 does convert+multiply+accumulate of 2 elements per VALU op.
+//  * Fused prologue  PRO_NORM: x <- bf16(rmsnorm(x) * w_norm)  (the layer's input norm), so the
+//    decode layer needs no separate norm launch.
+//  * Fused epilogues: bf16 store | f32 store (logits) | in-place residual add h += W.x |
+//    SiLU-mul over interleaved gate/up rows (row 2i = gate_i, 2i+1 = up_i).
+#pragma once
+#include "common.h"
+
+namespace llmc {
+
+enum { PRO_NONE = 0, PRO_NORM = 1 };
+enum { EPI_BF16 = 0, EPI_F32 = 1, EPI_RESADD = 2, EPI_SILU = 3 };
+
+constexpr int kGemvThreads = 256;
+constexpr int kGemvWaves = kGemvThreads / kWave;
+
+template <int M, int RPW, int UNROLL, int PRO, int EPI, bool EXPERT = false>
+__global__ __launch_bounds__(kGemvThreads) void gemv_kernel(const bf16_t* __restrict__ x, int x_stride,
+                                                            const bf16_t* __restrict__ norm_w, float eps,
+                                                            const bf16_t* __restrict__ W, void* __restrict__ out,
+                                                            int out_stride, int N, int K,
+                                                            const int32_t* __restrict__ expert_ids = nullptr,
+                                                            int x_div = 1) {
+  // EXPERT (MoE decode): blockIdx.y = (token, slot) pair; weights of expert expert_ids[pair],
+  // input row pair / x_div, output row pair (M must be 1).
+  if constexpr (EXPERT) {
+    const int pair = blockIdx.y;
+    W += static_cast<int64_t>(expert_ids[pair]) * N * K;
+    x += static_cast<int64_t>(pair / x_div) * x_stride;
+    out = reinterpret_cast<char*>(out) + static_cast<int64_t>(pair) * out_stride * (EPI == EPI_F32 ? 4 : 2);
+  }
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  bf16_t* xs = reinterpret_cast<bf16_t*>(smem);  // [M][K]
+  const int tid = threadIdx.x;
+  const int nchunk = K / 8;
+
+  // ---- prologue: x -> LDS (optionally RMS-normalised) ----
+  if constexpr (PRO == PRO_NORM) {
+    float(*red)[kGemvWaves] = reinterpret_cast<float(*)[kGemvWaves]>(smem + static_cast<size_t>(M) * K * sizeof(bf16_t));
+    float ss[M];
+#pragma unroll
+    for (int m = 0; m < M; ++m) ss[m] = 0.f;
+    for (int c = tid; c < nchunk; c += kGemvThreads) {
+#pragma unroll
+      for (int m = 0; m < M; ++m) {
+        float f[8];
+        unpack8(reinterpret_cast<const u32x4*>(x + static_cast<int64_t>(m) * x_stride)[c], f);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) ss[m] += f[j] * f[j];
+      }
+    }
+#pragma unroll
+    for (int m = 0; m < M; ++m) {
+      const float s = wave_sum(ss[m]);
+      if ((tid & 63) == 0) red[m][tid / 64] = s;
+    }
+    __syncthreads();
+    float inv[M];
+#pragma unroll
+    for (int m = 0; m < M; ++m) {
+      float t = 0.f;
+#pragma unroll
+      for (int w = 0; w < kGemvWaves; ++w) t += red[m][w];
+      inv[m] = rsqrtf(t / K + eps);
+    }
+    for (int c = tid; c < nchunk; c += kGemvThreads) {
+      float g[8];
+      unpack8(reinterpret_cast<const u32x4*>(norm_w)[c], g);
+#pragma unroll
+      for (int m = 0; m < M; ++m) {
+        float f[8];
+        unpack8(reinterpret_cast<const u32x4*>(x + static_cast<int64_t>(m) * x_stride)[c], f);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) f[j] = f[j] * inv[m] * g[j];
+        reinterpret_cast<u32x4*>(xs + m * K)[c] = pack8(f);
+      }
+    }
+  } else {
+    for (int c = tid; c < nchunk; c += kGemvThreads) {
+#pragma unroll
+      for (int m = 0; m < M; ++m)
+        reinterpret_cast<u32x4*>(xs + m * K)[c] =
+            reinterpret_cast<const u32x4*>(x + static_cast<int64_t>(m) * x_stride)[c];
+    }
+  }
+  __syncthreads();
+
+  // ---- main loop: stream RPW weight rows per wave ----
+  const int wave = tid / kWave, lane = tid % kWave;
+  const int row0 = (blockIdx.x * kGemvWaves + wave) * RPW;
+  if (row0 >= N) return;
+  const u32x4* wrow[RPW];
+#pragma unroll
+  for (int r = 0; r < RPW; ++r) {
+    const int n = min(row0 + r, N - 1);
+    wrow[r] = reinterpret_cast<const u32x4*>(W + static_cast<int64_t>(n) * K);
+  }
+  float acc[RPW][M];
+#pragma unroll
+  for (int r = 0; r < RPW; ++r)
+#pragma unroll
+    for (int m = 0; m < M; ++m) acc[r][m] = 0.f;
+
+  const u32x4* xv = reinterpret_cast<const u32x4*>(xs);
+  const int full = nchunk / (kWave * UNROLL);  // iterations with every lane in range
+  int c0 = lane;
+  for (int it = 0; it < full; ++it, c0 += kWave * UNROLL) {
+    u32x4 wv[RPW][UNROLL];
+#pragma unroll
+    for (int u = 0; u < UNROLL; ++u)
+#pragma unroll
+      for (int r = 0; r < RPW; ++r) wv[r][u] = load16<true>(wrow[r] + c0 + u * kWave);
+#pragma unroll
+    for (int u = 0; u < UNROLL; ++u) {
+#pragma unroll
+      for (int m = 0; m < M; ++m) {
+        const u32x4 xx = xv[m * nchunk + c0 + u * kWave];
+#pragma unroll
+        for (int r = 0; r < RPW; ++r) acc[r][m] = dot8_bf16(wv[r][u], xx, acc[r][m]);
+      }
+    }
+  }
+  // tail (K not a multiple of 64*8*UNROLL)
+  for (int c = c0; c < nchunk; c += kWave) {
+    u32x4 wv[RPW];
+#pragma unroll
+    for (int r = 0; r < RPW; ++r) wv[r] = load16<true>(wrow[r] + c);
+#pragma unroll
+    for (int m = 0; m < M; ++m) {
+      const u32x4 xx = xv[m * nchunk + c];
+#pragma unroll
+      for (int r = 0; r < RPW; ++r) acc[r][m] = dot8_bf16(wv[r], xx, acc[r][m]);
+    }
+  }
+
+#pragma unroll
+  for (int r = 0; r < RPW; ++r)
+#pragma unroll
+    for (int m = 0; m < M; ++m) acc[r][m] = wave_sum(acc[r][m]);
+
+  // ---- epilogue: lane (r*M + m) stores one value ----
+#pragma unroll
+  for (int r = 0; r < RPW; ++r) {
+#pragma unroll
+    for (int m = 0; m < M; ++m) {
+      const int n = row0 + r;
+      if (lane != r * M + m || n >= N) continue;
+      const float v = acc[r][m];
+      if constexpr (EPI == EPI_BF16) {
+        reinterpret_cast<bf16_t*>(out)[static_cast<int64_t>(m) * out_stride + n] = f32_to_bf16(v);
+      } else if constexpr (EPI == EPI_F32) {
+        reinterpret_cast<float*>(out)[static_cast<int64_t>(m) * out_stride + n] = v;
+      } else if constexpr (EPI == EPI_RESADD) {
+        bf16_t* h = reinterpret_cast<bf16_t*>(out) + static_cast<int64_t>(m) * out_stride + n;
+        *h = f32_to_bf16(bf16_to_f32(*h) + v);
+      } else {  // EPI_SILU: rows (2j, 2j+1) = (gate, up) -> output column n/2
+        if ((r & 1) == 0) {
+          reinterpret_cast<bf16_t*>(out)[static_cast<int64_t>(m) * out_stride + n / 2] =
+              f32_to_bf16(silu(v) * acc[r + 1][m]);
+        }
+      }
+    }
+  }
+}
+
+}  // namespace llmc

@@ -1,0 +1,141 @@
+// K9 router top-k, K10 permute/align, K12 combine for Mixtral-style MoE.
+// The expert GEMMs themselves are K11: gemm_kernel<.., GATHER> (prefill) and
+// gemv_kernel<.., EXPERT> (decode) — same MFMA / weight-streaming cores as the dense layers.
+//
+// Data flow (prefill, T tokens, top-k):
+//   router logits [T, E] f32 --moe_route--> w [T, k] f32, ids [T, k] i32
+//   ids --moe_align--> sorted_rows [cap] (pair index t*k+j grouped by expert, each expert padded
+//                      to 128-row tiles, -1 = pad), tile_expert [max_tiles], tile_count [1]
+//   x [T, H] --gemm<GATHER>(a_row_div = k)--> gu [T*k, 2I] --silu_mul--> act [T*k, I]
+//   act --gemm<GATHER>(a_row_div = 1)--> y [T*k, H] --moe_combine--> h[t] += sum_j w[t,j] y[t*k+j]
+// The combine is a fixed-order sum in f32 (no float atomics: bitwise reproducible,
+// MI355X_MICROARCH.md "Global float atomics" pitfall).
+#include "common.h"
+
+namespace llmc {
+
+// one thread per token; E <= 64, k <= 8. Mixtral: softmax over all experts, top-k, renormalise.
+__global__ void moe_route_kernel(const float* __restrict__ logits, int T, int E, int k, float* __restrict__ w,
+                                 int32_t* __restrict__ ids) {
+  const int t = blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= T) return;
+  const float* l = logits + static_cast<int64_t>(t) * E;
+  float mx = -INFINITY;
+  for (int e = 0; e < E; ++e) mx = fmaxf(mx, l[e]);
+  float z = 0.f;
+  for (int e = 0; e < E; ++e) z += __expf(l[e] - mx);
+  uint64_t taken = 0;
+  float sel[8];
+  float ssum = 0.f;
+  for (int j = 0; j < k; ++j) {
+    int best = -1;
+    float bv = -INFINITY;
+    for (int e = 0; e < E; ++e) {
+      if ((taken >> e) & 1ull) continue;
+      if (l[e] > bv) {
+        bv = l[e];
+        best = e;
+      }
+    }
+    taken |= 1ull << best;
+    sel[j] = __expf(bv - mx) / z;
+    ssum += sel[j];
+    ids[static_cast<int64_t>(t) * k + j] = best;
+  }
+  for (int j = 0; j < k; ++j) w[static_cast<int64_t>(t) * k + j] = sel[j] / ssum;
+}
+
+constexpr int kAlignThreads = 1024;
+constexpr int kMoeTile = 128;
+
+__global__ __launch_bounds__(kAlignThreads) void moe_align_kernel(const int32_t* __restrict__ ids, int npairs, int E,
+                                                                  int cap, int max_tiles,
+                                                                  int32_t* __restrict__ sorted_rows,
+                                                                  int32_t* __restrict__ tile_expert,
+                                                                  int32_t* __restrict__ tile_count,
+                                                                  int32_t* __restrict__ counts_out) {
+  __shared__ int cnt[64];
+  __shared__ int off[65];
+  __shared__ int cur[64];
+  for (int e = threadIdx.x; e < E; e += kAlignThreads) {
+    cnt[e] = 0;
+    cur[e] = 0;
+  }
+  for (int i = threadIdx.x; i < cap; i += kAlignThreads) sorted_rows[i] = -1;
+  __syncthreads();
+  for (int i = threadIdx.x; i < npairs; i += kAlignThreads) atomicAdd(&cnt[ids[i]], 1);
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    int o = 0;
+    for (int e = 0; e < E; ++e) {
+      off[e] = o;
+      const int nt = (cnt[e] + kMoeTile - 1) / kMoeTile;
+      for (int tt = 0; tt < nt; ++tt) tile_expert[o / kMoeTile + tt] = e;
+      o += nt * kMoeTile;
+      if (counts_out) counts_out[e] = cnt[e];
+    }
+    off[E] = o;
+    tile_count[0] = o / kMoeTile;
+    for (int tt = o / kMoeTile; tt < max_tiles; ++tt) tile_expert[tt] = 0;
+  }
+  __syncthreads();
+  for (int i = threadIdx.x; i < npairs; i += kAlignThreads) {
+    const int e = ids[i];
+    const int pos = off[e] + atomicAdd(&cur[e], 1);
+    sorted_rows[pos] = i;
+  }
+}
+
+// h[t] (bf16, in place) += sum_j w[t, j] * y[t*k + j]
+__global__ __launch_bounds__(256) void moe_combine_kernel(const bf16_t* __restrict__ y, const float* __restrict__ w,
+                                                          bf16_t* __restrict__ h, int k, int H) {
+  const int t = blockIdx.x;
+  for (int c = threadIdx.x; c < H / 8; c += 256) {
+    float acc[8];
+    unpack8(reinterpret_cast<const u32x4*>(h + static_cast<int64_t>(t) * H)[c], acc);
+    float s[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    for (int j = 0; j < k; ++j) {
+      const float wj = w[static_cast<int64_t>(t) * k + j];
+      float f[8];
+      unpack8(reinterpret_cast<const u32x4*>(y + (static_cast<int64_t>(t) * k + j) * H)[c], f);
+#pragma unroll
+      for (int q = 0; q < 8; ++q) s[q] += wj * f[q];
+    }
+#pragma unroll
+    for (int q = 0; q < 8; ++q) acc[q] += s[q];
+    reinterpret_cast<u32x4*>(h + static_cast<int64_t>(t) * H)[c] = pack8(acc);
+  }
+}
+
+}  // namespace llmc
+
+using namespace llmc;
+
+extern "C" {
+
+int llmc_moe_route(const void* logits, int T, int E, int k, void* w, void* ids, hipStream_t s) {
+  if (E > 64 || k > 8 || k > E) return -1;
+  moe_route_kernel<<<(T + 255) / 256, 256, 0, s>>>((const float*)logits, T, E, k, (float*)w, (int32_t*)ids);
+  return static_cast<int>(hipGetLastError());
+}
+
+// tile must be 128 (the grouped GEMM's M tile); max_tiles = ceil(npairs/128) + E
+int llmc_moe_align(const void* ids, int T, int k, int E, int tile, void* sorted_rows, void* tile_expert,
+                   void* tile_count, void* counts, hipStream_t s) {
+  if (tile != kMoeTile || E > 64) return -1;
+  const int npairs = T * k;
+  const int max_tiles = (npairs + kMoeTile - 1) / kMoeTile + E;
+  moe_align_kernel<<<1, kAlignThreads, 0, s>>>((const int32_t*)ids, npairs, E, max_tiles * kMoeTile, max_tiles,
+                                               (int32_t*)sorted_rows, (int32_t*)tile_expert, (int32_t*)tile_count,
+                                               (int32_t*)counts);
+  return static_cast<int>(hipGetLastError());
+}
+
+int llmc_moe_combine(const void* y, const void* w, const void* ids, void* h, int T, int k, int H, hipStream_t s) {
+  (void)ids;
+  if (H % 8 != 0) return -1;
+  moe_combine_kernel<<<T, 256, 0, s>>>((const bf16_t*)y, (const float*)w, (bf16_t*)h, k, H);
+  return static_cast<int>(hipGetLastError());
+}
+
+}  // extern "C"

@@ -1,0 +1,346 @@
+"""``llm-consensus`` entry point (reference composition root ``cmd/llm-consensus/main.go:76-438``).
+
+Flow, strings, output routing and exit codes match the reference:
+parse flags → prompt (args > --file > piped stdin) → registry bootstrap (every ``--models``
+entry and the judge must resolve, main.go:395-415) → fan-out → judge → persist/print.
+"Providers" are local engines on the node's GPUs (``provider/local.py``) or the CPU stub.
+
+Extra engine flags (no reference counterpart): ``--max-tokens``,
+``--temperature``, ``--top-p``, ``--top-k``, ``--seed``, ``--gpus``, ``--trace``,
+``--list-models``.
+"""
+
+from __future__ import annotations
+
+import dataclasses
+import os
+import secrets
+import signal
+import stat
+import sys
+import time
+from typing import List, Optional, TextIO
+
+from . import ui
+from .catalog import PROVIDER_STUB, UnknownModel, dump_catalog, resolve
+from .consensus import Judge
+from .context import Context
+from .flags import FlagSet, parse_or_exit
+from .output import Result, encode_result
+from .provider.base import Request
+from .provider.registry import Registry
+from .runner import Callbacks, Runner
+from .utils.gostr import trim_space
+from .version import commit, date, get_version
+
+DEFAULT_JUDGE = "llama-3-8b@judge"
+PROG = "llm-consensus"
+
+
+class CLIError(Exception):
+    pass
+
+
+@dataclasses.dataclass
+class Config:
+    models: List[str]
+    judge: str
+    file: str
+    output: str
+    data_dir: str
+    timeout: float
+    prompt: str
+    quiet: bool
+    json: bool
+    no_save: bool
+    max_tokens: int
+    temperature: float
+    top_p: float
+    top_k: int
+    seed: int
+    gpus: str
+    trace: bool
+
+
+def make_flagset() -> FlagSet:
+    fs = FlagSet(PROG)
+    fs.add("models", "string", "", "Comma-separated list of models to query (required)")
+    fs.add("judge", "string", DEFAULT_JUDGE, "Model to use for consensus synthesis")
+    fs.add("file", "string", "", "Read prompt from file")
+    fs.add("output", "string", "", "Write JSON output to specific file (overrides auto-save)")
+    fs.add("data-dir", "string", "data", "Directory for auto-saved runs")
+    fs.add("timeout", "int", 120, "Per-model timeout in seconds")
+    fs.add("quiet", "bool", False, "Suppress progress output")
+    fs.add("q", "bool", False, "Suppress progress output (shorthand)", dest="quiet")
+    fs.add("json", "bool", False, "Output JSON to stdout (no interactive display, no auto-save)")
+    fs.add("no-save", "bool", False, "Don't auto-save results to data directory")
+    fs.add("version", "bool", False, "Print version information and exit")
+    # engine flags
+    fs.add("max-tokens", "int", 0, "Max generated tokens per model (0 = engine default: 4096 local, 24 stub)")
+    fs.add("temperature", "float", 1.0, "Sampling temperature (0 = greedy)")
+    fs.add("top-p", "float", 1.0, "Nucleus sampling mass")
+    fs.add("top-k", "int", 0, "Top-k sampling (0 = off)")
+    fs.add("seed", "int", 0, "Sampling seed (0 = derived from the model name)")
+    fs.add("gpus", "string", "", "Comma-separated GPU ids to place models on (default: all visible)")
+    fs.add("trace", "bool", False, "Write a Chrome trace of engine spans to the run directory")
+    fs.add("list-models", "bool", False, "Print the local model catalog as JSON and exit")
+    return fs
+
+
+def _stdin_is_pipe(stdin) -> bool:
+    try:
+        return not stat.S_ISCHR(os.fstat(stdin.fileno()).st_mode)
+    except Exception:  # noqa: BLE001
+        return False
+
+
+def get_prompt(args: List[str], file: str, stdin=None) -> str:
+    """main.go:363-393."""
+    if args:
+        return " ".join(args)
+    if file:
+        try:
+            with open(file, "rb") as f:
+                data = f.read()
+        except OSError as e:
+            raise CLIError(f"reading prompt file: {_go_path_err('open', file, e)}") from None
+        return trim_space(data.decode("utf-8", "surrogateescape"))
+    stdin = sys.stdin if stdin is None else stdin
+    if _stdin_is_pipe(stdin):
+        raw = stdin.buffer.read() if hasattr(stdin, "buffer") else stdin.read().encode()
+        lines = raw.split(b"\n")
+        if lines and lines[-1] == b"":
+            lines.pop()
+        out = []
+        for ln in lines:
+            if ln.endswith(b"\r"):  # bufio.ScanLines drops a trailing \r
+                ln = ln[:-1]
+            if len(ln) > 64 * 1024:
+                raise CLIError("reading stdin: bufio.Scanner: token too long")
+            out.append(ln.decode("utf-8", "surrogateescape"))
+        return "\n".join(out)
+    raise CLIError("no prompt provided: use positional argument, --file, or pipe to stdin")
+
+
+def _go_path_err(op: str, path: str, e: OSError) -> str:
+    msg = {2: "no such file or directory", 13: "permission denied", 21: "is a directory"}.get(e.errno, e.strerror or str(e))
+    return f"{op} {path}: {msg}"
+
+
+def parse_flags(argv: List[str], stdout: TextIO = sys.stdout, stderr: TextIO = sys.stderr, stdin=None) -> Config:
+    fs = make_flagset()
+    v, rest = parse_or_exit(fs, argv, stderr)
+    if v["list_models"]:
+        stdout.write(dump_catalog())
+        raise SystemExit(0)
+    if v["version"]:
+        stdout.write(f"llm-consensus {get_version()}\n  commit: {commit}\n  built:  {date}\n")
+        stdout.flush()
+        raise SystemExit(0)
+    if v["models"] == "":
+        raise CLIError("--models flag is required")
+    models = [trim_space(m) for m in v["models"].split(",")]
+    cfg = Config(models=models, judge=v["judge"], file=v["file"], output=v["output"], data_dir=v["data_dir"],
+                 timeout=float(v["timeout"]), prompt="", quiet=v["quiet"], json=v["json"], no_save=v["no_save"],
+                 max_tokens=v["max_tokens"], temperature=v["temperature"], top_p=v["top_p"], top_k=v["top_k"],
+                 seed=v["seed"], gpus=v["gpus"], trace=v["trace"])
+    cfg.prompt = get_prompt(rest, cfg.file, stdin)
+    return cfg
+
+
+def init_registry(cfg: Config) -> Registry:
+    """main.go:395-438: every model in --models plus the judge must resolve before any query."""
+    needed: List[str] = []
+    for m in cfg.models + [cfg.judge]:
+        if m not in needed:
+            needed.append(m)
+    reg = Registry()
+    local_specs = []
+    for m in needed:
+        try:
+            spec = resolve(m)
+        except UnknownModel as e:
+            raise CLIError(f"initializing provider for {m}: {e}") from None
+        if spec.provider == PROVIDER_STUB:
+            from .provider.stub import StubProvider
+
+            reg.register(m, StubProvider(m))
+        else:
+            local_specs.append(spec)
+    if local_specs:
+        from .provider.local import LocalBackend
+
+        gpus = [int(x) for x in cfg.gpus.split(",") if x.strip()] if cfg.gpus else None
+        try:
+            backend = LocalBackend(local_specs, judge=cfg.judge, gpus=gpus, trace=cfg.trace)
+        except Exception as e:  # noqa: BLE001
+            raise CLIError(f"initializing provider for {local_specs[0].name}: {e}") from None
+        for spec in local_specs:
+            reg.register(spec.name, backend.provider(spec.name))
+    return reg
+
+
+def generate_run_id() -> str:
+    """main.go:278-285: local time YYYYMMDD-HHMMSS + '-' + 3 random bytes hex."""
+    return time.strftime("%Y%m%d-%H%M%S", time.localtime()) + "-" + secrets.token_hex(3)
+
+
+def run(argv: List[str], stdout: TextIO = sys.stdout, stderr: TextIO = sys.stderr, stdin=None,
+        root_ctx: Optional[Context] = None) -> None:
+    cfg = parse_flags(argv, stdout, stderr, stdin)
+    ctx = root_ctx or Context.background()
+    show_ui = ui.is_terminal(stderr) and not cfg.quiet and not cfg.json
+    start = time.monotonic()
+
+    registry = init_registry(cfg)
+    try:
+        _run_with_registry(cfg, registry, ctx, show_ui, start, stdout, stderr)
+    finally:
+        registry.close()
+
+
+def _request_template(cfg: Config) -> Request:
+    return Request(model="", prompt="", max_tokens=cfg.max_tokens or None, temperature=cfg.temperature,
+                   top_p=cfg.top_p, top_k=cfg.top_k or None, seed=cfg.seed or None)
+
+
+def _run_with_registry(cfg: Config, registry: Registry, ctx: Context, show_ui: bool, start: float,
+                       stdout: TextIO, stderr: TextIO) -> None:
+    if show_ui:
+        ui.print_header(stderr, cfg.prompt)
+        ui.print_phase(stderr, "Querying models...")
+        ui._write(stderr, "\n")
+
+    progress = ui.Progress(stderr, cfg.models, not show_ui)
+    progress.start()
+    tmpl = _request_template(cfg)
+    runner = Runner(registry, cfg.timeout, tmpl).with_callbacks(Callbacks(
+        on_model_start=progress.model_started,
+        on_model_stream=progress.model_streaming,
+        on_model_complete=progress.model_completed,
+        on_model_error=progress.model_failed,
+    ))
+    try:
+        result = runner.run(ctx, cfg.models, cfg.prompt)
+    except Exception as e:  # noqa: BLE001
+        progress.stop()
+        raise CLIError(f"running queries: {e}") from None
+    progress.stop()
+
+    if show_ui:
+        ui.print_success(stderr, f"Received responses from {len(result.responses)} models")
+        ui._write(stderr, "\n")
+        ui.print_phase(stderr, "Synthesizing consensus...")
+        ui._write(stderr, "\n")
+
+    try:
+        judge_provider = registry.get(cfg.judge)
+    except Exception as e:  # noqa: BLE001
+        raise CLIError(f"judge model {cfg.judge}: {e}") from None
+    judge = Judge(judge_provider, cfg.judge, tmpl)
+    jprog = ui.Progress(stderr, [cfg.judge], not show_ui)
+    jprog.start()
+    jprog.model_started(cfg.judge)
+    # The judge gets the per-model timeout too (no hidden 60 s cap).
+    jctx = ctx.with_timeout(cfg.timeout)
+    try:
+        consensus = judge.synthesize_stream(jctx, cfg.prompt, result.responses,
+                                            lambda chunk: jprog.model_streaming(cfg.judge, chunk))
+        err = None
+    except Exception as e:  # noqa: BLE001
+        consensus, err = "", e
+    jprog.model_completed(cfg.judge)
+    jprog.stop()
+    if err is not None:
+        raise CLIError(f"consensus synthesis: {err}")
+
+    if show_ui:
+        ui.print_success(stderr, "Consensus reached!")
+
+    out = Result(prompt=cfg.prompt, responses=result.responses, consensus=consensus, judge=cfg.judge,
+                 warnings=result.warnings, failed_models=result.failed_models)
+
+    output_path = ""
+    run_dir = ""
+    if cfg.output:
+        output_path = cfg.output
+    elif not cfg.json and not cfg.no_save:
+        run_dir = os.path.join(cfg.data_dir, generate_run_id())
+        try:
+            os.makedirs(run_dir, mode=0o755, exist_ok=True)
+        except OSError as e:
+            raise CLIError(f"creating run directory: {_go_path_err('mkdir', run_dir, e)}") from None
+        output_path = os.path.join(run_dir, "result.json")
+        for fname, data, label in (("prompt.txt", cfg.prompt, "prompt"), ("consensus.md", consensus, "consensus")):
+            try:
+                _write_file(os.path.join(run_dir, fname), data.encode("utf-8", "surrogateescape"))
+            except OSError as e:
+                if show_ui:
+                    ui.print_error(stderr, f"Failed to save {label}: {_go_path_err('open', os.path.join(run_dir, fname), e)}")
+        if cfg.trace:
+            from .utils import trace
+
+            trace.dump(os.path.join(run_dir, "trace.json"))
+
+    text = encode_result(out)
+    if output_path:
+        try:
+            f = open(output_path, "wb")
+        except OSError as e:
+            raise CLIError(f"creating output file: {_go_path_err('open', output_path, e)}") from None
+        with f:
+            f.write(text.encode("utf-8", "surrogateescape"))
+        if show_ui:
+            ui._write(stderr, "\n")
+            ui.print_success(stderr, f"Run saved to {os.path.dirname(output_path) or '.'}")
+    elif cfg.json:
+        _emit(stdout, text)
+    elif show_ui:
+        ui._write(stderr, "\n")
+        for r in result.responses:
+            ui.print_model_response(stderr, r.model, r.provider, r.content, r.latency_s)
+        ui.print_consensus(stderr, consensus)
+        ui.print_summary(stderr, len(cfg.models), len(result.responses), len(result.failed_models or []),
+                         time.monotonic() - start)
+        if result.warnings:
+            ui._write(stderr, "\n")
+            for w in result.warnings:
+                ui.print_error(stderr, w)
+    else:
+        _emit(stdout, text)
+
+
+def _write_file(path: str, data: bytes) -> None:
+    fd = os.open(path, os.O_WRONLY | os.O_CREAT | os.O_TRUNC, 0o644)
+    with os.fdopen(fd, "wb") as f:
+        f.write(data)
+
+
+def _emit(stdout: TextIO, text: str) -> None:
+    ui._write(stdout, text)
+
+
+def main(argv: Optional[List[str]] = None) -> int:
+    argv = sys.argv[1:] if argv is None else argv
+    ctx = Context.background()
+
+    def _on_signal(signum, frame):  # main.go:90 signal.NotifyContext(SIGINT, SIGTERM)
+        ctx.cancel()
+
+    for s in (signal.SIGINT, signal.SIGTERM):
+        try:
+            signal.signal(s, _on_signal)
+        except ValueError:  # not in main thread
+            pass
+    try:
+        run(argv, root_ctx=ctx)
+    except CLIError as e:
+        ui._write(sys.stderr, f"error: {e}\n")
+        return 1
+    except SystemExit as e:
+        return int(e.code or 0)
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())

@@ -1,0 +1,245 @@
+"""Op layer: one entry point per kernel.
+
+CUDA (ROCm) tensors → hand-written gfx950 HIP kernels in ``_llmc_hip`` (raises if the module is
+missing: there is no silent PyTorch fallback on the GPU). CPU tensors → ``oracle`` (reference
+semantics; used by CPU tests of model/TP/engine logic). All launches go to torch's current
+stream, so every op is capturable in a HIP graph.
+"""
+
+from __future__ import annotations
+
+from typing import Optional
+
+import torch
+
+from ..utils.native import kernels
+from . import oracle
+
+EPI_BF16, EPI_F32, EPI_RESADD, EPI_SILU = 0, 1, 2, 3
+GEMV_MAX_M = 4
+
+
+def _p(t: Optional[torch.Tensor]) -> int:
+    return 0 if t is None else t.data_ptr()
+
+
+def _s(t: torch.Tensor) -> int:
+    return torch.cuda.current_stream(t.device).cuda_stream
+
+
+def _bf16(t: torch.Tensor, name: str) -> None:
+    if t.dtype != torch.bfloat16:
+        raise TypeError(f"{name}: expected bfloat16, got {t.dtype}")
+
+
+# ---------------------------------------------------------------------------------------------
+def rmsnorm(x: torch.Tensor, w: torch.Tensor, eps: float, out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    if not x.is_cuda:
+        r = oracle.rmsnorm(x, w, eps)
+        return out.copy_(r) if out is not None else r
+    _bf16(x, "rmsnorm.x")
+    H = x.shape[-1]
+    x2 = x.reshape(-1, H)
+    if out is None:
+        out = torch.empty_like(x)
+    kernels().rmsnorm(_p(x2), _p(w), _p(out), x2.shape[0], H, x2.stride(0), out.reshape(-1, H).stride(0), float(eps), _s(x))
+    return out
+
+
+def embedding(ids: torch.Tensor, table: torch.Tensor, out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    if not table.is_cuda:
+        r = oracle.embedding(ids, table)
+        return out.copy_(r) if out is not None else r
+    T = ids.numel()
+    if out is None:
+        out = torch.empty(T, table.shape[1], dtype=table.dtype, device=table.device)
+    kernels().embedding(_p(ids), _p(table), _p(out), T, table.shape[1], table.shape[0], _s(table))
+    return out
+
+
+def silu_mul_interleaved(gu: torch.Tensor, out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    if not gu.is_cuda:
+        r = oracle.silu_mul_interleaved(gu)
+        return out.copy_(r) if out is not None else r
+    T, I2 = gu.shape
+    if out is None:
+        out = torch.empty(T, I2 // 2, dtype=gu.dtype, device=gu.device)
+    kernels().silu_mul_interleaved(_p(gu), _p(out), T, I2 // 2, _s(gu))
+    return out
+
+
+def linear(x: torch.Tensor, W: torch.Tensor, epi: int = EPI_BF16, out: Optional[torch.Tensor] = None,
+           norm_w: Optional[torch.Tensor] = None, eps: float = 1e-5) -> torch.Tensor:
+    """y = (rmsnorm(x)*norm_w if norm_w else x) @ W^T with a fused epilogue.
+
+    M <= 4 rows → weight-streaming GEMV (decode); larger M → MFMA GEMM (prefill; a norm is
+    applied by a separate rmsnorm launch first). EPI_RESADD accumulates into ``out`` in place.
+    """
+    if not x.is_cuda:
+        return oracle.linear(x, W, epi, out, norm_w, eps)
+    _bf16(x, "linear.x")
+    _bf16(W, "linear.W")
+    M, K = x.shape
+    N = W.shape[0]
+    if W.shape[1] != K:
+        raise ValueError(f"linear: x[{M},{K}] vs W{tuple(W.shape)}")
+    if out is None:
+        if epi == EPI_RESADD:
+            raise ValueError("EPI_RESADD needs out")
+        n_out = N // 2 if epi == EPI_SILU else N
+        out = torch.empty(M, n_out, dtype=torch.float32 if epi == EPI_F32 else torch.bfloat16, device=x.device)
+    if M <= GEMV_MAX_M:
+        kernels().gemv(M, _p(x), x.stride(0), _p(norm_w), float(eps), _p(W), _p(out), out.stride(0), N, K, epi, _s(x))
+        return out
+    if norm_w is not None:
+        x = rmsnorm(x, norm_w, eps)
+    if epi == EPI_SILU:
+        gu = torch.empty(M, N, dtype=torch.bfloat16, device=x.device)
+        kernels().gemm(_p(x), x.stride(0), _p(W), W.stride(0), _p(gu), gu.stride(0), M, N, K, EPI_BF16, _s(x))
+        return silu_mul_interleaved(gu, out)
+    kernels().gemm(_p(x), x.stride(0), _p(W), W.stride(0), _p(out), out.stride(0), M, N, K, epi, _s(x))
+    return out
+
+
+def gemm(x: torch.Tensor, W: torch.Tensor, epi: int = EPI_BF16, out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """Always the MFMA GEMM path (for tests / prefill)."""
+    if not x.is_cuda:
+        return oracle.linear(x, W, epi, out)
+    M, K = x.shape
+    N = W.shape[0]
+    if out is None:
+        out = torch.empty(M, N, dtype=torch.float32 if epi == EPI_F32 else torch.bfloat16, device=x.device)
+    kernels().gemm(_p(x), x.stride(0), _p(W), W.stride(0), _p(out), out.stride(0), M, N, K, epi, _s(x))
+    return out
+
+
+def gemv(x: torch.Tensor, W: torch.Tensor, epi: int = EPI_BF16, out: Optional[torch.Tensor] = None,
+         norm_w: Optional[torch.Tensor] = None, eps: float = 1e-5) -> torch.Tensor:
+    """Always the GEMV path (M <= 4)."""
+    if not x.is_cuda:
+        return oracle.linear(x, W, epi, out, norm_w, eps)
+    M, K = x.shape
+    N = W.shape[0]
+    if out is None:
+        n_out = N // 2 if epi == EPI_SILU else N
+        out = torch.empty(M, n_out, dtype=torch.float32 if epi == EPI_F32 else torch.bfloat16, device=x.device)
+    kernels().gemv(M, _p(x), x.stride(0), _p(norm_w), float(eps), _p(W), _p(out), out.stride(0), N, K, epi, _s(x))
+    return out
+
+
+def rope_kv_write(qkv, positions, cos_t, sin_t, k_cache, v_cache, slots, nh, nkv, D, bs) -> None:
+    if not qkv.is_cuda:
+        oracle.rope_kv_write(qkv, positions, cos_t, sin_t, k_cache, v_cache, slots, nh, nkv, D, bs)
+        return
+    T = qkv.shape[0]
+    kernels().rope_kv_write(_p(qkv), qkv.stride(0), _p(positions), _p(cos_t), _p(sin_t), _p(k_cache), _p(v_cache),
+                            _p(slots), T, nh, nkv, D, bs, _s(qkv))
+
+
+def attn_decode(q, k_cache, v_cache, block_tables, seq_lens, out, part_o, part_ml, nh, nkv, D, bs, chunk, scale):
+    if not q.is_cuda:
+        out.copy_(oracle.attn_decode(q, k_cache, v_cache, block_tables, seq_lens, nh, nkv, D, bs, scale))
+        return out
+    B = q.shape[0]
+    max_chunks = part_o.shape[2] if part_o is not None else 1
+    kernels().attn_decode(_p(q), q.stride(0), _p(k_cache), _p(v_cache), _p(block_tables), block_tables.stride(0),
+                          _p(seq_lens), _p(part_o), _p(part_ml), _p(out), out.stride(0), B, nh, nkv, D, bs, chunk,
+                          max_chunks, float(scale), _s(q))
+    return out
+
+
+def attn_prefill(q, k_cache, v_cache, block_tables, q_start, q_lens, ctx_lens, out, max_qlen, nh, nkv, D, bs, scale):
+    if not q.is_cuda:
+        return oracle.attn_prefill(q, k_cache, v_cache, block_tables, q_start, q_lens, ctx_lens, nh, nkv, D, bs,
+                                   scale, out)
+    B = q_lens.shape[0]
+    kernels().attn_prefill(_p(q), q.stride(0), _p(k_cache), _p(v_cache), _p(block_tables), block_tables.stride(0),
+                           _p(q_start), _p(q_lens), _p(ctx_lens), _p(out), out.stride(0), B, int(max_qlen), nh, nkv,
+                           D, bs, float(scale), _s(q))
+    return out
+
+
+def sample_parts() -> int:
+    return kernels().sample_parts()
+
+
+def sample(logits, inv_temp, top_k, top_p, seeds, positions, next_tok, workspace_v=None, workspace_i=None,
+           tokens_in=None, seq_lens=None, slots=None, block_tables=None, bs=0, out_tokens=None, out_count=None,
+           use_topkp: bool = False):
+    """Sample one token per row and (optionally) advance the device decode state in the same launch."""
+    if not logits.is_cuda:
+        tok = oracle.sample(logits, inv_temp, top_k, top_p, seeds, positions)
+        next_tok.copy_(tok)
+        _advance_cpu(tok, tokens_in, positions, seq_lens, slots, block_tables, bs, out_tokens, out_count)
+        return next_tok
+    B, V = logits.shape
+    cap = out_tokens.shape[1] if out_tokens is not None else 0
+    kernels().sample(_p(logits), logits.stride(0), B, V, _p(inv_temp), _p(top_k), _p(top_p), _p(seeds), _p(positions),
+                     _p(workspace_v), _p(workspace_i), _p(next_tok), _p(tokens_in), _p(seq_lens), _p(slots),
+                     _p(block_tables), block_tables.stride(0) if block_tables is not None else 0, bs, _p(out_tokens),
+                     _p(out_count), cap, 1 if use_topkp else 0, _s(logits))
+    return next_tok
+
+
+def _advance_cpu(tok, tokens_in, positions, seq_lens, slots, block_tables, bs, out_tokens, out_count):
+    B = tok.shape[0]
+    for b in range(B):
+        t = int(tok[b])
+        if out_tokens is not None:
+            c = int(out_count[b])
+            if c < out_tokens.shape[1]:
+                out_tokens[b, c] = t
+            out_count[b] = c + 1
+        if tokens_in is not None:
+            tokens_in[b] = t
+        if positions is not None:
+            p = int(positions[b]) + 1
+            positions[b] = p
+            if seq_lens is not None:
+                seq_lens[b] = p + 1
+            if slots is not None and block_tables is not None:
+                slots[b] = int(block_tables[b, p // bs]) * bs + p % bs
+
+
+# -- MoE -----------------------------------------------------------------------------------------
+MOE_TILE = 128
+
+
+def moe_route(logits: torch.Tensor, k: int, w_out: torch.Tensor, ids_out: torch.Tensor):
+    if not logits.is_cuda:
+        w, ids = oracle.moe_route(logits, k)
+        w_out.copy_(w)
+        ids_out.copy_(ids)
+        return w_out, ids_out
+    T, E = logits.shape
+    kernels().moe_route(_p(logits), T, E, k, _p(w_out), _p(ids_out), _s(logits))
+    return w_out, ids_out
+
+
+def moe_max_tiles(npairs: int, E: int) -> int:
+    return (npairs + MOE_TILE - 1) // MOE_TILE + E
+
+
+def moe_align(ids: torch.Tensor, E: int, sorted_rows, tile_expert, tile_count, counts=None):
+    T, k = ids.shape
+    kernels().moe_align(_p(ids), T, k, E, MOE_TILE, _p(sorted_rows), _p(tile_expert), _p(tile_count), _p(counts),
+                        _s(ids))
+
+
+def moe_gemm(A, W_experts, sorted_rows, tile_expert, tile_count, out, N, K, max_tiles, a_row_div, epi=EPI_BF16):
+    kernels().moe_gemm(_p(A), A.stride(0), _p(W_experts), _p(sorted_rows), _p(tile_expert), _p(tile_count), _p(out),
+                       out.stride(0), N, K, max_tiles, a_row_div, epi, _s(A))
+    return out
+
+
+def moe_combine(y, w, ids, h):
+    T, k = w.shape
+    kernels().moe_combine(_p(y), _p(w), _p(ids), _p(h), T, k, h.shape[1], _s(h))
+    return h
+
+
+def moe_gemv(x, W_experts, ids, x_div, out, N, K, epi):
+    npairs = ids.numel()
+    kernels().moe_gemv(npairs, _p(x), x.stride(0), 0, 0.0, _p(W_experts), _p(ids), x_div, _p(out), out.stride(0), N, K,
+                       epi, _s(x))
+    return out

@@ -1,0 +1,217 @@
+"""PyTorch reference semantics of every HIP kernel (test oracles + CPU execution of model logic).
+
+These define the numerics the kernels implement (f32 math, bf16 rounding points). CUDA tensors
+NEVER route here — ``ops/__init__.py`` sends them to the HIP module and raises if it is missing;
+CPU tensors use these so the model / TP / engine logic is testable on the CPU-only runner.
+"""
+
+from __future__ import annotations
+
+import math
+from typing import Optional
+
+import torch
+
+EPI_BF16, EPI_F32, EPI_RESADD, EPI_SILU = 0, 1, 2, 3
+
+
+def rmsnorm(x: torch.Tensor, w: torch.Tensor, eps: float) -> torch.Tensor:
+    xf = x.float()
+    inv = torch.rsqrt(xf.pow(2).mean(-1, keepdim=True) + eps)
+    return (xf * inv * w.float()).to(torch.bfloat16)
+
+
+def embedding(ids: torch.Tensor, table: torch.Tensor) -> torch.Tensor:
+    return table[ids.long().clamp(0, table.shape[0] - 1)]
+
+
+def silu_mul_interleaved(gu: torch.Tensor) -> torch.Tensor:
+    g = gu[..., 0::2].float()
+    u = gu[..., 1::2].float()
+    return (torch.nn.functional.silu(g) * u).to(torch.bfloat16)
+
+
+def linear(x: torch.Tensor, W: torch.Tensor, epi: int, out: Optional[torch.Tensor] = None,
+           norm_w: Optional[torch.Tensor] = None, eps: float = 1e-5) -> torch.Tensor:
+    if norm_w is not None:
+        x = rmsnorm(x, norm_w, eps)
+    acc = x.float() @ W.float().t()
+    if epi == EPI_BF16:
+        res = acc.to(torch.bfloat16)
+    elif epi == EPI_F32:
+        res = acc
+    elif epi == EPI_RESADD:
+        assert out is not None
+        res = (out.float() + acc).to(torch.bfloat16)
+    elif epi == EPI_SILU:
+        res = (torch.nn.functional.silu(acc[..., 0::2]) * acc[..., 1::2]).to(torch.bfloat16)
+    else:
+        raise ValueError(epi)
+    if out is not None:
+        out.copy_(res)
+        return out
+    return res
+
+
+def rope_tables(inv_freq, max_pos: int):
+    inv = torch.tensor(inv_freq, dtype=torch.float64)
+    t = torch.arange(max_pos, dtype=torch.float64)
+    ang = torch.outer(t, inv)
+    return torch.cos(ang).float(), torch.sin(ang).float()
+
+
+def rope_kv_write(qkv, positions, cos_t, sin_t, k_cache, v_cache, slots, nh, nkv, D, bs):
+    T = qkv.shape[0]
+    half = D // 2
+    pos = positions.long()
+    c = cos_t[pos].unsqueeze(1)  # [T,1,half]
+    s = sin_t[pos].unsqueeze(1)
+    qk = qkv[:, : (nh + nkv) * D].view(T, nh + nkv, D).float()
+    x1, x2 = qk[..., :half], qk[..., half:]
+    rot = torch.cat([x1 * c - x2 * s, x2 * c + x1 * s], dim=-1).to(torch.bfloat16)
+    qkv[:, : nh * D] = rot[:, :nh].reshape(T, nh * D)
+    if slots is not None:
+        v = qkv[:, (nh + nkv) * D:(nh + 2 * nkv) * D].view(T, nkv, D)
+        for t in range(T):
+            sl = int(slots[t])
+            if sl < 0:
+                continue
+            page, off = sl // bs, sl % bs
+            k_cache[page, :, off] = rot[t, nh:]
+            v_cache[page, :, off] = v[t]
+
+
+def _gather_kv(cache, bt_row, L, bs):
+    """[L, nkv, D] from a paged cache [nb, nkv, bs, D]."""
+    idx = torch.arange(L)
+    pages = bt_row[(idx // bs)].long()
+    return cache[pages, :, (idx % bs)]
+
+
+def attn_decode(q, k_cache, v_cache, block_tables, seq_lens, nh, nkv, D, bs, scale):
+    B = q.shape[0]
+    G = nh // nkv
+    out = torch.empty(B, nh * D, dtype=torch.bfloat16)
+    for b in range(B):
+        L = int(seq_lens[b])
+        k = _gather_kv(k_cache, block_tables[b], L, bs).float()  # [L, nkv, D]
+        v = _gather_kv(v_cache, block_tables[b], L, bs).float()
+        qb = q[b, : nh * D].view(nh, D).float()
+        kk = k.repeat_interleave(G, dim=1)  # [L, nh, D]
+        vv = v.repeat_interleave(G, dim=1)
+        s = torch.einsum("hd,lhd->hl", qb, kk) * scale
+        p = torch.softmax(s, dim=-1)
+        out[b] = torch.einsum("hl,lhd->hd", p, vv).reshape(-1).to(torch.bfloat16)
+    return out
+
+
+def attn_prefill(q, k_cache, v_cache, block_tables, q_start, q_lens, ctx_lens, nh, nkv, D, bs, scale, out):
+    G = nh // nkv
+    for b in range(len(q_lens)):
+        ql, ctx, q0 = int(q_lens[b]), int(ctx_lens[b]), int(q_start[b])
+        if ql == 0:
+            continue
+        k = _gather_kv(k_cache, block_tables[b], ctx, bs).float().repeat_interleave(G, dim=1)
+        v = _gather_kv(v_cache, block_tables[b], ctx, bs).float().repeat_interleave(G, dim=1)
+        qb = q[q0:q0 + ql, : nh * D].view(ql, nh, D).float()
+        s = torch.einsum("qhd,khd->hqk", qb, k) * scale
+        qpos = torch.arange(ctx - ql, ctx).view(1, ql, 1)
+        kpos = torch.arange(ctx).view(1, 1, ctx)
+        s = s.masked_fill(kpos > qpos, float("-inf"))
+        p = torch.softmax(s, dim=-1)
+        o = torch.einsum("hqk,khd->qhd", p, v)
+        out[q0:q0 + ql, : nh * D] = o.reshape(ql, nh * D).to(torch.bfloat16)
+    return out
+
+
+# -- sampler ------------------------------------------------------------------------------------
+_M0, _M1, _W0, _W1 = 0xD2511F53, 0xCD9E8D57, 0x9E3779B9, 0xBB67AE85
+_MASK = 0xFFFFFFFF
+
+
+def philox_draw(key: int, idx: torch.Tensor, step: int) -> torch.Tensor:
+    """Vectorised Philox4x32-10, identical to the device version (returns word 0)."""
+    c0 = idx.to(torch.int64) & _MASK
+    c1 = torch.full_like(c0, step & _MASK)
+    c2 = torch.full_like(c0, 0x5EED)
+    c3 = torch.zeros_like(c0)
+    k0, k1 = key & _MASK, (key >> 32) & _MASK
+    for _ in range(10):
+        p0 = _M0 * c0
+        p1 = _M1 * c2
+        hi0, lo0 = (p0 >> 32) & _MASK, p0 & _MASK
+        hi1, lo1 = (p1 >> 32) & _MASK, p1 & _MASK
+        c0, c1, c2, c3 = (hi1 ^ c1 ^ k0) & _MASK, lo1, (hi0 ^ c3 ^ k1) & _MASK, lo0
+        k0 = (k0 + _W0) & _MASK
+        k1 = (k1 + _W1) & _MASK
+    return c0
+
+
+def gumbel(key: int, idx: torch.Tensor, step: int) -> torch.Tensor:
+    r = philox_draw(key, idx, step)
+    u = ((r >> 8).float() + 0.5) * (1.0 / 16777216.0)
+    return -torch.log(-torch.log(u))
+
+
+def sample(logits: torch.Tensor, inv_temp, top_k, top_p, seeds, positions) -> torch.Tensor:
+    """Reference sampler: greedy if inv_temp <= 0; else Gumbel-max over the top-k/top-p set."""
+    B, V = logits.shape
+    out = torch.empty(B, dtype=torch.int32)
+    idx = torch.arange(V)
+    for b in range(B):
+        row = logits[b].float()
+        it = float(inv_temp[b])
+        k = int(top_k[b]) if top_k is not None else 0
+        p = float(top_p[b]) if top_p is not None else 1.0
+        keep = torch.ones(V, dtype=torch.bool)
+        if k > 0 and k < V:
+            kth = torch.topk(row, k).values[-1]
+            keep &= row >= kth
+        if it > 0 and p < 1.0:
+            m = row.max()
+            w = torch.exp((row - m) * it) * keep
+            z = w.sum()
+            order = torch.argsort(row, descending=True, stable=True)
+            cum = torch.cumsum(w[order], 0)
+            cut = int(torch.searchsorted(cum, p * z).item())
+            cut = min(cut, V - 1)
+            thr = row[order[cut]]
+            keep &= row >= thr
+        if it <= 0:
+            v = torch.where(keep, row, torch.tensor(float("-inf")))
+        else:
+            g = gumbel(int(seeds[b]), idx, int(positions[b]))
+            v = torch.where(keep, row * it + g, torch.tensor(float("-inf")))
+        mx = v.max()
+        out[b] = int(torch.nonzero(v == mx)[0].item())
+    return out
+
+
+# -- MoE ------------------------------------------------------------------------------------------
+def moe_route(logits: torch.Tensor, k: int):
+    p = torch.softmax(logits.float(), dim=-1)
+    w, ids = torch.topk(p, k, dim=-1)
+    w = w / w.sum(-1, keepdim=True)
+    return w, ids.to(torch.int32)
+
+
+def moe_ffn(x: torch.Tensor, w_gu: torch.Tensor, w_down: torch.Tensor, rw: torch.Tensor, ids: torch.Tensor,
+            h: torch.Tensor) -> torch.Tensor:
+    """h += sum_j rw[t,j] * down_e(silu_mul(gate_up_e(x_t))) with per-pair bf16 rounding of the
+    intermediate tensors exactly where the kernels round."""
+    T, k = ids.shape
+    y = torch.empty(T * k, h.shape[1], dtype=torch.bfloat16)
+    for t in range(T):
+        for j in range(k):
+            e = int(ids[t, j])
+            gu = (x[t:t + 1].float() @ w_gu[e].float().t()).to(torch.bfloat16)
+            act = silu_mul_interleaved(gu)
+            y[t * k + j] = (act.float() @ w_down[e].float().t()).to(torch.bfloat16)[0]
+    yk = y.view(T, k, -1).float()
+    s = (rw.float().unsqueeze(-1) * yk).sum(1)
+    h.copy_((h.float() + s).to(torch.bfloat16))
+    return h
+
+
+def softmax_scale(D: int) -> float:
+    return 1.0 / math.sqrt(D)

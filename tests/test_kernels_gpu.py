@@ -1,0 +1,266 @@
+"""Kernel numerics on a real MI355X: each HIP kernel vs the fp32 PyTorch oracle of the same op
+(SURVEY.md §4.2 "Kernel numerics")."""
+
+import math
+
+import pytest
+import torch
+
+from llm_consensus_amd import ops
+from llm_consensus_amd.ops import oracle
+
+pytestmark = pytest.mark.gpu
+
+BF = torch.bfloat16
+
+
+def rnd(*shape, scale=1.0, dev="cuda"):
+    return (torch.randn(*shape, device=dev) * scale).to(BF)
+
+
+def close(a, b, atol, rtol=0.02):
+    a = a.float().cpu()
+    b = b.float().cpu()
+    err = (a - b).abs()
+    tol = atol + rtol * b.abs()
+    bad = (err > tol).sum().item()
+    assert bad == 0, f"{bad}/{a.numel()} mismatches, max err {err.max().item():.4g}"
+
+
+@pytest.mark.parametrize("H", [256, 3072, 4096, 8192])
+def test_rmsnorm(cuda, H):
+    torch.manual_seed(0)
+    x = rnd(7, H)
+    w = rnd(H)
+    y = ops.rmsnorm(x, w, 1e-5)
+    close(y, oracle.rmsnorm(x.cpu(), w.cpu(), 1e-5), 1e-2)
+
+
+def test_embedding_and_silu(cuda):
+    torch.manual_seed(0)
+    tab = rnd(1000, 512)
+    ids = torch.tensor([0, 5, 999, 17], dtype=torch.int32, device="cuda")
+    assert torch.equal(ops.embedding(ids, tab).cpu(), oracle.embedding(ids.cpu(), tab.cpu()))
+    gu = rnd(9, 2 * 768)
+    close(ops.silu_mul_interleaved(gu), oracle.silu_mul_interleaved(gu.cpu()), 1e-2)
+
+
+@pytest.mark.parametrize("M", [1, 2, 3, 4])
+@pytest.mark.parametrize("N,K", [(64, 256), (1000, 4096), (4096, 4096), (512, 14336), (130, 192)])
+@pytest.mark.parametrize("epi", [0, 1, 2, 3])
+def test_gemv(cuda, M, N, K, epi):
+    if M > 1 and K > 8192:
+        pytest.skip("LDS budget")
+    torch.manual_seed(M * 7 + N + K + epi)
+    x = rnd(M, K)
+    W = rnd(N, K, scale=0.05)
+    out = rnd(M, N) if epi == 2 else None
+    ref_out = out.cpu().clone() if out is not None else None
+    y = ops.gemv(x, W, epi, out=out)
+    ref = oracle.linear(x.cpu(), W.cpu(), epi, ref_out)
+    close(y, ref, 2e-2)
+
+
+@pytest.mark.parametrize("M", [1, 4])
+def test_gemv_fused_norm(cuda, M):
+    torch.manual_seed(1)
+    x = rnd(M, 4096)
+    W = rnd(6144, 4096, scale=0.05)
+    nw = rnd(4096)
+    y = ops.gemv(x, W, 0, norm_w=nw, eps=1e-5)
+    ref = oracle.linear(x.cpu(), W.cpu(), 0, None, nw.cpu(), 1e-5)
+    close(y, ref, 3e-2)
+
+
+@pytest.mark.parametrize("M,N,K", [(128, 128, 64), (37, 200, 256), (300, 512, 4096), (1024, 384, 1024)])
+@pytest.mark.parametrize("epi", [0, 1, 2])
+def test_gemm(cuda, M, N, K, epi):
+    torch.manual_seed(M + N + K + epi)
+    x = rnd(M, K)
+    W = rnd(N, K, scale=0.05)
+    out = rnd(M, N) if epi == 2 else None
+    ref_out = out.cpu().clone() if out is not None else None
+    y = ops.gemm(x, W, epi, out=out)
+    ref = oracle.linear(x.cpu(), W.cpu(), epi, ref_out)
+    close(y, ref, 2e-2)
+
+
+def test_gemm_identity_asymmetric(cuda):
+    """A = I with an asymmetric B catches a transposed C write (guide §3)."""
+    K = 128
+    A = torch.eye(K, dtype=BF, device="cuda")
+    W = (torch.arange(K * K, device="cuda").view(K, K) % 97).to(BF)  # asymmetric
+    y = ops.gemm(A, W, 0)
+    assert torch.equal(y.cpu(), W.t().contiguous().cpu())
+
+
+def _rope_setup(nh, nkv, D, T, bs=64, nblocks=8):
+    from llm_consensus_amd.models.config import LLAMA3_8B, rope_inv_freq
+
+    cos_t, sin_t = oracle.rope_tables(rope_inv_freq(LLAMA3_8B.with_(head_dim=D)), 4096)
+    qkv = rnd(T, (nh + 2 * nkv) * D)
+    pos = torch.randint(0, 4000, (T,), dtype=torch.int32)
+    perm = torch.randperm(nblocks * bs)[:T].to(torch.int32)
+    kc = torch.zeros(nblocks, nkv, bs, D, dtype=BF)
+    vc = torch.zeros_like(kc)
+    return cos_t, sin_t, qkv, pos, perm, kc, vc
+
+
+@pytest.mark.parametrize("nh,nkv,D", [(32, 8, 128), (32, 32, 96), (4, 2, 64)])
+def test_rope_kv_write(cuda, nh, nkv, D):
+    torch.manual_seed(2)
+    cos_t, sin_t, qkv, pos, slots, kc, vc = _rope_setup(nh, nkv, D, 11)
+    q_ref, kc_ref, vc_ref = qkv.cpu().clone(), kc.clone(), vc.clone()
+    oracle.rope_kv_write(q_ref, pos, cos_t, sin_t, kc_ref, vc_ref, slots, nh, nkv, D, 64)
+    qd, kd, vd = qkv.clone(), kc.cuda(), vc.cuda()
+    ops.rope_kv_write(qd, pos.cuda(), cos_t.cuda(), sin_t.cuda(), kd, vd, slots.cuda(), nh, nkv, D, 64)
+    close(qd, q_ref, 1e-2)
+    close(kd, kc_ref, 1e-2)
+    assert torch.equal(vd.cpu(), vc_ref)
+
+
+def _paged_kv(B, L_max, nkv, D, bs):
+    nblk_per = (L_max + bs - 1) // bs
+    nb = B * nblk_per + 3
+    kc = rnd(nb, nkv, bs, D)
+    vc = rnd(nb, nkv, bs, D)
+    perm = torch.randperm(nb)[: B * nblk_per].view(B, nblk_per).to(torch.int32)
+    return kc, vc, perm
+
+
+@pytest.mark.parametrize("nh,nkv,D", [(32, 8, 128), (32, 32, 96), (16, 2, 128), (4, 2, 64)])
+@pytest.mark.parametrize("lens", [[1, 7], [100, 1000], [3000, 257]])
+def test_attn_decode(cuda, nh, nkv, D, lens):
+    torch.manual_seed(3)
+    B, bs, chunk = len(lens), 64, 256
+    L_max = max(lens)
+    kc, vc, bt = _paged_kv(B, L_max, nkv, D, bs)
+    q = rnd(B, nh * D)
+    sl = torch.tensor(lens, dtype=torch.int32)
+    max_chunks = (4096 + chunk - 1) // chunk
+    po = torch.empty(B, nh, max_chunks, D, device="cuda")
+    pml = torch.empty(B, nh, max_chunks, 2, device="cuda")
+    out = torch.empty(B, nh * D, dtype=BF, device="cuda")
+    scale = 1 / math.sqrt(D)
+    ops.attn_decode(q, kc, vc, bt.cuda(), sl.cuda(), out, po, pml, nh, nkv, D, bs, chunk, scale)
+    ref = oracle.attn_decode(q.cpu(), kc.cpu(), vc.cpu(), bt, sl, nh, nkv, D, bs, scale)
+    close(out, ref, 2e-2)
+
+
+@pytest.mark.parametrize("nh,nkv,D", [(32, 8, 128), (32, 32, 96), (16, 2, 128), (4, 2, 64)])
+@pytest.mark.parametrize("case", ["full", "chunk", "ragged"])
+def test_attn_prefill(cuda, nh, nkv, D, case):
+    torch.manual_seed(4)
+    bs = 64
+    if case == "full":
+        qlens, ctx = [300], [300]
+    elif case == "chunk":
+        qlens, ctx = [200, 64], [1000, 64]
+    else:
+        qlens, ctx = [1, 33, 130], [1, 97, 700]
+    B = len(qlens)
+    kc, vc, bt = _paged_kv(B, max(ctx), nkv, D, bs)
+    qs = torch.tensor([0] + list(torch.cumsum(torch.tensor(qlens), 0)[:-1]), dtype=torch.int32)
+    T = sum(qlens)
+    q = rnd(T, nh * D)
+    out = torch.zeros(T, nh * D, dtype=BF, device="cuda")
+    ql = torch.tensor(qlens, dtype=torch.int32)
+    cl = torch.tensor(ctx, dtype=torch.int32)
+    scale = 1 / math.sqrt(D)
+    ops.attn_prefill(q, kc, vc, bt.cuda(), qs.cuda(), ql.cuda(), cl.cuda(), out, max(qlens), nh, nkv, D, bs, scale)
+    ref = torch.zeros(T, nh * D, dtype=BF)
+    oracle.attn_prefill(q.cpu(), kc.cpu(), vc.cpu(), bt, qs, ql, cl, nh, nkv, D, bs, scale, ref)
+    close(out, ref, 2e-2)
+
+
+def _sample_bufs(B, V):
+    P = ops.sample_parts()
+    return (torch.empty(B, P, device="cuda"), torch.empty(B, P, dtype=torch.int32, device="cuda"),
+            torch.empty(B, dtype=torch.int32, device="cuda"))
+
+
+@pytest.mark.parametrize("V", [1000, 128256])
+def test_sample_greedy_and_gumbel(cuda, V):
+    torch.manual_seed(5)
+    B = 3
+    logits = torch.randn(B, V, device="cuda") * 3
+    wv, wi, nxt = _sample_bufs(B, V)
+    seeds = torch.tensor([1, 2, 3], dtype=torch.int64, device="cuda")
+    pos = torch.tensor([10, 20, 30], dtype=torch.int32, device="cuda")
+    tk = torch.zeros(B, dtype=torch.int32, device="cuda")
+    tp = torch.ones(B, device="cuda")
+    it = torch.zeros(B, device="cuda")
+    ops.sample(logits, it, tk, tp, seeds, pos, nxt, wv, wi)
+    assert torch.equal(nxt.cpu(), logits.argmax(-1).to(torch.int32).cpu())
+    it = torch.ones(B, device="cuda") / 0.8
+    ops.sample(logits, it, tk, tp, seeds, pos, nxt, wv, wi)
+    ref = oracle.sample(logits.cpu(), it.cpu(), tk.cpu(), tp.cpu(), seeds.cpu(), pos.cpu())
+    for b in range(B):  # same Philox stream; allow fast-math ulps on near ties
+        g = oracle.gumbel(int(seeds[b]), torch.tensor([int(nxt[b]), int(ref[b])]), int(pos[b]))
+        s_dev = logits[b, nxt[b]].item() * it[b].item() + g[0].item()
+        s_ref = logits[b, ref[b]].item() * it[b].item() + g[1].item()
+        assert abs(s_dev - s_ref) < 1e-3
+
+
+def test_sample_topk_topp_and_advance(cuda):
+    torch.manual_seed(6)
+    B, V = 2, 32000
+    logits = torch.randn(B, V, device="cuda") * 2
+    wv, wi, nxt = _sample_bufs(B, V)
+    seeds = torch.tensor([7, 8], dtype=torch.int64, device="cuda")
+    it = torch.ones(B, device="cuda")
+    tk = torch.tensor([1, 50], dtype=torch.int32, device="cuda")
+    tp = torch.tensor([1.0, 0.9], device="cuda")
+    pos = torch.tensor([5, 6], dtype=torch.int32, device="cuda")
+    bt = torch.arange(8, dtype=torch.int32, device="cuda").view(2, 4)
+    tin = torch.zeros(B, dtype=torch.int32, device="cuda")
+    sl = torch.zeros(B, dtype=torch.int32, device="cuda")
+    slots = torch.zeros(B, dtype=torch.int32, device="cuda")
+    ot = torch.zeros(B, 8, dtype=torch.int32, device="cuda")
+    oc = torch.zeros(B, dtype=torch.int32, device="cuda")
+    ops.sample(logits, it, tk, tp, seeds, pos, nxt, wv, wi, tokens_in=tin, seq_lens=sl, slots=slots,
+               block_tables=bt, bs=4, out_tokens=ot, out_count=oc, use_topkp=True)
+    n = nxt.cpu()
+    assert int(n[0]) == int(logits[0].argmax())
+    top50 = set(torch.topk(logits[1], 50).indices.cpu().tolist())
+    assert int(n[1]) in top50
+    assert pos.cpu().tolist() == [6, 7] and sl.cpu().tolist() == [7, 8]
+    assert slots.cpu().tolist() == [int(bt[0, 1]) * 4 + 2, int(bt[1, 1]) * 4 + 3]
+    assert oc.cpu().tolist() == [1, 1] and ot[:, 0].cpu().tolist() == n.tolist() and tin.cpu().tolist() == n.tolist()
+
+
+@pytest.mark.parametrize("T", [1, 3, 300])
+def test_moe(cuda, T):
+    torch.manual_seed(7)
+    E, k, H, I = 8, 2, 256, 384
+    x = rnd(T, H)
+    wgu = rnd(E, 2 * I, H, scale=0.05)
+    wd = rnd(E, H, I, scale=0.05)
+    logits = torch.randn(T, E, device="cuda")
+    w = torch.empty(T, k, device="cuda")
+    ids = torch.empty(T, k, dtype=torch.int32, device="cuda")
+    ops.moe_route(logits, k, w, ids)
+    rw, rids = oracle.moe_route(logits.cpu(), k)
+    assert torch.equal(ids.cpu(), rids)
+    close(w, rw, 1e-4, 1e-4)
+    h = rnd(T, H)
+    href = h.cpu().clone()
+    oracle.moe_ffn(x.cpu(), wgu.cpu(), wd.cpu(), w.cpu(), ids.cpu(), href)
+    if T <= 4:
+        act = torch.empty(T * k, I, dtype=BF, device="cuda")
+        ops.moe_gemv(x, wgu, ids, k, act, 2 * I, H, ops.EPI_SILU)
+        y = torch.empty(T * k, H, dtype=BF, device="cuda")
+        ops.moe_gemv(act, wd, ids, 1, y, H, I, ops.EPI_BF16)
+    else:
+        mt = ops.moe_max_tiles(T * k, E)
+        sr = torch.empty(mt * 128, dtype=torch.int32, device="cuda")
+        te = torch.empty(mt, dtype=torch.int32, device="cuda")
+        tc = torch.empty(1, dtype=torch.int32, device="cuda")
+        ops.moe_align(ids, E, sr, te, tc)
+        gu = torch.empty(T * k, 2 * I, dtype=BF, device="cuda")
+        ops.moe_gemm(x, wgu, sr, te, tc, gu, 2 * I, H, mt, k)
+        act = ops.silu_mul_interleaved(gu)
+        y = torch.empty(T * k, H, dtype=BF, device="cuda")
+        ops.moe_gemm(act, wd, sr, te, tc, y, H, I, mt, 1)
+    ops.moe_combine(y, w, ids, h)
+    close(h, href, 3e-2)

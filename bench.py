@@ -1,0 +1,220 @@
+#!/usr/bin/env python3
+"""Consensus-round benchmark (BASELINE.json metric: p50 end-to-end consensus latency + aggregate
+output tokens/sec, N-model fan-out), configs 2/3 generalised to N GPUs:
+
+  * one process per GPU (torchrun; RCCL over xGMI for the gather), weak scaling:
+    each GPU hosts ``--models-per-gpu`` Llama-3-8B responders (distinct random-init replicas,
+    ``llama-3-8b@<i>``), so an N-GPU run is an (N x models-per-gpu)-model fan-out;
+  * the Llama-3-8B judge lives on GPU 0 beside rank 0's responder(s) on its own hipStream
+    (config 3: "judge time-shares GPU 0 via concurrent hipStreams");
+  * one timed step = one full consensus round exactly as ``llm-consensus`` runs it: every
+    responder prefills the prompt and decodes ``--max-tokens`` tokens, the responses are
+    gathered to rank 0, the judge prompt is rendered with the reference template
+    (internal/consensus/judge.go) and the judge prefills it and decodes ``--max-tokens`` tokens
+    (a single response is passed through without a judge call, judge.go:74-79).
+
+Reported ``value`` = total generated tokens (responders + judge) per second of wall time over
+the whole job; ``ms_per_step`` = mean end-to-end round latency; p50 is in ``extra``.
+Data: synthetic prompt (seeded synthetic-tokenizer text), random-init weights, bf16.
+"""
+
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import statistics
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+
+def log(*a):
+    print(f"[bench r{os.environ.get('RANK', '0')}]", *a, file=sys.stderr, flush=True)
+
+
+def main() -> None:
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=3)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--model", default="llama-3-8b")
+    ap.add_argument("--judge", default="llama-3-8b")
+    ap.add_argument("--models-per-gpu", type=int, default=1)
+    ap.add_argument("--max-tokens", type=int, default=4096)
+    ap.add_argument("--judge-max-tokens", type=int, default=0, help="0 = same as --max-tokens")
+    ap.add_argument("--prompt-tokens", type=int, default=128)
+    ap.add_argument("--temperature", type=float, default=1.0)
+    ap.add_argument("--steps-per-graph", type=int, default=8)
+    ap.add_argument("--no-graphs", action="store_true")
+    args = ap.parse_args()
+
+    import torch
+    import torch.distributed as dist
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        log(f"warning: --gpus {args.gpus} but WORLD_SIZE {world}; using WORLD_SIZE")
+    n_gpus = world
+    torch.cuda.set_device(local)
+    dev = f"cuda:{local}"
+    if world > 1:
+        dist.init_process_group("nccl", device_id=torch.device(dev))
+
+    from llm_consensus_amd.consensus import build_judge_prompt, prompt_header
+    from llm_consensus_amd.engine import Engine, EngineConfig, SamplingParams
+    from llm_consensus_amd.models.config import FAMILIES
+    from llm_consensus_amd.provider.base import Response
+    from llm_consensus_amd.utils.tokenizer import get_tokenizer
+
+    rcfg = FAMILIES[args.model]
+    jcfg = FAMILIES[args.judge]
+    mpg = args.models_per_gpu
+    n_models = n_gpus * mpg
+    jmax = args.judge_max_tokens or args.max_tokens
+    tok = get_tokenizer(rcfg.vocab)
+    jtok = get_tokenizer(jcfg.vocab)
+
+    # synthetic prompt: seeded piece ids -> text (identical on every rank)
+    g = torch.Generator().manual_seed(1234)
+    pids = torch.randint(256, 256 + 60000, (args.prompt_tokens,), generator=g).tolist()
+    prompt_text = tok.decode(pids).strip()
+    prompt_ids = tok.encode(prompt_text, add_bos=True)
+
+    resp_ctx = len(prompt_ids) + args.max_tokens + 64
+    t0 = time.time()
+    responders = []
+    for j in range(mpg):
+        idx = rank * mpg + j
+        e = Engine(rcfg, EngineConfig(device=dev, max_context=resp_ctx, seed=1000 + idx,
+                                      steps_per_graph=args.steps_per_graph, use_graphs=not args.no_graphs),
+                   name=f"{args.model}@{idx}")
+        responders.append((idx, e))
+    judge = None
+    judge_ctx = 0
+    if rank == 0 and n_models > 1:
+        judge_ctx = len(prompt_ids) + 1024 + n_models * (args.max_tokens + 32) + jmax + 64
+        judge = Engine(jcfg, EngineConfig(device=dev, max_context=judge_ctx, seed=777,
+                                          steps_per_graph=args.steps_per_graph, use_graphs=not args.no_graphs),
+                       name=f"{args.judge}@judge")
+    torch.cuda.synchronize()
+    log(f"engines ready in {time.time() - t0:.1f}s (responders {mpg}/gpu, judge ctx {judge_ctx})")
+
+    def one_round(step: int):
+        stats = {}
+        t_start = time.perf_counter()
+        # judge header prefill can start before any response exists
+        jseq = None
+        if judge is not None:
+            jseq = judge.new_sequence()
+            judge.prefill([jseq], [jtok.encode(prompt_header(prompt_text), add_bos=True)], want_logits=False)
+        outs = []
+        for idx, e in responders:
+            ids = e.generate_ids(prompt_ids, args.max_tokens, temperature=args.temperature,
+                                 seed=1000 * step + idx + 1, stop_on_eos=False)
+            outs.append(ids)
+        t_resp = time.perf_counter()
+        # gather responses to rank 0 (fixed-size int32 rows; RCCL over xGMI)
+        local_t = torch.full((mpg, args.max_tokens), -1, dtype=torch.int32, device=dev)
+        for j, ids in enumerate(outs):
+            local_t[j, : len(ids)] = torch.tensor(ids, dtype=torch.int32, device=dev)
+        if world > 1:
+            all_t = torch.empty((world, mpg, args.max_tokens), dtype=torch.int32, device=dev)
+            dist.all_gather_into_tensor(all_t, local_t)
+        else:
+            all_t = local_t.unsqueeze(0)
+        n_tokens = n_models * args.max_tokens
+        if rank == 0:
+            rows = all_t.view(n_models, args.max_tokens).cpu().tolist()
+            responses = []
+            for i, r in enumerate(rows):
+                r = [t for t in r if t >= 0]
+                responses.append(Response(model=f"{args.model}@{i}", content=tok.decode(r), provider="rocm"))
+            if judge is not None and len(responses) > 1:
+                full = build_judge_prompt(prompt_text, responses)
+                head = prompt_header(prompt_text)
+                rest_ids = jtok.encode(full[len(head):])
+                judge.prefill([jseq], [rest_ids])
+                t_jp = time.perf_counter()
+                jids = judge.decode([jseq], [SamplingParams(jmax, args.temperature, 1.0, 0, 99 + step, False)])[0]
+                stats["judge_prompt_tokens"] = jseq.length - len(jids)
+                stats["judge_prefill_s"] = t_jp - t_resp
+                n_tokens += len(jids)
+            if jseq is not None:
+                judge.free_sequence(jseq)
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        t_end = time.perf_counter()
+        stats["responders_s"] = t_resp - t_start
+        stats["e2e_s"] = t_end - t_start
+        stats["tokens"] = n_tokens
+        return stats
+
+    for w in range(args.warmup):
+        st = one_round(w)
+        log(f"warmup {w}: {st}")
+
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    lat = []
+    tot_tokens = 0
+    t0 = time.perf_counter()
+    per_step = []
+    for s in range(args.steps):
+        st = one_round(100 + s)
+        lat.append(st["e2e_s"])
+        tot_tokens += st["tokens"]
+        per_step.append(st)
+        log(f"step {s}: {st}")
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        tt = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        elapsed = float(tt.item())
+    if rank == 0:
+        value = tot_tokens / elapsed
+        resp_tok_s = n_models * args.max_tokens * args.steps / sum(p["responders_s"] for p in per_step)
+        out = {
+            "metric": "consensus_aggregate_output_tokens_per_s",
+            "value": round(value, 2),
+            "unit": "tokens/s",
+            "n_gpus": n_gpus,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(1000 * elapsed / args.steps, 2),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "bf16",
+            "data": "synthetic prompt (synthetic tokenizer), random-init weights",
+            "config": {
+                "model": f"{n_models}x {args.model} responders ({mpg}/GPU) + {args.judge} judge on GPU0 stream",
+                "global_batch": n_models,
+                "seq_len": len(prompt_ids) + args.max_tokens,
+                "max_tokens": args.max_tokens,
+                "prompt_tokens": len(prompt_ids),
+                "parallelism": f"fanout{n_models}" + ("" if n_gpus == 1 else f"-dp{n_gpus}"),
+            },
+            "extra": {
+                "p50_e2e_latency_s": round(statistics.median(lat), 3),
+                "responder_decode_tok_s_per_model": round(resp_tok_s / n_models, 2),
+                "judge_prompt_tokens": per_step[-1].get("judge_prompt_tokens", 0),
+                "judge_prefill_s": round(per_step[-1].get("judge_prefill_s", 0.0), 3),
+            },
+        }
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

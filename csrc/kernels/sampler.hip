@@ -116,7 +116,9 @@ struct DecodeState {
   int cap;
 };
 
+// No-op unless tokens_in is given (a bare sample call must not move the position/step counter).
 __device__ __forceinline__ void advance(const DecodeState& st, int b, int tok) {
+  if (st.tokens_in == nullptr) return;
   if (st.out_tokens != nullptr) {
     const int cnt = st.out_count[b];
     if (cnt < st.cap) st.out_tokens[static_cast<int64_t>(b) * st.cap + cnt] = tok;

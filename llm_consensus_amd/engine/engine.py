@@ -1,0 +1,552 @@
+"""Inference engine: paged-KV prefill + HIP-graph decode for one model instance (T2).
+
+One ``Engine`` = one model replica (or one TP shard of it) on one GPU, with its own hipStream, KV
+pool and captured decode graphs; several engines can share a GPU (responders + judge) and run
+concurrently on their streams.
+
+Decode is device-resident: tokens, positions, slots, seq_lens, sampling params and the token
+history live in device buffers; one decode step = embedding → L × (qkv GEMV [fused RMSNorm] →
+RoPE + paged-KV write → split-KV attention → o GEMV [+residual] → gate_up GEMV [fused RMSNorm,
+SiLU·up epilogue] → down GEMV [+residual]) → lm_head GEMV [fused final norm] → sample + advance.
+``steps_per_graph`` such steps are captured into ONE HIP graph and replayed; the host only polls
+the token history (pinned async copy + event, one replay behind) for streaming, EOS, deadline
+and cancellation — there is no per-token host↔device synchronisation.
+
+Prefill is eager, chunked (``prefill_chunk`` tokens), on MFMA GEMMs + the flash prefill kernel
+over the paged cache; a prefill may extend an existing sequence (incremental judge prefill,
+SURVEY.md §7.4).
+"""
+
+from __future__ import annotations
+
+import dataclasses
+import math
+import time
+from typing import Callable, Dict, List, Optional, Sequence as Seq
+
+import torch
+
+from .. import ops
+from ..context import Context, ContextError
+from ..models.config import ModelConfig, rope_inv_freq
+from ..models.transformer import TransformerWeights
+from ..ops import EPI_BF16, EPI_F32, EPI_RESADD, EPI_SILU, oracle
+from ..parallel.comm import TPGroup
+from ..utils import trace
+from ..utils.native import runtime
+
+
+@dataclasses.dataclass
+class EngineConfig:
+    device: str = "cuda:0"
+    max_context: int = 8192
+    max_batch: int = 1
+    block_size: int = 64
+    kv_blocks: int = 0
+    seed: int = 0
+    steps_per_graph: int = 8
+    use_graphs: bool = True
+    prefill_chunk: int = 8192
+    attn_chunk: int = 256
+    init_scale: float = 1.0
+    stream_priority: int = 0
+
+
+@dataclasses.dataclass
+class SamplingParams:
+    max_tokens: int = 256
+    temperature: float = 1.0
+    top_p: float = 1.0
+    top_k: int = 0
+    seed: int = 0
+    stop_on_eos: bool = True
+
+
+class Sequence:
+    def __init__(self, row: int):
+        self.row = row
+        self.blocks: List[int] = []
+        self.length = 0
+        self.has_logits = False
+
+
+class EngineError(Exception):
+    pass
+
+
+class Engine:
+    def __init__(self, cfg: ModelConfig, ecfg: Optional[EngineConfig] = None, tp: Optional[TPGroup] = None,
+                 name: str = "", weights: Optional[TransformerWeights] = None):
+        self.cfg = cfg
+        self.ecfg = ecfg or EngineConfig()
+        self.tp = tp or TPGroup.single()
+        self.name = name or cfg.name
+        self.device = torch.device(self.ecfg.device)
+        self.on_gpu = self.device.type == "cuda"
+        if self.on_gpu:
+            torch.cuda.set_device(self.device)
+            self.stream = torch.cuda.Stream(self.device, priority=self.ecfg.stream_priority)
+        else:
+            self.stream = None
+        e = self.ecfg
+        with self._on_stream():
+            with trace.span("weights_init", engine=self.name):
+                if weights is not None:
+                    self.w = weights.to(self.device)
+                else:
+                    self.w = TransformerWeights(cfg, self.tp, self.device, e.seed, e.init_scale)
+        self.nh, self.nkv, self.D = self.w.nh, self.w.nkv, cfg.head_dim
+        self.scale = 1.0 / math.sqrt(self.D)
+        self.bs = e.block_size
+        self.max_blocks_per_seq = (e.max_context + self.bs - 1) // self.bs + 1
+        nb = e.kv_blocks or e.max_batch * self.max_blocks_per_seq + 2
+        self.alloc = runtime().BlockAllocator(nb, self.bs)
+        dev = self.device
+        L = cfg.n_layers
+        self.k_cache = torch.zeros(L, nb, self.nkv, self.bs, self.D, dtype=torch.bfloat16, device=dev)
+        self.v_cache = torch.zeros_like(self.k_cache)
+        cos_t, sin_t = oracle.rope_tables(rope_inv_freq(cfg), e.max_context + e.steps_per_graph + 2)
+        self.cos_t, self.sin_t = cos_t.to(dev), sin_t.to(dev)
+        self._alloc_decode_buffers()
+        self._graphs: Dict[int, "torch.cuda.CUDAGraph"] = {}
+        self.free_rows = list(range(e.max_batch))
+
+    # ------------------------------------------------------------------------------------------
+    def _on_stream(self):
+        if self.stream is not None:
+            return torch.cuda.stream(self.stream)
+        import contextlib
+
+        return contextlib.nullcontext()
+
+    def _alloc_decode_buffers(self) -> None:
+        B, dev, c = self.ecfg.max_batch, self.device, self.cfg
+        i32 = dict(dtype=torch.int32, device=dev)
+        self.tokens_in = torch.zeros(B, **i32)
+        self.positions = torch.zeros(B, **i32)
+        self.seq_lens = torch.ones(B, **i32)
+        self.slots = torch.zeros(B, **i32)
+        self.block_tables = torch.zeros(B, self.max_blocks_per_seq, **i32)
+        self.cap = self.ecfg.max_context + self.ecfg.steps_per_graph + 1
+        self.out_tokens = torch.zeros(B, self.cap, **i32)
+        self.out_count = torch.zeros(B, **i32)
+        self.next_tok = torch.zeros(B, **i32)
+        self.inv_temp = torch.ones(B, dtype=torch.float32, device=dev)
+        self.top_k = torch.zeros(B, **i32)
+        self.top_p = torch.ones(B, dtype=torch.float32, device=dev)
+        self.seeds = torch.zeros(B, dtype=torch.int64, device=dev)
+        bf = dict(dtype=torch.bfloat16, device=dev)
+        self.h = torch.zeros(B, c.hidden, **bf)
+        self.qkv = torch.zeros(B, self.w.qkv_size, **bf)
+        self.attn = torch.zeros(B, self.w.q_size, **bf)
+        self.act = torch.zeros(B, self.w.inter, **bf)
+        self.logits_local = torch.zeros(B, self.w.vocab_local, dtype=torch.float32, device=dev)
+        self.logits = (self.logits_local if self.tp.size == 1
+                       else torch.zeros(B, c.vocab, dtype=torch.float32, device=dev))
+        self._gather_buf = (None if self.tp.size == 1 else
+                            torch.zeros(self.tp.size, B, self.w.vocab_local, dtype=torch.float32, device=dev))
+        max_chunks = (self.ecfg.max_context + self.ecfg.attn_chunk - 1) // self.ecfg.attn_chunk + 1
+        self.part_o = torch.zeros(B, self.nh, max_chunks, self.D, dtype=torch.float32, device=dev)
+        self.part_ml = torch.zeros(B, self.nh, max_chunks, 2, dtype=torch.float32, device=dev)
+        if self.on_gpu:
+            P = ops.sample_parts()
+            self.ws_v = torch.zeros(B, P, dtype=torch.float32, device=dev)
+            self.ws_i = torch.zeros(B, P, dtype=torch.int32, device=dev)
+        else:
+            self.ws_v = self.ws_i = None
+        if c.is_moe:
+            k = c.top_k_experts
+            self.xn = torch.zeros(B, c.hidden, **bf)
+            self.router_logits = torch.zeros(B, c.n_experts, dtype=torch.float32, device=dev)
+            self.moe_w = torch.zeros(B, k, dtype=torch.float32, device=dev)
+            self.moe_ids = torch.zeros(B, k, **i32)
+            self.moe_act = torch.zeros(B * k, self.w.inter, **bf)
+            self.moe_y = torch.zeros(B * k, c.hidden, **bf)
+        if self.on_gpu:
+            self.host_tokens = torch.zeros(B, self.cap, dtype=torch.int32, pin_memory=True)
+            self.host_count = torch.zeros(B, dtype=torch.int32, pin_memory=True)
+
+    # -- sequence management -------------------------------------------------------------------
+    def new_sequence(self) -> Sequence:
+        if not self.free_rows:
+            raise EngineError("no free decode rows")
+        return Sequence(self.free_rows.pop(0))
+
+    def free_sequence(self, seq: Sequence) -> None:
+        if seq.blocks:
+            self.alloc.free(seq.blocks)
+            seq.blocks = []
+        seq.length = 0
+        if seq.row not in self.free_rows:
+            self.free_rows.append(seq.row)
+            self.free_rows.sort()
+
+    def _reserve(self, seq: Sequence, total_tokens: int) -> None:
+        need = self.alloc.blocks_for(total_tokens) - len(seq.blocks)
+        if total_tokens > self.max_blocks_per_seq * self.bs:
+            raise EngineError(f"context {total_tokens} exceeds engine max_context {self.ecfg.max_context}")
+        if need > 0:
+            got = self.alloc.allocate(need)
+            if not got:
+                raise EngineError(f"KV cache exhausted ({self.alloc.num_free} blocks free, need {need})")
+            seq.blocks.extend(got)
+            bt = torch.tensor(seq.blocks, dtype=torch.int32)
+            self.block_tables[seq.row, : len(seq.blocks)].copy_(bt.to(self.device), non_blocking=False)
+
+    # -- prefill ----------------------------------------------------------------------------------
+    @torch.no_grad()
+    def prefill(self, seqs: List[Sequence], token_lists: List[List[int]], want_logits: bool = True) -> None:
+        """Append ``token_lists[i]`` to ``seqs[i]`` (chunked); optionally compute last-token logits."""
+        with self._on_stream(), trace.span("prefill", engine=self.name, tokens=sum(len(t) for t in token_lists)):
+            pending = [(s, list(t)) for s, t in zip(seqs, token_lists) if t]
+            chunk = self.ecfg.prefill_chunk
+            while pending:
+                batch, rest, budget = [], [], chunk
+                for s, t in pending:
+                    if budget <= 0:
+                        rest.append((s, t))
+                        continue
+                    take = t[:budget]
+                    batch.append((s, take))
+                    budget -= len(take)
+                    if len(take) < len(t):
+                        rest.append((s, t[len(take):]))
+                last = not rest
+                self._prefill_chunk(batch, want_logits and last, all_seqs=seqs if last else None)
+                pending = rest
+
+    def _prefill_chunk(self, batch, want_logits: bool, all_seqs) -> None:
+        dev, c = self.device, self.cfg
+        ids, pos, slots, q_start, q_lens, ctx_lens, rows = [], [], [], [], [], [], []
+        for s, toks in batch:
+            self._reserve(s, s.length + len(toks))
+            q_start.append(len(ids))
+            q_lens.append(len(toks))
+            for i, t in enumerate(toks):
+                p = s.length + i
+                ids.append(t)
+                pos.append(p)
+                slots.append(s.blocks[p // self.bs] * self.bs + p % self.bs)
+            s.length += len(toks)
+            ctx_lens.append(s.length)
+            rows.append(s.row)
+        T = len(ids)
+        i32 = dict(dtype=torch.int32)
+        ids_d = torch.tensor(ids, **i32).to(dev, non_blocking=True)
+        pos_d = torch.tensor(pos, **i32).to(dev, non_blocking=True)
+        slots_d = torch.tensor(slots, **i32).to(dev, non_blocking=True)
+        qs_d = torch.tensor(q_start, **i32).to(dev, non_blocking=True)
+        ql_d = torch.tensor(q_lens, **i32).to(dev, non_blocking=True)
+        cl_d = torch.tensor(ctx_lens, **i32).to(dev, non_blocking=True)
+        bt = self.block_tables[torch.tensor(rows, dtype=torch.long, device=dev)] if self.on_gpu else \
+            self.block_tables[torch.tensor(rows, dtype=torch.long)]
+        max_qlen = max(q_lens)
+
+        h = ops.embedding(ids_d, self.w.embed)
+        attn = torch.empty(T, self.w.q_size, dtype=torch.bfloat16, device=dev)
+        for li, Lw in enumerate(self.w.layers):
+            xn = ops.rmsnorm(h, Lw.ln1, c.rms_eps)
+            qkv = ops.linear(xn, Lw.w_qkv, EPI_BF16)
+            ops.rope_kv_write(qkv, pos_d, self.cos_t, self.sin_t, self.k_cache[li], self.v_cache[li], slots_d,
+                              self.nh, self.nkv, self.D, self.bs)
+            ops.attn_prefill(qkv, self.k_cache[li], self.v_cache[li], bt, qs_d, ql_d, cl_d, attn, max_qlen,
+                             self.nh, self.nkv, self.D, self.bs, self.scale)
+            self._row_parallel(attn, Lw.w_o, h)
+            xn = ops.rmsnorm(h, Lw.ln2, c.rms_eps)
+            if c.is_moe:
+                self._moe(xn, Lw, h)
+            else:
+                act = ops.linear(xn, Lw.w_gu, EPI_SILU)
+                self._row_parallel(act, Lw.w_down, h)
+        if want_logits:
+            last = []
+            for (s, toks), st in zip(batch, q_start):
+                last.append(st + len(toks) - 1)
+            last_d = torch.tensor(last, dtype=torch.long).to(dev)
+            hl = h.index_select(0, last_d)
+            rows_t = torch.tensor(rows, dtype=torch.long).to(dev)
+            B = len(rows)
+            lg = torch.empty(B, self.w.vocab_local, dtype=torch.float32, device=dev)
+            ops.linear(hl, self.w.lm_head, EPI_F32, out=lg, norm_w=self.w.final_norm, eps=c.rms_eps)
+            self.logits_local.index_copy_(0, rows_t, lg)
+            for s, _ in batch:
+                s.has_logits = True
+
+    def _row_parallel(self, x: torch.Tensor, W: torch.Tensor, h: torch.Tensor) -> None:
+        """h += x @ W^T across the TP group (residual folded into rank 0's partial)."""
+        ops.linear(x, W, EPI_RESADD if self.tp.rank == 0 else EPI_BF16, out=h)
+        self.tp.all_reduce_(h)
+
+    def _moe(self, xn: torch.Tensor, Lw, h: torch.Tensor) -> None:
+        c = self.cfg
+        T, k, E = xn.shape[0], c.top_k_experts, c.n_experts
+        if not xn.is_cuda:
+            rl = oracle.linear(xn, Lw.w_router, EPI_F32)
+            w, ids = oracle.moe_route(rl, k)
+            if self.tp.rank != 0:
+                h.zero_()
+            oracle.moe_ffn(xn, Lw.w_gu, Lw.w_down, w, ids, h)
+            self.tp.all_reduce_(h)
+            return
+        rl = ops.linear(xn, Lw.w_router, EPI_F32)
+        w = torch.empty(T, k, dtype=torch.float32, device=xn.device)
+        ids = torch.empty(T, k, dtype=torch.int32, device=xn.device)
+        ops.moe_route(rl, k, w, ids)
+        I_l, H = self.w.inter, c.hidden
+        y = torch.empty(T * k, H, dtype=torch.bfloat16, device=xn.device)
+        if T <= ops.GEMV_MAX_M:
+            act = torch.empty(T * k, I_l, dtype=torch.bfloat16, device=xn.device)
+            ops.moe_gemv(xn, Lw.w_gu, ids, k, act, 2 * I_l, H, EPI_SILU)
+            ops.moe_gemv(act, Lw.w_down, ids, 1, y, H, I_l, EPI_BF16)
+        else:
+            mt = ops.moe_max_tiles(T * k, E)
+            sr = torch.empty(mt * ops.MOE_TILE, dtype=torch.int32, device=xn.device)
+            te = torch.empty(mt, dtype=torch.int32, device=xn.device)
+            tc = torch.empty(1, dtype=torch.int32, device=xn.device)
+            ops.moe_align(ids, E, sr, te, tc)
+            gu = torch.empty(T * k, 2 * I_l, dtype=torch.bfloat16, device=xn.device)
+            ops.moe_gemm(xn, Lw.w_gu, sr, te, tc, gu, 2 * I_l, H, mt, k)
+            act = ops.silu_mul_interleaved(gu)
+            ops.moe_gemm(act, Lw.w_down, sr, te, tc, y, H, I_l, mt, 1)
+        if self.tp.rank != 0:
+            h.zero_()
+        ops.moe_combine(y, w, ids, h)
+        self.tp.all_reduce_(h)
+
+    # -- decode -------------------------------------------------------------------------------------
+    def _decode_step(self, B: int) -> None:
+        c = self.cfg
+        h, qkv, attn, act = self.h[:B], self.qkv[:B], self.attn[:B], self.act[:B]
+        ops.embedding(self.tokens_in[:B], self.w.embed, out=h)
+        for li, Lw in enumerate(self.w.layers):
+            ops.linear(h, Lw.w_qkv, EPI_BF16, out=qkv, norm_w=Lw.ln1, eps=c.rms_eps)
+            ops.rope_kv_write(qkv, self.positions[:B], self.cos_t, self.sin_t, self.k_cache[li], self.v_cache[li],
+                              self.slots[:B], self.nh, self.nkv, self.D, self.bs)
+            ops.attn_decode(qkv, self.k_cache[li], self.v_cache[li], self.block_tables[:B], self.seq_lens[:B], attn,
+                            self.part_o[:B], self.part_ml[:B], self.nh, self.nkv, self.D, self.bs,
+                            self.ecfg.attn_chunk, self.scale)
+            self._row_parallel(attn, Lw.w_o, h)
+            if c.is_moe:
+                self._moe_decode(h, Lw, B)
+            else:
+                ops.linear(h, Lw.w_gu, EPI_SILU, out=act, norm_w=Lw.ln2, eps=c.rms_eps)
+                self._row_parallel(act, Lw.w_down, h)
+        lg = self.logits_local[:B]
+        ops.linear(h, self.w.lm_head, EPI_F32, out=lg, norm_w=self.w.final_norm, eps=c.rms_eps)
+        logits = self._gather_logits(B)
+        self._sample(B, logits)
+
+    def _moe_decode(self, h, Lw, B) -> None:
+        c = self.cfg
+        xn = self.xn[:B]
+        ops.rmsnorm(h, Lw.ln2, c.rms_eps, out=xn)
+        if not h.is_cuda:
+            self._moe(xn, Lw, h)
+            return
+        k = c.top_k_experts
+        rl = self.router_logits[:B]
+        ops.linear(xn, Lw.w_router, EPI_F32, out=rl)
+        ops.moe_route(rl, k, self.moe_w[:B], self.moe_ids[:B])
+        I_l, H = self.w.inter, c.hidden
+        act, y = self.moe_act[: B * k], self.moe_y[: B * k]
+        ops.moe_gemv(xn, Lw.w_gu, self.moe_ids[:B], k, act, 2 * I_l, H, EPI_SILU)
+        ops.moe_gemv(act, Lw.w_down, self.moe_ids[:B], 1, y, H, I_l, EPI_BF16)
+        if self.tp.rank != 0:
+            h.zero_()
+        ops.moe_combine(y, self.moe_w[:B], self.moe_ids[:B], h)
+        self.tp.all_reduce_(h)
+
+    def _gather_logits(self, B: int) -> torch.Tensor:
+        """Vocab-parallel lm_head: all-gather [B, V/tp] shards into [B, V] (C3)."""
+        if self.tp.size == 1:
+            return self.logits_local[:B]
+        n = self.tp.size * B * self.w.vocab_local
+        buf = self._gather_buf.view(-1)[:n].view(self.tp.size, B, self.w.vocab_local)
+        self.tp.all_gather_rows(self.logits_local[:B], buf)
+        out = self.logits[:B]
+        if B == 1:
+            out.view(-1).copy_(buf.view(-1))
+        else:
+            out.view(B, self.tp.size, self.w.vocab_local).copy_(buf.permute(1, 0, 2))
+        return out
+
+    def _sample(self, B: int, logits: torch.Tensor) -> None:
+        use_topkp = bool(self._use_topkp)
+        ops.sample(logits, self.inv_temp[:B], self.top_k[:B], self.top_p[:B], self.seeds[:B], self.positions[:B],
+                   self.next_tok[:B], self.ws_v[:B] if self.ws_v is not None else None,
+                   self.ws_i[:B] if self.ws_i is not None else None, tokens_in=self.tokens_in[:B],
+                   seq_lens=self.seq_lens[:B], slots=self.slots[:B], block_tables=self.block_tables[:B], bs=self.bs,
+                   out_tokens=self.out_tokens[:B], out_count=self.out_count[:B], use_topkp=use_topkp)
+
+    def _graph(self, B: int):
+        key = (B, self._use_topkp)
+        g = self._graphs.get(key)
+        if g is not None:
+            return g
+        S = self.ecfg.steps_per_graph
+        # warm up once eagerly (kernel attributes, lazy module state) with the device state
+        # snapshotted and restored, then capture S steps. thread_local capture mode: other
+        # engines' threads may allocate / synchronise while this one captures.
+        snap = self._snapshot_state()
+        self._decode_step(B)
+        self._restore_state(snap)
+        self.stream.synchronize()
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g, stream=self.stream, capture_error_mode="thread_local"):
+            for _ in range(S):
+                self._decode_step(B)
+        self._graphs[key] = g
+        return g
+
+    _use_topkp = False
+
+    def _snapshot_state(self):
+        return [t.clone() for t in (self.tokens_in, self.positions, self.seq_lens, self.slots, self.out_tokens,
+                                    self.out_count, self.next_tok)]
+
+    def _restore_state(self, snap) -> None:
+        for dst, src in zip((self.tokens_in, self.positions, self.seq_lens, self.slots, self.out_tokens,
+                             self.out_count, self.next_tok), snap):
+            dst.copy_(src)
+
+    @torch.no_grad()
+    def decode(self, seqs: List[Sequence], params: List[SamplingParams], ctx: Optional[Context] = None,
+               on_tokens: Optional[Callable[[int, List[int]], None]] = None) -> List[List[int]]:
+        """Sample from each sequence's prefill logits, then decode until every row hits max_tokens /
+        EOS. ``on_tokens(i, new_ids)`` streams tokens (i indexes ``seqs``). Rows must be 0..B-1."""
+        B = len(seqs)
+        if sorted(s.row for s in seqs) != list(range(B)):
+            raise EngineError("decode rows must be 0..B-1")
+        S = self.ecfg.steps_per_graph
+        eos = self._eos_id()
+        with self._on_stream(), trace.span("decode", engine=self.name, rows=B):
+            order = sorted(range(B), key=lambda i: seqs[i].row)
+            max_new = max(p.max_tokens for p in params)
+            self._use_topkp = any((p.top_k > 0 or p.top_p < 1.0) for p in params)
+            for i in order:
+                s, p = seqs[i], params[i]
+                if not s.has_logits:
+                    raise EngineError("sequence has no prefill logits")
+                self._reserve(s, s.length + p.max_tokens + S + 1)
+                r = s.row
+                self.inv_temp[r] = 0.0 if p.temperature <= 0 else 1.0 / p.temperature
+                self.top_k[r] = p.top_k
+                self.top_p[r] = p.top_p
+                self.seeds[r] = p.seed
+                self.positions[r] = s.length - 1
+                self.out_count[r] = 0
+            if max_new > self.cap - S - 1:
+                raise EngineError("max_tokens exceeds engine capacity")
+            # first token from the prefill logits (+ device state advance)
+            self._sample(B, self._gather_logits(B))
+            produced = [0] * B
+            done = [False] * B
+            results: List[List[int]] = [[] for _ in range(B)]
+            issued = 1
+
+            def consume(counts, toks) -> None:
+                for i in range(B):
+                    r = seqs[i].row
+                    if done[i]:
+                        continue
+                    n = min(int(counts[r]), params[i].max_tokens)
+                    new = toks[r][produced[i]:n].tolist() if n > produced[i] else []
+                    stop = False
+                    if params[i].stop_on_eos and eos in new:
+                        new = new[: new.index(eos)]
+                        stop = True
+                    if new:
+                        results[i].extend(new)
+                        if on_tokens:
+                            on_tokens(i, new)
+                    produced[i] = n if not stop else produced[i] + len(new)
+                    if stop or n >= params[i].max_tokens:
+                        done[i] = True
+
+            if not self.on_gpu:
+                while True:
+                    consume(self.out_count, self.out_tokens)
+                    if all(done):
+                        break
+                    if ctx is not None:
+                        ctx.check()
+                    self._decode_step(B)
+                self._finish(seqs, results)
+                return results
+
+            graph = self._graph(B) if self.ecfg.use_graphs else None
+            pending_ev: Optional[torch.cuda.Event] = None
+
+            def launch_copy():
+                self.host_count.copy_(self.out_count, non_blocking=True)
+                self.host_tokens.copy_(self.out_tokens, non_blocking=True)
+                ev = torch.cuda.Event()
+                ev.record(self.stream)
+                return ev
+
+            pending_ev = launch_copy()
+            while True:
+                need_more = issued < max_new
+                if need_more:
+                    if graph is not None:
+                        graph.replay()
+                    else:
+                        for _ in range(S):
+                            self._decode_step(B)
+                    issued += S
+                # wait for the previous snapshot (the GPU keeps the just-issued replay queued)
+                pending_ev.synchronize()
+                consume(self.host_count, self.host_tokens)
+                if all(done):
+                    break
+                if ctx is not None and ctx.done():
+                    self.stream.synchronize()
+                    raise ContextError(ctx.err())
+                pending_ev = launch_copy()
+                if not need_more:
+                    pending_ev.synchronize()
+                    consume(self.host_count, self.host_tokens)
+                    break
+            self.stream.synchronize()
+            self._finish(seqs, results)
+            return results
+
+    def _finish(self, seqs, results) -> None:
+        for s, r in zip(seqs, results):
+            s.length += len(r)
+            s.has_logits = False
+
+    def _eos_id(self) -> int:
+        return self.cfg.vocab - 1
+
+    # -- convenience ----------------------------------------------------------------------------------
+    @torch.no_grad()
+    def generate_ids(self, prompt: Seq[int], max_tokens: int, temperature: float = 1.0, top_p: float = 1.0,
+                     top_k: int = 0, seed: int = 0, stop_on_eos: bool = True, ctx: Optional[Context] = None,
+                     on_tokens: Optional[Callable[[List[int]], None]] = None) -> List[int]:
+        seq = self.new_sequence()
+        try:
+            self.prefill([seq], [list(prompt)])
+            p = SamplingParams(max_tokens, temperature, top_p, top_k, seed, stop_on_eos)
+            cb = (lambda i, ids: on_tokens(ids)) if on_tokens else None
+            return self.decode([seq], [p], ctx, cb)[0]
+        finally:
+            self.free_sequence(seq)
+
+    @torch.no_grad()
+    def generate_batch(self, prompts: List[List[int]], params: List[SamplingParams], ctx: Optional[Context] = None,
+                       on_tokens=None) -> List[List[int]]:
+        seqs = [self.new_sequence() for _ in prompts]
+        try:
+            self.prefill(seqs, prompts)
+            return self.decode(seqs, params, ctx, on_tokens)
+        finally:
+            for s in seqs:
+                self.free_sequence(s)
+
+    def synchronize(self) -> None:
+        if self.stream is not None:
+            self.stream.synchronize()
+
+    def memory_bytes(self) -> int:
+        return self.w.nbytes() + 2 * self.k_cache.numel() * 2

@@ -1,0 +1,149 @@
+"""Decoder-only transformer weights for the Llama-3 / Mixtral / Phi-3 families (T1).
+
+All three families share one engine-facing layout, chosen for the kernels rather than for
+checkpoint compatibility:
+  * ``w_qkv``  [q + 2 kv, H]  fused Q|K|V rows (one GEMV/GEMM per layer);
+  * ``w_o``    [H, q];
+  * ``w_gu``   [2 I, H] gate/up rows INTERLEAVED (row 2i = gate_i, 2i + 1 = up_i) so the GEMV
+    epilogue produces silu(gate) * up directly and a TP shard is a contiguous row range;
+  * ``w_down`` [H, I];
+  * MoE (Mixtral): ``w_router`` [E, H], ``w_gu`` [E, 2I, H], ``w_down`` [E, H, I];
+  * ``embed`` [V, H] (replicated under TP), ``lm_head`` [V, H] (vocab-parallel under TP).
+Weights are random-init from a seed (no checkpoints offline). Each tensor is generated in full
+from its own (seed, name)-derived generator and then sliced to this rank's shard, so TP=1 and
+TP=n models are the SAME model (tested on CPU with gloo).
+"""
+
+from __future__ import annotations
+
+import math
+import zlib
+from typing import List, Optional
+
+import torch
+
+from ..parallel.comm import TPGroup, shard_range
+from .config import ModelConfig
+
+
+class LayerWeights:
+    __slots__ = ("ln1", "ln2", "w_qkv", "w_o", "w_gu", "w_down", "w_router")
+
+    def __init__(self):
+        for s in self.__slots__:
+            setattr(self, s, None)
+
+
+class TransformerWeights:
+    def __init__(self, cfg: ModelConfig, tp: TPGroup, device: torch.device, seed: int,
+                 init_scale: float = 1.0):
+        self.cfg = cfg
+        self.tp = tp
+        self.device = device
+        self.seed = seed
+        self.init_scale = init_scale
+        if cfg.n_heads % tp.size or cfg.n_kv_heads % tp.size or cfg.intermediate % tp.size or cfg.vocab % tp.size:
+            raise ValueError(f"{cfg.name}: not shardable with tp={tp.size}")
+        self.nh = cfg.n_heads // tp.size
+        self.nkv = cfg.n_kv_heads // tp.size
+        self.inter = cfg.intermediate // tp.size
+        self.vocab_local = cfg.vocab // tp.size
+        self.q_size = self.nh * cfg.head_dim
+        self.kv_size = self.nkv * cfg.head_dim
+        self.qkv_size = self.q_size + 2 * self.kv_size
+        self.layers: List[LayerWeights] = []
+        self._build()
+
+    # -- generation -------------------------------------------------------------------------
+    def _gen(self, name: str, shape, std: float, mean: float = 0.0) -> torch.Tensor:
+        s = (zlib.crc32(name.encode()) ^ (self.seed * 0x9E3779B1)) & 0x7FFFFFFFFFFF
+        g = torch.Generator(device=self.device)
+        g.manual_seed(s)
+        t = torch.randn(*shape, generator=g, device=self.device, dtype=torch.float32)
+        if std != 1.0:
+            t.mul_(std)
+        if mean != 0.0:
+            t.add_(mean)
+        return t.to(torch.bfloat16)
+
+    def _linear(self, name: str, n_out: int, n_in: int) -> torch.Tensor:
+        return self._gen(name, (n_out, n_in), self.init_scale / math.sqrt(n_in))
+
+    def _build(self) -> None:
+        c, r, n = self.cfg, self.tp.rank, self.tp.size
+        D = c.head_dim
+        with torch.no_grad():
+            self.embed = self._gen("embed", (c.vocab, c.hidden), 1.0)
+            self.final_norm = self._gen("final_norm", (c.hidden,), 0.02, 1.0)
+            lm = self._linear("lm_head", c.vocab, c.hidden)
+            v0, v1 = shard_range(c.vocab, r, n)
+            self.lm_head = lm[v0:v1].contiguous()
+            del lm
+            for i in range(c.n_layers):
+                L = LayerWeights()
+                p = f"layers.{i}."
+                L.ln1 = self._gen(p + "ln1", (c.hidden,), 0.02, 1.0)
+                L.ln2 = self._gen(p + "ln2", (c.hidden,), 0.02, 1.0)
+                qkv = self._linear(p + "w_qkv", c.qkv_size, c.hidden)
+                q0, q1 = shard_range(c.n_heads, r, n)
+                k0, k1 = shard_range(c.n_kv_heads, r, n)
+                qs = qkv[q0 * D:q1 * D]
+                ks = qkv[c.q_size + k0 * D:c.q_size + k1 * D]
+                vs = qkv[c.q_size + c.kv_size + k0 * D:c.q_size + c.kv_size + k1 * D]
+                L.w_qkv = torch.cat([qs, ks, vs], 0).contiguous()
+                del qkv
+                wo = self._linear(p + "w_o", c.hidden, c.q_size)
+                L.w_o = wo[:, q0 * D:q1 * D].contiguous()
+                del wo
+                i0, i1 = shard_range(c.intermediate, r, n)
+                if c.is_moe:
+                    L.w_router = self._linear(p + "w_router", c.n_experts, c.hidden)
+                    gus, downs = [], []
+                    for e in range(c.n_experts):
+                        gu = self._linear(p + f"experts.{e}.w_gu", 2 * c.intermediate, c.hidden)
+                        gus.append(gu[2 * i0:2 * i1])
+                        dn = self._linear(p + f"experts.{e}.w_down", c.hidden, c.intermediate)
+                        downs.append(dn[:, i0:i1])
+                    L.w_gu = torch.stack(gus).contiguous()
+                    L.w_down = torch.stack(downs).contiguous()
+                    del gus, downs
+                else:
+                    gu = self._linear(p + "w_gu", 2 * c.intermediate, c.hidden)
+                    L.w_gu = gu[2 * i0:2 * i1].contiguous()
+                    del gu
+                    dn = self._linear(p + "w_down", c.hidden, c.intermediate)
+                    L.w_down = dn[:, i0:i1].contiguous()
+                    del dn
+                self.layers.append(L)
+
+    def to(self, device) -> "TransformerWeights":
+        """Move every tensor (in place) to ``device``; returns self."""
+        device = torch.device(device)
+        self.device = device
+        self.embed = self.embed.to(device)
+        self.final_norm = self.final_norm.to(device)
+        self.lm_head = self.lm_head.to(device)
+        for L in self.layers:
+            for s in LayerWeights.__slots__:
+                t = getattr(L, s)
+                if t is not None:
+                    setattr(L, s, t.to(device))
+        return self
+
+    def nbytes(self) -> int:
+        tot = self.embed.numel() + self.final_norm.numel() + self.lm_head.numel()
+        for L in self.layers:
+            for s in LayerWeights.__slots__:
+                t = getattr(L, s)
+                if t is not None:
+                    tot += t.numel()
+        return tot * 2
+
+
+def full_reference_weights(cfg: ModelConfig, seed: int, device="cpu", init_scale: float = 1.0) -> TransformerWeights:
+    return TransformerWeights(cfg, TPGroup.single(), torch.device(device), seed, init_scale)
+
+
+def split_for_rank(full: Optional[TransformerWeights], cfg: ModelConfig, tp: TPGroup, device, seed: int,
+                   init_scale: float = 1.0) -> TransformerWeights:
+    return TransformerWeights(cfg, tp, torch.device(device), seed, init_scale)

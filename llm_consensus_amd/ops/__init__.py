@@ -182,6 +182,8 @@ def sample(logits, inv_temp, top_k, top_p, seeds, positions, next_tok, workspace
 
 
 def _advance_cpu(tok, tokens_in, positions, seq_lens, slots, block_tables, bs, out_tokens, out_count):
+    if tokens_in is None:
+        return
     B = tok.shape[0]
     for b in range(B):
         t = int(tok[b])

@@ -1,0 +1,66 @@
+"""Tensor-parallel communication.
+
+One process per GPU; a TP group is a ``torch.distributed`` sub-group (backend "nccl" = RCCL over
+xGMI on ROCm, "gloo" for CPU tests). The row-parallel reductions use the *residual-folding*
+trick: rank 0 adds its partial product onto the residual stream, the other ranks write their
+partial product into the same buffer, and ONE in-place all-reduce yields
+``h + sum_r partial_r`` — no separate residual-add kernel and no extra buffer per layer.
+"""
+
+from __future__ import annotations
+
+from typing import Optional
+
+import torch
+import torch.distributed as dist
+
+
+class TPGroup:
+    """Rank/size of a model's tensor-parallel group (size 1 = no communication)."""
+
+    def __init__(self, group: Optional["dist.ProcessGroup"] = None, rank: int = 0, size: int = 1):
+        self.group = group
+        self.rank = rank
+        self.size = size
+
+    @staticmethod
+    def single() -> "TPGroup":
+        return TPGroup(None, 0, 1)
+
+    @staticmethod
+    def from_group(group) -> "TPGroup":
+        return TPGroup(group, dist.get_rank(group), dist.get_world_size(group))
+
+    @property
+    def is_leader(self) -> bool:
+        return self.rank == 0
+
+    def all_reduce_(self, t: torch.Tensor) -> torch.Tensor:
+        if self.size > 1:
+            dist.all_reduce(t, group=self.group)
+        return t
+
+    def all_gather_rows(self, t: torch.Tensor, out: torch.Tensor) -> torch.Tensor:
+        """Gather [B, n] shards into [size, B, n] (rank-major)."""
+        if self.size == 1:
+            out.view_as(t).copy_(t)
+            return out
+        dist.all_gather_into_tensor(out, t.contiguous(), group=self.group)
+        return out
+
+    def broadcast_(self, t: torch.Tensor, src_rank_in_group: int = 0) -> torch.Tensor:
+        if self.size > 1:
+            src = dist.get_global_rank(self.group, src_rank_in_group) if self.group is not None else src_rank_in_group
+            dist.broadcast(t, src=src, group=self.group)
+        return t
+
+    def barrier(self) -> None:
+        if self.size > 1:
+            dist.barrier(group=self.group)
+
+
+def shard_range(n: int, rank: int, size: int):
+    if n % size != 0:
+        raise ValueError(f"dimension {n} not divisible by tp={size}")
+    s = n // size
+    return rank * s, (rank + 1) * s

@@ -1,0 +1,110 @@
+"""Engine on a real MI355X: HIP path vs the CPU oracle path on identical weights, HIP-graph
+replay vs eager decode, and prefill/decode consistency (SURVEY.md §4.2 "Model forward")."""
+
+import copy
+
+import pytest
+import torch
+
+from llm_consensus_amd.engine import Engine, EngineConfig, SamplingParams
+from llm_consensus_amd.models.config import FAMILIES
+from llm_consensus_amd.models.transformer import TransformerWeights
+from llm_consensus_amd.parallel.comm import TPGroup
+
+pytestmark = pytest.mark.gpu
+
+
+def _pair(name, ctx=512, **kw):
+    cfg = FAMILIES[name]
+    wc = TransformerWeights(cfg, TPGroup.single(), torch.device("cpu"), seed=3)
+    wg = copy.deepcopy(wc)
+    ecpu = Engine(cfg, EngineConfig(device="cpu", max_context=ctx), weights=wc)
+    egpu = Engine(cfg, EngineConfig(device="cuda:0", max_context=ctx, **kw), weights=wg)
+    return cfg, ecpu, egpu
+
+
+@pytest.mark.parametrize("name", ["llama-tiny", "mixtral-tiny", "phi3-tiny", "llama-small"])
+def test_prefill_logits_match_oracle(cuda, name):
+    cfg, ecpu, egpu = _pair(name)
+    prompt = [(i * 37) % (cfg.vocab - 300) + 256 for i in range(150)]
+    s1 = ecpu.new_sequence()
+    ecpu.prefill([s1], [prompt])
+    s2 = egpu.new_sequence()
+    egpu.prefill([s2], [prompt])
+    torch.cuda.synchronize()
+    lc = ecpu.logits[0].float()
+    lg = egpu.logits[0].float().cpu()
+    err = (lc - lg).abs().max().item()
+    assert err < 0.05 * max(1.0, lc.abs().max().item()), err
+    # first greedy token agrees unless the top-2 gap is within the error
+    top2 = torch.topk(lc, 2).values
+    if (top2[0] - top2[1]).item() > 2 * err:
+        assert int(lc.argmax()) == int(lg.argmax())
+
+
+@pytest.mark.parametrize("name", ["llama-tiny", "mixtral-tiny", "phi3-tiny"])
+def test_decode_logits_match_oracle(cuda, name):
+    """Teacher-forced: after greedy decode on GPU, the CPU oracle re-prefilling the same tokens
+    must give logits close to the GPU decode path's final logits."""
+    cfg, ecpu, egpu = _pair(name)
+    prompt = [(i * 53) % (cfg.vocab - 300) + 256 for i in range(40)]
+    gen = egpu.generate_ids(prompt, 12, temperature=0.0, stop_on_eos=False)
+    assert len(gen) == 12
+    s = ecpu.new_sequence()
+    ecpu.prefill([s], [prompt + gen[:-1]])
+    ref_next = int(ecpu.logits[0].argmax())
+    lc = ecpu.logits[0]
+    top2 = torch.topk(lc, 2).values
+    if (top2[0] - top2[1]).item() > 0.1:
+        assert ref_next == gen[-1]
+
+
+def test_graph_equals_eager(cuda):
+    cfg = FAMILIES["llama-small"]
+    w = TransformerWeights(cfg, TPGroup.single(), torch.device("cuda:0"), seed=9)
+    eg = Engine(cfg, EngineConfig(device="cuda:0", max_context=1024, use_graphs=True), weights=w)
+    ee = Engine(cfg, EngineConfig(device="cuda:0", max_context=1024, use_graphs=False), weights=w)
+    prompt = list(range(500, 600))
+    a = eg.generate_ids(prompt, 40, temperature=0.9, seed=42, stop_on_eos=False)
+    b = ee.generate_ids(prompt, 40, temperature=0.9, seed=42, stop_on_eos=False)
+    assert a == b
+    # replay again: graphs are reusable across requests and give identical streams
+    c = eg.generate_ids(prompt, 40, temperature=0.9, seed=42, stop_on_eos=False)
+    assert c == a
+
+
+def test_batched_rows_equal_single(cuda):
+    """Replica batching (M = 2 GEMV rows) gives the same tokens as two single-row runs."""
+    cfg = FAMILIES["llama-small"]
+    w = TransformerWeights(cfg, TPGroup.single(), torch.device("cuda:0"), seed=11)
+    e = Engine(cfg, EngineConfig(device="cuda:0", max_context=1024, max_batch=2), weights=w)
+    p1, p2 = list(range(300, 350)), list(range(700, 790))
+    sp = [SamplingParams(24, 0.7, 1.0, 0, 5, False), SamplingParams(24, 0.7, 1.0, 0, 6, False)]
+    both = e.generate_batch([p1, p2], sp)
+    one = e.generate_ids(p1, 24, 0.7, seed=5, stop_on_eos=False)
+    two = e.generate_ids(p2, 24, 0.7, seed=6, stop_on_eos=False)
+    # GEMV M=2 vs M=1 accumulate identically per row; attention per row is independent
+    assert both[0] == one and both[1] == two
+
+
+def test_topk_topp_decode(cuda):
+    cfg = FAMILIES["llama-tiny"]
+    e = Engine(cfg, EngineConfig(device="cuda:0", max_context=512, seed=1))
+    out = e.generate_ids(list(range(300, 320)), 16, temperature=1.0, top_p=0.9, top_k=20, seed=3, stop_on_eos=False)
+    assert len(out) == 16 and all(0 <= t < cfg.vocab for t in out)
+
+
+def test_long_context_chunked_prefill(cuda):
+    """Prefill in chunks (incl. across the attention split-KV chunk boundary) == one-shot prefill."""
+    cfg = FAMILIES["llama-small"]
+    w = TransformerWeights(cfg, TPGroup.single(), torch.device("cuda:0"), seed=13)
+    a = Engine(cfg, EngineConfig(device="cuda:0", max_context=4096, prefill_chunk=8192), weights=w)
+    b = Engine(cfg, EngineConfig(device="cuda:0", max_context=4096, prefill_chunk=700), weights=w)
+    prompt = [(i * 7919) % 30000 + 256 for i in range(2500)]
+    sa, sb = a.new_sequence(), b.new_sequence()
+    a.prefill([sa], [prompt])
+    b.prefill([sb], [prompt[:1000]], want_logits=False)
+    b.prefill([sb], [prompt[1000:]])
+    torch.cuda.synchronize()
+    err = (a.logits[0] - b.logits[0]).abs().max().item()
+    assert err < 0.05 * a.logits[0].abs().max().item()

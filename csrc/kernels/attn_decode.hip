@@ -1,27 +1,39 @@
-// K5: paged attention DECODE (one query token per sequence), split-KV + reduce.
+// K5: paged attention DECODE (one query token per sequence), split-KV with an in-kernel reduce.
 //
 // Memory-bound on the K/V stream (cdna_hip_programming.md App. B "Attention decode"): K/V go
 // straight to VGPRs, 16 B per lane. Geometry:
-//   grid (max_chunks, nkv, B), 256 threads = 4 waves; a block owns one kv head and one chunk of
-//   CHUNK context tokens, and ALL G = nh/nkv query heads of that kv head (GQA: K/V read once for
-//   the group). A 16-lane group holds one key row (D <= 128 -> 8 bf16 per lane), so a wave
-//   scores 4 keys per instruction; each 16-lane group runs its own online softmax, merged at
-//   the end with xor-shuffles (across groups) and LDS (across waves).
-// The grid is sized for the engine's maximum context so the launch is HIP-graph replayable;
-// chunks past seq_len exit immediately. With a single live chunk the block writes the final
-// bf16 output itself; otherwise f32 partials (unnormalised acc, running max m, sum l) go to a
-// workspace and attn_decode_reduce merges them.
+//   grid (grid_chunks, nkv, B), 256 threads = 4 waves; a block owns one kv head and one chunk of
+//   `chunk` context tokens (64 by default: a 1k-token context already yields 128 blocks for an
+//   8-kv-head model), and ALL G = nh/nkv query heads of that kv head (GQA: K/V read once for the
+//   group). A 16-lane group holds one key row (D <= 128 -> 8 bf16 per lane), so a wave scores
+//   4 keys per instruction; each 16-lane group runs its own online softmax, merged with
+//   xor-shuffles (across groups) and LDS (across waves).
+// Cross-block reduce WITHOUT a second launch (Guideline 16, "valid forms", row 1): every block
+// writes its partial (unnormalised acc, m, l) with write-through (sc1, relaxed agent-scope)
+// stores, drains them (s_waitcnt vmcnt(0)) in every storing wave, then one lane takes a ticket
+// on the (sequence, kv head) counter with an agent-scope atomic add; the block that draws the
+// last ticket reads all partials with sc1 loads, writes the bf16 output and re-arms the counter.
+// Placement-independent: no assumption on which XCD/CU runs which chunk.
+// The grid is sized per context bucket by the host (one captured decode graph per bucket); chunks
+// past seq_len exit immediately and take no ticket.
 #include "common.h"
 
 namespace llmc {
 
 constexpr float kNegBig = -1e30f;
 
+__device__ __forceinline__ void st_sc1(float* p, float v) {
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ float ld_sc1(const float* p) {
+  return __hip_atomic_load(const_cast<float*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
 template <int G>
 __global__ __launch_bounds__(256) void attn_decode_kernel(
     const bf16_t* __restrict__ q, int q_stride, const bf16_t* __restrict__ k_cache,
     const bf16_t* __restrict__ v_cache, const int32_t* __restrict__ block_tables, int bt_stride,
-    const int32_t* __restrict__ seq_lens, float* __restrict__ part_o, float* __restrict__ part_ml,
+    const int32_t* __restrict__ seq_lens, float* __restrict__ part, int* __restrict__ counters,
     bf16_t* __restrict__ out, int out_stride, int nkv, int D, int bs, int chunk, int max_chunks, float scale) {
   const int c = blockIdx.x, kvh = blockIdx.y, b = blockIdx.z;
   const int L = seq_lens[b];
@@ -29,7 +41,6 @@ __global__ __launch_bounds__(256) void attn_decode_kernel(
   if (start >= L) return;
   const int end = min(start + chunk, L);
   const int nchunks = (L + chunk - 1) / chunk;
-  const int nh = nkv * G;
 
   const int tid = threadIdx.x, wave = tid / kWave, lane = tid % kWave;
   const int grp = lane / 16, sub = lane % 16;
@@ -59,22 +70,29 @@ __global__ __launch_bounds__(256) void attn_decode_kernel(
   }
 
   const int32_t* bt = block_tables + static_cast<int64_t>(b) * bt_stride;
-  // token t handled by (wave, grp): t = start + wave*4 + grp + 16*i
-  for (int t0 = start + wave * 4; t0 < end; t0 += 32) {
-    u32x4 kv[2], vv[2];
-    bool ok[2];
+  // token t handled by (wave, grp): t = start + wave*4 + grp + 16*i; UN tokens per lane group are
+  // loaded at once (all page lookups first, then all K/V loads: two memory round trips total
+  // for a 64-token chunk instead of one pair per token).
+  constexpr int UN = 4;
+  for (int t0 = start + wave * 4; t0 < end; t0 += 16 * UN) {
+    u32x4 kv[UN], vv[UN];
+    bool ok[UN];
+    int64_t page[UN];
 #pragma unroll
-    for (int u = 0; u < 2; ++u) {
+    for (int u = 0; u < UN; ++u) {
       const int t = t0 + grp + u * 16;
       ok[u] = t < end;
-      const int tt = ok[u] ? t : start;
-      const int64_t page = bt[tt / bs];
-      const int64_t off = ((page * nkv + kvh) * bs + (tt % bs)) * D + d0;
+      page[u] = bt[(ok[u] ? t : start) / bs];
+    }
+#pragma unroll
+    for (int u = 0; u < UN; ++u) {
+      const int tt = ok[u] ? t0 + grp + u * 16 : start;
+      const int64_t off = ((page[u] * nkv + kvh) * bs + (tt % bs)) * D + d0;
       kv[u] = *reinterpret_cast<const u32x4*>(k_cache + off);
       vv[u] = *reinterpret_cast<const u32x4*>(v_cache + off);
     }
 #pragma unroll
-    for (int u = 0; u < 2; ++u) {
+    for (int u = 0; u < UN; ++u) {
       float vf[8];
       unpack8(vv[u], vf);
 #pragma unroll
@@ -112,7 +130,7 @@ __global__ __launch_bounds__(256) void attn_decode_kernel(
     }
   }
 
-  // merge the 4 waves through LDS: [wave][g][D + 2]
+  // merge the 4 waves through LDS: red[wave][g][D + 2]; then scratch for the reducer
   extern __shared__ __attribute__((aligned(16))) char smem[];
   float* red = reinterpret_cast<float*>(smem);
   const int stride = D + 2;
@@ -131,7 +149,8 @@ __global__ __launch_bounds__(256) void attn_decode_kernel(
     }
   }
   __syncthreads();
-  // thread -> (g, d) pairs
+  const int nh = nkv * G;
+  float* pb = part + ((static_cast<int64_t>(b) * nkv + kvh) * max_chunks) * G * stride;
   for (int idx = tid; idx < G * D; idx += 256) {
     const int g = idx / D, d = idx % D;
     float mx = kNegBig;
@@ -145,77 +164,113 @@ __global__ __launch_bounds__(256) void attn_decode_kernel(
       lsum += r[D + 1] * sc;
       o += r[d] * sc;
     }
-    const int h = kvh * G + g;
     if (nchunks == 1) {
-      out[static_cast<int64_t>(b) * out_stride + h * D + d] = f32_to_bf16(o / lsum);
+      out[static_cast<int64_t>(b) * out_stride + (kvh * G + g) * D + d] = f32_to_bf16(o / lsum);
     } else {
-      const int64_t pi = (static_cast<int64_t>(b) * nh + h) * max_chunks + c;
-      part_o[pi * D + d] = o;
+      float* pc = pb + (static_cast<int64_t>(c) * G + g) * stride;
+      st_sc1(pc + d, o);
       if (d == 0) {
-        part_ml[pi * 2] = mx;
-        part_ml[pi * 2 + 1] = lsum;
+        st_sc1(pc + D, mx);
+        st_sc1(pc + D + 1, lsum);
       }
     }
   }
-}
+  if (nchunks == 1) return;
 
-// grid (nh, B), 128 threads: merge chunk partials of sequences with > 1 live chunk.
-__global__ __launch_bounds__(128) void attn_decode_reduce_kernel(const float* __restrict__ part_o,
-                                                                 const float* __restrict__ part_ml,
-                                                                 const int32_t* __restrict__ seq_lens,
-                                                                 bf16_t* __restrict__ out, int out_stride, int nh,
-                                                                 int D, int chunk, int max_chunks) {
-  const int h = blockIdx.x, b = blockIdx.y;
-  const int L = seq_lens[b];
-  const int nchunks = (L + chunk - 1) / chunk;
-  if (nchunks <= 1) return;
-  const int64_t base = (static_cast<int64_t>(b) * nh + h) * max_chunks;
-  float mx = kNegBig;
-  for (int c = 0; c < nchunks; ++c) mx = fmaxf(mx, part_ml[(base + c) * 2]);
-  for (int d = threadIdx.x; d < D; d += 128) {
-    float lsum = 0.f, o = 0.f;
-    for (int c = 0; c < nchunks; ++c) {
-      const float sc = __expf(part_ml[(base + c) * 2] - mx);
-      lsum += part_ml[(base + c) * 2 + 1] * sc;
-      o += part_o[(base + c) * D + d] * sc;
-    }
-    out[static_cast<int64_t>(b) * out_stride + h * D + d] = f32_to_bf16(o / lsum);
+  // ---- ticket: the last-arriving chunk block reduces ----
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every storing wave drains its sc1 stores
+  __syncthreads();
+  int* flag = reinterpret_cast<int*>(red + 4 * G * stride);
+  int* ctr = counters + b * nkv + kvh;
+  if (tid == 0) {
+    const int old = __hip_atomic_fetch_add(ctr, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    *flag = (old == nchunks - 1) ? 1 : 0;
   }
+  __syncthreads();
+  if (*flag == 0) return;
+
+  // Reducer. Phase 1: every (g, chunk) m and l in parallel (one sc1 round trip) into LDS.
+  float* scl = red + 4 * G * stride + 4;  // [G][nchunks]: m, then exp(m - M)
+  float* lv = scl + G * nchunks;          // [G][nchunks]: l
+  float* Mg = lv + G * nchunks;           // [G]
+  float* Lg = Mg + G;                     // [G]
+  for (int i = tid; i < G * nchunks; i += 256) {
+    const int g = i / nchunks, cc = i % nchunks;
+    const float* pc = pb + (static_cast<int64_t>(cc) * G + g) * stride;
+    scl[i] = ld_sc1(pc + D);
+    lv[i] = ld_sc1(pc + D + 1);
+  }
+  __syncthreads();
+  if (tid < G) {
+    float mx = kNegBig;
+    for (int cc = 0; cc < nchunks; ++cc) mx = fmaxf(mx, scl[tid * nchunks + cc]);
+    float ls = 0.f;
+    for (int cc = 0; cc < nchunks; ++cc) ls += lv[tid * nchunks + cc] * __expf(scl[tid * nchunks + cc] - mx);
+    Mg[tid] = mx;
+    Lg[tid] = ls;
+  }
+  __syncthreads();
+  for (int i = tid; i < G * nchunks; i += 256) scl[i] = __expf(scl[i] - Mg[i / nchunks]);
+  __syncthreads();
+  // Phase 2: outputs; chunk partials loaded 16 at a time with clamped (branch-free) indices so
+  // all loads of a batch are in flight together (no per-load vmcnt(0)).
+  for (int idx = tid; idx < G * D; idx += 256) {
+    const int g = idx / D, d = idx % D;
+    float o = 0.f;
+    for (int c0 = 0; c0 < nchunks; c0 += 16) {
+      float v[16];
+#pragma unroll
+      for (int j = 0; j < 16; ++j) {
+        const int cc = min(c0 + j, nchunks - 1);
+        v[j] = ld_sc1(pb + (static_cast<int64_t>(cc) * G + g) * stride + d);
+      }
+#pragma unroll
+      for (int j = 0; j < 16; ++j) o += (c0 + j < nchunks) ? v[j] * scl[g * nchunks + c0 + j] : 0.f;
+    }
+    out[static_cast<int64_t>(b) * out_stride + (kvh * G + g) * D + d] = f32_to_bf16(o / Lg[g]);
+  }
+  if (tid == 0) __hip_atomic_store(ctr, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  (void)nh;
 }
 
 template <int G>
-static void launch_decode(dim3 grid, size_t lds, hipStream_t s, const void* q, int q_stride, const void* kc,
-                          const void* vc, const void* bt, int bt_stride, const void* sl, void* po, void* pml,
-                          void* out, int out_stride, int nkv, int D, int bs, int chunk, int max_chunks, float scale) {
-  attn_decode_kernel<G><<<grid, 256, lds, s>>>((const bf16_t*)q, q_stride, (const bf16_t*)kc, (const bf16_t*)vc,
-                                               (const int32_t*)bt, bt_stride, (const int32_t*)sl, (float*)po,
-                                               (float*)pml, (bf16_t*)out, out_stride, nkv, D, bs, chunk,
-                                               max_chunks, scale);
+static int launch_decode(dim3 grid, size_t lds, hipStream_t s, const void* q, int q_stride, const void* kc,
+                         const void* vc, const void* bt, int bt_stride, const void* sl, void* part, void* ctr,
+                         void* out, int out_stride, int nkv, int D, int bs, int chunk, int max_chunks, float scale) {
+  auto kern = attn_decode_kernel<G>;
+  static bool attr = false;
+  if (lds > 64 * 1024 && !attr) {
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize,
+                              160 * 1024);
+    attr = true;
+  }
+  kern<<<grid, 256, lds, s>>>((const bf16_t*)q, q_stride, (const bf16_t*)kc, (const bf16_t*)vc, (const int32_t*)bt,
+                              bt_stride, (const int32_t*)sl, (float*)part, (int*)ctr, (bf16_t*)out, out_stride, nkv,
+                              D, bs, chunk, max_chunks, scale);
+  return static_cast<int>(hipGetLastError());
 }
 
 }  // namespace llmc
 
 using namespace llmc;
 
+// part: f32 workspace [B, nkv, max_chunks, G, D + 2]; counters: int32 [B, nkv], zero-initialised
+// once (each launch re-arms them). grid_chunks <= max_chunks bounds the context of this launch.
 extern "C" int llmc_attn_decode(const void* q, int q_stride, const void* k_cache, const void* v_cache,
-                                const void* block_tables, int bt_stride, const void* seq_lens, void* part_o,
-                                void* part_ml, void* out, int out_stride, int B, int nh, int nkv, int D, int bs,
-                                int chunk, int max_chunks, float scale, hipStream_t s) {
-  if (D % 8 != 0 || D > 128 || nh % nkv != 0) return -1;
+                                const void* block_tables, int bt_stride, const void* seq_lens, void* part,
+                                void* counters, void* out, int out_stride, int B, int nh, int nkv, int D, int bs,
+                                int chunk, int grid_chunks, int max_chunks, float scale, hipStream_t s) {
+  if (D % 8 != 0 || D > 128 || nh % nkv != 0 || grid_chunks > max_chunks) return -1;
   const int G = nh / nkv;
-  dim3 grid(max_chunks, nkv, B);
-  const size_t lds = static_cast<size_t>(4) * G * (D + 2) * sizeof(float);
+  dim3 grid(grid_chunks, nkv, B);
+  const size_t lds =
+      (static_cast<size_t>(4) * G * (D + 2) + 4 + static_cast<size_t>(G) * (2 * max_chunks + 2)) * sizeof(float);
+  if (lds > 160 * 1024) return -3;
   switch (G) {
-    case 1: launch_decode<1>(grid, lds, s, q, q_stride, k_cache, v_cache, block_tables, bt_stride, seq_lens, part_o, part_ml, out, out_stride, nkv, D, bs, chunk, max_chunks, scale); break;
-    case 2: launch_decode<2>(grid, lds, s, q, q_stride, k_cache, v_cache, block_tables, bt_stride, seq_lens, part_o, part_ml, out, out_stride, nkv, D, bs, chunk, max_chunks, scale); break;
-    case 4: launch_decode<4>(grid, lds, s, q, q_stride, k_cache, v_cache, block_tables, bt_stride, seq_lens, part_o, part_ml, out, out_stride, nkv, D, bs, chunk, max_chunks, scale); break;
-    case 8: launch_decode<8>(grid, lds, s, q, q_stride, k_cache, v_cache, block_tables, bt_stride, seq_lens, part_o, part_ml, out, out_stride, nkv, D, bs, chunk, max_chunks, scale); break;
+    case 1: return launch_decode<1>(grid, lds, s, q, q_stride, k_cache, v_cache, block_tables, bt_stride, seq_lens, part, counters, out, out_stride, nkv, D, bs, chunk, max_chunks, scale);
+    case 2: return launch_decode<2>(grid, lds, s, q, q_stride, k_cache, v_cache, block_tables, bt_stride, seq_lens, part, counters, out, out_stride, nkv, D, bs, chunk, max_chunks, scale);
+    case 4: return launch_decode<4>(grid, lds, s, q, q_stride, k_cache, v_cache, block_tables, bt_stride, seq_lens, part, counters, out, out_stride, nkv, D, bs, chunk, max_chunks, scale);
+    case 8: return launch_decode<8>(grid, lds, s, q, q_stride, k_cache, v_cache, block_tables, bt_stride, seq_lens, part, counters, out, out_stride, nkv, D, bs, chunk, max_chunks, scale);
     default: return -2;
   }
-  hipError_t e = hipGetLastError();
-  if (e != hipSuccess) return static_cast<int>(e);
-  attn_decode_reduce_kernel<<<dim3(nh, B), 128, 0, s>>>((const float*)part_o, (const float*)part_ml,
-                                                         (const int32_t*)seq_lens, (bf16_t*)out, out_stride, nh, D,
-                                                         chunk, max_chunks);
-  return static_cast<int>(hipGetLastError());
 }

@@ -19,10 +19,12 @@ int llmc_embedding(const void*, const void*, void*, int, int, int, hipStream_t);
 int llmc_silu_mul_interleaved(const void*, void*, int, int, hipStream_t);
 int llmc_gemv(int, const void*, int, const void*, float, const void*, void*, int, int, int, int, hipStream_t);
 int llmc_gemm(const void*, int, const void*, int, void*, int, int, int, int, int, hipStream_t);
-int llmc_rope_kv_write(void*, int, const void*, const void*, const void*, void*, void*, const void*, int, int, int,
-                       int, int, hipStream_t);
+int llmc_rope_kv_write(const void*, int, void*, int, const void*, const void*, const void*, void*, void*, const void*,
+                       int, int, int, int, int, hipStream_t);
 int llmc_attn_decode(const void*, int, const void*, const void*, const void*, int, const void*, void*, void*, void*,
-                     int, int, int, int, int, int, int, int, float, hipStream_t);
+                     int, int, int, int, int, int, int, int, int, float, hipStream_t);
+int llmc_gemv_qkv_rope(int, const void*, int, const void*, float, const void*, int, int, void*, int, void*, void*,
+                       const void*, const void*, const void*, const void*, int, int, int, int, hipStream_t);
 int llmc_attn_prefill(const void*, int, const void*, const void*, const void*, int, const void*, const void*,
                       const void*, void*, int, int, int, int, int, int, int, float, hipStream_t);
 int llmc_sample(const void*, int64_t, int, int, const void*, const void*, const void*, const void*, const void*, void*,
@@ -64,16 +66,24 @@ PYBIND11_MODULE(_llmc_hip, m) {
   m.def("gemm", [](ptr A, int lda, ptr W, int ldw, ptr C, int ldc, int M, int N, int K, int epi, ptr s) {
     check(llmc_gemm(P(A), lda, P(W), ldw, P(C), ldc, M, N, K, epi, S(s)), "gemm");
   });
-  m.def("rope_kv_write", [](ptr qkv, int qs, ptr pos, ptr cos_t, ptr sin_t, ptr kc, ptr vc, ptr slots, int T, int nh,
-                            int nkv, int D, int bs, ptr s) {
-    check(llmc_rope_kv_write(P(qkv), qs, P(pos), P(cos_t), P(sin_t), P(kc), P(vc), P(slots), T, nh, nkv, D, bs, S(s)),
+  m.def("rope_kv_write", [](ptr qkv, int qs, ptr qo, int qos, ptr pos, ptr cos_t, ptr sin_t, ptr kc, ptr vc,
+                            ptr slots, int T, int nh, int nkv, int D, int bs, ptr s) {
+    check(llmc_rope_kv_write(P(qkv), qs, P(qo), qos, P(pos), P(cos_t), P(sin_t), P(kc), P(vc), P(slots), T, nh, nkv, D,
+                             bs, S(s)),
           "rope_kv_write");
   });
-  m.def("attn_decode", [](ptr q, int qs, ptr kc, ptr vc, ptr bt, int bts, ptr sl, ptr po, ptr pml, ptr out, int os,
-                          int B, int nh, int nkv, int D, int bs, int chunk, int max_chunks, float scale, ptr s) {
-    check(llmc_attn_decode(P(q), qs, P(kc), P(vc), P(bt), bts, P(sl), P(po), P(pml), P(out), os, B, nh, nkv, D, bs,
-                           chunk, max_chunks, scale, S(s)),
+  m.def("attn_decode", [](ptr q, int qs, ptr kc, ptr vc, ptr bt, int bts, ptr sl, ptr part, ptr ctr, ptr out, int os,
+                          int B, int nh, int nkv, int D, int bs, int chunk, int grid_chunks, int max_chunks,
+                          float scale, ptr s) {
+    check(llmc_attn_decode(P(q), qs, P(kc), P(vc), P(bt), bts, P(sl), P(part), P(ctr), P(out), os, B, nh, nkv, D, bs,
+                           chunk, grid_chunks, max_chunks, scale, S(s)),
           "attn_decode");
+  });
+  m.def("gemv_qkv_rope", [](int M, ptr x, int xs, ptr nw, float eps, ptr W, int N, int K, ptr qo, int qos, ptr kc,
+                            ptr vc, ptr pos, ptr slots, ptr cos_t, ptr sin_t, int nh, int nkv, int D, int bs, ptr s) {
+    check(llmc_gemv_qkv_rope(M, P(x), xs, P(nw), eps, P(W), N, K, P(qo), qos, P(kc), P(vc), P(pos), P(slots),
+                             P(cos_t), P(sin_t), nh, nkv, D, bs, S(s)),
+          "gemv_qkv_rope");
   });
   m.def("attn_prefill", [](ptr q, int qs, ptr kc, ptr vc, ptr bt, int bts, ptr qst, ptr ql, ptr cl, ptr out, int os,
                            int B, int max_qlen, int nh, int nkv, int D, int bs, float scale, ptr s) {

@@ -1,55 +1,80 @@
-// K6 (decode class): skinny GEMM  y[m, n] = sum_k x[m, k] * W[n, k]   for M = 1..4 rows.
+// Launchers for the decode GEMV (kernel body: gemv_core.h).
 //
-// Batch-1 decode is HBM-bound weight streaming (8B = 15 GB/token), so this is
-// THE hot kernel. Design (cdna_hip_programming.md §5 row "GEMV / M <= 16"; MI355X_MICROARCH
-// rows nt-weights, launches-baseline):
-//  * W [N, K] bf16, K contiguous. A wave owns RPW output rows; lane l streams chunks
-//    c = l + 64 i (16 B = 8 bf16 each) of all RPW rows -> RPW*UNROLL independent 16 B loads in
-//    flight per lane, straight to VGPRs (no LDS round trip for W), non-temporal (read once).
-//  * x is staged ONCE per block in LDS (M*K bf16); every lane reads the same chunk index it
-//    loads from W, so ds_read_b128 addresses are lane-consecutive (conflict-free).
-//  * v_dot2_f32_bf16 does convert+multiply+accumulate of 2 elements per VALU op.
-//  * Fused prologue  PRO_NORM: x <- bf16(rmsnorm(x) * w_norm)  (the layer's input norm), so the
-//    decode layer needs no separate norm launch.
-//  * Fused epilogues: bf16 store | f32 store (logits) | in-place residual add h += W.x |
-//    SiLU-mul over interleaved gate/up rows (row 2i = gate_i, 2i+1 = up_i).
-#include "common.h"
-
+// Geometry per shape (measured on MI355X, profiles/): a batch-1 decode GEMV is a few-µs kernel,
+// so the grid must be a balanced multiple of the 256 CUs with enough waves in flight per CU:
+//   N >= 16384 (gate_up, lm_head):        256 threads x 4 rows/wave  (1792 / 8016 blocks)
+//   paired epilogues (SiLU, RoPE):        256 threads x 2 rows/wave  (qkv 6144 -> 768 blocks)
+//   K > 8192 (down_proj, K = 14336):      512 threads x 1 row/wave   (N 4096 -> 512 blocks)
+//   otherwise (o_proj):                   256 threads x 1 row/wave   (N 4096 -> 1024 blocks)
 #include "gemv_core.h"
 
 namespace llmc {
 
-template <int M, int PRO, int EPI>
-static int launch_gemv(const void* x, int x_stride, const void* nw, float eps, const void* W, void* out,
-                       int out_stride, int N, int K, hipStream_t s) {
-  constexpr int RPW = 4;
-  constexpr int UNROLL = (M <= 2) ? 4 : 2;
-  auto kern = gemv_kernel<M, RPW, UNROLL, PRO, EPI>;
-  const size_t lds = static_cast<size_t>(M) * K * sizeof(bf16_t) + M * kGemvWaves * sizeof(float);
+template <int M, int NT, int RPW, int PRO, int EPI>
+static int launch_gemv_g(const void* x, int x_stride, const void* nw, float eps, const void* W, void* out,
+                         int out_stride, int N, int K, const RopeEpi& rope, hipStream_t s) {
+  constexpr int UNROLL = RPW == 1 ? (M <= 2 ? 8 : 4) : (RPW == 2 ? 4 : (M <= 2 ? 4 : 2));
+  constexpr int WAVES = NT / kWave;
+  auto kern = gemv_kernel<M, NT, RPW, UNROLL, PRO, EPI, false>;
+  const size_t lds = static_cast<size_t>(M) * K * sizeof(bf16_t) + M * WAVES * sizeof(float);
   if (lds > 160 * 1024) return -2;
   static bool attr_set = false;
   if (lds > 64 * 1024 && !attr_set) {
     (void)hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize,
-                        160 * 1024);
+                              160 * 1024);
     attr_set = true;
   }
-  const int rows_per_block = kGemvWaves * RPW;
+  const int rows_per_block = WAVES * RPW;
   const int grid = (N + rows_per_block - 1) / rows_per_block;
-  kern<<<grid, kGemvThreads, lds, s>>>((const bf16_t*)x, x_stride, (const bf16_t*)nw, eps, (const bf16_t*)W, out,
-                                       out_stride, N, K, nullptr, 1);
+  kern<<<grid, NT, lds, s>>>((const bf16_t*)x, x_stride, (const bf16_t*)nw, eps, (const bf16_t*)W, out, out_stride, N,
+                             K, nullptr, 1, rope);
   return static_cast<int>(hipGetLastError());
+}
+
+template <int M, int PRO, int EPI>
+static int launch_gemv(const void* x, int x_stride, const void* nw, float eps, const void* W, void* out,
+                       int out_stride, int N, int K, const RopeEpi& rope, hipStream_t s) {
+  if (N >= 16384) return launch_gemv_g<M, 256, 4, PRO, EPI>(x, x_stride, nw, eps, W, out, out_stride, N, K, rope, s);
+  if constexpr (EPI == EPI_SILU || EPI == EPI_ROPE) {
+    return launch_gemv_g<M, 256, 2, PRO, EPI>(x, x_stride, nw, eps, W, out, out_stride, N, K, rope, s);
+  } else {
+    if (K > 8192) return launch_gemv_g<M, 512, 1, PRO, EPI>(x, x_stride, nw, eps, W, out, out_stride, N, K, rope, s);
+    return launch_gemv_g<M, 256, 1, PRO, EPI>(x, x_stride, nw, eps, W, out, out_stride, N, K, rope, s);
+  }
 }
 
 template <int PRO, int EPI>
 static int dispatch_m(int M, const void* x, int x_stride, const void* nw, float eps, const void* W, void* out,
-                      int out_stride, int N, int K, hipStream_t s) {
+                      int out_stride, int N, int K, const RopeEpi& rope, hipStream_t s) {
   switch (M) {
-    case 1: return launch_gemv<1, PRO, EPI>(x, x_stride, nw, eps, W, out, out_stride, N, K, s);
-    case 2: return launch_gemv<2, PRO, EPI>(x, x_stride, nw, eps, W, out, out_stride, N, K, s);
-    case 3: return launch_gemv<3, PRO, EPI>(x, x_stride, nw, eps, W, out, out_stride, N, K, s);
-    case 4: return launch_gemv<4, PRO, EPI>(x, x_stride, nw, eps, W, out, out_stride, N, K, s);
+    case 1: return launch_gemv<1, PRO, EPI>(x, x_stride, nw, eps, W, out, out_stride, N, K, rope, s);
+    case 2: return launch_gemv<2, PRO, EPI>(x, x_stride, nw, eps, W, out, out_stride, N, K, rope, s);
+    case 3: return launch_gemv<3, PRO, EPI>(x, x_stride, nw, eps, W, out, out_stride, N, K, rope, s);
+    case 4: return launch_gemv<4, PRO, EPI>(x, x_stride, nw, eps, W, out, out_stride, N, K, rope, s);
     default: return -3;
   }
+}
+
+static int gemv_dispatch(int M, const void* x, int x_stride, const void* norm_w, float eps, const void* W, void* out,
+                         int out_stride, int N, int K, int epi, const RopeEpi& rope, hipStream_t s) {
+  if (K % 8 != 0) return -1;
+  if ((epi == EPI_SILU || epi == EPI_ROPE) && (N % 2 != 0)) return -1;
+  const bool norm = norm_w != nullptr;
+#define LLMC_GEMV_CASE(E)                                                                                   \
+  case E:                                                                                                   \
+    return norm ? dispatch_m<PRO_NORM, E>(M, x, x_stride, norm_w, eps, W, out, out_stride, N, K, rope, s)   \
+                : dispatch_m<PRO_NONE, E>(M, x, x_stride, norm_w, eps, W, out, out_stride, N, K, rope, s);
+  switch (epi) {
+    LLMC_GEMV_CASE(EPI_BF16)
+    LLMC_GEMV_CASE(EPI_F32)
+    LLMC_GEMV_CASE(EPI_RESADD)
+    LLMC_GEMV_CASE(EPI_SILU)
+    case EPI_ROPE:
+      if (!norm) return -5;
+      return dispatch_m<PRO_NORM, EPI_ROPE>(M, x, x_stride, norm_w, eps, W, out, out_stride, N, K, rope, s);
+    default: return -4;
+  }
+#undef LLMC_GEMV_CASE
 }
 
 }  // namespace llmc
@@ -58,21 +83,20 @@ using namespace llmc;
 
 extern "C" int llmc_gemv(int M, const void* x, int x_stride, const void* norm_w, float eps, const void* W, void* out,
                          int out_stride, int N, int K, int epi, hipStream_t s) {
-  if (K % 8 != 0) return -1;
-  if (epi == EPI_SILU && (N % 2 != 0)) return -1;
-  const bool norm = norm_w != nullptr;
-#define LLMC_GEMV_CASE(E)                                                                             \
-  case E:                                                                                             \
-    return norm ? dispatch_m<PRO_NORM, E>(M, x, x_stride, norm_w, eps, W, out, out_stride, N, K, s)   \
-                : dispatch_m<PRO_NONE, E>(M, x, x_stride, norm_w, eps, W, out, out_stride, N, K, s);
-  switch (epi) {
-    LLMC_GEMV_CASE(EPI_BF16)
-    LLMC_GEMV_CASE(EPI_F32)
-    LLMC_GEMV_CASE(EPI_RESADD)
-    LLMC_GEMV_CASE(EPI_SILU)
-    default: return -4;
-  }
-#undef LLMC_GEMV_CASE
+  if (epi == EPI_ROPE) return -5;
+  RopeEpi rope{};
+  return gemv_dispatch(M, x, x_stride, norm_w, eps, W, out, out_stride, N, K, epi, rope, s);
+}
+
+// qkv projection for decode with fused RMSNorm prologue and RoPE + paged-KV-write epilogue.
+extern "C" int llmc_gemv_qkv_rope(int M, const void* x, int x_stride, const void* norm_w, float eps, const void* W,
+                                  int N, int K, void* q_out, int q_stride, void* k_cache, void* v_cache,
+                                  const void* positions, const void* slots, const void* cos_t, const void* sin_t,
+                                  int nh, int nkv, int D, int bs, hipStream_t s) {
+  if (N != (nh + 2 * nkv) * D || D % 2 != 0) return -1;
+  RopeEpi rope{(bf16_t*)q_out, q_stride, (bf16_t*)k_cache, (bf16_t*)v_cache, (const int32_t*)positions,
+               (const int32_t*)slots, (const float*)cos_t, (const float*)sin_t, nh, nkv, D, bs};
+  return gemv_dispatch(M, x, x_stride, norm_w, eps, W, nullptr, 0, N, K, EPI_ROPE, rope, s);
 }
 
 // MoE decode (K11 at batch 1): one GEMV per (token, top-k slot) pair against the selected
@@ -81,13 +105,15 @@ extern "C" int llmc_moe_gemv(int npairs, const void* x, int x_stride, const void
                              const void* ids, int x_div, void* out, int out_stride, int N, int K, int epi,
                              hipStream_t s) {
   if (K % 8 != 0 || norm_w != nullptr) return -1;
-  constexpr int RPW = 4, UNROLL = 4;
-  const size_t lds = static_cast<size_t>(K) * sizeof(bf16_t) + kGemvWaves * sizeof(float);
+  constexpr int NT = 256, RPW = 2, UNROLL = 4;
+  const size_t lds = static_cast<size_t>(K) * sizeof(bf16_t) + (NT / kWave) * sizeof(float);
   if (lds > 64 * 1024) return -2;
-  dim3 grid((N + kGemvWaves * RPW - 1) / (kGemvWaves * RPW), npairs);
-#define LLMC_MOEGV(E)                                                                                              \
-  gemv_kernel<1, RPW, UNROLL, PRO_NONE, E, true><<<grid, kGemvThreads, lds, s>>>(                                 \
-      (const bf16_t*)x, x_stride, nullptr, eps, (const bf16_t*)W, out, out_stride, N, K, (const int32_t*)ids, x_div)
+  dim3 grid((N + (NT / kWave) * RPW - 1) / ((NT / kWave) * RPW), npairs);
+  RopeEpi rope{};
+#define LLMC_MOEGV(E)                                                                                            \
+  gemv_kernel<1, NT, RPW, UNROLL, PRO_NONE, E, true><<<grid, NT, lds, s>>>(                                      \
+      (const bf16_t*)x, x_stride, nullptr, eps, (const bf16_t*)W, out, out_stride, N, K, (const int32_t*)ids, x_div, \
+      rope)
   switch (epi) {
     case EPI_BF16: LLMC_MOEGV(EPI_BF16); break;
     case EPI_SILU: LLMC_MOEGV(EPI_SILU); break;

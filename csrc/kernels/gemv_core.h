@@ -6,31 +6,44 @@
 //  * W [N, K] bf16, K contiguous. A wave owns RPW output rows; lane l streams chunks
 //    c = l + 64 i (16 B = 8 bf16 each) of all RPW rows -> RPW*UNROLL independent 16 B loads in
 //    flight per lane, straight to VGPRs (no LDS round trip for W), non-temporal (read once).
+//  * Geometry (NT threads, RPW rows/wave) is chosen per shape on the host so the grid is a
+//    balanced multiple of the 256 CUs with >= 16 waves/CU in flight (launch_gemv in gemv.hip).
 //  * x is staged ONCE per block in LDS (M*K bf16); every lane reads the same chunk index it
 //    loads from W, so ds_read_b128 addresses are lane-consecutive (conflict-free).
 //  * v_dot2_f32_bf16 does convert+multiply+accumulate of 2 elements per VALU op.
-//  * Fused prologue  PRO_NORM: x <- bf16(rmsnorm(x) * w_norm)  (the layer's input norm), so the
-//    decode layer needs no separate norm launch.
+//  * Fused prologue  PRO_NORM: x <- bf16(rmsnorm(x) * w_norm)  (the layer's input norm).
 //  * Fused epilogues: bf16 store | f32 store (logits) | in-place residual add h += W.x |
-//    SiLU-mul over interleaved gate/up rows (row 2i = gate_i, 2i+1 = up_i).
+//    SiLU-mul over interleaved gate/up rows (row 2i = gate_i, 2i+1 = up_i) |
+//    ROPE: qkv projection with pair-interleaved Q/K head rows -> rotate-half RoPE from the f32
+//    accumulators, q to the q buffer, k/v straight into the paged KV cache at the device slot
+//    (replaces the separate RoPE + KV-write launch of the decode step).
 #pragma once
 #include "common.h"
 
 namespace llmc {
 
 enum { PRO_NONE = 0, PRO_NORM = 1 };
-enum { EPI_BF16 = 0, EPI_F32 = 1, EPI_RESADD = 2, EPI_SILU = 3 };
+enum { EPI_BF16 = 0, EPI_F32 = 1, EPI_RESADD = 2, EPI_SILU = 3, EPI_ROPE = 4 };
 
-constexpr int kGemvThreads = 256;
-constexpr int kGemvWaves = kGemvThreads / kWave;
+struct RopeEpi {
+  bf16_t* q_out;            // [M, q_stride], canonical head-major layout
+  int q_stride;
+  bf16_t* k_cache;          // [nb][nkv][bs][D]
+  bf16_t* v_cache;
+  const int32_t* positions; // [M]
+  const int32_t* slots;     // [M]
+  const float* cos_t;       // [max_pos][D/2]
+  const float* sin_t;
+  int nh, nkv, D, bs;
+};
 
-template <int M, int RPW, int UNROLL, int PRO, int EPI, bool EXPERT = false>
-__global__ __launch_bounds__(kGemvThreads) void gemv_kernel(const bf16_t* __restrict__ x, int x_stride,
-                                                            const bf16_t* __restrict__ norm_w, float eps,
-                                                            const bf16_t* __restrict__ W, void* __restrict__ out,
-                                                            int out_stride, int N, int K,
-                                                            const int32_t* __restrict__ expert_ids = nullptr,
-                                                            int x_div = 1) {
+template <int M, int NT, int RPW, int UNROLL, int PRO, int EPI, bool EXPERT = false>
+__global__ __launch_bounds__(NT) void gemv_kernel(const bf16_t* __restrict__ x, int x_stride,
+                                                  const bf16_t* __restrict__ norm_w, float eps,
+                                                  const bf16_t* __restrict__ W, void* __restrict__ out,
+                                                  int out_stride, int N, int K, const int32_t* __restrict__ expert_ids,
+                                                  int x_div, RopeEpi rope) {
+  constexpr int WAVES = NT / kWave;
   // EXPERT (MoE decode): blockIdx.y = (token, slot) pair; weights of expert expert_ids[pair],
   // input row pair / x_div, output row pair (M must be 1).
   if constexpr (EXPERT) {
@@ -46,11 +59,11 @@ __global__ __launch_bounds__(kGemvThreads) void gemv_kernel(const bf16_t* __rest
 
   // ---- prologue: x -> LDS (optionally RMS-normalised) ----
   if constexpr (PRO == PRO_NORM) {
-    float(*red)[kGemvWaves] = reinterpret_cast<float(*)[kGemvWaves]>(smem + static_cast<size_t>(M) * K * sizeof(bf16_t));
+    float(*red)[WAVES] = reinterpret_cast<float(*)[WAVES]>(smem + static_cast<size_t>(M) * K * sizeof(bf16_t));
     float ss[M];
 #pragma unroll
     for (int m = 0; m < M; ++m) ss[m] = 0.f;
-    for (int c = tid; c < nchunk; c += kGemvThreads) {
+    for (int c = tid; c < nchunk; c += NT) {
 #pragma unroll
       for (int m = 0; m < M; ++m) {
         float f[8];
@@ -70,10 +83,10 @@ __global__ __launch_bounds__(kGemvThreads) void gemv_kernel(const bf16_t* __rest
     for (int m = 0; m < M; ++m) {
       float t = 0.f;
 #pragma unroll
-      for (int w = 0; w < kGemvWaves; ++w) t += red[m][w];
+      for (int w = 0; w < WAVES; ++w) t += red[m][w];
       inv[m] = rsqrtf(t / K + eps);
     }
-    for (int c = tid; c < nchunk; c += kGemvThreads) {
+    for (int c = tid; c < nchunk; c += NT) {
       float g[8];
       unpack8(reinterpret_cast<const u32x4*>(norm_w)[c], g);
 #pragma unroll
@@ -86,7 +99,7 @@ __global__ __launch_bounds__(kGemvThreads) void gemv_kernel(const bf16_t* __rest
       }
     }
   } else {
-    for (int c = tid; c < nchunk; c += kGemvThreads) {
+    for (int c = tid; c < nchunk; c += NT) {
 #pragma unroll
       for (int m = 0; m < M; ++m)
         reinterpret_cast<u32x4*>(xs + m * K)[c] =
@@ -97,7 +110,7 @@ __global__ __launch_bounds__(kGemvThreads) void gemv_kernel(const bf16_t* __rest
 
   // ---- main loop: stream RPW weight rows per wave ----
   const int wave = tid / kWave, lane = tid % kWave;
-  const int row0 = (blockIdx.x * kGemvWaves + wave) * RPW;
+  const int row0 = (blockIdx.x * WAVES + wave) * RPW;
   if (row0 >= N) return;
   const u32x4* wrow[RPW];
 #pragma unroll
@@ -163,10 +176,40 @@ __global__ __launch_bounds__(kGemvThreads) void gemv_kernel(const bf16_t* __rest
       } else if constexpr (EPI == EPI_RESADD) {
         bf16_t* h = reinterpret_cast<bf16_t*>(out) + static_cast<int64_t>(m) * out_stride + n;
         *h = f32_to_bf16(bf16_to_f32(*h) + v);
-      } else {  // EPI_SILU: rows (2j, 2j+1) = (gate, up) -> output column n/2
+      } else if constexpr (EPI == EPI_SILU) {  // rows (2j, 2j+1) = (gate, up) -> output column n/2
         if ((r & 1) == 0) {
           reinterpret_cast<bf16_t*>(out)[static_cast<int64_t>(m) * out_stride + n / 2] =
               f32_to_bf16(silu(v) * acc[r + 1][m]);
+        }
+      } else {  // EPI_ROPE: rows (2j, 2j+1) of a Q/K head = dims (i, i + D/2), i = (n % D) / 2
+        if ((r & 1) == 0) {
+          const int D = rope.D, half = D / 2;
+          const int head = n / D;
+          const int slot = rope.slots[m];
+          const int64_t page = slot >= 0 ? slot / rope.bs : 0;
+          const int off = slot >= 0 ? slot % rope.bs : 0;
+          const float x2 = acc[r + 1][m];
+          if (head < rope.nh + rope.nkv) {
+            const int i = (n % D) / 2;
+            const int pos = rope.positions[m];
+            const float c = rope.cos_t[static_cast<int64_t>(pos) * half + i];
+            const float s = rope.sin_t[static_cast<int64_t>(pos) * half + i];
+            const float o1 = v * c - x2 * s, o2 = x2 * c + v * s;
+            if (head < rope.nh) {
+              bf16_t* q = rope.q_out + static_cast<int64_t>(m) * rope.q_stride + head * D;
+              q[i] = f32_to_bf16(o1);
+              q[i + half] = f32_to_bf16(o2);
+            } else if (slot >= 0) {
+              bf16_t* k = rope.k_cache + ((page * rope.nkv + (head - rope.nh)) * rope.bs + off) * D;
+              k[i] = f32_to_bf16(o1);
+              k[i + half] = f32_to_bf16(o2);
+            }
+          } else if (slot >= 0) {  // V rows keep canonical order
+            const int vh = head - rope.nh - rope.nkv, d = n % D;
+            bf16_t* vv = rope.v_cache + ((page * rope.nkv + vh) * rope.bs + off) * D;
+            vv[d] = f32_to_bf16(v);
+            vv[d + 1] = f32_to_bf16(x2);
+          }
         }
       }
     }

@@ -47,7 +47,7 @@ class EngineConfig:
     steps_per_graph: int = 8
     use_graphs: bool = True
     prefill_chunk: int = 8192
-    attn_chunk: int = 256
+    attn_chunk: int = 0  # 0 = by max_context (64 / 128 / 256 tokens per split-KV block)
     init_scale: float = 1.0
     stream_priority: int = 0
 
@@ -137,7 +137,7 @@ class Engine:
         self.seeds = torch.zeros(B, dtype=torch.int64, device=dev)
         bf = dict(dtype=torch.bfloat16, device=dev)
         self.h = torch.zeros(B, c.hidden, **bf)
-        self.qkv = torch.zeros(B, self.w.qkv_size, **bf)
+        self.q = torch.zeros(B, self.w.q_size, **bf)
         self.attn = torch.zeros(B, self.w.q_size, **bf)
         self.act = torch.zeros(B, self.w.inter, **bf)
         self.logits_local = torch.zeros(B, self.w.vocab_local, dtype=torch.float32, device=dev)
@@ -145,9 +145,12 @@ class Engine:
                        else torch.zeros(B, c.vocab, dtype=torch.float32, device=dev))
         self._gather_buf = (None if self.tp.size == 1 else
                             torch.zeros(self.tp.size, B, self.w.vocab_local, dtype=torch.float32, device=dev))
-        max_chunks = (self.ecfg.max_context + self.ecfg.attn_chunk - 1) // self.ecfg.attn_chunk + 1
-        self.part_o = torch.zeros(B, self.nh, max_chunks, self.D, dtype=torch.float32, device=dev)
-        self.part_ml = torch.zeros(B, self.nh, max_chunks, 2, dtype=torch.float32, device=dev)
+        # split-KV decode attention: small chunks (more blocks) for short contexts
+        ctxmax = self.ecfg.max_context + self.ecfg.steps_per_graph + 2
+        self.attn_chunk = self.ecfg.attn_chunk or (64 if ctxmax <= 16384 else 128 if ctxmax <= 65536 else 256)
+        self.max_chunks = (ctxmax + self.attn_chunk - 1) // self.attn_chunk
+        self.attn_part, self.attn_counters = ops.decode_attn_workspace(B, self.nh, self.nkv, self.D,
+                                                                        self.max_chunks, dev)
         if self.on_gpu:
             P = ops.sample_parts()
             self.ws_v = torch.zeros(B, P, dtype=torch.float32, device=dev)
@@ -244,12 +247,13 @@ class Engine:
 
         h = ops.embedding(ids_d, self.w.embed)
         attn = torch.empty(T, self.w.q_size, dtype=torch.bfloat16, device=dev)
+        qbuf = torch.empty(T, self.w.q_size, dtype=torch.bfloat16, device=dev)
         for li, Lw in enumerate(self.w.layers):
             xn = ops.rmsnorm(h, Lw.ln1, c.rms_eps)
             qkv = ops.linear(xn, Lw.w_qkv, EPI_BF16)
             ops.rope_kv_write(qkv, pos_d, self.cos_t, self.sin_t, self.k_cache[li], self.v_cache[li], slots_d,
-                              self.nh, self.nkv, self.D, self.bs)
-            ops.attn_prefill(qkv, self.k_cache[li], self.v_cache[li], bt, qs_d, ql_d, cl_d, attn, max_qlen,
+                              self.nh, self.nkv, self.D, self.bs, qbuf)
+            ops.attn_prefill(qbuf, self.k_cache[li], self.v_cache[li], bt, qs_d, ql_d, cl_d, attn, max_qlen,
                              self.nh, self.nkv, self.D, self.bs, self.scale)
             self._row_parallel(attn, Lw.w_o, h)
             xn = ops.rmsnorm(h, Lw.ln2, c.rms_eps)
@@ -314,17 +318,17 @@ class Engine:
         self.tp.all_reduce_(h)
 
     # -- decode -------------------------------------------------------------------------------------
-    def _decode_step(self, B: int) -> None:
+    def _decode_step(self, B: int, grid_chunks: Optional[int] = None) -> None:
+        """One token for rows 0..B-1. ``grid_chunks`` bounds the attention grid (context bucket)."""
         c = self.cfg
-        h, qkv, attn, act = self.h[:B], self.qkv[:B], self.attn[:B], self.act[:B]
+        h, q, attn, act = self.h[:B], self.q[:B], self.attn[:B], self.act[:B]
         ops.embedding(self.tokens_in[:B], self.w.embed, out=h)
         for li, Lw in enumerate(self.w.layers):
-            ops.linear(h, Lw.w_qkv, EPI_BF16, out=qkv, norm_w=Lw.ln1, eps=c.rms_eps)
-            ops.rope_kv_write(qkv, self.positions[:B], self.cos_t, self.sin_t, self.k_cache[li], self.v_cache[li],
-                              self.slots[:B], self.nh, self.nkv, self.D, self.bs)
-            ops.attn_decode(qkv, self.k_cache[li], self.v_cache[li], self.block_tables[:B], self.seq_lens[:B], attn,
-                            self.part_o[:B], self.part_ml[:B], self.nh, self.nkv, self.D, self.bs,
-                            self.ecfg.attn_chunk, self.scale)
+            ops.qkv_rope(h, Lw.w_qkv, Lw.ln1, c.rms_eps, q, self.k_cache[li], self.v_cache[li], self.positions[:B],
+                         self.slots[:B], self.cos_t, self.sin_t, self.nh, self.nkv, self.D, self.bs)
+            ops.attn_decode(q, self.k_cache[li], self.v_cache[li], self.block_tables[:B], self.seq_lens[:B], attn,
+                            self.attn_part[:B], self.attn_counters[:B], self.nh, self.nkv, self.D, self.bs,
+                            self.attn_chunk, self.scale, grid_chunks)
             self._row_parallel(attn, Lw.w_o, h)
             if c.is_moe:
                 self._moe_decode(h, Lw, B)
@@ -378,8 +382,17 @@ class Engine:
                    seq_lens=self.seq_lens[:B], slots=self.slots[:B], block_tables=self.block_tables[:B], bs=self.bs,
                    out_tokens=self.out_tokens[:B], out_count=self.out_count[:B], use_topkp=use_topkp)
 
-    def _graph(self, B: int):
-        key = (B, self._use_topkp)
+    def _bucket(self, ctx_tokens: int) -> int:
+        """Attention grid (chunks) for contexts up to ``ctx_tokens``: next power of two >= 8,
+        so the graph for a short context does not launch thousands of empty blocks."""
+        need = (ctx_tokens + self.attn_chunk - 1) // self.attn_chunk
+        b = 8
+        while b < need:
+            b *= 2
+        return min(b, self.max_chunks)
+
+    def _graph(self, B: int, bucket: int):
+        key = (B, self._use_topkp, bucket)
         g = self._graphs.get(key)
         if g is not None:
             return g
@@ -388,13 +401,13 @@ class Engine:
         # snapshotted and restored, then capture S steps. thread_local capture mode: other
         # engines' threads may allocate / synchronise while this one captures.
         snap = self._snapshot_state()
-        self._decode_step(B)
+        self._decode_step(B, bucket)
         self._restore_state(snap)
         self.stream.synchronize()
         g = torch.cuda.CUDAGraph()
         with torch.cuda.graph(g, stream=self.stream, capture_error_mode="thread_local"):
             for _ in range(S):
-                self._decode_step(B)
+                self._decode_step(B, bucket)
         self._graphs[key] = g
         return g
 
@@ -474,7 +487,7 @@ class Engine:
                 self._finish(seqs, results)
                 return results
 
-            graph = self._graph(B) if self.ecfg.use_graphs else None
+            base_len = max(s.length for s in seqs)
             pending_ev: Optional[torch.cuda.Event] = None
 
             def launch_copy():
@@ -488,11 +501,13 @@ class Engine:
             while True:
                 need_more = issued < max_new
                 if need_more:
-                    if graph is not None:
-                        graph.replay()
+                    # context reached by the end of this replay decides the attention bucket
+                    bucket = self._bucket(base_len + issued + S + 1)
+                    if self.ecfg.use_graphs:
+                        self._graph(B, bucket).replay()
                     else:
                         for _ in range(S):
-                            self._decode_step(B)
+                            self._decode_step(B, bucket)
                     issued += S
                 # wait for the previous snapshot (the GPU keeps the just-issued replay queued)
                 pending_ev.synchronize()

@@ -2,7 +2,10 @@
 
 All three families share one engine-facing layout, chosen for the kernels rather than for
 checkpoint compatibility:
-  * ``w_qkv``  [q + 2 kv, H]  fused Q|K|V rows (one GEMV/GEMM per layer);
+  * ``w_qkv``  [q + 2 kv, H]  fused Q|K|V rows (one GEMV/GEMM per layer); inside every Q and
+    K head the rows are PAIR-INTERLEAVED (row 2i = dim i, row 2i + 1 = dim i + D/2) so the
+    rotate-half RoPE pair of a head lands in one wave of the decode GEMV, whose epilogue applies
+    RoPE and writes K/V straight into the paged cache (no separate RoPE launch);
   * ``w_o``    [H, q];
   * ``w_gu``   [2 I, H] gate/up rows INTERLEAVED (row 2i = gate_i, 2i + 1 = up_i) so the GEMV
     epilogue produces silu(gate) * up directly and a TP shard is a contiguous row range;
@@ -90,7 +93,7 @@ class TransformerWeights:
                 qs = qkv[q0 * D:q1 * D]
                 ks = qkv[c.q_size + k0 * D:c.q_size + k1 * D]
                 vs = qkv[c.q_size + c.kv_size + k0 * D:c.q_size + c.kv_size + k1 * D]
-                L.w_qkv = torch.cat([qs, ks, vs], 0).contiguous()
+                L.w_qkv = torch.cat([pair_interleave_heads(qs, D), pair_interleave_heads(ks, D), vs], 0).contiguous()
                 del qkv
                 wo = self._linear(p + "w_o", c.hidden, c.q_size)
                 L.w_o = wo[:, q0 * D:q1 * D].contiguous()
@@ -138,6 +141,14 @@ class TransformerWeights:
                 if t is not None:
                     tot += t.numel()
         return tot * 2
+
+
+def pair_interleave_heads(rows: torch.Tensor, D: int) -> torch.Tensor:
+    """Reorder each head's D rows as [0, D/2, 1, D/2 + 1, ...] (see module docstring)."""
+    n = rows.shape[0] // D
+    half = D // 2
+    r = rows.view(n, 2, half, -1).transpose(1, 2)  # [head, i, {i, i+half}, H]
+    return r.reshape(n * D, -1)
 
 
 def full_reference_weights(cfg: ModelConfig, seed: int, device="cpu", init_scale: float = 1.0) -> TransformerWeights:

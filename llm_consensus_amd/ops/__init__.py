@@ -15,7 +15,7 @@ import torch
 from ..utils.native import kernels
 from . import oracle
 
-EPI_BF16, EPI_F32, EPI_RESADD, EPI_SILU = 0, 1, 2, 3
+EPI_BF16, EPI_F32, EPI_RESADD, EPI_SILU, EPI_ROPE = 0, 1, 2, 3, 4
 GEMV_MAX_M = 4
 
 
@@ -127,23 +127,47 @@ def gemv(x: torch.Tensor, W: torch.Tensor, epi: int = EPI_BF16, out: Optional[to
     return out
 
 
-def rope_kv_write(qkv, positions, cos_t, sin_t, k_cache, v_cache, slots, nh, nkv, D, bs) -> None:
+def rope_kv_write(qkv, positions, cos_t, sin_t, k_cache, v_cache, slots, nh, nkv, D, bs, q_out) -> None:
+    """Prefill RoPE: pair-interleaved Q/K rows of ``qkv`` -> canonical rotated q in ``q_out``,
+    rotated k and raw v into the paged cache."""
     if not qkv.is_cuda:
-        oracle.rope_kv_write(qkv, positions, cos_t, sin_t, k_cache, v_cache, slots, nh, nkv, D, bs)
+        oracle.rope_kv_write(qkv, positions, cos_t, sin_t, k_cache, v_cache, slots, nh, nkv, D, bs, q_out)
         return
     T = qkv.shape[0]
-    kernels().rope_kv_write(_p(qkv), qkv.stride(0), _p(positions), _p(cos_t), _p(sin_t), _p(k_cache), _p(v_cache),
-                            _p(slots), T, nh, nkv, D, bs, _s(qkv))
+    kernels().rope_kv_write(_p(qkv), qkv.stride(0), _p(q_out), q_out.stride(0), _p(positions), _p(cos_t), _p(sin_t),
+                            _p(k_cache), _p(v_cache), _p(slots), T, nh, nkv, D, bs, _s(qkv))
 
 
-def attn_decode(q, k_cache, v_cache, block_tables, seq_lens, out, part_o, part_ml, nh, nkv, D, bs, chunk, scale):
+def qkv_rope(x, W, norm_w, eps, q_out, k_cache, v_cache, positions, slots, cos_t, sin_t, nh, nkv, D, bs) -> None:
+    """Decode qkv projection: fused RMSNorm prologue + RoPE/KV-write epilogue (one launch)."""
+    if not x.is_cuda:
+        qkv = oracle.linear(x, W, EPI_BF16, None, norm_w, eps)
+        oracle.rope_kv_write(qkv, positions, cos_t, sin_t, k_cache, v_cache, slots, nh, nkv, D, bs, q_out)
+        return
+    M, K = x.shape
+    kernels().gemv_qkv_rope(M, _p(x), x.stride(0), _p(norm_w), float(eps), _p(W), W.shape[0], K, _p(q_out),
+                            q_out.stride(0), _p(k_cache), _p(v_cache), _p(positions), _p(slots), _p(cos_t), _p(sin_t),
+                            nh, nkv, D, bs, _s(x))
+
+
+def decode_attn_workspace(B, nh, nkv, D, max_chunks, device):
+    """(part, counters) for attn_decode: f32 partials [B, nkv, max_chunks, G, D+2] and zeroed tickets."""
+    G = nh // nkv
+    part = torch.zeros(B, nkv, max_chunks, G, D + 2, dtype=torch.float32, device=device)
+    counters = torch.zeros(B, nkv, dtype=torch.int32, device=device)
+    return part, counters
+
+
+def attn_decode(q, k_cache, v_cache, block_tables, seq_lens, out, part, counters, nh, nkv, D, bs, chunk, scale,
+                grid_chunks: Optional[int] = None):
     if not q.is_cuda:
         out.copy_(oracle.attn_decode(q, k_cache, v_cache, block_tables, seq_lens, nh, nkv, D, bs, scale))
         return out
     B = q.shape[0]
-    max_chunks = part_o.shape[2] if part_o is not None else 1
+    max_chunks = part.shape[2]
+    gc = max_chunks if grid_chunks is None else min(grid_chunks, max_chunks)
     kernels().attn_decode(_p(q), q.stride(0), _p(k_cache), _p(v_cache), _p(block_tables), block_tables.stride(0),
-                          _p(seq_lens), _p(part_o), _p(part_ml), _p(out), out.stride(0), B, nh, nkv, D, bs, chunk,
+                          _p(seq_lens), _p(part), _p(counters), _p(out), out.stride(0), B, nh, nkv, D, bs, chunk, gc,
                           max_chunks, float(scale), _s(q))
     return out
 

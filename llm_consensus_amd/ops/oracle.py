@@ -12,7 +12,7 @@ from typing import Optional
 
 import torch
 
-EPI_BF16, EPI_F32, EPI_RESADD, EPI_SILU = 0, 1, 2, 3
+EPI_BF16, EPI_F32, EPI_RESADD, EPI_SILU, EPI_ROPE = 0, 1, 2, 3, 4
 
 
 def rmsnorm(x: torch.Tensor, w: torch.Tensor, eps: float) -> torch.Tensor:
@@ -33,6 +33,8 @@ def silu_mul_interleaved(gu: torch.Tensor) -> torch.Tensor:
 
 def linear(x: torch.Tensor, W: torch.Tensor, epi: int, out: Optional[torch.Tensor] = None,
            norm_w: Optional[torch.Tensor] = None, eps: float = 1e-5) -> torch.Tensor:
+    if epi == EPI_ROPE:
+        raise ValueError("EPI_ROPE: use qkv_rope")
     if norm_w is not None:
         x = rmsnorm(x, norm_w, eps)
     acc = x.float() @ W.float().t()
@@ -60,16 +62,18 @@ def rope_tables(inv_freq, max_pos: int):
     return torch.cos(ang).float(), torch.sin(ang).float()
 
 
-def rope_kv_write(qkv, positions, cos_t, sin_t, k_cache, v_cache, slots, nh, nkv, D, bs):
+def rope_kv_write(qkv, positions, cos_t, sin_t, k_cache, v_cache, slots, nh, nkv, D, bs, q_out):
+    """qkv rows hold Q and K heads PAIR-INTERLEAVED ([x0, x_h, x1, x_{h+1}, ...], h = D/2);
+    rotated Q goes to ``q_out`` [T, nh*D] in canonical order, rotated K / raw V to the cache."""
     T = qkv.shape[0]
     half = D // 2
     pos = positions.long()
     c = cos_t[pos].unsqueeze(1)  # [T,1,half]
     s = sin_t[pos].unsqueeze(1)
-    qk = qkv[:, : (nh + nkv) * D].view(T, nh + nkv, D).float()
-    x1, x2 = qk[..., :half], qk[..., half:]
+    qk = qkv[:, : (nh + nkv) * D].view(T, nh + nkv, half, 2).float()
+    x1, x2 = qk[..., 0], qk[..., 1]
     rot = torch.cat([x1 * c - x2 * s, x2 * c + x1 * s], dim=-1).to(torch.bfloat16)
-    qkv[:, : nh * D] = rot[:, :nh].reshape(T, nh * D)
+    q_out[:, : nh * D] = rot[:, :nh].reshape(T, nh * D)
     if slots is not None:
         v = qkv[:, (nh + nkv) * D:(nh + 2 * nkv) * D].view(T, nkv, D)
         for t in range(T):

@@ -45,7 +45,8 @@ class TPGroup:
         if self.size == 1:
             out.view_as(t).copy_(t)
             return out
-        dist.all_gather_into_tensor(out, t.contiguous(), group=self.group)
+        flat = out.view(self.size * t.shape[0], *t.shape[1:])  # gloo wants dim-0 concatenation
+        dist.all_gather_into_tensor(flat, t.contiguous(), group=self.group)
         return out
 
     def broadcast_(self, t: torch.Tensor, src_rank_in_group: int = 0) -> torch.Tensor:

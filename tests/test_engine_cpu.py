@@ -1,0 +1,100 @@
+"""Engine logic on CPU (oracle op path): paged KV across chunked prefills, prefill == incremental
+decode logits, batched rows, MoE/Phi-3 families, sampling determinism, cancellation."""
+
+import pytest
+import torch
+
+from llm_consensus_amd.context import Context, ContextError
+from llm_consensus_amd.engine import Engine, EngineConfig, SamplingParams
+from llm_consensus_amd.models.config import FAMILIES
+from llm_consensus_amd.models.transformer import TransformerWeights, pair_interleave_heads
+from llm_consensus_amd.parallel.comm import TPGroup
+
+
+def eng(name, **kw):
+    kw.setdefault("max_context", 256)
+    kw.setdefault("seed", 1)
+    return Engine(FAMILIES[name], EngineConfig(device="cpu", **kw))
+
+
+@pytest.mark.parametrize("name", ["llama-tiny", "mixtral-tiny", "phi3-tiny"])
+def test_prefill_equals_incremental(name):
+    """Logits after one 40-token prefill == after 25 + 15-token prefills (paged KV reuse)."""
+    e = eng(name, block_size=16)
+    p = [(i * 31) % 700 + 256 for i in range(40)]
+    a = e.new_sequence()
+    e.prefill([a], [p])
+    la = e.logits[0].clone()
+    e.free_sequence(a)
+    b = e.new_sequence()
+    e.prefill([b], [p[:25]], want_logits=False)
+    e.prefill([b], [p[25:]])
+    assert torch.allclose(la, e.logits[0], atol=1e-3, rtol=1e-3)
+
+
+@pytest.mark.parametrize("name", ["llama-tiny", "mixtral-tiny"])
+def test_decode_matches_prefill_teacher_forced(name):
+    e = eng(name)
+    p = [(i * 17) % 700 + 256 for i in range(20)]
+    gen = e.generate_ids(p, 6, temperature=0.0, stop_on_eos=False)
+    s = e.new_sequence()
+    e.prefill([s], [p + gen[:-1]])
+    assert int(e.logits[0].argmax()) == gen[-1]
+
+
+def test_sampling_determinism_and_seed():
+    e = eng("llama-tiny")
+    p = list(range(300, 320))
+    a = e.generate_ids(p, 10, temperature=1.0, seed=7, stop_on_eos=False)
+    b = e.generate_ids(p, 10, temperature=1.0, seed=7, stop_on_eos=False)
+    c = e.generate_ids(p, 10, temperature=1.0, seed=8, stop_on_eos=False)
+    assert a == b and a != c
+
+
+def test_batched_rows_match_single():
+    e = eng("llama-tiny", max_batch=2)
+    p1, p2 = list(range(300, 330)), list(range(500, 512))
+    sp = [SamplingParams(8, 0.0, 1.0, 0, 0, False), SamplingParams(8, 0.0, 1.0, 0, 0, False)]
+    both = e.generate_batch([p1, p2], sp)
+    assert both[0] == e.generate_ids(p1, 8, 0.0, stop_on_eos=False)
+    assert both[1] == e.generate_ids(p2, 8, 0.0, stop_on_eos=False)
+
+
+def test_kv_blocks_freed_and_context_limit():
+    e = eng("llama-tiny", max_context=128, block_size=16)
+    free0 = e.alloc.num_free
+    e.generate_ids(list(range(300, 340)), 10, stop_on_eos=False)
+    assert e.alloc.num_free == free0
+    with pytest.raises(Exception, match="exceeds engine max_context"):
+        e.generate_ids(list(range(300, 420)), 50, stop_on_eos=False)
+    assert e.alloc.num_free == free0
+
+
+def test_cancellation():
+    e = eng("llama-tiny")
+    ctx = Context.background()
+    seen = []
+
+    def cb(ids):
+        seen.extend(ids)
+        if len(seen) >= 3:
+            ctx.cancel()
+
+    with pytest.raises(ContextError, match="context canceled"):
+        e.generate_ids(list(range(300, 320)), 50, ctx=ctx, on_tokens=cb, stop_on_eos=False)
+
+
+def test_pair_interleave_heads():
+    rows = torch.arange(2 * 8).view(2 * 8, 1)  # two heads of D=8
+    out = pair_interleave_heads(rows, 8).view(-1).tolist()
+    assert out == [0, 4, 1, 5, 2, 6, 3, 7, 8, 12, 9, 13, 10, 14, 11, 15]
+
+
+def test_weights_param_counts():
+    c = FAMILIES["llama-3-8b"]
+    assert 8.0e9 < c.num_params() < 8.1e9
+    assert 70e9 < FAMILIES["llama-3-70b"].num_params() < 71e9
+    assert 46e9 < FAMILIES["mixtral-8x7b"].num_params() < 47.5e9
+    assert 3.7e9 < FAMILIES["phi-3-mini"].num_params() < 3.9e9
+    w = TransformerWeights(FAMILIES["mixtral-tiny"], TPGroup.single(), torch.device("cpu"), 1)
+    assert w.layers[0].w_gu.shape == (4, 2 * 384, 256) and w.layers[0].w_router.shape == (4, 256)

@@ -110,13 +110,37 @@ def _rope_setup(nh, nkv, D, T, bs=64, nblocks=8):
 def test_rope_kv_write(cuda, nh, nkv, D):
     torch.manual_seed(2)
     cos_t, sin_t, qkv, pos, slots, kc, vc = _rope_setup(nh, nkv, D, 11)
-    q_ref, kc_ref, vc_ref = qkv.cpu().clone(), kc.clone(), vc.clone()
-    oracle.rope_kv_write(q_ref, pos, cos_t, sin_t, kc_ref, vc_ref, slots, nh, nkv, D, 64)
-    qd, kd, vd = qkv.clone(), kc.cuda(), vc.cuda()
-    ops.rope_kv_write(qd, pos.cuda(), cos_t.cuda(), sin_t.cuda(), kd, vd, slots.cuda(), nh, nkv, D, 64)
+    kc_ref, vc_ref = kc.clone(), vc.clone()
+    q_ref = torch.zeros(11, nh * D, dtype=BF)
+    oracle.rope_kv_write(qkv.cpu(), pos, cos_t, sin_t, kc_ref, vc_ref, slots, nh, nkv, D, 64, q_ref)
+    kd, vd = kc.cuda(), vc.cuda()
+    qd = torch.zeros(11, nh * D, dtype=BF, device="cuda")
+    ops.rope_kv_write(qkv, pos.cuda(), cos_t.cuda(), sin_t.cuda(), kd, vd, slots.cuda(), nh, nkv, D, 64, qd)
     close(qd, q_ref, 1e-2)
     close(kd, kc_ref, 1e-2)
     assert torch.equal(vd.cpu(), vc_ref)
+
+
+@pytest.mark.parametrize("M", [1, 2, 4])
+@pytest.mark.parametrize("nh,nkv,D,H", [(32, 8, 128, 4096), (32, 32, 96, 3072), (4, 2, 64, 256), (16, 2, 128, 8192)])
+def test_gemv_qkv_rope(cuda, M, nh, nkv, D, H):
+    """Fused decode qkv GEMV (norm prologue + RoPE/KV-write epilogue) vs the 2-step oracle."""
+    torch.manual_seed(12)
+    cos_t, sin_t, _, pos, slots, kc, vc = _rope_setup(nh, nkv, D, M)
+    N = (nh + 2 * nkv) * D
+    x = rnd(M, H)
+    W = rnd(N, H, scale=0.05)
+    nw = rnd(H)
+    kc_ref, vc_ref = kc.clone(), vc.clone()
+    q_ref = torch.zeros(M, nh * D, dtype=BF)
+    qkv = oracle.linear(x.cpu(), W.cpu(), 0, None, nw.cpu(), 1e-5)
+    oracle.rope_kv_write(qkv, pos, cos_t, sin_t, kc_ref, vc_ref, slots, nh, nkv, D, 64, q_ref)
+    kd, vd = kc.cuda(), vc.cuda()
+    qd = torch.zeros(M, nh * D, dtype=BF, device="cuda")
+    ops.qkv_rope(x, W, nw, 1e-5, qd, kd, vd, pos.cuda(), slots.cuda(), cos_t.cuda(), sin_t.cuda(), nh, nkv, D, 64)
+    close(qd, q_ref, 3e-2)
+    close(kd, kc_ref, 3e-2)
+    close(vd, vc_ref, 3e-2)
 
 
 def _paged_kv(B, L_max, nkv, D, bs):
@@ -130,21 +154,25 @@ def _paged_kv(B, L_max, nkv, D, bs):
 
 @pytest.mark.parametrize("nh,nkv,D", [(32, 8, 128), (32, 32, 96), (16, 2, 128), (4, 2, 64)])
 @pytest.mark.parametrize("lens", [[1, 7], [100, 1000], [3000, 257]])
-def test_attn_decode(cuda, nh, nkv, D, lens):
+@pytest.mark.parametrize("chunk", [64, 256])
+def test_attn_decode(cuda, nh, nkv, D, lens, chunk):
     torch.manual_seed(3)
-    B, bs, chunk = len(lens), 64, 256
+    B, bs = len(lens), 64
     L_max = max(lens)
     kc, vc, bt = _paged_kv(B, L_max, nkv, D, bs)
     q = rnd(B, nh * D)
     sl = torch.tensor(lens, dtype=torch.int32)
     max_chunks = (4096 + chunk - 1) // chunk
-    po = torch.empty(B, nh, max_chunks, D, device="cuda")
-    pml = torch.empty(B, nh, max_chunks, 2, device="cuda")
+    part, ctr = ops.decode_attn_workspace(B, nh, nkv, D, max_chunks, "cuda")
     out = torch.empty(B, nh * D, dtype=BF, device="cuda")
     scale = 1 / math.sqrt(D)
-    ops.attn_decode(q, kc, vc, bt.cuda(), sl.cuda(), out, po, pml, nh, nkv, D, bs, chunk, scale)
     ref = oracle.attn_decode(q.cpu(), kc.cpu(), vc.cpu(), bt, sl, nh, nkv, D, bs, scale)
-    close(out, ref, 2e-2)
+    # three launches: the in-kernel reduce must re-arm its tickets every time
+    for _ in range(3):
+        out.zero_()
+        ops.attn_decode(q, kc, vc, bt.cuda(), sl.cuda(), out, part, ctr, nh, nkv, D, bs, chunk, scale)
+        close(out, ref, 2e-2)
+    assert int(ctr.abs().sum()) == 0
 
 
 @pytest.mark.parametrize("nh,nkv,D", [(32, 8, 128), (32, 32, 96), (16, 2, 128), (4, 2, 64)])

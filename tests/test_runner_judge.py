@@ -1,0 +1,158 @@
+"""Ports of the reference's table-driven tests (internal/runner/runner_test.go:12-129,
+internal/consensus/judge_test.go:13-136) plus the semantics SURVEY.md §4.2 adds: completion-order
+append, duplicate models, callback ordering, single-response passthrough, timeout."""
+
+import threading
+import time
+
+import pytest
+
+from llm_consensus_amd.consensus import Judge, JudgeError, build_judge_prompt
+from llm_consensus_amd.context import Context, ContextError
+from llm_consensus_amd.provider import FuncProvider, Registry, Response
+from llm_consensus_amd.runner import AllModelsFailed, Callbacks, Runner
+
+
+def ok(model, content):
+    return FuncProvider(lambda ctx, req: Response(model=model, content=content, provider="test"))
+
+
+def fail(msg):
+    def f(ctx, req):
+        raise RuntimeError(msg)
+
+    return FuncProvider(f)
+
+
+@pytest.mark.parametrize("name,models,setup,resp,warn,failed,err", [
+    ("all models succeed", ["model-a", "model-b"],
+     lambda r: (r.register("model-a", ok("model-a", "response a")), r.register("model-b", ok("model-b", "response b"))),
+     2, 0, 0, False),
+    ("partial failure", ["model-a", "model-b"],
+     lambda r: (r.register("model-a", fail("api error")), r.register("model-b", ok("model-b", "response b"))),
+     1, 1, 1, False),
+    ("all models fail", ["model-a", "model-b"],
+     lambda r: (r.register("model-a", fail("error a")), r.register("model-b", fail("error b"))),
+     0, 0, 0, True),
+    ("unregistered model", ["unknown-model"], lambda r: None, 0, 0, 0, True),
+])
+def test_runner_run(name, models, setup, resp, warn, failed, err):
+    reg = Registry()
+    setup(reg)
+    r = Runner(reg, 5.0)
+    if err:
+        with pytest.raises(AllModelsFailed):
+            r.run(Context.background(), models, "test prompt")
+        return
+    res = r.run(Context.background(), models, "test prompt")
+    assert len(res.responses) == resp
+    assert len(res.warnings or []) == warn
+    assert len(res.failed_models or []) == failed
+    if warn == 0:
+        assert res.warnings is None and res.failed_models is None  # Go nil slices -> omitempty
+
+
+def test_runner_timeout():
+    reg = Registry()
+
+    def slow(ctx, req):
+        if ctx.wait(10.0):
+            raise ContextError(ctx.err())
+        return Response(model="slow-model", content="too slow")
+
+    reg.register("slow-model", FuncProvider(slow))
+    t = time.monotonic()
+    with pytest.raises(AllModelsFailed) as ei:
+        Runner(reg, 0.1).run(Context.background(), ["slow-model"], "test")
+    assert time.monotonic() - t < 5
+    assert "context deadline exceeded" in str(ei.value)
+    assert str(ei.value).startswith("all models failed: [slow-model: ")
+
+
+def test_runner_completion_order_duplicates_and_callbacks():
+    reg = Registry()
+
+    def delayed(d, name):
+        def f(ctx, req):
+            time.sleep(d)
+            return Response(model=req.model, content=name, provider="test")
+
+        return FuncProvider(f)
+
+    reg.register("slow", delayed(0.3, "slow"))
+    reg.register("fast", delayed(0.0, "fast"))
+    events = []
+    lock = threading.Lock()
+    cb = Callbacks(on_model_start=lambda m: events.append(("start", m)),
+                   on_model_complete=lambda m: events.append(("done", m)),
+                   on_model_stream=lambda m, c: None)
+    res = Runner(reg, 5.0).with_callbacks(cb).run(Context.background(), ["slow", "fast", "fast"], "p")
+    assert [r.content for r in res.responses] == ["fast", "fast", "slow"]  # completion order, dups kept
+    assert sum(1 for e in events if e[0] == "start") == 3
+    assert [e for e in events if e[0] == "done"][-1] == ("done", "slow")
+    del lock
+
+
+def test_runner_error_callback_and_warning_format():
+    reg = Registry()
+    reg.register("a", fail("boom"))
+    reg.register("b", ok("b", "x"))
+    errs = []
+    res = Runner(reg, 5.0).with_callbacks(Callbacks(on_model_error=lambda m, e: errs.append((m, str(e))))).run(
+        Context.background(), ["a", "b", "missing"], "p")
+    assert sorted(res.warnings) == ["a: boom", "missing: unknown model: missing"]
+    assert sorted(res.failed_models) == ["a", "missing"]
+    assert sorted(m for m, _ in errs) == ["a", "missing"]
+
+
+# ---- judge ----------------------------------------------------------------------------------
+def test_judge_empty_errors():
+    j = Judge(ok("x", ""), "test-model")
+    with pytest.raises(JudgeError, match="no responses to synthesize"):
+        j.synthesize(Context.background(), "original prompt", [])
+
+
+def test_judge_single_passthrough_no_call():
+    called = []
+    j = Judge(FuncProvider(lambda c, r: called.append(1) or Response()), "test-model")
+    chunks = []
+    out = j.synthesize_stream(Context.background(), "p", [Response(model="a", content="single answer", provider="t")],
+                              chunks.append)
+    assert out == "single answer" and chunks == ["single answer"] and not called
+
+
+def test_judge_multiple_calls_judge():
+    def jf(ctx, req):
+        assert "answer a" in req.prompt and "answer b" in req.prompt
+        assert req.model == "test-model"
+        return Response(content="synthesized consensus")
+
+    j = Judge(FuncProvider(jf), "test-model")
+    out = j.synthesize(Context.background(), "original prompt",
+                       [Response(model="a", content="answer a", provider="t"),
+                        Response(model="b", content="answer b", provider="t")])
+    assert out == "synthesized consensus"
+
+
+def test_judge_failure_propagates():
+    j = Judge(fail("judge api error"), "test-model")
+    with pytest.raises(JudgeError, match="judge query failed: judge api error"):
+        j.synthesize(Context.background(), "p", [Response(model="a", content="a"), Response(model="b", content="b")])
+
+
+def test_judge_prompt_template_golden():
+    captured = {}
+
+    def jf(ctx, req):
+        captured["p"] = req.prompt
+        return Response(content="consensus")
+
+    rs = [Response(model="gpt-4o", content="GPT says hello", provider="openai", latency_ns=100_000_000),
+          Response(model="claude-sonnet", content="Claude says hi", provider="anthropic", latency_ns=150_000_000)]
+    Judge(FuncProvider(jf), "judge-model").synthesize(Context.background(), "Say hello", rs)
+    for s in ["Say hello", "gpt-4o", "claude-sonnet", "GPT says hello", "Claude says hi", "openai", "anthropic"]:
+        assert s in captured["p"]
+    import os
+
+    golden = open(os.path.join(os.path.dirname(__file__), "golden", "judge_prompt_say_hello.txt")).read()
+    assert captured["p"] == golden == build_judge_prompt("Say hello", rs)

@@ -1,0 +1,57 @@
+"""Native host runtime: synthetic tokenizer and paged-KV block allocator."""
+
+import pytest
+
+from llm_consensus_amd.consensus import prompt_header, prompt_trailer, response_block
+from llm_consensus_amd.provider.base import Response
+from llm_consensus_amd.utils.native import runtime
+from llm_consensus_amd.utils.tokenizer import Tokenizer
+
+
+@pytest.mark.parametrize("V", [1024, 32000, 128256])
+def test_tokenizer_roundtrip_and_density(V):
+    t = Tokenizer(V)
+    s = "Hello world, this is a test ✓ of the tokenizer\n with\ttabs and 🚀"
+    ids = t.encode(s)
+    assert t.decode(ids) == s
+    assert all(0 <= i < V for i in ids)
+    # generated text = pieces -> ~4 chars/token and exact re-encoding
+    pieces = list(range(256, min(V - 2, 256 + 500)))
+    text = t.decode(pieces)
+    assert len(text) == 4 * len(pieces)
+    assert t.encode(text) == pieces
+
+
+def test_tokenizer_segment_stable_at_judge_blocks():
+    t = Tokenizer(128256)
+    rs = [Response(model="m@1", content=t.decode(list(range(300, 400))), provider="rocm"),
+          Response(model="m@2", content="x y z\n\nabc def", provider="rocm")]
+    segs = [prompt_header("What is 2+2?")] + [response_block(r) for r in rs] + [prompt_trailer()]
+    whole = t.encode("".join(segs))
+    parts = [i for s in segs for i in t.encode(s)]
+    assert whole == parts
+
+
+def test_tokenizer_specials_and_stream_decoder():
+    t = Tokenizer(1024)
+    assert t.eos_id == 1023 and t.bos_id == 1022
+    assert t.decode([t.bos_id, t.eos_id]) == ""
+    d = t.stream_decoder()
+    euro = "€".encode()
+    out = d.push([euro[0]]) + d.push([euro[1]]) + d.push([euro[2]]) + d.flush()
+    assert out == "€"
+
+
+def test_block_allocator():
+    A = runtime().BlockAllocator(10, 64)
+    assert A.num_free == 10 and A.blocks_for(65) == 2
+    a = A.allocate(4)
+    assert len(a) == 4 and A.num_free == 6
+    assert A.allocate(7) == []  # all-or-nothing
+    A.incref(a[:2])
+    A.free(a)
+    assert A.num_free == 8
+    A.free(a[:2])
+    assert A.num_free == 10
+    with pytest.raises(Exception):
+        A.free(a[:1])  # double free

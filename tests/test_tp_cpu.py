@@ -1,0 +1,80 @@
+"""Tensor parallelism on CPU with gloo (SURVEY.md §4.2 "TP / distributed" (a)): a TP=2 engine
+(column/row-parallel linears, residual-folded all-reduce, vocab-parallel lm_head + all-gather,
+sharded MoE experts) must reproduce the TP=1 model's logits and greedy tokens."""
+
+import os
+import socket
+
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _worker(rank, world, port, name, q):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        torch.set_num_threads(1)
+        from llm_consensus_amd.engine import Engine, EngineConfig
+        from llm_consensus_amd.models.config import FAMILIES
+        from llm_consensus_amd.parallel.comm import TPGroup
+
+        cfg = FAMILIES[name]
+        tp = TPGroup(dist.group.WORLD, rank, world)
+        e = Engine(cfg, EngineConfig(device="cpu", max_context=128, seed=5), tp=tp)
+        p = [(i * 13) % 700 + 256 for i in range(24)]
+        s = e.new_sequence()
+        e.prefill([s], [p])
+        logits = e._gather_logits(1).clone()
+        e.free_sequence(s)
+        gen = e.generate_ids(p, 6, temperature=0.0, stop_on_eos=False)
+        if rank == 0:
+            q.put((logits.tolist(), gen))  # plain lists: tensor handles die with the child
+        dist.barrier()
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("name", ["llama-tiny", "mixtral-tiny", "phi3-tiny"])
+def test_tp2_matches_tp1(name):
+    from llm_consensus_amd.engine import Engine, EngineConfig
+    from llm_consensus_amd.models.config import FAMILIES
+
+    ref = Engine(FAMILIES[name], EngineConfig(device="cpu", max_context=128, seed=5))
+    p = [(i * 13) % 700 + 256 for i in range(24)]
+    s = ref.new_sequence()
+    ref.prefill([s], [p])
+    ref_logits = ref.logits[0].clone()
+    ref.free_sequence(s)
+    ref_gen = ref.generate_ids(p, 6, temperature=0.0, stop_on_eos=False)
+
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, name, q)) for r in range(2)]
+    for pr in procs:
+        pr.start()
+    for pr in procs:
+        pr.join(timeout=240)
+    for pr in procs:
+        if pr.is_alive():
+            pr.kill()
+            pr.join()
+    assert all(pr.exitcode == 0 for pr in procs), [pr.exitcode for pr in procs]
+    logits, gen = q.get(timeout=10)
+    logits = torch.tensor(logits)
+    # TP sums partials in a different order (and rounds partials to bf16): small drift only
+    assert (logits[0] - ref_logits).abs().max().item() < 0.05 * ref_logits.abs().max().item()
+    top2 = torch.topk(ref_logits, 2).values
+    if (top2[0] - top2[1]).item() > 0.05:
+        assert gen[0] == ref_gen[0]

@@ -1,21 +1,22 @@
-// K5: paged attention DECODE (one query token per sequence), split-KV with an in-kernel reduce.
+// K5: paged attention DECODE (one query token per sequence), split-KV.
 //
-// Memory-bound on the K/V stream (cdna_hip_programming.md App. B "Attention decode"): K/V go
-// straight to VGPRs, 16 B per lane. Geometry:
+// Batch-1 decode attention on an 8-kv-head model is LATENCY-bound (a 1k-token context is 4 MB of
+// K/V: < 1 µs of HBM time), so the design minimises the serial chain of memory round trips:
 //   grid (grid_chunks, nkv, B), 256 threads = 4 waves; a block owns one kv head and one chunk of
-//   `chunk` context tokens (64 by default: a 1k-token context already yields 128 blocks for an
-//   8-kv-head model), and ALL G = nh/nkv query heads of that kv head (GQA: K/V read once for the
-//   group). A 16-lane group holds one key row (D <= 128 -> 8 bf16 per lane), so a wave scores
-//   4 keys per instruction; each 16-lane group runs its own online softmax, merged with
-//   xor-shuffles (across groups) and LDS (across waves).
-// Cross-block reduce WITHOUT a second launch (Guideline 16, "valid forms", row 1): every block
-// writes its partial (unnormalised acc, m, l) with write-through (sc1, relaxed agent-scope)
-// stores, drains them (s_waitcnt vmcnt(0)) in every storing wave, then one lane takes a ticket
-// on the (sequence, kv head) counter with an agent-scope atomic add; the block that draws the
-// last ticket reads all partials with sc1 loads, writes the bf16 output and re-arms the counter.
-// Placement-independent: no assumption on which XCD/CU runs which chunk.
-// The grid is sized per context bucket by the host (one captured decode graph per bucket); chunks
-// past seq_len exit immediately and take no ticket.
+//   `chunk` context tokens and ALL G = nh/nkv query heads of that kv head (GQA: K/V read once).
+//   * page lookup: when chunk divides the page size the whole block lives in ONE page -> one
+//     uniform (scalar) block-table load; otherwise per token;
+//   * every K/V load of a wave is issued before any math (UN tokens per 16-lane group, 16 B per
+//     lane, a 16-lane group holds one D <= 128 key row) -> one HBM round trip per block;
+//   * each 16-lane group runs an online softmax over its keys; groups merge by xor-shuffles,
+//     waves through LDS; a single live chunk writes the bf16 output directly.
+// Cross-chunk merge, two selectable forms (measured, see profiles/):
+//   REDUCE_KERNEL (default): partials with plain stores, then attn_decode_reduce_kernel —
+//     inside a HIP graph the kernel boundary (~1.2 µs) is cheaper than an in-launch hand-off;
+//   TICKET: write-through (sc1) partial stores + agent-scope ticket; the last-arriving block
+//     reduces with sc1 loads (Guideline 16 valid form, row 1) — no second launch.
+// Grid sized per context bucket by the host (one captured decode graph per bucket); chunks past
+// seq_len exit immediately.
 #include "common.h"
 
 namespace llmc {
@@ -29,7 +30,54 @@ __device__ __forceinline__ float ld_sc1(const float* p) {
   return __hip_atomic_load(const_cast<float*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
-template <int G>
+// Merge chunk partials [nchunks][G][D + 2] into bf16 out rows of the G heads. `lds` holds
+// 2 * G * nchunks + 2 * G floats. LOADER is plain or sc1.
+template <int G, bool SC1>
+__device__ __forceinline__ void reduce_chunks(const float* __restrict__ pb, int nchunks, int D, float* lds,
+                                              bf16_t* __restrict__ out_row) {
+  const int tid = threadIdx.x;
+  const int stride = D + 2;
+  auto ld = [](const float* p) { return SC1 ? ld_sc1(p) : *p; };
+  float* scl = lds;                // [G][nchunks]: m, then exp(m - M)
+  float* lv = scl + G * nchunks;   // [G][nchunks]: l
+  float* Mg = lv + G * nchunks;    // [G]
+  float* Lg = Mg + G;              // [G]
+  for (int i = tid; i < G * nchunks; i += 256) {
+    const int g = i / nchunks, cc = i % nchunks;
+    const float* pc = pb + (static_cast<int64_t>(cc) * G + g) * stride;
+    scl[i] = ld(pc + D);
+    lv[i] = ld(pc + D + 1);
+  }
+  __syncthreads();
+  if (tid < G) {
+    float mx = kNegBig;
+    for (int cc = 0; cc < nchunks; ++cc) mx = fmaxf(mx, scl[tid * nchunks + cc]);
+    float ls = 0.f;
+    for (int cc = 0; cc < nchunks; ++cc) ls += lv[tid * nchunks + cc] * __expf(scl[tid * nchunks + cc] - mx);
+    Mg[tid] = mx;
+    Lg[tid] = ls;
+  }
+  __syncthreads();
+  for (int i = tid; i < G * nchunks; i += 256) scl[i] = __expf(scl[i] - Mg[i / nchunks]);
+  __syncthreads();
+  for (int idx = tid; idx < G * D; idx += 256) {
+    const int g = idx / D, d = idx % D;
+    float o = 0.f;
+    for (int c0 = 0; c0 < nchunks; c0 += 16) {
+      float v[16];
+#pragma unroll
+      for (int j = 0; j < 16; ++j) {
+        const int cc = min(c0 + j, nchunks - 1);  // clamped: branch-free, all 16 loads in flight
+        v[j] = ld(pb + (static_cast<int64_t>(cc) * G + g) * stride + d);
+      }
+#pragma unroll
+      for (int j = 0; j < 16; ++j) o += (c0 + j < nchunks) ? v[j] * scl[g * nchunks + c0 + j] : 0.f;
+    }
+    out_row[g * D + d] = f32_to_bf16(o / Lg[g]);
+  }
+}
+
+template <int G, bool TICKET>
 __global__ __launch_bounds__(256) void attn_decode_kernel(
     const bf16_t* __restrict__ q, int q_stride, const bf16_t* __restrict__ k_cache,
     const bf16_t* __restrict__ v_cache, const int32_t* __restrict__ block_tables, int bt_stride,
@@ -46,6 +94,9 @@ __global__ __launch_bounds__(256) void attn_decode_kernel(
   const int grp = lane / 16, sub = lane % 16;
   const bool active = sub * 8 < D;
   const int d0 = active ? sub * 8 : 0;
+  const int32_t* bt = block_tables + static_cast<int64_t>(b) * bt_stride;
+  const bool one_page = (bs % chunk) == 0;
+  const int64_t page0 = bt[start / bs];  // uniform
 
   // q for the G heads of this kv head, pre-scaled, as packed bf16 for v_dot2.
   u32x4 qv[G];
@@ -69,25 +120,18 @@ __global__ __launch_bounds__(256) void attn_decode_kernel(
     for (int j = 0; j < 8; ++j) acc[g][j] = 0.f;
   }
 
-  const int32_t* bt = block_tables + static_cast<int64_t>(b) * bt_stride;
-  // token t handled by (wave, grp): t = start + wave*4 + grp + 16*i; UN tokens per lane group are
-  // loaded at once (all page lookups first, then all K/V loads: two memory round trips total
-  // for a 64-token chunk instead of one pair per token).
+  // token t handled by (wave, grp): t = start + wave*4 + grp + 16*u
   constexpr int UN = 4;
   for (int t0 = start + wave * 4; t0 < end; t0 += 16 * UN) {
     u32x4 kv[UN], vv[UN];
     bool ok[UN];
-    int64_t page[UN];
 #pragma unroll
     for (int u = 0; u < UN; ++u) {
       const int t = t0 + grp + u * 16;
       ok[u] = t < end;
-      page[u] = bt[(ok[u] ? t : start) / bs];
-    }
-#pragma unroll
-    for (int u = 0; u < UN; ++u) {
-      const int tt = ok[u] ? t0 + grp + u * 16 : start;
-      const int64_t off = ((page[u] * nkv + kvh) * bs + (tt % bs)) * D + d0;
+      const int tt = ok[u] ? t : start;
+      const int64_t page = one_page ? page0 : static_cast<int64_t>(bt[tt / bs]);
+      const int64_t off = ((page * nkv + kvh) * bs + (tt % bs)) * D + d0;
       kv[u] = *reinterpret_cast<const u32x4*>(k_cache + off);
       vv[u] = *reinterpret_cast<const u32x4*>(v_cache + off);
     }
@@ -130,7 +174,7 @@ __global__ __launch_bounds__(256) void attn_decode_kernel(
     }
   }
 
-  // merge the 4 waves through LDS: red[wave][g][D + 2]; then scratch for the reducer
+  // merge the 4 waves through LDS: red[wave][g][D + 2]
   extern __shared__ __attribute__((aligned(16))) char smem[];
   float* red = reinterpret_cast<float*>(smem);
   const int stride = D + 2;
@@ -149,8 +193,8 @@ __global__ __launch_bounds__(256) void attn_decode_kernel(
     }
   }
   __syncthreads();
-  const int nh = nkv * G;
   float* pb = part + ((static_cast<int64_t>(b) * nkv + kvh) * max_chunks) * G * stride;
+  bf16_t* out_row = out + static_cast<int64_t>(b) * out_stride + kvh * G * D;
   for (int idx = tid; idx < G * D; idx += 256) {
     const int g = idx / D, d = idx % D;
     float mx = kNegBig;
@@ -165,88 +209,96 @@ __global__ __launch_bounds__(256) void attn_decode_kernel(
       o += r[d] * sc;
     }
     if (nchunks == 1) {
-      out[static_cast<int64_t>(b) * out_stride + (kvh * G + g) * D + d] = f32_to_bf16(o / lsum);
+      out_row[g * D + d] = f32_to_bf16(o / lsum);
     } else {
       float* pc = pb + (static_cast<int64_t>(c) * G + g) * stride;
-      st_sc1(pc + d, o);
-      if (d == 0) {
-        st_sc1(pc + D, mx);
-        st_sc1(pc + D + 1, lsum);
+      if constexpr (TICKET) {
+        st_sc1(pc + d, o);
+        if (d == 0) {
+          st_sc1(pc + D, mx);
+          st_sc1(pc + D + 1, lsum);
+        }
+      } else {
+        pc[d] = o;
+        if (d == 0) {
+          pc[D] = mx;
+          pc[D + 1] = lsum;
+        }
       }
     }
   }
-  if (nchunks == 1) return;
-
-  // ---- ticket: the last-arriving chunk block reduces ----
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every storing wave drains its sc1 stores
-  __syncthreads();
-  int* flag = reinterpret_cast<int*>(red + 4 * G * stride);
-  int* ctr = counters + b * nkv + kvh;
-  if (tid == 0) {
-    const int old = __hip_atomic_fetch_add(ctr, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    *flag = (old == nchunks - 1) ? 1 : 0;
-  }
-  __syncthreads();
-  if (*flag == 0) return;
-
-  // Reducer. Phase 1: every (g, chunk) m and l in parallel (one sc1 round trip) into LDS.
-  float* scl = red + 4 * G * stride + 4;  // [G][nchunks]: m, then exp(m - M)
-  float* lv = scl + G * nchunks;          // [G][nchunks]: l
-  float* Mg = lv + G * nchunks;           // [G]
-  float* Lg = Mg + G;                     // [G]
-  for (int i = tid; i < G * nchunks; i += 256) {
-    const int g = i / nchunks, cc = i % nchunks;
-    const float* pc = pb + (static_cast<int64_t>(cc) * G + g) * stride;
-    scl[i] = ld_sc1(pc + D);
-    lv[i] = ld_sc1(pc + D + 1);
-  }
-  __syncthreads();
-  if (tid < G) {
-    float mx = kNegBig;
-    for (int cc = 0; cc < nchunks; ++cc) mx = fmaxf(mx, scl[tid * nchunks + cc]);
-    float ls = 0.f;
-    for (int cc = 0; cc < nchunks; ++cc) ls += lv[tid * nchunks + cc] * __expf(scl[tid * nchunks + cc] - mx);
-    Mg[tid] = mx;
-    Lg[tid] = ls;
-  }
-  __syncthreads();
-  for (int i = tid; i < G * nchunks; i += 256) scl[i] = __expf(scl[i] - Mg[i / nchunks]);
-  __syncthreads();
-  // Phase 2: outputs; chunk partials loaded 16 at a time with clamped (branch-free) indices so
-  // all loads of a batch are in flight together (no per-load vmcnt(0)).
-  for (int idx = tid; idx < G * D; idx += 256) {
-    const int g = idx / D, d = idx % D;
-    float o = 0.f;
-    for (int c0 = 0; c0 < nchunks; c0 += 16) {
-      float v[16];
-#pragma unroll
-      for (int j = 0; j < 16; ++j) {
-        const int cc = min(c0 + j, nchunks - 1);
-        v[j] = ld_sc1(pb + (static_cast<int64_t>(cc) * G + g) * stride + d);
-      }
-#pragma unroll
-      for (int j = 0; j < 16; ++j) o += (c0 + j < nchunks) ? v[j] * scl[g * nchunks + c0 + j] : 0.f;
+  if constexpr (TICKET) {
+    if (nchunks == 1) return;
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every storing wave drains its sc1 stores
+    __syncthreads();
+    int* flag = reinterpret_cast<int*>(red + 4 * G * stride);
+    int* ctr = counters + b * nkv + kvh;
+    if (tid == 0) {
+      const int old = __hip_atomic_fetch_add(ctr, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      *flag = (old == nchunks - 1) ? 1 : 0;
     }
-    out[static_cast<int64_t>(b) * out_stride + (kvh * G + g) * D + d] = f32_to_bf16(o / Lg[g]);
+    __syncthreads();
+    if (*flag == 0) return;
+    reduce_chunks<G, true>(pb, nchunks, D, red + 4 * G * stride + 4, out_row);
+    if (tid == 0) __hip_atomic_store(ctr, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
-  if (tid == 0) __hip_atomic_store(ctr, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  (void)nh;
+}
+
+// grid (nkv, B), 256 threads: merge the chunk partials of one kv head's G query heads.
+template <int G>
+__global__ __launch_bounds__(256) void attn_decode_reduce_kernel(const float* __restrict__ part,
+                                                                 const int32_t* __restrict__ seq_lens,
+                                                                 bf16_t* __restrict__ out, int out_stride, int nkv,
+                                                                 int D, int chunk, int max_chunks) {
+  const int kvh = blockIdx.x, b = blockIdx.y;
+  const int L = seq_lens[b];
+  const int nchunks = (L + chunk - 1) / chunk;
+  if (nchunks <= 1) return;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const float* pb = part + ((static_cast<int64_t>(b) * nkv + kvh) * max_chunks) * G * (D + 2);
+  reduce_chunks<G, false>(pb, nchunks, D, reinterpret_cast<float*>(smem),
+                          out + static_cast<int64_t>(b) * out_stride + kvh * G * D);
 }
 
 template <int G>
-static int launch_decode(dim3 grid, size_t lds, hipStream_t s, const void* q, int q_stride, const void* kc,
+static int launch_decode(int B, int nkv, int grid_chunks, hipStream_t s, const void* q, int q_stride, const void* kc,
                          const void* vc, const void* bt, int bt_stride, const void* sl, void* part, void* ctr,
-                         void* out, int out_stride, int nkv, int D, int bs, int chunk, int max_chunks, float scale) {
-  auto kern = attn_decode_kernel<G>;
-  static bool attr = false;
-  if (lds > 64 * 1024 && !attr) {
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize,
-                              160 * 1024);
-    attr = true;
+                         void* out, int out_stride, int D, int bs, int chunk, int max_chunks, float scale,
+                         bool ticket) {
+  const size_t red_lds = static_cast<size_t>(4) * G * (D + 2) * sizeof(float);
+  const size_t scl_lds = (static_cast<size_t>(G) * (2 * max_chunks + 2)) * sizeof(float);
+  if (red_lds + 16 + scl_lds > 160 * 1024) return -3;
+  dim3 grid(grid_chunks, nkv, B);
+  if (ticket) {
+    auto kern = attn_decode_kernel<G, true>;
+    const size_t lds = red_lds + 16 + scl_lds;
+    static bool attr = false;
+    if (lds > 64 * 1024 && !attr) {
+      (void)hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize,
+                                160 * 1024);
+      attr = true;
+    }
+    kern<<<grid, 256, lds, s>>>((const bf16_t*)q, q_stride, (const bf16_t*)kc, (const bf16_t*)vc, (const int32_t*)bt,
+                                bt_stride, (const int32_t*)sl, (float*)part, (int*)ctr, (bf16_t*)out, out_stride, nkv,
+                                D, bs, chunk, max_chunks, scale);
+    return static_cast<int>(hipGetLastError());
   }
-  kern<<<grid, 256, lds, s>>>((const bf16_t*)q, q_stride, (const bf16_t*)kc, (const bf16_t*)vc, (const int32_t*)bt,
-                              bt_stride, (const int32_t*)sl, (float*)part, (int*)ctr, (bf16_t*)out, out_stride, nkv,
-                              D, bs, chunk, max_chunks, scale);
+  attn_decode_kernel<G, false><<<grid, 256, red_lds, s>>>(
+      (const bf16_t*)q, q_stride, (const bf16_t*)kc, (const bf16_t*)vc, (const int32_t*)bt, bt_stride,
+      (const int32_t*)sl, (float*)part, (int*)ctr, (bf16_t*)out, out_stride, nkv, D, bs, chunk, max_chunks, scale);
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return static_cast<int>(e);
+  if (grid_chunks > 1) {
+    auto rk = attn_decode_reduce_kernel<G>;
+    static bool attr = false;
+    if (scl_lds > 64 * 1024 && !attr) {
+      (void)hipFuncSetAttribute(reinterpret_cast<const void*>(rk), hipFuncAttributeMaxDynamicSharedMemorySize,
+                                160 * 1024);
+      attr = true;
+    }
+    rk<<<dim3(nkv, B), 256, scl_lds, s>>>((const float*)part, (const int32_t*)sl, (bf16_t*)out, out_stride, nkv, D,
+                                           chunk, max_chunks);
+  }
   return static_cast<int>(hipGetLastError());
 }
 
@@ -255,22 +307,19 @@ static int launch_decode(dim3 grid, size_t lds, hipStream_t s, const void* q, in
 using namespace llmc;
 
 // part: f32 workspace [B, nkv, max_chunks, G, D + 2]; counters: int32 [B, nkv], zero-initialised
-// once (each launch re-arms them). grid_chunks <= max_chunks bounds the context of this launch.
+// once (the TICKET form re-arms them every launch). grid_chunks <= max_chunks bounds the context
+// of this launch. mode: 0 = partial + reduce kernel, 1 = in-launch ticket reduce.
 extern "C" int llmc_attn_decode(const void* q, int q_stride, const void* k_cache, const void* v_cache,
                                 const void* block_tables, int bt_stride, const void* seq_lens, void* part,
                                 void* counters, void* out, int out_stride, int B, int nh, int nkv, int D, int bs,
-                                int chunk, int grid_chunks, int max_chunks, float scale, hipStream_t s) {
+                                int chunk, int grid_chunks, int max_chunks, float scale, int mode, hipStream_t s) {
   if (D % 8 != 0 || D > 128 || nh % nkv != 0 || grid_chunks > max_chunks) return -1;
-  const int G = nh / nkv;
-  dim3 grid(grid_chunks, nkv, B);
-  const size_t lds =
-      (static_cast<size_t>(4) * G * (D + 2) + 4 + static_cast<size_t>(G) * (2 * max_chunks + 2)) * sizeof(float);
-  if (lds > 160 * 1024) return -3;
-  switch (G) {
-    case 1: return launch_decode<1>(grid, lds, s, q, q_stride, k_cache, v_cache, block_tables, bt_stride, seq_lens, part, counters, out, out_stride, nkv, D, bs, chunk, max_chunks, scale);
-    case 2: return launch_decode<2>(grid, lds, s, q, q_stride, k_cache, v_cache, block_tables, bt_stride, seq_lens, part, counters, out, out_stride, nkv, D, bs, chunk, max_chunks, scale);
-    case 4: return launch_decode<4>(grid, lds, s, q, q_stride, k_cache, v_cache, block_tables, bt_stride, seq_lens, part, counters, out, out_stride, nkv, D, bs, chunk, max_chunks, scale);
-    case 8: return launch_decode<8>(grid, lds, s, q, q_stride, k_cache, v_cache, block_tables, bt_stride, seq_lens, part, counters, out, out_stride, nkv, D, bs, chunk, max_chunks, scale);
+  const bool ticket = mode == 1;
+  switch (nh / nkv) {
+    case 1: return launch_decode<1>(B, nkv, grid_chunks, s, q, q_stride, k_cache, v_cache, block_tables, bt_stride, seq_lens, part, counters, out, out_stride, D, bs, chunk, max_chunks, scale, ticket);
+    case 2: return launch_decode<2>(B, nkv, grid_chunks, s, q, q_stride, k_cache, v_cache, block_tables, bt_stride, seq_lens, part, counters, out, out_stride, D, bs, chunk, max_chunks, scale, ticket);
+    case 4: return launch_decode<4>(B, nkv, grid_chunks, s, q, q_stride, k_cache, v_cache, block_tables, bt_stride, seq_lens, part, counters, out, out_stride, D, bs, chunk, max_chunks, scale, ticket);
+    case 8: return launch_decode<8>(B, nkv, grid_chunks, s, q, q_stride, k_cache, v_cache, block_tables, bt_stride, seq_lens, part, counters, out, out_stride, D, bs, chunk, max_chunks, scale, ticket);
     default: return -2;
   }
 }

@@ -23,7 +23,7 @@ from typing import List, Optional, TextIO
 
 from . import ui
 from .catalog import PROVIDER_STUB, UnknownModel, dump_catalog, resolve
-from .consensus import Judge
+from .consensus import Judge, prompt_header, response_block
 from .context import Context
 from .flags import FlagSet, parse_or_exit
 from .output import Result, encode_result
@@ -171,8 +171,9 @@ def init_registry(cfg: Config) -> Registry:
         from .provider.local import LocalBackend
 
         gpus = [int(x) for x in cfg.gpus.split(",") if x.strip()] if cfg.gpus else None
+        counts = {m: cfg.models.count(m) for m in cfg.models}
         try:
-            backend = LocalBackend(local_specs, judge=cfg.judge, gpus=gpus, trace=cfg.trace)
+            backend = LocalBackend(local_specs, judge=cfg.judge, gpus=gpus, trace=cfg.trace, counts=counts)
         except Exception as e:  # noqa: BLE001
             raise CLIError(f"initializing provider for {local_specs[0].name}: {e}") from None
         for spec in local_specs:
@@ -188,6 +189,10 @@ def generate_run_id() -> str:
 def run(argv: List[str], stdout: TextIO = sys.stdout, stderr: TextIO = sys.stderr, stdin=None,
         root_ctx: Optional[Context] = None) -> None:
     cfg = parse_flags(argv, stdout, stderr, stdin)
+    if cfg.trace:
+        from .utils import trace
+
+        trace.enable(True)
     ctx = root_ctx or Context.background()
     show_ui = ui.is_terminal(stderr) and not cfg.quiet and not cfg.json
     start = time.monotonic()
@@ -214,11 +219,22 @@ def _run_with_registry(cfg: Config, registry: Registry, ctx: Context, show_ui: b
     progress = ui.Progress(stderr, cfg.models, not show_ui)
     progress.start()
     tmpl = _request_template(cfg)
+    # Local judge: prefill the template header now and each response block as it completes
+    # (SURVEY.md §7.4), so only the last block + trailer remain on the critical path.
+    on_resp = None
+    try:
+        jp = registry.get(cfg.judge)
+    except Exception:  # noqa: BLE001
+        jp = None
+    if jp is not None and hasattr(jp, "open_session") and len(cfg.models) > 1:
+        jp.open_session(prompt_header(cfg.prompt))
+        on_resp = lambda r: jp.extend_session(response_block(r))  # noqa: E731
     runner = Runner(registry, cfg.timeout, tmpl).with_callbacks(Callbacks(
         on_model_start=progress.model_started,
         on_model_stream=progress.model_streaming,
         on_model_complete=progress.model_completed,
         on_model_error=progress.model_failed,
+        on_model_response=on_resp,
     ))
     try:
         result = runner.run(ctx, cfg.models, cfg.prompt)
@@ -280,6 +296,12 @@ def _run_with_registry(cfg: Config, registry: Registry, ctx: Context, show_ui: b
         if cfg.trace:
             from .utils import trace
 
+            seen = set()
+            for m in registry.models():
+                be = getattr(registry.get(m), "backend", None)
+                if be is not None and id(be) not in seen:
+                    seen.add(id(be))
+                    be.collect_traces()
             trace.dump(os.path.join(run_dir, "trace.json"))
 
     text = encode_result(out)

@@ -93,6 +93,9 @@ class Judge:
         if len(responses) == 0:
             raise JudgeError("no responses to synthesize")
         if len(responses) == 1:
+            close = getattr(self.provider, "close_session", None)
+            if close is not None:  # discard the partially prefilled judge KV
+                close()
             if callback is not None:
                 callback(responses[0].content)
             return responses[0].content
@@ -103,7 +106,11 @@ class Judge:
 
             req = dataclasses.replace(self._tmpl, model=self.model, prompt=prompt)
         try:
-            resp = self.provider.query_stream(ctx, req, callback)
+            finish = getattr(self.provider, "query_stream_session", None)
+            if finish is not None:  # local judge: header + blocks already prefilled incrementally
+                resp = finish(ctx, req, callback)
+            else:
+                resp = self.provider.query_stream(ctx, req, callback)
         except Exception as e:  # noqa: BLE001
             raise JudgeError(f"judge query failed: {e}") from e
         return resp.content

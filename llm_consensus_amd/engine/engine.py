@@ -40,7 +40,8 @@ from ..utils.native import runtime
 class EngineConfig:
     device: str = "cuda:0"
     max_context: int = 8192
-    max_batch: int = 1
+    max_batch: int = 1   # decode rows per step (GEMV M <= 4)
+    max_seqs: int = 0    # live sequences the KV pool is sized for (0 = max_batch)
     block_size: int = 64
     kv_blocks: int = 0
     seed: int = 0
@@ -63,11 +64,15 @@ class SamplingParams:
 
 
 class Sequence:
-    def __init__(self, row: int):
-        self.row = row
+    """A KV-cache-backed token sequence. It is bound to a decode row only while it decodes."""
+
+    def __init__(self, sid: int):
+        self.sid = sid
+        self.row = -1
         self.blocks: List[int] = []
         self.length = 0
         self.has_logits = False
+        self.logits: Optional[torch.Tensor] = None  # last-token logits [V_local] after prefill
 
 
 class EngineError(Exception):
@@ -99,7 +104,7 @@ class Engine:
         self.scale = 1.0 / math.sqrt(self.D)
         self.bs = e.block_size
         self.max_blocks_per_seq = (e.max_context + self.bs - 1) // self.bs + 1
-        nb = e.kv_blocks or e.max_batch * self.max_blocks_per_seq + 2
+        nb = e.kv_blocks or max(e.max_seqs, e.max_batch) * self.max_blocks_per_seq + 2
         self.alloc = runtime().BlockAllocator(nb, self.bs)
         dev = self.device
         L = cfg.n_layers
@@ -109,7 +114,7 @@ class Engine:
         self.cos_t, self.sin_t = cos_t.to(dev), sin_t.to(dev)
         self._alloc_decode_buffers()
         self._graphs: Dict[int, "torch.cuda.CUDAGraph"] = {}
-        self.free_rows = list(range(e.max_batch))
+        self._next_sid = 0
 
     # ------------------------------------------------------------------------------------------
     def _on_stream(self):
@@ -171,18 +176,16 @@ class Engine:
 
     # -- sequence management -------------------------------------------------------------------
     def new_sequence(self) -> Sequence:
-        if not self.free_rows:
-            raise EngineError("no free decode rows")
-        return Sequence(self.free_rows.pop(0))
+        self._next_sid += 1
+        return Sequence(self._next_sid)
 
     def free_sequence(self, seq: Sequence) -> None:
         if seq.blocks:
             self.alloc.free(seq.blocks)
             seq.blocks = []
         seq.length = 0
-        if seq.row not in self.free_rows:
-            self.free_rows.append(seq.row)
-            self.free_rows.sort()
+        seq.logits = None
+        seq.has_logits = False
 
     def _reserve(self, seq: Sequence, total_tokens: int) -> None:
         need = self.alloc.blocks_for(total_tokens) - len(seq.blocks)
@@ -193,8 +196,13 @@ class Engine:
             if not got:
                 raise EngineError(f"KV cache exhausted ({self.alloc.num_free} blocks free, need {need})")
             seq.blocks.extend(got)
-            bt = torch.tensor(seq.blocks, dtype=torch.int32)
-            self.block_tables[seq.row, : len(seq.blocks)].copy_(bt.to(self.device), non_blocking=False)
+
+    def _block_table(self, seqs: List[Sequence]) -> torch.Tensor:
+        """[len(seqs), max_blocks] int32 block table on the engine device."""
+        bt = torch.zeros(len(seqs), self.max_blocks_per_seq, dtype=torch.int32)
+        for i, s in enumerate(seqs):
+            bt[i, : len(s.blocks)] = torch.tensor(s.blocks, dtype=torch.int32)
+        return bt.to(self.device, non_blocking=True) if self.on_gpu else bt
 
     # -- prefill ----------------------------------------------------------------------------------
     @torch.no_grad()
@@ -204,7 +212,7 @@ class Engine:
             pending = [(s, list(t)) for s, t in zip(seqs, token_lists) if t]
             chunk = self.ecfg.prefill_chunk
             while pending:
-                batch, rest, budget = [], [], chunk
+                batch, rest, budget, finals = [], [], chunk, set()
                 for s, t in pending:
                     if budget <= 0:
                         rest.append((s, t))
@@ -214,13 +222,14 @@ class Engine:
                     budget -= len(take)
                     if len(take) < len(t):
                         rest.append((s, t[len(take):]))
-                last = not rest
-                self._prefill_chunk(batch, want_logits and last, all_seqs=seqs if last else None)
+                    else:
+                        finals.add(s)
+                self._prefill_chunk(batch, want_logits, finals)
                 pending = rest
 
-    def _prefill_chunk(self, batch, want_logits: bool, all_seqs) -> None:
+    def _prefill_chunk(self, batch, want_logits: bool, finals) -> None:
         dev, c = self.device, self.cfg
-        ids, pos, slots, q_start, q_lens, ctx_lens, rows = [], [], [], [], [], [], []
+        ids, pos, slots, q_start, q_lens, ctx_lens = [], [], [], [], [], []
         for s, toks in batch:
             self._reserve(s, s.length + len(toks))
             q_start.append(len(ids))
@@ -232,7 +241,6 @@ class Engine:
                 slots.append(s.blocks[p // self.bs] * self.bs + p % self.bs)
             s.length += len(toks)
             ctx_lens.append(s.length)
-            rows.append(s.row)
         T = len(ids)
         i32 = dict(dtype=torch.int32)
         ids_d = torch.tensor(ids, **i32).to(dev, non_blocking=True)
@@ -241,8 +249,7 @@ class Engine:
         qs_d = torch.tensor(q_start, **i32).to(dev, non_blocking=True)
         ql_d = torch.tensor(q_lens, **i32).to(dev, non_blocking=True)
         cl_d = torch.tensor(ctx_lens, **i32).to(dev, non_blocking=True)
-        bt = self.block_tables[torch.tensor(rows, dtype=torch.long, device=dev)] if self.on_gpu else \
-            self.block_tables[torch.tensor(rows, dtype=torch.long)]
+        bt = self._block_table([s for s, _ in batch])
         max_qlen = max(q_lens)
 
         h = ops.embedding(ids_d, self.w.embed)
@@ -262,18 +269,17 @@ class Engine:
             else:
                 act = ops.linear(xn, Lw.w_gu, EPI_SILU)
                 self._row_parallel(act, Lw.w_down, h)
-        if want_logits:
-            last = []
-            for (s, toks), st in zip(batch, q_start):
-                last.append(st + len(toks) - 1)
-            last_d = torch.tensor(last, dtype=torch.long).to(dev)
+        # last-token logits for every sequence whose final prompt token is in this chunk
+        sel = [i for i, (s, _) in enumerate(batch) if want_logits and s in finals]
+        for i0 in range(0, len(sel), ops.GEMV_MAX_M):
+            part = sel[i0:i0 + ops.GEMV_MAX_M]
+            last_d = torch.tensor([q_start[i] + q_lens[i] - 1 for i in part], dtype=torch.long).to(dev)
             hl = h.index_select(0, last_d)
-            rows_t = torch.tensor(rows, dtype=torch.long).to(dev)
-            B = len(rows)
-            lg = torch.empty(B, self.w.vocab_local, dtype=torch.float32, device=dev)
+            lg = torch.empty(len(part), self.w.vocab_local, dtype=torch.float32, device=dev)
             ops.linear(hl, self.w.lm_head, EPI_F32, out=lg, norm_w=self.w.final_norm, eps=c.rms_eps)
-            self.logits_local.index_copy_(0, rows_t, lg)
-            for s, _ in batch:
+            for j, i in enumerate(part):
+                s = batch[i][0]
+                s.logits = lg[j]
                 s.has_logits = True
 
     def _row_parallel(self, x: torch.Tensor, W: torch.Tensor, h: torch.Tensor) -> None:
@@ -374,6 +380,13 @@ class Engine:
             out.view(B, self.tp.size, self.w.vocab_local).copy_(buf.permute(1, 0, 2))
         return out
 
+    def full_logits(self, seq: Sequence) -> torch.Tensor:
+        """Full-vocabulary last-token logits of a prefilled sequence (collective under TP)."""
+        if self.tp.size == 1:
+            return seq.logits
+        self.logits_local[0].copy_(seq.logits)
+        return self._gather_logits(1)[0]
+
     def _sample(self, B: int, logits: torch.Tensor) -> None:
         use_topkp = bool(self._use_topkp)
         ops.sample(logits, self.inv_temp[:B], self.top_k[:B], self.top_p[:B], self.seeds[:B], self.positions[:B],
@@ -428,20 +441,23 @@ class Engine:
         """Sample from each sequence's prefill logits, then decode until every row hits max_tokens /
         EOS. ``on_tokens(i, new_ids)`` streams tokens (i indexes ``seqs``). Rows must be 0..B-1."""
         B = len(seqs)
-        if sorted(s.row for s in seqs) != list(range(B)):
-            raise EngineError("decode rows must be 0..B-1")
+        if B > self.ecfg.max_batch:
+            raise EngineError(f"{B} sequences > max_batch {self.ecfg.max_batch}")
         S = self.ecfg.steps_per_graph
         eos = self._eos_id()
         with self._on_stream(), trace.span("decode", engine=self.name, rows=B):
-            order = sorted(range(B), key=lambda i: seqs[i].row)
             max_new = max(p.max_tokens for p in params)
             self._use_topkp = any((p.top_k > 0 or p.top_p < 1.0) for p in params)
-            for i in order:
-                s, p = seqs[i], params[i]
+            for i, (s, p) in enumerate(zip(seqs, params)):
                 if not s.has_logits:
                     raise EngineError("sequence has no prefill logits")
                 self._reserve(s, s.length + p.max_tokens + S + 1)
-                r = s.row
+            # bind sequences to decode rows 0..B-1: block tables and prefill logits into the rows
+            self.block_tables[:B].copy_(self._block_table(seqs))
+            for i, (s, p) in enumerate(zip(seqs, params)):
+                s.row = i
+                r = i
+                self.logits_local[r].copy_(s.logits)
                 self.inv_temp[r] = 0.0 if p.temperature <= 0 else 1.0 / p.temperature
                 self.top_k[r] = p.top_k
                 self.top_p[r] = p.top_p

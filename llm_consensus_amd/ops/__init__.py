@@ -8,6 +8,7 @@ stream, so every op is capturable in a HIP graph.
 
 from __future__ import annotations
 
+import os
 from typing import Optional
 
 import torch
@@ -158,8 +159,11 @@ def decode_attn_workspace(B, nh, nkv, D, max_chunks, device):
     return part, counters
 
 
+ATTN_DECODE_MODE = int(os.environ.get("LLMC_ATTN_TICKET", "0"))  # 0: partial + reduce kernel, 1: ticket
+
+
 def attn_decode(q, k_cache, v_cache, block_tables, seq_lens, out, part, counters, nh, nkv, D, bs, chunk, scale,
-                grid_chunks: Optional[int] = None):
+                grid_chunks: Optional[int] = None, mode: Optional[int] = None):
     if not q.is_cuda:
         out.copy_(oracle.attn_decode(q, k_cache, v_cache, block_tables, seq_lens, nh, nkv, D, bs, scale))
         return out
@@ -168,7 +172,7 @@ def attn_decode(q, k_cache, v_cache, block_tables, seq_lens, out, part, counters
     gc = max_chunks if grid_chunks is None else min(grid_chunks, max_chunks)
     kernels().attn_decode(_p(q), q.stride(0), _p(k_cache), _p(v_cache), _p(block_tables), block_tables.stride(0),
                           _p(seq_lens), _p(part), _p(counters), _p(out), out.stride(0), B, nh, nkv, D, bs, chunk, gc,
-                          max_chunks, float(scale), _s(q))
+                          max_chunks, float(scale), ATTN_DECODE_MODE if mode is None else mode, _s(q))
     return out
 
 

@@ -1,0 +1,101 @@
+"""Placement solver: which GPU(s) host each model engine (T3).
+
+Replaces "the remote API's job". Inputs: the distinct local models of a run (responders + judge),
+each with a TP degree, and the node's GPUs (288 GB HBM3E each). Rules:
+  1. TP groups first, on contiguous, aligned GPU ranges (xGMI is fully connected, but aligned
+     groups {0-3},{4-7} keep two TP=4 models on disjoint halves — BASELINE config 4);
+  2. single-GPU responders spread over the GPUs with the fewest engines (one replica per GPU
+     when possible: decode is HBM-bound, co-located engines share bandwidth);
+  3. the judge goes to the least-loaded GPU (a free GPU if any; else GPU 0, time-sharing via its
+     own hipStream — BASELINE config 3);
+  4. memory check: weights + KV pool must fit in the usable HBM of every GPU it touches.
+"""
+
+from __future__ import annotations
+
+import dataclasses
+from typing import Dict, List, Optional, Sequence
+
+HBM_BYTES = 288 * 10**9
+USABLE_FRACTION = 0.92
+
+
+@dataclasses.dataclass
+class ModelDemand:
+    name: str
+    weight_bytes: int
+    kv_bytes: int
+    tp: int = 1
+    is_judge: bool = False
+
+
+@dataclasses.dataclass
+class Placement:
+    gpus: Dict[str, List[int]]  # model name -> GPU ids (len == tp)
+
+    def models_on(self, gpu: int) -> List[str]:
+        return [m for m, g in self.gpus.items() if gpu in g]
+
+    def used_gpus(self) -> List[int]:
+        return sorted({g for gs in self.gpus.values() for g in gs})
+
+
+class PlacementError(Exception):
+    pass
+
+
+def solve(demands: Sequence[ModelDemand], gpu_ids: Sequence[int], hbm_bytes: int = HBM_BYTES) -> Placement:
+    gpu_ids = list(gpu_ids)
+    if not gpu_ids:
+        raise PlacementError("no GPUs available")
+    cap = hbm_bytes * USABLE_FRACTION
+    used = {g: 0.0 for g in gpu_ids}
+    count = {g: 0 for g in gpu_ids}
+    out: Dict[str, List[int]] = {}
+
+    def fits(g: int, b: float) -> bool:
+        return used[g] + b <= cap
+
+    def take(name: str, gs: List[int], per_gpu: float) -> None:
+        for g in gs:
+            used[g] += per_gpu
+            count[g] += 1
+        out[name] = gs
+
+    # 1. tensor-parallel models: aligned contiguous groups, least-loaded group first
+    for d in sorted((d for d in demands if d.tp > 1), key=lambda d: -d.tp):
+        if d.tp > len(gpu_ids):
+            raise PlacementError(f"{d.name}: tp={d.tp} needs {d.tp} GPUs, only {len(gpu_ids)} available")
+        per = (d.weight_bytes + d.kv_bytes) / d.tp
+        groups = [gpu_ids[i:i + d.tp] for i in range(0, len(gpu_ids) - d.tp + 1, d.tp)]
+        groups = [g for g in groups if all(fits(x, per) for x in g)]
+        if not groups:
+            raise PlacementError(f"{d.name}: no GPU group with {per / 1e9:.1f} GB free per GPU")
+        best = min(groups, key=lambda g: (sum(count[x] for x in g), g[0]))
+        take(d.name, best, per)
+    # 2. single-GPU responders, then 3. the judge
+    singles = [d for d in demands if d.tp == 1 and not d.is_judge] + [d for d in demands if d.tp == 1 and d.is_judge]
+    for d in singles:
+        per = d.weight_bytes + d.kv_bytes
+        cands = [g for g in gpu_ids if fits(g, per)]
+        if not cands:
+            raise PlacementError(f"{d.name}: needs {per / 1e9:.1f} GB, no GPU has that free")
+        best = min(cands, key=lambda g: (count[g], used[g], g))
+        take(d.name, [best], per)
+    return Placement(out)
+
+
+def describe(p: Placement) -> str:
+    return "; ".join(f"{m}->{','.join(map(str, g))}" for m, g in sorted(p.gpus.items()))
+
+
+def default_gpus(requested: Optional[List[int]] = None) -> List[int]:
+    if requested:
+        return list(requested)
+    try:
+        import torch
+
+        n = torch.cuda.device_count()  # does not initialise the GPU on this image
+    except Exception:  # noqa: BLE001
+        n = 0
+    return list(range(n))

@@ -1,0 +1,349 @@
+"""Local MI355X provider: the replacement for the remote OpenAI/Anthropic/Google adapters
+(reference ``internal/provider/{openai,anthropic,google}.go``).
+
+``LocalBackend`` places every local model of the run on the node's GPUs (``parallel/placement``),
+spawns one worker process per used GPU (``runtime/worker``), and multiplexes their token streams.
+``LocalProvider.query_stream`` keeps the reference contract: incremental text chunks go to the
+callback, the returned ``content`` is their concatenation, ``latency`` spans request → end of
+stream. The "transport" is a pipe to the worker instead of HTTPS+SSE; cancellation/deadline
+are checked between token batches and propagate to the worker (the engine stops within one
+decode graph replay, a few ms).
+
+Judge sessions: the judge prompt is rendered as header + per-response blocks in
+completion order + trailer, so the judge engine prefills the header at run start and each block
+as its response completes (``open_session`` / ``extend_session``); at synthesis time only the
+last block's remainder and the trailer are prefilled before decoding.
+"""
+
+from __future__ import annotations
+
+import itertools
+import os
+import queue
+import socket
+import threading
+import time
+import zlib
+from typing import Dict, List, Optional
+
+from ..catalog import PROVIDER_LOCAL, ModelSpec
+from ..context import Context, ContextError
+from ..parallel.placement import ModelDemand, default_gpus, describe, solve
+from ..utils import trace as tracing
+from ..utils.tokenizer import get_tokenizer
+from .base import Request, Response, StreamCallback
+
+DEFAULT_MAX_TOKENS = 4096
+RESPONDER_CONTEXT = 16384
+JUDGE_CONTEXT = 131072
+
+
+class LocalError(Exception):
+    pass
+
+
+def _free_port() -> int:
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+class _Worker:
+    def __init__(self, backend: "LocalBackend", gpu: int, conn, proc):
+        self.backend = backend
+        self.gpu = gpu
+        self.conn = conn
+        self.proc = proc
+        self.send_lock = threading.Lock()
+        self.ready = threading.Event()
+        self.fatal: Optional[str] = None
+        self.info = None
+        self.t = threading.Thread(target=self._recv_loop, daemon=True, name=f"worker-rx:{gpu}")
+        self.t.start()
+
+    def send(self, msg) -> None:
+        with self.send_lock:
+            self.conn.send(msg)
+
+    def _recv_loop(self) -> None:
+        while True:
+            try:
+                msg = self.conn.recv()
+            except (EOFError, OSError):
+                self.fatal = self.fatal or f"worker gpu{self.gpu} exited"
+                self.ready.set()
+                self.backend._worker_died(self)
+                return
+            kind = msg[0]
+            if kind == "ready":
+                self.info = msg[1]
+                self.ready.set()
+            elif kind == "fatal":
+                self.fatal = msg[1]
+                self.ready.set()
+            elif kind == "trace":
+                tracing.add_events(msg[1])
+            else:
+                self.backend._deliver(msg)
+
+
+class LocalBackend:
+    """Owns the worker processes of one run and routes requests to them."""
+
+    def __init__(self, specs: List[ModelSpec], judge: Optional[str] = None, gpus: Optional[List[int]] = None,
+                 trace: bool = False, counts: Optional[Dict[str, int]] = None,
+                 max_context: Optional[Dict[str, int]] = None, start_timeout: float = 1800.0):
+        import multiprocessing as mp
+
+        self.specs = {s.name: s for s in specs}
+        self.judge = judge
+        force_cpu = os.environ.get("LLMC_DEVICE", "") == "cpu"
+        gpu_ids = [-1] if force_cpu else default_gpus(gpus)
+        if not gpu_ids:
+            raise LocalError("no ROCm GPU visible (set LLMC_DEVICE=cpu to run local models on the CPU)")
+        self._queues: Dict[int, "queue.Queue"] = {}
+        self._qlock = threading.Lock()
+        self._ids = itertools.count(1)
+        self.closed = False
+
+        demands = []
+        self._ctx = {}
+        for s in specs:
+            c = s.config
+            ctx_len = (max_context or {}).get(s.name) or min(c.max_position,
+                                                             JUDGE_CONTEXT if s.name == judge else RESPONDER_CONTEXT)
+            self._ctx[s.name] = ctx_len
+            tp = 1 if force_cpu else min(c.default_tp, len(gpu_ids))
+            demands.append(ModelDemand(s.name, c.weight_bytes(), c.kv_bytes_per_token() * ctx_len, tp, s.name == judge))
+        self.placement = solve(demands, gpu_ids) if not force_cpu else None
+        if force_cpu:
+            from ..parallel.placement import Placement
+
+            self.placement = Placement({s.name: [-1] for s in specs})
+        trace_on = trace
+        used = self.placement.used_gpus()
+        groups = [(m, sorted(g)) for m, g in self.placement.gpus.items() if len(g) > 1]
+        dist_info = None
+        rank_of = {g: i for i, g in enumerate(used)}
+        port = _free_port() if groups else 0
+        ctxm = mp.get_context("spawn")
+        self.workers: Dict[int, _Worker] = {}
+        from ..runtime.worker import worker_main
+
+        for g in used:
+            models = []
+            for m, gs in self.placement.gpus.items():
+                if g in gs:
+                    s = self.specs[m]
+                    n = (counts or {}).get(m, 1)
+                    models.append({"name": m, "family": s.family, "seed": s.seed, "max_context": self._ctx[m],
+                                   "max_batch": max(1, min(4, n)),
+                                   "max_seqs": max(1, n) + (1 if m == judge else 0)})
+            if groups:
+                dist_info = {"port": port, "rank": rank_of[g], "world": len(used),
+                             "groups": [(m, [rank_of[x] for x in gs]) for m, gs in groups]}
+            a, b = ctxm.Pipe(duplex=True)
+            p = ctxm.Process(target=worker_main, args=(g, b, models, dist_info, trace_on), daemon=True,
+                             name=f"llmc-worker-gpu{g}")
+            p.start()
+            b.close()
+            self.workers[g] = _Worker(self, g, a, p)
+        deadline = time.monotonic() + start_timeout
+        for w in self.workers.values():
+            if not w.ready.wait(max(0.0, deadline - time.monotonic())):
+                self.close()
+                raise LocalError(f"worker gpu{w.gpu} did not start in {start_timeout:.0f}s")
+            if w.fatal:
+                msg = w.fatal
+                self.close()
+                raise LocalError(msg.splitlines()[0])
+        tracing.instant("placement", plan=describe(self.placement))
+
+    # -- routing ----------------------------------------------------------------------------------
+    def _workers_for(self, model: str) -> List[_Worker]:
+        return [self.workers[g] for g in self.placement.gpus[model]]
+
+    def _new_request(self) -> (int, "queue.Queue"):
+        rid = next(self._ids)
+        q: "queue.Queue" = queue.Queue()
+        with self._qlock:
+            self._queues[rid] = q
+        return rid, q
+
+    def _end_request(self, rid: int) -> None:
+        with self._qlock:
+            self._queues.pop(rid, None)
+
+    def _deliver(self, msg) -> None:
+        with self._qlock:
+            q = self._queues.get(msg[1])
+        if q is not None:
+            q.put(msg)
+
+    def _worker_died(self, w: _Worker) -> None:
+        with self._qlock:
+            qs = list(self._queues.items())
+        for rid, q in qs:
+            q.put(("error", rid, w.fatal or "worker died"))
+
+    def broadcast(self, model: str, msg) -> None:
+        for w in self._workers_for(model):
+            if w.fatal:
+                raise LocalError(w.fatal.splitlines()[0])
+            w.send(msg)
+
+    def provider(self, name: str) -> "LocalProvider":
+        return LocalProvider(self, name)
+
+    def collect_traces(self) -> None:
+        for w in self.workers.values():
+            try:
+                w.send(("trace",))
+            except Exception:  # noqa: BLE001
+                pass
+        time.sleep(0.2)
+
+    def close(self) -> None:
+        if self.closed:
+            return
+        self.closed = True
+        for w in self.workers.values():
+            try:
+                w.send(("shutdown",))
+            except Exception:  # noqa: BLE001
+                pass
+        for w in self.workers.values():
+            w.proc.join(timeout=60)
+            if w.proc.is_alive():
+                w.proc.terminate()
+                w.proc.join(timeout=10)
+
+
+class LocalProvider:
+    """Provider facade for one local model (``query_stream`` contract of provider.go:13-21)."""
+
+    provider_name = PROVIDER_LOCAL
+
+    def __init__(self, backend: LocalBackend, model: str):
+        self.backend = backend
+        self.model = model
+        self.spec = backend.specs[model]
+        self.tok = get_tokenizer(self.spec.config.vocab)
+        self._sess_lock = threading.Lock()
+        self._session: Optional[dict] = None
+
+    # -- helpers ------------------------------------------------------------------------------------
+    def _params(self, req: Request, prompt_len: int) -> dict:
+        ctx_cap = self.backend._ctx[self.model] - prompt_len - 16
+        if ctx_cap < 1:
+            raise LocalError(f"prompt of {prompt_len} tokens exceeds {self.model} context {self.backend._ctx[self.model]}")
+        mt = min(req.max_tokens or DEFAULT_MAX_TOKENS, ctx_cap)
+        seed = req.seed if req.seed is not None else (zlib.crc32(self.model.encode()) & 0x7FFFFFFF)
+        return {"max_tokens": int(mt), "temperature": 1.0 if req.temperature is None else float(req.temperature),
+                "top_p": 1.0 if req.top_p is None else float(req.top_p), "top_k": int(req.top_k or 0),
+                "seed": int(seed), "stop_on_eos": True}
+
+    def _stream(self, ctx: Context, rid: int, q: "queue.Queue", callback: Optional[StreamCallback], t0: int,
+                prompt_tokens: int) -> Response:
+        dec = self.tok.stream_decoder()
+        parts: List[str] = []
+        ntok = 0
+        ttft = 0
+        try:
+            while True:
+                try:
+                    msg = q.get(timeout=0.05)
+                except queue.Empty:
+                    if ctx.done():
+                        self.backend.broadcast(self.model, ("cancel", rid))
+                        raise ContextError(ctx.err())
+                    continue
+                kind = msg[0]
+                if kind == "tokens":
+                    if not ttft:
+                        ttft = time.monotonic_ns() - t0
+                    ntok += len(msg[2])
+                    chunk = dec.push(msg[2])
+                    if chunk:
+                        parts.append(chunk)
+                        if callback is not None:
+                            callback(chunk)
+                elif kind == "done":
+                    break
+                elif kind == "error":
+                    raise LocalError(msg[2])
+            tail = dec.flush()
+            if tail:
+                parts.append(tail)
+                if callback is not None:
+                    callback(tail)
+        finally:
+            self.backend._end_request(rid)
+        return Response(model=self.model, content="".join(parts), provider=self.provider_name,
+                        latency_ns=time.monotonic_ns() - t0, prompt_tokens=prompt_tokens, output_tokens=ntok,
+                        ttft_ns=ttft)
+
+    # -- Provider API -------------------------------------------------------------------------------
+    def query(self, ctx: Context, req: Request) -> Response:
+        return self.query_stream(ctx, req, None)
+
+    def query_stream(self, ctx: Context, req: Request, callback: Optional[StreamCallback]) -> Response:
+        t0 = time.monotonic_ns()
+        ids = self.tok.encode(req.prompt, add_bos=True)
+        params = self._params(req, len(ids))
+        rid, q = self.backend._new_request()
+        with tracing.span("query", cat="driver", model=self.model, prompt_tokens=len(ids)):
+            self.backend.broadcast(self.model, ("generate", rid, self.model, ids, params))
+            return self._stream(ctx, rid, q, callback, t0, len(ids))
+
+    # -- judge sessions (incremental prefill) ---------------------------------------------------------
+    def open_session(self, header: str) -> None:
+        with self._sess_lock:
+            self.close_session()
+            sid = next(self.backend._ids)
+            ids = self.tok.encode(header, add_bos=True)
+            self._session = {"sid": sid, "text": header, "ntok": len(ids)}
+            self.backend.broadcast(self.model, ("sess_open", sid, self.model, ids))
+
+    def extend_session(self, text: str) -> None:
+        with self._sess_lock:
+            s = self._session
+            if s is None:
+                return
+            ids = self.tok.encode(text)
+            s["text"] += text
+            s["ntok"] += len(ids)
+            self.backend.broadcast(self.model, ("sess_extend", s["sid"], ids))
+
+    def close_session(self) -> None:
+        s = self._session
+        self._session = None
+        if s is not None:
+            try:
+                self.backend.broadcast(self.model, ("sess_close", s["sid"]))
+            except Exception:  # noqa: BLE001
+                pass
+
+    def query_stream_session(self, ctx: Context, req: Request, callback: Optional[StreamCallback]) -> Response:
+        """Finish the session whose prefilled text is a prefix of ``req.prompt``."""
+        with self._sess_lock:
+            s = self._session
+            self._session = None
+        if s is None or not req.prompt.startswith(s["text"]):
+            if s is not None:
+                self.backend.broadcast(self.model, ("sess_close", s["sid"]))
+            return self.query_stream(ctx, req, callback)
+        t0 = time.monotonic_ns()
+        rest = self.tok.encode(req.prompt[len(s["text"]):])
+        total = s["ntok"] + len(rest)
+        params = self._params(req, total)
+        rid, q = self.backend._new_request()
+        with tracing.span("judge_session_finish", cat="driver", model=self.model, rest_tokens=len(rest)):
+            self.backend.broadcast(self.model, ("sess_generate", s["sid"], rid, rest, params))
+            return self._stream(ctx, rid, q, callback, t0, total)
+
+    def close(self) -> None:
+        self.close_session()
+        self.backend.close()

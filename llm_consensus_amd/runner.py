@@ -32,6 +32,9 @@ class Callbacks:
     on_model_stream: Optional[Callable[[str, str], None]] = None
     on_model_complete: Optional[Callable[[str], None]] = None
     on_model_error: Optional[Callable[[str, BaseException], None]] = None
+    # Extension (no reference counterpart): the Response itself, called under the result lock
+    # right after it is appended, i.e. in final slice order — drives incremental judge prefill.
+    on_model_response: Optional[Callable[[Response], None]] = None
 
 
 @dataclasses.dataclass
@@ -105,6 +108,8 @@ class Runner:
                         cb.on_model_error(model, err)
                     return
                 responses.append(resp)
+                if cb and cb.on_model_response:
+                    cb.on_model_response(resp)
                 if cb and cb.on_model_complete:
                     cb.on_model_complete(model)
 

@@ -1,0 +1,259 @@
+"""GPU worker process: one per GPU, hosting every engine placed on that GPU (T3).
+
+Control plane (C6): a duplex pipe to the driver carrying commands and token-id streams.
+  driver -> worker  ("generate", rid, model, prompt_ids, params)
+                    ("sess_open", sid, model, ids) / ("sess_extend", sid, ids)
+                    ("sess_generate", sid, rid, ids, params) / ("sess_close", sid)
+                    ("cancel", rid) / ("shutdown",)
+  worker -> driver  ("ready", info) / ("fatal", msg)
+                    ("tokens", rid, ids) / ("done", rid, stats) / ("error", rid, msg)
+Each engine has its own thread, hipStream and FIFO work queue, so engines co-located on a GPU
+(responders + judge, config 3) run concurrently, and requests for the same engine are BATCHED
+into one decode (replica batching: up to ``max_batch`` rows share every weight read).
+TP engines: every rank of the group runs the same command sequence (the driver sends each
+command to all ranks in the same order); only TP rank 0 streams tokens back.
+"""
+
+from __future__ import annotations
+
+import os
+import queue
+import threading
+import time
+import traceback
+from typing import Dict, List, Optional
+
+
+class _Req:
+    __slots__ = ("rid", "ids", "params", "ctx")
+
+    def __init__(self, rid, ids, params, ctx):
+        self.rid, self.ids, self.params, self.ctx = rid, ids, params, ctx
+
+
+class _EngineHost:
+    def __init__(self, name: str, engine, send, leader: bool):
+        self.name = name
+        self.engine = engine
+        self.send = send
+        self.leader = leader
+        self.q: "queue.Queue" = queue.Queue()
+        self.sessions: Dict[int, object] = {}
+        self.t = threading.Thread(target=self._loop, daemon=True, name=f"engine:{name}")
+        self.t.start()
+
+    def _emit(self, *msg) -> None:
+        if self.leader:
+            self.send(msg)
+
+    def _loop(self) -> None:
+        from ..engine import SamplingParams
+
+        while True:
+            item = self.q.get()
+            if item is None:
+                return
+            kind = item[0]
+            try:
+                if kind == "gen":
+                    batch = [item[1]]
+                    # replica batching: drain queued generate requests for this engine
+                    while len(batch) < self.engine.ecfg.max_batch:
+                        try:
+                            nxt = self.q.get_nowait()
+                        except queue.Empty:
+                            break
+                        if nxt is None or nxt[0] != "gen":
+                            self.q.put(nxt)  # keep ordering for non-generate work
+                            break
+                        batch.append(nxt[1])
+                    self._generate(batch, SamplingParams)
+                elif kind == "sess_open":
+                    _, sid, ids = item
+                    seq = self.engine.new_sequence()
+                    self.sessions[sid] = seq
+                    if ids:
+                        self.engine.prefill([seq], [ids], want_logits=False)
+                elif kind == "sess_extend":
+                    _, sid, ids = item
+                    seq = self.sessions.get(sid)
+                    if seq is not None and ids:
+                        self.engine.prefill([seq], [ids], want_logits=False)
+                elif kind == "sess_generate":
+                    _, sid, req = item
+                    seq = self.sessions.pop(sid, None)
+                    if seq is None:
+                        raise RuntimeError(f"unknown judge session {sid}")
+                    try:
+                        self._run([seq], [req], [req.ids], SamplingParams)
+                    finally:
+                        self.engine.free_sequence(seq)
+                elif kind == "sess_close":
+                    seq = self.sessions.pop(item[1], None)
+                    if seq is not None:
+                        self.engine.free_sequence(seq)
+            except Exception as e:  # noqa: BLE001 - engine-level failure = that request's error
+                rids = []
+                if kind == "gen":
+                    rids = [r.rid for r in batch]
+                elif kind == "sess_generate":
+                    rids = [item[2].rid]
+                msg = f"{type(e).__name__}: {e}"
+                if os.environ.get("LLMC_DEBUG"):
+                    msg += "\n" + traceback.format_exc()
+                for rid in rids:
+                    self._emit("error", rid, msg)
+
+    def _generate(self, batch: List[_Req], SP) -> None:
+        seqs = [self.engine.new_sequence() for _ in batch]
+        try:
+            self._run(seqs, batch, [r.ids for r in batch], SP)
+        finally:
+            for s in seqs:
+                self.engine.free_sequence(s)
+
+    def _run(self, seqs, reqs: List[_Req], prompts, SP) -> None:
+        from ..context import Context
+
+        t0 = time.monotonic_ns()
+        self.engine.prefill(seqs, prompts)
+        params = [SP(**r.params) for r in reqs]
+        first = [0] * len(reqs)
+
+        def on_tokens(i, ids):
+            if not first[i]:
+                first[i] = time.monotonic_ns() - t0
+            self._emit("tokens", reqs[i].rid, ids)
+
+        # a batch is cancelled only if every member is; single requests use their own context
+        ctx = reqs[0].ctx if len(reqs) == 1 else _AllCtx([r.ctx for r in reqs])
+        del Context
+        outs = self.engine.decode(seqs, params, ctx, on_tokens)
+        t1 = time.monotonic_ns()
+        for i, r in enumerate(reqs):
+            self._emit("done", r.rid, {"prompt_tokens": len(prompts[i]), "output_tokens": len(outs[i]),
+                                       "ttft_ns": first[i], "latency_ns": t1 - t0})
+
+
+class _AllCtx:
+    """Context view over a batch: done only when every member is cancelled."""
+
+    def __init__(self, ctxs):
+        self.ctxs = ctxs
+
+    def done(self) -> bool:
+        return all(c.done() for c in self.ctxs)
+
+    def err(self):
+        return self.ctxs[0].err()
+
+    def check(self) -> None:
+        if self.done():
+            from ..context import ContextError
+
+            raise ContextError(self.err())
+
+
+def worker_main(gpu: int, conn, models: List[dict], dist_info: Optional[dict], trace_on: bool) -> None:
+    """Entry point of a worker process (multiprocessing spawn target)."""
+    send_lock = threading.Lock()
+
+    def send(msg) -> None:
+        with send_lock:
+            conn.send(msg)
+
+    try:
+        import torch
+
+        from ..context import Context
+        from ..engine import Engine, EngineConfig
+        from ..models.config import FAMILIES
+        from ..parallel.comm import TPGroup
+        from ..utils import trace
+
+        trace.enable(trace_on)
+        on_cpu = gpu < 0  # CPU worker (tests / no-GPU hosts): oracle op path, gloo collectives
+        if not on_cpu:
+            torch.cuda.set_device(gpu)
+        groups = {}
+        if dist_info:
+            import torch.distributed as dist
+
+            kw = {} if on_cpu else {"device_id": torch.device("cuda", gpu)}
+            dist.init_process_group("gloo" if on_cpu else "nccl", init_method=f"tcp://127.0.0.1:{dist_info['port']}",
+                                    rank=dist_info["rank"], world_size=dist_info["world"], **kw)
+            for gname, ranks in dist_info["groups"]:  # every worker creates every group, same order
+                g = dist.new_group(ranks)
+                if dist_info["rank"] in ranks:
+                    groups[gname] = (g, ranks.index(dist_info["rank"]), len(ranks))
+        hosts: Dict[str, _EngineHost] = {}
+        for m in models:
+            cfg = FAMILIES[m["family"]]
+            if m["name"] in groups:
+                g, r, n = groups[m["name"]]
+                tp = TPGroup(g, r, n)
+            else:
+                tp = TPGroup.single()
+            ecfg = EngineConfig(device="cpu" if on_cpu else f"cuda:{gpu}", max_context=m["max_context"],
+                                max_batch=m.get("max_batch", 1), max_seqs=m.get("max_seqs", 0), seed=m["seed"],
+                                use_graphs=tp.size == 1 or os.environ.get("LLMC_TP_GRAPHS") == "1")
+            eng = Engine(cfg, ecfg, tp=tp, name=m["name"])
+            hosts[m["name"]] = _EngineHost(m["name"], eng, send, tp.is_leader)
+        if not on_cpu:
+            torch.cuda.synchronize()
+        send(("ready", {"gpu": gpu, "models": list(hosts)}))
+    except Exception as e:  # noqa: BLE001
+        send(("fatal", f"worker gpu{gpu} init failed: {type(e).__name__}: {e}\n{traceback.format_exc()}"))
+        return
+
+    ctxs: Dict[int, Context] = {}
+    sess_host: Dict[int, _EngineHost] = {}
+    while True:
+        try:
+            msg = conn.recv()
+        except EOFError:
+            break
+        kind = msg[0]
+        if kind == "shutdown":
+            break
+        if kind == "generate":
+            _, rid, model, ids, params = msg
+            ctx = Context.background()
+            ctxs[rid] = ctx
+            hosts[model].q.put(("gen", _Req(rid, ids, params, ctx)))
+        elif kind == "cancel":
+            c = ctxs.get(msg[1])
+            if c is not None:
+                c.cancel()
+        elif kind == "sess_open":
+            _, sid, model, ids = msg
+            sess_host[sid] = hosts[model]
+            hosts[model].q.put(("sess_open", sid, ids))
+        elif kind == "sess_extend":
+            _, sid, ids = msg
+            if sid in sess_host:
+                sess_host[sid].q.put(("sess_extend", sid, ids))
+        elif kind == "sess_generate":
+            _, sid, rid, ids, params = msg
+            ctx = Context.background()
+            ctxs[rid] = ctx
+            sess_host.pop(sid).q.put(("sess_generate", sid, _Req(rid, ids, params, ctx)))
+        elif kind == "sess_close":
+            h = sess_host.pop(msg[1], None)
+            if h is not None:
+                h.q.put(("sess_close", msg[1]))
+        elif kind == "trace":
+            from ..utils import trace
+
+            send(("trace", trace.drain()))
+    for h in hosts.values():
+        h.q.put(None)
+    for h in hosts.values():
+        h.t.join(timeout=30)
+    try:
+        import torch.distributed as dist
+
+        if dist.is_initialized():
+            dist.destroy_process_group()
+    except Exception:  # noqa: BLE001
+        pass

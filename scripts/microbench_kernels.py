@@ -1,0 +1,88 @@
+"""Micro-benchmarks of individual decode kernels (device time via HIP events over many launches).
+
+Usage: python scripts/microbench_kernels.py [attn|gemv|all]
+"""
+import math
+import os
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import torch
+
+from llm_consensus_amd import ops
+
+BF = torch.bfloat16
+
+
+def timeit(fn, iters=50, warm=5):
+    """Device time per call: `iters` calls captured in one HIP graph, replayed 10x (no host
+    launch overhead; includes the inter-kernel boundary as in the real decode graph)."""
+    s = torch.cuda.Stream()
+    with torch.cuda.stream(s):
+        for _ in range(warm):
+            fn()
+    torch.cuda.synchronize()
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g, stream=s):
+        for _ in range(iters):
+            fn()
+    g.replay()
+    torch.cuda.synchronize()
+    a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    a.record()
+    for _ in range(10):
+        g.replay()
+    b.record()
+    torch.cuda.synchronize()
+    return a.elapsed_time(b) * 1000 / (10 * iters)  # us
+
+
+def bench_attn():
+    nh, nkv, D, bs = 32, 8, 128, 64
+    for L in [128, 600, 2048, 4096, 16384]:
+        nb = (L + bs - 1) // bs + 2
+        kc = torch.randn(nb, nkv, bs, D, device="cuda").to(BF)
+        vc = torch.randn_like(kc)
+        bt = torch.arange(nb, dtype=torch.int32, device="cuda").view(1, -1)
+        sl = torch.tensor([L], dtype=torch.int32, device="cuda")
+        q = torch.randn(1, nh * D, device="cuda").to(BF)
+        out = torch.empty(1, nh * D, dtype=BF, device="cuda")
+        for chunk in [32, 64, 128, 256]:
+            mc = (L + chunk - 1) // chunk
+            part, ctr = ops.decode_attn_workspace(1, nh, nkv, D, max(mc, 1), "cuda")
+            res = []
+            for mode in (0, 1):
+                us = timeit(lambda: ops.attn_decode(q, kc, vc, bt, sl, out, part, ctr, nh, nkv, D, bs, chunk,
+                                                    1 / math.sqrt(D), mode=mode))
+                res.append(us)
+            gb = L * nkv * D * 2 * 2 / 1e9
+            print(f"attn L={L:6d} chunk={chunk:5d} chunks={mc:4d}: reduce-kernel {res[0]:7.2f} us  ticket {res[1]:7.2f} us"
+                  f"  ({gb / min(res) * 1e6 / 1e3:5.2f} TB/s)")
+
+
+def bench_gemv():
+    for (N, K, epi, norm) in [(6144, 4096, 0, True), (4096, 4096, 2, False), (28672, 4096, 3, True),
+                              (4096, 14336, 2, False), (128256, 4096, 1, True)]:
+        x = torch.randn(1, K, device="cuda").to(BF)
+        W = (torch.randn(N, K, device="cuda") * 0.02).to(BF)
+        nw = torch.ones(K, dtype=BF, device="cuda")
+        out = torch.zeros(1, N // 2 if epi == 3 else N, dtype=torch.float32 if epi == 1 else BF, device="cuda")
+        us = timeit(lambda: ops.gemv(x, W, epi, out=out, norm_w=nw if norm else None))
+        print(f"gemv N={N:6d} K={K:5d} epi={epi}: {us:8.2f} us  {N * K * 2 / us / 1e6:6.2f} TB/s")
+
+
+def bench_launch():
+    x = torch.zeros(1, 4096, dtype=BF, device="cuda")
+    w = torch.ones(4096, dtype=BF, device="cuda")
+    us = timeit(lambda: ops.rmsnorm(x, w, 1e-5, out=x))
+    print(f"rmsnorm [1,4096] (launch-bound floor): {us:.2f} us")
+
+
+if __name__ == "__main__":
+    what = sys.argv[1] if len(sys.argv) > 1 else "all"
+    if what in ("launch", "all"):
+        bench_launch()
+    if what in ("attn", "all"):
+        bench_attn()
+    if what in ("gemv", "all"):
+        bench_gemv()

@@ -1,0 +1,54 @@
+"""End-to-end CLI with LOCAL models: worker processes, placement, incremental judge session,
+replica batching. CPU variant uses CPU workers (LLMC_DEVICE=cpu, oracle op path); the GPU
+variant runs the real HIP path on the box's MI355X (SURVEY.md §7.3 minimum slice)."""
+
+import json
+import os
+import subprocess
+import sys
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def run_cli(args, env=None, timeout=600):
+    e = dict(os.environ)
+    e.update(env or {})
+    r = subprocess.run([sys.executable, "-m", "llm_consensus_amd", *args], capture_output=True, cwd=ROOT, env=e,
+                       timeout=timeout, stdin=subprocess.DEVNULL)
+    return r.returncode, r.stdout.decode("utf-8", "replace"), r.stderr.decode("utf-8", "replace")
+
+
+def test_cli_local_models_cpu_workers(tmp_path):
+    rc, out, err = run_cli(["--models", "llama-tiny@1,llama-tiny@2,mixtral-tiny,phi3-tiny", "--judge", "llama-tiny@j",
+                            "--max-tokens", "10", "--data-dir", str(tmp_path), "--trace", "Explain RoPE."],
+                           env={"LLMC_DEVICE": "cpu"})
+    assert rc == 0, err
+    run = tmp_path / os.listdir(tmp_path)[0]
+    res = json.loads((run / "result.json").read_text())
+    assert sorted(r["model"] for r in res["responses"]) == ["llama-tiny@1", "llama-tiny@2", "mixtral-tiny", "phi3-tiny"]
+    assert all(r["provider"] == "rocm" and len(r["content"]) > 0 for r in res["responses"])
+    assert res["judge"] == "llama-tiny@j" and len(res["consensus"]) > 0
+    tr = json.loads((run / "trace.json").read_text())
+    names = {e["name"] for e in tr["traceEvents"]}
+    assert {"prefill", "decode", "query"} <= names
+
+
+def test_cli_duplicate_local_model_batched_cpu():
+    rc, out, err = run_cli(["--models", "llama-tiny,llama-tiny", "--judge", "llama-tiny", "--max-tokens", "6",
+                            "--temperature", "0", "--json", "hi"], env={"LLMC_DEVICE": "cpu"})
+    assert rc == 0, err
+    d = json.loads(out)
+    # same model, same prompt, greedy: identical responses (served as two rows of one batch)
+    assert d["responses"][0]["content"] == d["responses"][1]["content"]
+
+
+@pytest.mark.gpu
+def test_cli_local_models_gpu(cuda, tmp_path):
+    rc, out, err = run_cli(["--models", "llama-small@1,llama-small@2,mixtral-tiny,phi3-tiny", "--judge",
+                            "llama-small@j", "--max-tokens", "64", "--json", "What is 2+2?"])
+    assert rc == 0, err
+    d = json.loads(out)
+    assert len(d["responses"]) == 4 and all(len(r["content"]) > 0 for r in d["responses"])
+    assert len(d["consensus"]) > 0

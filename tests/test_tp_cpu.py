@@ -35,7 +35,7 @@ def _worker(rank, world, port, name, q):
         p = [(i * 13) % 700 + 256 for i in range(24)]
         s = e.new_sequence()
         e.prefill([s], [p])
-        logits = e._gather_logits(1).clone()
+        logits = e.full_logits(s).clone().unsqueeze(0)
         e.free_sequence(s)
         gen = e.generate_ids(p, 6, temperature=0.0, stop_on_eos=False)
         if rank == 0:
@@ -54,7 +54,7 @@ def test_tp2_matches_tp1(name):
     p = [(i * 13) % 700 + 256 for i in range(24)]
     s = ref.new_sequence()
     ref.prefill([s], [p])
-    ref_logits = ref.logits[0].clone()
+    ref_logits = ref.full_logits(s).clone()
     ref.free_sequence(s)
     ref_gen = ref.generate_ids(p, 6, temperature=0.0, stop_on_eos=False)
 

@@ -404,15 +404,43 @@ class Engine:
             b *= 2
         return min(b, self.max_chunks)
 
+    def buckets(self) -> List[int]:
+        out, b = [], 8
+        while True:
+            out.append(min(b, self.max_chunks))
+            if b >= self.max_chunks:
+                return out
+            b *= 2
+
+    @torch.no_grad()
+    def warmup_graphs(self, batch_sizes: Optional[List[int]] = None, topkp: bool = False) -> int:
+        """Capture every decode graph this engine can need (per batch size x context bucket) up
+        front. A process hosting several engines must do this before serving: a capture running
+        beside another engine's work is invalidated by HIP, so serving never captures
+        (``capture_on_demand`` False -> a missing graph runs eagerly)."""
+        if not (self.on_gpu and self.ecfg.use_graphs):
+            return 0
+        n = 0
+        with self._on_stream():
+            for B in batch_sizes or list(range(1, self.ecfg.max_batch + 1)):
+                for bk in self.buckets():
+                    self._use_topkp = topkp
+                    self._graph(B, bk)
+                    n += 1
+        self._use_topkp = False
+        self.capture_on_demand = False
+        return n
+
+    capture_on_demand = True
+
     def _graph(self, B: int, bucket: int):
         key = (B, self._use_topkp, bucket)
         g = self._graphs.get(key)
-        if g is not None:
+        if g is not None or not self.capture_on_demand:
             return g
         S = self.ecfg.steps_per_graph
         # warm up once eagerly (kernel attributes, lazy module state) with the device state
-        # snapshotted and restored, then capture S steps. thread_local capture mode: other
-        # engines' threads may allocate / synchronise while this one captures.
+        # snapshotted and restored, then capture S steps.
         snap = self._snapshot_state()
         self._decode_step(B, bucket)
         self._restore_state(snap)
@@ -519,8 +547,9 @@ class Engine:
                 if need_more:
                     # context reached by the end of this replay decides the attention bucket
                     bucket = self._bucket(base_len + issued + S + 1)
-                    if self.ecfg.use_graphs:
-                        self._graph(B, bucket).replay()
+                    graph = self._graph(B, bucket) if self.ecfg.use_graphs else None
+                    if graph is not None:
+                        graph.replay()
                     else:
                         for _ in range(S):
                             self._decode_step(B, bucket)

@@ -200,6 +200,10 @@ def worker_main(gpu: int, conn, models: List[dict], dist_info: Optional[dict], t
             eng = Engine(cfg, ecfg, tp=tp, name=m["name"])
             hosts[m["name"]] = _EngineHost(m["name"], eng, send, tp.is_leader)
         if not on_cpu:
+            # capture all decode graphs now, while nothing else runs in this process
+            for h in hosts.values():
+                with trace.span("graph_warmup", engine=h.name):
+                    h.engine.warmup_graphs()
             torch.cuda.synchronize()
         send(("ready", {"gpu": gpu, "models": list(hosts)}))
     except Exception as e:  # noqa: BLE001

@@ -244,21 +244,73 @@ __global__ __launch_bounds__(256) void attn_decode_kernel(
   }
 }
 
-// grid (nkv, B), 256 threads: merge the chunk partials of one kv head's G query heads.
+// grid (nkv * G, B, ceil(D / 64)), 256 threads: one query head x 64 dims per block; the 256
+// threads are 64 dims x 4 chunk groups, so each thread reads only nchunks/4 partials (one batch
+// of in-flight loads for ~64 chunks) and the chunk groups meet in LDS. Parallel over heads and
+// dim slices so a 33k-token context (hundreds of chunks) reduces in ~two memory round trips.
 template <int G>
 __global__ __launch_bounds__(256) void attn_decode_reduce_kernel(const float* __restrict__ part,
                                                                  const int32_t* __restrict__ seq_lens,
                                                                  bf16_t* __restrict__ out, int out_stride, int nkv,
                                                                  int D, int chunk, int max_chunks) {
-  const int kvh = blockIdx.x, b = blockIdx.y;
+  const int kvh = blockIdx.x / G, g = blockIdx.x % G, b = blockIdx.y;
   const int L = seq_lens[b];
   const int nchunks = (L + chunk - 1) / chunk;
   if (nchunks <= 1) return;
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  const float* pb = part + ((static_cast<int64_t>(b) * nkv + kvh) * max_chunks) * G * (D + 2);
-  reduce_chunks<G, false>(pb, nchunks, D, reinterpret_cast<float*>(smem),
-                          out + static_cast<int64_t>(b) * out_stride + kvh * G * D);
+  float* sc = reinterpret_cast<float*>(smem);  // [nchunks]
+  float* red = sc + max_chunks;                // [4][64] + 8 scratch
+  const int tid = threadIdx.x, stride = D + 2;
+  const float* pb = part + ((static_cast<int64_t>(b) * nkv + kvh) * max_chunks * G + g) * stride;
+  const int64_t cstride = static_cast<int64_t>(G) * stride;  // between consecutive chunks
+  // phase 1: m_c into LDS, block max
+  float mx = kNegBig;
+  for (int c = tid; c < nchunks; c += 256) {
+    const float m = pb[c * cstride + D];
+    sc[c] = m;
+    mx = fmaxf(mx, m);
+  }
+  mx = wave_max(mx);
+  if ((tid & 63) == 0) red[256 + tid / 64] = mx;
+  __syncthreads();
+  mx = fmaxf(fmaxf(red[256], red[257]), fmaxf(red[258], red[259]));
+  // phase 2: scale factors and the normaliser
+  float ls = 0.f;
+  for (int c = tid; c < nchunks; c += 256) {
+    const float e = __expf(sc[c] - mx);
+    sc[c] = e;
+    ls += pb[c * cstride + D + 1] * e;
+  }
+  ls = wave_sum(ls);
+  __syncthreads();
+  if ((tid & 63) == 0) red[260 + tid / 64] = ls;
+  __syncthreads();
+  const float lsum = red[260] + red[261] + red[262] + red[263];
+  // phase 3: weighted sum of the chunk outputs, 4 chunk groups in parallel
+  const int dl = tid & 63, cg = tid >> 6;
+  const int d = blockIdx.z * 64 + dl;
+  float o = 0.f;
+  if (d < D) {
+    for (int c0 = cg; c0 < nchunks; c0 += 4 * 16) {
+      float v[16];
+#pragma unroll
+      for (int j = 0; j < 16; ++j) {
+        const int c = min(c0 + 4 * j, nchunks - 1);  // clamped: all 16 loads in flight
+        v[j] = pb[c * cstride + d];
+      }
+#pragma unroll
+      for (int j = 0; j < 16; ++j) o += (c0 + 4 * j < nchunks) ? v[j] * sc[c0 + 4 * j] : 0.f;
+    }
+  }
+  red[cg * 64 + dl] = o;
+  __syncthreads();
+  if (cg == 0 && d < D) {
+    const float tot = red[dl] + red[64 + dl] + red[128 + dl] + red[192 + dl];
+    out[static_cast<int64_t>(b) * out_stride + (kvh * G + g) * D + d] = f32_to_bf16(tot / lsum);
+  }
 }
+
+static size_t reduce_lds(int max_chunks) { return (static_cast<size_t>(max_chunks) + 256 + 8) * sizeof(float); }
 
 template <int G>
 static int launch_decode(int B, int nkv, int grid_chunks, hipStream_t s, const void* q, int q_stride, const void* kc,
@@ -289,15 +341,8 @@ static int launch_decode(int B, int nkv, int grid_chunks, hipStream_t s, const v
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return static_cast<int>(e);
   if (grid_chunks > 1) {
-    auto rk = attn_decode_reduce_kernel<G>;
-    static bool attr = false;
-    if (scl_lds > 64 * 1024 && !attr) {
-      (void)hipFuncSetAttribute(reinterpret_cast<const void*>(rk), hipFuncAttributeMaxDynamicSharedMemorySize,
-                                160 * 1024);
-      attr = true;
-    }
-    rk<<<dim3(nkv, B), 256, scl_lds, s>>>((const float*)part, (const int32_t*)sl, (bf16_t*)out, out_stride, nkv, D,
-                                           chunk, max_chunks);
+    attn_decode_reduce_kernel<G><<<dim3(nkv * G, B, (D + 63) / 64), 256, reduce_lds(max_chunks), s>>>(
+        (const float*)part, (const int32_t*)sl, (bf16_t*)out, out_stride, nkv, D, chunk, max_chunks);
   }
   return static_cast<int>(hipGetLastError());
 }
@@ -309,11 +354,36 @@ using namespace llmc;
 // part: f32 workspace [B, nkv, max_chunks, G, D + 2]; counters: int32 [B, nkv], zero-initialised
 // once (the TICKET form re-arms them every launch). grid_chunks <= max_chunks bounds the context
 // of this launch. mode: 0 = partial + reduce kernel, 1 = in-launch ticket reduce.
+extern "C" int llmc_attn_decode_mfma_partials(const void*, int, const void*, const void*, const void*, int, const void*,
+                                              void*, void*, int, int, int, int, int, int, int, int, int, float,
+                                              hipStream_t);
+
+template <int G>
+static int launch_reduce_only(int B, int nkv, int D, int chunk, int max_chunks, hipStream_t s, const void* part,
+                              const void* sl, void* out, int out_stride) {
+  attn_decode_reduce_kernel<G><<<dim3(nkv * G, B, (D + 63) / 64), 256, reduce_lds(max_chunks), s>>>(
+      (const float*)part, (const int32_t*)sl, (bf16_t*)out, out_stride, nkv, D, chunk, max_chunks);
+  return static_cast<int>(hipGetLastError());
+}
+
 extern "C" int llmc_attn_decode(const void* q, int q_stride, const void* k_cache, const void* v_cache,
                                 const void* block_tables, int bt_stride, const void* seq_lens, void* part,
                                 void* counters, void* out, int out_stride, int B, int nh, int nkv, int D, int bs,
                                 int chunk, int grid_chunks, int max_chunks, float scale, int mode, hipStream_t s) {
   if (D % 8 != 0 || D > 128 || nh % nkv != 0 || grid_chunks > max_chunks) return -1;
+  if (mode == 2) {  // MFMA partials (attn_decode_mfma.hip) + reduce kernel
+    int rc = llmc_attn_decode_mfma_partials(q, q_stride, k_cache, v_cache, block_tables, bt_stride, seq_lens, part,
+                                            out, out_stride, B, nh, nkv, D, bs, chunk, grid_chunks, max_chunks, scale,
+                                            s);
+    if (rc != 0 || grid_chunks <= 1) return rc;
+    switch (nh / nkv) {
+      case 1: return launch_reduce_only<1>(B, nkv, D, chunk, max_chunks, s, part, seq_lens, out, out_stride);
+      case 2: return launch_reduce_only<2>(B, nkv, D, chunk, max_chunks, s, part, seq_lens, out, out_stride);
+      case 4: return launch_reduce_only<4>(B, nkv, D, chunk, max_chunks, s, part, seq_lens, out, out_stride);
+      case 8: return launch_reduce_only<8>(B, nkv, D, chunk, max_chunks, s, part, seq_lens, out, out_stride);
+      default: return -2;
+    }
+  }
   const bool ticket = mode == 1;
   switch (nh / nkv) {
     case 1: return launch_decode<1>(B, nkv, grid_chunks, s, q, q_stride, k_cache, v_cache, block_tables, bt_stride, seq_lens, part, counters, out, out_stride, D, bs, chunk, max_chunks, scale, ticket);

@@ -48,9 +48,26 @@ class EngineConfig:
     steps_per_graph: int = 8
     use_graphs: bool = True
     prefill_chunk: int = 8192
-    attn_chunk: int = 0  # 0 = by max_context (64 / 128 / 256 tokens per split-KV block)
+    attn_chunk: int = 0  # 0 = per context bucket (128 / 256 / 512 tokens per split-KV block)
     init_scale: float = 1.0
     stream_priority: int = 0
+
+
+def attn_buckets(ctxmax: int, fixed_chunk: int = 0) -> List[tuple]:
+    """Decode-attention shapes per context bucket: [(capacity_tokens, chunk, grid_chunks)].
+
+    Capacities double from 1024 up to ``ctxmax``. The chunk (keys per split-KV block) grows with
+    the bucket so the grid stays ~32-256 blocks per kv head — enough work for 256 CUs without
+    many-chunk reductions (measured on MI355X, profiles/r1_attn_decode_microbench.md): 128 keys up
+    to 4k context, 256 up to 8k, 512 beyond. Multiples of 128 select the MFMA decode kernel."""
+    out, cap = [], 1024
+    while True:
+        c = min(cap, ctxmax)
+        chunk = fixed_chunk or (128 if cap <= 4096 else 256 if cap <= 8192 else 512)
+        out.append((c, chunk, (c + chunk - 1) // chunk))
+        if cap >= ctxmax:
+            return out
+        cap *= 2
 
 
 @dataclasses.dataclass
@@ -150,10 +167,10 @@ class Engine:
                        else torch.zeros(B, c.vocab, dtype=torch.float32, device=dev))
         self._gather_buf = (None if self.tp.size == 1 else
                             torch.zeros(self.tp.size, B, self.w.vocab_local, dtype=torch.float32, device=dev))
-        # split-KV decode attention: small chunks (more blocks) for short contexts
+        # split-KV decode attention: one (chunk, grid) shape per context bucket
         ctxmax = self.ecfg.max_context + self.ecfg.steps_per_graph + 2
-        self.attn_chunk = self.ecfg.attn_chunk or (64 if ctxmax <= 16384 else 128 if ctxmax <= 65536 else 256)
-        self.max_chunks = (ctxmax + self.attn_chunk - 1) // self.attn_chunk
+        self.attn_buckets = attn_buckets(ctxmax, self.ecfg.attn_chunk)
+        self.max_chunks = max(gc for _, _, gc in self.attn_buckets)
         self.attn_part, self.attn_counters = ops.decode_attn_workspace(B, self.nh, self.nkv, self.D,
                                                                         self.max_chunks, dev)
         if self.on_gpu:
@@ -324,9 +341,10 @@ class Engine:
         self.tp.all_reduce_(h)
 
     # -- decode -------------------------------------------------------------------------------------
-    def _decode_step(self, B: int, grid_chunks: Optional[int] = None) -> None:
-        """One token for rows 0..B-1. ``grid_chunks`` bounds the attention grid (context bucket)."""
+    def _decode_step(self, B: int, bucket: Optional[int] = None) -> None:
+        """One token for rows 0..B-1. ``bucket`` indexes ``attn_buckets`` (default: the largest)."""
         c = self.cfg
+        _, chunk, grid_chunks = self.attn_buckets[-1 if bucket is None else bucket]
         h, q, attn, act = self.h[:B], self.q[:B], self.attn[:B], self.act[:B]
         ops.embedding(self.tokens_in[:B], self.w.embed, out=h)
         for li, Lw in enumerate(self.w.layers):
@@ -334,7 +352,7 @@ class Engine:
                          self.slots[:B], self.cos_t, self.sin_t, self.nh, self.nkv, self.D, self.bs)
             ops.attn_decode(q, self.k_cache[li], self.v_cache[li], self.block_tables[:B], self.seq_lens[:B], attn,
                             self.attn_part[:B], self.attn_counters[:B], self.nh, self.nkv, self.D, self.bs,
-                            self.attn_chunk, self.scale, grid_chunks)
+                            chunk, self.scale, grid_chunks)
             self._row_parallel(attn, Lw.w_o, h)
             if c.is_moe:
                 self._moe_decode(h, Lw, B)
@@ -396,21 +414,15 @@ class Engine:
                    out_tokens=self.out_tokens[:B], out_count=self.out_count[:B], use_topkp=use_topkp)
 
     def _bucket(self, ctx_tokens: int) -> int:
-        """Attention grid (chunks) for contexts up to ``ctx_tokens``: next power of two >= 8,
-        so the graph for a short context does not launch thousands of empty blocks."""
-        need = (ctx_tokens + self.attn_chunk - 1) // self.attn_chunk
-        b = 8
-        while b < need:
-            b *= 2
-        return min(b, self.max_chunks)
+        """Smallest attention bucket covering ``ctx_tokens`` (so a short context's graph does not
+        launch thousands of empty blocks)."""
+        for i, (cap, _, _) in enumerate(self.attn_buckets):
+            if cap >= ctx_tokens:
+                return i
+        return len(self.attn_buckets) - 1
 
     def buckets(self) -> List[int]:
-        out, b = [], 8
-        while True:
-            out.append(min(b, self.max_chunks))
-            if b >= self.max_chunks:
-                return out
-            b *= 2
+        return list(range(len(self.attn_buckets)))
 
     @torch.no_grad()
     def warmup_graphs(self, batch_sizes: Optional[List[int]] = None, topkp: bool = False) -> int:

@@ -39,7 +39,7 @@ def timeit(fn, iters=50, warm=5):
 
 def bench_attn():
     nh, nkv, D, bs = 32, 8, 128, 64
-    for L in [128, 600, 2048, 4096, 16384]:
+    for L in [128, 600, 2048, 4096, 16384, 33000]:
         nb = (L + bs - 1) // bs + 2
         kc = torch.randn(nb, nkv, bs, D, device="cuda").to(BF)
         vc = torch.randn_like(kc)
@@ -47,16 +47,19 @@ def bench_attn():
         sl = torch.tensor([L], dtype=torch.int32, device="cuda")
         q = torch.randn(1, nh * D, device="cuda").to(BF)
         out = torch.empty(1, nh * D, dtype=BF, device="cuda")
-        for chunk in [32, 64, 128, 256]:
+        for chunk in [64, 128, 256, 512]:
             mc = (L + chunk - 1) // chunk
             part, ctr = ops.decode_attn_workspace(1, nh, nkv, D, max(mc, 1), "cuda")
             res = []
-            for mode in (0, 1):
+            for mode in (0, 2):
+                if mode == 2 and chunk % 128:
+                    res.append(float("inf"))
+                    continue
                 us = timeit(lambda: ops.attn_decode(q, kc, vc, bt, sl, out, part, ctr, nh, nkv, D, bs, chunk,
                                                     1 / math.sqrt(D), mode=mode))
                 res.append(us)
             gb = L * nkv * D * 2 * 2 / 1e9
-            print(f"attn L={L:6d} chunk={chunk:5d} chunks={mc:4d}: reduce-kernel {res[0]:7.2f} us  ticket {res[1]:7.2f} us"
+            print(f"attn L={L:6d} chunk={chunk:5d} chunks={mc:4d}: valu {res[0]:7.2f} us  mfma {res[1]:7.2f} us"
                   f"  ({gb / min(res) * 1e6 / 1e3:5.2f} TB/s)")
 
 

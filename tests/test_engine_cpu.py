@@ -98,3 +98,16 @@ def test_weights_param_counts():
     assert 3.7e9 < FAMILIES["phi-3-mini"].num_params() < 3.9e9
     w = TransformerWeights(FAMILIES["mixtral-tiny"], TPGroup.single(), torch.device("cpu"), 1)
     assert w.layers[0].w_gu.shape == (4, 2 * 384, 256) and w.layers[0].w_router.shape == (4, 256)
+
+
+def test_attn_buckets_cover_context():
+    from llm_consensus_amd.engine.engine import attn_buckets
+
+    for ctxmax in [100, 1024, 4106, 16394, 131082]:
+        bks = attn_buckets(ctxmax)
+        assert bks[-1][0] == ctxmax
+        for cap, chunk, gc in bks:
+            assert chunk % 128 == 0 and gc * chunk >= cap
+        caps = [b[0] for b in bks]
+        assert caps == sorted(caps)
+    assert {c for _, c, _ in attn_buckets(4106, 64)} == {64}

@@ -154,8 +154,8 @@ def _paged_kv(B, L_max, nkv, D, bs):
 
 @pytest.mark.parametrize("nh,nkv,D", [(32, 8, 128), (32, 32, 96), (16, 2, 128), (4, 2, 64)])
 @pytest.mark.parametrize("lens", [[1, 7], [100, 1000], [3000, 257]])
-@pytest.mark.parametrize("chunk", [64, 256])
-def test_attn_decode(cuda, nh, nkv, D, lens, chunk):
+@pytest.mark.parametrize("mode,chunk", [(0, 64), (0, 256), (1, 64), (2, 128), (2, 256), (2, 512)])
+def test_attn_decode(cuda, nh, nkv, D, lens, mode, chunk):
     torch.manual_seed(3)
     B, bs = len(lens), 64
     L_max = max(lens)
@@ -170,7 +170,7 @@ def test_attn_decode(cuda, nh, nkv, D, lens, chunk):
     # three launches: the in-kernel reduce must re-arm its tickets every time
     for _ in range(3):
         out.zero_()
-        ops.attn_decode(q, kc, vc, bt.cuda(), sl.cuda(), out, part, ctr, nh, nkv, D, bs, chunk, scale)
+        ops.attn_decode(q, kc, vc, bt.cuda(), sl.cuda(), out, part, ctr, nh, nkv, D, bs, chunk, scale, mode=mode)
         close(out, ref, 2e-2)
     assert int(ctr.abs().sum()) == 0
 

@@ -17,65 +17,9 @@
 //     reduces with sc1 loads (Guideline 16 valid form, row 1) — no second launch.
 // Grid sized per context bucket by the host (one captured decode graph per bucket); chunks past
 // seq_len exit immediately.
-#include "common.h"
+#include "attn_reduce.h"
 
 namespace llmc {
-
-constexpr float kNegBig = -1e30f;
-
-__device__ __forceinline__ void st_sc1(float* p, float v) {
-  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-__device__ __forceinline__ float ld_sc1(const float* p) {
-  return __hip_atomic_load(const_cast<float*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-
-// Merge chunk partials [nchunks][G][D + 2] into bf16 out rows of the G heads. `lds` holds
-// 2 * G * nchunks + 2 * G floats. LOADER is plain or sc1.
-template <int G, bool SC1>
-__device__ __forceinline__ void reduce_chunks(const float* __restrict__ pb, int nchunks, int D, float* lds,
-                                              bf16_t* __restrict__ out_row) {
-  const int tid = threadIdx.x;
-  const int stride = D + 2;
-  auto ld = [](const float* p) { return SC1 ? ld_sc1(p) : *p; };
-  float* scl = lds;                // [G][nchunks]: m, then exp(m - M)
-  float* lv = scl + G * nchunks;   // [G][nchunks]: l
-  float* Mg = lv + G * nchunks;    // [G]
-  float* Lg = Mg + G;              // [G]
-  for (int i = tid; i < G * nchunks; i += 256) {
-    const int g = i / nchunks, cc = i % nchunks;
-    const float* pc = pb + (static_cast<int64_t>(cc) * G + g) * stride;
-    scl[i] = ld(pc + D);
-    lv[i] = ld(pc + D + 1);
-  }
-  __syncthreads();
-  if (tid < G) {
-    float mx = kNegBig;
-    for (int cc = 0; cc < nchunks; ++cc) mx = fmaxf(mx, scl[tid * nchunks + cc]);
-    float ls = 0.f;
-    for (int cc = 0; cc < nchunks; ++cc) ls += lv[tid * nchunks + cc] * __expf(scl[tid * nchunks + cc] - mx);
-    Mg[tid] = mx;
-    Lg[tid] = ls;
-  }
-  __syncthreads();
-  for (int i = tid; i < G * nchunks; i += 256) scl[i] = __expf(scl[i] - Mg[i / nchunks]);
-  __syncthreads();
-  for (int idx = tid; idx < G * D; idx += 256) {
-    const int g = idx / D, d = idx % D;
-    float o = 0.f;
-    for (int c0 = 0; c0 < nchunks; c0 += 16) {
-      float v[16];
-#pragma unroll
-      for (int j = 0; j < 16; ++j) {
-        const int cc = min(c0 + j, nchunks - 1);  // clamped: branch-free, all 16 loads in flight
-        v[j] = ld(pb + (static_cast<int64_t>(cc) * G + g) * stride + d);
-      }
-#pragma unroll
-      for (int j = 0; j < 16; ++j) o += (c0 + j < nchunks) ? v[j] * scl[g * nchunks + c0 + j] : 0.f;
-    }
-    out_row[g * D + d] = f32_to_bf16(o / Lg[g]);
-  }
-}
 
 template <int G, bool TICKET>
 __global__ __launch_bounds__(256) void attn_decode_kernel(
@@ -252,9 +196,10 @@ template <int G>
 __global__ __launch_bounds__(256) void attn_decode_reduce_kernel(const float* __restrict__ part,
                                                                  const int32_t* __restrict__ seq_lens,
                                                                  bf16_t* __restrict__ out, int out_stride, int nkv,
-                                                                 int D, int chunk, int max_chunks) {
+                                                                 int D, int chunk_arg, int gc, int max_chunks) {
   const int kvh = blockIdx.x / G, g = blockIdx.x % G, b = blockIdx.y;
   const int L = seq_lens[b];
+  const int chunk = decode_chunk(L, gc, chunk_arg);
   const int nchunks = (L + chunk - 1) / chunk;
   if (nchunks <= 1) return;
   extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -342,7 +287,7 @@ static int launch_decode(int B, int nkv, int grid_chunks, hipStream_t s, const v
   if (e != hipSuccess) return static_cast<int>(e);
   if (grid_chunks > 1) {
     attn_decode_reduce_kernel<G><<<dim3(nkv * G, B, (D + 63) / 64), 256, reduce_lds(max_chunks), s>>>(
-        (const float*)part, (const int32_t*)sl, (bf16_t*)out, out_stride, nkv, D, chunk, max_chunks);
+        (const float*)part, (const int32_t*)sl, (bf16_t*)out, out_stride, nkv, D, chunk, grid_chunks, max_chunks);
   }
   return static_cast<int>(hipGetLastError());
 }
@@ -353,16 +298,18 @@ using namespace llmc;
 
 // part: f32 workspace [B, nkv, max_chunks, G, D + 2]; counters: int32 [B, nkv], zero-initialised
 // once (the TICKET form re-arms them every launch). grid_chunks <= max_chunks bounds the context
-// of this launch. mode: 0 = partial + reduce kernel, 1 = in-launch ticket reduce.
-extern "C" int llmc_attn_decode_mfma_partials(const void*, int, const void*, const void*, const void*, int, const void*,
-                                              void*, void*, int, int, int, int, int, int, int, int, int, float,
-                                              hipStream_t);
+// of this launch. mode: 0 = VALU partials + reduce kernel, 1 = VALU in-launch ticket reduce,
+// 2 = MFMA balanced split + reduce kernel, 3 = MFMA balanced split + in-launch ticket reduce
+// (modes 2/3: chunk = minimum keys per block, a multiple of 128).
+extern "C" int llmc_attn_decode_mfma(const void*, int, const void*, const void*, const void*, int, const void*, void*,
+                                     void*, void*, int, int, int, int, int, int, int, int, int, float, int,
+                                     hipStream_t);
 
 template <int G>
-static int launch_reduce_only(int B, int nkv, int D, int chunk, int max_chunks, hipStream_t s, const void* part,
+static int launch_reduce_only(int B, int nkv, int D, int chunk, int gc, int max_chunks, hipStream_t s, const void* part,
                               const void* sl, void* out, int out_stride) {
   attn_decode_reduce_kernel<G><<<dim3(nkv * G, B, (D + 63) / 64), 256, reduce_lds(max_chunks), s>>>(
-      (const float*)part, (const int32_t*)sl, (bf16_t*)out, out_stride, nkv, D, chunk, max_chunks);
+      (const float*)part, (const int32_t*)sl, (bf16_t*)out, out_stride, nkv, D, chunk, gc, max_chunks);
   return static_cast<int>(hipGetLastError());
 }
 
@@ -371,16 +318,16 @@ extern "C" int llmc_attn_decode(const void* q, int q_stride, const void* k_cache
                                 void* counters, void* out, int out_stride, int B, int nh, int nkv, int D, int bs,
                                 int chunk, int grid_chunks, int max_chunks, float scale, int mode, hipStream_t s) {
   if (D % 8 != 0 || D > 128 || nh % nkv != 0 || grid_chunks > max_chunks) return -1;
-  if (mode == 2) {  // MFMA partials (attn_decode_mfma.hip) + reduce kernel
-    int rc = llmc_attn_decode_mfma_partials(q, q_stride, k_cache, v_cache, block_tables, bt_stride, seq_lens, part,
-                                            out, out_stride, B, nh, nkv, D, bs, chunk, grid_chunks, max_chunks, scale,
-                                            s);
-    if (rc != 0 || grid_chunks <= 1) return rc;
+  if (mode == 2 || mode == 3) {  // MFMA (attn_decode_mfma.hip) [+ reduce kernel]
+    int rc = llmc_attn_decode_mfma(q, q_stride, k_cache, v_cache, block_tables, bt_stride, seq_lens, part, counters,
+                                   out, out_stride, B, nh, nkv, D, bs, chunk, grid_chunks, max_chunks, scale,
+                                   mode == 3, s);
+    if (rc != 0 || grid_chunks <= 1 || mode == 3) return rc;
     switch (nh / nkv) {
-      case 1: return launch_reduce_only<1>(B, nkv, D, chunk, max_chunks, s, part, seq_lens, out, out_stride);
-      case 2: return launch_reduce_only<2>(B, nkv, D, chunk, max_chunks, s, part, seq_lens, out, out_stride);
-      case 4: return launch_reduce_only<4>(B, nkv, D, chunk, max_chunks, s, part, seq_lens, out, out_stride);
-      case 8: return launch_reduce_only<8>(B, nkv, D, chunk, max_chunks, s, part, seq_lens, out, out_stride);
+      case 1: return launch_reduce_only<1>(B, nkv, D, -chunk, grid_chunks, max_chunks, s, part, seq_lens, out, out_stride);
+      case 2: return launch_reduce_only<2>(B, nkv, D, -chunk, grid_chunks, max_chunks, s, part, seq_lens, out, out_stride);
+      case 4: return launch_reduce_only<4>(B, nkv, D, -chunk, grid_chunks, max_chunks, s, part, seq_lens, out, out_stride);
+      case 8: return launch_reduce_only<8>(B, nkv, D, -chunk, grid_chunks, max_chunks, s, part, seq_lens, out, out_stride);
       default: return -2;
     }
   }

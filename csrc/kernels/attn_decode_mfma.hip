@@ -14,9 +14,12 @@
 //                             LDS image of the 32 V rows, chunk-swizzled c ^ ((row & 7) << 1) so a
 //                             half-wave's 8 rows x 32 B hit 64 distinct banks. O^T keeps the head on
 //                             the lane, so the online-softmax rescale uses lane-local alpha.
-// Grid (grid_chunks, nkv, B); a block = 4 waves = one kv head x `chunk` keys (chunk % 128 == 0);
-// the cross-chunk merge reuses attn_decode.hip's partial layout and reduce kernel.
-#include "common.h"
+// Grid (grid_chunks, nkv, B); a block = 4 waves = one kv head x one balanced chunk: the L keys of
+// the sequence are split evenly over the grid_chunks blocks (decode_chunk: multiples of 128 keys,
+// at least `min_chunk`), so a graph captured for a context bucket keeps every block equally busy
+// whatever the actual L (no 2-blocks-per-CU tail at long judge contexts). The cross-chunk merge
+// reuses attn_decode.hip's partial layout and reduce kernel.
+#include "attn_reduce.h"
 
 namespace llmc {
 
@@ -28,18 +31,19 @@ constexpr int kVRowBytes = 256;  // LDS pitch of one V row (D <= 128)
 
 __device__ __forceinline__ int vswz(int row, int chunk) { return row * kVRowBytes + ((chunk ^ ((row & 7) << 1)) << 4); }
 
-template <int G, int D>
+template <int G, int D, bool TICKET>
 __global__ __launch_bounds__(256) void attn_decode_mfma_kernel(
     const bf16_t* __restrict__ q, int q_stride, const bf16_t* __restrict__ k_cache,
     const bf16_t* __restrict__ v_cache, const int32_t* __restrict__ block_tables, int bt_stride,
-    const int32_t* __restrict__ seq_lens, float* __restrict__ part, bf16_t* __restrict__ out, int out_stride, int nkv,
-    int bs, int chunk, int max_chunks, float scale_log2) {
+    const int32_t* __restrict__ seq_lens, float* __restrict__ part, int* __restrict__ counters,
+    bf16_t* __restrict__ out, int out_stride, int nkv, int bs, int min_chunk, int max_chunks, float scale_log2) {
   static_assert(G <= 16 && D % 32 == 0 && D <= 128, "shape");
   constexpr int KS = D / 32;  // dim slabs for Q.K
   constexpr int DT = D / 16;  // 16-dim tiles of O^T
   constexpr int VCH = D / 8;  // 16-B chunks per V row
   const int c = blockIdx.x, kvh = blockIdx.y, b = blockIdx.z;
   const int L = seq_lens[b];
+  const int chunk = decode_chunk(L, gridDim.x, -min_chunk);
   const int start = c * chunk;
   if (start >= L) return;
   const int end = min(start + chunk, L);
@@ -227,39 +231,69 @@ __global__ __launch_bounds__(256) void attn_decode_mfma_kernel(
     if (nchunks == 1) {
       out_row[hh * D + d] = f32_to_bf16(o / lsum);
     } else {
-      // partials in the natural-log domain expected by attn_decode_reduce_kernel
+      // partials in the natural-log domain expected by the reducers
       float* pc = pb + (static_cast<int64_t>(c) * G + hh) * stride;
-      pc[d] = o;
-      if (d == 0) {
-        pc[D] = mxw * 0.6931471805599453f;
-        pc[D + 1] = lsum;
+      if constexpr (TICKET) {
+        st_sc1(pc + d, o);
+        if (d == 0) {
+          st_sc1(pc + D, mxw * 0.6931471805599453f);
+          st_sc1(pc + D + 1, lsum);
+        }
+      } else {
+        pc[d] = o;
+        if (d == 0) {
+          pc[D] = mxw * 0.6931471805599453f;
+          pc[D + 1] = lsum;
+        }
       }
     }
+  }
+  if constexpr (TICKET) {
+    // last-arriving chunk block of this (sequence, kv head) merges all partials in-launch
+    if (nchunks == 1) return;
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's sc1 stores are done
+    __syncthreads();
+    int* flag = pages;  // page ids are no longer needed
+    int* ctr = counters + b * nkv + kvh;
+    if (tid == 0) {
+      const int old = __hip_atomic_fetch_add(ctr, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      *flag = (old == nchunks - 1) ? 1 : 0;
+    }
+    __syncthreads();
+    if (*flag == 0) return;
+    reduce_chunks<G, true>(pb, nchunks, D, reinterpret_cast<float*>(smem), out_row);  // reuses the V images
+    if (tid == 0) __hip_atomic_store(ctr, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
 }
 
 template <int G, int D>
 static int launch_mfma(dim3 grid, hipStream_t s, const void* q, int q_stride, const void* kc, const void* vc,
-                       const void* bt, int bt_stride, const void* sl, void* part, void* out, int out_stride, int nkv,
-                       int bs, int chunk, int max_chunks, float scale) {
+                       const void* bt, int bt_stride, const void* sl, void* part, void* ctr, void* out, int out_stride,
+                       int nkv, int bs, int chunk, int max_chunks, float scale, bool ticket) {
+  // page-id staging sized for the largest balanced chunk any sequence of this table can get
+  const int grid_chunks = static_cast<int>(grid.x);
+  const int bal = ((bt_stride * bs + grid_chunks - 1) / grid_chunks + 127) / 128 * 128;
+  const int max_chunk = bal > chunk ? bal : chunk;
   const size_t lds = 4 * 32 * kVRowBytes + static_cast<size_t>(4) * G * (D + 2) * sizeof(float) +
-                     static_cast<size_t>((chunk + bs - 1) / bs + 2) * sizeof(int);
+                     static_cast<size_t>((max_chunk + bs - 1) / bs + 2) * sizeof(int);
   if (lds > 64 * 1024) return -4;
-  attn_decode_mfma_kernel<G, D><<<grid, 256, lds, s>>>(
-      (const bf16_t*)q, q_stride, (const bf16_t*)kc, (const bf16_t*)vc, (const int32_t*)bt, bt_stride,
-      (const int32_t*)sl, (float*)part, (bf16_t*)out, out_stride, nkv, bs, chunk, max_chunks,
-      scale * 1.4426950408889634f);
+  // the in-launch reduce stages 2 * G * nchunks + 2 * G floats in the (32 KB) V-image region
+  if (ticket && (2 * G * grid_chunks + 2 * G) * sizeof(float) > 4 * 32 * kVRowBytes) return -5;
+  auto kern = ticket ? attn_decode_mfma_kernel<G, D, true> : attn_decode_mfma_kernel<G, D, false>;
+  kern<<<grid, 256, lds, s>>>((const bf16_t*)q, q_stride, (const bf16_t*)kc, (const bf16_t*)vc, (const int32_t*)bt,
+                              bt_stride, (const int32_t*)sl, (float*)part, (int*)ctr, (bf16_t*)out, out_stride, nkv,
+                              bs, chunk, max_chunks, scale * 1.4426950408889634f);
   return static_cast<int>(hipGetLastError());
 }
 
 template <int G>
 static int launch_mfma_d(int D, dim3 grid, hipStream_t s, const void* q, int q_stride, const void* kc, const void* vc,
-                         const void* bt, int bt_stride, const void* sl, void* part, void* out, int out_stride, int nkv,
-                         int bs, int chunk, int max_chunks, float scale) {
+                         const void* bt, int bt_stride, const void* sl, void* part, void* ctr, void* out,
+                         int out_stride, int nkv, int bs, int chunk, int max_chunks, float scale, bool ticket) {
   switch (D) {
-    case 64: return launch_mfma<G, 64>(grid, s, q, q_stride, kc, vc, bt, bt_stride, sl, part, out, out_stride, nkv, bs, chunk, max_chunks, scale);
-    case 96: return launch_mfma<G, 96>(grid, s, q, q_stride, kc, vc, bt, bt_stride, sl, part, out, out_stride, nkv, bs, chunk, max_chunks, scale);
-    case 128: return launch_mfma<G, 128>(grid, s, q, q_stride, kc, vc, bt, bt_stride, sl, part, out, out_stride, nkv, bs, chunk, max_chunks, scale);
+    case 64: return launch_mfma<G, 64>(grid, s, q, q_stride, kc, vc, bt, bt_stride, sl, part, ctr, out, out_stride, nkv, bs, chunk, max_chunks, scale, ticket);
+    case 96: return launch_mfma<G, 96>(grid, s, q, q_stride, kc, vc, bt, bt_stride, sl, part, ctr, out, out_stride, nkv, bs, chunk, max_chunks, scale, ticket);
+    case 128: return launch_mfma<G, 128>(grid, s, q, q_stride, kc, vc, bt, bt_stride, sl, part, ctr, out, out_stride, nkv, bs, chunk, max_chunks, scale, ticket);
     default: return -2;
   }
 }
@@ -268,19 +302,21 @@ static int launch_mfma_d(int D, dim3 grid, hipStream_t s, const void* q, int q_s
 
 using namespace llmc;
 
-// Same workspace/contract as llmc_attn_decode (mode 0); chunk must be a multiple of 128.
-extern "C" int llmc_attn_decode_mfma_partials(const void* q, int q_stride, const void* k_cache, const void* v_cache,
-                                              const void* block_tables, int bt_stride, const void* seq_lens,
-                                              void* part, void* out, int out_stride, int B, int nh, int nkv, int D,
-                                              int bs, int chunk, int grid_chunks, int max_chunks, float scale,
-                                              hipStream_t s) {
+// Same workspace/contract as llmc_attn_decode; chunk (the minimum balanced chunk) must be a
+// multiple of 128. ticket: merge in-launch (last arriver) instead of leaving partials for the
+// reduce kernel.
+extern "C" int llmc_attn_decode_mfma(const void* q, int q_stride, const void* k_cache, const void* v_cache,
+                                     const void* block_tables, int bt_stride, const void* seq_lens, void* part,
+                                     void* counters, void* out, int out_stride, int B, int nh, int nkv, int D, int bs,
+                                     int chunk, int grid_chunks, int max_chunks, float scale, int ticket,
+                                     hipStream_t s) {
   if (nh % nkv != 0 || chunk % 128 != 0 || grid_chunks > max_chunks) return -1;
   dim3 grid(grid_chunks, nkv, B);
   switch (nh / nkv) {
-    case 1: return launch_mfma_d<1>(D, grid, s, q, q_stride, k_cache, v_cache, block_tables, bt_stride, seq_lens, part, out, out_stride, nkv, bs, chunk, max_chunks, scale);
-    case 2: return launch_mfma_d<2>(D, grid, s, q, q_stride, k_cache, v_cache, block_tables, bt_stride, seq_lens, part, out, out_stride, nkv, bs, chunk, max_chunks, scale);
-    case 4: return launch_mfma_d<4>(D, grid, s, q, q_stride, k_cache, v_cache, block_tables, bt_stride, seq_lens, part, out, out_stride, nkv, bs, chunk, max_chunks, scale);
-    case 8: return launch_mfma_d<8>(D, grid, s, q, q_stride, k_cache, v_cache, block_tables, bt_stride, seq_lens, part, out, out_stride, nkv, bs, chunk, max_chunks, scale);
+    case 1: return launch_mfma_d<1>(D, grid, s, q, q_stride, k_cache, v_cache, block_tables, bt_stride, seq_lens, part, counters, out, out_stride, nkv, bs, chunk, max_chunks, scale, ticket != 0);
+    case 2: return launch_mfma_d<2>(D, grid, s, q, q_stride, k_cache, v_cache, block_tables, bt_stride, seq_lens, part, counters, out, out_stride, nkv, bs, chunk, max_chunks, scale, ticket != 0);
+    case 4: return launch_mfma_d<4>(D, grid, s, q, q_stride, k_cache, v_cache, block_tables, bt_stride, seq_lens, part, counters, out, out_stride, nkv, bs, chunk, max_chunks, scale, ticket != 0);
+    case 8: return launch_mfma_d<8>(D, grid, s, q, q_stride, k_cache, v_cache, block_tables, bt_stride, seq_lens, part, counters, out, out_stride, nkv, bs, chunk, max_chunks, scale, ticket != 0);
     default: return -3;
   }
 }

@@ -103,6 +103,16 @@ __device__ __forceinline__ float block_sum(float v, float* red) {
 
 __device__ __forceinline__ float silu(float x) { return x / (1.f + __expf(-x)); }
 
+// Split-KV decode attention, balanced form: a fixed grid of `gc` chunk-blocks per (sequence, kv
+// head) shares the sequence's L keys evenly (multiples of 128 keys, at least `min_chunk`), so the
+// grid shape (and a captured graph) is independent of L while every block gets equal work.
+// chunk_arg < 0 encodes this form (min_chunk = -chunk_arg); >= 0 is a fixed chunk size.
+__device__ __forceinline__ int decode_chunk(int L, int gc, int chunk_arg) {
+  if (chunk_arg >= 0) return chunk_arg;
+  const int per = ((L + gc - 1) / gc + 127) & ~127;
+  return per > -chunk_arg ? per : -chunk_arg;
+}
+
 }  // namespace llmc
 
 #define LLMC_CHECK_LAUNCH() (void)0

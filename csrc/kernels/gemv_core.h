@@ -56,6 +56,31 @@ __global__ __launch_bounds__(NT) void gemv_kernel(const bf16_t* __restrict__ x, 
   bf16_t* xs = reinterpret_cast<bf16_t*>(smem);  // [M][K]
   const int tid = threadIdx.x;
   const int nchunk = K / 8;
+  const int wave = tid / kWave, lane = tid % kWave;
+  const int row0 = (blockIdx.x * WAVES + wave) * RPW;
+
+  // Weight rows (clamped: waves past N still load a valid row and discard it, so no lane
+  // diverges before the block barrier). The first UNROLL-batch of W is issued BEFORE the x
+  // prologue: W does not depend on x, so the HBM latency of the first batch overlaps the
+  // x staging / RMS norm, and the loop keeps the next batch in flight while it computes.
+  const u32x4* wrow[RPW];
+#pragma unroll
+  for (int r = 0; r < RPW; ++r) {
+    const int n = min(row0 + r, N - 1);
+    wrow[r] = reinterpret_cast<const u32x4*>(W + static_cast<int64_t>(n) * K);
+  }
+  constexpr int STEP = kWave * UNROLL;
+  const int iters = (nchunk + STEP - 1) / STEP;
+  u32x4 cur[RPW][UNROLL];
+  auto issue = [&](u32x4 (&dst)[RPW][UNROLL], int cbase) {
+#pragma unroll
+    for (int u = 0; u < UNROLL; ++u) {
+      const int c = min(cbase + u * kWave, nchunk - 1);  // clamped tail: loads stay batched
+#pragma unroll
+      for (int r = 0; r < RPW; ++r) dst[r][u] = load16<true>(wrow[r] + c);
+    }
+  };
+  issue(cur, lane);
 
   // ---- prologue: x -> LDS (optionally RMS-normalised) ----
   if constexpr (PRO == PRO_NORM) {
@@ -107,17 +132,9 @@ __global__ __launch_bounds__(NT) void gemv_kernel(const bf16_t* __restrict__ x, 
     }
   }
   __syncthreads();
-
-  // ---- main loop: stream RPW weight rows per wave ----
-  const int wave = tid / kWave, lane = tid % kWave;
-  const int row0 = (blockIdx.x * WAVES + wave) * RPW;
   if (row0 >= N) return;
-  const u32x4* wrow[RPW];
-#pragma unroll
-  for (int r = 0; r < RPW; ++r) {
-    const int n = min(row0 + r, N - 1);
-    wrow[r] = reinterpret_cast<const u32x4*>(W + static_cast<int64_t>(n) * K);
-  }
+
+  // ---- main loop: RPW weight rows per wave, one UNROLL-batch ahead ----
   float acc[RPW][M];
 #pragma unroll
   for (int r = 0; r < RPW; ++r)
@@ -125,36 +142,31 @@ __global__ __launch_bounds__(NT) void gemv_kernel(const bf16_t* __restrict__ x, 
     for (int m = 0; m < M; ++m) acc[r][m] = 0.f;
 
   const u32x4* xv = reinterpret_cast<const u32x4*>(xs);
-  const int full = nchunk / (kWave * UNROLL);  // iterations with every lane in range
+  auto consume = [&](const u32x4 (&wv)[RPW][UNROLL], int cbase) {
+#pragma unroll
+    for (int u = 0; u < UNROLL; ++u) {
+      const int c = cbase + u * kWave;
+      if (c < nchunk) {
+#pragma unroll
+        for (int m = 0; m < M; ++m) {
+          const u32x4 xx = xv[m * nchunk + c];
+#pragma unroll
+          for (int r = 0; r < RPW; ++r) acc[r][m] = dot8_bf16(wv[r][u], xx, acc[r][m]);
+        }
+      }
+    }
+  };
   int c0 = lane;
-  for (int it = 0; it < full; ++it, c0 += kWave * UNROLL) {
-    u32x4 wv[RPW][UNROLL];
+  for (int it = 0; it + 1 < iters; ++it, c0 += STEP) {
+    u32x4 nxt[RPW][UNROLL];
+    issue(nxt, c0 + STEP);
+    consume(cur, c0);
 #pragma unroll
     for (int u = 0; u < UNROLL; ++u)
 #pragma unroll
-      for (int r = 0; r < RPW; ++r) wv[r][u] = load16<true>(wrow[r] + c0 + u * kWave);
-#pragma unroll
-    for (int u = 0; u < UNROLL; ++u) {
-#pragma unroll
-      for (int m = 0; m < M; ++m) {
-        const u32x4 xx = xv[m * nchunk + c0 + u * kWave];
-#pragma unroll
-        for (int r = 0; r < RPW; ++r) acc[r][m] = dot8_bf16(wv[r][u], xx, acc[r][m]);
-      }
-    }
+      for (int r = 0; r < RPW; ++r) cur[r][u] = nxt[r][u];
   }
-  // tail (K not a multiple of 64*8*UNROLL)
-  for (int c = c0; c < nchunk; c += kWave) {
-    u32x4 wv[RPW];
-#pragma unroll
-    for (int r = 0; r < RPW; ++r) wv[r] = load16<true>(wrow[r] + c);
-#pragma unroll
-    for (int m = 0; m < M; ++m) {
-      const u32x4 xx = xv[m * nchunk + c];
-#pragma unroll
-      for (int r = 0; r < RPW; ++r) acc[r][m] = dot8_bf16(wv[r], xx, acc[r][m]);
-    }
-  }
+  consume(cur, c0);
 
 #pragma unroll
   for (int r = 0; r < RPW; ++r)

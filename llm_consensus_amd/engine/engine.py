@@ -21,6 +21,7 @@ from __future__ import annotations
 
 import dataclasses
 import math
+import os
 import time
 from typing import Callable, Dict, List, Optional, Sequence as Seq
 
@@ -48,23 +49,31 @@ class EngineConfig:
     steps_per_graph: int = 8
     use_graphs: bool = True
     prefill_chunk: int = 8192
-    attn_chunk: int = 0  # 0 = per context bucket (128 / 256 / 512 tokens per split-KV block)
+    attn_chunk: int = 0  # 0 = balanced MFMA split (>= 128 keys per block); > 0 = fixed chunk size
     init_scale: float = 1.0
     stream_priority: int = 0
 
 
-def attn_buckets(ctxmax: int, fixed_chunk: int = 0) -> List[tuple]:
+def attn_buckets(ctxmax: int, fixed_chunk: int = 0, blocks_per_head: int = 64) -> List[tuple]:
     """Decode-attention shapes per context bucket: [(capacity_tokens, chunk, grid_chunks)].
 
-    Capacities double from 1024 up to ``ctxmax``. The chunk (keys per split-KV block) grows with
-    the bucket so the grid stays ~32-256 blocks per kv head — enough work for 256 CUs without
-    many-chunk reductions (measured on MI355X, profiles/r1_attn_decode_microbench.md): 128 keys up
-    to 4k context, 256 up to 8k, 512 beyond. Multiples of 128 select the MFMA decode kernel."""
+    Default (MFMA kernel, balanced split): ``chunk`` is the minimum of 128 keys per split-KV block
+    and the kernel spreads a sequence's keys evenly over ``grid_chunks`` blocks, so the grid only
+    grows with the context until ``blocks_per_head`` (~1 block per CU over the kv heads of one
+    row, measured on MI355X: profiles/r1_attn_decode_microbench.md) and one bucket then covers
+    every longer context. ``fixed_chunk`` > 0 selects fixed-size chunks (VALU kernel when not a
+    multiple of 128): capacities double from 1024 and grid_chunks * chunk covers the bucket."""
     out, cap = [], 1024
     while True:
         c = min(cap, ctxmax)
-        chunk = fixed_chunk or (128 if cap <= 4096 else 256 if cap <= 8192 else 512)
-        out.append((c, chunk, (c + chunk - 1) // chunk))
+        if fixed_chunk:
+            out.append((c, fixed_chunk, (c + fixed_chunk - 1) // fixed_chunk))
+        else:
+            gc = min((c + 127) // 128, blocks_per_head)
+            if out and out[-1][2] == gc:
+                out[-1] = (c, 128, gc)  # same grid: widen the previous bucket
+            else:
+                out.append((c, 128, gc))
         if cap >= ctxmax:
             return out
         cap *= 2
@@ -169,7 +178,9 @@ class Engine:
                             torch.zeros(self.tp.size, B, self.w.vocab_local, dtype=torch.float32, device=dev))
         # split-KV decode attention: one (chunk, grid) shape per context bucket
         ctxmax = self.ecfg.max_context + self.ecfg.steps_per_graph + 2
-        self.attn_buckets = attn_buckets(ctxmax, self.ecfg.attn_chunk)
+        blocks = int(os.environ.get("LLMC_ATTN_BLOCKS", "256"))  # target blocks per decode row (1/CU)
+        fixed = self.ecfg.attn_chunk or (0 if ops.ATTN_DECODE_MODE >= 2 else 128)  # VALU modes: fixed chunks
+        self.attn_buckets = attn_buckets(ctxmax, fixed, max(1, blocks // self.nkv))
         self.max_chunks = max(gc for _, _, gc in self.attn_buckets)
         self.attn_part, self.attn_counters = ops.decode_attn_workspace(B, self.nh, self.nkv, self.D,
                                                                         self.max_chunks, dev)

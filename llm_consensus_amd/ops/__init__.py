@@ -159,9 +159,9 @@ def decode_attn_workspace(B, nh, nkv, D, max_chunks, device):
     return part, counters
 
 
-# decode attention kernel: 2 = MFMA partials + reduce (default; chunk % 128 == 0), 0 = VALU
-# partials + reduce, 1 = VALU with in-kernel last-arriver reduce. Chunks not a multiple of 128
-# fall back to mode 0.
+# decode attention kernel: 2 = MFMA balanced split + reduce kernel (default), 3 = MFMA with the
+# in-launch last-arriver reduce, 0 = VALU fixed chunks + reduce kernel, 1 = VALU + in-launch
+# reduce. MFMA modes need chunk % 128 == 0 (else mode 0 runs).
 ATTN_DECODE_MODE = int(os.environ.get("LLMC_ATTN_MODE", "2"))
 
 
@@ -174,7 +174,7 @@ def attn_decode(q, k_cache, v_cache, block_tables, seq_lens, out, part, counters
     max_chunks = part.shape[2]
     gc = max_chunks if grid_chunks is None else min(grid_chunks, max_chunks)
     if mode is None:
-        mode = ATTN_DECODE_MODE if (ATTN_DECODE_MODE != 2 or chunk % 128 == 0) else 0
+        mode = ATTN_DECODE_MODE if (ATTN_DECODE_MODE < 2 or chunk % 128 == 0) else 0
     kernels().attn_decode(_p(q), q.stride(0), _p(k_cache), _p(v_cache), _p(block_tables), block_tables.stride(0),
                           _p(seq_lens), _p(part), _p(counters), _p(out), out.stride(0), B, nh, nkv, D, bs, chunk, gc,
                           max_chunks, float(scale), mode, _s(q))

@@ -38,8 +38,10 @@ def timeit(fn, iters=50, warm=5):
 
 
 def bench_attn():
+    """VALU fixed chunks (mode 0) vs the MFMA balanced split (mode 2, min 128 keys per block) at
+    several grid sizes (blocks per kv head)."""
     nh, nkv, D, bs = 32, 8, 128, 64
-    for L in [128, 600, 2048, 4096, 16384, 33000]:
+    for L in [128, 600, 2048, 4096, 16384, 33000, 65000]:
         nb = (L + bs - 1) // bs + 2
         kc = torch.randn(nb, nkv, bs, D, device="cuda").to(BF)
         vc = torch.randn_like(kc)
@@ -47,20 +49,24 @@ def bench_attn():
         sl = torch.tensor([L], dtype=torch.int32, device="cuda")
         q = torch.randn(1, nh * D, device="cuda").to(BF)
         out = torch.empty(1, nh * D, dtype=BF, device="cuda")
-        for chunk in [64, 128, 256, 512]:
+        gb = L * nkv * D * 2 * 2 / 1e9
+        line = []
+        for chunk in [64, 256]:
             mc = (L + chunk - 1) // chunk
             part, ctr = ops.decode_attn_workspace(1, nh, nkv, D, max(mc, 1), "cuda")
-            res = []
-            for mode in (0, 2):
-                if mode == 2 and chunk % 128:
-                    res.append(float("inf"))
-                    continue
-                us = timeit(lambda: ops.attn_decode(q, kc, vc, bt, sl, out, part, ctr, nh, nkv, D, bs, chunk,
-                                                    1 / math.sqrt(D), mode=mode))
-                res.append(us)
-            gb = L * nkv * D * 2 * 2 / 1e9
-            print(f"attn L={L:6d} chunk={chunk:5d} chunks={mc:4d}: valu {res[0]:7.2f} us  mfma {res[1]:7.2f} us"
-                  f"  ({gb / min(res) * 1e6 / 1e3:5.2f} TB/s)")
+            us = timeit(lambda: ops.attn_decode(q, kc, vc, bt, sl, out, part, ctr, nh, nkv, D, bs, chunk,
+                                                1 / math.sqrt(D), mode=0))
+            line.append(f"valu c{chunk} {us:6.2f}")
+        best = 1e9
+        for mode in (2, 3):
+            for gc in [16, 24, 32, 48, 64]:
+                gc_eff = min(gc, (L + 127) // 128)
+                part, ctr = ops.decode_attn_workspace(1, nh, nkv, D, gc_eff, "cuda")
+                us = timeit(lambda: ops.attn_decode(q, kc, vc, bt, sl, out, part, ctr, nh, nkv, D, bs, 128,
+                                                    1 / math.sqrt(D), grid_chunks=gc_eff, mode=mode))
+                best = min(best, us)
+                line.append(f"m{mode} g{gc} {us:6.2f}")
+        print(f"attn L={L:6d}: " + "  ".join(line) + f"  | best {gb / best * 1e6 / 1e3:5.2f} TB/s")
 
 
 def bench_gemv():
@@ -72,6 +78,27 @@ def bench_gemv():
         out = torch.zeros(1, N // 2 if epi == 3 else N, dtype=torch.float32 if epi == 1 else BF, device="cuda")
         us = timeit(lambda: ops.gemv(x, W, epi, out=out, norm_w=nw if norm else None))
         print(f"gemv N={N:6d} K={K:5d} epi={epi}: {us:8.2f} us  {N * K * 2 / us / 1e6:6.2f} TB/s")
+
+
+def bench_mall():
+    """Does a weight matrix read shortly before a GEMV (e.g. by idle CUs during attention) make the
+    GEMV faster (MALL / L2 hits)? Each variant first streams 1 GiB to flush the caches."""
+    big = torch.empty(512 * 1024 * 1024, dtype=BF, device="cuda")
+    sink = torch.empty(1, dtype=BF, device="cuda")
+    for (N, K) in [(4096, 4096), (6144, 4096)]:
+        x = torch.randn(1, K, device="cuda").to(BF)
+        W = (torch.randn(N, K, device="cuda") * 0.02).to(BF)
+        W2 = torch.empty_like(W)
+        out = torch.zeros(1, N, dtype=BF, device="cuda")
+        t_flush = timeit(lambda: torch.sum(big, dim=0, keepdim=True, out=sink), iters=5)
+        t_pre = timeit(lambda: (torch.sum(big, dim=0, keepdim=True, out=sink),
+                                torch.sum(W.view(-1), dim=0, keepdim=True, out=sink),
+                                ops.gemv(x, W, 0, out=out)), iters=5)
+        t_other = timeit(lambda: (torch.sum(big, dim=0, keepdim=True, out=sink),
+                                  torch.sum(W2.view(-1), dim=0, keepdim=True, out=sink),
+                                  ops.gemv(x, W, 0, out=out)), iters=5)
+        print(f"mall N={N} K={K}: flush {t_flush:.1f} us; flush+read(W)+gemv {t_pre:.1f}; "
+              f"flush+read(W2)+gemv {t_other:.1f} -> gemv saving from prior read {t_other - t_pre:.2f} us")
 
 
 def bench_launch():
@@ -89,3 +116,5 @@ if __name__ == "__main__":
         bench_attn()
     if what in ("gemv", "all"):
         bench_gemv()
+    if what in ("mall",):
+        bench_mall()

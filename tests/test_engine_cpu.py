@@ -107,7 +107,9 @@ def test_attn_buckets_cover_context():
         bks = attn_buckets(ctxmax)
         assert bks[-1][0] == ctxmax
         for cap, chunk, gc in bks:
-            assert chunk % 128 == 0 and gc * chunk >= cap
-        caps = [b[0] for b in bks]
-        assert caps == sorted(caps)
-    assert {c for _, c, _ in attn_buckets(4106, 64)} == {64}
+            assert chunk == 128 and 1 <= gc <= 64
+        assert [b[0] for b in bks] == sorted(b[0] for b in bks)
+        assert len({b[2] for b in bks}) == len(bks)  # one graph per distinct grid
+    assert attn_buckets(131082, 0, 32)[-1] == (131082, 128, 32)
+    fixed = attn_buckets(4106, 64)
+    assert {c for _, c, _ in fixed} == {64} and all(gc * 64 >= cap for cap, _, gc in fixed)

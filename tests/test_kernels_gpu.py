@@ -154,7 +154,7 @@ def _paged_kv(B, L_max, nkv, D, bs):
 
 @pytest.mark.parametrize("nh,nkv,D", [(32, 8, 128), (32, 32, 96), (16, 2, 128), (4, 2, 64)])
 @pytest.mark.parametrize("lens", [[1, 7], [100, 1000], [3000, 257]])
-@pytest.mark.parametrize("mode,chunk", [(0, 64), (0, 256), (1, 64), (2, 128), (2, 256), (2, 512)])
+@pytest.mark.parametrize("mode,chunk", [(0, 64), (0, 256), (1, 64), (2, 128), (2, 256), (2, 512), (3, 128), (3, 256)])
 def test_attn_decode(cuda, nh, nkv, D, lens, mode, chunk):
     torch.manual_seed(3)
     B, bs = len(lens), 64
@@ -171,6 +171,29 @@ def test_attn_decode(cuda, nh, nkv, D, lens, mode, chunk):
     for _ in range(3):
         out.zero_()
         ops.attn_decode(q, kc, vc, bt.cuda(), sl.cuda(), out, part, ctr, nh, nkv, D, bs, chunk, scale, mode=mode)
+        close(out, ref, 2e-2)
+    assert int(ctr.abs().sum()) == 0
+
+
+@pytest.mark.parametrize("nh,nkv,D", [(32, 8, 128), (32, 32, 96), (16, 2, 128)])
+@pytest.mark.parametrize("gc", [1, 3, 7, 64])
+@pytest.mark.parametrize("mode", [2, 3])
+def test_attn_decode_balanced_split(cuda, nh, nkv, D, gc, mode):
+    """MFMA form with a fixed grid: each sequence's keys spread evenly over gc blocks (>= 128)."""
+    torch.manual_seed(5)
+    lens, bs = [5000, 130, 1], 64
+    B = len(lens)
+    kc, vc, bt = _paged_kv(B, max(lens), nkv, D, bs)
+    q = rnd(B, nh * D)
+    sl = torch.tensor(lens, dtype=torch.int32)
+    part, ctr = ops.decode_attn_workspace(B, nh, nkv, D, gc, "cuda")
+    out = torch.empty(B, nh * D, dtype=BF, device="cuda")
+    scale = 1 / math.sqrt(D)
+    ref = oracle.attn_decode(q.cpu(), kc.cpu(), vc.cpu(), bt, sl, nh, nkv, D, bs, scale)
+    for _ in range(2):  # the ticket form must re-arm its counters
+        out.zero_()
+        ops.attn_decode(q, kc, vc, bt.cuda(), sl.cuda(), out, part, ctr, nh, nkv, D, bs, 128, scale, grid_chunks=gc,
+                        mode=mode)
         close(out, ref, 2e-2)
     assert int(ctr.abs().sum()) == 0
 

@@ -60,7 +60,7 @@ def describe(name: str, tp: Optional[int] = None) -> Dict:
     c = spec.config
     tp = tp or c.default_tp
     return {
-        "source": "local",
+        "source": "checkpoint" if c.checkpoint else "local",
         "id": c.name,
         "arch": c.arch,
         "params": c.num_params(),
@@ -73,6 +73,7 @@ def describe(name: str, tp: Optional[int] = None) -> Dict:
         "layers": c.n_layers, "hidden": c.hidden, "heads": c.n_heads, "kv_heads": c.n_kv_heads,
         "head_dim": c.head_dim, "intermediate": c.intermediate, "vocab": c.vocab,
         "experts": c.n_experts, "top_k": c.top_k_experts,
+        **({"path": c.checkpoint} if c.checkpoint else {}),
     }
 
 

@@ -7,7 +7,7 @@ entry and the judge must resolve, main.go:395-415) → fan-out → judge → per
 
 Extra engine flags (no reference counterpart): ``--max-tokens``,
 ``--temperature``, ``--top-p``, ``--top-k``, ``--seed``, ``--gpus``, ``--trace``,
-``--list-models``.
+``--list-models``, ``--weights-dir`` (Hugging Face checkpoints as extra local model families).
 """
 
 from __future__ import annotations
@@ -84,7 +84,25 @@ def make_flagset() -> FlagSet:
     fs.add("gpus", "string", "", "Comma-separated GPU ids to place models on (default: all visible)")
     fs.add("trace", "bool", False, "Write a Chrome trace of engine spans to the run directory")
     fs.add("list-models", "bool", False, "Print the local model catalog as JSON and exit")
+    fs.add("weights-dir", "string", "",
+           "Comma-separated Hugging Face checkpoint dirs (or parents of them) to serve as models ($LLMC_WEIGHTS_DIR)")
     return fs
+
+
+def register_weights(spec: str) -> List[str]:
+    """Register every checkpoint under the comma-separated dirs ``spec`` as a model family."""
+    from .models.checkpoint import CheckpointError, register_dir
+
+    names: List[str] = []
+    for d in (x for x in (trim_space(p) for p in spec.split(",")) if x):
+        try:
+            found = register_dir(d)
+        except (CheckpointError, OSError, ValueError, KeyError) as e:
+            raise CLIError(f"loading checkpoint config from {d}: {e}") from None
+        if not found:
+            raise CLIError(f"no Hugging Face checkpoint (config.json + *.safetensors) under {d}")
+        names.extend(found)
+    return names
 
 
 def _stdin_is_pipe(stdin) -> bool:
@@ -130,6 +148,9 @@ def _go_path_err(op: str, path: str, e: OSError) -> str:
 def parse_flags(argv: List[str], stdout: TextIO = sys.stdout, stderr: TextIO = sys.stderr, stdin=None) -> Config:
     fs = make_flagset()
     v, rest = parse_or_exit(fs, argv, stderr)
+    wd = v["weights_dir"] or os.environ.get("LLMC_WEIGHTS_DIR", "")
+    if wd:
+        register_weights(wd)
     if v["list_models"]:
         stdout.write(dump_catalog())
         raise SystemExit(0)

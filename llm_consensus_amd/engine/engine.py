@@ -215,6 +215,15 @@ class Engine:
         seq.logits = None
         seq.has_logits = False
 
+    def truncate(self, seq: Sequence, length: int) -> None:
+        """Forget every token of ``seq`` from position ``length`` on (their KV slots are simply
+        overwritten by the next prefill; blocks stay reserved)."""
+        if not 0 <= length <= seq.length:
+            raise EngineError(f"truncate to {length} of a {seq.length}-token sequence")
+        seq.length = length
+        seq.logits = None
+        seq.has_logits = False
+
     def _reserve(self, seq: Sequence, total_tokens: int) -> None:
         need = self.alloc.blocks_for(total_tokens) - len(seq.blocks)
         if total_tokens > self.max_blocks_per_seq * self.bs:
@@ -495,7 +504,7 @@ class Engine:
         if B > self.ecfg.max_batch:
             raise EngineError(f"{B} sequences > max_batch {self.ecfg.max_batch}")
         S = self.ecfg.steps_per_graph
-        eos = self._eos_id()
+        eos_set = set(self.cfg.eos)
         with self._on_stream(), trace.span("decode", engine=self.name, rows=B):
             max_new = max(p.max_tokens for p in params)
             self._use_topkp = any((p.top_k > 0 or p.top_p < 1.0) for p in params)
@@ -532,8 +541,9 @@ class Engine:
                     n = min(int(counts[r]), params[i].max_tokens)
                     new = toks[r][produced[i]:n].tolist() if n > produced[i] else []
                     stop = False
-                    if params[i].stop_on_eos and eos in new:
-                        new = new[: new.index(eos)]
+                    hit = next((j for j, t in enumerate(new) if t in eos_set), -1) if params[i].stop_on_eos else -1
+                    if hit >= 0:
+                        new = new[:hit]
                         stop = True
                     if new:
                         results[i].extend(new)
@@ -600,7 +610,7 @@ class Engine:
             s.has_logits = False
 
     def _eos_id(self) -> int:
-        return self.cfg.vocab - 1
+        return self.cfg.eos[0]
 
     # -- convenience ----------------------------------------------------------------------------------
     @torch.no_grad()

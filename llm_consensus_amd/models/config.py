@@ -39,6 +39,15 @@ class ModelConfig:
     top_k_experts: int = 0
     rope_scaling: Optional[RopeScaling] = None
     default_tp: int = 1
+    # Hugging Face checkpoint directory (models/checkpoint.py); None = seeded random init
+    checkpoint: Optional[str] = None
+    bos_id: int = -1            # -1: the synthetic tokenizer's (vocab - 2)
+    eos_ids: tuple = ()         # empty: the synthetic tokenizer's (vocab - 1)
+    tie_embeddings: bool = False
+
+    @property
+    def eos(self) -> tuple:
+        return self.eos_ids or (self.vocab - 1,)
 
     # -- derived sizes ---------------------------------------------------------------------
     @property

@@ -12,9 +12,10 @@ checkpoint compatibility:
   * ``w_down`` [H, I];
   * MoE (Mixtral): ``w_router`` [E, H], ``w_gu`` [E, 2I, H], ``w_down`` [E, H, I];
   * ``embed`` [V, H] (replicated under TP), ``lm_head`` [V, H] (vocab-parallel under TP).
-Weights are random-init from a seed (no checkpoints offline). Each tensor is generated in full
-from its own (seed, name)-derived generator and then sliced to this rank's shard, so TP=1 and
-TP=n models are the SAME model (tested on CPU with gloo).
+Weights are random-init from a seed, or read from a Hugging Face checkpoint when the config
+names one (``models/checkpoint.py``). Either way each tensor is produced in full in the logical
+layout (from its own (seed, name)-derived generator, or from the safetensors shards) and then
+sliced to this rank's shard, so TP=1 and TP=n models are the SAME model (tested on CPU with gloo).
 """
 
 from __future__ import annotations
@@ -39,7 +40,12 @@ class LayerWeights:
 
 class TransformerWeights:
     def __init__(self, cfg: ModelConfig, tp: TPGroup, device: torch.device, seed: int,
-                 init_scale: float = 1.0):
+                 init_scale: float = 1.0, source=None):
+        if source is None and cfg.checkpoint:
+            from .checkpoint import HFCheckpoint
+
+            source = HFCheckpoint(cfg.checkpoint, cfg)
+        self.source = source
         self.cfg = cfg
         self.tp = tp
         self.device = device
@@ -56,6 +62,7 @@ class TransformerWeights:
         self.qkv_size = self.q_size + 2 * self.kv_size
         self.layers: List[LayerWeights] = []
         self._build()
+        self.source = None  # release the checkpoint's file handles
 
     # -- generation -------------------------------------------------------------------------
     def _gen(self, name: str, shape, std: float, mean: float = 0.0) -> torch.Tensor:
@@ -69,15 +76,28 @@ class TransformerWeights:
             t.add_(mean)
         return t.to(torch.bfloat16)
 
+    def _full(self, name: str, shape, kind: str = "linear") -> torch.Tensor:
+        """Full (unsharded) logical tensor ``name``: checkpoint or seeded random init."""
+        if self.source is not None:
+            t = self.source.get(name)
+            if tuple(t.shape) != tuple(shape):
+                raise ValueError(f"checkpoint tensor {name}: shape {tuple(t.shape)} != expected {tuple(shape)}")
+            return t.to(device=self.device, dtype=torch.bfloat16)
+        if kind == "embed":
+            return self._gen(name, shape, 1.0)
+        if kind == "norm":
+            return self._gen(name, shape, 0.02, 1.0)
+        return self._gen(name, shape, self.init_scale / math.sqrt(shape[1]))
+
     def _linear(self, name: str, n_out: int, n_in: int) -> torch.Tensor:
-        return self._gen(name, (n_out, n_in), self.init_scale / math.sqrt(n_in))
+        return self._full(name, (n_out, n_in))
 
     def _build(self) -> None:
         c, r, n = self.cfg, self.tp.rank, self.tp.size
         D = c.head_dim
         with torch.no_grad():
-            self.embed = self._gen("embed", (c.vocab, c.hidden), 1.0)
-            self.final_norm = self._gen("final_norm", (c.hidden,), 0.02, 1.0)
+            self.embed = self._full("embed", (c.vocab, c.hidden), "embed")
+            self.final_norm = self._full("final_norm", (c.hidden,), "norm")
             lm = self._linear("lm_head", c.vocab, c.hidden)
             v0, v1 = shard_range(c.vocab, r, n)
             self.lm_head = lm[v0:v1].contiguous()
@@ -85,8 +105,8 @@ class TransformerWeights:
             for i in range(c.n_layers):
                 L = LayerWeights()
                 p = f"layers.{i}."
-                L.ln1 = self._gen(p + "ln1", (c.hidden,), 0.02, 1.0)
-                L.ln2 = self._gen(p + "ln2", (c.hidden,), 0.02, 1.0)
+                L.ln1 = self._full(p + "ln1", (c.hidden,), "norm")
+                L.ln2 = self._full(p + "ln2", (c.hidden,), "norm")
                 qkv = self._linear(p + "w_qkv", c.qkv_size, c.hidden)
                 q0, q1 = shard_range(c.n_heads, r, n)
                 k0, k1 = shard_range(c.n_kv_heads, r, n)

@@ -30,7 +30,7 @@ from ..catalog import PROVIDER_LOCAL, ModelSpec
 from ..context import Context, ContextError
 from ..parallel.placement import ModelDemand, default_gpus, describe, solve
 from ..utils import trace as tracing
-from ..utils.tokenizer import get_tokenizer
+from ..utils.tokenizer import tokenizer_for
 from .base import Request, Response, StreamCallback
 
 DEFAULT_MAX_TOKENS = 4096
@@ -139,6 +139,7 @@ class LocalBackend:
                     s = self.specs[m]
                     n = (counts or {}).get(m, 1)
                     models.append({"name": m, "family": s.family, "seed": s.seed, "max_context": self._ctx[m],
+                                   "checkpoint": s.config.checkpoint,
                                    "max_batch": max(1, min(4, n)),
                                    "max_seqs": max(1, n) + (1 if m == judge else 0)})
             if groups:
@@ -230,7 +231,7 @@ class LocalProvider:
         self.backend = backend
         self.model = model
         self.spec = backend.specs[model]
-        self.tok = get_tokenizer(self.spec.config.vocab)
+        self.tok = tokenizer_for(self.spec.config)
         self._sess_lock = threading.Lock()
         self._session: Optional[dict] = None
 
@@ -291,7 +292,7 @@ class LocalProvider:
 
     def query_stream(self, ctx: Context, req: Request, callback: Optional[StreamCallback]) -> Response:
         t0 = time.monotonic_ns()
-        ids = self.tok.encode(req.prompt, add_bos=True)
+        ids = self.tok.encode_prompt(req.prompt)
         params = self._params(req, len(ids))
         rid, q = self.backend._new_request()
         with tracing.span("query", cat="driver", model=self.model, prompt_tokens=len(ids)):
@@ -303,8 +304,8 @@ class LocalProvider:
         with self._sess_lock:
             self.close_session()
             sid = next(self.backend._ids)
-            ids = self.tok.encode(header, add_bos=True)
-            self._session = {"sid": sid, "text": header, "ntok": len(ids)}
+            ids = self.tok.prompt_prefix_ids(header)
+            self._session = {"sid": sid, "text": header, "ids": list(ids)}
             self.backend.broadcast(self.model, ("sess_open", sid, self.model, ids))
 
     def extend_session(self, text: str) -> None:
@@ -314,7 +315,7 @@ class LocalProvider:
                 return
             ids = self.tok.encode(text)
             s["text"] += text
-            s["ntok"] += len(ids)
+            s["ids"].extend(ids)
             self.backend.broadcast(self.model, ("sess_extend", s["sid"], ids))
 
     def close_session(self) -> None:
@@ -327,7 +328,11 @@ class LocalProvider:
                 pass
 
     def query_stream_session(self, ctx: Context, req: Request, callback: Optional[StreamCallback]) -> Response:
-        """Finish the session whose prefilled text is a prefix of ``req.prompt``."""
+        """Finish the session whose prefilled text is a prefix of ``req.prompt``.
+
+        The prompt is tokenized whole (exactly as ``query_stream`` would) and matched against the
+        ids already prefilled: only the unmatched tail is prefilled, after truncating the session
+        to the common prefix (tokenizers that are not segment-stable, chat templates)."""
         with self._sess_lock:
             s = self._session
             self._session = None
@@ -336,13 +341,21 @@ class LocalProvider:
                 self.backend.broadcast(self.model, ("sess_close", s["sid"]))
             return self.query_stream(ctx, req, callback)
         t0 = time.monotonic_ns()
-        rest = self.tok.encode(req.prompt[len(s["text"]):])
-        total = s["ntok"] + len(rest)
-        params = self._params(req, total)
+        full = self.tok.encode_prompt(req.prompt)
+        done = s["ids"]
+        cp = 0
+        n = min(len(done), len(full))
+        while cp < n and done[cp] == full[cp]:
+            cp += 1
+        if cp == len(full):  # keep at least one token to prefill (its logits start the decode)
+            cp -= 1
+        rest = full[cp:]
+        params = self._params(req, len(full))
         rid, q = self.backend._new_request()
-        with tracing.span("judge_session_finish", cat="driver", model=self.model, rest_tokens=len(rest)):
-            self.backend.broadcast(self.model, ("sess_generate", s["sid"], rid, rest, params))
-            return self._stream(ctx, rid, q, callback, t0, total)
+        with tracing.span("judge_session_finish", cat="driver", model=self.model, rest_tokens=len(rest),
+                          reused_tokens=cp):
+            self.backend.broadcast(self.model, ("sess_generate", s["sid"], rid, rest, params, cp))
+            return self._stream(ctx, rid, q, callback, t0, len(full))
 
     def close(self) -> None:
         self.close_session()

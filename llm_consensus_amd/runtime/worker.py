@@ -3,7 +3,7 @@
 Control plane (C6): a duplex pipe to the driver carrying commands and token-id streams.
   driver -> worker  ("generate", rid, model, prompt_ids, params)
                     ("sess_open", sid, model, ids) / ("sess_extend", sid, ids)
-                    ("sess_generate", sid, rid, ids, params) / ("sess_close", sid)
+                    ("sess_generate", sid, rid, ids, params, keep) / ("sess_close", sid)
                     ("cancel", rid) / ("shutdown",)
   worker -> driver  ("ready", info) / ("fatal", msg)
                     ("tokens", rid, ids) / ("done", rid, stats) / ("error", rid, msg)
@@ -80,10 +80,12 @@ class _EngineHost:
                     if seq is not None and ids:
                         self.engine.prefill([seq], [ids], want_logits=False)
                 elif kind == "sess_generate":
-                    _, sid, req = item
+                    _, sid, req, keep = item
                     seq = self.sessions.pop(sid, None)
                     if seq is None:
                         raise RuntimeError(f"unknown judge session {sid}")
+                    if keep < seq.length:  # drop the prefilled tail that the full tokenization differs on
+                        self.engine.truncate(seq, keep)
                     try:
                         self._run([seq], [req], [req.ids], SamplingParams)
                     finally:
@@ -188,7 +190,12 @@ def worker_main(gpu: int, conn, models: List[dict], dist_info: Optional[dict], t
                     groups[gname] = (g, ranks.index(dist_info["rank"]), len(ranks))
         hosts: Dict[str, _EngineHost] = {}
         for m in models:
-            cfg = FAMILIES[m["family"]]
+            cfg = FAMILIES.get(m["family"])
+            if cfg is None and m.get("checkpoint"):  # --weights-dir family (spawned: re-register)
+                from ..models.checkpoint import register_dir
+
+                register_dir(m["checkpoint"])
+                cfg = FAMILIES[m["family"]]
             if m["name"] in groups:
                 g, r, n = groups[m["name"]]
                 tp = TPGroup(g, r, n)
@@ -238,10 +245,10 @@ def worker_main(gpu: int, conn, models: List[dict], dist_info: Optional[dict], t
             if sid in sess_host:
                 sess_host[sid].q.put(("sess_extend", sid, ids))
         elif kind == "sess_generate":
-            _, sid, rid, ids, params = msg
+            _, sid, rid, ids, params, keep = msg
             ctx = Context.background()
             ctxs[rid] = ctx
-            sess_host.pop(sid).q.put(("sess_generate", sid, _Req(rid, ids, params, ctx)))
+            sess_host.pop(sid).q.put(("sess_generate", sid, _Req(rid, ids, params, ctx), keep))
         elif kind == "sess_close":
             h = sess_host.pop(msg[1], None)
             if h is not None:

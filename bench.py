@@ -49,6 +49,8 @@ def main() -> None:
     ap.add_argument("--temperature", type=float, default=1.0)
     ap.add_argument("--steps-per-graph", type=int, default=8)
     ap.add_argument("--no-graphs", action="store_true")
+    ap.add_argument("--results-dir", default=os.path.join(ROOT, "bench", "results"),
+                    help="rank 0 also writes the full record (per-step stats, p50/p90) here ('' = off)")
     args = ap.parse_args()
 
     import torch
@@ -212,6 +214,17 @@ def main() -> None:
             },
         }
         print(json.dumps(out), flush=True)
+        if args.results_dir:
+            srt = sorted(lat)
+            rec = dict(out, per_step=per_step, p90_e2e_latency_s=round(srt[min(len(srt) - 1, int(0.9 * len(srt)))], 3),
+                       time_utc=time.strftime("%Y%m%dT%H%M%SZ", time.gmtime()), argv=sys.argv[1:])
+            try:
+                os.makedirs(args.results_dir, exist_ok=True)
+                fn = os.path.join(args.results_dir, f"bench_{rec['time_utc']}_n{n_gpus}.json")
+                with open(fn, "w") as f:
+                    json.dump(rec, f, indent=2)
+            except OSError as e:
+                log(f"could not write results record: {e}")
     if world > 1:
         dist.destroy_process_group()
 

@@ -24,6 +24,28 @@ import traceback
 from typing import Dict, List, Optional
 
 
+def parse_faults(spec: str) -> Dict[str, tuple]:
+    """Fault-injection hook: ``LLMC_FAULT="<model>:<stage>[:<k>],..."`` makes that
+    model's engine fail — stage ``init`` (every request errors), ``prefill`` (before prefill) or
+    ``decode`` (after k streamed tokens, default 1). Used by tests to exercise the best-effort
+    failure path (runner.go:73-83) with real engines."""
+    out: Dict[str, tuple] = {}
+    for item in filter(None, (x.strip() for x in (spec or "").split(","))):
+        parts = item.rsplit(":", 2) if item.count(":") >= 2 else item.rsplit(":", 1)
+        if len(parts) == 3 and not parts[2].isdigit():
+            parts = [parts[0] + ":" + parts[1], parts[2]]
+        model, stage = parts[0], parts[1]
+        k = int(parts[2]) if len(parts) == 3 else 1
+        if stage not in ("init", "prefill", "decode"):
+            raise ValueError(f"LLMC_FAULT: unknown stage {stage!r} in {item!r}")
+        out[model] = (stage, k)
+    return out
+
+
+class InjectedFault(RuntimeError):
+    pass
+
+
 class _Req:
     __slots__ = ("rid", "ids", "params", "ctx")
 
@@ -32,8 +54,9 @@ class _Req:
 
 
 class _EngineHost:
-    def __init__(self, name: str, engine, send, leader: bool):
+    def __init__(self, name: str, engine, send, leader: bool, fault: Optional[tuple] = None):
         self.name = name
+        self.fault = fault
         self.engine = engine
         self.send = send
         self.leader = leader
@@ -118,13 +141,20 @@ class _EngineHost:
         from ..context import Context
 
         t0 = time.monotonic_ns()
+        stage, k = self.fault or ("", 0)
+        if stage in ("init", "prefill"):
+            raise InjectedFault(f"injected fault: {self.name} {stage}")
         self.engine.prefill(seqs, prompts)
         params = [SP(**r.params) for r in reqs]
         first = [0] * len(reqs)
+        sent = [0] * len(reqs)
 
         def on_tokens(i, ids):
             if not first[i]:
                 first[i] = time.monotonic_ns() - t0
+            if stage == "decode" and sent[i] + len(ids) >= k:
+                raise InjectedFault(f"injected fault: {self.name} decode after {k} tokens")
+            sent[i] += len(ids)
             self._emit("tokens", reqs[i].rid, ids)
 
         # a batch is cancelled only if every member is; single requests use their own context
@@ -189,6 +219,7 @@ def worker_main(gpu: int, conn, models: List[dict], dist_info: Optional[dict], t
                 if dist_info["rank"] in ranks:
                     groups[gname] = (g, ranks.index(dist_info["rank"]), len(ranks))
         hosts: Dict[str, _EngineHost] = {}
+        faults = parse_faults(os.environ.get("LLMC_FAULT", ""))
         for m in models:
             cfg = FAMILIES.get(m["family"])
             if cfg is None and m.get("checkpoint"):  # --weights-dir family (spawned: re-register)
@@ -205,7 +236,7 @@ def worker_main(gpu: int, conn, models: List[dict], dist_info: Optional[dict], t
                                 max_batch=m.get("max_batch", 1), max_seqs=m.get("max_seqs", 0), seed=m["seed"],
                                 use_graphs=tp.size == 1 or os.environ.get("LLMC_TP_GRAPHS") == "1")
             eng = Engine(cfg, ecfg, tp=tp, name=m["name"])
-            hosts[m["name"]] = _EngineHost(m["name"], eng, send, tp.is_leader)
+            hosts[m["name"]] = _EngineHost(m["name"], eng, send, tp.is_leader, faults.get(m["name"]))
         if not on_cpu:
             # capture all decode graphs now, while nothing else runs in this process
             for h in hosts.values():

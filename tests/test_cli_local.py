@@ -52,3 +52,31 @@ def test_cli_local_models_gpu(cuda, tmp_path):
     d = json.loads(out)
     assert len(d["responses"]) == 4 and all(len(r["content"]) > 0 for r in d["responses"])
     assert len(d["consensus"]) > 0
+
+
+def test_cli_fault_injection_best_effort_cpu():
+    """LLMC_FAULT: one local model fails mid-decode -> warning + failed_models, run succeeds
+    (runner.go:73-83 best-effort semantics with real engines)."""
+    rc, out, err = run_cli(["--models", "llama-tiny@1,phi3-tiny", "--judge", "llama-tiny@j", "--max-tokens", "12",
+                            "--json", "hi"], env={"LLMC_DEVICE": "cpu", "LLMC_FAULT": "phi3-tiny:decode:3"})
+    assert rc == 0, err
+    d = json.loads(out)
+    assert [r["model"] for r in d["responses"]] == ["llama-tiny@1"]
+    assert d["failed_models"] == ["phi3-tiny"]
+    assert any("injected fault" in w for w in d["warnings"])
+
+
+def test_cli_fault_all_models_fail_cpu():
+    rc, out, err = run_cli(["--models", "llama-tiny@1", "--judge", "llama-tiny@j", "--max-tokens", "4", "--json", "hi"],
+                           env={"LLMC_DEVICE": "cpu", "LLMC_FAULT": "llama-tiny@1:prefill"})
+    assert rc == 1
+    assert "all models failed" in err
+
+
+def test_parse_faults():
+    from llm_consensus_amd.runtime.worker import parse_faults
+
+    assert parse_faults("a@1:decode:3, b:init") == {"a@1": ("decode", 3), "b": ("init", 1)}
+    assert parse_faults("") == {}
+    with pytest.raises(ValueError):
+        parse_faults("a:boom")

@@ -213,3 +213,18 @@ def test_ui_rendering_tty_path():
     ui.print_summary(buf, 3, 2, 1, 1.25)
     assert buf.getvalue() == ("\n\033[2m─── Summary ───\033[0m\nModels queried: 3 (\033[32m2 succeeded\033[0m, "
                               "\033[31m1 failed\033[0m)\nTotal time: 1.2s\n")
+
+
+def test_model_registry_sync(tmp_path):
+    import subprocess
+
+    out = tmp_path / "models.json"
+    r = subprocess.run([sys.executable, "-m", "llm_consensus_amd.registry_sync", "-out", str(out), "-hf-cache=false",
+                        "-weights-dir", str(tmp_path / "missing")], capture_output=True, cwd=ROOT, timeout=120)
+    assert r.returncode == 0
+    recs = json.loads(out.read_text())
+    assert [(x["source"], x["id"]) for x in recs] == sorted((x["source"], x["id"]) for x in recs)
+    ids = {x["id"] for x in recs}
+    assert {"llama-3-8b", "llama-3-70b", "mixtral-8x7b", "phi-3-mini"} <= ids
+    assert all("raw" not in x for x in recs)
+    assert b"WARN: some sources failed:" in r.stderr and b"checkpoint:" in r.stderr

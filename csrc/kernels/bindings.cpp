@@ -7,8 +7,11 @@
 #include <hip/hip_runtime_api.h>
 #include <pybind11/pybind11.h>
 
+#include <pybind11/stl.h>
+
 #include <stdexcept>
 #include <string>
+#include <vector>
 
 namespace py = pybind11;
 typedef uintptr_t ptr;
@@ -37,6 +40,16 @@ int llmc_moe_gemm(const void*, int, const void*, const void*, const void*, const
 int llmc_moe_combine(const void*, const void*, const void*, void*, int, int, int, hipStream_t);
 int llmc_moe_gemv(int, const void*, int, const void*, float, const void*, const void*, int, void*, int, int, int, int,
                   hipStream_t);
+size_t llmc_car_sig_bytes();
+int llmc_car_alloc(size_t, void**);
+int llmc_car_free(void*);
+int llmc_ipc_handle(void*, void*);
+int llmc_ipc_handle_size();
+int llmc_ipc_open(const void*, void**);
+int llmc_ipc_close(void*);
+int llmc_car_timed_out(void*, int*);
+int llmc_car_allreduce(const void* const*, int, int, size_t, void*, size_t, hipStream_t);
+int llmc_car_allgather(const void* const*, int, int, size_t, const void*, void*, size_t, hipStream_t);
 }
 
 static inline void check(int rc, const char* what) {
@@ -121,4 +134,42 @@ PYBIND11_MODULE(_llmc_hip, m) {
     check(llmc_moe_gemv(k, P(x), xs, P(nw), eps, P(W), P(ids), ids_stride, P(out), os, N, K, epi, S(s)), "moe_gemv");
   });
   m.def("device_synchronize", []() { check(static_cast<int>(hipDeviceSynchronize()), "hipDeviceSynchronize"); });
+  // ---- K13 custom all-reduce / all-gather over IPC peer buffers ----
+  m.def("car_sig_bytes", []() { return llmc_car_sig_bytes(); });
+  m.def("car_alloc", [](size_t cap) {
+    void* p = nullptr;
+    check(llmc_car_alloc(cap, &p), "car_alloc");
+    return reinterpret_cast<ptr>(p);
+  });
+  m.def("car_free", [](ptr p) { check(llmc_car_free(P(p)), "car_free"); });
+  m.def("ipc_handle", [](ptr p) {
+    std::string h(static_cast<size_t>(llmc_ipc_handle_size()), '\0');
+    check(llmc_ipc_handle(P(p), h.data()), "ipc_handle");
+    return py::bytes(h);
+  });
+  m.def("ipc_open", [](py::bytes h) {
+    std::string s = h;
+    if (static_cast<int>(s.size()) != llmc_ipc_handle_size()) throw std::runtime_error("ipc_open: bad handle size");
+    void* p = nullptr;
+    check(llmc_ipc_open(s.data(), &p), "ipc_open");
+    return reinterpret_cast<ptr>(p);
+  });
+  m.def("ipc_close", [](ptr p) { check(llmc_ipc_close(P(p)), "ipc_close"); });
+  m.def("car_timed_out", [](ptr own) {
+    int v = 0;
+    check(llmc_car_timed_out(P(own), &v), "car_timed_out");
+    return v;
+  });
+  m.def("car_allreduce", [](const std::vector<ptr>& bases, int rank, int world, size_t cap, ptr x, size_t nbytes,
+                            ptr s) {
+    std::vector<const void*> b(bases.size());
+    for (size_t i = 0; i < bases.size(); ++i) b[i] = P(bases[i]);
+    check(llmc_car_allreduce(b.data(), rank, world, cap, P(x), nbytes, S(s)), "car_allreduce");
+  });
+  m.def("car_allgather", [](const std::vector<ptr>& bases, int rank, int world, size_t cap, ptr x, ptr out,
+                            size_t nbytes, ptr s) {
+    std::vector<const void*> b(bases.size());
+    for (size_t i = 0; i < bases.size(); ++i) b[i] = P(bases[i]);
+    check(llmc_car_allgather(b.data(), rank, world, cap, P(x), P(out), nbytes, S(s)), "car_allgather");
+  });
 }

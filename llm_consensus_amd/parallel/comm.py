@@ -5,6 +5,11 @@ xGMI on ROCm, "gloo" for CPU tests). The row-parallel reductions use the *residu
 trick: rank 0 adds its partial product onto the residual stream, the other ranks write their
 partial product into the same buffer, and ONE in-place all-reduce yields
 ``h + sum_r partial_r`` — no separate residual-add kernel and no extra buffer per layer.
+
+On GPUs the decode-sized collectives go through the custom one-shot xGMI kernels
+(``custom_ar.py``, K13) once ``enable_custom()`` has mapped the peers: no RCCL call and no host
+work per collective, so a TP engine's decode step is capturable in one HIP graph. Larger messages
+(prefill) and CPU/gloo groups use torch.distributed.
 """
 
 from __future__ import annotations
@@ -22,6 +27,16 @@ class TPGroup:
         self.group = group
         self.rank = rank
         self.size = size
+        self.custom = None  # CustomAllReduce once enable_custom() ran
+
+    def enable_custom(self, device, cap: Optional[int] = None) -> bool:
+        """Map the group's IPC buffers for the custom collectives (GPU groups of 2..8 ranks)."""
+        if self.size == 1 or self.custom is not None:
+            return self.custom is not None
+        from .custom_ar import DEFAULT_CAP, CustomAllReduce
+
+        self.custom = CustomAllReduce(self.group, self.rank, self.size, device, cap or DEFAULT_CAP)
+        return True
 
     @staticmethod
     def single() -> "TPGroup":
@@ -37,6 +52,9 @@ class TPGroup:
 
     def all_reduce_(self, t: torch.Tensor) -> torch.Tensor:
         if self.size > 1:
+            c = self.custom
+            if c is not None and t.is_cuda and t.dtype == torch.bfloat16 and t.is_contiguous() and c.fits(t.numel() * 2):
+                return c.all_reduce_(t)
             dist.all_reduce(t, group=self.group)
         return t
 
@@ -45,6 +63,10 @@ class TPGroup:
         if self.size == 1:
             out.view_as(t).copy_(t)
             return out
+        c = self.custom
+        nbytes = t.numel() * t.element_size()
+        if c is not None and t.is_cuda and t.is_contiguous() and out.is_contiguous() and c.fits(nbytes):
+            return c.all_gather(t, out)
         flat = out.view(self.size * t.shape[0], *t.shape[1:])  # gloo wants dim-0 concatenation
         dist.all_gather_into_tensor(flat, t.contiguous(), group=self.group)
         return out

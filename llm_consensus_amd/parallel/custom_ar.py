@@ -1,0 +1,83 @@
+"""K13: custom one-shot all-reduce / all-gather for decode-sized TP collectives.
+
+Each rank allocates one uncached device buffer (signals + two data parities, see
+``csrc/kernels/allreduce.hip``), exports it with hipIpc, and maps every peer's buffer; the
+collective is then ONE kernel that stages the local slice, signals each peer over xGMI, waits
+for theirs (bounded spin) and reads every peer's copy directly. No host involvement per call, so
+it is capturable in the decode HIP graph (RCCL is used for bootstrap and for messages larger
+than the buffer).
+"""
+
+from __future__ import annotations
+
+from typing import List, Optional
+
+import torch
+
+from ..utils.native import kernels
+
+DEFAULT_CAP = 1 << 20  # bytes per parity: [4, 8192] bf16 hidden = 64 KiB; logits gather [4, 32064] f32 = 512 KiB
+
+
+class CustomAllReduce:
+    def __init__(self, group, rank: int, world: int, device: torch.device, cap: int = DEFAULT_CAP):
+        import torch.distributed as dist
+
+        if world > 8:
+            raise ValueError("custom all-reduce supports up to 8 ranks (one xGMI hop)")
+        self.rank, self.world, self.cap = rank, world, int(cap)
+        self.device = torch.device(device)
+        k = kernels()
+        with torch.cuda.device(self.device):
+            self.own = k.car_alloc(self.cap)
+            handle = k.ipc_handle(self.own)
+        handles: List[Optional[bytes]] = [None] * world
+        dist.all_gather_object(handles, handle, group=group)
+        self.bases: List[int] = []
+        self._opened: List[int] = []
+        with torch.cuda.device(self.device):
+            for r, h in enumerate(handles):
+                if r == rank:
+                    self.bases.append(self.own)
+                else:
+                    p = k.ipc_open(h)
+                    self.bases.append(p)
+                    self._opened.append(p)
+        dist.barrier(group=group)
+
+    def fits(self, nbytes: int) -> bool:
+        return nbytes % 16 == 0 and nbytes <= self.cap
+
+    def all_reduce_(self, t: torch.Tensor) -> torch.Tensor:
+        """In-place bf16 sum over the group (f32 accumulation in rank order: every rank gets the
+        same bits)."""
+        if t.dtype != torch.bfloat16 or not t.is_contiguous():
+            raise TypeError("custom all-reduce: contiguous bf16 only")
+        nbytes = t.numel() * 2
+        kernels().car_allreduce(self.bases, self.rank, self.world, self.cap, t.data_ptr(), nbytes,
+                                torch.cuda.current_stream(t.device).cuda_stream)
+        return t
+
+    def all_gather(self, x: torch.Tensor, out: torch.Tensor) -> torch.Tensor:
+        """out.view(world, -1)[r] = x of rank r (any dtype; x contiguous)."""
+        nbytes = x.numel() * x.element_size()
+        if out.numel() * out.element_size() != nbytes * self.world:
+            raise ValueError("custom all-gather: out must hold world * x")
+        kernels().car_allgather(self.bases, self.rank, self.world, self.cap, x.data_ptr(), out.data_ptr(), nbytes,
+                                torch.cuda.current_stream(x.device).cuda_stream)
+        return out
+
+    def timed_out(self) -> bool:
+        return bool(kernels().car_timed_out(self.own))
+
+    def close(self) -> None:
+        k = kernels()
+        for p in self._opened:
+            try:
+                k.ipc_close(p)
+            except Exception:  # noqa: BLE001
+                pass
+        self._opened = []
+        if self.own:
+            k.car_free(self.own)
+            self.own = 0

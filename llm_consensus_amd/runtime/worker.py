@@ -230,11 +230,15 @@ def worker_main(gpu: int, conn, models: List[dict], dist_info: Optional[dict], t
             if m["name"] in groups:
                 g, r, n = groups[m["name"]]
                 tp = TPGroup(g, r, n)
+                if not on_cpu and os.environ.get("LLMC_CUSTOM_AR", "1") != "0":
+                    tp.enable_custom(f"cuda:{gpu}")  # collective over the group: same order on every rank
             else:
                 tp = TPGroup.single()
+            # TP decode is graph-captured when its collectives are the custom xGMI kernels
+            graphs = tp.size == 1 or tp.custom is not None or os.environ.get("LLMC_TP_GRAPHS") == "1"
             ecfg = EngineConfig(device="cpu" if on_cpu else f"cuda:{gpu}", max_context=m["max_context"],
                                 max_batch=m.get("max_batch", 1), max_seqs=m.get("max_seqs", 0), seed=m["seed"],
-                                use_graphs=tp.size == 1 or os.environ.get("LLMC_TP_GRAPHS") == "1")
+                                use_graphs=graphs)
             eng = Engine(cfg, ecfg, tp=tp, name=m["name"])
             hosts[m["name"]] = _EngineHost(m["name"], eng, send, tp.is_leader, faults.get(m["name"]))
         if not on_cpu:

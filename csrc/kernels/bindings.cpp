@@ -40,6 +40,7 @@ int llmc_moe_gemm(const void*, int, const void*, const void*, const void*, const
 int llmc_moe_combine(const void*, const void*, const void*, void*, int, int, int, hipStream_t);
 int llmc_moe_gemv(int, const void*, int, const void*, float, const void*, const void*, int, void*, int, int, int, int,
                   hipStream_t);
+int llmc_gemv_sweep(int, const void*, const void*, const void*, void*, int, int, hipStream_t);
 size_t llmc_car_sig_bytes();
 int llmc_car_alloc(size_t, void**);
 int llmc_car_free(void*);
@@ -171,5 +172,8 @@ PYBIND11_MODULE(_llmc_hip, m) {
     std::vector<const void*> b(bases.size());
     for (size_t i = 0; i < bases.size(); ++i) b[i] = P(bases[i]);
     check(llmc_car_allgather(b.data(), rank, world, cap, P(x), P(out), nbytes, S(s)), "car_allgather");
+  });
+  m.def("gemv_sweep", [](int v, ptr x, ptr nw, ptr W, ptr out, int N, int K, ptr s) {
+    check(llmc_gemv_sweep(v, P(x), P(nw), P(W), P(out), N, K, S(s)), "gemv_sweep");
   });
 }

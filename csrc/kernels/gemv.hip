@@ -1,11 +1,11 @@
 // Launchers for the decode GEMV (kernel body: gemv_core.h).
 //
-// Geometry per shape (measured on MI355X, profiles/): a batch-1 decode GEMV is a few-µs kernel,
-// so the grid must be a balanced multiple of the 256 CUs with enough waves in flight per CU:
-//   N >= 16384 (gate_up, lm_head):        256 threads x 4 rows/wave  (1792 / 8016 blocks)
-//   paired epilogues (SiLU, RoPE):        256 threads x 2 rows/wave  (qkv 6144 -> 768 blocks)
-//   K > 8192 (down_proj, K = 14336):      512 threads x 1 row/wave   (N 4096 -> 512 blocks)
-//   otherwise (o_proj):                   256 threads x 1 row/wave   (N 4096 -> 1024 blocks)
+// Geometry (cold-weight sweep on MI355X, scripts/microbench_kernels.py sweep,
+// profiles/r1_gemv_geometry_sweep.md): 1024-thread blocks (16 waves), one row per wave, 4 x 16 B
+// loads per lane in flight (+ the next batch prefetched) were fastest on every Llama-3-8B shape:
+// fewer, fatter blocks stage/normalise x once per 16 rows instead of once per 4, and keep 16
+// waves per CU streaming. Paired epilogues (SiLU gate/up, RoPE) meet their partner row of the
+// next wave through LDS (PAIR_LDS); shapes that do not tile by 32 rows keep 256 x 2 rows/wave.
 #include "gemv_core.h"
 
 namespace llmc {
@@ -13,10 +13,11 @@ namespace llmc {
 template <int M, int NT, int RPW, int PRO, int EPI>
 static int launch_gemv_g(const void* x, int x_stride, const void* nw, float eps, const void* W, void* out,
                          int out_stride, int N, int K, const RopeEpi& rope, hipStream_t s) {
-  constexpr int UNROLL = RPW == 1 ? (M <= 2 ? 8 : 4) : (RPW == 2 ? 4 : (M <= 2 ? 4 : 2));
+  constexpr int UNROLL = RPW == 1 ? 4 : (RPW == 2 ? 4 : (M <= 2 ? 4 : 2));
   constexpr int WAVES = NT / kWave;
   auto kern = gemv_kernel<M, NT, RPW, UNROLL, PRO, EPI, false>;
-  const size_t lds = static_cast<size_t>(M) * K * sizeof(bf16_t) + M * WAVES * sizeof(float);
+  // x [M][K] bf16 | norm partials [M][WAVES] f32 | pair exchange [WAVES/2][M] f32
+  const size_t lds = static_cast<size_t>(M) * K * sizeof(bf16_t) + 2 * M * WAVES * sizeof(float);
   if (lds > 160 * 1024) return -2;
   static bool attr_set = false;
   if (lds > 64 * 1024 && !attr_set) {
@@ -34,13 +35,11 @@ static int launch_gemv_g(const void* x, int x_stride, const void* nw, float eps,
 template <int M, int PRO, int EPI>
 static int launch_gemv(const void* x, int x_stride, const void* nw, float eps, const void* W, void* out,
                        int out_stride, int N, int K, const RopeEpi& rope, hipStream_t s) {
-  if (N >= 16384) return launch_gemv_g<M, 256, 4, PRO, EPI>(x, x_stride, nw, eps, W, out, out_stride, N, K, rope, s);
   if constexpr (EPI == EPI_SILU || EPI == EPI_ROPE) {
-    return launch_gemv_g<M, 256, 2, PRO, EPI>(x, x_stride, nw, eps, W, out, out_stride, N, K, rope, s);
-  } else {
-    if (K > 8192) return launch_gemv_g<M, 512, 1, PRO, EPI>(x, x_stride, nw, eps, W, out, out_stride, N, K, rope, s);
-    return launch_gemv_g<M, 256, 1, PRO, EPI>(x, x_stride, nw, eps, W, out, out_stride, N, K, rope, s);
+    if (N % 32 != 0)  // the 16-wave pair exchange needs whole 32-row blocks
+      return launch_gemv_g<M, 256, 2, PRO, EPI>(x, x_stride, nw, eps, W, out, out_stride, N, K, rope, s);
   }
+  return launch_gemv_g<M, 1024, 1, PRO, EPI>(x, x_stride, nw, eps, W, out, out_stride, N, K, rope, s);
 }
 
 template <int PRO, int EPI>
@@ -121,4 +120,44 @@ extern "C" int llmc_moe_gemv(int npairs, const void* x, int x_stride, const void
   }
 #undef LLMC_MOEGV
   return static_cast<int>(hipGetLastError());
+}
+
+// ---- geometry sweep entry (microbenchmarks only: M = 1, fused norm, bf16 out) ----
+namespace llmc {
+template <int NT, int RPW, int UNROLL>
+static int launch_sweep(const void* x, const void* nw, const void* W, void* out, int N, int K, hipStream_t s) {
+  constexpr int WAVES = NT / kWave;
+  const size_t lds = static_cast<size_t>(K) * sizeof(bf16_t) + WAVES * sizeof(float);
+  const int grid = (N + WAVES * RPW - 1) / (WAVES * RPW);
+  gemv_kernel<1, NT, RPW, UNROLL, PRO_NORM, EPI_BF16, false><<<grid, NT, lds, s>>>(
+      (const bf16_t*)x, K, (const bf16_t*)nw, 1e-5f, (const bf16_t*)W, out, N, N, K, nullptr, 1, RopeEpi{});
+  return static_cast<int>(hipGetLastError());
+}
+}  // namespace llmc
+
+extern "C" int llmc_gemv_sweep(int variant, const void* x, const void* nw, const void* W, void* out, int N, int K,
+                               hipStream_t s) {
+  if (K % 8 != 0 || K * 2 > 64 * 1024) return -1;
+  switch (variant) {
+    case 0: return launch_sweep<256, 1, 8>(x, nw, W, out, N, K, s);
+    case 1: return launch_sweep<256, 2, 4>(x, nw, W, out, N, K, s);
+    case 2: return launch_sweep<256, 4, 4>(x, nw, W, out, N, K, s);
+    case 3: return launch_sweep<512, 1, 8>(x, nw, W, out, N, K, s);
+    case 4: return launch_sweep<512, 2, 4>(x, nw, W, out, N, K, s);
+    case 5: return launch_sweep<128, 1, 8>(x, nw, W, out, N, K, s);
+    case 6: return launch_sweep<64, 1, 8>(x, nw, W, out, N, K, s);
+    case 7: return launch_sweep<1024, 1, 4>(x, nw, W, out, N, K, s);
+    case 8: return launch_sweep<256, 1, 4>(x, nw, W, out, N, K, s);
+    case 9: return launch_sweep<256, 2, 8>(x, nw, W, out, N, K, s);
+    case 10: return launch_sweep<512, 4, 2>(x, nw, W, out, N, K, s);
+    case 11: return launch_sweep<128, 2, 4>(x, nw, W, out, N, K, s);
+    case 12: return launch_sweep<1024, 1, 8>(x, nw, W, out, N, K, s);
+    case 13: return launch_sweep<1024, 2, 4>(x, nw, W, out, N, K, s);
+    case 14: return launch_sweep<1024, 2, 2>(x, nw, W, out, N, K, s);
+    case 15: return launch_sweep<1024, 1, 2>(x, nw, W, out, N, K, s);
+    case 16: return launch_sweep<768, 1, 4>(x, nw, W, out, N, K, s);
+    case 17: return launch_sweep<1024, 4, 2>(x, nw, W, out, N, K, s);
+    case 18: return launch_sweep<1024, 1, 6>(x, nw, W, out, N, K, s);
+    default: return -2;
+  }
 }

@@ -44,6 +44,7 @@ __global__ __launch_bounds__(NT) void gemv_kernel(const bf16_t* __restrict__ x, 
                                                   int out_stride, int N, int K, const int32_t* __restrict__ expert_ids,
                                                   int x_div, RopeEpi rope) {
   constexpr int WAVES = NT / kWave;
+  constexpr bool PAIR_LDS = (EPI == EPI_SILU || EPI == EPI_ROPE) && RPW == 1;  // host: N % (2 * WAVES) == 0
   // EXPERT (MoE decode): blockIdx.y = (token, slot) pair; weights of expert expert_ids[pair],
   // input row pair / x_div, output row pair (M must be 1).
   if constexpr (EXPERT) {
@@ -132,7 +133,23 @@ __global__ __launch_bounds__(NT) void gemv_kernel(const bf16_t* __restrict__ x, 
     }
   }
   __syncthreads();
-  if (row0 >= N) return;
+  if (!PAIR_LDS && row0 >= N) return;  // PAIR_LDS blocks are full (host), all waves reach its barrier
+
+  // RoPE epilogue operands (PAIR_LDS: one row per even wave) issued now, landing under the stream
+  float pre_c = 1.f, pre_s = 0.f;
+  int pre_slot = -1;
+  if constexpr (PAIR_LDS && EPI == EPI_ROPE) {
+    if (!(wave & 1) && lane < M && row0 < N) {
+      const int D = rope.D, half = D / 2;
+      pre_slot = rope.slots[lane];
+      if (row0 / D < rope.nh + rope.nkv) {
+        const int i = (row0 % D) / 2;
+        const int pos = rope.positions[lane];
+        pre_c = rope.cos_t[static_cast<int64_t>(pos) * half + i];
+        pre_s = rope.sin_t[static_cast<int64_t>(pos) * half + i];
+      }
+    }
+  }
 
   // ---- main loop: RPW weight rows per wave, one UNROLL-batch ahead ----
   float acc[RPW][M];
@@ -173,7 +190,65 @@ __global__ __launch_bounds__(NT) void gemv_kernel(const bf16_t* __restrict__ x, 
 #pragma unroll
     for (int m = 0; m < M; ++m) acc[r][m] = wave_sum(acc[r][m]);
 
-  // ---- epilogue: lane (r*M + m) stores one value ----
+  // ---- epilogue ----
+  // paired epilogues (SiLU, RoPE) combine rows (2j, 2j + 1): the same wave holds both when
+  // RPW >= 2; with RPW == 1 they sit in waves (w, w + 1) and meet through LDS (PAIR_LDS).
+  // RoPE operands of (row n, token m): cos/sin of the pair's frequency and the KV slot
+  auto rope_ops = [&](int n, int m, float& c, float& sn, int& slot) {
+    const int D = rope.D, half = D / 2;
+    slot = rope.slots[m];
+    c = 1.f;
+    sn = 0.f;
+    if (n / D < rope.nh + rope.nkv) {
+      const int i = (n % D) / 2;
+      const int pos = rope.positions[m];
+      c = rope.cos_t[static_cast<int64_t>(pos) * half + i];
+      sn = rope.sin_t[static_cast<int64_t>(pos) * half + i];
+    }
+  };
+  auto pair_epi = [&](int n, int m, float v, float x2, float c, float sn, int slot) {
+    if constexpr (EPI == EPI_SILU) {  // rows (2j, 2j+1) = (gate, up) -> output column n/2
+      reinterpret_cast<bf16_t*>(out)[static_cast<int64_t>(m) * out_stride + n / 2] = f32_to_bf16(silu(v) * x2);
+    } else if constexpr (EPI == EPI_ROPE) {  // rows (2j, 2j+1) of a Q/K head = dims (i, i + D/2)
+      const int D = rope.D, half = D / 2;
+      const int head = n / D;
+      const int64_t page = slot >= 0 ? slot / rope.bs : 0;
+      const int off = slot >= 0 ? slot % rope.bs : 0;
+      if (head < rope.nh + rope.nkv) {
+        const int i = (n % D) / 2;
+        const float o1 = v * c - x2 * sn, o2 = x2 * c + v * sn;
+        if (head < rope.nh) {
+          bf16_t* qo = rope.q_out + static_cast<int64_t>(m) * rope.q_stride + head * D;
+          qo[i] = f32_to_bf16(o1);
+          qo[i + half] = f32_to_bf16(o2);
+        } else if (slot >= 0) {
+          bf16_t* ko = rope.k_cache + ((page * rope.nkv + (head - rope.nh)) * rope.bs + off) * D;
+          ko[i] = f32_to_bf16(o1);
+          ko[i + half] = f32_to_bf16(o2);
+        }
+      } else if (slot >= 0) {  // V rows keep canonical order
+        const int vh = head - rope.nh - rope.nkv, d = n % D;
+        bf16_t* vv = rope.v_cache + ((page * rope.nkv + vh) * rope.bs + off) * D;
+        vv[d] = f32_to_bf16(v);
+        vv[d + 1] = f32_to_bf16(x2);
+      }
+    }
+  };
+  if constexpr (PAIR_LDS) {
+    float* pairx = reinterpret_cast<float*>(smem + static_cast<size_t>(M) * K * sizeof(bf16_t)) + M * WAVES;
+    if ((wave & 1) && lane < M) {
+#pragma unroll
+      for (int m = 0; m < M; ++m)
+        if (lane == m) pairx[(wave >> 1) * M + m] = acc[0][m];
+    }
+    __syncthreads();
+    if (!(wave & 1)) {
+#pragma unroll
+      for (int m = 0; m < M; ++m)
+        if (lane == m && row0 < N) pair_epi(row0, m, acc[0][m], pairx[(wave >> 1) * M + m], pre_c, pre_s, pre_slot);
+    }
+    return;
+  }
 #pragma unroll
   for (int r = 0; r < RPW; ++r) {
 #pragma unroll
@@ -188,39 +263,13 @@ __global__ __launch_bounds__(NT) void gemv_kernel(const bf16_t* __restrict__ x, 
       } else if constexpr (EPI == EPI_RESADD) {
         bf16_t* h = reinterpret_cast<bf16_t*>(out) + static_cast<int64_t>(m) * out_stride + n;
         *h = f32_to_bf16(bf16_to_f32(*h) + v);
-      } else if constexpr (EPI == EPI_SILU) {  // rows (2j, 2j+1) = (gate, up) -> output column n/2
-        if ((r & 1) == 0) {
-          reinterpret_cast<bf16_t*>(out)[static_cast<int64_t>(m) * out_stride + n / 2] =
-              f32_to_bf16(silu(v) * acc[r + 1][m]);
-        }
-      } else {  // EPI_ROPE: rows (2j, 2j+1) of a Q/K head = dims (i, i + D/2), i = (n % D) / 2
-        if ((r & 1) == 0) {
-          const int D = rope.D, half = D / 2;
-          const int head = n / D;
-          const int slot = rope.slots[m];
-          const int64_t page = slot >= 0 ? slot / rope.bs : 0;
-          const int off = slot >= 0 ? slot % rope.bs : 0;
-          const float x2 = acc[r + 1][m];
-          if (head < rope.nh + rope.nkv) {
-            const int i = (n % D) / 2;
-            const int pos = rope.positions[m];
-            const float c = rope.cos_t[static_cast<int64_t>(pos) * half + i];
-            const float s = rope.sin_t[static_cast<int64_t>(pos) * half + i];
-            const float o1 = v * c - x2 * s, o2 = x2 * c + v * s;
-            if (head < rope.nh) {
-              bf16_t* q = rope.q_out + static_cast<int64_t>(m) * rope.q_stride + head * D;
-              q[i] = f32_to_bf16(o1);
-              q[i + half] = f32_to_bf16(o2);
-            } else if (slot >= 0) {
-              bf16_t* k = rope.k_cache + ((page * rope.nkv + (head - rope.nh)) * rope.bs + off) * D;
-              k[i] = f32_to_bf16(o1);
-              k[i + half] = f32_to_bf16(o2);
-            }
-          } else if (slot >= 0) {  // V rows keep canonical order
-            const int vh = head - rope.nh - rope.nkv, d = n % D;
-            bf16_t* vv = rope.v_cache + ((page * rope.nkv + vh) * rope.bs + off) * D;
-            vv[d] = f32_to_bf16(v);
-            vv[d + 1] = f32_to_bf16(x2);
+      } else {
+        if constexpr (RPW >= 2) {
+          if ((r & 1) == 0) {
+            float c = 1.f, sn = 0.f;
+            int slot = -1;
+            if constexpr (EPI == EPI_ROPE) rope_ops(n, m, c, sn, slot);
+            pair_epi(n, m, v, acc[r + 1][m], c, sn, slot);
           }
         }
       }

@@ -101,6 +101,41 @@ def bench_mall():
               f"flush+read(W2)+gemv {t_other:.1f} -> gemv saving from prior read {t_other - t_pre:.2f} us")
 
 
+SWEEP = ["256x1u8", "256x2u4", "256x4u4", "512x1u8", "512x2u4", "128x1u8", "64x1u8", "1024x1u4", "256x1u4",
+         "256x2u8", "512x4u2", "128x2u4", "1024x1u8", "1024x2u4", "1024x2u2", "1024x1u2", "768x1u4", "1024x4u2", "1024x1u6"]
+
+
+def bench_gemv_sweep():
+    """GEMV geometry sweep on COLD weights: the graph cycles through enough copies of W to exceed
+    the 256 MB MALL, as in a real decode step (16 GB streamed per token)."""
+    from llm_consensus_amd.utils.native import kernels
+
+    k = kernels()
+    for (N, K) in [(6144, 4096), (4096, 4096), (28672, 4096), (4096, 14336), (128256, 4096)]:
+        if K * 2 > 64 * 1024:
+            continue
+        copies = max(2, (1 << 30) // (N * K * 2))
+        Ws = [(torch.randn(N, K, device="cuda") * 0.02).to(BF) for _ in range(copies)]
+        x = torch.randn(1, K, device="cuda").to(BF)
+        nw = torch.ones(K, dtype=BF, device="cuda")
+        out = torch.zeros(1, N, dtype=BF, device="cuda")
+        res = []
+        for v, name in enumerate(SWEEP):
+            if name not in ("256x4u4", "256x2u4", "512x1u8", "1024x1u4", "1024x1u6", "1024x1u8"):
+                continue
+            st = torch.cuda.current_stream().cuda_stream
+
+            def run():
+                for W in Ws:
+                    k.gemv_sweep(v, x.data_ptr(), nw.data_ptr(), W.data_ptr(), out.data_ptr(), N, K,
+                                 torch.cuda.current_stream().cuda_stream)
+            us = timeit(run, iters=2, warm=1) / copies
+            res.append(f"{name} {us:6.2f}")
+        del Ws
+        torch.cuda.empty_cache()
+        print(f"sweep N={N} K={K} ({N * K * 2 / 1e6:.0f} MB, {copies} copies): " + "  ".join(res), flush=True)
+
+
 def bench_launch():
     x = torch.zeros(1, 4096, dtype=BF, device="cuda")
     w = torch.ones(4096, dtype=BF, device="cuda")
@@ -118,3 +153,5 @@ if __name__ == "__main__":
         bench_gemv()
     if what in ("mall",):
         bench_mall()
+    if what in ("sweep",):
+        bench_gemv_sweep()

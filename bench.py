@@ -25,6 +25,7 @@ import json
 import os
 import statistics
 import sys
+import threading
 import time
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
@@ -103,6 +104,13 @@ def main() -> None:
         judge = Engine(jcfg, EngineConfig(device=dev, max_context=judge_ctx, seed=777,
                                           steps_per_graph=args.steps_per_graph, use_graphs=not args.no_graphs),
                        name=f"{args.judge}@judge")
+    # capture every decode graph up front (a capture beside another engine's running stream is
+    # invalid; the worker process does the same before serving)
+    if not args.no_graphs:
+        for _, e in responders:
+            e.warmup_graphs()
+        if judge is not None:
+            judge.warmup_graphs()
     torch.cuda.synchronize()
     log(f"engines ready in {time.time() - t0:.1f}s (responders {mpg}/gpu, judge ctx {judge_ctx})")
 
@@ -114,11 +122,23 @@ def main() -> None:
         if judge is not None:
             jseq = judge.new_sequence()
             judge.prefill([jseq], [jtok.encode(prompt_header(prompt_text), add_bos=True)], want_logits=False)
-        outs = []
-        for idx, e in responders:
-            ids = e.generate_ids(prompt_ids, args.max_tokens, temperature=args.temperature,
-                                 seed=1000 * step + idx + 1, stop_on_eos=False)
-            outs.append(ids)
+        # co-located responders decode concurrently, one engine thread + hipStream each (as the
+        # CLI's worker runs them)
+        outs = [None] * len(responders)
+
+        def run_one(j):
+            idx, e = responders[j]
+            outs[j] = e.generate_ids(prompt_ids, args.max_tokens, temperature=args.temperature,
+                                     seed=1000 * step + idx + 1, stop_on_eos=False)
+
+        if len(responders) == 1:
+            run_one(0)
+        else:
+            ths = [threading.Thread(target=run_one, args=(j,)) for j in range(len(responders))]
+            for t in ths:
+                t.start()
+            for t in ths:
+                t.join()
         t_resp = time.perf_counter()
         # gather responses to rank 0 (fixed-size int32 rows; RCCL over xGMI)
         local_t = torch.full((mpg, args.max_tokens), -1, dtype=torch.int32, device=dev)

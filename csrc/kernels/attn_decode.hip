@@ -189,9 +189,10 @@ __global__ __launch_bounds__(256) void attn_decode_kernel(
 }
 
 // grid (nkv * G, B, ceil(D / 64)), 256 threads: one query head x 64 dims per block; the 256
-// threads are 64 dims x 4 chunk groups, so each thread reads only nchunks/4 partials (one batch
-// of in-flight loads for ~64 chunks) and the chunk groups meet in LDS. Parallel over heads and
-// dim slices so a 33k-token context (hundreds of chunks) reduces in ~two memory round trips.
+// threads are 64 dims x 4 chunk groups. ONE memory round trip for up to 64 chunks: every thread
+// issues its (up to 16) partial-value loads and the block its m / l loads together — the values
+// do not depend on the softmax max — then the max, the scale factors and the weighted sums are
+// formed from registers and LDS; chunk groups meet in LDS.
 template <int G>
 __global__ __launch_bounds__(256) void attn_decode_reduce_kernel(const float* __restrict__ part,
                                                                  const int32_t* __restrict__ seq_lens,
@@ -199,63 +200,68 @@ __global__ __launch_bounds__(256) void attn_decode_reduce_kernel(const float* __
                                                                  int D, int chunk_arg, int gc, int max_chunks) {
   const int kvh = blockIdx.x / G, g = blockIdx.x % G, b = blockIdx.y;
   const int L = seq_lens[b];
-  const int chunk = decode_chunk(L, gc, chunk_arg);
-  const int nchunks = (L + chunk - 1) / chunk;
+  const int nchunks = decode_nsplit(L, gc, chunk_arg);
   if (nchunks <= 1) return;
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  float* sc = reinterpret_cast<float*>(smem);  // [nchunks]
-  float* red = sc + max_chunks;                // [4][64] + 8 scratch
+  float* sc = reinterpret_cast<float*>(smem);  // [max_chunks]: m, then exp(m - M)
+  float* lv = sc + max_chunks;                 // [max_chunks]: l
+  float* red = lv + max_chunks;                // [4][64] + 8 scratch
   const int tid = threadIdx.x, stride = D + 2;
   const float* pb = part + ((static_cast<int64_t>(b) * nkv + kvh) * max_chunks * G + g) * stride;
   const int64_t cstride = static_cast<int64_t>(G) * stride;  // between consecutive chunks
-  // phase 1: m_c into LDS, block max
+  const int dl = tid & 63, cg = tid >> 6;
+  const int d = blockIdx.z * 64 + dl;
+  const bool live = d < D;
+  // issue: this thread's first 16 partial values (chunks cg, cg + 4, ...) and the m / l words
+  float v[16];
+#pragma unroll
+  for (int j = 0; j < 16; ++j) {
+    const int c = min(cg + 4 * j, nchunks - 1);  // clamped: all loads in flight, masked below
+    v[j] = live ? pb[c * cstride + d] : 0.f;
+  }
   float mx = kNegBig;
   for (int c = tid; c < nchunks; c += 256) {
     const float m = pb[c * cstride + D];
     sc[c] = m;
+    lv[c] = pb[c * cstride + D + 1];
     mx = fmaxf(mx, m);
   }
   mx = wave_max(mx);
   if ((tid & 63) == 0) red[256 + tid / 64] = mx;
   __syncthreads();
   mx = fmaxf(fmaxf(red[256], red[257]), fmaxf(red[258], red[259]));
-  // phase 2: scale factors and the normaliser
   float ls = 0.f;
   for (int c = tid; c < nchunks; c += 256) {
     const float e = __expf(sc[c] - mx);
     sc[c] = e;
-    ls += pb[c * cstride + D + 1] * e;
+    ls += lv[c] * e;
   }
   ls = wave_sum(ls);
-  __syncthreads();
   if ((tid & 63) == 0) red[260 + tid / 64] = ls;
   __syncthreads();
   const float lsum = red[260] + red[261] + red[262] + red[263];
-  // phase 3: weighted sum of the chunk outputs, 4 chunk groups in parallel
-  const int dl = tid & 63, cg = tid >> 6;
-  const int d = blockIdx.z * 64 + dl;
   float o = 0.f;
-  if (d < D) {
-    for (int c0 = cg; c0 < nchunks; c0 += 4 * 16) {
-      float v[16];
 #pragma unroll
-      for (int j = 0; j < 16; ++j) {
-        const int c = min(c0 + 4 * j, nchunks - 1);  // clamped: all 16 loads in flight
-        v[j] = pb[c * cstride + d];
-      }
+  for (int j = 0; j < 16; ++j) o += (cg + 4 * j < nchunks) ? v[j] * sc[cg + 4 * j] : 0.f;
+  for (int c0 = cg + 64; c0 < nchunks; c0 += 64) {  // > 64 chunks: further batches
+    float w[16];
 #pragma unroll
-      for (int j = 0; j < 16; ++j) o += (c0 + 4 * j < nchunks) ? v[j] * sc[c0 + 4 * j] : 0.f;
+    for (int j = 0; j < 16; ++j) {
+      const int c = min(c0 + 4 * j, nchunks - 1);
+      w[j] = live ? pb[c * cstride + d] : 0.f;
     }
+#pragma unroll
+    for (int j = 0; j < 16; ++j) o += (c0 + 4 * j < nchunks) ? w[j] * sc[c0 + 4 * j] : 0.f;
   }
   red[cg * 64 + dl] = o;
   __syncthreads();
-  if (cg == 0 && d < D) {
+  if (cg == 0 && live) {
     const float tot = red[dl] + red[64 + dl] + red[128 + dl] + red[192 + dl];
     out[static_cast<int64_t>(b) * out_stride + (kvh * G + g) * D + d] = f32_to_bf16(tot / lsum);
   }
 }
 
-static size_t reduce_lds(int max_chunks) { return (static_cast<size_t>(max_chunks) + 256 + 8) * sizeof(float); }
+static size_t reduce_lds(int max_chunks) { return (2 * static_cast<size_t>(max_chunks) + 256 + 8) * sizeof(float); }
 
 template <int G>
 static int launch_decode(int B, int nkv, int grid_chunks, hipStream_t s, const void* q, int q_stride, const void* kc,

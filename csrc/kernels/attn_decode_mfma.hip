@@ -14,11 +14,11 @@
 //                             LDS image of the 32 V rows, chunk-swizzled c ^ ((row & 7) << 1) so a
 //                             half-wave's 8 rows x 32 B hit 64 distinct banks. O^T keeps the head on
 //                             the lane, so the online-softmax rescale uses lane-local alpha.
-// Grid (grid_chunks, nkv, B); a block = 4 waves = one kv head x one balanced chunk: the L keys of
-// the sequence are split evenly over the grid_chunks blocks (decode_chunk: multiples of 128 keys,
-// at least `min_chunk`), so a graph captured for a context bucket keeps every block equally busy
-// whatever the actual L (no 2-blocks-per-CU tail at long judge contexts). The cross-chunk merge
-// reuses attn_decode.hip's partial layout and reduce kernel.
+// Grid (grid_chunks, nkv, B); a block = 4 waves = one kv head x one balanced key range: the L keys
+// of the sequence are split evenly, in 32-key units, over min(grid_chunks, L / min_chunk) blocks
+// (common.h decode_nsplit / decode_range), so a graph captured for a context bucket keeps every
+// block equally busy whatever the actual L (one block per CU at long judge contexts, no tail).
+// The cross-chunk merge reuses attn_decode.hip's partial layout and reduce kernel.
 #include "attn_reduce.h"
 
 namespace llmc {
@@ -43,11 +43,10 @@ __global__ __launch_bounds__(256) void attn_decode_mfma_kernel(
   constexpr int VCH = D / 8;  // 16-B chunks per V row
   const int c = blockIdx.x, kvh = blockIdx.y, b = blockIdx.z;
   const int L = seq_lens[b];
-  const int chunk = decode_chunk(L, gridDim.x, -min_chunk);
-  const int start = c * chunk;
-  if (start >= L) return;
-  const int end = min(start + chunk, L);
-  const int nchunks = (L + chunk - 1) / chunk;
+  const int nchunks = decode_nsplit(L, gridDim.x, -min_chunk);
+  if (c >= nchunks) return;
+  int start, end;
+  decode_range(L, nchunks, c, -min_chunk, start, end);
 
   const int tid = threadIdx.x, wave = tid / 64, lane = tid % 64;
   const int h = lane & 15, g4 = lane >> 4;
@@ -182,21 +181,22 @@ __global__ __launch_bounds__(256) void attn_decode_mfma_kernel(
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
   };
 
-  const int per_wave = chunk / 4;
+  const int per_wave = (((end - start + 3) / 4) + 31) & ~31;  // 32-key sub-tiles per wave
   const int wbase = start + wave * per_wave;
   bf16x8 kfA[2][KS], kfB[2][KS];
   u32x4 vsA[NV], vsB[NV];
-  if (wbase < end) issue(wbase, kfA, vsA);
+  auto valid = [&](int k) { return k - wbase < per_wave && k < end; };  // wave-uniform
   // two named register sets, hand-unrolled (no runtime-indexed register arrays, guide rule 20):
-  // the next sub-tile's loads are in flight while the current one computes
-  for (int st = 0; st < per_wave; st += 64) {
-    const int k0 = wbase + st, k1 = k0 + 32;
-    if (k0 >= end) break;  // wave-uniform
-    if (st + 32 < per_wave && k1 < end) issue(k1, kfB, vsB);
+  // the next sub-tile's loads are in flight while the current one computes. (A third set, two
+  // sub-tiles ahead, measured no faster at 16k-65k keys: profiles/r1_attn_decode_microbench.md.)
+  if (valid(wbase)) issue(wbase, kfA, vsA);
+  for (int k0 = wbase;; k0 += 64) {
+    if (!valid(k0)) break;
+    if (valid(k0 + 32)) issue(k0 + 32, kfB, vsB);
     compute(k0, kfA, vsA);
-    if (!(st + 32 < per_wave && k1 < end)) break;
-    if (st + 64 < per_wave && k1 + 32 < end) issue(k1 + 32, kfA, vsA);
-    compute(k1, kfB, vsB);
+    if (!valid(k0 + 32)) break;
+    if (valid(k0 + 64)) issue(k0 + 64, kfA, vsA);
+    compute(k0 + 32, kfB, vsB);
   }
 
   // ---- merge the 4 waves: red[wave][h][D + 2] (only lanes with h < G carry data) ----
@@ -270,10 +270,11 @@ template <int G, int D>
 static int launch_mfma(dim3 grid, hipStream_t s, const void* q, int q_stride, const void* kc, const void* vc,
                        const void* bt, int bt_stride, const void* sl, void* part, void* ctr, void* out, int out_stride,
                        int nkv, int bs, int chunk, int max_chunks, float scale, bool ticket) {
-  // page-id staging sized for the largest balanced chunk any sequence of this table can get
+  // page-id staging sized for the largest balanced range any sequence of this table can get
   const int grid_chunks = static_cast<int>(grid.x);
-  const int bal = ((bt_stride * bs + grid_chunks - 1) / grid_chunks + 127) / 128 * 128;
-  const int max_chunk = bal > chunk ? bal : chunk;
+  const int units = (bt_stride * bs + 31) / 32;
+  const int bal = 32 * ((units + grid_chunks - 1) / grid_chunks) + 32;
+  const int max_chunk = bal > 2 * chunk ? bal : 2 * chunk;
   const size_t lds = 4 * 32 * kVRowBytes + static_cast<size_t>(4) * G * (D + 2) * sizeof(float) +
                      static_cast<size_t>((max_chunk + bs - 1) / bs + 2) * sizeof(int);
   if (lds > 64 * 1024) return -4;

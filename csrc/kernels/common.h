@@ -103,14 +103,26 @@ __device__ __forceinline__ float block_sum(float v, float* red) {
 
 __device__ __forceinline__ float silu(float x) { return x / (1.f + __expf(-x)); }
 
-// Split-KV decode attention, balanced form: a fixed grid of `gc` chunk-blocks per (sequence, kv
-// head) shares the sequence's L keys evenly (multiples of 128 keys, at least `min_chunk`), so the
-// grid shape (and a captured graph) is independent of L while every block gets equal work.
-// chunk_arg < 0 encodes this form (min_chunk = -chunk_arg); >= 0 is a fixed chunk size.
-__device__ __forceinline__ int decode_chunk(int L, int gc, int chunk_arg) {
-  if (chunk_arg >= 0) return chunk_arg;
-  const int per = ((L + gc - 1) / gc + 127) & ~127;
-  return per > -chunk_arg ? per : -chunk_arg;
+// Split-KV decode attention, balanced form: a fixed grid of `gc` blocks per (sequence, kv head)
+// shares the sequence's L keys evenly in 32-key units (the MFMA sub-tile): n = min(gc,
+// ceil(L / min_chunk)) blocks, block c owning units [c*U/n, (c+1)*U/n) of U = ceil(L/32), so
+// the grid shape (and a captured graph) is independent of L and every live block gets the same
+// work to within one sub-tile. chunk_arg < 0 encodes this form (min_chunk = -chunk_arg);
+// chunk_arg >= 0 is the fixed-chunk form (blocks of chunk_arg keys; VALU kernels).
+__device__ __forceinline__ int decode_nsplit(int L, int gc, int chunk_arg) {
+  if (chunk_arg >= 0) return (L + chunk_arg - 1) / chunk_arg;
+  const int n = (L + (-chunk_arg) - 1) / (-chunk_arg);
+  return n < 1 ? 1 : (n < gc ? n : gc);
+}
+__device__ __forceinline__ void decode_range(int L, int n, int c, int chunk_arg, int& start, int& end) {
+  if (chunk_arg >= 0) {
+    start = c * chunk_arg;
+    end = min(start + chunk_arg, L);
+    return;
+  }
+  const int64_t units = (L + 31) / 32;
+  start = static_cast<int>(32 * (c * units / n));
+  end = min(L, static_cast<int>(32 * ((c + 1) * units / n)));
 }
 
 }  // namespace llmc

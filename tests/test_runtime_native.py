@@ -1,5 +1,7 @@
 """Native host runtime: synthetic tokenizer and paged-KV block allocator."""
 
+import os
+
 import pytest
 
 from llm_consensus_amd.consensus import prompt_header, prompt_trailer, response_block
@@ -55,3 +57,26 @@ def test_block_allocator():
     assert A.num_free == 10
     with pytest.raises(Exception):
         A.free(a[:1])  # double free
+
+
+def test_runtime_selftest_asan_ubsan(tmp_path):
+    """The native runtime built standalone with AddressSanitizer + UBSan (host code only,
+    SURVEY.md §5.2) and driven by csrc/tests/runtime_selftest.cpp, incl. 8-thread allocator churn."""
+    import shutil
+    import subprocess
+
+    if shutil.which("g++") is None:
+        pytest.skip("no g++")
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    rt = os.path.join(root, "csrc", "runtime")
+    exe = str(tmp_path / "selftest")
+    cmd = ["g++", "-std=c++17", "-O1", "-g", "-fno-omit-frame-pointer", "-fsanitize=address,undefined",
+           "-fno-sanitize-recover=undefined", os.path.join(root, "csrc", "tests", "runtime_selftest.cpp"),
+           os.path.join(rt, "tokenizer.cpp"), os.path.join(rt, "block_allocator.cpp"), os.path.join(rt, "gojson.cpp"),
+           "-pthread", "-o", exe]
+    subprocess.run(cmd, check=True, capture_output=True, timeout=300)
+    env = dict(os.environ)
+    env["ASAN_OPTIONS"] = "detect_leaks=1:abort_on_error=0:verify_asan_link_order=0"
+    r = subprocess.run([exe], capture_output=True, timeout=300, env=env)
+    assert r.returncode == 0, r.stderr.decode()[-4000:]
+    assert b"runtime selftest ok" in r.stdout

@@ -1,11 +1,12 @@
 // Launchers for the decode GEMV (kernel body: gemv_core.h).
 //
 // Geometry (cold-weight sweep on MI355X, scripts/microbench_kernels.py sweep,
-// profiles/r1_gemv_geometry_sweep.md): 1024-thread blocks (16 waves), one row per wave, 4 x 16 B
-// loads per lane in flight (+ the next batch prefetched) were fastest on every Llama-3-8B shape:
-// fewer, fatter blocks stage/normalise x once per 16 rows instead of once per 4, and keep 16
-// waves per CU streaming. Paired epilogues (SiLU gate/up, RoPE) meet their partner row of the
-// next wave through LDS (PAIR_LDS); shapes that do not tile by 32 rows keep 256 x 2 rows/wave.
+// profiles/r1_gemv_geometry_sweep.md): fat blocks (8-16 waves), one row per wave, 4 x 16 B loads
+// per lane in flight (+ the next batch prefetched) were fastest on every Llama-3-8B shape: x is
+// staged/normalised once per 8-16 rows, and 12-16 waves per CU keep streaming. The waves per
+// block are picked so the grid fills whole rounds of the 256 CUs (pick_waves). Paired epilogues
+// (SiLU gate/up, RoPE) meet their partner row of the next wave through LDS (PAIR_LDS); shapes
+// that do not tile keep 256 threads x 2 rows/wave.
 #include "gemv_core.h"
 
 namespace llmc {
@@ -32,14 +33,36 @@ static int launch_gemv_g(const void* x, int x_stride, const void* nw, float eps,
   return static_cast<int>(hipGetLastError());
 }
 
+// Waves per block so that the grid fills whole rounds of the 256 CUs (a 6144-row qkv at 16
+// rows/block = 384 blocks leaves half the CUs with twice the work; 12 rows/block = 512 blocks
+// is exact): the smallest idle fraction of the last round, ties to the larger block.
+static int pick_waves(int N, bool paired) {
+  int best = 16;
+  double best_idle = 2.0;
+  for (int w : {16, 12, 8}) {
+    if (paired && N % (2 * w) != 0) continue;
+    const long blocks = (N + w - 1) / w;
+    const long slots = (blocks + 255) / 256 * 256;
+    const double idle = static_cast<double>(slots - blocks) / static_cast<double>(slots);
+    if (idle < best_idle - 1e-9) {
+      best_idle = idle;
+      best = w;
+    }
+  }
+  return best_idle > 1.0 ? 0 : best;
+}
+
 template <int M, int PRO, int EPI>
 static int launch_gemv(const void* x, int x_stride, const void* nw, float eps, const void* W, void* out,
                        int out_stride, int N, int K, const RopeEpi& rope, hipStream_t s) {
-  if constexpr (EPI == EPI_SILU || EPI == EPI_ROPE) {
-    if (N % 32 != 0)  // the 16-wave pair exchange needs whole 32-row blocks
+  constexpr bool paired = EPI == EPI_SILU || EPI == EPI_ROPE;
+  switch (pick_waves(N, paired)) {
+    case 16: return launch_gemv_g<M, 1024, 1, PRO, EPI>(x, x_stride, nw, eps, W, out, out_stride, N, K, rope, s);
+    case 12: return launch_gemv_g<M, 768, 1, PRO, EPI>(x, x_stride, nw, eps, W, out, out_stride, N, K, rope, s);
+    case 8: return launch_gemv_g<M, 512, 1, PRO, EPI>(x, x_stride, nw, eps, W, out, out_stride, N, K, rope, s);
+    default:  // paired rows that do not tile by 16-32 rows: pairs inside one wave
       return launch_gemv_g<M, 256, 2, PRO, EPI>(x, x_stride, nw, eps, W, out, out_stride, N, K, rope, s);
   }
-  return launch_gemv_g<M, 1024, 1, PRO, EPI>(x, x_stride, nw, eps, W, out, out_stride, N, K, rope, s);
 }
 
 template <int PRO, int EPI>

@@ -18,6 +18,8 @@
 //    accumulators, q to the q buffer, k/v straight into the paged KV cache at the device slot
 //    (replaces the separate RoPE + KV-write launch of the decode step).
 #pragma once
+#include <type_traits>
+
 #include "common.h"
 
 namespace llmc {
@@ -89,39 +91,96 @@ __global__ __launch_bounds__(NT) void gemv_kernel(const bf16_t* __restrict__ x, 
     float ss[M];
 #pragma unroll
     for (int m = 0; m < M; ++m) ss[m] = 0.f;
-    for (int c = tid; c < nchunk; c += NT) {
+    if (nchunk <= 2 * NT) {
+      // ONE global round trip: x and the norm weights stay in registers between the sum of
+      // squares and the normalisation (K <= 16 Ki at 1024 threads)
+      u32x4 xr[2][M], gr[2];
 #pragma unroll
-      for (int m = 0; m < M; ++m) {
-        float f[8];
-        unpack8(reinterpret_cast<const u32x4*>(x + static_cast<int64_t>(m) * x_stride)[c], f);
+      for (int j = 0; j < 2; ++j) {
+        const int c = tid + j * NT;
+        if (c < nchunk) {
+          gr[j] = reinterpret_cast<const u32x4*>(norm_w)[c];
 #pragma unroll
-        for (int j = 0; j < 8; ++j) ss[m] += f[j] * f[j];
+          for (int m = 0; m < M; ++m) xr[j][m] = reinterpret_cast<const u32x4*>(x + static_cast<int64_t>(m) * x_stride)[c];
+        }
       }
-    }
 #pragma unroll
-    for (int m = 0; m < M; ++m) {
-      const float s = wave_sum(ss[m]);
-      if ((tid & 63) == 0) red[m][tid / 64] = s;
-    }
-    __syncthreads();
-    float inv[M];
+      for (int j = 0; j < 2; ++j) {
+        if (tid + j * NT < nchunk) {
 #pragma unroll
-    for (int m = 0; m < M; ++m) {
-      float t = 0.f;
+          for (int m = 0; m < M; ++m) {
+            float f[8];
+            unpack8(xr[j][m], f);
 #pragma unroll
-      for (int w = 0; w < WAVES; ++w) t += red[m][w];
-      inv[m] = rsqrtf(t / K + eps);
-    }
-    for (int c = tid; c < nchunk; c += NT) {
-      float g[8];
-      unpack8(reinterpret_cast<const u32x4*>(norm_w)[c], g);
+            for (int e = 0; e < 8; ++e) ss[m] += f[e] * f[e];
+          }
+        }
+      }
 #pragma unroll
       for (int m = 0; m < M; ++m) {
-        float f[8];
-        unpack8(reinterpret_cast<const u32x4*>(x + static_cast<int64_t>(m) * x_stride)[c], f);
+        const float sm = wave_sum(ss[m]);
+        if ((tid & 63) == 0) red[m][tid / 64] = sm;
+      }
+      __syncthreads();
+      float inv[M];
 #pragma unroll
-        for (int j = 0; j < 8; ++j) f[j] = f[j] * inv[m] * g[j];
-        reinterpret_cast<u32x4*>(xs + m * K)[c] = pack8(f);
+      for (int m = 0; m < M; ++m) {
+        float t = 0.f;
+#pragma unroll
+        for (int w = 0; w < WAVES; ++w) t += red[m][w];
+        inv[m] = rsqrtf(t / K + eps);
+      }
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        const int c = tid + j * NT;
+        if (c < nchunk) {
+          float g[8];
+          unpack8(gr[j], g);
+#pragma unroll
+          for (int m = 0; m < M; ++m) {
+            float f[8];
+            unpack8(xr[j][m], f);
+#pragma unroll
+            for (int e = 0; e < 8; ++e) f[e] = f[e] * inv[m] * g[e];
+            reinterpret_cast<u32x4*>(xs + m * K)[c] = pack8(f);
+          }
+        }
+      }
+    } else {  // long rows: two passes over x (L2-resident)
+      for (int c = tid; c < nchunk; c += NT) {
+#pragma unroll
+        for (int m = 0; m < M; ++m) {
+          float f[8];
+          unpack8(reinterpret_cast<const u32x4*>(x + static_cast<int64_t>(m) * x_stride)[c], f);
+#pragma unroll
+          for (int j = 0; j < 8; ++j) ss[m] += f[j] * f[j];
+        }
+      }
+#pragma unroll
+      for (int m = 0; m < M; ++m) {
+        const float sm = wave_sum(ss[m]);
+        if ((tid & 63) == 0) red[m][tid / 64] = sm;
+      }
+      __syncthreads();
+      float inv[M];
+#pragma unroll
+      for (int m = 0; m < M; ++m) {
+        float t = 0.f;
+#pragma unroll
+        for (int w = 0; w < WAVES; ++w) t += red[m][w];
+        inv[m] = rsqrtf(t / K + eps);
+      }
+      for (int c = tid; c < nchunk; c += NT) {
+        float g[8];
+        unpack8(reinterpret_cast<const u32x4*>(norm_w)[c], g);
+#pragma unroll
+        for (int m = 0; m < M; ++m) {
+          float f[8];
+          unpack8(reinterpret_cast<const u32x4*>(x + static_cast<int64_t>(m) * x_stride)[c], f);
+#pragma unroll
+          for (int j = 0; j < 8; ++j) f[j] = f[j] * inv[m] * g[j];
+          reinterpret_cast<u32x4*>(xs + m * K)[c] = pack8(f);
+        }
       }
     }
   } else {
@@ -159,11 +218,13 @@ __global__ __launch_bounds__(NT) void gemv_kernel(const bf16_t* __restrict__ x, 
     for (int m = 0; m < M; ++m) acc[r][m] = 0.f;
 
   const u32x4* xv = reinterpret_cast<const u32x4*>(xs);
-  auto consume = [&](const u32x4 (&wv)[RPW][UNROLL], int cbase) {
+  // MASKED only for the last batch when K is not a multiple of 64 * 8 * UNROLL elements: the
+  // full batches run branch-free (no per-chunk exec-mask juggling between the waits)
+  auto consume = [&](const u32x4 (&wv)[RPW][UNROLL], int cbase, auto masked) {
 #pragma unroll
     for (int u = 0; u < UNROLL; ++u) {
       const int c = cbase + u * kWave;
-      if (c < nchunk) {
+      if (!decltype(masked)::value || c < nchunk) {
 #pragma unroll
         for (int m = 0; m < M; ++m) {
           const u32x4 xx = xv[m * nchunk + c];
@@ -173,17 +234,24 @@ __global__ __launch_bounds__(NT) void gemv_kernel(const bf16_t* __restrict__ x, 
       }
     }
   };
+  using Full = std::integral_constant<bool, false>;
+  using Masked = std::integral_constant<bool, true>;
+  const int full = nchunk / STEP;  // batches in which every lane's chunks are all in range
   int c0 = lane;
-  for (int it = 0; it + 1 < iters; ++it, c0 += STEP) {
+  for (int it = 0; it + 1 < iters; ++it, c0 += STEP) {  // it < iters - 1 <= full
     u32x4 nxt[RPW][UNROLL];
     issue(nxt, c0 + STEP);
-    consume(cur, c0);
+    consume(cur, c0, Full{});
 #pragma unroll
     for (int u = 0; u < UNROLL; ++u)
 #pragma unroll
       for (int r = 0; r < RPW; ++r) cur[r][u] = nxt[r][u];
   }
-  consume(cur, c0);
+  if (full == iters) {
+    consume(cur, c0, Full{});
+  } else {
+    consume(cur, c0, Masked{});
+  }
 
 #pragma unroll
   for (int r = 0; r < RPW; ++r)

@@ -123,26 +123,43 @@ extern "C" int llmc_gemv_qkv_rope(int M, const void* x, int x_stride, const void
 
 // MoE decode (K11 at batch 1): one GEMV per (token, top-k slot) pair against the selected
 // expert's weights; expert ids are read on device, so the launch is graph-replayable.
+namespace llmc {
+template <int NT, int RPW, int EPI>
+static int launch_moe_gemv(int npairs, const void* x, int x_stride, float eps, const void* W, const void* ids,
+                           int x_div, void* out, int out_stride, int N, int K, hipStream_t s) {
+  constexpr int WAVES = NT / kWave;
+  const size_t lds = static_cast<size_t>(K) * sizeof(bf16_t) + 2 * WAVES * sizeof(float);
+  if (lds > 64 * 1024) return -2;
+  dim3 grid((N + WAVES * RPW - 1) / (WAVES * RPW), npairs);
+  gemv_kernel<1, NT, RPW, 4, PRO_NONE, EPI, true><<<grid, NT, lds, s>>>(
+      (const bf16_t*)x, x_stride, nullptr, eps, (const bf16_t*)W, out, out_stride, N, K, (const int32_t*)ids, x_div,
+      RopeEpi{});
+  return static_cast<int>(hipGetLastError());
+}
+
+template <int EPI>
+static int moe_gemv_geom(int npairs, const void* x, int x_stride, float eps, const void* W, const void* ids, int x_div,
+                         void* out, int out_stride, int N, int K, hipStream_t s) {
+  // same geometry rule as the dense GEMV; the grid's y dimension (token, expert) pairs multiplies
+  // the rounds, so whole rounds per pair are whole rounds overall
+  switch (pick_waves(N, EPI == EPI_SILU)) {
+    case 16: return launch_moe_gemv<1024, 1, EPI>(npairs, x, x_stride, eps, W, ids, x_div, out, out_stride, N, K, s);
+    case 12: return launch_moe_gemv<768, 1, EPI>(npairs, x, x_stride, eps, W, ids, x_div, out, out_stride, N, K, s);
+    case 8: return launch_moe_gemv<512, 1, EPI>(npairs, x, x_stride, eps, W, ids, x_div, out, out_stride, N, K, s);
+    default: return launch_moe_gemv<256, 2, EPI>(npairs, x, x_stride, eps, W, ids, x_div, out, out_stride, N, K, s);
+  }
+}
+}  // namespace llmc
+
 extern "C" int llmc_moe_gemv(int npairs, const void* x, int x_stride, const void* norm_w, float eps, const void* W,
                              const void* ids, int x_div, void* out, int out_stride, int N, int K, int epi,
                              hipStream_t s) {
   if (K % 8 != 0 || norm_w != nullptr) return -1;
-  constexpr int NT = 256, RPW = 2, UNROLL = 4;
-  const size_t lds = static_cast<size_t>(K) * sizeof(bf16_t) + (NT / kWave) * sizeof(float);
-  if (lds > 64 * 1024) return -2;
-  dim3 grid((N + (NT / kWave) * RPW - 1) / ((NT / kWave) * RPW), npairs);
-  RopeEpi rope{};
-#define LLMC_MOEGV(E)                                                                                            \
-  gemv_kernel<1, NT, RPW, UNROLL, PRO_NONE, E, true><<<grid, NT, lds, s>>>(                                      \
-      (const bf16_t*)x, x_stride, nullptr, eps, (const bf16_t*)W, out, out_stride, N, K, (const int32_t*)ids, x_div, \
-      rope)
   switch (epi) {
-    case EPI_BF16: LLMC_MOEGV(EPI_BF16); break;
-    case EPI_SILU: LLMC_MOEGV(EPI_SILU); break;
+    case EPI_BF16: return moe_gemv_geom<EPI_BF16>(npairs, x, x_stride, eps, W, ids, x_div, out, out_stride, N, K, s);
+    case EPI_SILU: return moe_gemv_geom<EPI_SILU>(npairs, x, x_stride, eps, W, ids, x_div, out, out_stride, N, K, s);
     default: return -4;
   }
-#undef LLMC_MOEGV
-  return static_cast<int>(hipGetLastError());
 }
 
 // ---- geometry sweep entry (microbenchmarks only: M = 1, fused norm, bf16 out) ----

@@ -143,6 +143,36 @@ def bench_launch():
     print(f"rmsnorm [1,4096] (launch-bound floor): {us:.2f} us")
 
 
+def bench_prefill():
+    """Prefill GEMM (ours vs torch.matmul = hipBLASLt) and flash prefill attention throughput."""
+    for (M, N, K) in [(2048, 6144, 4096), (2048, 28672, 4096), (8192, 6144, 4096), (8192, 28672, 4096),
+                      (8192, 4096, 14336)]:
+        x = torch.randn(M, K, device="cuda").to(BF)
+        W = (torch.randn(N, K, device="cuda") * 0.02).to(BF)
+        out = torch.empty(M, N, dtype=BF, device="cuda")
+        t_ours = timeit(lambda: ops.gemm(x, W, 0, out=out), iters=10)
+        t_ref = timeit(lambda: torch.matmul(x, W.t(), out=out), iters=10)
+        fl = 2 * M * N * K
+        print(f"gemm M={M} N={N} K={K}: ours {t_ours:8.1f} us {fl / t_ours / 1e6:6.0f} TF/s | torch {t_ref:8.1f} us "
+              f"{fl / t_ref / 1e6:6.0f} TF/s", flush=True)
+    nh, nkv, D, bs = 32, 8, 128, 64
+    for (T, ctx) in [(2048, 2048), (8192, 8192), (8192, 32768)]:
+        nb = (ctx + bs - 1) // bs + 1
+        kc = torch.randn(nb, nkv, bs, D, device="cuda").to(BF)
+        vc = torch.randn_like(kc)
+        bt = torch.arange(nb, dtype=torch.int32, device="cuda").view(1, -1)
+        q = torch.randn(T, nh * D, device="cuda").to(BF)
+        out = torch.empty_like(q)
+        qs = torch.tensor([0], dtype=torch.int32, device="cuda")
+        ql = torch.tensor([T], dtype=torch.int32, device="cuda")
+        cl = torch.tensor([ctx], dtype=torch.int32, device="cuda")
+        us = timeit(lambda: ops.attn_prefill(q, kc, vc, bt, qs, ql, cl, out, T, nh, nkv, D, bs, 1 / math.sqrt(D)),
+                    iters=3)
+        # causal FLOPs of the last T queries over ctx keys
+        fl = 4 * nh * D * (T * ctx - T * (T - 1) / 2)
+        print(f"attn_prefill T={T} ctx={ctx}: {us:8.1f} us {fl / us / 1e6:6.0f} TF/s", flush=True)
+
+
 if __name__ == "__main__":
     what = sys.argv[1] if len(sys.argv) > 1 else "all"
     if what in ("launch", "all"):
@@ -155,3 +185,5 @@ if __name__ == "__main__":
         bench_mall()
     if what in ("sweep",):
         bench_gemv_sweep()
+    if what in ("prefill",):
+        bench_prefill()

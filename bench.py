@@ -63,10 +63,18 @@ def main() -> None:
     if world != args.gpus:
         log(f"warning: --gpus {args.gpus} but WORLD_SIZE {world}; using WORLD_SIZE")
     n_gpus = world
-    torch.cuda.set_device(local)
-    dev = f"cuda:{local}"
+    # rehearsal mode for the multi-rank flow on a 1-GPU box: every rank on cuda:0, gloo collectives
+    # (LLMC_BENCH_BACKEND=gloo LLMC_BENCH_SAME_GPU=1); the driver's runs use RCCL, one GPU per rank
+    backend = os.environ.get("LLMC_BENCH_BACKEND", "nccl")
+    gpu = 0 if os.environ.get("LLMC_BENCH_SAME_GPU") == "1" else local
+    torch.cuda.set_device(gpu)
+    dev = f"cuda:{gpu}"
+    cdev = dev if backend == "nccl" else "cpu"  # where collective buffers live
     if world > 1:
-        dist.init_process_group("nccl", device_id=torch.device(dev))
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device(dev))
+        else:
+            dist.init_process_group(backend)
 
     from llm_consensus_amd.consensus import build_judge_prompt, prompt_header
     from llm_consensus_amd.engine import Engine, EngineConfig, SamplingParams
@@ -145,8 +153,8 @@ def main() -> None:
         for j, ids in enumerate(outs):
             local_t[j, : len(ids)] = torch.tensor(ids, dtype=torch.int32, device=dev)
         if world > 1:
-            all_t = torch.empty((world, mpg, args.max_tokens), dtype=torch.int32, device=dev)
-            dist.all_gather_into_tensor(all_t, local_t)
+            all_t = torch.empty((world, mpg, args.max_tokens), dtype=torch.int32, device=cdev)
+            dist.all_gather_into_tensor(all_t.view(world * mpg, args.max_tokens), local_t.to(cdev))
         else:
             all_t = local_t.unsqueeze(0)
         n_tokens = n_models * args.max_tokens
@@ -199,7 +207,7 @@ def main() -> None:
         dist.barrier()
     elapsed = time.perf_counter() - t0
     if world > 1:
-        tt = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        tt = torch.tensor([elapsed], dtype=torch.float64, device=cdev)
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         elapsed = float(tt.item())
     if rank == 0:

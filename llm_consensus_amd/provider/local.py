@@ -100,10 +100,13 @@ class LocalBackend:
         self.specs = {s.name: s for s in specs}
         self.judge = judge
         force_cpu = os.environ.get("LLMC_DEVICE", "") == "cpu"
-        gpu_ids = [-1] if force_cpu else default_gpus(gpus)
+        # CPU workers (tests): LLMC_CPU_WORKERS=k spreads the models over k worker processes
+        n_cpu = max(1, int(os.environ.get("LLMC_CPU_WORKERS", "1")))
+        gpu_ids = [-(i + 1) for i in range(n_cpu)] if force_cpu else default_gpus(gpus)
         if not gpu_ids:
             raise LocalError("no ROCm GPU visible (set LLMC_DEVICE=cpu to run local models on the CPU)")
         self._queues: Dict[int, "queue.Queue"] = {}
+        self._rid_model: Dict[int, str] = {}
         self._qlock = threading.Lock()
         self._ids = itertools.count(1)
         self.closed = False
@@ -121,7 +124,7 @@ class LocalBackend:
         if force_cpu:
             from ..parallel.placement import Placement
 
-            self.placement = Placement({s.name: [-1] for s in specs})
+            self.placement = Placement({s.name: [gpu_ids[i % len(gpu_ids)]] for i, s in enumerate(specs)})
         trace_on = trace
         used = self.placement.used_gpus()
         groups = [(m, sorted(g)) for m, g in self.placement.gpus.items() if len(g) > 1]
@@ -166,16 +169,18 @@ class LocalBackend:
     def _workers_for(self, model: str) -> List[_Worker]:
         return [self.workers[g] for g in self.placement.gpus[model]]
 
-    def _new_request(self) -> (int, "queue.Queue"):
+    def _new_request(self, model: str = "") -> (int, "queue.Queue"):
         rid = next(self._ids)
         q: "queue.Queue" = queue.Queue()
         with self._qlock:
             self._queues[rid] = q
+            self._rid_model[rid] = model
         return rid, q
 
     def _end_request(self, rid: int) -> None:
         with self._qlock:
             self._queues.pop(rid, None)
+            self._rid_model.pop(rid, None)
 
     def _deliver(self, msg) -> None:
         with self._qlock:
@@ -184,8 +189,12 @@ class LocalBackend:
             q.put(msg)
 
     def _worker_died(self, w: _Worker) -> None:
+        """Liveness: a dead worker fails the requests of the models it hosts
+        (every rank of a TP group counts); models on other workers keep running."""
+        hosted = {m for m, gs in self.placement.gpus.items() if w.gpu in gs} if self.placement else None
         with self._qlock:
-            qs = list(self._queues.items())
+            qs = [(rid, q) for rid, q in self._queues.items()
+                  if hosted is None or not self._rid_model.get(rid) or self._rid_model[rid] in hosted]
         for rid, q in qs:
             q.put(("error", rid, w.fatal or "worker died"))
 
@@ -294,7 +303,7 @@ class LocalProvider:
         t0 = time.monotonic_ns()
         ids = self.tok.encode_prompt(req.prompt)
         params = self._params(req, len(ids))
-        rid, q = self.backend._new_request()
+        rid, q = self.backend._new_request(self.model)
         with tracing.span("query", cat="driver", model=self.model, prompt_tokens=len(ids)):
             self.backend.broadcast(self.model, ("generate", rid, self.model, ids, params))
             return self._stream(ctx, rid, q, callback, t0, len(ids))
@@ -351,7 +360,7 @@ class LocalProvider:
             cp -= 1
         rest = full[cp:]
         params = self._params(req, len(full))
-        rid, q = self.backend._new_request()
+        rid, q = self.backend._new_request(self.model)
         with tracing.span("judge_session_finish", cat="driver", model=self.model, rest_tokens=len(rest),
                           reused_tokens=cp):
             self.backend.broadcast(self.model, ("sess_generate", s["sid"], rid, rest, params, cp))

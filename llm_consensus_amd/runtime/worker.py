@@ -26,8 +26,9 @@ from typing import Dict, List, Optional
 
 def parse_faults(spec: str) -> Dict[str, tuple]:
     """Fault-injection hook: ``LLMC_FAULT="<model>:<stage>[:<k>],..."`` makes that
-    model's engine fail — stage ``init`` (every request errors), ``prefill`` (before prefill) or
-    ``decode`` (after k streamed tokens, default 1). Used by tests to exercise the best-effort
+    model's engine fail — stage ``init`` (every request errors), ``prefill`` (before prefill),
+    ``decode`` (after k streamed tokens, default 1) or ``crash`` (the whole worker process dies
+    abruptly on the first request: liveness path). Used by tests to exercise the best-effort
     failure path (runner.go:73-83) with real engines."""
     out: Dict[str, tuple] = {}
     for item in filter(None, (x.strip() for x in (spec or "").split(","))):
@@ -36,7 +37,7 @@ def parse_faults(spec: str) -> Dict[str, tuple]:
             parts = [parts[0] + ":" + parts[1], parts[2]]
         model, stage = parts[0], parts[1]
         k = int(parts[2]) if len(parts) == 3 else 1
-        if stage not in ("init", "prefill", "decode"):
+        if stage not in ("init", "prefill", "decode", "crash"):
             raise ValueError(f"LLMC_FAULT: unknown stage {stage!r} in {item!r}")
         out[model] = (stage, k)
     return out
@@ -142,6 +143,8 @@ class _EngineHost:
 
         t0 = time.monotonic_ns()
         stage, k = self.fault or ("", 0)
+        if stage == "crash":
+            os._exit(17)  # simulated worker death (no cleanup, like a segfault or OOM kill)
         if stage in ("init", "prefill"):
             raise InjectedFault(f"injected fault: {self.name} {stage}")
         self.engine.prefill(seqs, prompts)

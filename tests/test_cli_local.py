@@ -80,3 +80,16 @@ def test_parse_faults():
     assert parse_faults("") == {}
     with pytest.raises(ValueError):
         parse_faults("a:boom")
+
+
+def test_cli_worker_crash_isolated_cpu():
+    """A worker process dying mid-run (LLMC_FAULT=<model>:crash) fails only the models it hosts;
+    the run completes with the others (liveness via pipe EOF)."""
+    rc, out, err = run_cli(["--models", "llama-tiny@1,phi3-tiny", "--judge", "llama-tiny@j", "--max-tokens", "8",
+                            "--json", "hi"],
+                           env={"LLMC_DEVICE": "cpu", "LLMC_CPU_WORKERS": "2", "LLMC_FAULT": "phi3-tiny:crash"})
+    assert rc == 0, err
+    d = json.loads(out)
+    assert [r["model"] for r in d["responses"]] == ["llama-tiny@1"]
+    assert d["failed_models"] == ["phi3-tiny"]
+    assert any("exited" in w for w in d["warnings"]), d["warnings"]

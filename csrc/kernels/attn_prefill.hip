@@ -35,17 +35,18 @@ constexpr int kTileBytes = kKT * kRowBytes;  // 16 KB
 __device__ __forceinline__ int k_swz(int row, int ch) { return row * kRowBytes + ((ch ^ (row & 15)) << 4); }
 __device__ __forceinline__ int v_swz(int row, int ch) { return row * kRowBytes + ((ch ^ ((row & 3) << 2)) << 4); }
 
-template <int D>
-__global__ __launch_bounds__(256, 2) void attn_prefill_kernel(
+template <int D, int WPB>
+__global__ __launch_bounds__(WPB * 64) void attn_prefill_kernel(
     const bf16_t* __restrict__ q, int q_stride, const bf16_t* __restrict__ k_cache, const bf16_t* __restrict__ v_cache,
     const int32_t* __restrict__ block_tables, int bt_stride, const int32_t* __restrict__ q_start,
     const int32_t* __restrict__ q_lens, const int32_t* __restrict__ ctx_lens, bf16_t* __restrict__ out,
     int out_stride, int nh, int nkv, int bs, float scale_log2) {
   constexpr int CH = D / 8;            // 16-B chunks per row
-  constexpr int NL = (kKT * CH) / 256; // staging chunks per thread per tensor
+  constexpr int NT = WPB * 64;
+  constexpr int NL = (kKT * CH + NT - 1) / NT;  // staging chunks per thread per tensor
+  constexpr bool NL_EXACT = (kKT * CH) % NT == 0;
   constexpr int KS = D / 16;           // k-steps for Q.K
   constexpr int DT = D / 32;           // 32-wide d tiles of O
-  static_assert((kKT * CH) % 256 == 0, "tile chunking");
 
   __shared__ __attribute__((aligned(16))) char smem[2 * 2 * kTileBytes];  // [buf][K|V]
 
@@ -57,7 +58,8 @@ __global__ __launch_bounds__(256, 2) void attn_prefill_kernel(
   const int q0 = q_start[b];
   const int npb = (qlen + 31) / 32;
   const int nrt = G * npb;
-  const int rt_base = blockIdx.x * 4;
+  // longest (latest query rows: most causal key tiles) blocks first -> no long-job tail
+  const int rt_base = (gridDim.x - 1 - blockIdx.x) * WPB;
   if (rt_base >= nrt) return;  // block-uniform
 
   const int tid = threadIdx.x, wave = tid / 64, lane = tid % 64;
@@ -71,11 +73,12 @@ __global__ __launch_bounds__(256, 2) void attn_prefill_kernel(
   const int row_i = pb * 32 + r;                  // query row within the sequence chunk
   const int qi = min(row_i, qlen - 1);
   const int qpos = first_pos + qi;                 // absolute position (causal limit)
-  const int last_rt = min(rt_base + 3, nrt - 1);
+  const int last_rt = min(rt_base + WPB - 1, nrt - 1);
   const int pb_last = last_rt / G;
   const int kend = min(ctx, first_pos + min(pb_last * 32 + 31, qlen - 1) + 1);
   const int ntiles = (kend + kKT - 1) / kKT;
   const int wave_kend = wvalid ? first_pos + min(pb * 32 + 31, qlen - 1) + 1 : 0;
+  const int wave_qpos0 = first_pos + pb * 32;  // smallest query position of this wave
 
   // Q^T fragments (B operand): lane (r, hh) holds Q[qi][h*D + ks*16 + 8hh .. +8]
   bf16x8 qf[KS];
@@ -99,7 +102,8 @@ __global__ __launch_bounds__(256, 2) void attn_prefill_kernel(
   auto issue = [&](int t) {
 #pragma unroll
     for (int u = 0; u < NL; ++u) {
-      const int idx = tid + u * 256;
+      const int idx = tid + u * NT;
+      if (!NL_EXACT && idx >= kKT * CH) continue;
       const int row = idx / CH, ch = idx % CH;
       int key = t * kKT + row;
       key = min(key, ctx - 1);
@@ -114,7 +118,8 @@ __global__ __launch_bounds__(256, 2) void attn_prefill_kernel(
     char* vb = kb + kTileBytes;
 #pragma unroll
     for (int u = 0; u < NL; ++u) {
-      const int idx = tid + u * 256;
+      const int idx = tid + u * NT;
+      if (!NL_EXACT && idx >= kKT * CH) continue;
       const int row = idx / CH, ch = idx % CH;
       *reinterpret_cast<u32x4*>(kb + k_swz(row, ch)) = stk[u];
       *reinterpret_cast<u32x4*>(vb + v_swz(row, ch)) = stv[u];
@@ -146,37 +151,62 @@ __global__ __launch_bounds__(256, 2) void attn_prefill_kernel(
         }
       }
       // ---- online softmax (lane owns query qpos; keys in registers) ----
+      // Causal masking only on tiles that reach past the wave's first query position (the
+      // diagonal band); the others are plain scale + max. Raw v_exp_f32 (inputs are <= 0 after
+      // the max subtraction, so no range reduction is needed).
+      const bool diag = kt + kKT - 1 > wave_qpos0;  // wave-uniform
       float mx = -1e30f;
+      if (diag) {
 #pragma unroll
-      for (int kb2 = 0; kb2 < 2; ++kb2)
+        for (int kb2 = 0; kb2 < 2; ++kb2)
 #pragma unroll
-        for (int i = 0; i < 16; ++i) {
-          const int key = kt + kb2 * 32 + (i & 3) + 8 * (i >> 2) + 4 * hh;
-          const float v = s[kb2][i] * scale_log2;
-          const bool keep = key <= qpos;
-          s[kb2][i] = keep ? v : -1e30f;
-          mx = fmaxf(mx, s[kb2][i]);
-        }
+          for (int i = 0; i < 16; ++i) {
+            const int key = kt + kb2 * 32 + (i & 3) + 8 * (i >> 2) + 4 * hh;
+            s[kb2][i] = key <= qpos ? s[kb2][i] * scale_log2 : -1e30f;
+            mx = fmaxf(mx, s[kb2][i]);
+          }
+      } else {
+#pragma unroll
+        for (int kb2 = 0; kb2 < 2; ++kb2)
+#pragma unroll
+          for (int i = 0; i < 16; ++i) {
+            s[kb2][i] *= scale_log2;
+            mx = fmaxf(mx, s[kb2][i]);
+          }
+      }
       mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
       const float m_new = fmaxf(m_run, mx);
-      const float alpha = exp2f(m_run - m_new);
+      const float alpha = __builtin_amdgcn_exp2f(m_run - m_new);
       float rs = 0.f;
+      if (diag) {
 #pragma unroll
-      for (int kb2 = 0; kb2 < 2; ++kb2)
+        for (int kb2 = 0; kb2 < 2; ++kb2)
 #pragma unroll
-        for (int i = 0; i < 16; ++i) {
-          const float sv = s[kb2][i];
-          const float p = sv <= -1e29f ? 0.f : exp2f(sv - m_new);
-          s[kb2][i] = p;
-          rs += p;
-        }
+          for (int i = 0; i < 16; ++i) {
+            const float sv = s[kb2][i];
+            const float p = sv <= -1e29f ? 0.f : __builtin_amdgcn_exp2f(sv - m_new);
+            s[kb2][i] = p;
+            rs += p;
+          }
+      } else {
+#pragma unroll
+        for (int kb2 = 0; kb2 < 2; ++kb2)
+#pragma unroll
+          for (int i = 0; i < 16; ++i) {
+            const float p = __builtin_amdgcn_exp2f(s[kb2][i] - m_new);
+            s[kb2][i] = p;
+            rs += p;
+          }
+      }
       rs += __shfl_xor(rs, 32, 64);
       l_run = l_run * alpha + rs;
       m_run = m_new;
+      if (__any(alpha != 1.f)) {  // the running max moved for some query of the wave
 #pragma unroll
-      for (int dt = 0; dt < DT; ++dt)
+        for (int dt = 0; dt < DT; ++dt)
 #pragma unroll
-        for (int i = 0; i < 16; ++i) acc_o[dt][i] *= alpha;
+          for (int i = 0; i < 16; ++i) acc_o[dt][i] *= alpha;
+      }
       // ---- P fragments: k-step k4 = kb2*2 + sidx uses registers 8*sidx .. +7 of s[kb2] ----
       bf16x8 pf[4];
 #pragma unroll
@@ -236,10 +266,11 @@ extern "C" int llmc_attn_prefill(const void* q, int q_stride, const void* k_cach
   if (nh % nkv != 0) return -1;
   const int G = nh / nkv;
   const int npb = (max_qlen + 31) / 32;
-  dim3 grid((G * npb + 3) / 4, nkv, B);
+  constexpr int WPB = 8;  // 8 waves = 2 row tiles x 4 heads share every staged K/V tile
+  dim3 grid((G * npb + WPB - 1) / WPB, nkv, B);
   const float sl2 = scale * 1.4426950408889634f;
 #define LLMC_PF(DD)                                                                                            \
-  attn_prefill_kernel<DD><<<grid, 256, 0, s>>>((const bf16_t*)q, q_stride, (const bf16_t*)k_cache,           \
+  attn_prefill_kernel<DD, WPB><<<grid, WPB * 64, 0, s>>>((const bf16_t*)q, q_stride, (const bf16_t*)k_cache, \
                                                (const bf16_t*)v_cache, (const int32_t*)block_tables, bt_stride, \
                                                (const int32_t*)q_start, (const int32_t*)q_lens,                \
                                                (const int32_t*)ctx_lens, (bf16_t*)out, out_stride, nh, nkv, bs, sl2)

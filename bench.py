@@ -108,7 +108,9 @@ def main() -> None:
     judge = None
     judge_ctx = 0
     if rank == 0 and n_models > 1:
-        judge_ctx = len(prompt_ids) + 1024 + n_models * (args.max_tokens + 32) + jmax + 64
+        # responses are decoded to text and re-tokenized by the judge: random byte tokens can expand
+        # (invalid UTF-8 -> U+FFFD -> 3 byte tokens), so budget 2x per response
+        judge_ctx = len(prompt_ids) + 1024 + n_models * (2 * args.max_tokens + 64) + jmax + 64
         judge = Engine(jcfg, EngineConfig(device=dev, max_context=judge_ctx, seed=777,
                                           steps_per_graph=args.steps_per_graph, use_graphs=not args.no_graphs),
                        name=f"{args.judge}@judge")

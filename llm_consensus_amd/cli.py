@@ -7,7 +7,8 @@ entry and the judge must resolve, main.go:395-415) → fan-out → judge → per
 
 Extra engine flags (no reference counterpart): ``--max-tokens``,
 ``--temperature``, ``--top-p``, ``--top-k``, ``--seed``, ``--gpus``, ``--trace``,
-``--list-models``, ``--weights-dir`` (Hugging Face checkpoints as extra local model families).
+``--list-models``, ``--weights-dir`` (Hugging Face checkpoints as extra local model families),
+``--placement`` (pin models / TP groups to GPUs).
 """
 
 from __future__ import annotations
@@ -60,6 +61,7 @@ class Config:
     seed: int
     gpus: str
     trace: bool
+    placement: str = ""
 
 
 def make_flagset() -> FlagSet:
@@ -83,6 +85,8 @@ def make_flagset() -> FlagSet:
     fs.add("seed", "int", 0, "Sampling seed (0 = derived from the model name)")
     fs.add("gpus", "string", "", "Comma-separated GPU ids to place models on (default: all visible)")
     fs.add("trace", "bool", False, "Write a Chrome trace of engine spans to the run directory")
+    fs.add("placement", "string", "",
+           "Pin models to GPUs: model=gpu[+gpu...],... ('+' = tensor-parallel group); the rest are placed automatically")
     fs.add("list-models", "bool", False, "Print the local model catalog as JSON and exit")
     fs.add("weights-dir", "string", "",
            "Comma-separated Hugging Face checkpoint dirs (or parents of them) to serve as models ($LLMC_WEIGHTS_DIR)")
@@ -164,7 +168,7 @@ def parse_flags(argv: List[str], stdout: TextIO = sys.stdout, stderr: TextIO = s
     cfg = Config(models=models, judge=v["judge"], file=v["file"], output=v["output"], data_dir=v["data_dir"],
                  timeout=float(v["timeout"]), prompt="", quiet=v["quiet"], json=v["json"], no_save=v["no_save"],
                  max_tokens=v["max_tokens"], temperature=v["temperature"], top_p=v["top_p"], top_k=v["top_k"],
-                 seed=v["seed"], gpus=v["gpus"], trace=v["trace"])
+                 seed=v["seed"], gpus=v["gpus"], trace=v["trace"], placement=v["placement"])
     cfg.prompt = get_prompt(rest, cfg.file, stdin)
     return cfg
 
@@ -194,7 +198,11 @@ def init_registry(cfg: Config) -> Registry:
         gpus = [int(x) for x in cfg.gpus.split(",") if x.strip()] if cfg.gpus else None
         counts = {m: cfg.models.count(m) for m in cfg.models}
         try:
-            backend = LocalBackend(local_specs, judge=cfg.judge, gpus=gpus, trace=cfg.trace, counts=counts)
+            from .parallel.placement import parse_pins
+
+            pins = parse_pins(cfg.placement) if cfg.placement else None
+            backend = LocalBackend(local_specs, judge=cfg.judge, gpus=gpus, trace=cfg.trace, counts=counts,
+                                   pins=pins)
         except Exception as e:  # noqa: BLE001
             raise CLIError(f"initializing provider for {local_specs[0].name}: {e}") from None
         for spec in local_specs:

@@ -44,7 +44,27 @@ class PlacementError(Exception):
     pass
 
 
-def solve(demands: Sequence[ModelDemand], gpu_ids: Sequence[int], hbm_bytes: int = HBM_BYTES) -> Placement:
+def parse_pins(spec: str) -> Dict[str, List[int]]:
+    """``--placement`` syntax: ``model=g[+g...][,model=g...]`` (a '+'-joined list is a TP group)."""
+    pins: Dict[str, List[int]] = {}
+    for item in filter(None, (x.strip() for x in (spec or "").split(","))):
+        name, sep, gs = item.rpartition("=")
+        if not sep or not name.strip():
+            raise PlacementError(f"bad placement entry {item!r} (want model=gpu[+gpu...])")
+        try:
+            ids = [int(x) for x in gs.split("+")]
+        except ValueError:
+            raise PlacementError(f"bad GPU list in placement entry {item!r}") from None
+        if len(set(ids)) != len(ids):
+            raise PlacementError(f"duplicate GPU in placement entry {item!r}")
+        pins[name.strip()] = ids
+    return pins
+
+
+def solve(demands: Sequence[ModelDemand], gpu_ids: Sequence[int], hbm_bytes: int = HBM_BYTES,
+          pins: Optional[Dict[str, List[int]]] = None) -> Placement:
+    """Place every demand; ``pins`` (``--placement``) fixes some models' GPUs first — a pinned
+    list of n GPUs makes that model TP=n — and the rules below place the rest around them."""
     gpu_ids = list(gpu_ids)
     if not gpu_ids:
         raise PlacementError("no GPUs available")
@@ -52,6 +72,10 @@ def solve(demands: Sequence[ModelDemand], gpu_ids: Sequence[int], hbm_bytes: int
     used = {g: 0.0 for g in gpu_ids}
     count = {g: 0 for g in gpu_ids}
     out: Dict[str, List[int]] = {}
+    pins = dict(pins or {})
+    unknown = sorted(set(pins) - {d.name for d in demands})
+    if unknown:
+        raise PlacementError(f"placement names models not in the run: {unknown}")
 
     def fits(g: int, b: float) -> bool:
         return used[g] + b <= cap
@@ -62,6 +86,19 @@ def solve(demands: Sequence[ModelDemand], gpu_ids: Sequence[int], hbm_bytes: int
             count[g] += 1
         out[name] = gs
 
+    # 0. pinned models, as given
+    for d in demands:
+        gs = pins.get(d.name)
+        if gs is None:
+            continue
+        bad = [g for g in gs if g not in used]
+        if bad:
+            raise PlacementError(f"{d.name}: placement GPU(s) {bad} not available (have {gpu_ids})")
+        per = (d.weight_bytes + d.kv_bytes) / len(gs)
+        if not all(fits(g, per) for g in gs):
+            raise PlacementError(f"{d.name}: {per / 1e9:.1f} GB per GPU does not fit on {gs}")
+        take(d.name, list(gs), per)
+    demands = [dataclasses.replace(d) for d in demands if d.name not in pins]
     # 1. tensor-parallel models: aligned contiguous groups, least-loaded group first
     for d in sorted((d for d in demands if d.tp > 1), key=lambda d: -d.tp):
         if d.tp > len(gpu_ids):

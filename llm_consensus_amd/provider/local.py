@@ -94,7 +94,8 @@ class LocalBackend:
 
     def __init__(self, specs: List[ModelSpec], judge: Optional[str] = None, gpus: Optional[List[int]] = None,
                  trace: bool = False, counts: Optional[Dict[str, int]] = None,
-                 max_context: Optional[Dict[str, int]] = None, start_timeout: float = 1800.0):
+                 max_context: Optional[Dict[str, int]] = None, start_timeout: float = 1800.0,
+                 pins: Optional[Dict[str, List[int]]] = None):
         import multiprocessing as mp
 
         self.specs = {s.name: s for s in specs}
@@ -118,9 +119,9 @@ class LocalBackend:
             ctx_len = (max_context or {}).get(s.name) or min(c.max_position,
                                                              JUDGE_CONTEXT if s.name == judge else RESPONDER_CONTEXT)
             self._ctx[s.name] = ctx_len
-            tp = 1 if force_cpu else min(c.default_tp, len(gpu_ids))
+            tp = 1 if force_cpu else (len(pins[s.name]) if pins and s.name in pins else min(c.default_tp, len(gpu_ids)))
             demands.append(ModelDemand(s.name, c.weight_bytes(), c.kv_bytes_per_token() * ctx_len, tp, s.name == judge))
-        self.placement = solve(demands, gpu_ids) if not force_cpu else None
+        self.placement = solve(demands, gpu_ids, pins=pins) if not force_cpu else None
         if force_cpu:
             from ..parallel.placement import Placement
 

@@ -80,27 +80,6 @@ def bench_gemv():
         print(f"gemv N={N:6d} K={K:5d} epi={epi}: {us:8.2f} us  {N * K * 2 / us / 1e6:6.2f} TB/s")
 
 
-def bench_mall():
-    """Does a weight matrix read shortly before a GEMV (e.g. by idle CUs during attention) make the
-    GEMV faster (MALL / L2 hits)? Each variant first streams 1 GiB to flush the caches."""
-    big = torch.empty(512 * 1024 * 1024, dtype=BF, device="cuda")
-    sink = torch.empty(1, dtype=BF, device="cuda")
-    for (N, K) in [(4096, 4096), (6144, 4096)]:
-        x = torch.randn(1, K, device="cuda").to(BF)
-        W = (torch.randn(N, K, device="cuda") * 0.02).to(BF)
-        W2 = torch.empty_like(W)
-        out = torch.zeros(1, N, dtype=BF, device="cuda")
-        t_flush = timeit(lambda: torch.sum(big, dim=0, keepdim=True, out=sink), iters=5)
-        t_pre = timeit(lambda: (torch.sum(big, dim=0, keepdim=True, out=sink),
-                                torch.sum(W.view(-1), dim=0, keepdim=True, out=sink),
-                                ops.gemv(x, W, 0, out=out)), iters=5)
-        t_other = timeit(lambda: (torch.sum(big, dim=0, keepdim=True, out=sink),
-                                  torch.sum(W2.view(-1), dim=0, keepdim=True, out=sink),
-                                  ops.gemv(x, W, 0, out=out)), iters=5)
-        print(f"mall N={N} K={K}: flush {t_flush:.1f} us; flush+read(W)+gemv {t_pre:.1f}; "
-              f"flush+read(W2)+gemv {t_other:.1f} -> gemv saving from prior read {t_other - t_pre:.2f} us")
-
-
 SWEEP = ["256x1u8", "256x2u4", "256x4u4", "512x1u8", "512x2u4", "128x1u8", "64x1u8", "1024x1u4", "256x1u4",
          "256x2u8", "512x4u2", "128x2u4", "1024x1u8", "1024x2u4", "1024x2u2", "1024x1u2", "768x1u4", "1024x4u2", "1024x1u6"]
 
@@ -181,8 +160,6 @@ if __name__ == "__main__":
         bench_attn()
     if what in ("gemv", "all"):
         bench_gemv()
-    if what in ("mall",):
-        bench_mall()
     if what in ("sweep",):
         bench_gemv_sweep()
     if what in ("prefill",):

@@ -156,3 +156,22 @@ def test_judge_prompt_template_golden():
 
     golden = open(os.path.join(os.path.dirname(__file__), "golden", "judge_prompt_say_hello.txt")).read()
     assert captured["p"] == golden == build_judge_prompt("Say hello", rs)
+
+
+def test_placement_pins_and_parse():
+    from llm_consensus_amd.parallel.placement import ModelDemand, PlacementError, parse_pins, solve
+
+    assert parse_pins("a=0, b@1=2+3") == {"a": [0], "b@1": [2, 3]}
+    for bad in ("a", "a=x", "a=1+1", "=2"):
+        with pytest.raises(PlacementError):
+            parse_pins(bad)
+    G = 10**9
+    ds = [ModelDemand("big", 140 * G, 10 * G, tp=4), ModelDemand("r1", 16 * G, 2 * G), ModelDemand("r2", 16 * G, 2 * G),
+          ModelDemand("j", 16 * G, 5 * G, is_judge=True)]
+    p = solve(ds, list(range(8)), pins={"big": [4, 5, 6, 7], "j": [0]})
+    assert p.gpus["big"] == [4, 5, 6, 7] and p.gpus["j"] == [0]
+    assert all(g[0] in (1, 2, 3) for m, g in p.gpus.items() if m in ("r1", "r2"))  # spread off the pinned GPUs
+    with pytest.raises(PlacementError):
+        solve(ds, list(range(8)), pins={"nope": [0]})
+    with pytest.raises(PlacementError):
+        solve(ds, list(range(4)), pins={"j": [5]})

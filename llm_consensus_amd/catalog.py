@@ -1,5 +1,9 @@
 """Model catalog: which names the CLI accepts and which provider serves them.
 
+Three kinds of names: local architectures (and ``--weights-dir`` checkpoints) served by the
+MI355X engines, the reference's hosted model ids (served by ``provider/remote.py`` when their API
+key is set), and the deterministic ``stub-*`` CPU family.
+
 Reference: the closed ``knownModels`` map + ``createProvider`` (``cmd/llm-consensus/main.go:38-61,
 417-438``) and the never-loaded ``models.json`` catalog produced by ``model-registry-sync``.
 Here the catalog is the set of local architectures (``models/config.py``) plus a deterministic
@@ -40,10 +44,16 @@ class ModelSpec:
 
 
 def available_models() -> List[str]:
-    return sorted(FAMILIES) + ["stub-<name>"]
+    from .provider.remote import KNOWN_REMOTE
+
+    return sorted(FAMILIES) + sorted(KNOWN_REMOTE) + ["stub-<name>"]
 
 
 def resolve(name: str) -> ModelSpec:
+    from .provider.remote import KNOWN_REMOTE
+
+    if name in KNOWN_REMOTE:  # the reference's hosted models (main.go:47-61), exact ids
+        return ModelSpec(name, name, "", KNOWN_REMOTE[name], None)
     family, _, tag = name.partition("@")
     if family in FAMILIES:
         return ModelSpec(name, family, tag, PROVIDER_LOCAL, FAMILIES[family])
@@ -56,7 +66,7 @@ def describe(name: str, tp: Optional[int] = None) -> Dict:
     """One catalog record (the ``model-registry-sync`` analogue)."""
     spec = resolve(name)
     if spec.config is None:
-        return {"source": "stub", "id": name}
+        return {"source": spec.provider, "id": name}
     c = spec.config
     tp = tp or c.default_tp
     return {

@@ -23,7 +23,7 @@ import time
 from typing import List, Optional, TextIO
 
 from . import ui
-from .catalog import PROVIDER_STUB, UnknownModel, dump_catalog, resolve
+from .catalog import PROVIDER_LOCAL, PROVIDER_STUB, UnknownModel, dump_catalog, resolve
 from .consensus import Judge, prompt_header, response_block
 from .context import Context
 from .flags import FlagSet, parse_or_exit
@@ -190,8 +190,15 @@ def init_registry(cfg: Config) -> Registry:
             from .provider.stub import StubProvider
 
             reg.register(m, StubProvider(m))
-        else:
+        elif spec.provider == PROVIDER_LOCAL:
             local_specs.append(spec)
+        else:  # hosted API (reference providers)
+            from .provider.remote import RemoteError, create
+
+            try:
+                reg.register(m, create(m, spec.provider))
+            except RemoteError as e:
+                raise CLIError(f"initializing provider for {m}: {e}") from None
     if local_specs:
         from .provider.local import LocalBackend
 

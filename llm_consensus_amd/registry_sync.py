@@ -8,7 +8,10 @@ local sources, kept with the same flag style, record shape and failure semantics
 
 * ``local``       — the built-in random-init architectures (``models/config.py``);
 * ``checkpoint``  — Hugging Face checkpoint directories (``-weights-dir``, ``$LLMC_WEIGHTS_DIR``);
-* ``hf-cache``    — snapshots in the Hugging Face hub cache (``$HF_HOME``/hub, read-only scan).
+* ``hf-cache``    — snapshots in the Hugging Face hub cache (``$HF_HOME``/hub, read-only scan);
+* ``openai`` / ``openrouter`` — the reference's own remote sources, same requests and records
+  (``GET {base}/models``; OpenAI needs ``OPENAI_API_KEY``, OpenRouter sends ``OPENROUTER_API_KEY``
+  when set; main.go:129-213), base URLs overridable (``OPENAI_BASE_URL``, ``OPENROUTER_BASE_URL``).
 
 Each record: ``source``, ``id``, ``name``, ``context_length`` (the reference's fields, pricing
 dropped: local inference has none) plus what placement needs (params, bf16 weight bytes, KV bytes
@@ -85,6 +88,52 @@ def hf_cache_records(raw: bool, deadline: float) -> List[dict]:
     return out
 
 
+def _get_json(url: str, headers: dict, timeout: float):
+    import httpx
+
+    r = httpx.get(url, headers=headers, timeout=timeout)
+    if r.status_code < 200 or r.status_code >= 300:
+        body = r.text
+        raise RuntimeError(f"http {r.status_code}: {body[:600] + ('…' if len(body) > 600 else '')}")
+    try:
+        return r.json()
+    except ValueError as e:
+        raise RuntimeError(f"unmarshal: {e}; body={r.text[:600]}") from None
+
+
+def openai_records(raw: bool, timeout: float) -> List[dict]:
+    key = os.environ.get("OPENAI_API_KEY", "").strip()
+    if not key:
+        raise RuntimeError("OPENAI_API_KEY not set")
+    base = os.environ.get("OPENAI_BASE_URL", "https://api.openai.com/v1").rstrip("/")
+    data = _get_json(f"{base}/models", {"Authorization": f"Bearer {key}"}, timeout)
+    out = []
+    for m in data.get("data") or []:
+        rec = {"source": "openai", "id": m.get("id", "")}
+        if raw:
+            rec["raw"] = m
+        out.append(rec)
+    return out
+
+
+def openrouter_records(raw: bool, timeout: float) -> List[dict]:
+    base = os.environ.get("OPENROUTER_BASE_URL", "https://openrouter.ai/api/v1").rstrip("/")
+    key = os.environ.get("OPENROUTER_API_KEY", "").strip()
+    data = _get_json(f"{base}/models", {"Authorization": f"Bearer {key}"} if key else {}, timeout)
+    out = []
+    for m in data.get("data") or []:
+        rec = {"source": "openrouter", "id": m.get("id", "")}
+        if m.get("name"):
+            rec["name"] = m["name"]
+        if m.get("context_length"):
+            rec["context_length"] = m["context_length"]
+        rec["pricing"] = {k: (m.get("pricing") or {}).get(k, "") for k in ("prompt", "completion", "request", "image")}
+        if raw:
+            rec["raw"] = m
+        out.append(rec)
+    return out
+
+
 def main(argv: Optional[List[str]] = None, stdout: TextIO = sys.stdout, stderr: TextIO = sys.stderr) -> int:
     fs = FlagSet("model-registry-sync")
     fs.add("out", "string", "", "output file path (defaults to stdout)")
@@ -92,7 +141,9 @@ def main(argv: Optional[List[str]] = None, stdout: TextIO = sys.stdout, stderr: 
     fs.add("local", "bool", True, "list the built-in architectures")
     fs.add("weights-dir", "string", "", "comma-separated checkpoint dirs to scan (default $LLMC_WEIGHTS_DIR)")
     fs.add("hf-cache", "bool", True, "scan the Hugging Face hub cache")
-    fs.add("timeout", "int", 20, "scan timeout in seconds")
+    fs.add("openai", "bool", True, "fetch OpenAI models (requires OPENAI_API_KEY)")
+    fs.add("openrouter", "bool", True, "fetch OpenRouter models (uses OPENROUTER_API_KEY if set)")
+    fs.add("timeout", "int", 20, "HTTP / scan timeout in seconds")
     v, _ = parse_or_exit(fs, list(sys.argv[1:] if argv is None else argv), stderr)
     deadline = time.monotonic() + max(1, v["timeout"])
     all_recs: List[dict] = []
@@ -111,6 +162,12 @@ def main(argv: Optional[List[str]] = None, stdout: TextIO = sys.stdout, stderr: 
             all_recs += hf_cache_records(v["raw"], deadline)
         except Exception as e:  # noqa: BLE001
             errs.append(f"hf-cache: {e}")
+    for flag, name, fn in (("openai", "openai", openai_records), ("openrouter", "openrouter", openrouter_records)):
+        if v[flag]:
+            try:
+                all_recs += fn(v["raw"], float(v["timeout"]))
+            except Exception as e:  # noqa: BLE001
+                errs.append(f"{name}: {e}")
     all_recs.sort(key=lambda r: (r["source"], r["id"]))
     payload = json.dumps(all_recs, indent=2)
     if v["out"] == "":

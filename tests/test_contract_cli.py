@@ -220,7 +220,8 @@ def test_model_registry_sync(tmp_path):
 
     out = tmp_path / "models.json"
     r = subprocess.run([sys.executable, "-m", "llm_consensus_amd.registry_sync", "-out", str(out), "-hf-cache=false",
-                        "-weights-dir", str(tmp_path / "missing")], capture_output=True, cwd=ROOT, timeout=120)
+                        "-openai=false", "-openrouter=false", "-weights-dir", str(tmp_path / "missing")],
+                       capture_output=True, cwd=ROOT, timeout=120)
     assert r.returncode == 0
     recs = json.loads(out.read_text())
     assert [(x["source"], x["id"]) for x in recs] == sorted((x["source"], x["id"]) for x in recs)

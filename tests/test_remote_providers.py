@@ -41,6 +41,15 @@ class _H(BaseHTTPRequestHandler):
         self.end_headers()
         self.wfile.write(data)
 
+    def do_GET(self):
+        SEEN.append((self.path, dict(self.headers), None))
+        if self.path == "/oa/models":
+            return self._json({"object": "list", "data": [{"id": "gpt-b", "object": "model"}, {"id": "gpt-a"}]})
+        if self.path == "/or/models":
+            return self._json({"data": [{"id": "x/y", "name": "Y", "context_length": 8192,
+                                         "pricing": {"prompt": "1", "completion": "2"}}]})
+        self._json({"error": "no route"}, 404)
+
     def do_POST(self):
         body = json.loads(self.rfile.read(int(self.headers["Content-Length"])))
         SEEN.append((self.path, dict(self.headers), body))
@@ -144,3 +153,18 @@ def test_cli_with_hosted_models(server, tmp_path):
                         "x"], cwd=ROOT, env=env, capture_output=True, timeout=120)
     assert r.returncode == 1
     assert b"error: initializing provider for gemini-3-pro-preview: GOOGLE_API_KEY environment variable required" in r.stderr
+
+
+def test_registry_sync_remote_sources(server, tmp_path):
+    env = dict(os.environ, OPENAI_API_KEY="k", OPENAI_BASE_URL=server + "/oa", OPENROUTER_BASE_URL=server + "/or")
+    r = subprocess.run([sys.executable, "-m", "llm_consensus_amd.registry_sync", "-local=false", "-hf-cache=false"],
+                       cwd=ROOT, env=env, capture_output=True, timeout=120)
+    assert r.returncode == 0, r.stderr.decode()
+    recs = json.loads(r.stdout)
+    assert recs == [{"source": "openai", "id": "gpt-a"}, {"source": "openai", "id": "gpt-b"},
+                    {"source": "openrouter", "id": "x/y", "name": "Y", "context_length": 8192,
+                     "pricing": {"prompt": "1", "completion": "2", "request": "", "image": ""}}]
+    env.pop("OPENAI_API_KEY")
+    r = subprocess.run([sys.executable, "-m", "llm_consensus_amd.registry_sync", "-local=false", "-hf-cache=false"],
+                       cwd=ROOT, env=env, capture_output=True, timeout=120)
+    assert r.returncode == 0 and b"openai: OPENAI_API_KEY not set" in r.stderr

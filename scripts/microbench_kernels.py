@@ -84,13 +84,13 @@ SWEEP = ["256x1u8", "256x2u4", "256x4u4", "512x1u8", "512x2u4", "128x1u8", "64x1
          "256x2u8", "512x4u2", "128x2u4", "1024x1u8", "1024x2u4", "1024x2u2", "1024x1u2", "768x1u4", "1024x4u2", "1024x1u6"]
 
 
-def bench_gemv_sweep():
+def bench_gemv_sweep(shapes=None):
     """GEMV geometry sweep on COLD weights: the graph cycles through enough copies of W to exceed
     the 256 MB MALL, as in a real decode step (16 GB streamed per token)."""
     from llm_consensus_amd.utils.native import kernels
 
     k = kernels()
-    for (N, K) in [(6144, 4096), (4096, 4096), (28672, 4096), (4096, 14336), (128256, 4096)]:
+    for (N, K) in shapes or [(6144, 4096), (4096, 4096), (28672, 4096), (4096, 14336), (128256, 4096)]:
         if K * 2 > 64 * 1024:
             continue
         copies = max(2, (1 << 30) // (N * K * 2))
@@ -100,7 +100,7 @@ def bench_gemv_sweep():
         out = torch.zeros(1, N, dtype=BF, device="cuda")
         res = []
         for v, name in enumerate(SWEEP):
-            if name not in ("256x4u4", "256x2u4", "512x1u8", "1024x1u4", "1024x1u6", "1024x1u8"):
+            if name not in ("256x2u4", "512x1u8", "1024x1u4", "1024x1u6", "1024x1u8", "768x1u4", "1024x1u2"):
                 continue
             st = torch.cuda.current_stream().cuda_stream
 
@@ -162,5 +162,7 @@ if __name__ == "__main__":
         bench_gemv()
     if what in ("sweep",):
         bench_gemv_sweep()
+    if what in ("sweep-phi3",):  # Phi-3-mini shapes (K = 3072 / 8192)
+        bench_gemv_sweep([(9216, 3072), (16384, 3072), (3072, 3072), (3072, 8192)])
     if what in ("prefill",):
         bench_prefill()

@@ -46,7 +46,7 @@ def test_embedding_and_silu(cuda):
 
 
 @pytest.mark.parametrize("M", [1, 2, 3, 4])
-@pytest.mark.parametrize("N,K", [(64, 256), (1000, 4096), (4096, 4096), (512, 14336), (130, 192)])
+@pytest.mark.parametrize("N,K", [(64, 256), (1000, 4096), (4096, 4096), (512, 14336), (130, 192), (6144, 512), (9216, 256)])
 @pytest.mark.parametrize("epi", [0, 1, 2, 3])
 def test_gemv(cuda, M, N, K, epi):
     if M > 1 and K > 8192:

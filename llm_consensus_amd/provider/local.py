@@ -119,13 +119,19 @@ class LocalBackend:
             ctx_len = (max_context or {}).get(s.name) or min(c.max_position,
                                                              JUDGE_CONTEXT if s.name == judge else RESPONDER_CONTEXT)
             self._ctx[s.name] = ctx_len
-            tp = 1 if force_cpu else (len(pins[s.name]) if pins and s.name in pins else min(c.default_tp, len(gpu_ids)))
+            if pins and s.name in pins:
+                tp = len(pins[s.name])
+            else:
+                tp = 1 if force_cpu else min(c.default_tp, len(gpu_ids))
             demands.append(ModelDemand(s.name, c.weight_bytes(), c.kv_bytes_per_token() * ctx_len, tp, s.name == judge))
-        self.placement = solve(demands, gpu_ids, pins=pins) if not force_cpu else None
-        if force_cpu:
+        if force_cpu and not pins:
             from ..parallel.placement import Placement
 
+            # CPU workers: round-robin (tests); with --placement pins, the solver as on GPUs (CPU TP
+            # groups run over gloo, so config-4/5 style TP judges are testable without GPUs)
             self.placement = Placement({s.name: [gpu_ids[i % len(gpu_ids)]] for i, s in enumerate(specs)})
+        else:
+            self.placement = solve(demands, gpu_ids, pins=pins)
         trace_on = trace
         used = self.placement.used_gpus()
         groups = [(m, sorted(g)) for m, g in self.placement.gpus.items() if len(g) > 1]

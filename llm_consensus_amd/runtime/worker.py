@@ -191,6 +191,15 @@ class _AllCtx:
 
 def worker_main(gpu: int, conn, models: List[dict], dist_info: Optional[dict], trace_on: bool) -> None:
     """Entry point of a worker process (multiprocessing spawn target)."""
+    # The driver owns stdout (--json writes the result there); native libraries in the worker
+    # (gloo's connection banner, RCCL debug output) print to fd 1 -> send it to stderr.
+    try:
+        import sys
+
+        sys.stdout.flush()
+        os.dup2(2, 1)
+    except OSError:
+        pass
     send_lock = threading.Lock()
 
     def send(msg) -> None:

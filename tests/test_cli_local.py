@@ -93,3 +93,17 @@ def test_cli_worker_crash_isolated_cpu():
     assert [r["model"] for r in d["responses"]] == ["llama-tiny@1"]
     assert d["failed_models"] == ["phi3-tiny"]
     assert any("exited" in w for w in d["warnings"]), d["warnings"]
+
+
+def test_cli_tp_judge_over_cpu_workers():
+    """Config-5 shape on CPU workers: responders of three families plus a TP=2 judge pinned over two
+    worker processes (gloo collectives): the incremental judge session (open / extend / finish) is
+    broadcast to both TP ranks and only rank 0 streams."""
+    rc, out, err = run_cli(["--models", "mixtral-tiny,llama-tiny@1,phi3-tiny", "--judge", "llama-tiny@j",
+                            "--placement", "llama-tiny@j=-1+-2", "--max-tokens", "8", "--temperature", "0",
+                            "--json", "Explain paged attention."],
+                           env={"LLMC_DEVICE": "cpu", "LLMC_CPU_WORKERS": "3"})
+    assert rc == 0, err
+    d = json.loads(out)
+    assert sorted(r["model"] for r in d["responses"]) == ["llama-tiny@1", "mixtral-tiny", "phi3-tiny"]
+    assert d["judge"] == "llama-tiny@j" and len(d["consensus"]) > 0

@@ -268,6 +268,7 @@ def _run_with_registry(cfg: Config, registry: Registry, ctx: Context, show_ui: b
     runner = Runner(registry, cfg.timeout, tmpl).with_callbacks(Callbacks(
         on_model_start=progress.model_started,
         on_model_stream=progress.model_streaming,
+        on_model_tokens=progress.model_tokens,
         on_model_complete=progress.model_completed,
         on_model_error=progress.model_failed,
         on_model_response=on_resp,
@@ -295,9 +296,12 @@ def _run_with_registry(cfg: Config, registry: Registry, ctx: Context, show_ui: b
     jprog.model_started(cfg.judge)
     # The judge gets the per-model timeout too (no hidden 60 s cap).
     jctx = ctx.with_timeout(cfg.timeout)
+    def judge_stream(chunk: str) -> None:
+        jprog.model_streaming(cfg.judge, chunk)
+
+    judge_stream.tokens_hook = lambda n: jprog.model_tokens(cfg.judge, n)  # type: ignore[attr-defined]
     try:
-        consensus = judge.synthesize_stream(jctx, cfg.prompt, result.responses,
-                                            lambda chunk: jprog.model_streaming(cfg.judge, chunk))
+        consensus = judge.synthesize_stream(jctx, cfg.prompt, result.responses, judge_stream)
         err = None
     except Exception as e:  # noqa: BLE001
         consensus, err = "", e

@@ -282,6 +282,9 @@ class LocalProvider:
                     if not ttft:
                         ttft = time.monotonic_ns() - t0
                     ntok += len(msg[2])
+                    hook = getattr(callback, "tokens_hook", None)
+                    if hook is not None:
+                        hook(len(msg[2]))
                     chunk = dec.push(msg[2])
                     if chunk:
                         parts.append(chunk)

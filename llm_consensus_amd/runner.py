@@ -30,6 +30,9 @@ from .provider.registry import Registry
 class Callbacks:
     on_model_start: Optional[Callable[[str], None]] = None
     on_model_stream: Optional[Callable[[str, str], None]] = None
+    # extension: exact generated-token counts from local engines (the UI shows them instead of
+    # the reference's chars/4 estimate, ui.go:142)
+    on_model_tokens: Optional[Callable[[str, int], None]] = None
     on_model_complete: Optional[Callable[[str], None]] = None
     on_model_error: Optional[Callable[[str, BaseException], None]] = None
     # Extension (no reference counterpart): the Response itself, called under the result lock
@@ -93,6 +96,9 @@ class Runner:
             def stream(chunk: str) -> None:
                 if cb and cb.on_model_stream:
                     cb.on_model_stream(model, chunk)
+
+            if cb and cb.on_model_tokens:
+                stream.tokens_hook = lambda n, _m=model: cb.on_model_tokens(_m, n)  # type: ignore[attr-defined]
 
             err: Optional[BaseException] = None
             resp: Optional[Response] = None

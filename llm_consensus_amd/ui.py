@@ -130,6 +130,14 @@ class Progress:
                 st.token_est = st.exact_tokens if st.exact_tokens is not None else st.char_count // 4
                 st.last_chunk = truncate_bytes(chunk, 30)
 
+    def model_tokens(self, model: str, n: int) -> None:
+        """Exact generated-token count from a local engine (replaces the chars/4 estimate)."""
+        with self._lock:
+            st = self._models.get(model)
+            if st:
+                st.exact_tokens = (st.exact_tokens or 0) + n
+                st.token_est = st.exact_tokens
+
     def model_completed(self, model: str) -> None:
         with self._lock:
             st = self._models.get(model)

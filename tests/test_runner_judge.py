@@ -175,3 +175,17 @@ def test_placement_pins_and_parse():
         solve(ds, list(range(8)), pins={"nope": [0]})
     with pytest.raises(PlacementError):
         solve(ds, list(range(4)), pins={"j": [5]})
+
+
+def test_progress_exact_token_counts():
+    import io
+
+    from llm_consensus_amd.ui import Progress
+
+    p = Progress(io.StringIO(), ["m"], quiet=False)
+    p.model_started("m")
+    p.model_streaming("m", "abcdefgh")  # chars/4 estimate: 2
+    assert p._models["m"].token_est == 2
+    p.model_tokens("m", 5)  # exact counts from a local engine take over
+    p.model_streaming("m", "ijkl")
+    assert p._models["m"].token_est == 5

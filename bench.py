@@ -5,8 +5,13 @@ output tokens/sec, N-model fan-out), configs 2/3 generalised to N GPUs:
   * one process per GPU (torchrun; RCCL over xGMI for the gather), weak scaling:
     each GPU hosts ``--models-per-gpu`` Llama-3-8B responders (distinct random-init replicas,
     ``llama-3-8b@<i>``), so an N-GPU run is an (N x models-per-gpu)-model fan-out;
-  * the Llama-3-8B judge lives on GPU 0 beside rank 0's responder(s) on its own hipStream
-    (config 3: "judge time-shares GPU 0 via concurrent hipStreams");
+  * the Llama-3-8B judge time-shares the responders' GPUs on its own hipStream(s): by default
+    it is tensor-parallel over the first ``--judge-tp`` ranks (auto = every rank whose count
+    divides the judge's heads/vocab), so the judge phase — which the reference's semantics make
+    strictly sequential after the fan-out (cmd/llm-consensus/main.go:132 then :161) — uses the
+    HBM bandwidth of every GPU that just went idle instead of one: TP shards with RCCL for
+    prefill-sized all-reduces and the custom one-shot xGMI all-reduce/all-gather inside the
+    captured decode graphs. ``--judge-tp 1`` keeps it on GPU 0 only (config 3 as written);
   * one timed step = one full consensus round exactly as ``llm-consensus`` runs it: every
     responder prefills the prompt and decodes ``--max-tokens`` tokens, the responses are
     gathered to rank 0, the judge prompt is rendered with the reference template
@@ -36,6 +41,17 @@ def log(*a):
     print(f"[bench r{os.environ.get('RANK', '0')}]", *a, file=sys.stderr, flush=True)
 
 
+def judge_tp_degree(cfg, world: int, requested: int) -> int:
+    """TP degree of the bench judge: ``requested`` if > 0, else the largest t <= min(world, 8)
+    that shards the judge's heads, kv heads, FFN and vocab evenly (8 = custom all-reduce limit)."""
+    if requested > 0:
+        return requested
+    for t in range(min(world, 8), 0, -1):
+        if not (cfg.n_heads % t or cfg.n_kv_heads % t or cfg.intermediate % t or cfg.vocab % t):
+            return t
+    return 1
+
+
 def main() -> None:
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -48,6 +64,7 @@ def main() -> None:
     ap.add_argument("--judge-max-tokens", type=int, default=0, help="0 = same as --max-tokens")
     ap.add_argument("--prompt-tokens", type=int, default=128)
     ap.add_argument("--temperature", type=float, default=1.0)
+    ap.add_argument("--judge-tp", type=int, default=0, help="0 = auto (largest valid TP <= ranks), 1 = GPU 0 only")
     ap.add_argument("--steps-per-graph", type=int, default=8)
     ap.add_argument("--no-graphs", action="store_true")
     ap.add_argument("--results-dir", default=os.path.join(ROOT, "bench", "results"),
@@ -107,13 +124,24 @@ def main() -> None:
         responders.append((idx, e))
     judge = None
     judge_ctx = 0
-    if rank == 0 and n_models > 1:
+    jtp = judge_tp_degree(jcfg, world, args.judge_tp) if n_models > 1 else 1
+    if n_models > 1 and rank < jtp:
+        from llm_consensus_amd.parallel.comm import TPGroup
+
+        tp = TPGroup.single()
+        if jtp > 1:
+            # judge TP group = ranks 0..jtp-1 (the whole world by default); new_group is collective
+            grp = dist.group.WORLD if jtp == world else dist.new_group(list(range(jtp)))
+            tp = TPGroup(grp, rank, jtp)
+            tp.enable_custom(dev)
         # responses are decoded to text and re-tokenized by the judge: random byte tokens can expand
         # (invalid UTF-8 -> U+FFFD -> 3 byte tokens), so budget 2x per response
         judge_ctx = len(prompt_ids) + 1024 + n_models * (2 * args.max_tokens + 64) + jmax + 64
         judge = Engine(jcfg, EngineConfig(device=dev, max_context=judge_ctx, seed=777,
                                           steps_per_graph=args.steps_per_graph, use_graphs=not args.no_graphs),
-                       name=f"{args.judge}@judge")
+                       tp=tp, name=f"{args.judge}@judge")
+    elif n_models > 1 and 1 < jtp < world:
+        dist.new_group(list(range(jtp)))  # every rank takes part in creating the sub-group
     # capture every decode graph up front (a capture beside another engine's running stream is
     # invalid; the worker process does the same before serving)
     if not args.no_graphs:
@@ -160,24 +188,26 @@ def main() -> None:
         else:
             all_t = local_t.unsqueeze(0)
         n_tokens = n_models * args.max_tokens
-        if rank == 0:
+        if judge is not None:
+            # every judge rank renders the same prompt from the gathered rows (deterministic), so
+            # the TP shards prefill/decode in lockstep; rank 0 accounts the tokens
             rows = all_t.view(n_models, args.max_tokens).cpu().tolist()
             responses = []
             for i, r in enumerate(rows):
                 r = [t for t in r if t >= 0]
                 responses.append(Response(model=f"{args.model}@{i}", content=tok.decode(r), provider="rocm"))
-            if judge is not None and len(responses) > 1:
-                full = build_judge_prompt(prompt_text, responses)
-                head = prompt_header(prompt_text)
-                rest_ids = jtok.encode(full[len(head):])
-                judge.prefill([jseq], [rest_ids])
-                t_jp = time.perf_counter()
-                jids = judge.decode([jseq], [SamplingParams(jmax, args.temperature, 1.0, 0, 99 + step, False)])[0]
-                stats["judge_prompt_tokens"] = jseq.length - len(jids)
-                stats["judge_prefill_s"] = t_jp - t_resp
+            full = build_judge_prompt(prompt_text, responses)
+            head = prompt_header(prompt_text)
+            rest_ids = jtok.encode(full[len(head):])
+            judge.prefill([jseq], [rest_ids])
+            t_jp = time.perf_counter()
+            jids = judge.decode([jseq], [SamplingParams(jmax, args.temperature, 1.0, 0, 99 + step, False)])[0]
+            stats["judge_prompt_tokens"] = jseq.length - len(jids)
+            stats["judge_prefill_s"] = t_jp - t_resp
+            stats["judge_decode_s"] = time.perf_counter() - t_jp
+            if rank == 0:
                 n_tokens += len(jids)
-            if jseq is not None:
-                judge.free_sequence(jseq)
+            judge.free_sequence(jseq)
         torch.cuda.synchronize()
         if world > 1:
             dist.barrier()
@@ -229,18 +259,22 @@ def main() -> None:
             "dtype": "bf16",
             "data": "synthetic prompt (synthetic tokenizer), random-init weights",
             "config": {
-                "model": f"{n_models}x {args.model} responders ({mpg}/GPU) + {args.judge} judge on GPU0 stream",
+                "model": f"{n_models}x {args.model} responders ({mpg}/GPU) + {args.judge} judge "
+                         + (f"TP={jtp} on GPUs 0-{jtp - 1} (own streams)" if jtp > 1 else "on GPU0 stream"),
                 "global_batch": n_models,
                 "seq_len": len(prompt_ids) + args.max_tokens,
                 "max_tokens": args.max_tokens,
                 "prompt_tokens": len(prompt_ids),
-                "parallelism": f"fanout{n_models}" + ("" if n_gpus == 1 else f"-dp{n_gpus}"),
+                "parallelism": f"fanout{n_models}" + ("" if n_gpus == 1 else f"-dp{n_gpus}")
+                               + (f"-judge_tp{jtp}" if jtp > 1 else ""),
             },
             "extra": {
                 "p50_e2e_latency_s": round(statistics.median(lat), 3),
                 "responder_decode_tok_s_per_model": round(resp_tok_s / n_models, 2),
                 "judge_prompt_tokens": per_step[-1].get("judge_prompt_tokens", 0),
                 "judge_prefill_s": round(per_step[-1].get("judge_prefill_s", 0.0), 3),
+                "judge_decode_s": round(per_step[-1].get("judge_decode_s", 0.0), 3),
+                "judge_tp": jtp,
             },
         }
         print(json.dumps(out), flush=True)

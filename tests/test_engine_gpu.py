@@ -13,6 +13,15 @@ from llm_consensus_amd.parallel.comm import TPGroup
 
 pytestmark = pytest.mark.gpu
 
+# Per-rank shapes of the Llama-3-8B judge under TP=8 / TP=4 (bench.py shards it over every GPU):
+# 4 or 8 query heads, ONE or two KV heads, 1792/3584 FFN rows, a 16032/32064-row vocab shard,
+# q_size != hidden. Two layers keep the CPU oracle fast.
+for _tp in (4, 8):
+    _b = FAMILIES["llama-3-8b"]
+    FAMILIES.setdefault(f"llama-8b-tp{_tp}-shard", _b.with_(
+        name=f"llama-8b-tp{_tp}-shard", n_layers=2, n_heads=_b.n_heads // _tp, n_kv_heads=_b.n_kv_heads // _tp,
+        intermediate=_b.intermediate // _tp, vocab=_b.vocab // _tp))
+
 
 def _pair(name, ctx=512, **kw):
     cfg = FAMILIES[name]
@@ -23,7 +32,8 @@ def _pair(name, ctx=512, **kw):
     return cfg, ecpu, egpu
 
 
-@pytest.mark.parametrize("name", ["llama-tiny", "mixtral-tiny", "phi3-tiny", "llama-small"])
+@pytest.mark.parametrize("name", ["llama-tiny", "mixtral-tiny", "phi3-tiny", "llama-small", "llama-8b-tp8-shard",
+                                  "llama-8b-tp4-shard"])
 def test_prefill_logits_match_oracle(cuda, name):
     cfg, ecpu, egpu = _pair(name)
     prompt = [(i * 37) % (cfg.vocab - 300) + 256 for i in range(150)]
@@ -42,7 +52,7 @@ def test_prefill_logits_match_oracle(cuda, name):
         assert int(lc.argmax()) == int(lg.argmax())
 
 
-@pytest.mark.parametrize("name", ["llama-tiny", "mixtral-tiny", "phi3-tiny"])
+@pytest.mark.parametrize("name", ["llama-tiny", "mixtral-tiny", "phi3-tiny", "llama-8b-tp8-shard"])
 def test_decode_logits_match_oracle(cuda, name):
     """Teacher-forced: after greedy decode on GPU, the CPU oracle re-prefilling the same tokens
     must give logits close to the GPU decode path's final logits."""

@@ -324,11 +324,12 @@ extern "C" int llmc_attn_decode(const void* q, int q_stride, const void* k_cache
                                 void* counters, void* out, int out_stride, int B, int nh, int nkv, int D, int bs,
                                 int chunk, int grid_chunks, int max_chunks, float scale, int mode, hipStream_t s) {
   if (D % 8 != 0 || D > 128 || nh % nkv != 0 || grid_chunks > max_chunks) return -1;
-  if (mode == 2 || mode == 3) {  // MFMA (attn_decode_mfma.hip) [+ reduce kernel]
+  if (mode == 2 || mode == 3 || mode == 4) {  // MFMA (attn_decode_mfma.hip) [+ reduce kernel]
     int rc = llmc_attn_decode_mfma(q, q_stride, k_cache, v_cache, block_tables, bt_stride, seq_lens, part, counters,
                                    out, out_stride, B, nh, nkv, D, bs, chunk, grid_chunks, max_chunks, scale,
                                    mode == 3, s);
-    if (rc != 0 || grid_chunks <= 1 || mode == 3) return rc;
+    // mode 4: partials are left for the consumer (o_proj GEMV with the PRO_MERGE prologue)
+    if (rc != 0 || grid_chunks <= 1 || mode >= 3) return rc;
     switch (nh / nkv) {
       case 1: return launch_reduce_only<1>(B, nkv, D, -chunk, grid_chunks, max_chunks, s, part, seq_lens, out, out_stride);
       case 2: return launch_reduce_only<2>(B, nkv, D, -chunk, grid_chunks, max_chunks, s, part, seq_lens, out, out_stride);

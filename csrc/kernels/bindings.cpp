@@ -28,6 +28,8 @@ int llmc_attn_decode(const void*, int, const void*, const void*, const void*, in
                      int, int, int, int, int, int, int, int, int, float, int, hipStream_t);
 int llmc_gemv_qkv_rope(int, const void*, int, const void*, float, const void*, int, int, void*, int, void*, void*,
                        const void*, const void*, const void*, const void*, int, int, int, int, hipStream_t);
+int llmc_gemv_attn_merge(int, const void*, int, const void*, const void*, int, int, int, int, int, int, const void*,
+                         void*, int, int, int, int, hipStream_t);
 int llmc_attn_prefill(const void*, int, const void*, const void*, const void*, int, const void*, const void*,
                       const void*, void*, int, int, int, int, int, int, int, float, hipStream_t);
 int llmc_sample(const void*, int64_t, int, int, const void*, const void*, const void*, const void*, const void*, void*,
@@ -98,6 +100,12 @@ PYBIND11_MODULE(_llmc_hip, m) {
     check(llmc_gemv_qkv_rope(M, P(x), xs, P(nw), eps, P(W), N, K, P(qo), qos, P(kc), P(vc), P(pos), P(slots),
                              P(cos_t), P(sin_t), nh, nkv, D, bs, S(s)),
           "gemv_qkv_rope");
+  });
+  m.def("gemv_attn_merge", [](int M, ptr x, int xs, ptr part, ptr sl, int nkv, int G, int D, int gc, int min_chunk,
+                              int max_chunks, ptr W, ptr out, int os, int N, int K, int epi, ptr s) {
+    check(llmc_gemv_attn_merge(M, P(x), xs, P(part), P(sl), nkv, G, D, gc, min_chunk, max_chunks, P(W), P(out), os, N,
+                               K, epi, S(s)),
+          "gemv_attn_merge");
   });
   m.def("attn_prefill", [](ptr q, int qs, ptr kc, ptr vc, ptr bt, int bts, ptr qst, ptr ql, ptr cl, ptr out, int os,
                            int B, int max_qlen, int nh, int nkv, int D, int bs, float scale, ptr s) {

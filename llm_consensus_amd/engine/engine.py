@@ -182,6 +182,12 @@ class Engine:
         fixed = self.ecfg.attn_chunk or (0 if ops.ATTN_DECODE_MODE >= 2 else 128)  # VALU modes: fixed chunks
         self.attn_buckets = attn_buckets(ctxmax, fixed, max(1, blocks // self.nkv))
         self.max_chunks = max(gc for _, _, gc in self.attn_buckets)
+        # LLMC_ATTN_MERGE=1: merge the split-KV partials in o_proj's prologue instead of the reduce
+        # launch. Measured SLOWER on MI355X (8B decode 2.95 vs 2.90 ms/token at 2k context, 3.72
+        # vs 3.61 at 33k: every o_proj block re-reads all partials and the chunk groups are
+        # dependent L2 round trips before its weight stream resumes), so it is off by default.
+        self._attn_merge = (self.on_gpu and ops.ATTN_DECODE_MODE == 2 and fixed == 0
+                            and os.environ.get("LLMC_ATTN_MERGE", "0") == "1")
         self.attn_part, self.attn_counters = ops.decode_attn_workspace(B, self.nh, self.nkv, self.D,
                                                                         self.max_chunks, dev)
         if self.on_gpu:
@@ -370,10 +376,20 @@ class Engine:
         for li, Lw in enumerate(self.w.layers):
             ops.qkv_rope(h, Lw.w_qkv, Lw.ln1, c.rms_eps, q, self.k_cache[li], self.v_cache[li], self.positions[:B],
                          self.slots[:B], self.cos_t, self.sin_t, self.nh, self.nkv, self.D, self.bs)
-            ops.attn_decode(q, self.k_cache[li], self.v_cache[li], self.block_tables[:B], self.seq_lens[:B], attn,
-                            self.attn_part[:B], self.attn_counters[:B], self.nh, self.nkv, self.D, self.bs,
-                            chunk, self.scale, grid_chunks)
-            self._row_parallel(attn, Lw.w_o, h)
+            if self._attn_merge:
+                # split-KV partials merged inside the o_proj GEMV's prologue (no reduce launch)
+                ops.attn_decode(q, self.k_cache[li], self.v_cache[li], self.block_tables[:B], self.seq_lens[:B], attn,
+                                self.attn_part[:B], self.attn_counters[:B], self.nh, self.nkv, self.D, self.bs,
+                                chunk, self.scale, grid_chunks, mode=4)
+                ops.attn_o_proj(attn, self.attn_part[:B], self.seq_lens[:B], Lw.w_o, h,
+                                EPI_RESADD if self.tp.rank == 0 else EPI_BF16, self.nh, self.nkv, self.D, chunk,
+                                grid_chunks)
+                self.tp.all_reduce_(h)
+            else:
+                ops.attn_decode(q, self.k_cache[li], self.v_cache[li], self.block_tables[:B], self.seq_lens[:B], attn,
+                                self.attn_part[:B], self.attn_counters[:B], self.nh, self.nkv, self.D, self.bs,
+                                chunk, self.scale, grid_chunks)
+                self._row_parallel(attn, Lw.w_o, h)
             if c.is_moe:
                 self._moe_decode(h, Lw, B)
             else:

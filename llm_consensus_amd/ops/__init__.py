@@ -175,7 +175,9 @@ def decode_attn_workspace(B, nh, nkv, D, max_chunks, device):
 
 # decode attention kernel: 2 = MFMA balanced split + reduce kernel (default), 3 = MFMA with the
 # in-launch last-arriver reduce, 0 = VALU fixed chunks + reduce kernel, 1 = VALU + in-launch
-# reduce. MFMA modes need chunk % 128 == 0 (else mode 0 runs).
+# reduce, 4 = MFMA leaving the partials to the o_proj GEMV's merge prologue (attn_o_proj; the
+# engine's decode step uses it with LLMC_ATTN_MERGE=1; measured slower, off by default). MFMA modes need chunk % 128 == 0 (else
+# mode 0 runs).
 ATTN_DECODE_MODE = int(os.environ.get("LLMC_ATTN_MODE", "2"))
 
 
@@ -192,6 +194,20 @@ def attn_decode(q, k_cache, v_cache, block_tables, seq_lens, out, part, counters
     kernels().attn_decode(_p(q), q.stride(0), _p(k_cache), _p(v_cache), _p(block_tables), block_tables.stride(0),
                           _p(seq_lens), _p(part), _p(counters), _p(out), out.stride(0), B, nh, nkv, D, bs, chunk, gc,
                           max_chunks, float(scale), mode, _s(q))
+    return out
+
+
+def attn_o_proj(attn, part, seq_lens, W, out, epi, nh, nkv, D, chunk, grid_chunks):
+    """Decode o_proj with the split-KV merge fused in: ``attn`` holds the attention output of rows
+    whose sequence took one chunk, ``part`` the per-chunk partials of an ``attn_decode(...,
+    mode=4)`` launch with the same ``chunk``/``grid_chunks``; ``out`` (+)= merge(...) @ W^T."""
+    if not attn.is_cuda:
+        return oracle.linear(attn, W, epi, out)
+    M, K = attn.shape
+    max_chunks = part.shape[2]
+    gc = min(grid_chunks, max_chunks)
+    kernels().gemv_attn_merge(M, _p(attn), attn.stride(0), _p(part), _p(seq_lens), nkv, nh // nkv, D, gc, chunk,
+                              max_chunks, _p(W), _p(out), out.stride(0), W.shape[0], K, epi, _s(attn))
     return out
 
 

@@ -315,3 +315,36 @@ def test_moe(cuda, T):
         ops.moe_gemm(act, wd, sr, te, tc, y, H, I, mt, 1)
     ops.moe_combine(y, w, ids, h)
     close(h, href, 3e-2)
+
+
+@pytest.mark.parametrize("nh,nkv,D", [(32, 8, 128), (4, 1, 128), (32, 32, 96), (16, 2, 64)])
+@pytest.mark.parametrize("gc", [1, 5, 32])
+@pytest.mark.parametrize("epi", [0, 2])
+def test_attn_o_proj_merge(cuda, nh, nkv, D, gc, epi):
+    """o_proj GEMV with the split-KV merge in its prologue (attention mode 4) == attention with its
+    reduce kernel followed by the plain GEMV, and both match the fp32 oracle. Rows mix single-chunk
+    sequences (direct attention output) and many-chunk ones."""
+    torch.manual_seed(21 + gc)
+    lens, bs = [3000, 60, 700, 4100], 64
+    B = len(lens)
+    H = 512
+    kc, vc, bt = _paged_kv(B, max(lens), nkv, D, bs)
+    q = rnd(B, nh * D)
+    W = rnd(H, nh * D, scale=0.05)
+    sl = torch.tensor(lens, dtype=torch.int32)
+    part, ctr = ops.decode_attn_workspace(B, nh, nkv, D, max(gc, 8), "cuda")
+    scale = 1 / math.sqrt(D)
+    attn = torch.zeros(B, nh * D, dtype=BF, device="cuda")
+    ops.attn_decode(q, kc, vc, bt.cuda(), sl.cuda(), attn, part, ctr, nh, nkv, D, bs, 128, scale, grid_chunks=gc, mode=2)
+    h0 = rnd(B, H)
+    y_ref = ops.gemv(attn, W, epi, out=h0.clone() if epi == 2 else None)
+    attn2 = torch.zeros_like(attn)
+    part.zero_()
+    ops.attn_decode(q, kc, vc, bt.cuda(), sl.cuda(), attn2, part, ctr, nh, nkv, D, bs, 128, scale, grid_chunks=gc,
+                    mode=4)
+    y = h0.clone() if epi == 2 else torch.empty(B, H, dtype=BF, device="cuda")
+    ops.attn_o_proj(attn2, part, sl.cuda(), W, y, epi, nh, nkv, D, 128, gc)
+    close(y, y_ref.float().cpu(), 2e-2)
+    ref_attn = oracle.attn_decode(q.cpu(), kc.cpu(), vc.cpu(), bt, sl, nh, nkv, D, bs, scale)
+    ref = oracle.linear(ref_attn, W.cpu(), epi, h0.cpu().clone() if epi == 2 else None)
+    close(y, ref, 3e-2)

@@ -125,23 +125,31 @@ def main() -> None:
     judge = None
     judge_ctx = 0
     jtp = judge_tp_degree(jcfg, world, args.judge_tp) if n_models > 1 else 1
-    if n_models > 1 and rank < jtp:
-        from llm_consensus_amd.parallel.comm import TPGroup
+    from llm_consensus_amd.parallel.comm import TPGroup
 
-        tp = TPGroup.single()
-        if jtp > 1:
-            # judge TP group = ranks 0..jtp-1 (the whole world by default); new_group is collective
-            grp = dist.group.WORLD if jtp == world else dist.new_group(list(range(jtp)))
+    tp = TPGroup.single()
+    if jtp > 1:
+        # judge TP group = ranks 0..jtp-1 (the whole world by default); new_group is collective
+        grp = dist.group.WORLD if jtp == world else dist.new_group(list(range(jtp)))
+        ok = 1
+        if rank < jtp:
             tp = TPGroup(grp, rank, jtp)
-            tp.enable_custom(dev)
+            try:
+                tp.enable_custom(dev)
+            except Exception as ex:  # noqa: BLE001 - IPC mapping refused: fall back to a 1-GPU judge
+                log(f"custom all-reduce unavailable ({ex!r}); judge falls back to TP=1 on GPU 0")
+                ok = 0
+        flag = torch.tensor([ok], dtype=torch.int32, device=cdev)
+        dist.all_reduce(flag, op=dist.ReduceOp.MIN)
+        if int(flag.item()) == 0:
+            jtp, tp = 1, TPGroup.single()
+    if n_models > 1 and rank < jtp:
         # responses are decoded to text and re-tokenized by the judge: random byte tokens can expand
         # (invalid UTF-8 -> U+FFFD -> 3 byte tokens), so budget 2x per response
         judge_ctx = len(prompt_ids) + 1024 + n_models * (2 * args.max_tokens + 64) + jmax + 64
         judge = Engine(jcfg, EngineConfig(device=dev, max_context=judge_ctx, seed=777,
                                           steps_per_graph=args.steps_per_graph, use_graphs=not args.no_graphs),
                        tp=tp, name=f"{args.judge}@judge")
-    elif n_models > 1 and 1 < jtp < world:
-        dist.new_group(list(range(jtp)))  # every rank takes part in creating the sub-group
     # capture every decode graph up front (a capture beside another engine's running stream is
     # invalid; the worker process does the same before serving)
     if not args.no_graphs:
@@ -208,6 +216,8 @@ def main() -> None:
             if rank == 0:
                 n_tokens += len(jids)
             judge.free_sequence(jseq)
+            if judge.tp.custom is not None and judge.tp.custom.timed_out():
+                log("WARNING: a custom all-reduce spin timed out (a peer stalled); judge tokens are suspect")
         torch.cuda.synchronize()
         if world > 1:
             dist.barrier()

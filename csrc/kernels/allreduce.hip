@@ -10,9 +10,12 @@
 //   signals: ctr[kBlocks] (per-block launch epoch, persists across graph replays),
 //            flag[kMaxBlocks][kMaxRanks] (epoch of the last arrival of rank r for block b),
 //            timeout word (set when a bounded spin gives up).
-// Every launch runs exactly kBlocks blocks and block b always owns the same 4 KiB chunks
-// (c % kBlocks == b) whatever the message size, so block b's epochs and data slices line up
-// across ranks and across calls of different sizes. Protocol per launch, per block b:
+// Block b always owns the same 4 KiB chunks (c % kBlocks == b) whatever the message size, so
+// block b's epochs and data slices line up across ranks and across calls of different sizes. A
+// launch runs only the blocks that own data (min(kBlocks, chunks)): every rank issues the same
+// sequence of sizes, so an idle block's epoch simply stays put on every rank, and a decode-sized
+// [1, 4096] bf16 message costs 2 blocks' flag exchanges over xGMI instead of 32. Protocol per
+// launch, per block b:
 //   1. epoch = ctr[b] + 1; stage my slice into my data[epoch & 1] (uncached stores);
 //   2. every wave drains its stores (s_waitcnt vmcnt(0)), barrier, then ONE lane per peer
 //      stores `epoch` into peer.flag[b][me] (system-scope release);
@@ -33,7 +36,7 @@ namespace llmc {
 
 constexpr int kMaxRanks = 8;
 constexpr int kMaxBlocks = 64;  // signal slots
-constexpr int kBlocks = 32;     // blocks per launch (fixed)
+constexpr int kBlocks = 32;     // blocks per launch (at most; see car_grid)
 constexpr int kChunk = 256;     // 16-B vectors per chunk (one per thread)
 constexpr size_t kSigBytes = 64 * 1024;
 constexpr int kFlagOff = 1024;                             // bytes: after ctr[]
@@ -146,6 +149,11 @@ __global__ __launch_bounds__(256) void car_allgather_kernel(CarPeers P, const ch
 
 using namespace llmc;
 
+static int car_grid(int n16) {
+  const int chunks = (n16 + kChunk - 1) / kChunk;
+  return chunks < 1 ? 1 : (chunks < kBlocks ? chunks : kBlocks);
+}
+
 extern "C" {
 
 size_t llmc_car_sig_bytes() { return kSigBytes; }
@@ -192,7 +200,7 @@ int llmc_car_allreduce(const void* const* bases, int rank, int world, size_t cap
   CarPeers P;
   for (int r = 0; r < kMaxRanks; ++r) P.base[r] = r < world ? static_cast<char*>(const_cast<void*>(bases[r])) : nullptr;
   const int n16 = static_cast<int>(nbytes / 16);
-  car_allreduce_kernel<<<kBlocks, 256, 0, s>>>(P, static_cast<bf16_t*>(x), n16, rank, world, cap);
+  car_allreduce_kernel<<<car_grid(n16), 256, 0, s>>>(P, static_cast<bf16_t*>(x), n16, rank, world, cap);
   return static_cast<int>(hipGetLastError());
 }
 
@@ -202,7 +210,7 @@ int llmc_car_allgather(const void* const* bases, int rank, int world, size_t cap
   CarPeers P;
   for (int r = 0; r < kMaxRanks; ++r) P.base[r] = r < world ? static_cast<char*>(const_cast<void*>(bases[r])) : nullptr;
   const int n16 = static_cast<int>(nbytes / 16);
-  car_allgather_kernel<<<kBlocks, 256, 0, s>>>(P, static_cast<const char*>(x), static_cast<char*>(out), n16, rank,
+  car_allgather_kernel<<<car_grid(n16), 256, 0, s>>>(P, static_cast<const char*>(x), static_cast<char*>(out), n16, rank,
                                                world, cap);
   return static_cast<int>(hipGetLastError());
 }

@@ -42,6 +42,7 @@ int llmc_moe_gemm(const void*, int, const void*, const void*, const void*, const
 int llmc_moe_combine(const void*, const void*, const void*, void*, int, int, int, hipStream_t);
 int llmc_moe_gemv(int, const void*, int, const void*, float, const void*, const void*, int, void*, int, int, int, int,
                   hipStream_t);
+int llmc_moe_ep_localize(const void*, const void*, int, int, int, void*, void*, hipStream_t);
 int llmc_gemv_sweep(int, const void*, const void*, const void*, void*, int, int, hipStream_t);
 size_t llmc_car_sig_bytes();
 int llmc_car_alloc(size_t, void**);
@@ -141,6 +142,9 @@ PYBIND11_MODULE(_llmc_hip, m) {
   m.def("moe_gemv", [](int k, ptr x, int xs, ptr nw, float eps, ptr W, ptr ids, int ids_stride, ptr out, int os,
                        int N, int K, int epi, ptr s) {
     check(llmc_moe_gemv(k, P(x), xs, P(nw), eps, P(W), P(ids), ids_stride, P(out), os, N, K, epi, S(s)), "moe_gemv");
+  });
+  m.def("moe_ep_localize", [](ptr ids, ptr w, int n, int e0, int nl, ptr lids, ptr lw, ptr s) {
+    check(llmc_moe_ep_localize(P(ids), P(w), n, e0, nl, P(lids), P(lw), S(s)), "moe_ep_localize");
   });
   m.def("device_synchronize", []() { check(static_cast<int>(hipDeviceSynchronize()), "hipDeviceSynchronize"); });
   // ---- K13 custom all-reduce / all-gather over IPC peer buffers ----

@@ -63,6 +63,7 @@ __global__ __launch_bounds__(NT) void gemv_kernel(const bf16_t* __restrict__ x, 
   // input row pair / x_div, output row pair (M must be 1).
   if constexpr (EXPERT) {
     const int pair = blockIdx.y;
+    if (expert_ids[pair] < 0) return;  // another rank's expert (expert parallel): whole block exits
     W += static_cast<int64_t>(expert_ids[pair]) * N * K;
     x += static_cast<int64_t>(pair / x_div) * x_stride;
     out = reinterpret_cast<char*>(out) + static_cast<int64_t>(pair) * out_stride * (EPI == EPI_F32 ? 4 : 2);

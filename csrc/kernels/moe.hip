@@ -9,7 +9,9 @@
 //   x [T, H] --gemm<GATHER>(a_row_div = k)--> gu [T*k, 2I] --silu_mul--> act [T*k, I]
 //   act --gemm<GATHER>(a_row_div = 1)--> y [T*k, H] --moe_combine--> h[t] += sum_j w[t,j] y[t*k+j]
 // The combine is a fixed-order sum in f32 (no float atomics: bitwise reproducible,
-// MI355X_MICROARCH.md "Global float atomics" pitfall).
+// MI355X_MICROARCH.md "Global float atomics" pitfall). Expert parallel: moe_ep_localize maps the
+// router's global ids to this rank's experts (-1, weight 0 elsewhere); expert GEMV blocks of a -1
+// pair exit and the combine skips zero-weight pairs.
 #include "common.h"
 
 namespace llmc {
@@ -96,6 +98,7 @@ __global__ __launch_bounds__(256) void moe_combine_kernel(const bf16_t* __restri
     float s[8] = {0, 0, 0, 0, 0, 0, 0, 0};
     for (int j = 0; j < k; ++j) {
       const float wj = w[static_cast<int64_t>(t) * k + j];
+      if (wj == 0.f) continue;  // another rank's expert (expert parallel): its y row is not written
       float f[8];
       unpack8(reinterpret_cast<const u32x4*>(y + (static_cast<int64_t>(t) * k + j) * H)[c], f);
 #pragma unroll
@@ -105,6 +108,17 @@ __global__ __launch_bounds__(256) void moe_combine_kernel(const bf16_t* __restri
     for (int q = 0; q < 8; ++q) acc[q] += s[q];
     reinterpret_cast<u32x4*>(h + static_cast<int64_t>(t) * H)[c] = pack8(acc);
   }
+}
+
+// expert parallel: global expert id -> local id on this rank (-1 + weight 0 for other ranks')
+__global__ void moe_ep_localize_kernel(const int32_t* __restrict__ ids, const float* __restrict__ w, int n, int e0,
+                                       int n_local, int32_t* __restrict__ lids, float* __restrict__ lw) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const int e = ids[i] - e0;
+  const bool mine = e >= 0 && e < n_local;
+  lids[i] = mine ? e : -1;
+  lw[i] = mine ? w[i] : 0.f;
 }
 
 }  // namespace llmc
@@ -135,6 +149,14 @@ int llmc_moe_combine(const void* y, const void* w, const void* ids, void* h, int
   (void)ids;
   if (H % 8 != 0) return -1;
   moe_combine_kernel<<<T, 256, 0, s>>>((const bf16_t*)y, (const float*)w, (bf16_t*)h, k, H);
+  return static_cast<int>(hipGetLastError());
+}
+
+int llmc_moe_ep_localize(const void* ids, const void* w, int n, int e0, int n_local, void* lids, void* lw,
+                         hipStream_t s) {
+  if (n <= 0) return 0;
+  moe_ep_localize_kernel<<<(n + 255) / 256, 256, 0, s>>>((const int32_t*)ids, (const float*)w, n, e0, n_local,
+                                                         (int32_t*)lids, (float*)lw);
   return static_cast<int>(hipGetLastError());
 }
 

@@ -52,6 +52,12 @@ class EngineConfig:
     attn_chunk: int = 0  # 0 = balanced MFMA split (>= 128 keys per block); > 0 = fixed chunk size
     init_scale: float = 1.0
     stream_priority: int = 0
+    # TP prefill: shard the residual stream by token rows between layers (reduce-scatter +
+    # all-gather instead of all-reduce) for chunks of >= sp_min_tokens tokens
+    sequence_parallel: bool = True
+    sp_min_tokens: int = 256
+    # MoE under TP: each rank holds n_experts / tp whole experts instead of 1/tp of every expert
+    expert_parallel: bool = False
 
 
 def attn_buckets(ctxmax: int, fixed_chunk: int = 0, blocks_per_head: int = 64) -> List[tuple]:
@@ -125,7 +131,8 @@ class Engine:
                 if weights is not None:
                     self.w = weights.to(self.device)
                 else:
-                    self.w = TransformerWeights(cfg, self.tp, self.device, e.seed, e.init_scale)
+                    self.w = TransformerWeights(cfg, self.tp, self.device, e.seed, e.init_scale,
+                                                expert_parallel=e.expert_parallel)
         self.nh, self.nkv, self.D = self.w.nh, self.w.nkv, cfg.head_dim
         self.scale = 1.0 / math.sqrt(self.D)
         self.bs = e.block_size
@@ -204,6 +211,8 @@ class Engine:
             self.moe_ids = torch.zeros(B, k, **i32)
             self.moe_act = torch.zeros(B * k, self.w.inter, **bf)
             self.moe_y = torch.zeros(B * k, c.hidden, **bf)
+            self.moe_lw = torch.zeros(B, k, dtype=torch.float32, device=dev)
+            self.moe_lids = torch.zeros(B, k, **i32)
         if self.on_gpu:
             self.host_tokens = torch.zeros(B, self.cap, dtype=torch.int32, pin_memory=True)
             self.host_count = torch.zeros(B, dtype=torch.int32, pin_memory=True)
@@ -298,13 +307,38 @@ class Engine:
         h = ops.embedding(ids_d, self.w.embed)
         attn = torch.empty(T, self.w.q_size, dtype=torch.bfloat16, device=dev)
         qbuf = torch.empty(T, self.w.q_size, dtype=torch.bfloat16, device=dev)
+        sp = self._sp_plan(T)
+        if sp is not None:  # sequence parallel: this rank keeps rows [r*Ts, (r+1)*Ts) of the stream
+            Ts, gbuf, pbuf = sp
+            r0 = self.tp.rank * Ts
+            hs = torch.zeros(Ts, c.hidden, dtype=torch.bfloat16, device=dev)
+            mine = max(0, min(T, r0 + Ts) - r0)
+            if mine:
+                hs[:mine].copy_(h[r0:r0 + mine])
+            del h
         for li, Lw in enumerate(self.w.layers):
-            xn = ops.rmsnorm(h, Lw.ln1, c.rms_eps)
+            if sp is not None:
+                xn = self._sp_gather(ops.rmsnorm(hs, Lw.ln1, c.rms_eps), gbuf, T)
+            else:
+                xn = ops.rmsnorm(h, Lw.ln1, c.rms_eps)
             qkv = ops.linear(xn, Lw.w_qkv, EPI_BF16)
             ops.rope_kv_write(qkv, pos_d, self.cos_t, self.sin_t, self.k_cache[li], self.v_cache[li], slots_d,
                               self.nh, self.nkv, self.D, self.bs, qbuf)
             ops.attn_prefill(qbuf, self.k_cache[li], self.v_cache[li], bt, qs_d, ql_d, cl_d, attn, max_qlen,
                              self.nh, self.nkv, self.D, self.bs, self.scale)
+            if sp is not None:
+                self._sp_row_parallel(lambda out: ops.linear(attn, Lw.w_o, EPI_RESADD, out=out), hs, pbuf, T)
+                if c.is_moe and self.w.ep:
+                    # expert parallel on token shards: tokens go to their experts' ranks (all-to-all)
+                    self._moe_ep_a2a(ops.rmsnorm(hs, Lw.ln2, c.rms_eps), Lw, hs)
+                    continue
+                xn = self._sp_gather(ops.rmsnorm(hs, Lw.ln2, c.rms_eps), gbuf, T)
+                if c.is_moe:
+                    self._sp_row_parallel(lambda out: self._moe(xn, Lw, out, reduce=False), hs, pbuf, T)
+                else:
+                    act = ops.linear(xn, Lw.w_gu, EPI_SILU)
+                    self._sp_row_parallel(lambda out: ops.linear(act, Lw.w_down, EPI_RESADD, out=out), hs, pbuf, T)
+                continue
             self._row_parallel(attn, Lw.w_o, h)
             xn = ops.rmsnorm(h, Lw.ln2, c.rms_eps)
             if c.is_moe:
@@ -312,6 +346,8 @@ class Engine:
             else:
                 act = ops.linear(xn, Lw.w_gu, EPI_SILU)
                 self._row_parallel(act, Lw.w_down, h)
+        if sp is not None:  # whole stream back on every rank (only the last rows are read below)
+            h = self._sp_gather(hs, sp[1], T)
         # last-token logits for every sequence whose final prompt token is in this chunk
         sel = [i for i, (s, _) in enumerate(batch) if want_logits and s in finals]
         for i0 in range(0, len(sel), ops.GEMV_MAX_M):
@@ -325,46 +361,129 @@ class Engine:
                 s.logits = lg[j]
                 s.has_logits = True
 
+    # -- sequence parallel (TP prefill) ---------------------------------------------------------
+    def _sp_plan(self, T: int):
+        """(rows per rank, gather buffer, partial buffer) when this chunk runs sequence parallel."""
+        n = self.tp.size
+        if n == 1 or not self.ecfg.sequence_parallel or T < max(self.ecfg.sp_min_tokens, n):
+            return None
+        Ts = (T + n - 1) // n
+        H = self.cfg.hidden
+        gbuf = torch.empty(n * Ts, H, dtype=torch.bfloat16, device=self.device)
+        pbuf = torch.empty(n * Ts, H, dtype=torch.bfloat16, device=self.device)
+        return Ts, gbuf, pbuf
+
+    def _sp_gather(self, xs: torch.Tensor, gbuf: torch.Tensor, T: int) -> torch.Tensor:
+        """All-gather the row shards [Ts, H] of every rank -> the first T rows of [n*Ts, H]."""
+        self.tp.all_gather_rows(xs, gbuf.view(self.tp.size, xs.shape[0], xs.shape[1]))
+        return gbuf[:T]
+
+    def _sp_row_parallel(self, accumulate, hs: torch.Tensor, pbuf: torch.Tensor, T: int) -> None:
+        """hs += (this row block of) sum_r partial_r: every rank seeds the rows it owns with its
+        residual shard (zeros elsewhere), ``accumulate(out)`` adds its partial product into the
+        first T rows, and a reduce-scatter leaves each rank its own summed rows — the residual
+        is folded in exactly once per row, with no separate add."""
+        Ts = hs.shape[0]
+        r0 = self.tp.rank * Ts
+        pbuf.zero_()
+        pbuf[r0:r0 + Ts].copy_(hs)
+        accumulate(pbuf[:T])
+        self.tp.reduce_scatter_rows(pbuf, hs)
+
     def _row_parallel(self, x: torch.Tensor, W: torch.Tensor, h: torch.Tensor) -> None:
         """h += x @ W^T across the TP group (residual folded into rank 0's partial)."""
         ops.linear(x, W, EPI_RESADD if self.tp.rank == 0 else EPI_BF16, out=h)
         self.tp.all_reduce_(h)
 
-    def _moe(self, xn: torch.Tensor, Lw, h: torch.Tensor) -> None:
+    def _expert_ffn(self, A: torch.Tensor, ids: torch.Tensor, Lw) -> torch.Tensor:
+        """y[p] = down_e(silu(gate_up_e(A[p // k]))) for every (row, slot) pair p of ``ids`` [n, k]
+        (expert ids index this rank's expert tensors): expert GEMVs for <= 4 rows, else expert
+        alignment + the gathered-row grouped MFMA GEMM (K10/K11)."""
         c = self.cfg
-        T, k, E = xn.shape[0], c.top_k_experts, c.n_experts
-        if not xn.is_cuda:
-            rl = oracle.linear(xn, Lw.w_router, EPI_F32)
-            w, ids = oracle.moe_route(rl, k)
-            if self.tp.rank != 0:
-                h.zero_()
-            oracle.moe_ffn(xn, Lw.w_gu, Lw.w_down, w, ids, h)
-            self.tp.all_reduce_(h)
-            return
+        n, k = ids.shape
+        E_l, I_l, H = Lw.w_gu.shape[0], self.w.inter, c.hidden
+        y = torch.empty(n * k, H, dtype=torch.bfloat16, device=A.device)
+        if n == 0:
+            return y
+        if not A.is_cuda:
+            for p in range(n * k):
+                e = int(ids.view(-1)[p])
+                gu = (A[p // k:p // k + 1].float() @ Lw.w_gu[e].float().t()).to(torch.bfloat16)
+                y[p] = (oracle.silu_mul_interleaved(gu).float() @ Lw.w_down[e].float().t()).to(torch.bfloat16)[0]
+            return y
+        if n <= ops.GEMV_MAX_M:
+            act = torch.empty(n * k, I_l, dtype=torch.bfloat16, device=A.device)
+            ops.moe_gemv(A, Lw.w_gu, ids, k, act, 2 * I_l, H, EPI_SILU)
+            ops.moe_gemv(act, Lw.w_down, ids, 1, y, H, I_l, EPI_BF16)
+            return y
+        mt = ops.moe_max_tiles(n * k, E_l)
+        sr = torch.empty(mt * ops.MOE_TILE, dtype=torch.int32, device=A.device)
+        te = torch.empty(mt, dtype=torch.int32, device=A.device)
+        tc = torch.empty(1, dtype=torch.int32, device=A.device)
+        ops.moe_align(ids, E_l, sr, te, tc)
+        gu = torch.empty(n * k, 2 * I_l, dtype=torch.bfloat16, device=A.device)
+        ops.moe_gemm(A, Lw.w_gu, sr, te, tc, gu, 2 * I_l, H, mt, k)
+        act = ops.silu_mul_interleaved(gu)
+        ops.moe_gemm(act, Lw.w_down, sr, te, tc, y, H, I_l, mt, 1)
+        return y
+
+    def _route(self, xn: torch.Tensor, Lw):
+        c = self.cfg
+        T, k = xn.shape[0], c.top_k_experts
         rl = ops.linear(xn, Lw.w_router, EPI_F32)
         w = torch.empty(T, k, dtype=torch.float32, device=xn.device)
         ids = torch.empty(T, k, dtype=torch.int32, device=xn.device)
         ops.moe_route(rl, k, w, ids)
-        I_l, H = self.w.inter, c.hidden
-        y = torch.empty(T * k, H, dtype=torch.bfloat16, device=xn.device)
-        if T <= ops.GEMV_MAX_M:
-            act = torch.empty(T * k, I_l, dtype=torch.bfloat16, device=xn.device)
-            ops.moe_gemv(xn, Lw.w_gu, ids, k, act, 2 * I_l, H, EPI_SILU)
-            ops.moe_gemv(act, Lw.w_down, ids, 1, y, H, I_l, EPI_BF16)
+        return w, ids
+
+    def _moe(self, xn: torch.Tensor, Lw, h: torch.Tensor, reduce: bool = True) -> None:
+        """h += MoE(xn). ``reduce`` (the all-reduce path): rank 0 folds the residual, the others
+        start from zero, then all-reduce; False: just accumulate this rank's partial into h.
+        Expert parallel (replicated tokens): only the pairs routed to this rank's experts run;
+        the other pairs weigh 0 in the combine, and the reduction sums the ranks' shares."""
+        c = self.cfg
+        T, k = xn.shape[0], c.top_k_experts
+        w, ids = self._route(xn, Lw)
+        if self.w.ep:
+            lids = torch.empty_like(ids)
+            lw = torch.empty_like(w)
+            ops.moe_ep_localize(ids, w, self.w.e0, self.w.n_local_experts, lids, lw)
+            sel = torch.nonzero(lids.view(-1) >= 0).view(-1)  # host sync: prefill only
+            y = torch.zeros(T * k, c.hidden, dtype=torch.bfloat16, device=xn.device)
+            if sel.numel():
+                y.index_copy_(0, sel, self._expert_ffn(xn.index_select(0, sel // k),
+                                                       lids.view(-1).index_select(0, sel).view(-1, 1), Lw))
+            w, ids = lw, lids
         else:
-            mt = ops.moe_max_tiles(T * k, E)
-            sr = torch.empty(mt * ops.MOE_TILE, dtype=torch.int32, device=xn.device)
-            te = torch.empty(mt, dtype=torch.int32, device=xn.device)
-            tc = torch.empty(1, dtype=torch.int32, device=xn.device)
-            ops.moe_align(ids, E, sr, te, tc)
-            gu = torch.empty(T * k, 2 * I_l, dtype=torch.bfloat16, device=xn.device)
-            ops.moe_gemm(xn, Lw.w_gu, sr, te, tc, gu, 2 * I_l, H, mt, k)
-            act = ops.silu_mul_interleaved(gu)
-            ops.moe_gemm(act, Lw.w_down, sr, te, tc, y, H, I_l, mt, 1)
-        if self.tp.rank != 0:
+            y = self._expert_ffn(xn, ids, Lw)
+        if reduce and self.tp.rank != 0:
             h.zero_()
         ops.moe_combine(y, w, ids, h)
-        self.tp.all_reduce_(h)
+        if reduce:
+            self.tp.all_reduce_(h)
+
+    def _moe_ep_a2a(self, xs: torch.Tensor, Lw, hs: torch.Tensor) -> None:
+        """hs += MoE(xs) for this rank's token shard, experts sharded over the TP group: every
+        (token, slot) pair is sent to the rank owning its expert (all-to-all, C4), computed there
+        by the grouped GEMM, and sent back for the deterministic combine."""
+        c = self.cfg
+        k, H = c.top_k_experts, c.hidden
+        El = self.w.n_local_experts
+        w, ids = self._route(xs, Lw)
+        flat = ids.view(-1).long()
+        owner = flat // El
+        order = torch.argsort(owner, stable=True)
+        send = torch.bincount(owner, minlength=self.tp.size).tolist()
+        recv = self.tp.exchange_counts(send)
+        send_x = xs.index_select(0, order // k)
+        send_e = (flat - owner * El).index_select(0, order).to(torch.int32)
+        recv_x = self.tp.all_to_all_rows(send_x, send, recv)
+        recv_e = self.tp.all_to_all_rows(send_e, send, recv)
+        y_recv = self._expert_ffn(recv_x, recv_e.view(-1, 1), Lw)
+        y_back = self.tp.all_to_all_rows(y_recv, recv, send)
+        y = torch.empty(flat.numel(), H, dtype=torch.bfloat16, device=xs.device)
+        y.index_copy_(0, order, y_back)
+        ops.moe_combine(y, w, ids, hs)
 
     # -- decode -------------------------------------------------------------------------------------
     def _decode_step(self, B: int, bucket: Optional[int] = None) -> None:
@@ -410,14 +529,18 @@ class Engine:
         k = c.top_k_experts
         rl = self.router_logits[:B]
         ops.linear(xn, Lw.w_router, EPI_F32, out=rl)
-        ops.moe_route(rl, k, self.moe_w[:B], self.moe_ids[:B])
+        w, ids = self.moe_w[:B], self.moe_ids[:B]
+        ops.moe_route(rl, k, w, ids)
+        if self.w.ep:  # pairs of other ranks' experts: id -1 (GEMV blocks exit), weight 0
+            ops.moe_ep_localize(ids, w, self.w.e0, self.w.n_local_experts, self.moe_lids[:B], self.moe_lw[:B])
+            w, ids = self.moe_lw[:B], self.moe_lids[:B]
         I_l, H = self.w.inter, c.hidden
         act, y = self.moe_act[: B * k], self.moe_y[: B * k]
-        ops.moe_gemv(xn, Lw.w_gu, self.moe_ids[:B], k, act, 2 * I_l, H, EPI_SILU)
-        ops.moe_gemv(act, Lw.w_down, self.moe_ids[:B], 1, y, H, I_l, EPI_BF16)
+        ops.moe_gemv(xn, Lw.w_gu, ids, k, act, 2 * I_l, H, EPI_SILU)
+        ops.moe_gemv(act, Lw.w_down, ids, 1, y, H, I_l, EPI_BF16)
         if self.tp.rank != 0:
             h.zero_()
-        ops.moe_combine(y, self.moe_w[:B], self.moe_ids[:B], h)
+        ops.moe_combine(y, w, ids, h)
         self.tp.all_reduce_(h)
 
     def _gather_logits(self, B: int) -> torch.Tensor:

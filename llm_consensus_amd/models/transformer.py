@@ -10,7 +10,8 @@ checkpoint compatibility:
   * ``w_gu``   [2 I, H] gate/up rows INTERLEAVED (row 2i = gate_i, 2i + 1 = up_i) so the GEMV
     epilogue produces silu(gate) * up directly and a TP shard is a contiguous row range;
   * ``w_down`` [H, I];
-  * MoE (Mixtral): ``w_router`` [E, H], ``w_gu`` [E, 2I, H], ``w_down`` [E, H, I];
+  * MoE (Mixtral): ``w_router`` [E, H], ``w_gu`` [E, 2I, H], ``w_down`` [E, H, I] (under TP: 1/tp
+    of every expert's FFN rows, or with ``expert_parallel`` E/tp whole experts per rank);
   * ``embed`` [V, H] (replicated under TP), ``lm_head`` [V, H] (vocab-parallel under TP).
 Weights are random-init from a seed, or read from a Hugging Face checkpoint when the config
 names one (``models/checkpoint.py``). Either way each tensor is produced in full in the logical
@@ -40,7 +41,7 @@ class LayerWeights:
 
 class TransformerWeights:
     def __init__(self, cfg: ModelConfig, tp: TPGroup, device: torch.device, seed: int,
-                 init_scale: float = 1.0, source=None):
+                 init_scale: float = 1.0, source=None, expert_parallel: bool = False):
         if source is None and cfg.checkpoint:
             from .checkpoint import HFCheckpoint
 
@@ -53,9 +54,15 @@ class TransformerWeights:
         self.init_scale = init_scale
         if cfg.n_heads % tp.size or cfg.n_kv_heads % tp.size or cfg.intermediate % tp.size or cfg.vocab % tp.size:
             raise ValueError(f"{cfg.name}: not shardable with tp={tp.size}")
+        # expert parallel (MoE under TP): whole experts [e0, e0 + n_local_experts) on this rank
+        self.ep = bool(expert_parallel and cfg.is_moe and tp.size > 1)
+        if self.ep and cfg.n_experts % tp.size:
+            raise ValueError(f"{cfg.name}: {cfg.n_experts} experts not shardable over ep={tp.size}")
+        self.n_local_experts = cfg.n_experts // tp.size if self.ep else cfg.n_experts
+        self.e0 = tp.rank * self.n_local_experts if self.ep else 0
         self.nh = cfg.n_heads // tp.size
         self.nkv = cfg.n_kv_heads // tp.size
-        self.inter = cfg.intermediate // tp.size
+        self.inter = cfg.intermediate if self.ep else cfg.intermediate // tp.size
         self.vocab_local = cfg.vocab // tp.size
         self.q_size = self.nh * cfg.head_dim
         self.kv_size = self.nkv * cfg.head_dim
@@ -122,11 +129,15 @@ class TransformerWeights:
                 if c.is_moe:
                     L.w_router = self._linear(p + "w_router", c.n_experts, c.hidden)
                     gus, downs = [], []
-                    for e in range(c.n_experts):
+                    for e in range(self.e0, self.e0 + self.n_local_experts):
                         gu = self._linear(p + f"experts.{e}.w_gu", 2 * c.intermediate, c.hidden)
-                        gus.append(gu[2 * i0:2 * i1])
                         dn = self._linear(p + f"experts.{e}.w_down", c.hidden, c.intermediate)
-                        downs.append(dn[:, i0:i1])
+                        if self.ep:  # whole experts
+                            gus.append(gu)
+                            downs.append(dn)
+                        else:        # every expert, 1/tp of its FFN rows
+                            gus.append(gu[2 * i0:2 * i1])
+                            downs.append(dn[:, i0:i1])
                     L.w_gu = torch.stack(gus).contiguous()
                     L.w_down = torch.stack(downs).contiguous()
                     del gus, downs

@@ -298,6 +298,8 @@ def moe_gemm(A, W_experts, sorted_rows, tile_expert, tile_count, out, N, K, max_
 
 
 def moe_combine(y, w, ids, h):
+    if not h.is_cuda:
+        return oracle.moe_combine(y, w, h)
     T, k = w.shape
     kernels().moe_combine(_p(y), _p(w), _p(ids), _p(h), T, k, h.shape[1], _s(h))
     return h
@@ -308,3 +310,15 @@ def moe_gemv(x, W_experts, ids, x_div, out, N, K, epi):
     kernels().moe_gemv(npairs, _p(x), x.stride(0), 0, 0.0, _p(W_experts), _p(ids), x_div, _p(out), out.stride(0), N, K,
                        epi, _s(x))
     return out
+
+
+def moe_ep_localize(ids, w, e0: int, n_local: int, lids_out, lw_out):
+    """Expert parallel: global expert ids -> local ids of experts [e0, e0 + n_local) on this rank,
+    -1 (and weight 0) for the others; device-side, so the decode graph stays replayable."""
+    if not ids.is_cuda:
+        lids, lw = oracle.moe_ep_localize(ids, w, e0, n_local)
+        lids_out.copy_(lids)
+        lw_out.copy_(lw)
+        return lids_out, lw_out
+    kernels().moe_ep_localize(_p(ids), _p(w), ids.numel(), int(e0), int(n_local), _p(lids_out), _p(lw_out), _s(ids))
+    return lids_out, lw_out

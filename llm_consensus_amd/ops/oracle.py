@@ -217,5 +217,24 @@ def moe_ffn(x: torch.Tensor, w_gu: torch.Tensor, w_down: torch.Tensor, rw: torch
     return h
 
 
+def moe_combine(y: torch.Tensor, w: torch.Tensor, h: torch.Tensor) -> torch.Tensor:
+    """h[t] += sum_j w[t,j] * y[t*k + j] in f32 (pairs with weight 0 — other ranks' experts
+    under expert parallelism — are skipped, their y rows may be garbage)."""
+    T, k = w.shape
+    yk = y.view(T, k, -1).float()
+    wf = w.float().unsqueeze(-1)
+    s = torch.where(wf != 0, wf * yk, torch.zeros((), dtype=torch.float32)).sum(1)
+    h.copy_((h.float() + s).to(torch.bfloat16))
+    return h
+
+
+def moe_ep_localize(ids: torch.Tensor, w: torch.Tensor, e0: int, n_local: int):
+    """Global expert ids -> this rank's local ids (-1 = another rank's expert, weight 0)."""
+    loc = (ids >= e0) & (ids < e0 + n_local)
+    lids = torch.where(loc, ids - e0, torch.full_like(ids, -1))
+    lw = torch.where(loc, w, torch.zeros_like(w))
+    return lids.to(torch.int32), lw
+
+
 def softmax_scale(D: int) -> float:
     return 1.0 / math.sqrt(D)

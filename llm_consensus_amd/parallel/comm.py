@@ -10,11 +10,19 @@ On GPUs the decode-sized collectives go through the custom one-shot xGMI kernels
 (``custom_ar.py``, K13) once ``enable_custom()`` has mapped the peers: no RCCL call and no host
 work per collective, so a TP engine's decode step is capturable in one HIP graph. Larger messages
 (prefill) and CPU/gloo groups use torch.distributed.
+
+Prefill under TP can run Megatron-style SEQUENCE PARALLEL (engine ``EngineConfig.sequence_parallel``):
+the residual stream is sharded by token rows between the layers, so each row-parallel output is a
+reduce-scatter (``reduce_scatter_rows``) and each norm runs on 1/tp of the tokens before an
+all-gather (``all_gather_rows``) feeds the next column-parallel GEMM — the same bytes on xGMI as
+the all-reduce, 1/tp of the norm/residual work and activation memory per rank. MoE models can
+shard EXPERTS instead of their FFN rows (``EngineConfig.expert_parallel``); with sequence-parallel
+token shards the tokens travel to their experts' ranks and back by all-to-all (``all_to_all_rows``).
 """
 
 from __future__ import annotations
 
-from typing import Optional
+from typing import List, Optional
 
 import torch
 import torch.distributed as dist
@@ -68,7 +76,56 @@ class TPGroup:
         if c is not None and t.is_cuda and t.is_contiguous() and out.is_contiguous() and c.fits(nbytes):
             return c.all_gather(t, out)
         flat = out.view(self.size * t.shape[0], *t.shape[1:])  # gloo wants dim-0 concatenation
+        if self._bounce(t):
+            f = flat.cpu()
+            dist.all_gather_into_tensor(f, t.contiguous().cpu(), group=self.group)
+            flat.copy_(f)
+            return out
         dist.all_gather_into_tensor(flat, t.contiguous(), group=self.group)
+        return out
+
+    def _bounce(self, t: torch.Tensor) -> bool:
+        """gloo collectives on GPU tensors (one-GPU rehearsals) go through host copies."""
+        return t.is_cuda and dist.get_backend(self.group) != "nccl"
+
+    def reduce_scatter_rows(self, full: torch.Tensor, out: torch.Tensor) -> torch.Tensor:
+        """Sum ``full`` [size * n, ...] over the group and keep this rank's row block
+        ``out`` [n, ...] = rows [rank * n, (rank + 1) * n) (Megatron SP)."""
+        if self.size == 1:
+            return out.copy_(full)
+        n = out.shape[0]
+        if full.is_cuda and not self._bounce(full):
+            dist.reduce_scatter_tensor(out, full.contiguous(), group=self.group)
+            return out
+        # gloo has no reduce-scatter: all-reduce, then keep the local block (same result)
+        f = full.cpu() if full.is_cuda else full
+        dist.all_reduce(f, group=self.group)
+        return out.copy_(f[self.rank * n:(self.rank + 1) * n])
+
+    def exchange_counts(self, send_counts: List[int]) -> List[int]:
+        """All-to-all of one int per peer: how many rows every peer will send me."""
+        if self.size == 1:
+            return list(send_counts)
+        nccl = dist.get_backend(self.group) == "nccl"
+        dev = torch.device("cuda", torch.cuda.current_device()) if nccl else torch.device("cpu")
+        s = torch.tensor(send_counts, dtype=torch.int64, device=dev)
+        r = torch.empty_like(s)
+        dist.all_to_all_single(r, s, group=self.group)
+        return [int(v) for v in r.tolist()]
+
+    def all_to_all_rows(self, x: torch.Tensor, send_counts: List[int], recv_counts: List[int]) -> torch.Tensor:
+        """Rows [sum(send_counts), ...] split by destination rank -> rows from every peer (C4,
+        expert-parallel token dispatch/combine)."""
+        out = x.new_empty((sum(recv_counts),) + tuple(x.shape[1:]))
+        if self.size == 1:
+            return out.copy_(x)
+        if self._bounce(x):
+            o = out.cpu()
+            dist.all_to_all_single(o, x.contiguous().cpu(), output_split_sizes=recv_counts,
+                                   input_split_sizes=send_counts, group=self.group)
+            return out.copy_(o)
+        dist.all_to_all_single(out, x.contiguous(), output_split_sizes=recv_counts, input_split_sizes=send_counts,
+                               group=self.group)
         return out
 
     def broadcast_(self, t: torch.Tensor, src_rank_in_group: int = 0) -> torch.Tensor:

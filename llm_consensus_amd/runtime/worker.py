@@ -250,7 +250,9 @@ def worker_main(gpu: int, conn, models: List[dict], dist_info: Optional[dict], t
             graphs = tp.size == 1 or tp.custom is not None or os.environ.get("LLMC_TP_GRAPHS") == "1"
             ecfg = EngineConfig(device="cpu" if on_cpu else f"cuda:{gpu}", max_context=m["max_context"],
                                 max_batch=m.get("max_batch", 1), max_seqs=m.get("max_seqs", 0), seed=m["seed"],
-                                use_graphs=graphs)
+                                use_graphs=graphs,
+                                # MoE under TP: whole experts per rank (LLMC_EXPERT_PARALLEL=1)
+                                expert_parallel=os.environ.get("LLMC_EXPERT_PARALLEL", "0") == "1")
             eng = Engine(cfg, ecfg, tp=tp, name=m["name"])
             hosts[m["name"]] = _EngineHost(m["name"], eng, send, tp.is_leader, faults.get(m["name"]))
         if not on_cpu:

@@ -19,7 +19,7 @@ def _free_port():
     return p
 
 
-def _worker(rank, world, port, name, q):
+def _worker(rank, world, port, name, q, ekw=None, prompt_len=24):
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
@@ -31,8 +31,8 @@ def _worker(rank, world, port, name, q):
 
         cfg = FAMILIES[name]
         tp = TPGroup(dist.group.WORLD, rank, world)
-        e = Engine(cfg, EngineConfig(device="cpu", max_context=128, seed=5), tp=tp)
-        p = [(i * 13) % 700 + 256 for i in range(24)]
+        e = Engine(cfg, EngineConfig(device="cpu", max_context=128, seed=5, **(ekw or {})), tp=tp)
+        p = [(i * 13) % 700 + 256 for i in range(prompt_len)]
         s = e.new_sequence()
         e.prefill([s], [p])
         logits = e.full_logits(s).clone().unsqueeze(0)
@@ -75,6 +75,51 @@ def test_tp2_matches_tp1(name):
     logits = torch.tensor(logits)
     # TP sums partials in a different order (and rounds partials to bf16): small drift only
     assert (logits[0] - ref_logits).abs().max().item() < 0.05 * ref_logits.abs().max().item()
+    top2 = torch.topk(ref_logits, 2).values
+    if (top2[0] - top2[1]).item() > 0.05:
+        assert gen[0] == ref_gen[0]
+
+
+def _run_tp(name, world, ekw, prompt_len):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, name, q, ekw, prompt_len)) for r in range(world)]
+    for pr in procs:
+        pr.start()
+    for pr in procs:
+        pr.join(timeout=240)
+    for pr in procs:
+        if pr.is_alive():
+            pr.kill()
+            pr.join()
+    assert all(pr.exitcode == 0 for pr in procs), [pr.exitcode for pr in procs]
+    logits, gen = q.get(timeout=10)
+    return torch.tensor(logits)[0], gen
+
+
+@pytest.mark.parametrize("name,ekw", [
+    ("llama-tiny", {"sp_min_tokens": 8}),                                   # sequence parallel prefill
+    ("mixtral-tiny", {"sp_min_tokens": 8}),                                 # SP + TP-sharded experts
+    ("mixtral-tiny", {"expert_parallel": True, "sequence_parallel": False}),  # EP, replicated tokens
+    ("mixtral-tiny", {"expert_parallel": True, "sp_min_tokens": 8}),        # EP + SP: all-to-all
+])
+def test_sp_ep_match_tp1(name, ekw):
+    """Megatron sequence parallelism (reduce-scatter / all-gather around the norms, a ragged 25-token
+    prompt padded to the shard size) and expert parallelism (whole experts per rank; all-to-all
+    token dispatch under SP) reproduce the TP=1 model (SURVEY.md §2.5 SP / EP rows, C4)."""
+    from llm_consensus_amd.engine import Engine, EngineConfig
+    from llm_consensus_amd.models.config import FAMILIES
+
+    ref = Engine(FAMILIES[name], EngineConfig(device="cpu", max_context=128, seed=5))
+    p = [(i * 13) % 700 + 256 for i in range(25)]
+    s = ref.new_sequence()
+    ref.prefill([s], [p])
+    ref_logits = ref.full_logits(s).clone()
+    ref.free_sequence(s)
+    ref_gen = ref.generate_ids(p, 6, temperature=0.0, stop_on_eos=False)
+    logits, gen = _run_tp(name, 2, ekw, 25)
+    assert (logits - ref_logits).abs().max().item() < 0.05 * ref_logits.abs().max().item()
     top2 = torch.topk(ref_logits, 2).values
     if (top2[0] - top2[1]).item() > 0.05:
         assert gen[0] == ref_gen[0]

@@ -22,7 +22,7 @@ def _free_port():
     return p
 
 
-def _worker(rank, world, port, name, q):
+def _worker(rank, world, port, name, q, ekw=None):
     import torch.distributed as dist
 
     try:
@@ -34,7 +34,7 @@ def _worker(rank, world, port, name, q):
 
         tp = TPGroup(dist.group.WORLD, rank, world)
         tp.enable_custom("cuda:0")
-        e = Engine(FAMILIES[name], EngineConfig(device="cuda:0", max_context=512, seed=5), tp=tp)
+        e = Engine(FAMILIES[name], EngineConfig(device="cuda:0", max_context=512, seed=5, **(ekw or {})), tp=tp)
         e.warmup_graphs()
         s = e.new_sequence()
         e.prefill([s], [PROMPT])
@@ -52,8 +52,13 @@ def _worker(rank, world, port, name, q):
         q.put((repr(ex) + traceback.format_exc(), None, True))
 
 
-@pytest.mark.parametrize("name", ["llama-small", "mixtral-tiny"])
-def test_tp2_gpu_matches_tp1(cuda, name):
+@pytest.mark.parametrize("name,ekw", [
+    ("llama-small", {}), ("mixtral-tiny", {}),
+    ("llama-small", {"sp_min_tokens": 16}),                            # sequence-parallel prefill
+    ("mixtral-tiny", {"expert_parallel": True}),                       # EP: localized ids in the graphs
+    ("mixtral-tiny", {"expert_parallel": True, "sp_min_tokens": 16}),  # EP + SP: all-to-all dispatch
+])
+def test_tp2_gpu_matches_tp1(cuda, name, ekw):
     from llm_consensus_amd.engine import Engine, EngineConfig
     from llm_consensus_amd.models.config import FAMILIES
 
@@ -69,7 +74,7 @@ def test_tp2_gpu_matches_tp1(cuda, name):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, 2, port, name, q)) for r in range(2)]
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, name, q, ekw)) for r in range(2)]
     for p in procs:
         p.start()
     logits, gen, tmo = q.get(timeout=400)

@@ -12,9 +12,10 @@ P = [(i * 13) % 700 + 256 for i in range(40)]
 NAME = os.environ.get("DBG_MODEL", "mixtral-tiny")
 
 
-def kv_rows(e, seq, layer):
+def kv_rows(e, seq, layer, n=None, cache=None):
     bs = e.bs
-    rows = [e.k_cache[layer, seq.blocks[p // bs], :, p % bs].float().cpu() for p in range(len(P))]
+    c = e.k_cache if cache is None else cache
+    rows = [c[layer, seq.blocks[p // bs], :, p % bs].float().cpu() for p in range(n or len(P))]
     return torch.stack(rows)  # [T, nkv, D]
 
 
@@ -32,8 +33,32 @@ def w(rank, world, port, ekw, q):
     e.prefill([s], [P])
     torch.cuda.synchronize()
     out = [kv_rows(e, s, li) for li in range(e.cfg.n_layers)]
+    e.free_sequence(s)
+    wsum = sum(float(L.w_gu.float().sum()) + float(L.w_down.float().sum()) for L in e.w.layers if L.w_gu is not None)
+    gen = e.generate_ids(P, 12, temperature=0.0, stop_on_eos=False)
+    wsum2 = sum(float(L.w_gu.float().sum()) + float(L.w_down.float().sum()) for L in e.w.layers if L.w_gu is not None)
+    if os.environ.get("DBG_KV_AFTER"):  # prefill + greedy decode on a kept sequence: K and V rows
+        from llm_consensus_amd.engine import SamplingParams
+        s2 = e.new_sequence()
+        e.prefill([s2], [P])
+        g2 = e.decode([s2], [SamplingParams(2, 0.0, 1.0, 0, 0, False)])[0]
+        torch.cuda.synchronize()
+        lg = e.logits[0].float().cpu()
+        # teacher-forced: prefill P + [first token] on a fresh sequence, full logits of the last row
+        s3 = e.new_sequence()
+        e.prefill([s3], [P + g2[:1]])
+        lt = e.full_logits(s3).float().cpu()
+        print(f"rank {rank} decode-step logits vs teacher-forced prefill: max err {float((lg - lt).abs().max()):.4f}"
+              f" argmax {int(lg.argmax())} vs {int(lt.argmax())}", flush=True)
+        kv = [(kv_rows(e, s2, li, len(P) + 5).tolist(), kv_rows(e, s2, li, len(P) + 5, e.v_cache).tolist())
+              for li in range(e.cfg.n_layers)]
+        torch.save({"gen": g2, "kv": kv}, f"gpurun_out/kv_{os.environ.get('DBG_TAG', 'x')}_r{rank}.pt")
+    if os.environ.get("DBG_NOSP_AFTER"):
+        e.ecfg.sequence_parallel = False  # (c): decode after a non-SP prefill, state left by the SP one
+        gen = e.generate_ids(P, 12, temperature=0.0, stop_on_eos=False)
+    print(f"rank {rank} weights {wsum} -> {wsum2} gen {gen} timed_out {e.tp.custom.timed_out()}", flush=True)
     if rank == 0:
-        q.put([o.tolist() for o in out])
+        q.put(([o.tolist() for o in out], gen))
     dist.barrier()
     dist.destroy_process_group()
 
@@ -47,13 +72,22 @@ if __name__ == "__main__":
     ref.prefill([s], [P])
     torch.cuda.synchronize()
     refs = [kv_rows(ref, s, li) for li in range(ref.cfg.n_layers)]
-    for i, ekw in enumerate([{}, {"expert_parallel": True}, {"expert_parallel": True, "sp_min_tokens": 16},
-                             {"sp_min_tokens": 16}]):
+    ref.free_sequence(s)
+    print("ref gen", ref.generate_ids(P, 12, temperature=0.0, stop_on_eos=False), flush=True)
+    cfgs = [{}, {"expert_parallel": True}, {"expert_parallel": True, "sp_min_tokens": 16}, {"sp_min_tokens": 16},
+            {"expert_parallel": True, "sp_min_tokens": 16, "use_graphs": False},
+            {"expert_parallel": True, "use_graphs": False, "steps_per_graph": 1},
+            {"expert_parallel": True, "sp_min_tokens": 16, "use_graphs": False, "steps_per_graph": 1}]
+    only = os.environ.get("DBG_ONLY")
+    for i, ekw in enumerate(cfgs):
+        if only and str(i) not in only.split(","):
+            continue
         ctx = mp.get_context("spawn")
         q = ctx.Queue()
         ps = [ctx.Process(target=w, args=(r, 2, 29700 + i, ekw, q)) for r in range(2)]
         [p.start() for p in ps]
-        out = q.get(timeout=200)
+        out, gen = q.get(timeout=200)
+        print(ekw, "gen", gen, flush=True)
         [p.join() for p in ps]
         for li, o in enumerate(out):
             o = torch.tensor(o)

@@ -84,10 +84,18 @@ def test_tp2_gpu_matches_tp1(cuda, name, ekw):
     assert not tmo
     logits = torch.tensor(logits)
     assert (logits - ref_logits).abs().max().item() < 0.05 * ref_logits.abs().max().item()
-    # greedy continuation: equal until the first numerical near-tie
+    # greedy continuation: equal until the first numerical near-tie, which the TP=1 model must
+    # confirm (teacher-forced: its logits at the diverging position put the TP token within noise
+    # of its own argmax)
     agree = 0
     for a, b in zip(gen, ref_gen):
         if a != b:
             break
         agree += 1
-    assert agree >= 8, (gen, ref_gen)
+    if agree < 8:
+        ref = Engine(FAMILIES[name], EngineConfig(device="cuda:0", max_context=512, seed=5))
+        s = ref.new_sequence()
+        ref.prefill([s], [PROMPT + gen[:agree]])
+        lt = ref.full_logits(s).float().cpu()
+        gap = float(lt.max() - lt[gen[agree]])
+        assert gap < 0.01 * float(lt.abs().max()), (agree, gap, gen, ref_gen)

@@ -62,6 +62,7 @@ class Config:
     gpus: str
     trace: bool
     placement: str = ""
+    judge_tp: int = 0
 
 
 def make_flagset() -> FlagSet:
@@ -87,6 +88,8 @@ def make_flagset() -> FlagSet:
     fs.add("trace", "bool", False, "Write a Chrome trace of engine spans to the run directory")
     fs.add("placement", "string", "",
            "Pin models to GPUs: model=gpu[+gpu...],... ('+' = tensor-parallel group); the rest are placed automatically")
+    fs.add("judge-tp", "int", 0,
+           "Run a local judge tensor-parallel over the first N GPUs, beside the responders (0 = placed by the solver)")
     fs.add("list-models", "bool", False, "Print the local model catalog as JSON and exit")
     fs.add("weights-dir", "string", "",
            "Comma-separated Hugging Face checkpoint dirs (or parents of them) to serve as models ($LLMC_WEIGHTS_DIR)")
@@ -168,7 +171,8 @@ def parse_flags(argv: List[str], stdout: TextIO = sys.stdout, stderr: TextIO = s
     cfg = Config(models=models, judge=v["judge"], file=v["file"], output=v["output"], data_dir=v["data_dir"],
                  timeout=float(v["timeout"]), prompt="", quiet=v["quiet"], json=v["json"], no_save=v["no_save"],
                  max_tokens=v["max_tokens"], temperature=v["temperature"], top_p=v["top_p"], top_k=v["top_k"],
-                 seed=v["seed"], gpus=v["gpus"], trace=v["trace"], placement=v["placement"])
+                 seed=v["seed"], gpus=v["gpus"], trace=v["trace"], placement=v["placement"],
+                 judge_tp=v["judge_tp"])
     cfg.prompt = get_prompt(rest, cfg.file, stdin)
     return cfg
 
@@ -209,7 +213,7 @@ def init_registry(cfg: Config) -> Registry:
 
             pins = parse_pins(cfg.placement) if cfg.placement else None
             backend = LocalBackend(local_specs, judge=cfg.judge, gpus=gpus, trace=cfg.trace, counts=counts,
-                                   pins=pins)
+                                   pins=pins, judge_tp=cfg.judge_tp)
         except Exception as e:  # noqa: BLE001
             raise CLIError(f"initializing provider for {local_specs[0].name}: {e}") from None
         for spec in local_specs:

@@ -95,7 +95,7 @@ class LocalBackend:
     def __init__(self, specs: List[ModelSpec], judge: Optional[str] = None, gpus: Optional[List[int]] = None,
                  trace: bool = False, counts: Optional[Dict[str, int]] = None,
                  max_context: Optional[Dict[str, int]] = None, start_timeout: float = 1800.0,
-                 pins: Optional[Dict[str, List[int]]] = None):
+                 pins: Optional[Dict[str, List[int]]] = None, judge_tp: int = 0):
         import multiprocessing as mp
 
         self.specs = {s.name: s for s in specs}
@@ -112,6 +112,13 @@ class LocalBackend:
         self._ids = itertools.count(1)
         self.closed = False
 
+        if judge_tp > 1 and judge in self.specs and not (pins and judge in pins):
+            # the judge phase follows the fan-out, when the responders' GPUs are idle: shard the
+            # judge over the first judge_tp of them (co-located on its own streams)
+            if judge_tp > len(gpu_ids):
+                raise LocalError(f"--judge-tp {judge_tp} needs {judge_tp} GPUs, {len(gpu_ids)} available")
+            pins = dict(pins or {})
+            pins[judge] = list(gpu_ids[:judge_tp])
         demands = []
         self._ctx = {}
         for s in specs:

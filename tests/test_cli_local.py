@@ -107,3 +107,14 @@ def test_cli_tp_judge_over_cpu_workers():
     d = json.loads(out)
     assert sorted(r["model"] for r in d["responses"]) == ["llama-tiny@1", "mixtral-tiny", "phi3-tiny"]
     assert d["judge"] == "llama-tiny@j" and len(d["consensus"]) > 0
+
+
+def test_cli_judge_tp_flag_cpu():
+    """--judge-tp 2 shards the judge over the first two workers, beside the responders (the bench's
+    idle-GPU judge, through the CLI)."""
+    rc, out, err = run_cli(["--models", "llama-tiny@1,llama-tiny@2", "--judge", "llama-tiny@j", "--judge-tp", "2",
+                            "--max-tokens", "8", "--temperature", "0", "--json", "Explain tensor parallelism."],
+                           env={"LLMC_DEVICE": "cpu", "LLMC_CPU_WORKERS": "2"})
+    assert rc == 0, err
+    d = json.loads(out)
+    assert d["judge"] == "llama-tiny@j" and len(d["consensus"]) > 0 and len(d["responses"]) == 2

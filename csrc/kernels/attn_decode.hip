@@ -188,16 +188,21 @@ __global__ __launch_bounds__(256) void attn_decode_kernel(
   }
 }
 
-// grid (nkv * G, B, ceil(D / 64)), 256 threads: one query head x 64 dims per block; the 256
-// threads are 64 dims x 4 chunk groups. ONE memory round trip for up to 64 chunks: every thread
-// issues its (up to 16) partial-value loads and the block its m / l loads together — the values
-// do not depend on the softmax max — then the max, the scale factors and the weighted sums are
-// formed from registers and LDS; chunk groups meet in LDS.
-template <int G>
+// grid (nkv * G, B, ceil(D / DB)), 256 threads: one query head x DB dims per block; the 256
+// threads are DB dims x (256 / DB) chunk groups. ONE memory round trip for up to 16 * 256 / DB
+// chunks: every thread issues its (up to 16) partial-value loads and the block its m / l loads
+// together — the values do not depend on the softmax max — then the max, the scale factors and
+// the weighted sums are formed from registers and LDS; chunk groups meet in LDS. The host picks
+// DB from the grid's chunk count (64 / 32 / 16 for <= 64 / 128 / 256 chunks) so a wide split
+// (a TP rank's single kv head spread over 256 blocks) still merges in one round trip, on 4x the
+// blocks, instead of 4 dependent batches.
+template <int G, int DB>
 __global__ __launch_bounds__(256) void attn_decode_reduce_kernel(const float* __restrict__ part,
                                                                  const int32_t* __restrict__ seq_lens,
                                                                  bf16_t* __restrict__ out, int out_stride, int nkv,
                                                                  int D, int chunk_arg, int gc, int max_chunks) {
+  static_assert(DB == 16 || DB == 32 || DB == 64, "DB");
+  constexpr int CG = 256 / DB;  // chunk groups
   const int kvh = blockIdx.x / G, g = blockIdx.x % G, b = blockIdx.y;
   const int L = seq_lens[b];
   const int nchunks = decode_nsplit(L, gc, chunk_arg);
@@ -205,18 +210,18 @@ __global__ __launch_bounds__(256) void attn_decode_reduce_kernel(const float* __
   extern __shared__ __attribute__((aligned(16))) char smem[];
   float* sc = reinterpret_cast<float*>(smem);  // [max_chunks]: m, then exp(m - M)
   float* lv = sc + max_chunks;                 // [max_chunks]: l
-  float* red = lv + max_chunks;                // [4][64] + 8 scratch
+  float* red = lv + max_chunks;                // [CG][DB] + 8 scratch
   const int tid = threadIdx.x, stride = D + 2;
   const float* pb = part + ((static_cast<int64_t>(b) * nkv + kvh) * max_chunks * G + g) * stride;
   const int64_t cstride = static_cast<int64_t>(G) * stride;  // between consecutive chunks
-  const int dl = tid & 63, cg = tid >> 6;
-  const int d = blockIdx.z * 64 + dl;
+  const int dl = tid % DB, cg = tid / DB;
+  const int d = blockIdx.z * DB + dl;
   const bool live = d < D;
-  // issue: this thread's first 16 partial values (chunks cg, cg + 4, ...) and the m / l words
+  // issue: this thread's first 16 partial values (chunks cg, cg + CG, ...) and the m / l words
   float v[16];
 #pragma unroll
   for (int j = 0; j < 16; ++j) {
-    const int c = min(cg + 4 * j, nchunks - 1);  // clamped: all loads in flight, masked below
+    const int c = min(cg + CG * j, nchunks - 1);  // clamped: all loads in flight, masked below
     v[j] = live ? pb[c * cstride + d] : 0.f;
   }
   float mx = kNegBig;
@@ -242,24 +247,31 @@ __global__ __launch_bounds__(256) void attn_decode_reduce_kernel(const float* __
   const float lsum = red[260] + red[261] + red[262] + red[263];
   float o = 0.f;
 #pragma unroll
-  for (int j = 0; j < 16; ++j) o += (cg + 4 * j < nchunks) ? v[j] * sc[cg + 4 * j] : 0.f;
-  for (int c0 = cg + 64; c0 < nchunks; c0 += 64) {  // > 64 chunks: further batches
+  for (int j = 0; j < 16; ++j) o += (cg + CG * j < nchunks) ? v[j] * sc[cg + CG * j] : 0.f;
+  for (int c0 = cg + 16 * CG; c0 < nchunks; c0 += 16 * CG) {  // beyond one round trip: further batches
     float w[16];
 #pragma unroll
     for (int j = 0; j < 16; ++j) {
-      const int c = min(c0 + 4 * j, nchunks - 1);
+      const int c = min(c0 + CG * j, nchunks - 1);
       w[j] = live ? pb[c * cstride + d] : 0.f;
     }
 #pragma unroll
-    for (int j = 0; j < 16; ++j) o += (c0 + 4 * j < nchunks) ? w[j] * sc[c0 + 4 * j] : 0.f;
+    for (int j = 0; j < 16; ++j) o += (c0 + CG * j < nchunks) ? w[j] * sc[c0 + CG * j] : 0.f;
   }
-  red[cg * 64 + dl] = o;
+  red[cg * DB + dl] = o;
   __syncthreads();
   if (cg == 0 && live) {
-    const float tot = red[dl] + red[64 + dl] + red[128 + dl] + red[192 + dl];
+    float tot = 0.f;
+#pragma unroll
+    for (int i = 0; i < CG; ++i) tot += red[i * DB + dl];
     out[static_cast<int64_t>(b) * out_stride + (kvh * G + g) * D + d] = f32_to_bf16(tot / lsum);
   }
 }
+
+// One reduce launch; DB (dims per block) from the largest chunk count this grid can produce.
+template <int G>
+static int launch_reduce(int B, int nkv, int D, int chunk, int gc, int max_chunks, hipStream_t s, const void* part,
+                         const void* sl, void* out, int out_stride);
 
 static size_t reduce_lds(int max_chunks) { return (2 * static_cast<size_t>(max_chunks) + 256 + 8) * sizeof(float); }
 
@@ -292,8 +304,7 @@ static int launch_decode(int B, int nkv, int grid_chunks, hipStream_t s, const v
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return static_cast<int>(e);
   if (grid_chunks > 1) {
-    attn_decode_reduce_kernel<G><<<dim3(nkv * G, B, (D + 63) / 64), 256, reduce_lds(max_chunks), s>>>(
-        (const float*)part, (const int32_t*)sl, (bf16_t*)out, out_stride, nkv, D, chunk, grid_chunks, max_chunks);
+    return launch_reduce<G>(B, nkv, D, chunk, grid_chunks, max_chunks, s, part, sl, out, out_stride);
   }
   return static_cast<int>(hipGetLastError());
 }
@@ -311,12 +322,32 @@ extern "C" int llmc_attn_decode_mfma(const void*, int, const void*, const void*,
                                      void*, void*, int, int, int, int, int, int, int, int, int, float, int,
                                      hipStream_t);
 
+namespace llmc {
+template <int G>
+static int launch_reduce(int B, int nkv, int D, int chunk, int gc, int max_chunks, hipStream_t s, const void* part,
+                         const void* sl, void* out, int out_stride) {
+  // chunks this grid can produce: gc (balanced form) or ceil(context / chunk) (fixed chunks: gc
+  // is the bucket's chunk count as well)
+  const int nmax = gc;
+  const size_t lds = reduce_lds(max_chunks);
+  if (nmax <= 64) {
+    attn_decode_reduce_kernel<G, 64><<<dim3(nkv * G, B, (D + 63) / 64), 256, lds, s>>>(
+        (const float*)part, (const int32_t*)sl, (bf16_t*)out, out_stride, nkv, D, chunk, gc, max_chunks);
+  } else if (nmax <= 128) {
+    attn_decode_reduce_kernel<G, 32><<<dim3(nkv * G, B, (D + 31) / 32), 256, lds, s>>>(
+        (const float*)part, (const int32_t*)sl, (bf16_t*)out, out_stride, nkv, D, chunk, gc, max_chunks);
+  } else {
+    attn_decode_reduce_kernel<G, 16><<<dim3(nkv * G, B, (D + 15) / 16), 256, lds, s>>>(
+        (const float*)part, (const int32_t*)sl, (bf16_t*)out, out_stride, nkv, D, chunk, gc, max_chunks);
+  }
+  return static_cast<int>(hipGetLastError());
+}
+}  // namespace llmc
+
 template <int G>
 static int launch_reduce_only(int B, int nkv, int D, int chunk, int gc, int max_chunks, hipStream_t s, const void* part,
                               const void* sl, void* out, int out_stride) {
-  attn_decode_reduce_kernel<G><<<dim3(nkv * G, B, (D + 63) / 64), 256, reduce_lds(max_chunks), s>>>(
-      (const float*)part, (const int32_t*)sl, (bf16_t*)out, out_stride, nkv, D, chunk, gc, max_chunks);
-  return static_cast<int>(hipGetLastError());
+  return launch_reduce<G>(B, nkv, D, chunk, gc, max_chunks, s, part, sl, out, out_stride);
 }
 
 extern "C" int llmc_attn_decode(const void* q, int q_stride, const void* k_cache, const void* v_cache,

@@ -69,6 +69,35 @@ def bench_attn():
         print(f"attn L={L:6d}: " + "  ".join(line) + f"  | best {gb / best * 1e6 / 1e3:5.2f} TB/s")
 
 
+def bench_attn_tp():
+    """Decode attention at the per-rank head counts of a tensor-parallel Llama-3-8B (TP = 1, 2, 4,
+    8 -> 8, 4, 2, 1 kv heads, GQA group 4): attention alone (mode 4 = MFMA partials, no merge)
+    and attention + reduce kernel (mode 2) over the grid size (blocks per kv head)."""
+    D, bs = 128, 64
+    for nkv in [8, 4, 2, 1]:
+        nh = 4 * nkv
+        for L in [2048, 8192, 33000]:
+            nb = (L + bs - 1) // bs + 2
+            kc = torch.randn(nb, nkv, bs, D, device="cuda").to(BF)
+            vc = torch.randn_like(kc)
+            bt = torch.arange(nb, dtype=torch.int32, device="cuda").view(1, -1)
+            sl = torch.tensor([L], dtype=torch.int32, device="cuda")
+            q = torch.randn(1, nh * D, device="cuda").to(BF)
+            out = torch.empty(1, nh * D, dtype=BF, device="cuda")
+            line = []
+            for gc in [16, 32, 64, 128, 256, 512]:
+                gc_eff = min(gc, (L + 127) // 128)
+                if gc_eff < gc and gc > 16:
+                    continue
+                part, ctr = ops.decode_attn_workspace(1, nh, nkv, D, gc_eff, "cuda")
+                t2 = timeit(lambda: ops.attn_decode(q, kc, vc, bt, sl, out, part, ctr, nh, nkv, D, bs, 128,
+                                                    1 / math.sqrt(D), grid_chunks=gc_eff, mode=2))
+                t4 = timeit(lambda: ops.attn_decode(q, kc, vc, bt, sl, out, part, ctr, nh, nkv, D, bs, 128,
+                                                    1 / math.sqrt(D), grid_chunks=gc_eff, mode=4))
+                line.append(f"g{gc_eff}: {t2:5.2f} (attn {t4:5.2f})")
+            print(f"attn nkv={nkv} L={L:6d}: " + "  ".join(line), flush=True)
+
+
 def bench_gemv():
     for (N, K, epi, norm) in [(6144, 4096, 0, True), (4096, 4096, 2, False), (28672, 4096, 3, True),
                               (4096, 14336, 2, False), (128256, 4096, 1, True)]:
@@ -160,6 +189,8 @@ if __name__ == "__main__":
         bench_attn()
     if what in ("gemv", "all"):
         bench_gemv()
+    if what in ("attn-tp",):
+        bench_attn_tp()
     if what in ("sweep",):
         bench_gemv_sweep()
     if what in ("sweep-phi3",):  # Phi-3-mini shapes (K = 3072 / 8192)

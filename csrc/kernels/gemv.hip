@@ -11,10 +11,10 @@
 
 namespace llmc {
 
-template <int M, int NT, int RPW, int PRO, int EPI>
+template <int M, int NT, int RPW, int PRO, int EPI, int UNROLL_OVERRIDE = 0>
 static int launch_gemv_g(const void* x, int x_stride, const void* nw, float eps, const void* W, void* out,
                          int out_stride, int N, int K, const RopeEpi& rope, const MergePro& mp, hipStream_t s) {
-  constexpr int UNROLL = RPW == 1 ? 4 : (RPW == 2 ? 4 : (M <= 2 ? 4 : 2));
+  constexpr int UNROLL = UNROLL_OVERRIDE ? UNROLL_OVERRIDE : (RPW == 1 ? 4 : (RPW == 2 ? 4 : (M <= 2 ? 4 : 2)));
   constexpr int WAVES = NT / kWave;
   auto kern = gemv_kernel<M, NT, RPW, UNROLL, PRO, EPI, false>;
   // x [M][K] bf16 | norm partials [M][WAVES] f32 | pair exchange [WAVES/2][M] f32
@@ -37,6 +37,10 @@ static int launch_gemv_g(const void* x, int x_stride, const void* nw, float eps,
 // rows/block = 384 blocks leaves half the CUs with twice the work; 12 rows/block = 512 blocks
 // is exact): the smallest idle fraction of the last round, ties to the larger block.
 static int pick_waves(int N, bool paired) {
+  // short outputs (a TP rank's qkv: 768 / 1536 rows) cannot fill the chip with fat blocks: 4-wave
+  // blocks with 8 loads per lane spread them over 3-6x the CUs (768x4096: 4.04 vs 5.68 us,
+  // profiles/r1_attn_decode_tp_shapes.md)
+  if (N < 2048 && (!paired || N % 8 == 0)) return 4;
   int best = 16;
   double best_idle = 2.0;
   for (int w : {16, 12, 8}) {
@@ -60,6 +64,7 @@ static int launch_gemv(const void* x, int x_stride, const void* nw, float eps, c
     case 16: return launch_gemv_g<M, 1024, 1, PRO, EPI>(x, x_stride, nw, eps, W, out, out_stride, N, K, rope, mp, s);
     case 12: return launch_gemv_g<M, 768, 1, PRO, EPI>(x, x_stride, nw, eps, W, out, out_stride, N, K, rope, mp, s);
     case 8: return launch_gemv_g<M, 512, 1, PRO, EPI>(x, x_stride, nw, eps, W, out, out_stride, N, K, rope, mp, s);
+    case 4: return launch_gemv_g<M, 256, 1, PRO, EPI, 8>(x, x_stride, nw, eps, W, out, out_stride, N, K, rope, mp, s);
     default:  // paired rows that do not tile by 16-32 rows: pairs inside one wave
       return launch_gemv_g<M, 256, 2, PRO, EPI>(x, x_stride, nw, eps, W, out, out_stride, N, K, rope, mp, s);
   }
@@ -162,6 +167,7 @@ static int moe_gemv_geom(int npairs, const void* x, int x_stride, float eps, con
     case 16: return launch_moe_gemv<1024, 1, EPI>(npairs, x, x_stride, eps, W, ids, x_div, out, out_stride, N, K, s);
     case 12: return launch_moe_gemv<768, 1, EPI>(npairs, x, x_stride, eps, W, ids, x_div, out, out_stride, N, K, s);
     case 8: return launch_moe_gemv<512, 1, EPI>(npairs, x, x_stride, eps, W, ids, x_div, out, out_stride, N, K, s);
+    case 4: return launch_moe_gemv<256, 1, EPI>(npairs, x, x_stride, eps, W, ids, x_div, out, out_stride, N, K, s);
     default: return launch_moe_gemv<256, 2, EPI>(npairs, x, x_stride, eps, W, ids, x_div, out, out_stride, N, K, s);
   }
 }

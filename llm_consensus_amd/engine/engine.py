@@ -185,7 +185,10 @@ class Engine:
                             torch.zeros(self.tp.size, B, self.w.vocab_local, dtype=torch.float32, device=dev))
         # split-KV decode attention: one (chunk, grid) shape per context bucket
         ctxmax = self.ecfg.max_context + self.ecfg.steps_per_graph + 2
-        blocks = int(os.environ.get("LLMC_ATTN_BLOCKS", "256"))  # target blocks per decode row (1/CU)
+        # target blocks per decode row: ~1 per CU; without GQA (Phi-3: one query head per kv head)
+        # a block's key range costs less, and 2 per CU measured faster (9.45 vs 9.85 us at 2k keys,
+        # 14.9 vs 15.9 at 4k: profiles/r1_attn_decode_tp_shapes.md)
+        blocks = int(os.environ.get("LLMC_ATTN_BLOCKS", "512" if self.nh == self.nkv else "256"))
         fixed = self.ecfg.attn_chunk or (0 if ops.ATTN_DECODE_MODE >= 2 else 128)  # VALU modes: fixed chunks
         self.attn_buckets = attn_buckets(ctxmax, fixed, max(1, blocks // self.nkv))
         self.max_chunks = max(gc for _, _, gc in self.attn_buckets)

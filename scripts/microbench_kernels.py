@@ -69,6 +69,32 @@ def bench_attn():
         print(f"attn L={L:6d}: " + "  ".join(line) + f"  | best {gb / best * 1e6 / 1e3:5.2f} TB/s")
 
 
+def bench_attn_phi3():
+    """Phi-3-mini decode attention (32 heads = 32 kv heads, D = 96, no GQA) over the grid size."""
+    nh = nkv = 32
+    D, bs = 96, 64
+    for L in [512, 1024, 2048, 4096]:
+        nb = (L + bs - 1) // bs + 2
+        kc = torch.randn(nb, nkv, bs, D, device="cuda").to(BF)
+        vc = torch.randn_like(kc)
+        bt = torch.arange(nb, dtype=torch.int32, device="cuda").view(1, -1)
+        sl = torch.tensor([L], dtype=torch.int32, device="cuda")
+        q = torch.randn(1, nh * D, device="cuda").to(BF)
+        out = torch.empty(1, nh * D, dtype=BF, device="cuda")
+        line = []
+        for gc in [1, 2, 4, 8, 16, 32]:
+            gc_eff = min(gc, (L + 127) // 128)
+            if gc_eff < gc:
+                continue
+            part, ctr = ops.decode_attn_workspace(1, nh, nkv, D, gc_eff, "cuda")
+            t2 = timeit(lambda: ops.attn_decode(q, kc, vc, bt, sl, out, part, ctr, nh, nkv, D, bs, 128,
+                                                1 / math.sqrt(D), grid_chunks=gc_eff, mode=2))
+            t4 = timeit(lambda: ops.attn_decode(q, kc, vc, bt, sl, out, part, ctr, nh, nkv, D, bs, 128,
+                                                1 / math.sqrt(D), grid_chunks=gc_eff, mode=4))
+            line.append(f"g{gc_eff}: {t2:5.2f} (attn {t4:5.2f})")
+        print(f"phi3 attn L={L:6d}: " + "  ".join(line), flush=True)
+
+
 def bench_attn_tp():
     """Decode attention at the per-rank head counts of a tensor-parallel Llama-3-8B (TP = 1, 2, 4,
     8 -> 8, 4, 2, 1 kv heads, GQA group 4): attention alone (mode 4 = MFMA partials, no merge)
@@ -113,6 +139,9 @@ SWEEP = ["256x1u8", "256x2u4", "256x4u4", "512x1u8", "512x2u4", "128x1u8", "64x1
          "256x2u8", "512x4u2", "128x2u4", "1024x1u8", "1024x2u4", "1024x2u2", "1024x1u2", "768x1u4", "1024x4u2", "1024x1u6"]
 
 
+ALL_VARIANTS = os.environ.get("SWEEP_ALL") == "1"
+
+
 def bench_gemv_sweep(shapes=None):
     """GEMV geometry sweep on COLD weights: the graph cycles through enough copies of W to exceed
     the 256 MB MALL, as in a real decode step (16 GB streamed per token)."""
@@ -129,7 +158,8 @@ def bench_gemv_sweep(shapes=None):
         out = torch.zeros(1, N, dtype=BF, device="cuda")
         res = []
         for v, name in enumerate(SWEEP):
-            if name not in ("256x2u4", "512x1u8", "1024x1u4", "1024x1u6", "1024x1u8", "768x1u4", "1024x1u2"):
+            if not ALL_VARIANTS and name not in ("256x2u4", "512x1u8", "1024x1u4", "1024x1u6", "1024x1u8", "768x1u4",
+                                                 "1024x1u2"):
                 continue
             st = torch.cuda.current_stream().cuda_stream
 
@@ -189,11 +219,15 @@ if __name__ == "__main__":
         bench_attn()
     if what in ("gemv", "all"):
         bench_gemv()
+    if what in ("attn-phi3",):
+        bench_attn_phi3()
     if what in ("attn-tp",):
         bench_attn_tp()
     if what in ("sweep",):
         bench_gemv_sweep()
     if what in ("sweep-phi3",):  # Phi-3-mini shapes (K = 3072 / 8192)
         bench_gemv_sweep([(9216, 3072), (16384, 3072), (3072, 3072), (3072, 8192)])
+    if what in ("sweep-tp8",):  # one TP=8 rank of Llama-3-8B: qkv, gate_up, o, down
+        bench_gemv_sweep([(768, 4096), (1536, 4096), (3584, 4096), (4096, 512), (4096, 1792)])
     if what in ("prefill",):
         bench_prefill()

@@ -46,7 +46,8 @@ def test_embedding_and_silu(cuda):
 
 
 @pytest.mark.parametrize("M", [1, 2, 3, 4])
-@pytest.mark.parametrize("N,K", [(64, 256), (1000, 4096), (4096, 4096), (512, 14336), (130, 192), (6144, 512), (9216, 256)])
+@pytest.mark.parametrize("N,K", [(64, 256), (1000, 4096), (4096, 4096), (512, 14336), (130, 192), (6144, 512), (9216, 256),
+                                 (1792, 4096)])
 @pytest.mark.parametrize("epi", [0, 1, 2, 3])
 def test_gemv(cuda, M, N, K, epi):
     if M > 1 and K > 8192:
@@ -122,7 +123,8 @@ def test_rope_kv_write(cuda, nh, nkv, D):
 
 
 @pytest.mark.parametrize("M", [1, 2, 4])
-@pytest.mark.parametrize("nh,nkv,D,H", [(32, 8, 128, 4096), (32, 32, 96, 3072), (4, 2, 64, 256), (16, 2, 128, 8192)])
+@pytest.mark.parametrize("nh,nkv,D,H", [(32, 8, 128, 4096), (32, 32, 96, 3072), (4, 2, 64, 256), (16, 2, 128, 8192),
+                                          (4, 1, 128, 4096), (8, 2, 128, 4096)])
 def test_gemv_qkv_rope(cuda, M, nh, nkv, D, H):
     """Fused decode qkv GEMV (norm prologue + RoPE/KV-write epilogue) vs the 2-step oracle."""
     torch.manual_seed(12)

@@ -21,11 +21,12 @@ ap = argparse.ArgumentParser()
 ap.add_argument("--tp", default="1,2,4,8")
 ap.add_argument("--ctx", default="2048,33000")
 ap.add_argument("--tokens", type=int, default=256)
+ap.add_argument("--model", default="llama-3-8b")
 a = ap.parse_args()
 
-base = FAMILIES["llama-3-8b"]
+base = FAMILIES[a.model]
 for tp in [int(t) for t in a.tp.split(",")]:
-    cfg = base.with_(name=f"llama-8b-tp{tp}-shard32", n_heads=base.n_heads // tp, n_kv_heads=base.n_kv_heads // tp,
+    cfg = base.with_(name=f"{a.model}-tp{tp}-shard", n_heads=base.n_heads // tp, n_kv_heads=base.n_kv_heads // tp,
                      intermediate=base.intermediate // tp, vocab=base.vocab // tp)
     ctxs = [int(c) for c in a.ctx.split(",")]
     e = Engine(cfg, EngineConfig(device="cuda:0", max_context=max(ctxs) + a.tokens + 64, seed=1))
@@ -50,7 +51,7 @@ for tp in [int(t) for t in a.tp.split(",")]:
         tp_s = time.perf_counter() - t
         e.free_sequence(s)
         ms = 1000 * (dt - tp_s) / len(out)
-        print(f"tp={tp} ctx={ctx}: decode {ms:.3f} ms/token ({mb:.0f} MB streamed/token -> "
+        print(f"{a.model} tp={tp} ctx={ctx}: decode {ms:.3f} ms/token ({mb:.0f} MB streamed/token -> "
               f"{mb / 1e3 / ms:.2f} TB/s effective), prefill {ctx} tokens {1000 * tp_s:.1f} ms", flush=True)
     del e
     torch.cuda.empty_cache()

@@ -186,6 +186,8 @@ def main() -> None:
             for t in ths:
                 t.join()
         t_resp = time.perf_counter()
+        if rank == 0:
+            log(f"round {step}: responders done in {t_resp - t_start:.2f}s")
         # gather responses to rank 0 (fixed-size int32 rows; RCCL over xGMI)
         local_t = torch.full((mpg, args.max_tokens), -1, dtype=torch.int32, device=dev)
         for j, ids in enumerate(outs):
@@ -209,6 +211,8 @@ def main() -> None:
             rest_ids = jtok.encode(full[len(head):])
             judge.prefill([jseq], [rest_ids])
             t_jp = time.perf_counter()
+            if rank == 0:
+                log(f"round {step}: judge prefill of {len(rest_ids)} tokens in {t_jp - t_resp:.2f}s (TP={jtp})")
             jids = judge.decode([jseq], [SamplingParams(jmax, args.temperature, 1.0, 0, 99 + step, False)])[0]
             stats["judge_prompt_tokens"] = jseq.length - len(jids)
             stats["judge_prefill_s"] = t_jp - t_resp

@@ -63,6 +63,8 @@ class Config:
     trace: bool
     placement: str = ""
     judge_tp: int = 0
+    server: str = ""
+    judge_explicit: bool = True
 
 
 def make_flagset() -> FlagSet:
@@ -90,6 +92,8 @@ def make_flagset() -> FlagSet:
            "Pin models to GPUs: model=gpu[+gpu...],... ('+' = tensor-parallel group); the rest are placed automatically")
     fs.add("judge-tp", "int", 0,
            "Run a local judge tensor-parallel over the first N GPUs, beside the responders (0 = placed by the solver)")
+    fs.add("server", "string", "",
+           "Send the run to a running llm-consensus server (URL) instead of starting engines ($LLMC_SERVER)")
     fs.add("list-models", "bool", False, "Print the local model catalog as JSON and exit")
     fs.add("weights-dir", "string", "",
            "Comma-separated Hugging Face checkpoint dirs (or parents of them) to serve as models ($LLMC_WEIGHTS_DIR)")
@@ -172,13 +176,15 @@ def parse_flags(argv: List[str], stdout: TextIO = sys.stdout, stderr: TextIO = s
                  timeout=float(v["timeout"]), prompt="", quiet=v["quiet"], json=v["json"], no_save=v["no_save"],
                  max_tokens=v["max_tokens"], temperature=v["temperature"], top_p=v["top_p"], top_k=v["top_k"],
                  seed=v["seed"], gpus=v["gpus"], trace=v["trace"], placement=v["placement"],
-                 judge_tp=v["judge_tp"])
+                 judge_tp=v["judge_tp"], server=v["server"] or os.environ.get("LLMC_SERVER", ""),
+                 judge_explicit=any(a.lstrip("-").split("=")[0] == "judge" for a in argv[:len(argv) - len(rest)]))
     cfg.prompt = get_prompt(rest, cfg.file, stdin)
     return cfg
 
 
-def init_registry(cfg: Config) -> Registry:
-    """main.go:395-438: every model in --models plus the judge must resolve before any query."""
+def init_registry(cfg: Config, concurrency: int = 1) -> Registry:
+    """main.go:395-438: every model in --models plus the judge must resolve before any query.
+    ``concurrency``: consensus requests the local engines are sized for (the server)."""
     needed: List[str] = []
     for m in cfg.models + [cfg.judge]:
         if m not in needed:
@@ -213,7 +219,7 @@ def init_registry(cfg: Config) -> Registry:
 
             pins = parse_pins(cfg.placement) if cfg.placement else None
             backend = LocalBackend(local_specs, judge=cfg.judge, gpus=gpus, trace=cfg.trace, counts=counts,
-                                   pins=pins, judge_tp=cfg.judge_tp)
+                                   pins=pins, judge_tp=cfg.judge_tp, concurrency=concurrency)
         except Exception as e:  # noqa: BLE001
             raise CLIError(f"initializing provider for {local_specs[0].name}: {e}") from None
         for spec in local_specs:
@@ -237,6 +243,10 @@ def run(argv: List[str], stdout: TextIO = sys.stdout, stderr: TextIO = sys.stder
     show_ui = ui.is_terminal(stderr) and not cfg.quiet and not cfg.json
     start = time.monotonic()
 
+    if cfg.server:
+        out = _run_remote(cfg, ctx, show_ui, stderr)
+        _write_outputs(cfg, out, show_ui, start, stdout, stderr, None)
+        return
     registry = init_registry(cfg)
     try:
         _run_with_registry(cfg, registry, ctx, show_ui, start, stdout, stderr)
@@ -319,7 +329,13 @@ def _run_with_registry(cfg: Config, registry: Registry, ctx: Context, show_ui: b
 
     out = Result(prompt=cfg.prompt, responses=result.responses, consensus=consensus, judge=cfg.judge,
                  warnings=result.warnings, failed_models=result.failed_models)
+    _write_outputs(cfg, out, show_ui, start, stdout, stderr, registry)
 
+
+def _write_outputs(cfg: Config, out: Result, show_ui: bool, start: float, stdout: TextIO, stderr: TextIO,
+                   registry: Optional[Registry]) -> None:
+    """Persistence + output routing (main.go:186-273)."""
+    consensus = out.consensus
     output_path = ""
     run_dir = ""
     if cfg.output:
@@ -337,7 +353,7 @@ def _run_with_registry(cfg: Config, registry: Registry, ctx: Context, show_ui: b
             except OSError as e:
                 if show_ui:
                     ui.print_error(stderr, f"Failed to save {label}: {_go_path_err('open', os.path.join(run_dir, fname), e)}")
-        if cfg.trace:
+        if cfg.trace and registry is not None:
             from .utils import trace
 
             seen = set()
@@ -363,17 +379,128 @@ def _run_with_registry(cfg: Config, registry: Registry, ctx: Context, show_ui: b
         _emit(stdout, text)
     elif show_ui:
         ui._write(stderr, "\n")
-        for r in result.responses:
+        for r in out.responses:
             ui.print_model_response(stderr, r.model, r.provider, r.content, r.latency_s)
         ui.print_consensus(stderr, consensus)
-        ui.print_summary(stderr, len(cfg.models), len(result.responses), len(result.failed_models or []),
+        ui.print_summary(stderr, len(cfg.models), len(out.responses), len(out.failed_models or []),
                          time.monotonic() - start)
-        if result.warnings:
+        if out.warnings:
             ui._write(stderr, "\n")
-            for w in result.warnings:
+            for w in out.warnings:
                 ui.print_error(stderr, w)
     else:
         _emit(stdout, text)
+
+
+def _run_remote(cfg: Config, ctx: Context, show_ui: bool, stderr: TextIO) -> Result:
+    """Run the consensus on a warm ``llm-consensus`` server (``server.py``): same phases, UI and
+    errors as a local run; the server streams progress as server-sent events."""
+    import http.client
+    import json
+    import urllib.parse
+
+    from .provider.base import Response
+
+    u = urllib.parse.urlsplit(cfg.server if "://" in cfg.server else "http://" + cfg.server)
+    body = {"prompt": cfg.prompt, "models": cfg.models, "timeout": cfg.timeout, "stream": True,
+            "max_tokens": cfg.max_tokens or None, "temperature": cfg.temperature, "top_p": cfg.top_p,
+            "top_k": cfg.top_k or None, "seed": cfg.seed or None}
+    if cfg.judge_explicit:
+        body["judge"] = cfg.judge
+    conn_cls = http.client.HTTPSConnection if u.scheme == "https" else http.client.HTTPConnection
+    try:
+        conn = conn_cls(u.hostname or "127.0.0.1", u.port, timeout=None)
+        conn.request("POST", (u.path.rstrip("/") or "") + "/v1/consensus", body=json.dumps(body).encode(),
+                     headers={"Content-Type": "application/json"})
+        resp = conn.getresponse()
+    except OSError as e:
+        raise CLIError(f"connecting to server {cfg.server}: {e}") from None
+    if resp.status != 200:
+        data = resp.read()
+        try:
+            msg = json.loads(data)["error"]
+        except (ValueError, KeyError, TypeError):
+            msg = f"server returned {resp.status}: {data[:200]!r}"
+        raise CLIError(msg)
+
+    if show_ui:
+        ui.print_header(stderr, cfg.prompt)
+        ui.print_phase(stderr, "Querying models...")
+        ui._write(stderr, "\n")
+    progress = ui.Progress(stderr, cfg.models, not show_ui)
+    progress.start()
+    jprog = None
+    judge_name = cfg.judge
+    result_text = None
+    error = None
+    try:
+        name, data = "", []
+        while True:
+            if ctx.done():
+                raise CLIError(f"running queries: {ctx.err()}")
+            line = resp.readline()
+            if not line:
+                break
+            line = line.decode("utf-8", "surrogateescape").rstrip("\r\n")
+            if line.startswith("event: "):
+                name = line[7:]
+                continue
+            if line.startswith("data: "):
+                data.append(line[6:])
+                continue
+            if line or not name:
+                continue
+            payload = "\n".join(data)
+            ev, name, data = name, "", []
+            if ev == "result":
+                result_text = payload
+                continue
+            d = json.loads(payload)
+            if ev == "model_start":
+                progress.model_started(d["model"])
+            elif ev == "chunk":
+                progress.model_streaming(d["model"], d["text"])
+            elif ev == "tokens":
+                progress.model_tokens(d["model"], d["n"])
+            elif ev == "model_done":
+                progress.model_completed(d["model"])
+            elif ev == "model_error":
+                progress.model_failed(d["model"], Exception(d["error"]))
+            elif ev == "judge_start":
+                progress.stop()
+                judge_name = d["judge"]
+                if show_ui:
+                    ui.print_success(stderr, f"Received responses from {d['responses']} models")
+                    ui._write(stderr, "\n")
+                    ui.print_phase(stderr, "Synthesizing consensus...")
+                    ui._write(stderr, "\n")
+                jprog = ui.Progress(stderr, [judge_name], not show_ui)
+                jprog.start()
+                jprog.model_started(judge_name)
+            elif ev == "judge_chunk" and jprog is not None:
+                jprog.model_streaming(judge_name, d["text"])
+            elif ev == "error":
+                error = d["error"]
+    except (OSError, ValueError, KeyError, http.client.HTTPException) as e:
+        error = f"reading server stream: {e}"
+    finally:
+        progress.stop()
+        if jprog is not None:
+            jprog.model_completed(judge_name)
+            jprog.stop()
+        conn.close()
+    if error is not None:
+        raise CLIError(error)
+    if result_text is None:
+        raise CLIError(f"server {cfg.server} closed the stream without a result")
+    if show_ui:
+        ui.print_success(stderr, "Consensus reached!")
+    r = json.loads(result_text)
+    return Result(prompt=r["prompt"],
+                  responses=[Response(model=x["model"], content=x["content"], provider=x["provider"],
+                                      latency_ns=int(x["latency_ms"]) * 1_000_000) for x in r["responses"] or []],
+                  consensus=r["consensus"], judge=r["judge"], warnings=r.get("warnings"),
+                  failed_models=r.get("failed_models"))
 
 
 def _write_file(path: str, data: bytes) -> None:

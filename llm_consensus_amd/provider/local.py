@@ -95,7 +95,10 @@ class LocalBackend:
     def __init__(self, specs: List[ModelSpec], judge: Optional[str] = None, gpus: Optional[List[int]] = None,
                  trace: bool = False, counts: Optional[Dict[str, int]] = None,
                  max_context: Optional[Dict[str, int]] = None, start_timeout: float = 1800.0,
-                 pins: Optional[Dict[str, List[int]]] = None, judge_tp: int = 0):
+                 pins: Optional[Dict[str, List[int]]] = None, judge_tp: int = 0, concurrency: int = 1):
+        """``concurrency``: consensus requests served at once (the server): each engine gets decode
+        rows for that many requests (replica batching, up to 4 rows) and KV for their sequences
+        plus one judge session per request."""
         import multiprocessing as mp
 
         self.specs = {s.name: s for s in specs}
@@ -154,11 +157,15 @@ class LocalBackend:
             for m, gs in self.placement.gpus.items():
                 if g in gs:
                     s = self.specs[m]
-                    n = (counts or {}).get(m, 1)
+                    conc = max(1, concurrency)
+                    # responder rows: one per --models entry per request in flight; a judge-only
+                    # engine needs a session per request (and a row for plain queries)
+                    n = (counts or {}).get(m, 0 if m == judge else 1) * conc
+                    sess = conc if m == judge else 0
                     models.append({"name": m, "family": s.family, "seed": s.seed, "max_context": self._ctx[m],
                                    "checkpoint": s.config.checkpoint,
-                                   "max_batch": max(1, min(4, n)),
-                                   "max_seqs": max(1, n) + (1 if m == judge else 0)})
+                                   "max_batch": max(1, min(4, max(n, sess))),
+                                   "max_seqs": max(1, n) + sess})
             if groups:
                 dist_info = {"port": port, "rank": rank_of[g], "world": len(used),
                              "groups": [(m, [rank_of[x] for x in gs]) for m, gs in groups]}
@@ -256,7 +263,7 @@ class LocalProvider:
         self.spec = backend.specs[model]
         self.tok = tokenizer_for(self.spec.config)
         self._sess_lock = threading.Lock()
-        self._session: Optional[dict] = None
+        self._session: Optional["JudgeSession"] = None
 
     # -- helpers ------------------------------------------------------------------------------------
     def _params(self, req: Request, prompt_len: int) -> dict:
@@ -326,49 +333,92 @@ class LocalProvider:
             return self._stream(ctx, rid, q, callback, t0, len(ids))
 
     # -- judge sessions (incremental prefill) ---------------------------------------------------------
+    def new_session(self, header: str) -> "JudgeSession":
+        """A judge KV session of its own (the server runs one per concurrent request)."""
+        return JudgeSession(self, header)
+
     def open_session(self, header: str) -> None:
+        """The provider's default session (one consensus run at a time: the CLI)."""
         with self._sess_lock:
             self.close_session()
-            sid = next(self.backend._ids)
-            ids = self.tok.prompt_prefix_ids(header)
-            self._session = {"sid": sid, "text": header, "ids": list(ids)}
-            self.backend.broadcast(self.model, ("sess_open", sid, self.model, ids))
+            self._session = JudgeSession(self, header)
 
     def extend_session(self, text: str) -> None:
-        with self._sess_lock:
-            s = self._session
-            if s is None:
-                return
-            ids = self.tok.encode(text)
-            s["text"] += text
-            s["ids"].extend(ids)
-            self.backend.broadcast(self.model, ("sess_extend", s["sid"], ids))
+        s = self._session
+        if s is not None:
+            s.extend(text)
 
     def close_session(self) -> None:
         s = self._session
         self._session = None
         if s is not None:
-            try:
-                self.backend.broadcast(self.model, ("sess_close", s["sid"]))
-            except Exception:  # noqa: BLE001
-                pass
+            s.close()
 
     def query_stream_session(self, ctx: Context, req: Request, callback: Optional[StreamCallback]) -> Response:
-        """Finish the session whose prefilled text is a prefix of ``req.prompt``.
+        with self._sess_lock:
+            s = self._session
+            self._session = None
+        if s is None:
+            return self.query_stream(ctx, req, callback)
+        return s.finish(ctx, req, callback)
+
+    def close(self) -> None:
+        self.close_session()
+        self.backend.close()
+
+
+class JudgeSession:
+    """A judge prompt being prefilled incrementally on the judge engine: the
+    header at open, each response block as it completes (``extend``), then ``finish`` prefills
+    what is left and decodes. Sessions are independent (own engine sequence), so concurrent
+    consensus requests each keep their own."""
+
+    def __init__(self, provider: LocalProvider, header: str):
+        self.provider = provider
+        self._lock = threading.Lock()
+        self.sid = next(provider.backend._ids)
+        ids = provider.tok.prompt_prefix_ids(header)
+        self.text = header
+        self.ids = list(ids)
+        self.open = True
+        provider.backend.broadcast(provider.model, ("sess_open", self.sid, provider.model, ids))
+
+    def extend(self, text: str) -> None:
+        with self._lock:
+            if not self.open:
+                return
+            ids = self.provider.tok.encode(text)
+            self.text += text
+            self.ids.extend(ids)
+            self.provider.backend.broadcast(self.provider.model, ("sess_extend", self.sid, ids))
+
+    def close(self) -> None:
+        with self._lock:
+            if not self.open:
+                return
+            self.open = False
+        try:
+            self.provider.backend.broadcast(self.provider.model, ("sess_close", self.sid))
+        except Exception:  # noqa: BLE001
+            pass
+
+    def finish(self, ctx: Context, req: Request, callback: Optional[StreamCallback]) -> Response:
+        """Decode the judge answer for ``req.prompt``, whose prefix this session holds.
 
         The prompt is tokenized whole (exactly as ``query_stream`` would) and matched against the
         ids already prefilled: only the unmatched tail is prefilled, after truncating the session
         to the common prefix (tokenizers that are not segment-stable, chat templates)."""
-        with self._sess_lock:
-            s = self._session
-            self._session = None
-        if s is None or not req.prompt.startswith(s["text"]):
-            if s is not None:
-                self.backend.broadcast(self.model, ("sess_close", s["sid"]))
-            return self.query_stream(ctx, req, callback)
+        p = self.provider
+        with self._lock:
+            live = self.open
+            self.open = False
+        if not live or not req.prompt.startswith(self.text):
+            if live:
+                p.backend.broadcast(p.model, ("sess_close", self.sid))
+            return p.query_stream(ctx, req, callback)
         t0 = time.monotonic_ns()
-        full = self.tok.encode_prompt(req.prompt)
-        done = s["ids"]
+        full = p.tok.encode_prompt(req.prompt)
+        done = self.ids
         cp = 0
         n = min(len(done), len(full))
         while cp < n and done[cp] == full[cp]:
@@ -376,13 +426,9 @@ class LocalProvider:
         if cp == len(full):  # keep at least one token to prefill (its logits start the decode)
             cp -= 1
         rest = full[cp:]
-        params = self._params(req, len(full))
-        rid, q = self.backend._new_request(self.model)
-        with tracing.span("judge_session_finish", cat="driver", model=self.model, rest_tokens=len(rest),
+        params = p._params(req, len(full))
+        rid, q = p.backend._new_request(p.model)
+        with tracing.span("judge_session_finish", cat="driver", model=p.model, rest_tokens=len(rest),
                           reused_tokens=cp):
-            self.backend.broadcast(self.model, ("sess_generate", s["sid"], rid, rest, params, cp))
-            return self._stream(ctx, rid, q, callback, t0, len(full))
-
-    def close(self) -> None:
-        self.close_session()
-        self.backend.close()
+            p.backend.broadcast(p.model, ("sess_generate", self.sid, rid, rest, params, cp))
+            return p._stream(ctx, rid, q, callback, t0, len(full))

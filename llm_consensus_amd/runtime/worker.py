@@ -47,6 +47,10 @@ class InjectedFault(RuntimeError):
     pass
 
 
+_EMPTY = object()
+BATCH_WINDOW_S = float(os.environ.get("LLMC_BATCH_WINDOW_MS", "5")) / 1000.0
+
+
 class _Req:
     __slots__ = ("rid", "ids", "params", "ctx")
 
@@ -55,14 +59,16 @@ class _Req:
 
 
 class _EngineHost:
-    def __init__(self, name: str, engine, send, leader: bool, fault: Optional[tuple] = None):
+    def __init__(self, name: str, engine, send, leader: bool, fault: Optional[tuple] = None, on_finished=None):
         self.name = name
+        self.on_finished = on_finished  # rid -> None: the worker drops the request's context
         self.fault = fault
         self.engine = engine
         self.send = send
         self.leader = leader
         self.q: "queue.Queue" = queue.Queue()
         self.sessions: Dict[int, object] = {}
+        self._stash = _EMPTY  # an item taken off the queue while batching, processed next
         self.t = threading.Thread(target=self._loop, daemon=True, name=f"engine:{name}")
         self.t.start()
 
@@ -74,23 +80,15 @@ class _EngineHost:
         from ..engine import SamplingParams
 
         while True:
-            item = self.q.get()
+            item, self._stash = (self._stash, _EMPTY) if self._stash is not _EMPTY else (self.q.get(), _EMPTY)
             if item is None:
                 return
             kind = item[0]
             try:
                 if kind == "gen":
-                    batch = [item[1]]
-                    # replica batching: drain queued generate requests for this engine
-                    while len(batch) < self.engine.ecfg.max_batch:
-                        try:
-                            nxt = self.q.get_nowait()
-                        except queue.Empty:
-                            break
-                        if nxt is None or nxt[0] != "gen":
-                            self.q.put(nxt)  # keep ordering for non-generate work
-                            break
-                        batch.append(nxt[1])
+                    # replica batching: gather the generate requests for this engine that arrive
+                    # within the batching window (concurrent requests are issued within ~1 ms)
+                    batch = [r[1] for r in self._gather(item, "gen")]
                     self._generate(batch, SamplingParams)
                 elif kind == "sess_open":
                     _, sid, ids = item
@@ -104,31 +102,59 @@ class _EngineHost:
                     if seq is not None and ids:
                         self.engine.prefill([seq], [ids], want_logits=False)
                 elif kind == "sess_generate":
-                    _, sid, req, keep = item
-                    seq = self.sessions.pop(sid, None)
-                    if seq is None:
-                        raise RuntimeError(f"unknown judge session {sid}")
-                    if keep < seq.length:  # drop the prefilled tail that the full tokenization differs on
-                        self.engine.truncate(seq, keep)
+                    # concurrent judge sessions (server) finishing together decode as one batch
+                    items = self._gather(item, "sess_generate")
+                    batch = [it[2] for it in items]
+                    seqs = []
                     try:
-                        self._run([seq], [req], [req.ids], SamplingParams)
+                        for _, sid, req, keep in items:
+                            seq = self.sessions.pop(sid, None)
+                            if seq is None:
+                                raise RuntimeError(f"unknown judge session {sid}")
+                            seqs.append(seq)
+                            if keep < seq.length:  # drop the prefilled tail the full tokenization differs on
+                                self.engine.truncate(seq, keep)
+                        self._run(seqs, batch, [r.ids for r in batch], SamplingParams)
                     finally:
-                        self.engine.free_sequence(seq)
+                        for seq in seqs:
+                            self.engine.free_sequence(seq)
                 elif kind == "sess_close":
                     seq = self.sessions.pop(item[1], None)
                     if seq is not None:
                         self.engine.free_sequence(seq)
             except Exception as e:  # noqa: BLE001 - engine-level failure = that request's error
                 rids = []
-                if kind == "gen":
+                if kind in ("gen", "sess_generate"):
                     rids = [r.rid for r in batch]
-                elif kind == "sess_generate":
-                    rids = [item[2].rid]
                 msg = f"{type(e).__name__}: {e}"
                 if os.environ.get("LLMC_DEBUG"):
                     msg += "\n" + traceback.format_exc()
                 for rid in rids:
                     self._emit("error", rid, msg)
+            finally:
+                if self.on_finished is not None and kind in ("gen", "sess_generate"):
+                    for r in batch:
+                        self.on_finished(r.rid)
+
+    def _gather(self, first, kind: str) -> list:
+        """``first`` plus the queued items of the same kind, up to the engine's decode rows; waits
+        up to the batching window (LLMC_BATCH_WINDOW_MS, default 5 ms, engines with > 1 row only)
+        for items still arriving. A different kind ends the batch and is processed next."""
+        items = [first]
+        cap = self.engine.ecfg.max_batch
+        if cap <= 1:
+            return items
+        deadline = time.monotonic() + BATCH_WINDOW_S
+        while len(items) < cap:
+            try:
+                nxt = self.q.get(timeout=max(0.0, deadline - time.monotonic()))
+            except queue.Empty:
+                break
+            if nxt is None or nxt[0] != kind:
+                self._stash = nxt  # next in line: keeps the queue's order
+                break
+            items.append(nxt)
+        return items
 
     def _generate(self, batch: List[_Req], SP) -> None:
         seqs = [self.engine.new_sequence() for _ in batch]
@@ -231,6 +257,7 @@ def worker_main(gpu: int, conn, models: List[dict], dist_info: Optional[dict], t
                 if dist_info["rank"] in ranks:
                     groups[gname] = (g, ranks.index(dist_info["rank"]), len(ranks))
         hosts: Dict[str, _EngineHost] = {}
+        ctxs: Dict[int, Context] = {}  # live requests' contexts (cancel); dropped when they finish
         faults = parse_faults(os.environ.get("LLMC_FAULT", ""))
         for m in models:
             cfg = FAMILIES.get(m["family"])
@@ -254,7 +281,8 @@ def worker_main(gpu: int, conn, models: List[dict], dist_info: Optional[dict], t
                                 # MoE under TP: whole experts per rank (LLMC_EXPERT_PARALLEL=1)
                                 expert_parallel=os.environ.get("LLMC_EXPERT_PARALLEL", "0") == "1")
             eng = Engine(cfg, ecfg, tp=tp, name=m["name"])
-            hosts[m["name"]] = _EngineHost(m["name"], eng, send, tp.is_leader, faults.get(m["name"]))
+            hosts[m["name"]] = _EngineHost(m["name"], eng, send, tp.is_leader, faults.get(m["name"]),
+                                           on_finished=lambda rid: ctxs.pop(rid, None))
         if not on_cpu:
             # capture all decode graphs now, while nothing else runs in this process
             for h in hosts.values():
@@ -266,7 +294,6 @@ def worker_main(gpu: int, conn, models: List[dict], dist_info: Optional[dict], t
         send(("fatal", f"worker gpu{gpu} init failed: {type(e).__name__}: {e}\n{traceback.format_exc()}"))
         return
 
-    ctxs: Dict[int, Context] = {}
     sess_host: Dict[int, _EngineHost] = {}
     while True:
         try:

@@ -36,6 +36,7 @@ setup(
                     "remote": ["httpx"]},
     entry_points={"console_scripts": [
         "llm-consensus = llm_consensus_amd.cli:main",
+        "llm-consensus-server = llm_consensus_amd.server:main",
         "model-registry-sync = llm_consensus_amd.registry_sync:main",
     ]},
     distclass=_BinaryDistribution,

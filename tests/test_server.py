@@ -1,0 +1,192 @@
+"""Consensus server (``server.py``): HTTP/SSE API over warm engines, concurrent requests, and the
+CLI's ``--server`` client mode. Stub models cover the protocol; CPU workers (LLMC_DEVICE=cpu,
+oracle op path) cover concurrent local engines with per-request judge sessions and batched decode."""
+
+import json
+import os
+import subprocess
+import sys
+import threading
+import urllib.error
+import urllib.request
+
+import pytest
+
+from llm_consensus_amd.server import ConsensusServer, ConsensusService
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+@pytest.fixture
+def stub_server():
+    svc = ConsensusService(["stub-a", "stub-b", "stub-fail", "stub-echo"], "stub-j", concurrency=3)
+    srv = ConsensusServer(("127.0.0.1", 0), svc)
+    t = threading.Thread(target=srv.serve_forever, kwargs={"poll_interval": 0.05}, daemon=True)
+    t.start()
+    yield f"http://127.0.0.1:{srv.server_address[1]}", svc
+    srv.shutdown()
+    srv.server_close()
+    svc.close()
+
+
+def post(url, body, raw=False):
+    req = urllib.request.Request(url + "/v1/consensus", data=json.dumps(body).encode(),
+                                 headers={"Content-Type": "application/json"})
+    try:
+        with urllib.request.urlopen(req, timeout=120) as r:
+            data = r.read().decode()
+            return r.status, (data if raw else json.loads(data))
+    except urllib.error.HTTPError as e:
+        return e.code, json.loads(e.read().decode())
+
+
+def sse_events(text):
+    out = []
+    for block in text.split("\n\n"):
+        if not block.strip():
+            continue
+        name, data = "", []
+        for ln in block.split("\n"):
+            if ln.startswith("event: "):
+                name = ln[7:]
+            elif ln.startswith("data: "):
+                data.append(ln[6:])
+        out.append((name, "\n".join(data)))
+    return out
+
+
+def test_server_roundtrip_go_json(stub_server):
+    url, _ = stub_server
+    code, text = post(url, {"prompt": "What is 2+2?", "models": ["stub-a", "stub-b"]}, raw=True)
+    assert code == 200
+    assert text.endswith("}\n") and text.startswith('{\n  "prompt": "What is 2+2?",\n  "responses": [')
+    d = json.loads(text)
+    assert list(d) == ["prompt", "responses", "consensus", "judge"]  # omitempty warnings/failed_models
+    assert sorted(r["model"] for r in d["responses"]) == ["stub-a", "stub-b"]
+    assert all(list(r) == ["model", "content", "provider", "latency_ms"] for r in d["responses"])
+    assert d["judge"] == "stub-j" and d["consensus"]
+
+
+def test_server_stream_events(stub_server):
+    url, _ = stub_server
+    code, text = post(url, {"prompt": "hi", "models": ["stub-a", "stub-fail", "stub-b"], "stream": True}, raw=True)
+    assert code == 200
+    evs = sse_events(text)
+    names = [n for n, _ in evs]
+    assert names.count("model_start") == 3 and names.count("model_done") == 2 and names.count("model_error") == 1
+    assert names.index("judge_start") > max(i for i, n in enumerate(names) if n in ("model_done", "model_error"))
+    assert "judge_chunk" in names and names[-1] == "result"
+    res = json.loads(evs[-1][1])
+    assert res["failed_models"] == ["stub-fail"] and res["warnings"] == ["stub-fail: stub: scripted failure"]
+    err = [json.loads(d) for n, d in evs if n == "model_error"][0]
+    assert err == {"model": "stub-fail", "error": "stub: scripted failure"}
+
+
+def test_server_passthrough_and_failures(stub_server):
+    url, _ = stub_server
+    code, d = post(url, {"prompt": "echo me", "models": ["stub-echo"]})
+    assert code == 200 and d["consensus"] == d["responses"][0]["content"]  # judge.go:74-79
+    code, d = post(url, {"prompt": "x", "models": ["stub-fail"]})
+    assert code == 502 and d["error"] == "running queries: all models failed: [stub-fail: stub: scripted failure]"
+
+
+def test_server_bad_requests(stub_server):
+    url, svc = stub_server
+    code, d = post(url, {"prompt": "x", "models": ["stub-a", "nope"]})
+    assert code == 400 and 'unknown model "nope"' in d["error"] and d["error"].startswith("initializing provider for nope")
+    assert post(url, {"models": ["stub-a"]})[0] == 400
+    assert post(url, {"prompt": "x", "max_tokens": "many"})[0] == 400
+    assert post(url, {"prompt": "x", "max_tokens": 2.5})[0] == 400
+    with urllib.request.urlopen(url + "/healthz", timeout=30) as r:
+        h = json.loads(r.read())
+    assert h["status"] == "ok" and h["judge"] == "stub-j" and "stub-a" in h["models"]
+    with urllib.request.urlopen(url + "/v1/models", timeout=30) as r:
+        ms = json.loads(r.read())["models"]
+    assert {"id": "stub-j", "provider": "stub", "role": "judge"} in ms
+    with pytest.raises(urllib.error.HTTPError) as ei:
+        urllib.request.urlopen(url + "/nope", timeout=30)
+    assert ei.value.code == 404
+
+
+def test_server_concurrent_requests(stub_server):
+    url, svc = stub_server
+    out = [None] * 8
+
+    def one(i):
+        out[i] = post(url, {"prompt": f"q{i % 2}", "models": ["stub-a", "stub-b"]})
+
+    ts = [threading.Thread(target=one, args=(i,)) for i in range(8)]
+    for t in ts:
+        t.start()
+    for t in ts:
+        t.join()
+    assert all(c == 200 for c, _ in out)
+    # deterministic stubs: the same prompt gives the same answers whatever the interleaving
+    by_prompt = {}
+    for _, d in out:
+        key = d["prompt"]
+        val = (sorted((r["model"], r["content"]) for r in d["responses"]))
+        assert by_prompt.setdefault(key, val) == val
+    assert svc.stats["requests"] >= 8 and svc.stats["in_flight"] == 0
+
+
+def run_cli(args, env=None):
+    e = dict(os.environ)
+    e.update(env or {})
+    r = subprocess.run([sys.executable, "-m", "llm_consensus_amd", *args], capture_output=True, cwd=ROOT, env=e,
+                       timeout=300, stdin=subprocess.DEVNULL)
+    return r.returncode, r.stdout.decode(), r.stderr.decode()
+
+
+def test_cli_server_mode_matches_local_run(stub_server, tmp_path):
+    url, _ = stub_server
+    rc, out, err = run_cli(["--server", url, "--models", "stub-a,stub-b", "--judge", "stub-j", "--json", "2+2?"])
+    assert rc == 0, err
+    remote = json.loads(out)
+    rc, out, err = run_cli(["--models", "stub-a,stub-b", "--judge", "stub-j", "--json", "2+2?"])
+    assert rc == 0, err
+    local = json.loads(out)
+    key = lambda d: sorted((r["model"], r["content"], r["provider"]) for r in d["responses"])  # noqa: E731
+    assert key(remote) == key(local) and remote["judge"] == local["judge"] == "stub-j"
+    # auto-save layout through the server (data/<run-id>/{result.json,prompt.txt,consensus.md})
+    rc, out, err = run_cli(["--server", url, "--models", "stub-a,stub-b", "--data-dir", str(tmp_path), "hello"],
+                           env={"LLMC_SERVER": ""})
+    assert rc == 0 and out == "", err
+    (run,) = list(tmp_path.iterdir())
+    assert sorted(p.name for p in run.iterdir()) == ["consensus.md", "prompt.txt", "result.json"]
+    assert (run / "prompt.txt").read_text() == "hello"
+    # errors keep the reference's strings and exit code
+    rc, out, err = run_cli(["--server", url, "--models", "stub-a,zzz", "--json", "x"])
+    assert rc == 1 and err.startswith("error: initializing provider for zzz: unknown model")
+    rc, out, err = run_cli(["--server", "http://127.0.0.1:9", "--models", "stub-a", "--json", "x"])
+    assert rc == 1 and "connecting to server" in err
+
+
+def test_server_local_engines_concurrent_cpu(monkeypatch):
+    """Three concurrent requests on CPU-worker engines: replica-batched responder decodes and one
+    judge session per request. Greedy sampling: every request must get the same answers as a lone
+    request (batching and session isolation do not change results)."""
+    monkeypatch.setenv("LLMC_DEVICE", "cpu")
+    svc = ConsensusService(["llama-tiny@1", "llama-tiny@2"], "llama-tiny@j", concurrency=3, max_tokens=6,
+                           temperature=0.0)
+    try:
+        ctx_req = {"prompt": "Compare two sorting algorithms.", "max_tokens": 6, "temperature": 0.0}
+        from llm_consensus_amd.context import Context
+
+        lone = svc.run(Context.background(), svc.parse(dict(ctx_req)))
+        outs = [None] * 3
+
+        def one(i):
+            outs[i] = svc.run(Context.background(), svc.parse(dict(ctx_req)))
+
+        ts = [threading.Thread(target=one, args=(i,)) for i in range(3)]
+        for t in ts:
+            t.start()
+        for t in ts:
+            t.join()
+        ref = sorted((r.model, r.content) for r in lone.responses)
+        for o in outs:
+            assert o is not None and sorted((r.model, r.content) for r in o.responses) == ref
+            assert o.consensus == lone.consensus and o.consensus
+    finally:
+        svc.close()

@@ -69,7 +69,12 @@ class _EngineHost:
         self.q: "queue.Queue" = queue.Queue()
         self.sessions: Dict[int, object] = {}
         self._stash = _EMPTY  # an item taken off the queue while batching, processed next
-        self.t = threading.Thread(target=self._loop, daemon=True, name=f"engine:{name}")
+        # continuous batching (rows join/leave between graph replays) for single-GPU engines sized
+        # for several requests (the server, duplicate --models entries); LLMC_CONTINUOUS=0 = off
+        cont = (engine.ecfg.max_batch > 1 and engine.tp.size == 1
+                and os.environ.get("LLMC_CONTINUOUS", "1") != "0")
+        self.t = threading.Thread(target=self._loop_continuous if cont else self._loop, daemon=True,
+                                  name=f"engine:{name}")
         self.t.start()
 
     def _emit(self, *msg) -> None:
@@ -155,6 +160,145 @@ class _EngineHost:
                 break
             items.append(nxt)
         return items
+
+    # -- continuous batching -------------------------------------------------------------------
+    def _loop_continuous(self) -> None:
+        """Commands are taken between replays: generate requests and judge-session finishes wait
+        in ``waiting`` and are prefilled + admitted into free decode rows as rows retire; session
+        open/extend/close prefill at once (they are short and order-sensitive)."""
+        from collections import deque
+
+        from ..engine import SamplingParams
+        from ..engine.batcher import ContinuousBatcher
+
+        stage, k = self.fault or ("", 0)
+        sent: Dict[int, int] = {}
+
+        def on_tokens(row, ids):
+            req = row.tag[0]
+            if not row.tag[2]:
+                row.tag[2] = time.monotonic_ns() - row.tag[1]
+            if stage == "decode" and sent.get(req.rid, 0) + len(ids) >= k:
+                raise InjectedFault(f"injected fault: {self.name} decode after {k} tokens")
+            sent[req.rid] = sent.get(req.rid, 0) + len(ids)
+            self._emit("tokens", req.rid, ids)
+
+        bat = ContinuousBatcher(self.engine, on_tokens)
+        waiting: "deque" = deque()
+        stop = False
+
+        def fail(req, e) -> None:
+            msg = f"{type(e).__name__}: {e}"
+            if os.environ.get("LLMC_DEBUG"):
+                msg += "\n" + traceback.format_exc()
+            self._emit("error", req.rid, msg)
+            if self.on_finished is not None:
+                self.on_finished(req.rid)
+
+        while not stop or bat.rows:
+            # 1. commands: block only when there is nothing to decode
+            items = []
+            if not bat.rows and not waiting and not stop:
+                if self._stash is not _EMPTY:
+                    items.append(self._stash)
+                    self._stash = _EMPTY
+                else:
+                    items.append(self.q.get())
+                if items[0] is not None and items[0][0] in ("gen", "sess_generate") and self.engine.ecfg.max_batch > 1:
+                    # a burst of concurrent requests: let the rest arrive before the first prefill
+                    time.sleep(BATCH_WINDOW_S)
+            while True:
+                try:
+                    items.append(self.q.get_nowait())
+                except queue.Empty:
+                    break
+            for item in items:
+                if item is None:
+                    stop = True
+                    continue
+                kind = item[0]
+                try:
+                    if kind == "gen":
+                        waiting.append(("gen", item[1], None, 0))
+                    elif kind == "sess_generate":
+                        _, sid, req, keep = item
+                        seq = self.sessions.pop(sid, None)
+                        if seq is None:
+                            fail(req, RuntimeError(f"unknown judge session {sid}"))
+                        else:
+                            waiting.append(("sess", req, seq, keep))
+                    elif kind == "sess_open":
+                        _, sid, ids = item
+                        seq = self.engine.new_sequence()
+                        self.sessions[sid] = seq
+                        if ids:
+                            self.engine.prefill([seq], [ids], want_logits=False)
+                    elif kind == "sess_extend":
+                        _, sid, ids = item
+                        seq = self.sessions.get(sid)
+                        if seq is not None and ids:
+                            self.engine.prefill([seq], [ids], want_logits=False)
+                    elif kind == "sess_close":
+                        seq = self.sessions.pop(item[1], None)
+                        if seq is not None:
+                            self.engine.free_sequence(seq)
+                except Exception:  # noqa: BLE001 - a session command failed: drop the session, so its
+                    if os.environ.get("LLMC_DEBUG"):  # finish reports "unknown judge session"
+                        traceback.print_exc()
+                    if kind in ("sess_open", "sess_extend"):
+                        seq = self.sessions.pop(item[1], None)
+                        if seq is not None:
+                            self.engine.free_sequence(seq)
+            # 2. admit waiting requests into free rows (prefilled together)
+            if waiting and bat.free_rows and not stop:
+                take = [waiting.popleft() for _ in range(min(bat.free_rows, len(waiting)))]
+                t0 = time.monotonic_ns()
+                seqs, ids_list, reqs = [], [], []
+                for kind, req, seq, keep in take:
+                    if kind == "gen":
+                        seq = self.engine.new_sequence()
+                    elif keep < seq.length:  # drop the prefilled tail the full tokenization differs on
+                        self.engine.truncate(seq, keep)
+                    seqs.append(seq)
+                    ids_list.append(req.ids)
+                    reqs.append(req)
+                try:
+                    if stage == "crash":
+                        os._exit(17)
+                    if stage in ("init", "prefill"):
+                        raise InjectedFault(f"injected fault: {self.name} {stage}")
+                    self.engine.prefill(seqs, ids_list)
+                except Exception as e:  # noqa: BLE001
+                    for seq, req in zip(seqs, reqs):
+                        self.engine.free_sequence(seq)
+                        fail(req, e)
+                    seqs = []
+                for seq, req, ids in zip(seqs, reqs, ids_list):
+                    try:
+                        bat.admit(seq, SamplingParams(**req.params), tag=[req, t0, 0, len(ids)], ctx=req.ctx)
+                    except Exception as e:  # noqa: BLE001
+                        self.engine.free_sequence(seq)
+                        fail(req, e)
+            # 3. one replay for every live row; report the rows it retired
+            if bat.rows:
+                try:
+                    gone = bat.step()
+                except Exception as e:  # noqa: BLE001 - engine failure: every live request fails
+                    gone = list(bat.rows)
+                    bat.rows = []
+                    for row in gone:
+                        row.error = row.error or e
+                for row in gone:
+                    req, t0, ttft, plen = row.tag
+                    if row.error is not None:
+                        fail(req, row.error)
+                    else:
+                        self._emit("done", req.rid, {"prompt_tokens": plen, "output_tokens": len(row.tokens),
+                                                     "ttft_ns": ttft, "latency_ns": time.monotonic_ns() - t0})
+                        if self.on_finished is not None:
+                            self.on_finished(req.rid)
+                    sent.pop(req.rid, None)
+                    self.engine.free_sequence(row.seq)
 
     def _generate(self, batch: List[_Req], SP) -> None:
         seqs = [self.engine.new_sequence() for _ in batch]

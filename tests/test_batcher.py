@@ -1,0 +1,71 @@
+"""Continuous batching (engine/batcher.py): rows join and leave between replays; every request
+must get exactly the tokens it gets when decoded alone (greedy and seeded sampling), whatever
+rows it shared the batch with and wherever compaction moved it."""
+
+import pytest
+import torch
+
+from llm_consensus_amd.engine import Engine, EngineConfig, SamplingParams
+from llm_consensus_amd.engine.batcher import ContinuousBatcher
+from llm_consensus_amd.models.config import FAMILIES
+
+
+def _engine(device, max_batch=3):
+    return Engine(FAMILIES["llama-tiny"], EngineConfig(device=device, max_context=512, max_batch=max_batch,
+                                                       max_seqs=6, seed=11))
+
+
+def _alone(eng, prompt, p):
+    s = eng.new_sequence()
+    eng.prefill([s], [prompt])
+    out = eng.decode([s], [p])[0]
+    eng.free_sequence(s)
+    return out
+
+
+def _run_schedule(eng, reqs, admit_at):
+    """reqs: [(prompt, params)]; admit_at[i] = step index at which request i is admitted."""
+    bat = ContinuousBatcher(eng)
+    done = {}
+    step, pending = 0, list(range(len(reqs)))
+    while pending or bat.rows:
+        for i in [i for i in pending if admit_at[i] <= step and bat.free_rows]:
+            s = eng.new_sequence()
+            eng.prefill([s], [reqs[i][0]])
+            bat.admit(s, reqs[i][1], tag=i)
+            pending.remove(i)
+        for row in bat.step():
+            assert row.error is None
+            done[row.tag] = row.tokens
+            eng.free_sequence(row.seq)
+        step += 1
+    return [done[i] for i in range(len(reqs))]
+
+
+def _check(device):
+    eng = _engine(device)
+    reqs = [
+        ([300 + i for i in range(40)], SamplingParams(max_tokens=40, temperature=0.0, stop_on_eos=False)),
+        ([500 + i for i in range(9)], SamplingParams(max_tokens=7, temperature=0.0, stop_on_eos=False)),
+        ([700 + 3 * i for i in range(23)], SamplingParams(max_tokens=30, temperature=1.0, seed=5, stop_on_eos=False)),
+        ([100 + i for i in range(5)], SamplingParams(max_tokens=12, temperature=0.8, top_k=20, seed=9,
+                                                     stop_on_eos=False)),
+    ]
+    free0 = eng.alloc.num_free
+    ref = [_alone(eng, p, sp) for p, sp in reqs]
+    # 0 and 1 start together; 1 retires first; 2 joins mid-flight; 0 retires -> 2 moves down; 3
+    # joins after the batch was full
+    got = _run_schedule(eng, reqs, admit_at=[0, 0, 2, 3])
+    for i, (g, r) in enumerate(zip(got, ref)):
+        assert g == r, (i, g, r)
+        assert len(g) == reqs[i][1].max_tokens
+    assert eng.alloc.num_free == free0  # every retired row's KV blocks came back
+
+
+def test_continuous_batching_cpu():
+    _check("cpu")
+
+
+@pytest.mark.gpu
+def test_continuous_batching_gpu(cuda):
+    _check("cuda:0")

@@ -190,3 +190,33 @@ def test_server_local_engines_concurrent_cpu(monkeypatch):
             assert o.consensus == lone.consensus and o.consensus
     finally:
         svc.close()
+
+
+def test_server_tp_judge_concurrent_cpu(monkeypatch):
+    """A TP=2 judge (gloo over two CPU workers, beside the responders) serving two concurrent
+    requests: each keeps its own judge session on both ranks; results equal a lone request's."""
+    monkeypatch.setenv("LLMC_DEVICE", "cpu")
+    monkeypatch.setenv("LLMC_CPU_WORKERS", "2")
+    svc = ConsensusService(["llama-tiny@1", "llama-tiny@2"], "llama-tiny@j", judge_tp=2, concurrency=2,
+                           max_tokens=5, temperature=0.0)
+    try:
+        from llm_consensus_amd.context import Context
+
+        body = {"prompt": "Name three prime numbers.", "max_tokens": 5, "temperature": 0.0}
+        lone = svc.run(Context.background(), svc.parse(dict(body)))
+        outs = [None, None]
+
+        def one(i):
+            outs[i] = svc.run(Context.background(), svc.parse(dict(body)))
+
+        ts = [threading.Thread(target=one, args=(i,)) for i in range(2)]
+        for t in ts:
+            t.start()
+        for t in ts:
+            t.join()
+        for o in outs:
+            assert o is not None and o.consensus == lone.consensus and o.consensus
+            assert sorted((r.model, r.content) for r in o.responses) == sorted((r.model, r.content)
+                                                                                for r in lone.responses)
+    finally:
+        svc.close()

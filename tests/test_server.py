@@ -220,3 +220,35 @@ def test_server_tp_judge_concurrent_cpu(monkeypatch):
                                                                                 for r in lone.responses)
     finally:
         svc.close()
+
+
+@pytest.mark.gpu
+def test_server_local_engines_concurrent_gpu(cuda):
+    """The same on the MI355X: continuous-batched responder rows (retiring at different replays)
+    and judge sessions through the HIP kernels and decode graphs. Token-exactness against a lone
+    request is not asserted here: a batched prefill of >= 64 tokens takes the hipBLASLt GEMM path
+    instead of the MFMA kernel, and with random weights greedy decoding flips on near-ties; the
+    batcher's exactness is tests/test_batcher.py (rows prefilled alone)."""
+    svc = ConsensusService(["llama-small@1", "llama-small@2"], "llama-small@j", concurrency=3, max_tokens=40,
+                           temperature=0.0)
+    try:
+        from llm_consensus_amd.context import Context
+
+        body = {"prompt": "Compare two sorting algorithms.", "temperature": 0.0}
+        outs = [None] * 3
+
+        def one(i):
+            b = dict(body, max_tokens=40 - 8 * i)  # rows retire at different replays
+            outs[i] = (b["max_tokens"], svc.run(Context.background(), svc.parse(b)))
+
+        ts = [threading.Thread(target=one, args=(i,)) for i in range(3)]
+        for t in ts:
+            t.start()
+        for t in ts:
+            t.join()
+        for mt, o in outs:
+            assert o is not None and len(o.responses) == 2 and o.consensus and o.judge == "llama-small@j"
+            assert all(r.output_tokens == mt and r.content for r in o.responses), [r.output_tokens for r in o.responses]
+        assert svc.stats["in_flight"] == 0 and svc.stats["failed"] == 0
+    finally:
+        svc.close()

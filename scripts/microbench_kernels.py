@@ -229,5 +229,7 @@ if __name__ == "__main__":
         bench_gemv_sweep([(9216, 3072), (16384, 3072), (3072, 3072), (3072, 8192)])
     if what in ("sweep-tp8",):  # one TP=8 rank of Llama-3-8B: qkv, gate_up, o, down
         bench_gemv_sweep([(768, 4096), (1536, 4096), (3584, 4096), (4096, 512), (4096, 1792)])
+    if what in ("sweep-70b-tp4",):  # one TP=4 rank of Llama-3-70B: qkv, gate_up, o, down
+        bench_gemv_sweep([(2560, 8192), (14336, 8192), (8192, 2048), (8192, 7168)])
     if what in ("prefill",):
         bench_prefill()

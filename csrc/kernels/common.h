@@ -68,6 +68,14 @@ __device__ __forceinline__ u32x4 load16(const void* p) {
   }
 }
 
+// Load of a wave-uniform address through the scalar cache (s_load_dword, counted by lgkmcnt, so
+// it does not queue behind the vector loads in flight). Read-only data only.
+template <typename T>
+__device__ __forceinline__ T ld_scalar(const T* p) {
+  static_assert(sizeof(T) == 4, "32-bit scalar loads");
+  return *reinterpret_cast<const __attribute__((address_space(4))) T*>(reinterpret_cast<uintptr_t>(p));
+}
+
 // Full-wave reductions (xor butterfly over 64 lanes).
 __device__ __forceinline__ float wave_sum(float v) {
 #pragma unroll

@@ -98,6 +98,23 @@ __global__ __launch_bounds__(NT) void gemv_kernel(const bf16_t* __restrict__ x, 
   };
   issue(cur, lane);
 
+
+  // RoPE epilogue operands (PAIR_LDS: one row per even wave) are wave-uniform, so they come
+  // through the SCALAR cache (s_load, counted by lgkmcnt): as vector loads they queued behind the
+  // weight stream in the in-order vmcnt counter, and the position -> cos/sin dependency held the
+  // second weight batch back by a memory round trip (qkv 11.2 -> ~10.3 us for Llama-3-8B
+  // without them). Position and slot are issued here, behind the first weight batch; the
+  // dependent cos/sin loads after the prologue, when the position has landed.
+  int pre_pos[M], pre_slot[M];
+  float pre_c[M], pre_s[M];
+  if constexpr (PAIR_LDS && EPI == EPI_ROPE) {
+#pragma unroll
+    for (int m = 0; m < M; ++m) {
+      pre_slot[m] = ld_scalar(rope.slots + m);
+      pre_pos[m] = ld_scalar(rope.positions + m);
+    }
+  }
+
   // ---- prologue: x -> LDS (optionally RMS-normalised) ----
   if constexpr (PRO == PRO_NORM) {
     float(*red)[WAVES] = reinterpret_cast<float(*)[WAVES]>(smem + static_cast<size_t>(M) * K * sizeof(bf16_t));
@@ -261,19 +278,20 @@ __global__ __launch_bounds__(NT) void gemv_kernel(const bf16_t* __restrict__ x, 
   }
   __syncthreads();
   if (!PAIR_LDS && row0 >= N) return;  // PAIR_LDS blocks are full (host), all waves reach its barrier
-
-  // RoPE epilogue operands (PAIR_LDS: one row per even wave) issued now, landing under the stream
-  float pre_c = 1.f, pre_s = 0.f;
-  int pre_slot = -1;
   if constexpr (PAIR_LDS && EPI == EPI_ROPE) {
-    if (!(wave & 1) && lane < M && row0 < N) {
-      const int D = rope.D, half = D / 2;
-      pre_slot = rope.slots[lane];
-      if (row0 / D < rope.nh + rope.nkv) {
-        const int i = (row0 % D) / 2;
-        const int pos = rope.positions[lane];
-        pre_c = rope.cos_t[static_cast<int64_t>(pos) * half + i];
-        pre_s = rope.sin_t[static_cast<int64_t>(pos) * half + i];
+    const int w_u = __builtin_amdgcn_readfirstlane(wave);
+    const int r_u = (blockIdx.x * WAVES + w_u) * RPW;
+    const int D = rope.D, half = D / 2;
+    const bool qk = r_u / D < rope.nh + rope.nkv;
+    const int i = (r_u % D) / 2;
+#pragma unroll
+    for (int m = 0; m < M; ++m) {
+      pre_c[m] = 1.f;
+      pre_s[m] = 0.f;
+      if (qk) {
+        const int64_t t = static_cast<int64_t>(pre_pos[m]) * half + i;
+        pre_c[m] = ld_scalar(rope.cos_t + t);
+        pre_s[m] = ld_scalar(rope.sin_t + t);
       }
     }
   }
@@ -381,7 +399,13 @@ __global__ __launch_bounds__(NT) void gemv_kernel(const bf16_t* __restrict__ x, 
     if (!(wave & 1)) {
 #pragma unroll
       for (int m = 0; m < M; ++m)
-        if (lane == m && row0 < N) pair_epi(row0, m, acc[0][m], pairx[(wave >> 1) * M + m], pre_c, pre_s, pre_slot);
+        if (lane == m && row0 < N) {
+          if constexpr (EPI == EPI_ROPE) {
+            pair_epi(row0, m, acc[0][m], pairx[(wave >> 1) * M + m], pre_c[m], pre_s[m], pre_slot[m]);
+          } else {
+            pair_epi(row0, m, acc[0][m], pairx[(wave >> 1) * M + m], 1.f, 0.f, -1);
+          }
+        }
     }
     return;
   }

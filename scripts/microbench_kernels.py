@@ -174,6 +174,40 @@ def bench_gemv_sweep(shapes=None):
         print(f"sweep N={N} K={K} ({N * K * 2 / 1e6:.0f} MB, {copies} copies): " + "  ".join(res), flush=True)
 
 
+def bench_qkv_rope():
+    """qkv GEMV with the RoPE + paged-KV-write epilogue vs the same GEMV with a plain bf16
+    epilogue (both with the fused RMSNorm prologue), cold weights: what the epilogue costs."""
+    from llm_consensus_amd.ops import oracle
+
+    for (nh, nkv, D, H) in [(32, 8, 128, 4096), (32, 32, 96, 3072), (4, 1, 128, 4096)]:
+        N = (nh + 2 * nkv) * D
+        copies = max(2, (1 << 30) // (N * H * 2))
+        Ws = [(torch.randn(N, H, device="cuda") * 0.02).to(BF) for _ in range(copies)]
+        x = torch.randn(1, H, device="cuda").to(BF)
+        nw = torch.ones(H, dtype=BF, device="cuda")
+        bs, nb = 64, 64
+        kc = torch.zeros(nb, nkv, bs, D, dtype=BF, device="cuda")
+        vc = torch.zeros_like(kc)
+        cos_t, sin_t = oracle.rope_tables([1.0 / (10000 ** (2 * i / D)) for i in range(D // 2)], 4096)
+        cos_t, sin_t = cos_t.cuda(), sin_t.cuda()
+        pos = torch.tensor([1000], dtype=torch.int32, device="cuda")
+        slots = torch.tensor([1000], dtype=torch.int32, device="cuda")
+        q = torch.zeros(1, nh * D, dtype=BF, device="cuda")
+        out = torch.zeros(1, N, dtype=BF, device="cuda")
+
+        def rope():
+            for W in Ws:
+                ops.qkv_rope(x, W, nw, 1e-5, q, kc, vc, pos, slots, cos_t, sin_t, nh, nkv, D, bs)
+
+        def plain():
+            for W in Ws:
+                ops.gemv(x, W, 0, out=out, norm_w=nw)
+        tr = timeit(rope, iters=2, warm=1) / copies
+        tp = timeit(plain, iters=2, warm=1) / copies
+        print(f"qkv nh={nh} nkv={nkv} D={D} H={H} (N={N}): rope+kv epilogue {tr:6.2f} us, plain {tp:6.2f} us",
+              flush=True)
+
+
 def bench_launch():
     x = torch.zeros(1, 4096, dtype=BF, device="cuda")
     w = torch.ones(4096, dtype=BF, device="cuda")
@@ -231,5 +265,7 @@ if __name__ == "__main__":
         bench_gemv_sweep([(768, 4096), (1536, 4096), (3584, 4096), (4096, 512), (4096, 1792)])
     if what in ("sweep-70b-tp4",):  # one TP=4 rank of Llama-3-70B: qkv, gate_up, o, down
         bench_gemv_sweep([(2560, 8192), (14336, 8192), (8192, 2048), (8192, 7168)])
+    if what in ("qkv-rope",):
+        bench_qkv_rope()
     if what in ("prefill",):
         bench_prefill()

@@ -96,7 +96,29 @@ __global__ __launch_bounds__(NT) void gemv_kernel(const bf16_t* __restrict__ x, 
       for (int r = 0; r < RPW; ++r) dst[r][u] = load16<true>(wrow[r] + c);
     }
   };
+  // x (and the norm weights) are loaded BEFORE the first weight batch: vmcnt retires loads in
+  // issue order, so the prologue's wait for x then leaves the weight batch in flight, and the main
+  // loop issues the second batch while the first is still landing (x last would make the
+  // prologue wait for the whole first batch and open a bubble in every wave's stream).
+  constexpr bool kXRegs = (PRO == PRO_NORM || PRO == PRO_NONE);
+  const bool x_fast = nchunk <= 2 * NT;  // x fits in two 16-B chunks per thread
+  u32x4 xr[2][M], gr[2];
+  if constexpr (kXRegs) {
+    if (x_fast) {
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        const int c = tid + j * NT;
+        if (c < nchunk) {
+          if constexpr (PRO == PRO_NORM) gr[j] = reinterpret_cast<const u32x4*>(norm_w)[c];
+#pragma unroll
+          for (int m = 0; m < M; ++m) xr[j][m] = reinterpret_cast<const u32x4*>(x + static_cast<int64_t>(m) * x_stride)[c];
+        }
+      }
+    }
+  }
+  __builtin_amdgcn_sched_barrier(0);
   issue(cur, lane);
+  __builtin_amdgcn_sched_barrier(0);
 
 
   // RoPE epilogue operands (PAIR_LDS: one row per even wave) are wave-uniform, so they come
@@ -121,19 +143,9 @@ __global__ __launch_bounds__(NT) void gemv_kernel(const bf16_t* __restrict__ x, 
     float ss[M];
 #pragma unroll
     for (int m = 0; m < M; ++m) ss[m] = 0.f;
-    if (nchunk <= 2 * NT) {
-      // ONE global round trip: x and the norm weights stay in registers between the sum of
-      // squares and the normalisation (K <= 16 Ki at 1024 threads)
-      u32x4 xr[2][M], gr[2];
-#pragma unroll
-      for (int j = 0; j < 2; ++j) {
-        const int c = tid + j * NT;
-        if (c < nchunk) {
-          gr[j] = reinterpret_cast<const u32x4*>(norm_w)[c];
-#pragma unroll
-          for (int m = 0; m < M; ++m) xr[j][m] = reinterpret_cast<const u32x4*>(x + static_cast<int64_t>(m) * x_stride)[c];
-        }
-      }
+    if (x_fast) {
+      // ONE global round trip (issued above): x and the norm weights stay in registers between
+      // the sum of squares and the normalisation (K <= 16 Ki at 1024 threads)
 #pragma unroll
       for (int j = 0; j < 2; ++j) {
         if (tid + j * NT < nchunk) {
@@ -266,6 +278,15 @@ __global__ __launch_bounds__(NT) void gemv_kernel(const bf16_t* __restrict__ x, 
 #pragma unroll
         for (int e = 0; e < 8; ++e) o[e] *= inv;
         reinterpret_cast<u32x4*>(xs + m * K)[c] = pack8(o);
+      }
+    }
+  } else if (x_fast) {
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int c = tid + j * NT;
+      if (c < nchunk) {
+#pragma unroll
+        for (int m = 0; m < M; ++m) reinterpret_cast<u32x4*>(xs + m * K)[c] = xr[j][m];
       }
     }
   } else {

@@ -36,6 +36,9 @@ int llmc_sample(const void*, int64_t, int, int, const void*, const void*, const 
                 void*, void*, void*, void*, void*, const void*, int, int, void*, void*, int, int, hipStream_t);
 int llmc_sample_parts();
 int llmc_moe_route(const void*, int, int, int, void*, void*, hipStream_t);
+int llmc_moe_down_combine(int, const void*, int, const void*, const void*, const void*, void*, int, int, int, int,
+                          hipStream_t);
+int llmc_moe_router(const void*, int, const void*, float, const void*, int, int, int, int, void*, void*, hipStream_t);
 int llmc_moe_align(const void*, int, int, int, int, void*, void*, void*, void*, hipStream_t);
 int llmc_moe_gemm(const void*, int, const void*, const void*, const void*, const void*, void*, int, int, int, int, int,
                   int, hipStream_t);
@@ -124,6 +127,13 @@ PYBIND11_MODULE(_llmc_hip, m) {
   m.def("sample_parts", []() { return llmc_sample_parts(); });
   m.def("moe_route", [](ptr logits, int T, int E, int k, ptr w, ptr ids, ptr s) {
     check(llmc_moe_route(P(logits), T, E, k, P(w), P(ids), S(s)), "moe_route");
+  });
+  m.def("moe_down_combine", [](int T, ptr act, int as, ptr W, ptr ids, ptr w, ptr h, int hs, int N, int K, int k,
+                               ptr s) {
+    check(llmc_moe_down_combine(T, P(act), as, P(W), P(ids), P(w), P(h), hs, N, K, k, S(s)), "moe_down_combine");
+  });
+  m.def("moe_router", [](ptr x, int xs, ptr nw, float eps, ptr Wr, int T, int E, int H, int k, ptr w, ptr ids, ptr s) {
+    check(llmc_moe_router(P(x), xs, P(nw), eps, P(Wr), T, E, H, k, P(w), P(ids), S(s)), "moe_router");
   });
   m.def("moe_align", [](ptr ids, int T, int k, int E, int tile, ptr sorted_rows, ptr tile_expert, ptr tile_count,
                         ptr counts, ptr s) {

@@ -145,41 +145,72 @@ extern "C" int llmc_gemv_attn_merge(int M, const void* x, int x_stride, const vo
 // MoE decode (K11 at batch 1): one GEMV per (token, top-k slot) pair against the selected
 // expert's weights; expert ids are read on device, so the launch is graph-replayable.
 namespace llmc {
-template <int NT, int RPW, int EPI>
-static int launch_moe_gemv(int npairs, const void* x, int x_stride, float eps, const void* W, const void* ids,
-                           int x_div, void* out, int out_stride, int N, int K, hipStream_t s) {
+template <int NT, int RPW, int EPI, int PRO>
+static int launch_moe_gemv(int npairs, const void* x, int x_stride, const void* nw, float eps, const void* W,
+                           const void* ids, int x_div, void* out, int out_stride, int N, int K, hipStream_t s) {
   constexpr int WAVES = NT / kWave;
   const size_t lds = static_cast<size_t>(K) * sizeof(bf16_t) + 2 * WAVES * sizeof(float);
   if (lds > 64 * 1024) return -2;
   dim3 grid((N + WAVES * RPW - 1) / (WAVES * RPW), npairs);
-  gemv_kernel<1, NT, RPW, 4, PRO_NONE, EPI, true><<<grid, NT, lds, s>>>(
-      (const bf16_t*)x, x_stride, nullptr, eps, (const bf16_t*)W, out, out_stride, N, K, (const int32_t*)ids, x_div,
-      RopeEpi{}, MergePro{});
+  gemv_kernel<1, NT, RPW, 4, PRO, EPI, true><<<grid, NT, lds, s>>>(
+      (const bf16_t*)x, x_stride, (const bf16_t*)nw, eps, (const bf16_t*)W, out, out_stride, N, K,
+      (const int32_t*)ids, x_div, RopeEpi{}, MergePro{});
   return static_cast<int>(hipGetLastError());
 }
 
-template <int EPI>
-static int moe_gemv_geom(int npairs, const void* x, int x_stride, float eps, const void* W, const void* ids, int x_div,
-                         void* out, int out_stride, int N, int K, hipStream_t s) {
+template <int EPI, int PRO>
+static int moe_gemv_geom(int npairs, const void* x, int x_stride, const void* nw, float eps, const void* W,
+                         const void* ids, int x_div, void* out, int out_stride, int N, int K, hipStream_t s) {
   // same geometry rule as the dense GEMV; the grid's y dimension (token, expert) pairs multiplies
   // the rounds, so whole rounds per pair are whole rounds overall
   switch (pick_waves(N, EPI == EPI_SILU)) {
-    case 16: return launch_moe_gemv<1024, 1, EPI>(npairs, x, x_stride, eps, W, ids, x_div, out, out_stride, N, K, s);
-    case 12: return launch_moe_gemv<768, 1, EPI>(npairs, x, x_stride, eps, W, ids, x_div, out, out_stride, N, K, s);
-    case 8: return launch_moe_gemv<512, 1, EPI>(npairs, x, x_stride, eps, W, ids, x_div, out, out_stride, N, K, s);
-    case 4: return launch_moe_gemv<256, 1, EPI>(npairs, x, x_stride, eps, W, ids, x_div, out, out_stride, N, K, s);
-    default: return launch_moe_gemv<256, 2, EPI>(npairs, x, x_stride, eps, W, ids, x_div, out, out_stride, N, K, s);
+    case 16: return launch_moe_gemv<1024, 1, EPI, PRO>(npairs, x, x_stride, nw, eps, W, ids, x_div, out, out_stride, N, K, s);
+    case 12: return launch_moe_gemv<768, 1, EPI, PRO>(npairs, x, x_stride, nw, eps, W, ids, x_div, out, out_stride, N, K, s);
+    case 8: return launch_moe_gemv<512, 1, EPI, PRO>(npairs, x, x_stride, nw, eps, W, ids, x_div, out, out_stride, N, K, s);
+    case 4: return launch_moe_gemv<256, 1, EPI, PRO>(npairs, x, x_stride, nw, eps, W, ids, x_div, out, out_stride, N, K, s);
+    default: return launch_moe_gemv<256, 2, EPI, PRO>(npairs, x, x_stride, nw, eps, W, ids, x_div, out, out_stride, N, K, s);
   }
 }
 }  // namespace llmc
 
+// MoE decode down projection fused with the combine: h[t] += sum_j w[t, j] * (W_down[ids[t, j]] . act[t*k + j])
+// for top-2 routing (k == 2), one block per 16 output rows per token, each wave streaming its row
+// of both experts. Expert-parallel ranks (ids -1) keep the separate GEMV + combine.
+extern "C" int llmc_moe_down_combine(int T, const void* act, int act_stride, const void* W, const void* ids,
+                                     const void* w, void* h, int h_stride, int N, int K, int k, hipStream_t s) {
+  if (k != 2 || K % 8 != 0) return -1;
+  constexpr int NT = 1024, WAVES = NT / kWave;
+  auto kern = gemv_kernel<2, NT, 2, 4, PRO_NONE, EPI_COMBINE, true>;
+  const size_t lds = static_cast<size_t>(2) * K * sizeof(bf16_t) + 2 * 2 * WAVES * sizeof(float);
+  if (lds > 160 * 1024) return -2;
+  static bool attr_set = false;
+  if (lds > 64 * 1024 && !attr_set) {
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize,
+                              160 * 1024);
+    attr_set = true;
+  }
+  RopeEpi wts{};
+  wts.cos_t = static_cast<const float*>(w);
+  dim3 grid((N + WAVES - 1) / WAVES, T);
+  kern<<<grid, NT, lds, s>>>((const bf16_t*)act, act_stride, nullptr, 0.f, (const bf16_t*)W, h, h_stride, N, K,
+                             (const int32_t*)ids, 1, wts, MergePro{});
+  return static_cast<int>(hipGetLastError());
+}
+
 extern "C" int llmc_moe_gemv(int npairs, const void* x, int x_stride, const void* norm_w, float eps, const void* W,
                              const void* ids, int x_div, void* out, int out_stride, int N, int K, int epi,
                              hipStream_t s) {
-  if (K % 8 != 0 || norm_w != nullptr) return -1;
+  // norm_w: x is the raw hidden row, RMS-normalised in the prologue (the decode gate_up after the
+  // fused router); nullptr: x is used as is (down projection)
+  if (K % 8 != 0) return -1;
+  const void* nw = norm_w;
   switch (epi) {
-    case EPI_BF16: return moe_gemv_geom<EPI_BF16>(npairs, x, x_stride, eps, W, ids, x_div, out, out_stride, N, K, s);
-    case EPI_SILU: return moe_gemv_geom<EPI_SILU>(npairs, x, x_stride, eps, W, ids, x_div, out, out_stride, N, K, s);
+    case EPI_BF16:
+      return nw ? moe_gemv_geom<EPI_BF16, PRO_NORM>(npairs, x, x_stride, nw, eps, W, ids, x_div, out, out_stride, N, K, s)
+                : moe_gemv_geom<EPI_BF16, PRO_NONE>(npairs, x, x_stride, nw, eps, W, ids, x_div, out, out_stride, N, K, s);
+    case EPI_SILU:
+      return nw ? moe_gemv_geom<EPI_SILU, PRO_NORM>(npairs, x, x_stride, nw, eps, W, ids, x_div, out, out_stride, N, K, s)
+                : moe_gemv_geom<EPI_SILU, PRO_NONE>(npairs, x, x_stride, nw, eps, W, ids, x_div, out, out_stride, N, K, s);
     default: return -4;
   }
 }

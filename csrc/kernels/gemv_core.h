@@ -28,7 +28,7 @@
 namespace llmc {
 
 enum { PRO_NONE = 0, PRO_NORM = 1, PRO_MERGE = 2 };
-enum { EPI_BF16 = 0, EPI_F32 = 1, EPI_RESADD = 2, EPI_SILU = 3, EPI_ROPE = 4 };
+enum { EPI_BF16 = 0, EPI_F32 = 1, EPI_RESADD = 2, EPI_SILU = 3, EPI_ROPE = 4, EPI_COMBINE = 5 };
 
 struct RopeEpi {
   bf16_t* q_out;            // [M, q_stride], canonical head-major layout
@@ -61,19 +61,31 @@ __global__ __launch_bounds__(NT) void gemv_kernel(const bf16_t* __restrict__ x, 
   constexpr bool PAIR_LDS = (EPI == EPI_SILU || EPI == EPI_ROPE) && RPW == 1;  // host: N % (2 * WAVES) == 0
   // EXPERT (MoE decode): blockIdx.y = (token, slot) pair; weights of expert expert_ids[pair],
   // input row pair / x_div, output row pair (M must be 1).
-  if constexpr (EXPERT) {
+  // EPI_COMBINE (MoE decode down projection fused with the combine; EXPERT, M == RPW == top-k):
+  // blockIdx.y = token t; wave row n streams row n of each of the token's k experts ("rows" r =
+  // slots), x row r = the slot's activation; acc[r][r] is that expert's output and the epilogue
+  // does h[t][n] += sum_r w[t][r] * acc[r][r] in a fixed order (replaces moe_combine's launch and
+  // the y round trip). x_div carries nothing here; the router weights come in through `rope.cos_t`.
+  constexpr bool COMBINE = EPI == EPI_COMBINE;
+  static_assert(!COMBINE || (EXPERT && M == RPW), "combine: one x row per expert slot");
+  if constexpr (EXPERT && !COMBINE) {
     const int pair = blockIdx.y;
     if (expert_ids[pair] < 0) return;  // another rank's expert (expert parallel): whole block exits
     W += static_cast<int64_t>(expert_ids[pair]) * N * K;
     x += static_cast<int64_t>(pair / x_div) * x_stride;
     out = reinterpret_cast<char*>(out) + static_cast<int64_t>(pair) * out_stride * (EPI == EPI_F32 ? 4 : 2);
   }
+  if constexpr (COMBINE) {
+    const int t = blockIdx.y;
+    x += static_cast<int64_t>(t) * RPW * x_stride;
+    out = reinterpret_cast<char*>(out) + static_cast<int64_t>(t) * out_stride * 2;
+  }
   extern __shared__ __attribute__((aligned(16))) char smem[];
   bf16_t* xs = reinterpret_cast<bf16_t*>(smem);  // [M][K]
   const int tid = threadIdx.x;
   const int nchunk = K / 8;
   const int wave = tid / kWave, lane = tid % kWave;
-  const int row0 = (blockIdx.x * WAVES + wave) * RPW;
+  const int row0 = COMBINE ? blockIdx.x * WAVES + wave : (blockIdx.x * WAVES + wave) * RPW;
 
   // Weight rows (clamped: waves past N still load a valid row and discard it, so no lane
   // diverges before the block barrier). The first UNROLL-batch of W is issued BEFORE the x
@@ -82,8 +94,13 @@ __global__ __launch_bounds__(NT) void gemv_kernel(const bf16_t* __restrict__ x, 
   const u32x4* wrow[RPW];
 #pragma unroll
   for (int r = 0; r < RPW; ++r) {
-    const int n = min(row0 + r, N - 1);
-    wrow[r] = reinterpret_cast<const u32x4*>(W + static_cast<int64_t>(n) * K);
+    if constexpr (COMBINE) {
+      const int e = expert_ids[blockIdx.y * RPW + r];
+      wrow[r] = reinterpret_cast<const u32x4*>(W + (static_cast<int64_t>(e) * N + min(row0, N - 1)) * K);
+    } else {
+      const int n = min(row0 + r, N - 1);
+      wrow[r] = reinterpret_cast<const u32x4*>(W + static_cast<int64_t>(n) * K);
+    }
   }
   constexpr int STEP = kWave * UNROLL;
   const int iters = (nchunk + STEP - 1) / STEP;
@@ -336,7 +353,8 @@ __global__ __launch_bounds__(NT) void gemv_kernel(const bf16_t* __restrict__ x, 
         for (int m = 0; m < M; ++m) {
           const u32x4 xx = xv[m * nchunk + c];
 #pragma unroll
-          for (int r = 0; r < RPW; ++r) acc[r][m] = dot8_bf16(wv[r][u], xx, acc[r][m]);
+          for (int r = 0; r < RPW; ++r)
+            if (!COMBINE || r == m) acc[r][m] = dot8_bf16(wv[r][u], xx, acc[r][m]);
         }
       }
     }
@@ -363,7 +381,8 @@ __global__ __launch_bounds__(NT) void gemv_kernel(const bf16_t* __restrict__ x, 
 #pragma unroll
   for (int r = 0; r < RPW; ++r)
 #pragma unroll
-    for (int m = 0; m < M; ++m) acc[r][m] = wave_sum(acc[r][m]);
+    for (int m = 0; m < M; ++m)
+      if (!COMBINE || r == m) acc[r][m] = wave_sum(acc[r][m]);
 
   // ---- epilogue ----
   // paired epilogues (SiLU, RoPE) combine rows (2j, 2j + 1): the same wave holds both when
@@ -427,6 +446,17 @@ __global__ __launch_bounds__(NT) void gemv_kernel(const bf16_t* __restrict__ x, 
             pair_epi(row0, m, acc[0][m], pairx[(wave >> 1) * M + m], 1.f, 0.f, -1);
           }
         }
+    }
+    return;
+  }
+  if constexpr (COMBINE) {
+    if (lane == 0 && row0 < N) {
+      const float* wt = rope.cos_t + blockIdx.y * RPW;  // router weights [T, k]
+      bf16_t* h = reinterpret_cast<bf16_t*>(out) + row0;
+      float v = bf16_to_f32(*h);
+#pragma unroll
+      for (int r = 0; r < RPW; ++r) v += wt[r] * acc[r][r];
+      *h = f32_to_bf16(v);
     }
     return;
   }

@@ -47,6 +47,93 @@ __global__ void moe_route_kernel(const float* __restrict__ logits, int T, int E,
   for (int j = 0; j < k; ++j) w[static_cast<int64_t>(t) * k + j] = sel[j] / ssum;
 }
 
+// Decode router, fused: RMSNorm of the token's hidden row -> router GEMV (one wave per expert,
+// the E x H router weights streamed once) -> softmax / top-k / renormalise, in ONE launch of one
+// block per token (replaces rmsnorm + router GEMV + moe_route: three latency-bound launches per
+// MoE layer). The expert GEMVs normalise x again in their own prologue (PRO_NORM), so the normed
+// row is never written to memory. H <= 8 * 512 * 2 (two 16-B chunks per thread).
+constexpr int kRouterThreads = 512;
+
+__global__ __launch_bounds__(kRouterThreads) void moe_router_kernel(
+    const bf16_t* __restrict__ x, int x_stride, const bf16_t* __restrict__ norm_w, float eps,
+    const bf16_t* __restrict__ Wr, int E, int H, int k, float* __restrict__ w_out, int32_t* __restrict__ ids_out) {
+  constexpr int WAVES = kRouterThreads / kWave;
+  __shared__ __attribute__((aligned(16))) bf16_t xs[8192];
+  __shared__ float red[WAVES];
+  __shared__ float logit[64];
+  const int t = blockIdx.x, tid = threadIdx.x, wave = tid / kWave, lane = tid % kWave;
+  const int nchunk = H / 8;
+  const bf16_t* xr = x + static_cast<int64_t>(t) * x_stride;
+  u32x4 xv[2], gv[2];
+  float ss = 0.f;
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    const int c = tid + j * kRouterThreads;
+    if (c < nchunk) {
+      xv[j] = reinterpret_cast<const u32x4*>(xr)[c];
+      gv[j] = reinterpret_cast<const u32x4*>(norm_w)[c];
+    }
+  }
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    if (tid + j * kRouterThreads < nchunk) {
+      float f[8];
+      unpack8(xv[j], f);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) ss += f[e] * f[e];
+    }
+  }
+  const float tot = block_sum<kRouterThreads>(ss, red);
+  const float inv = rsqrtf(tot / H + eps);
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    const int c = tid + j * kRouterThreads;
+    if (c < nchunk) {
+      float f[8], g[8];
+      unpack8(xv[j], f);
+      unpack8(gv[j], g);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) f[e] = f[e] * inv * g[e];
+      reinterpret_cast<u32x4*>(xs)[c] = pack8(f);  // bf16, as the standalone rmsnorm would store it
+    }
+  }
+  __syncthreads();
+  const u32x4* xsv = reinterpret_cast<const u32x4*>(xs);
+  for (int e = wave; e < E; e += WAVES) {
+    const u32x4* wr = reinterpret_cast<const u32x4*>(Wr + static_cast<int64_t>(e) * H);
+    float acc = 0.f;
+    for (int c = lane; c < nchunk; c += kWave) acc = dot8_bf16(load16<true>(wr + c), xsv[c], acc);
+    acc = wave_sum(acc);
+    if (lane == 0) logit[e] = acc;
+  }
+  __syncthreads();
+  if (tid == 0) {
+    float mx = -INFINITY;
+    for (int e = 0; e < E; ++e) mx = fmaxf(mx, logit[e]);
+    float z = 0.f;
+    for (int e = 0; e < E; ++e) z += __expf(logit[e] - mx);
+    uint64_t taken = 0;
+    float sel[8];
+    float ssum = 0.f;
+    for (int j = 0; j < k; ++j) {
+      int best = -1;
+      float bv = -INFINITY;
+      for (int e = 0; e < E; ++e) {
+        if ((taken >> e) & 1ull) continue;
+        if (logit[e] > bv) {
+          bv = logit[e];
+          best = e;
+        }
+      }
+      taken |= 1ull << best;
+      sel[j] = __expf(bv - mx) / z;
+      ssum += sel[j];
+      ids_out[static_cast<int64_t>(t) * k + j] = best;
+    }
+    for (int j = 0; j < k; ++j) w_out[static_cast<int64_t>(t) * k + j] = sel[j] / ssum;
+  }
+}
+
 constexpr int kAlignThreads = 1024;
 constexpr int kMoeTile = 128;
 
@@ -130,6 +217,14 @@ extern "C" {
 int llmc_moe_route(const void* logits, int T, int E, int k, void* w, void* ids, hipStream_t s) {
   if (E > 64 || k > 8 || k > E) return -1;
   moe_route_kernel<<<(T + 255) / 256, 256, 0, s>>>((const float*)logits, T, E, k, (float*)w, (int32_t*)ids);
+  return static_cast<int>(hipGetLastError());
+}
+
+int llmc_moe_router(const void* x, int x_stride, const void* norm_w, float eps, const void* Wr, int T, int E, int H,
+                    int k, void* w, void* ids, hipStream_t s) {
+  if (E > 64 || k > 8 || k > E || H % 8 != 0 || H > 8192) return -1;
+  moe_router_kernel<<<T, kRouterThreads, 0, s>>>((const bf16_t*)x, x_stride, (const bf16_t*)norm_w, eps,
+                                                 (const bf16_t*)Wr, E, H, k, (float*)w, (int32_t*)ids);
   return static_cast<int>(hipGetLastError());
 }
 

@@ -524,26 +524,30 @@ class Engine:
 
     def _moe_decode(self, h, Lw, B) -> None:
         c = self.cfg
-        xn = self.xn[:B]
-        ops.rmsnorm(h, Lw.ln2, c.rms_eps, out=xn)
         if not h.is_cuda:
+            xn = self.xn[:B]
+            ops.rmsnorm(h, Lw.ln2, c.rms_eps, out=xn)
             self._moe(xn, Lw, h)
             return
         k = c.top_k_experts
-        rl = self.router_logits[:B]
-        ops.linear(xn, Lw.w_router, EPI_F32, out=rl)
         w, ids = self.moe_w[:B], self.moe_ids[:B]
-        ops.moe_route(rl, k, w, ids)
+        # one launch: rmsnorm -> router logits -> top-k; the expert gate_up GEMV normalises h
+        # again in its own prologue, so the normed row never goes through memory
+        ops.moe_router(h, Lw.ln2, c.rms_eps, Lw.w_router, k, w, ids)
         if self.w.ep:  # pairs of other ranks' experts: id -1 (GEMV blocks exit), weight 0
             ops.moe_ep_localize(ids, w, self.w.e0, self.w.n_local_experts, self.moe_lids[:B], self.moe_lw[:B])
             w, ids = self.moe_lw[:B], self.moe_lids[:B]
         I_l, H = self.w.inter, c.hidden
         act, y = self.moe_act[: B * k], self.moe_y[: B * k]
-        ops.moe_gemv(xn, Lw.w_gu, ids, k, act, 2 * I_l, H, EPI_SILU)
-        ops.moe_gemv(act, Lw.w_down, ids, 1, y, H, I_l, EPI_BF16)
-        if self.tp.rank != 0:
+        ops.moe_gemv(h, Lw.w_gu, ids, k, act, 2 * I_l, H, EPI_SILU, norm_w=Lw.ln2, eps=c.rms_eps)
+        if self.tp.rank != 0:  # row-parallel partial: only rank 0 carries the residual
             h.zero_()
-        ops.moe_combine(y, w, ids, h)
+        if k == 2 and not self.w.ep:
+            # down projection + combine in one launch (each wave streams its row of both experts)
+            ops.moe_down_combine(act, Lw.w_down, ids, w, h, H, I_l)
+        else:
+            ops.moe_gemv(act, Lw.w_down, ids, 1, y, H, I_l, EPI_BF16)
+            ops.moe_combine(y, w, ids, h)
         self.tp.all_reduce_(h)
 
     def _gather_logits(self, B: int) -> torch.Tensor:

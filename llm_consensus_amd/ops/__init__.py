@@ -305,11 +305,36 @@ def moe_combine(y, w, ids, h):
     return h
 
 
-def moe_gemv(x, W_experts, ids, x_div, out, N, K, epi):
+def moe_gemv(x, W_experts, ids, x_div, out, N, K, epi, norm_w=None, eps: float = 1e-5):
+    """Decode expert GEMV over (token, slot) pairs; ``norm_w``: RMS-normalise x (raw hidden rows)
+    in the prologue."""
     npairs = ids.numel()
-    kernels().moe_gemv(npairs, _p(x), x.stride(0), 0, 0.0, _p(W_experts), _p(ids), x_div, _p(out), out.stride(0), N, K,
-                       epi, _s(x))
+    kernels().moe_gemv(npairs, _p(x), x.stride(0), _p(norm_w) if norm_w is not None else 0, float(eps),
+                       _p(W_experts), _p(ids), x_div, _p(out), out.stride(0), N, K, epi, _s(x))
     return out
+
+
+def moe_down_combine(act, W_down, ids, w, h, N, K):
+    """Decode MoE down projection fused with the combine (top-2): h[t] += sum_j w[t, j] *
+    (W_down[ids[t, j]] . act[t*2 + j]), fixed order, f32."""
+    T, k = ids.shape
+    kernels().moe_down_combine(T, _p(act), act.stride(0), _p(W_down), _p(ids), _p(w), _p(h), h.stride(0), N, K, k,
+                               _s(act))
+    return h
+
+
+def moe_router(x, norm_w, eps: float, W_router, k: int, w_out, ids_out):
+    """Decode router, one launch: rmsnorm(x) * norm_w -> router logits -> softmax top-k (renormalised).
+    x [T, H] bf16 (raw hidden rows), W_router [E, H]."""
+    if not x.is_cuda:
+        xn = oracle.rmsnorm(x, norm_w, eps)
+        logits = oracle.linear(xn, W_router, EPI_F32)
+        return moe_route(logits, k, w_out, ids_out)
+    T, H = x.shape
+    E = W_router.shape[0]
+    kernels().moe_router(_p(x), x.stride(0), _p(norm_w), float(eps), _p(W_router), T, E, H, k, _p(w_out), _p(ids_out),
+                         _s(x))
+    return w_out, ids_out
 
 
 def moe_ep_localize(ids, w, e0: int, n_local: int, lids_out, lw_out):

@@ -339,6 +339,46 @@ def test_moe(cuda, T):
     close(h, href, 3e-2)
 
 
+@pytest.mark.parametrize("T,E,H", [(1, 8, 4096), (4, 8, 256), (2, 16, 1024), (3, 4, 192)])
+def test_moe_router_fused(cuda, T, E, H):
+    """Decode router in one launch (rmsnorm -> router GEMV -> softmax top-k) vs the fp32 oracle, and
+    the expert gate_up GEMV normalising raw hidden rows in its prologue vs normed rows."""
+    torch.manual_seed(9)
+    k = 2
+    h = rnd(T, H)
+    nw = (1 + 0.1 * torch.randn(H, device="cuda")).to(BF)
+    wr = rnd(E, H, scale=0.05)
+    w = torch.empty(T, k, device="cuda")
+    ids = torch.empty(T, k, dtype=torch.int32, device="cuda")
+    ops.moe_router(h, nw, 1e-5, wr, k, w, ids)
+    xn = oracle.rmsnorm(h.cpu(), nw.cpu(), 1e-5)
+    logits = oracle.linear(xn, wr.cpu(), ops.EPI_F32)
+    rw, rids = oracle.moe_route(logits, k)
+    # a near-tie of the logits may order two experts differently: compare the selected sets' logits
+    got = torch.gather(logits, 1, ids.cpu().long())
+    ref = torch.gather(logits, 1, rids.long())
+    close(got, ref, 1e-3, 1e-3)
+    close(w, rw, 2e-3, 2e-3)
+    I = 384
+    wgu = rnd(E, 2 * I, H, scale=0.05)
+    a1 = torch.empty(T * k, I, dtype=BF, device="cuda")
+    a2 = torch.empty(T * k, I, dtype=BF, device="cuda")
+    ops.moe_gemv(h, wgu, ids, k, a1, 2 * I, H, ops.EPI_SILU, norm_w=nw, eps=1e-5)
+    ops.moe_gemv(xn.to(h.device), wgu, ids, k, a2, 2 * I, H, ops.EPI_SILU)
+    close(a1, a2, 2e-2)
+    # down projection + combine in one launch vs an fp32 reference (the unfused path rounds each
+    # expert output to bf16 before the combine, so it is the less exact one)
+    wd = rnd(E, H, I, scale=0.05)
+    h1 = h.clone()
+    ops.moe_down_combine(a1, wd, ids, w, h1, H, I)
+    href = h.float().cpu().clone()
+    a1c, wdc, idc, wc = a1.float().cpu(), wd.float().cpu(), ids.cpu().long(), w.cpu()
+    for t in range(T):
+        for j in range(k):
+            href[t] += wc[t, j] * (wdc[idc[t, j]] @ a1c[t * k + j])
+    close(h1, href, 2e-2)
+
+
 @pytest.mark.parametrize("nh,nkv,D", [(32, 8, 128), (4, 1, 128), (32, 32, 96), (16, 2, 64)])
 @pytest.mark.parametrize("gc", [1, 5, 32])
 @pytest.mark.parametrize("epi", [0, 2])

@@ -60,7 +60,12 @@ template <int M, int PRO, int EPI>
 static int launch_gemv(const void* x, int x_stride, const void* nw, float eps, const void* W, void* out,
                        int out_stride, int N, int K, const RopeEpi& rope, const MergePro& mp, hipStream_t s) {
   constexpr bool paired = EPI == EPI_SILU || EPI == EPI_ROPE;
-  switch (pick_waves(N, paired)) {
+  const int w = pick_waves(N, paired);
+  // long rows on few blocks (a 70B TP=4 rank's qkv: 2560 x 8192 = 160 fat blocks): 8 loads per
+  // lane in flight instead of 4 (9.67 vs 10.99 us, profiles/r1_attn_decode_tp_shapes.md)
+  if (w == 16 && K >= 8192 && N <= 4096)
+    return launch_gemv_g<M, 1024, 1, PRO, EPI, 8>(x, x_stride, nw, eps, W, out, out_stride, N, K, rope, mp, s);
+  switch (w) {
     case 16: return launch_gemv_g<M, 1024, 1, PRO, EPI>(x, x_stride, nw, eps, W, out, out_stride, N, K, rope, mp, s);
     case 12: return launch_gemv_g<M, 768, 1, PRO, EPI>(x, x_stride, nw, eps, W, out, out_stride, N, K, rope, mp, s);
     case 8: return launch_gemv_g<M, 512, 1, PRO, EPI>(x, x_stride, nw, eps, W, out, out_stride, N, K, rope, mp, s);

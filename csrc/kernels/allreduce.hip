@@ -94,12 +94,17 @@ __device__ __forceinline__ void car_end(const CarPeers& P, int rank, uint32_t ep
 __global__ __launch_bounds__(256) void car_allreduce_kernel(CarPeers P, bf16_t* __restrict__ x, int n16, int rank,
                                                             int world, size_t cap) {
   __shared__ uint32_t lds_epoch;
+  const int v0 = blockIdx.x * kChunk + threadIdx.x, vstep = kBlocks * kChunk;
+  const u32x4* xv = reinterpret_cast<const u32x4*>(x);
+  // this thread's first vector is loaded before the epoch: the two memory round trips overlap
+  // (a decode-sized message is one vector per thread)
+  u32x4 first{};
+  if (v0 < n16) first = xv[v0];
   const uint32_t epoch = car_begin(P, rank, &lds_epoch);
   const size_t doff = kSigBytes + (epoch & 1) * cap;
-  const int v0 = blockIdx.x * kChunk + threadIdx.x, vstep = kBlocks * kChunk;
   u32x4* mine = reinterpret_cast<u32x4*>(P.base[rank] + doff);
-  const u32x4* xv = reinterpret_cast<const u32x4*>(x);
-  for (int v = v0; v < n16; v += vstep) mine[v] = xv[v];
+  if (v0 < n16) mine[v0] = first;
+  for (int v = v0 + vstep; v < n16; v += vstep) mine[v] = xv[v];
   car_arrive_and_wait(P, rank, world, &lds_epoch);
   for (int v = v0; v < n16; v += vstep) {
     float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
@@ -125,12 +130,15 @@ __global__ __launch_bounds__(256) void car_allreduce_kernel(CarPeers P, bf16_t* 
 __global__ __launch_bounds__(256) void car_allgather_kernel(CarPeers P, const char* __restrict__ x, char* __restrict__ out,
                                                             int n16, int rank, int world, size_t cap) {
   __shared__ uint32_t lds_epoch;
+  const int v0 = blockIdx.x * kChunk + threadIdx.x, vstep = kBlocks * kChunk;
+  const u32x4* xv = reinterpret_cast<const u32x4*>(x);
+  u32x4 first{};
+  if (v0 < n16) first = xv[v0];  // overlaps the epoch load (see car_allreduce_kernel)
   const uint32_t epoch = car_begin(P, rank, &lds_epoch);
   const size_t doff = kSigBytes + (epoch & 1) * cap;
-  const int v0 = blockIdx.x * kChunk + threadIdx.x, vstep = kBlocks * kChunk;
   u32x4* mine = reinterpret_cast<u32x4*>(P.base[rank] + doff);
-  const u32x4* xv = reinterpret_cast<const u32x4*>(x);
-  for (int v = v0; v < n16; v += vstep) mine[v] = xv[v];
+  if (v0 < n16) mine[v0] = first;
+  for (int v = v0 + vstep; v < n16; v += vstep) mine[v] = xv[v];
   car_arrive_and_wait(P, rank, world, &lds_epoch);
   u32x4* ov = reinterpret_cast<u32x4*>(out);
   for (int v = v0; v < n16; v += vstep) {

@@ -69,3 +69,32 @@ def test_continuous_batching_cpu():
 @pytest.mark.gpu
 def test_continuous_batching_gpu(cuda):
     _check("cuda:0")
+
+
+def test_continuous_batching_cancelled_row_cpu():
+    """A row whose request is cancelled mid-decode is retired with the context's error; the rows
+    around it (moved by compaction) still get their solo tokens."""
+    from llm_consensus_amd.context import Context, ContextError
+
+    eng = _engine("cpu")
+    reqs = [([300 + i for i in range(12)], SamplingParams(max_tokens=30, temperature=0.0, stop_on_eos=False)),
+            ([400 + i for i in range(7)], SamplingParams(max_tokens=30, temperature=0.0, stop_on_eos=False)),
+            ([500 + i for i in range(9)], SamplingParams(max_tokens=25, temperature=0.0, stop_on_eos=False))]
+    ref = [_alone(eng, p, sp) for p, sp in reqs]
+    bat = ContinuousBatcher(eng)
+    ctxs = [Context.background() for _ in reqs]
+    for i, (p, sp) in enumerate(reqs):
+        s = eng.new_sequence()
+        eng.prefill([s], [p])
+        bat.admit(s, sp, tag=i, ctx=ctxs[i])
+    done, step = {}, 0
+    while bat.rows:
+        if step == 1:
+            ctxs[0].cancel()  # row 0: the others move down when it retires
+        for row in bat.step():
+            done[row.tag] = row
+            eng.free_sequence(row.seq)
+        step += 1
+    assert isinstance(done[0].error, ContextError)
+    for i in (1, 2):
+        assert done[i].error is None and done[i].tokens == ref[i]

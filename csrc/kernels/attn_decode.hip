@@ -204,9 +204,6 @@ __global__ __launch_bounds__(256) void attn_decode_reduce_kernel(const float* __
   static_assert(DB == 16 || DB == 32 || DB == 64, "DB");
   constexpr int CG = 256 / DB;  // chunk groups
   const int kvh = blockIdx.x / G, g = blockIdx.x % G, b = blockIdx.y;
-  const int L = seq_lens[b];
-  const int nchunks = decode_nsplit(L, gc, chunk_arg);
-  if (nchunks <= 1) return;
   extern __shared__ __attribute__((aligned(16))) char smem[];
   float* sc = reinterpret_cast<float*>(smem);  // [max_chunks]: m, then exp(m - M)
   float* lv = sc + max_chunks;                 // [max_chunks]: l
@@ -217,18 +214,29 @@ __global__ __launch_bounds__(256) void attn_decode_reduce_kernel(const float* __
   const int dl = tid % DB, cg = tid / DB;
   const int d = blockIdx.z * DB + dl;
   const bool live = d < D;
-  // issue: this thread's first 16 partial values (chunks cg, cg + CG, ...) and the m / l words
+  // The partial values and this thread's (m, l) words are loaded for the GRID's chunk count gc
+  // before the sequence length arrives: they do not depend on it, so the length's round trip
+  // and theirs overlap. Slots past the sequence's own chunk count hold finite stale partials
+  // (the workspace starts zeroed) and are masked below, never multiplied in.
   float v[16];
 #pragma unroll
   for (int j = 0; j < 16; ++j) {
-    const int c = min(cg + CG * j, nchunks - 1);  // clamped: all loads in flight, masked below
+    const int c = min(cg + CG * j, gc - 1);  // clamped: all loads in flight, masked below
     v[j] = live ? pb[c * cstride + d] : 0.f;
   }
+  float m0 = kNegBig, l0 = 0.f;
+  if (tid < gc) {
+    m0 = pb[tid * cstride + D];
+    l0 = pb[tid * cstride + D + 1];
+  }
+  const int L = seq_lens[b];
+  const int nchunks = decode_nsplit(L, gc, chunk_arg);
+  if (nchunks <= 1) return;
   float mx = kNegBig;
   for (int c = tid; c < nchunks; c += 256) {
-    const float m = pb[c * cstride + D];
+    const float m = c == tid ? m0 : pb[c * cstride + D];
     sc[c] = m;
-    lv[c] = pb[c * cstride + D + 1];
+    lv[c] = c == tid ? l0 : pb[c * cstride + D + 1];
     mx = fmaxf(mx, m);
   }
   mx = wave_max(mx);

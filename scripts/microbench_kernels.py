@@ -92,6 +92,12 @@ def bench_attn_phi3():
             t4 = timeit(lambda: ops.attn_decode(q, kc, vc, bt, sl, out, part, ctr, nh, nkv, D, bs, 128,
                                                 1 / math.sqrt(D), grid_chunks=gc_eff, mode=4))
             line.append(f"g{gc_eff}: {t2:5.2f} (attn {t4:5.2f})")
+        for chunk in (64, 128, 256):  # VALU split-KV kernel, fixed chunks (mode 0)
+            mc = (L + chunk - 1) // chunk
+            part, ctr = ops.decode_attn_workspace(1, nh, nkv, D, mc, "cuda")
+            t0 = timeit(lambda: ops.attn_decode(q, kc, vc, bt, sl, out, part, ctr, nh, nkv, D, bs, chunk,
+                                                1 / math.sqrt(D), mode=0))
+            line.append(f"valu c{chunk}: {t0:5.2f}")
         print(f"phi3 attn L={L:6d}: " + "  ".join(line), flush=True)
 
 

@@ -36,6 +36,8 @@ int llmc_sample(const void*, int64_t, int, int, const void*, const void*, const 
                 void*, void*, void*, void*, void*, const void*, int, int, void*, void*, int, int, hipStream_t);
 int llmc_sample_parts();
 int llmc_moe_route(const void*, int, int, int, void*, void*, hipStream_t);
+int llmc_gemv_rowpar_ar(int, const void*, int, const void*, void*, int, int, int, const void* const*, int, int, long,
+                        hipStream_t);
 int llmc_moe_down_combine(int, const void*, int, const void*, const void*, const void*, void*, int, int, int, int,
                           hipStream_t);
 int llmc_moe_router(const void*, int, const void*, float, const void*, int, int, int, int, void*, void*, hipStream_t);
@@ -188,6 +190,12 @@ PYBIND11_MODULE(_llmc_hip, m) {
     std::vector<const void*> b(bases.size());
     for (size_t i = 0; i < bases.size(); ++i) b[i] = P(bases[i]);
     check(llmc_car_allreduce(b.data(), rank, world, cap, P(x), nbytes, S(s)), "car_allreduce");
+  });
+  m.def("gemv_rowpar_ar", [](int M, ptr x, int xs, ptr W, ptr h, int hs, int N, int K, const std::vector<ptr>& bases,
+                             int rank, int world, long cap, ptr s) {
+    std::vector<const void*> b(bases.size());
+    for (size_t i = 0; i < bases.size(); ++i) b[i] = P(bases[i]);
+    check(llmc_gemv_rowpar_ar(M, P(x), xs, P(W), P(h), hs, N, K, b.data(), rank, world, cap, S(s)), "gemv_rowpar_ar");
   });
   m.def("car_allgather", [](const std::vector<ptr>& bases, int rank, int world, size_t cap, ptr x, ptr out,
                             size_t nbytes, ptr s) {

@@ -395,6 +395,10 @@ class Engine:
 
     def _row_parallel(self, x: torch.Tensor, W: torch.Tensor, h: torch.Tensor) -> None:
         """h += x @ W^T across the TP group (residual folded into rank 0's partial)."""
+        rp = self.tp.rowpar
+        if rp is not None and x.is_cuda and x.shape[0] <= ops.GEMV_MAX_M and W.shape[0] <= 4096:
+            rp.gemv_rowpar_ar(x, W, h)  # decode: the all-reduce runs in the GEMV's epilogue
+            return
         ops.linear(x, W, EPI_RESADD if self.tp.rank == 0 else EPI_BF16, out=h)
         self.tp.all_reduce_(h)
 

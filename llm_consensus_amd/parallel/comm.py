@@ -22,6 +22,8 @@ token shards the tokens travel to their experts' ranks and back by all-to-all (`
 
 from __future__ import annotations
 
+import os
+
 from typing import List, Optional
 
 import torch
@@ -36,6 +38,7 @@ class TPGroup:
         self.rank = rank
         self.size = size
         self.custom = None  # CustomAllReduce once enable_custom() ran
+        self.rowpar = None  # its twin for the row-parallel GEMVs with a fused all-reduce (LLMC_FUSED_AR=1)
 
     def enable_custom(self, device, cap: Optional[int] = None) -> bool:
         """Map the group's IPC buffers for the custom collectives (GPU groups of 2..8 ranks)."""
@@ -44,6 +47,10 @@ class TPGroup:
         from .custom_ar import DEFAULT_CAP, CustomAllReduce
 
         self.custom = CustomAllReduce(self.group, self.rank, self.size, device, cap or DEFAULT_CAP)
+        if os.environ.get("LLMC_FUSED_AR", "0") == "1":
+            # a second buffer, dedicated to the row-parallel GEMVs with the all-reduce in their
+            # epilogue (block epochs of their own)
+            self.rowpar = CustomAllReduce(self.group, self.rank, self.size, device, 128 * 1024)
         return True
 
     @staticmethod

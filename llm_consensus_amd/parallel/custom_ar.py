@@ -70,6 +70,21 @@ class CustomAllReduce:
     def timed_out(self) -> bool:
         return bool(kernels().car_timed_out(self.own))
 
+    def rowpar_timed_out(self) -> bool:
+        """Timeout word of a buffer used by gemv_rowpar_ar (its signal layout: ctr[1024] | flags
+        [1024][8] | timeout at 36864; car_timed_out reads at the all-reduce layout's 3072)."""
+        return bool(kernels().car_timed_out(self.own + (4 * 1024 + 1024 * 8 * 4) - (1024 + 64 * 8 * 4)))
+
+    def gemv_rowpar_ar(self, x: torch.Tensor, W: torch.Tensor, h: torch.Tensor) -> torch.Tensor:
+        """Row-parallel decode projection with the all-reduce in the GEMV epilogue (EPI_AR):
+        h = sum over ranks of x_r @ W_r^T, rank 0 folding the residual already in h. This
+        object's buffer must be dedicated to it (block epochs of its own, cap >= 128 KiB)."""
+        M, K = x.shape
+        kernels().gemv_rowpar_ar(M, x.data_ptr(), x.stride(0), W.data_ptr(), h.data_ptr(), h.stride(0), W.shape[0], K,
+                                 self.bases, self.rank, self.world, self.cap,
+                                 torch.cuda.current_stream(x.device).cuda_stream)
+        return h
+
     def close(self) -> None:
         k = kernels()
         for p in self._opened:

@@ -134,10 +134,9 @@ def main() -> None:
         ok = 1
         if rank < jtp:
             tp = TPGroup(grp, rank, jtp)
-            try:
-                tp.enable_custom(dev)
-            except Exception as ex:  # noqa: BLE001 - IPC mapping refused: fall back to a 1-GPU judge
-                log(f"custom all-reduce unavailable ({ex!r}); judge falls back to TP=1 on GPU 0")
+            # collective: every judge rank agrees on the outcome (peer mapping + a self-test)
+            if not tp.enable_custom(dev):
+                log("custom all-reduce unavailable; judge falls back to TP=1 on GPU 0")
                 ok = 0
         flag = torch.tensor([ok], dtype=torch.int32, device=cdev)
         dist.all_reduce(flag, op=dist.ReduceOp.MIN)

@@ -23,6 +23,7 @@ token shards the tokens travel to their experts' ranks and back by all-to-all (`
 from __future__ import annotations
 
 import os
+import warnings
 
 from typing import List, Optional
 
@@ -41,16 +42,24 @@ class TPGroup:
         self.rowpar = None  # its twin for the row-parallel GEMVs with a fused all-reduce (LLMC_FUSED_AR=1)
 
     def enable_custom(self, device, cap: Optional[int] = None) -> bool:
-        """Map the group's IPC buffers for the custom collectives (GPU groups of 2..8 ranks)."""
+        """Map the group's IPC buffers for the custom collectives (GPU groups of 2..8 ranks).
+        Collective; returns False on every rank (RCCL stays in charge) when any rank failed."""
         if self.size == 1 or self.custom is not None:
             return self.custom is not None
-        from .custom_ar import DEFAULT_CAP, CustomAllReduce
+        from .custom_ar import DEFAULT_CAP, CustomAllReduce, CustomAllReduceUnavailable
 
-        self.custom = CustomAllReduce(self.group, self.rank, self.size, device, cap or DEFAULT_CAP)
-        if os.environ.get("LLMC_FUSED_AR", "0") == "1":
-            # a second buffer, dedicated to the row-parallel GEMVs with the all-reduce in their
-            # epilogue (block epochs of their own)
-            self.rowpar = CustomAllReduce(self.group, self.rank, self.size, device, 128 * 1024)
+        try:
+            self.custom = CustomAllReduce(self.group, self.rank, self.size, device, cap or DEFAULT_CAP)
+            if os.environ.get("LLMC_FUSED_AR", "0") == "1":
+                # a second buffer, dedicated to the row-parallel GEMVs with the all-reduce in
+                # their epilogue (block epochs of their own, so no all-reduce self-test on it)
+                self.rowpar = CustomAllReduce(self.group, self.rank, self.size, device, 128 * 1024, selftest=False)
+        except CustomAllReduceUnavailable as e:
+            warnings.warn(f"custom all-reduce disabled, using RCCL: {e}")
+            if self.custom is not None:
+                self.custom.close()
+            self.custom = self.rowpar = None
+            return False
         return True
 
     @staticmethod

@@ -10,6 +10,7 @@ than the buffer).
 
 from __future__ import annotations
 
+import contextlib
 from typing import List, Optional
 
 import torch
@@ -19,31 +20,87 @@ from ..utils.native import kernels
 DEFAULT_CAP = 1 << 20  # bytes per parity: [4, 8192] bf16 hidden = 64 KiB; logits gather [4, 32064] f32 = 512 KiB
 
 
+def _on(device: torch.device):
+    return torch.cuda.device(device) if device.type == "cuda" else contextlib.nullcontext()
+
+
+class CustomAllReduceUnavailable(RuntimeError):
+    """Raised on EVERY rank of the group when any rank could not map the peers or the self-test
+    failed: the group agrees before anyone raises, so the callers fall back together (RCCL)."""
+
+
 class CustomAllReduce:
-    def __init__(self, group, rank: int, world: int, device: torch.device, cap: int = DEFAULT_CAP):
+    def __init__(self, group, rank: int, world: int, device: torch.device, cap: int = DEFAULT_CAP,
+                 selftest: bool = True):
         import torch.distributed as dist
 
         if world > 8:
             raise ValueError("custom all-reduce supports up to 8 ranks (one xGMI hop)")
         self.rank, self.world, self.cap = rank, world, int(cap)
         self.device = torch.device(device)
-        k = kernels()
-        with torch.cuda.device(self.device):
-            self.own = k.car_alloc(self.cap)
-            handle = k.ipc_handle(self.own)
-        handles: List[Optional[bytes]] = [None] * world
-        dist.all_gather_object(handles, handle, group=group)
+        self.group = group
+        self.own = 0
         self.bases: List[int] = []
         self._opened: List[int] = []
-        with torch.cuda.device(self.device):
-            for r, h in enumerate(handles):
-                if r == rank:
-                    self.bases.append(self.own)
-                else:
-                    p = k.ipc_open(h)
-                    self.bases.append(p)
-                    self._opened.append(p)
+        err: Optional[BaseException] = None
+        handle: Optional[bytes] = None
+        k = None
+        try:
+            k = kernels()
+            with _on(self.device):
+                self.own = k.car_alloc(self.cap)
+                handle = k.ipc_handle(self.own)
+        except Exception as e:  # noqa: BLE001 - reported collectively below
+            err = e
+        # every rank reaches every collective below, whatever failed locally (no mismatched calls)
+        handles: List[Optional[bytes]] = [None] * world
+        dist.all_gather_object(handles, handle, group=group)
+        if err is None and any(h is None for h in handles):
+            err = RuntimeError("a peer could not export its buffer")
+        if err is None:
+            try:
+                with _on(self.device):
+                    for r, h in enumerate(handles):
+                        if r == rank:
+                            self.bases.append(self.own)
+                        else:
+                            p = k.ipc_open(h)
+                            self.bases.append(p)
+                            self._opened.append(p)
+            except Exception as e:  # noqa: BLE001
+                err = e
+        ok = self._agree(err is None)
+        if ok and selftest:
+            ok = self._agree(self._selftest())
+            if not ok and err is None:
+                err = RuntimeError("self-test all-reduce returned wrong values or timed out")
+        if not ok:
+            self.close()
+            raise CustomAllReduceUnavailable(f"rank {rank}: {err!r}" if err else f"rank {rank}: a peer failed")
         dist.barrier(group=group)
+
+    def _agree(self, ok: bool) -> bool:
+        """MIN over the group of a local success flag (nccl wants a device tensor, gloo a host one)."""
+        import torch.distributed as dist
+
+        dev = self.device if dist.get_backend(self.group) == "nccl" else torch.device("cpu")
+        f = torch.tensor([1 if ok else 0], dtype=torch.int32, device=dev)
+        dist.all_reduce(f, op=dist.ReduceOp.MIN, group=self.group)
+        return bool(int(f.item()))
+
+    def _selftest(self) -> bool:
+        """One real collective through the mapped peers before anything depends on it: a wrong
+        sum or a spin that gave up (peer writes not visible over the link) disables the path."""
+        try:
+            n = 8192  # 16 KiB: the decode hidden state of an 8B model
+            x = torch.full((n,), float(self.rank + 1), dtype=torch.bfloat16, device=self.device)
+            self.all_reduce_(x)
+            if x.is_cuda:
+                torch.cuda.synchronize(self.device)
+            want = self.world * (self.world + 1) // 2
+            return bool((x == want).all().item()) and not self.timed_out()
+        except Exception:  # noqa: BLE001
+            return False
 
     def fits(self, nbytes: int) -> bool:
         return nbytes % 16 == 0 and nbytes <= self.cap
@@ -54,8 +111,8 @@ class CustomAllReduce:
         if t.dtype != torch.bfloat16 or not t.is_contiguous():
             raise TypeError("custom all-reduce: contiguous bf16 only")
         nbytes = t.numel() * 2
-        kernels().car_allreduce(self.bases, self.rank, self.world, self.cap, t.data_ptr(), nbytes,
-                                torch.cuda.current_stream(t.device).cuda_stream)
+        stream = torch.cuda.current_stream(t.device).cuda_stream if t.is_cuda else 0
+        kernels().car_allreduce(self.bases, self.rank, self.world, self.cap, t.data_ptr(), nbytes, stream)
         return t
 
     def all_gather(self, x: torch.Tensor, out: torch.Tensor) -> torch.Tensor:
@@ -86,6 +143,8 @@ class CustomAllReduce:
         return h
 
     def close(self) -> None:
+        if not self.own and not self._opened:
+            return
         k = kernels()
         for p in self._opened:
             try:

@@ -123,3 +123,85 @@ def test_sp_ep_match_tp1(name, ekw):
     top2 = torch.topk(ref_logits, 2).values
     if (top2[0] - top2[1]).item() > 0.05:
         assert gen[0] == ref_gen[0]
+
+
+class _FakeCarKernels:
+    """Stand-in for the HIP module: mapping succeeds or fails per rank, and the all-reduce
+    writes the right sum only where told to (exercises the group agreement, not the kernel)."""
+
+    def __init__(self, rank, fail_open_rank=-1, correct_ranks=()):
+        self.rank, self.fail_open_rank, self.correct = rank, fail_open_rank, set(correct_ranks)
+
+    def car_alloc(self, cap):
+        return 4096 * (self.rank + 1)
+
+    def ipc_handle(self, p):
+        return bytes([self.rank]) * 64
+
+    def ipc_open(self, h):
+        if self.rank == self.fail_open_rank:
+            raise RuntimeError("ipc_open: invalid argument")
+        return 1 << 20
+
+    def ipc_close(self, p):
+        pass
+
+    def car_free(self, p):
+        pass
+
+    def car_timed_out(self, own):
+        return 0
+
+    def car_allreduce(self, bases, rank, world, cap, ptr, nbytes, stream):
+        import ctypes
+
+        if rank in self.correct:
+            want = torch.full((nbytes // 2,), float(world * (world + 1) // 2), dtype=torch.bfloat16)
+            ctypes.memmove(ptr, want.data_ptr(), nbytes)
+
+
+def _car_agree_worker(rank, world, port, case, q):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        import warnings
+
+        from llm_consensus_amd.parallel import custom_ar
+        from llm_consensus_amd.parallel.comm import TPGroup
+
+        fake = {"open_fails": _FakeCarKernels(rank, fail_open_rank=1, correct_ranks=(0, 1)),
+                "selftest_wrong": _FakeCarKernels(rank, correct_ranks=(0,)),
+                "ok": _FakeCarKernels(rank, correct_ranks=(0, 1))}[case]
+        custom_ar.kernels = lambda: fake
+        tp = TPGroup(dist.group.WORLD, rank, world)
+        with warnings.catch_warnings():
+            warnings.simplefilter("ignore")
+            enabled = tp.enable_custom(torch.device("cpu"))
+        # the group is still in step afterwards: a plain collective gives the right answer
+        t = torch.tensor([rank + 1.0])
+        dist.all_reduce(t)
+        q.put((rank, enabled, tp.custom is None, float(t.item())))
+    except Exception as e:  # noqa: BLE001
+        q.put((rank, repr(e)))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("case,want", [("open_fails", False), ("selftest_wrong", False), ("ok", True)])
+def test_custom_ar_enable_is_collective(case, want):
+    """One rank failing to map a peer (or a self-test sum that is wrong on one rank) disables the
+    custom all-reduce on EVERY rank, with no mismatched collectives: RCCL keeps the group."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    ps = [ctx.Process(target=_car_agree_worker, args=(r, 2, port, case, q)) for r in range(2)]
+    for p in ps:
+        p.start()
+    res = sorted(q.get(timeout=120) for _ in ps)
+    for p in ps:
+        p.join(timeout=60)
+    for r in res:
+        assert len(r) == 4, r
+        _, enabled, custom_none, tot = r
+        assert enabled is want and custom_none is (not want) and tot == 3.0, r

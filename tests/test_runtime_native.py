@@ -80,3 +80,28 @@ def test_runtime_selftest_asan_ubsan(tmp_path):
     r = subprocess.run([exe], capture_output=True, timeout=300, env=env)
     assert r.returncode == 0, r.stderr.decode()[-4000:]
     assert b"runtime selftest ok" in r.stdout
+
+
+def test_runtime_selftest_tsan(tmp_path):
+    """The same selftest under ThreadSanitizer: the 8-thread block-allocator churn must be free
+    of data races (host code only, no GPU)."""
+    import shutil
+    import subprocess
+
+    if shutil.which("g++") is None:
+        pytest.skip("no g++")
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    rt = os.path.join(root, "csrc", "runtime")
+    exe = str(tmp_path / "selftest_tsan")
+    cmd = ["g++", "-std=c++17", "-O1", "-g", "-fsanitize=thread", os.path.join(root, "csrc", "tests", "runtime_selftest.cpp"),
+           os.path.join(rt, "tokenizer.cpp"), os.path.join(rt, "block_allocator.cpp"), os.path.join(rt, "gojson.cpp"),
+           "-pthread", "-o", exe]
+    subprocess.run(cmd, check=True, capture_output=True, timeout=300)
+    env = dict(os.environ)
+    env["TSAN_OPTIONS"] = "halt_on_error=1"
+    r = subprocess.run([exe], capture_output=True, timeout=300, env=env)
+    if r.returncode != 0 and b"unexpected memory mapping" in r.stderr:
+        pytest.skip("ThreadSanitizer cannot map its shadow memory on this kernel (ASLR layout)")
+    assert r.returncode == 0, r.stderr.decode()[-4000:]
+    assert b"ThreadSanitizer" not in r.stderr, r.stderr.decode()[-4000:]
+    assert b"runtime selftest ok" in r.stdout

@@ -1,0 +1,68 @@
+"""Placement solver on the BASELINE.json configs (SURVEY.md §4.2 "Scheduler: placement solver
+unit tests"; rules in llm_consensus_amd/parallel/placement.py). Pure CPU: demands are sized from
+the public architecture shapes, 288 GB of HBM per GPU."""
+
+import pytest
+
+from llm_consensus_amd.parallel.placement import ModelDemand, PlacementError, describe, solve
+
+G = 10**9
+W8B, W70B, WMIX, WPHI = 16 * G, 141 * G, 93 * G, 8 * G  # bf16 weights (GiB -> GB)
+
+
+def test_config2_three_8b_responders_plus_judge_on_four_gpus():
+    ds = [ModelDemand(f"llama-3-8b@{i}", W8B, 2 * G) for i in range(3)]
+    ds.append(ModelDemand("llama-3-8b@judge", W8B, 8 * G, is_judge=True))
+    p = solve(ds, list(range(4)))
+    # one engine per GPU: the responders spread out, the judge takes the free GPU
+    assert sorted(g[0] for g in p.gpus.values()) == [0, 1, 2, 3]
+    assert p.gpus["llama-3-8b@judge"] == [3]
+
+
+def test_config3_eight_responders_judge_time_shares_gpu0():
+    ds = [ModelDemand(f"llama-3-8b@{i}", W8B, 2 * G) for i in range(8)]
+    ds.append(ModelDemand("llama-3-8b@judge", W8B, 10 * G, is_judge=True))
+    p = solve(ds, list(range(8)))
+    assert sorted(p.gpus[f"llama-3-8b@{i}"][0] for i in range(8)) == list(range(8))
+    assert p.gpus["llama-3-8b@judge"] == [0]  # no free GPU: lowest id, own hipStream
+    assert p.models_on(0) == ["llama-3-8b@0", "llama-3-8b@judge"]
+
+
+def test_config4_two_70b_tp4_on_disjoint_halves():
+    ds = [ModelDemand("llama-3-70b@0", W70B, 20 * G, tp=4), ModelDemand("llama-3-70b@1", W70B, 20 * G, tp=4),
+          ModelDemand("llama-3-8b@judge", W8B, 5 * G, is_judge=True)]
+    p = solve(ds, list(range(8)))
+    groups = sorted(p.gpus["llama-3-70b@0"] + p.gpus["llama-3-70b@1"])
+    assert groups == list(range(8))
+    assert {tuple(p.gpus["llama-3-70b@0"]), tuple(p.gpus["llama-3-70b@1"])} == {(0, 1, 2, 3), (4, 5, 6, 7)}
+    assert p.gpus["llama-3-8b@judge"] == [0]  # every GPU busy: spare stream on the lowest
+    assert "llama-3-70b@0->" in describe(p)
+
+
+def test_config5_mixed_fleet_with_70b_tp4_judge():
+    ds = [ModelDemand("mixtral-8x7b", WMIX, 5 * G), ModelDemand("llama-3-8b", W8B, 2 * G),
+          ModelDemand("phi-3-mini", WPHI, 6 * G), ModelDemand("llama-3-70b@judge", W70B, 30 * G, tp=4, is_judge=True)]
+    p = solve(ds, list(range(8)))
+    assert p.gpus["llama-3-70b@judge"] == [0, 1, 2, 3]  # TP groups first, aligned
+    singles = [p.gpus[m][0] for m in ("mixtral-8x7b", "llama-3-8b", "phi-3-mini")]
+    assert len(set(singles)) == 3 and all(g >= 4 for g in singles)  # the free half, one each
+
+
+def test_memory_is_checked_per_gpu():
+    # 70B unsharded (141 GB) + 120 GB of KV does not fit one 288 GB GPU's usable 92 %
+    with pytest.raises(PlacementError, match="no GPU has that free"):
+        solve([ModelDemand("llama-3-70b", W70B, 130 * G)], [0])
+    # fits once it is TP=2 (135.5 GB per GPU)
+    p = solve([ModelDemand("llama-3-70b", W70B, 130 * G, tp=2)], [0, 1])
+    assert p.gpus["llama-3-70b"] == [0, 1]
+    # co-location fills the least-loaded GPU until memory runs out
+    ds = [ModelDemand(f"m{i}", 100 * G, 0) for i in range(5)]
+    with pytest.raises(PlacementError):
+        solve(ds, [0, 1])
+
+
+def test_tp_larger_than_node_and_no_gpus():
+    with pytest.raises(PlacementError, match="tp=8"):
+        solve([ModelDemand("llama-3-70b", W70B, 0, tp=8)], list(range(4)))
+    with pytest.raises(PlacementError, match="no GPUs"):
+        solve([ModelDemand("x", 1, 0)], [])

@@ -1,25 +1,35 @@
 #!/usr/bin/env python3
 """Consensus-round benchmark (BASELINE.json metric: p50 end-to-end consensus latency + aggregate
-output tokens/sec, N-model fan-out), configs 2/3 generalised to N GPUs:
+output tokens/sec, N-model fan-out) for the BASELINE.json configs on N GPUs of one node.
 
-  * one process per GPU (torchrun; RCCL over xGMI for the gather), weak scaling:
-    each GPU hosts ``--models-per-gpu`` Llama-3-8B responders (distinct random-init replicas,
-    ``llama-3-8b@<i>``), so an N-GPU run is an (N x models-per-gpu)-model fan-out;
-  * the Llama-3-8B judge time-shares the responders' GPUs on its own hipStream(s): by default
-    it is tensor-parallel over the first ``--judge-tp`` ranks (auto = every rank whose count
-    divides the judge's heads/vocab), so the judge phase — which the reference's semantics make
-    strictly sequential after the fan-out (cmd/llm-consensus/main.go:132 then :161) — uses the
-    HBM bandwidth of every GPU that just went idle instead of one: TP shards with RCCL for
-    prefill-sized all-reduces and the custom one-shot xGMI all-reduce/all-gather inside the
-    captured decode graphs. ``--judge-tp 1`` keeps it on GPU 0 only (config 3 as written);
-  * one timed step = one full consensus round exactly as ``llm-consensus`` runs it: every
-    responder prefills the prompt and decodes ``--max-tokens`` tokens, the responses are
-    gathered to rank 0, the judge prompt is rendered with the reference template
-    (internal/consensus/judge.go) and the judge prefills it and decodes ``--max-tokens`` tokens
-    (a single response is passed through without a judge call, judge.go:74-79).
+One process per GPU (torchrun; RCCL over xGMI). One timed step = one full consensus round as
+``llm-consensus`` runs it (reference ``internal/runner/runner.go:62-115`` fan-out, then
+``internal/consensus/judge.go:81-104`` judge): every responder prefills the prompt and decodes
+``--max-tokens`` tokens, the responses are gathered, the judge prompt is rendered with the
+reference template and the judge prefills it (header first, incrementally) and
+decodes ``--max-tokens`` tokens.
 
-Reported ``value`` = total generated tokens (responders + judge) per second of wall time over
-the whole job; ``ms_per_step`` = mean end-to-end round latency; p50 is in ``extra``.
+``--config`` presets (the engines named in the JSON ``config.model`` are exactly the ones that run):
+
+* ``fanout`` (default; configs 2/3): ``max(3, N)`` Llama-3-8B responders (distinct random-init
+  replicas ``llama-3-8b@i``) placed round-robin over the N GPUs, plus a Llama-3-8B judge
+  tensor-parallel over the GPUs (``--judge-tp``, auto = largest valid degree <= N) on its own
+  hipStreams beside the responders. N=1: 3 co-located responders + judge (config-2 shape);
+  N=4: 4 responders + TP=4 judge; N=8: config 3 (one responder per GPU, judge shares GPU 0..).
+* ``4``: 2 x Llama-3-70B responders, each TP=N/2 over its half of the node (RCCL + custom xGMI
+  all-reduce), + Llama-3-8B judge. Needs an even N >= 2.
+* ``5``: mixed fleet — Mixtral-8x7B (MoE grouped GEMM) + Llama-3-8B + Phi-3-mini responders, one
+  per GPU, + Llama-3-70B judge TP=4 (long-context prefill). Needs N >= 4.
+
+A config that does not fit N prints ONE JSON line with ``"skipped"`` and ``value`` null — never a
+smaller config under the same name.
+
+``--shapes tiny`` swaps every family for its tiny twin (same code paths; CPU / same-GPU
+rehearsals of the multi-rank flows: ``LLMC_BENCH_DEVICE=cpu`` or ``LLMC_BENCH_SAME_GPU=1`` with
+``LLMC_BENCH_BACKEND=gloo``).
+
+Reported ``value`` = total generated tokens (responders + judge) per second of wall time over the
+whole job (max over ranks); ``ms_per_step`` = mean round latency; p50/p90 are in ``extra``.
 Data: synthetic prompt (seeded synthetic-tokenizer text), random-init weights, bf16.
 """
 
@@ -32,9 +42,14 @@ import statistics
 import sys
 import threading
 import time
+from typing import Dict, List, Optional
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
+
+METRIC = "consensus_aggregate_output_tokens_per_s"
+TINY = {"llama-3-8b": "llama-tiny", "llama-3-70b": "llama-tiny-tp4", "mixtral-8x7b": "mixtral-tiny",
+        "phi-3-mini": "phi3-tiny"}
 
 
 def log(*a):
@@ -42,8 +57,8 @@ def log(*a):
 
 
 def judge_tp_degree(cfg, world: int, requested: int) -> int:
-    """TP degree of the bench judge: ``requested`` if > 0, else the largest t <= min(world, 8)
-    that shards the judge's heads, kv heads, FFN and vocab evenly (8 = custom all-reduce limit)."""
+    """TP degree of the judge: ``requested`` if > 0, else the largest t <= min(world, 8) that
+    shards the judge's heads, kv heads, FFN and vocab evenly (8 = custom all-reduce limit)."""
     if requested > 0:
         return requested
     for t in range(min(world, 8), 0, -1):
@@ -52,19 +67,72 @@ def judge_tp_degree(cfg, world: int, requested: int) -> int:
     return 1
 
 
+def make_plan(args, world: int):
+    """(responders, judge, skip_reason): responders = [{name, family, ranks}], judge likewise.
+    Ranks of a TP engine are consecutive global ranks; rank ranks[0] leads it."""
+    fam = (lambda f: TINY.get(f, f)) if args.shapes == "tiny" else (lambda f: f)
+    from llm_consensus_amd.models.config import FAMILIES
+
+    if args.config == "fanout":
+        n = args.n_models or max(3, world)
+        rf = fam(args.model)
+        resp = [{"name": f"{args.model}@{i}", "family": rf, "ranks": [i % world], "seed": 1000 + i} for i in range(n)]
+        jf = fam(args.judge)
+        jtp = judge_tp_degree(FAMILIES[jf], world, args.judge_tp)
+        judge = {"name": f"{args.judge}@judge", "family": jf, "ranks": list(range(jtp)), "seed": 777}
+        return resp, judge, None
+    if args.config == "4":
+        if world < 2 or world % 2:
+            return None, None, f"config 4 (2 x llama-3-70b TP=N/2 + llama-3-8b judge) needs an even N >= 2, got {world}"
+        half = world // 2
+        rf = fam("llama-3-70b")
+        resp = [{"name": f"llama-3-70b@{i}", "family": rf, "ranks": list(range(i * half, (i + 1) * half)),
+                 "seed": 1000 + i} for i in range(2)]
+        jf = fam("llama-3-8b")
+        jtp = judge_tp_degree(FAMILIES[jf], world, args.judge_tp)
+        return resp, {"name": "llama-3-8b@judge", "family": jf, "ranks": list(range(jtp)), "seed": 777}, None
+    if args.config == "5":
+        if world < 4:
+            return None, None, f"config 5 (mixed fleet + llama-3-70b TP=4 judge) needs N >= 4, got {world}"
+        fleet = ["mixtral-8x7b", "llama-3-8b", "phi-3-mini"]
+        resp = [{"name": f"{m}@0", "family": fam(m), "ranks": [i % world], "seed": 1000 + i} for i, m in enumerate(fleet)]
+        jtp = args.judge_tp or 4
+        # the 70B judge shards over the last 4 GPUs (off the responders' GPUs when N >= 7)
+        return resp, {"name": "llama-3-70b@judge", "family": fam("llama-3-70b"),
+                      "ranks": list(range(world - jtp, world)), "seed": 777}, None
+    raise SystemExit(f"unknown --config {args.config}")
+
+
+def describe(resp, judge) -> str:
+    def one(e):
+        tp = len(e["ranks"])
+        return e["family"] + (f" TP={tp}" if tp > 1 else "")
+
+    counts: Dict[str, int] = {}
+    for e in resp:
+        counts[one(e)] = counts.get(one(e), 0) + 1
+    rs = " + ".join(f"{n}x {k}" for k, n in counts.items())
+    j = one(judge)
+    jr = judge["ranks"]
+    where = f"GPU {jr[0]}" if len(jr) == 1 else f"GPUs {jr[0]}-{jr[-1]}"
+    return f"{rs} responders + {j} judge on {where} (own streams)"
+
+
 def main() -> None:
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--warmup", type=int, default=1)
-    ap.add_argument("--model", default="llama-3-8b")
-    ap.add_argument("--judge", default="llama-3-8b")
-    ap.add_argument("--models-per-gpu", type=int, default=1)
+    ap.add_argument("--config", default="fanout", choices=["fanout", "4", "5"])
+    ap.add_argument("--shapes", default="full", choices=["full", "tiny"])
+    ap.add_argument("--model", default="llama-3-8b", help="fanout: responder family")
+    ap.add_argument("--judge", default="llama-3-8b", help="fanout: judge family")
+    ap.add_argument("--n-models", type=int, default=0, help="fanout: responders (0 = max(3, N))")
     ap.add_argument("--max-tokens", type=int, default=4096)
     ap.add_argument("--judge-max-tokens", type=int, default=0, help="0 = same as --max-tokens")
     ap.add_argument("--prompt-tokens", type=int, default=128)
     ap.add_argument("--temperature", type=float, default=1.0)
-    ap.add_argument("--judge-tp", type=int, default=0, help="0 = auto (largest valid TP <= ranks), 1 = GPU 0 only")
+    ap.add_argument("--judge-tp", type=int, default=0, help="0 = auto (config 5: 4)")
     ap.add_argument("--steps-per-graph", type=int, default=8)
     ap.add_argument("--no-graphs", action="store_true")
     ap.add_argument("--results-dir", default=os.path.join(ROOT, "bench", "results"),
@@ -80,13 +148,34 @@ def main() -> None:
     if world != args.gpus:
         log(f"warning: --gpus {args.gpus} but WORLD_SIZE {world}; using WORLD_SIZE")
     n_gpus = world
-    # rehearsal mode for the multi-rank flow on a 1-GPU box: every rank on cuda:0, gloo collectives
-    # (LLMC_BENCH_BACKEND=gloo LLMC_BENCH_SAME_GPU=1); the driver's runs use RCCL, one GPU per rank
-    backend = os.environ.get("LLMC_BENCH_BACKEND", "nccl")
-    gpu = 0 if os.environ.get("LLMC_BENCH_SAME_GPU") == "1" else local
-    torch.cuda.set_device(gpu)
-    dev = f"cuda:{gpu}"
+
+    resp_plan, judge_plan, skip = make_plan(args, world)
+    if skip is not None:
+        if rank == 0:
+            print(json.dumps({"metric": METRIC, "value": None, "unit": "tokens/s", "n_gpus": n_gpus,
+                              "steps": args.steps, "warmup": args.warmup, "ms_per_step": None,
+                              "higher_is_better": True, "scaling": "strong", "vs_baseline": None, "dtype": "bf16",
+                              "data": "synthetic", "skipped": skip,
+                              "config": {"model": f"config {args.config}", "parallelism": "n/a"}}), flush=True)
+        return
+
+    # rehearsal modes for the multi-rank flow: every rank on cuda:0 (LLMC_BENCH_SAME_GPU=1) or on
+    # the CPU (LLMC_BENCH_DEVICE=cpu), gloo collectives (LLMC_BENCH_BACKEND=gloo); the driver's
+    # runs use RCCL, one GPU per rank
+    on_cpu = os.environ.get("LLMC_BENCH_DEVICE") == "cpu"
+    backend = "gloo" if on_cpu else os.environ.get("LLMC_BENCH_BACKEND", "nccl")
+    if on_cpu:
+        dev = "cpu"
+    else:
+        gpu = 0 if os.environ.get("LLMC_BENCH_SAME_GPU") == "1" else local
+        torch.cuda.set_device(gpu)
+        dev = f"cuda:{gpu}"
     cdev = dev if backend == "nccl" else "cpu"  # where collective buffers live
+
+    def sync():
+        if not on_cpu:
+            torch.cuda.synchronize()
+
     if world > 1:
         if backend == "nccl":
             dist.init_process_group("nccl", device_id=torch.device(dev))
@@ -96,68 +185,74 @@ def main() -> None:
     from llm_consensus_amd.consensus import build_judge_prompt, prompt_header
     from llm_consensus_amd.engine import Engine, EngineConfig, SamplingParams
     from llm_consensus_amd.models.config import FAMILIES
+    from llm_consensus_amd.parallel.comm import TPGroup
     from llm_consensus_amd.provider.base import Response
     from llm_consensus_amd.utils.tokenizer import get_tokenizer
 
-    rcfg = FAMILIES[args.model]
-    jcfg = FAMILIES[args.judge]
-    mpg = args.models_per_gpu
-    n_models = n_gpus * mpg
+    jcfg = FAMILIES[judge_plan["family"]]
     jmax = args.judge_max_tokens or args.max_tokens
-    tok = get_tokenizer(rcfg.vocab)
     jtok = get_tokenizer(jcfg.vocab)
+    n_resp = len(resp_plan)
 
     # synthetic prompt: seeded piece ids -> text (identical on every rank)
+    ptok = get_tokenizer(FAMILIES[resp_plan[0]["family"]].vocab)
     g = torch.Generator().manual_seed(1234)
-    pids = torch.randint(256, 256 + 60000, (args.prompt_tokens,), generator=g).tolist()
-    prompt_text = tok.decode(pids).strip()
-    prompt_ids = tok.encode(prompt_text, add_bos=True)
+    lo = 256
+    pids = torch.randint(lo, min(lo + 60000, ptok.vocab_size - 2), (args.prompt_tokens,), generator=g).tolist()
+    prompt_text = ptok.decode(pids).strip()
 
-    resp_ctx = len(prompt_ids) + args.max_tokens + 64
+    def tp_group(ranks: List[int]):
+        """Collective over the world (dist.new_group): every rank calls it for every TP engine in
+        plan order; returns this rank's TPGroup or None when it is not a member."""
+        if len(ranks) == 1:
+            return TPGroup.single() if rank == ranks[0] else None
+        grp = dist.group.WORLD if len(ranks) == world else dist.new_group(ranks)
+        if rank not in ranks:
+            return None
+        tp = TPGroup(grp, ranks.index(rank), len(ranks))
+        if not on_cpu:
+            # collective over the group: every member agrees on the outcome (peer mapping + a
+            # self-test); on failure the group stays on RCCL (same-GPU rehearsals: gloo)
+            tp.enable_custom(dev)
+        return tp
+
     t0 = time.time()
-    responders = []
-    for j in range(mpg):
-        idx = rank * mpg + j
-        e = Engine(rcfg, EngineConfig(device=dev, max_context=resp_ctx, seed=1000 + idx,
-                                      steps_per_graph=args.steps_per_graph, use_graphs=not args.no_graphs),
-                   name=f"{args.model}@{idx}")
-        responders.append((idx, e))
+    responders = []  # (index, engine, prompt ids, tokenizer)
+    for i, e in enumerate(resp_plan):
+        tp = tp_group(e["ranks"])
+        if tp is None:
+            continue
+        cfg = FAMILIES[e["family"]]
+        tok = get_tokenizer(cfg.vocab)
+        ids = tok.encode(prompt_text, add_bos=True)
+        ctx = len(ids) + args.max_tokens + 64
+        graphs = not args.no_graphs and (tp.size == 1 or tp.custom is not None)
+        eng = Engine(cfg, EngineConfig(device=dev, max_context=ctx, seed=e["seed"], steps_per_graph=args.steps_per_graph,
+                                       use_graphs=graphs), tp=tp, name=e["name"])
+        responders.append((i, eng, ids, tok))
+    jtp_grp = tp_group(judge_plan["ranks"])
     judge = None
     judge_ctx = 0
-    jtp = judge_tp_degree(jcfg, world, args.judge_tp) if n_models > 1 else 1
-    from llm_consensus_amd.parallel.comm import TPGroup
-
-    tp = TPGroup.single()
-    if jtp > 1:
-        # judge TP group = ranks 0..jtp-1 (the whole world by default); new_group is collective
-        grp = dist.group.WORLD if jtp == world else dist.new_group(list(range(jtp)))
-        ok = 1
-        if rank < jtp:
-            tp = TPGroup(grp, rank, jtp)
-            # collective: every judge rank agrees on the outcome (peer mapping + a self-test)
-            if not tp.enable_custom(dev):
-                log("custom all-reduce unavailable; judge falls back to TP=1 on GPU 0")
-                ok = 0
-        flag = torch.tensor([ok], dtype=torch.int32, device=cdev)
-        dist.all_reduce(flag, op=dist.ReduceOp.MIN)
-        if int(flag.item()) == 0:
-            jtp, tp = 1, TPGroup.single()
-    if n_models > 1 and rank < jtp:
-        # responses are decoded to text and re-tokenized by the judge: random byte tokens can expand
-        # (invalid UTF-8 -> U+FFFD -> 3 byte tokens), so budget 2x per response
-        judge_ctx = len(prompt_ids) + 1024 + n_models * (2 * args.max_tokens + 64) + jmax + 64
-        judge = Engine(jcfg, EngineConfig(device=dev, max_context=judge_ctx, seed=777,
-                                          steps_per_graph=args.steps_per_graph, use_graphs=not args.no_graphs),
-                       tp=tp, name=f"{args.judge}@judge")
+    if jtp_grp is not None:
+        # responses are decoded to text and re-tokenized by the judge: random byte tokens can
+        # expand (invalid UTF-8 -> U+FFFD -> 3 byte tokens), so budget 2x per response
+        fixed = len(jtok.encode(build_judge_prompt(prompt_text, []), add_bos=True))
+        judge_ctx = min(jcfg.max_position, fixed + n_resp * (2 * args.max_tokens + 64) + jmax + 64)
+        graphs = not args.no_graphs and (jtp_grp.size == 1 or jtp_grp.custom is not None)
+        judge = Engine(jcfg, EngineConfig(device=dev, max_context=judge_ctx, seed=judge_plan["seed"],
+                                          steps_per_graph=args.steps_per_graph, use_graphs=graphs),
+                       tp=jtp_grp, name=judge_plan["name"])
     # capture every decode graph up front (a capture beside another engine's running stream is
     # invalid; the worker process does the same before serving)
-    if not args.no_graphs:
-        for _, e in responders:
-            e.warmup_graphs()
-        if judge is not None:
-            judge.warmup_graphs()
-    torch.cuda.synchronize()
-    log(f"engines ready in {time.time() - t0:.1f}s (responders {mpg}/gpu, judge ctx {judge_ctx})")
+    for _, e, _, _ in responders:
+        e.warmup_graphs()
+    if judge is not None:
+        judge.warmup_graphs()
+    sync()
+    if world > 1:
+        dist.barrier()
+    log(f"engines ready in {time.time() - t0:.1f}s: {[e.name for _, e, _, _ in responders]}"
+        + (f" + {judge.name} (TP={judge.tp.size}, ctx {judge_ctx})" if judge else ""))
 
     def one_round(step: int):
         stats = {}
@@ -168,75 +263,81 @@ def main() -> None:
             jseq = judge.new_sequence()
             judge.prefill([jseq], [jtok.encode(prompt_header(prompt_text), add_bos=True)], want_logits=False)
         # co-located responders decode concurrently, one engine thread + hipStream each (as the
-        # CLI's worker runs them)
-        outs = [None] * len(responders)
+        # CLI's worker runs them); TP engines run in lockstep on every rank of their group
+        outs: Dict[int, List[int]] = {}
+        errs = []
 
         def run_one(j):
-            idx, e = responders[j]
-            outs[j] = e.generate_ids(prompt_ids, args.max_tokens, temperature=args.temperature,
-                                     seed=1000 * step + idx + 1, stop_on_eos=False)
+            try:
+                i, e, ids, _ = responders[j]
+                outs[i] = e.generate_ids(ids, args.max_tokens, temperature=args.temperature,
+                                         seed=1000 * step + i + 1, stop_on_eos=False)
+            except BaseException as ex:  # noqa: BLE001
+                errs.append(ex)
 
-        if len(responders) == 1:
-            run_one(0)
-        else:
-            ths = [threading.Thread(target=run_one, args=(j,)) for j in range(len(responders))]
-            for t in ths:
-                t.start()
-            for t in ths:
-                t.join()
+        ths = [threading.Thread(target=run_one, args=(j,)) for j in range(len(responders))]
+        for t in ths:
+            t.start()
+        for t in ths:
+            t.join()
+        if errs:
+            raise errs[0]
         t_resp = time.perf_counter()
         if rank == 0:
             log(f"round {step}: responders done in {t_resp - t_start:.2f}s")
-        # gather responses to rank 0 (fixed-size int32 rows; RCCL over xGMI)
-        local_t = torch.full((mpg, args.max_tokens), -1, dtype=torch.int32, device=dev)
-        for j, ids in enumerate(outs):
-            local_t[j, : len(ids)] = torch.tensor(ids, dtype=torch.int32, device=dev)
+        # gather every response to every rank: the leader of each responder writes its row
+        # (token + 1; 0 = empty) and one SUM all-reduce assembles the table
+        table = torch.zeros((n_resp, args.max_tokens), dtype=torch.int32)
+        for i, e, _, _ in responders:
+            if e.tp.is_leader:
+                r = torch.tensor(outs[i], dtype=torch.int32) + 1
+                table[i, : r.numel()] = r
         if world > 1:
-            all_t = torch.empty((world, mpg, args.max_tokens), dtype=torch.int32, device=cdev)
-            dist.all_gather_into_tensor(all_t.view(world * mpg, args.max_tokens), local_t.to(cdev))
-        else:
-            all_t = local_t.unsqueeze(0)
-        n_tokens = n_models * args.max_tokens
+            tt = table.to(cdev)
+            dist.all_reduce(tt)
+            table = tt.cpu()
+        n_tokens = n_resp * args.max_tokens
         if judge is not None:
             # every judge rank renders the same prompt from the gathered rows (deterministic), so
-            # the TP shards prefill/decode in lockstep; rank 0 accounts the tokens
-            rows = all_t.view(n_models, args.max_tokens).cpu().tolist()
+            # the TP shards prefill/decode in lockstep; rank 0 accounts the judge tokens
             responses = []
-            for i, r in enumerate(rows):
-                r = [t for t in r if t >= 0]
-                responses.append(Response(model=f"{args.model}@{i}", content=tok.decode(r), provider="rocm"))
+            for i, e in enumerate(resp_plan):
+                r = [t - 1 for t in table[i].tolist() if t > 0]
+                rtok = get_tokenizer(FAMILIES[e["family"]].vocab)
+                responses.append(Response(model=e["name"], content=rtok.decode(r), provider="rocm"))
             full = build_judge_prompt(prompt_text, responses)
             head = prompt_header(prompt_text)
             rest_ids = jtok.encode(full[len(head):])
             judge.prefill([jseq], [rest_ids])
+            sync()
             t_jp = time.perf_counter()
             if rank == 0:
-                log(f"round {step}: judge prefill of {len(rest_ids)} tokens in {t_jp - t_resp:.2f}s (TP={jtp})")
+                log(f"round {step}: judge prefill of {len(rest_ids)} tokens in {t_jp - t_resp:.2f}s (TP={judge.tp.size})")
             jids = judge.decode([jseq], [SamplingParams(jmax, args.temperature, 1.0, 0, 99 + step, False)])[0]
             stats["judge_prompt_tokens"] = jseq.length - len(jids)
             stats["judge_prefill_s"] = t_jp - t_resp
             stats["judge_decode_s"] = time.perf_counter() - t_jp
-            if rank == 0:
-                n_tokens += len(jids)
+            if judge.tp.is_leader:
+                stats["judge_tokens"] = len(jids)
             judge.free_sequence(jseq)
             if judge.tp.custom is not None and judge.tp.custom.timed_out():
-                log("WARNING: a custom all-reduce spin timed out (a peer stalled); judge tokens are suspect")
-        torch.cuda.synchronize()
+                raise RuntimeError("a custom all-reduce spin timed out (a peer stalled): judge tokens are invalid")
+        sync()
         if world > 1:
             dist.barrier()
         t_end = time.perf_counter()
         stats["responders_s"] = t_resp - t_start
         stats["e2e_s"] = t_end - t_start
-        stats["tokens"] = n_tokens
+        stats["tokens"] = n_tokens + (jmax if judge_plan else 0)
         return stats
 
     for w in range(args.warmup):
         st = one_round(w)
         log(f"warmup {w}: {st}")
 
+    sync()
     if world > 1:
         dist.barrier()
-    torch.cuda.synchronize()
     lat = []
     tot_tokens = 0
     t0 = time.perf_counter()
@@ -247,19 +348,29 @@ def main() -> None:
         tot_tokens += st["tokens"]
         per_step.append(st)
         log(f"step {s}: {st}")
-    torch.cuda.synchronize()
+    sync()
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
+    judge_stats = per_step[-1] if per_step else {}
     if world > 1:
         tt = torch.tensor([elapsed], dtype=torch.float64, device=cdev)
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         elapsed = float(tt.item())
+        # judge timings live on the judge's ranks: rank 0 is not one of them in config 5 at N > 4
+        jt = torch.tensor([judge_stats.get(k, 0.0) for k in ("judge_prompt_tokens", "judge_prefill_s",
+                                                             "judge_decode_s")], dtype=torch.float64, device=cdev)
+        dist.all_reduce(jt, op=dist.ReduceOp.MAX)
+        judge_stats = dict(judge_stats, judge_prompt_tokens=int(jt[0].item()), judge_prefill_s=float(jt[1].item()),
+                           judge_decode_s=float(jt[2].item()))
     if rank == 0:
         value = tot_tokens / elapsed
-        resp_tok_s = n_models * args.max_tokens * args.steps / sum(p["responders_s"] for p in per_step)
+        resp_tok_s = n_resp * args.max_tokens * args.steps / sum(p["responders_s"] for p in per_step)
+        jtp = len(judge_plan["ranks"])
+        par = {"fanout": f"fanout{n_resp}", "4": f"fanout2-tp{len(resp_plan[0]['ranks'])}",
+               "5": "fanout3-mixed"}[args.config]
         out = {
-            "metric": "consensus_aggregate_output_tokens_per_s",
+            "metric": METRIC,
             "value": round(value, 2),
             "unit": "tokens/s",
             "n_gpus": n_gpus,
@@ -267,34 +378,38 @@ def main() -> None:
             "warmup": args.warmup,
             "ms_per_step": round(1000 * elapsed / args.steps, 2),
             "higher_is_better": True,
-            "scaling": "weak",
+            # fanout: responders grow with N (one per GPU from N=3); configs 4/5 fix the fleet
+            "scaling": "weak" if args.config == "fanout" else "strong",
             "vs_baseline": None,
             "dtype": "bf16",
             "data": "synthetic prompt (synthetic tokenizer), random-init weights",
             "config": {
-                "model": f"{n_models}x {args.model} responders ({mpg}/GPU) + {args.judge} judge "
-                         + (f"TP={jtp} on GPUs 0-{jtp - 1} (own streams)" if jtp > 1 else "on GPU0 stream"),
-                "global_batch": n_models,
-                "seq_len": len(prompt_ids) + args.max_tokens,
+                "name": {"fanout": "fanout (BASELINE configs 2/3)", "4": "BASELINE config 4",
+                         "5": "BASELINE config 5"}[args.config],
+                "model": describe(resp_plan, judge_plan),
+                "global_batch": n_resp,
+                "seq_len": args.prompt_tokens + args.max_tokens,
                 "max_tokens": args.max_tokens,
-                "prompt_tokens": len(prompt_ids),
-                "parallelism": f"fanout{n_models}" + ("" if n_gpus == 1 else f"-dp{n_gpus}")
-                               + (f"-judge_tp{jtp}" if jtp > 1 else ""),
+                "prompt_tokens": args.prompt_tokens,
+                "parallelism": par + ("" if n_gpus == 1 else f"-over{n_gpus}gpus") + (f"-judge_tp{jtp}" if jtp > 1 else ""),
             },
             "extra": {
                 "p50_e2e_latency_s": round(statistics.median(lat), 3),
-                "responder_decode_tok_s_per_model": round(resp_tok_s / n_models, 2),
-                "judge_prompt_tokens": per_step[-1].get("judge_prompt_tokens", 0),
-                "judge_prefill_s": round(per_step[-1].get("judge_prefill_s", 0.0), 3),
-                "judge_decode_s": round(per_step[-1].get("judge_decode_s", 0.0), 3),
+                "p90_e2e_latency_s": round(sorted(lat)[min(len(lat) - 1, int(0.9 * len(lat)))], 3),
+                "responders_s": round(statistics.median(p["responders_s"] for p in per_step), 3),
+                "responder_decode_tok_s_per_model": round(resp_tok_s / n_resp, 2),
+                "judge_prompt_tokens": judge_stats.get("judge_prompt_tokens", 0),
+                "judge_prefill_s": round(judge_stats.get("judge_prefill_s", 0.0), 3),
+                "judge_decode_s": round(judge_stats.get("judge_decode_s", 0.0), 3),
                 "judge_tp": jtp,
+                "custom_allreduce": {e.name: e.tp.custom is not None for _, e, _, _ in responders if e.tp.size > 1}
+                | ({judge.name: judge.tp.custom is not None} if judge is not None and judge.tp.size > 1 else {}),
             },
         }
         print(json.dumps(out), flush=True)
         if args.results_dir:
-            srt = sorted(lat)
-            rec = dict(out, per_step=per_step, p90_e2e_latency_s=round(srt[min(len(srt) - 1, int(0.9 * len(srt)))], 3),
-                       time_utc=time.strftime("%Y%m%dT%H%M%SZ", time.gmtime()), argv=sys.argv[1:])
+            rec = dict(out, per_step=per_step, time_utc=time.strftime("%Y%m%dT%H%M%SZ", time.gmtime()),
+                       argv=sys.argv[1:])
             try:
                 os.makedirs(args.results_dir, exist_ok=True)
                 fn = os.path.join(args.results_dir, f"bench_{rec['time_utc']}_n{n_gpus}.json")

@@ -108,9 +108,12 @@ LLAMA_SMALL = ModelConfig("llama-small", "llama", 4, 1024, 8, 2, 128, 2816, 3200
 MIXTRAL_TINY = ModelConfig("mixtral-tiny", "mixtral", 2, 256, 4, 2, 64, 384, 1024, 1000000.0,
                            max_position=4096, n_experts=4, top_k_experts=2)
 PHI3_TINY = ModelConfig("phi3-tiny", "phi3", 2, 192, 2, 2, 96, 384, 1024, 10000.0, max_position=4096)
+# tiny stand-in for Llama-3-70B in TP=4 rehearsals (heads, kv heads, FFN and vocab shard over 4)
+LLAMA_TINY_TP4 = ModelConfig("llama-tiny-tp4", "llama", 2, 512, 8, 4, 64, 1024, 1024, 500000.0, max_position=16384,
+                             default_tp=4)
 
 FAMILIES = {c.name: c for c in (LLAMA3_8B, LLAMA3_70B, MIXTRAL_8X7B, PHI3_MINI,
-                                LLAMA_TINY, LLAMA_SMALL, MIXTRAL_TINY, PHI3_TINY)}
+                                LLAMA_TINY, LLAMA_SMALL, MIXTRAL_TINY, PHI3_TINY, LLAMA_TINY_TP4)}
 
 
 def rope_inv_freq(cfg: ModelConfig):

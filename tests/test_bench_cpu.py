@@ -1,0 +1,55 @@
+"""bench.py multi-rank flows on CPU ranks (gloo, oracle ops, tiny shapes): the fan-out with a TP
+judge, config 4 (two TP=2 responder groups + judge) and config 5 (mixed Mixtral/Llama/Phi-3 fleet +
+TP=4 judge), and the explicit "skipped" record of a config that does not fit the GPU count."""
+
+import json
+import os
+import subprocess
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "tests"))
+
+
+def _run(n, args, port):
+    env = dict(os.environ, LLMC_BENCH_DEVICE="cpu", OMP_NUM_THREADS="1")
+    cmd = ([sys.executable, "bench.py"] if n == 1 else
+           [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", str(n), "--master-addr",
+            "127.0.0.1", "--master-port", str(port), "bench.py", "--gpus", str(n)])
+    r = subprocess.run(cmd + args + ["--results-dir", ""], cwd=ROOT, capture_output=True, timeout=600, env=env)
+    assert r.returncode == 0, r.stderr.decode()[-3000:]
+    lines = [ln for ln in r.stdout.decode().splitlines() if ln.strip().startswith("{")]
+    assert len(lines) == 1
+    return json.loads(lines[0])
+
+
+def _tokens_ok(d, max_tokens):
+    tokens = (d["config"]["global_batch"] + 1) * max_tokens
+    assert abs(d["value"] - tokens / (d["ms_per_step"] / 1000)) < 0.02 * d["value"]
+    assert d["extra"]["judge_prompt_tokens"] > 0 and d["extra"]["judge_decode_s"] > 0
+
+
+def test_fanout_one_rank_runs_judge():
+    d = _run(1, ["--shapes", "tiny", "--steps", "1", "--warmup", "0", "--max-tokens", "12"], 0)
+    assert d["config"]["global_batch"] == 3 and d["scaling"] == "weak"
+    _tokens_ok(d, 12)
+
+
+def test_config4_two_tp_groups():
+    d = _run(4, ["--config", "4", "--shapes", "tiny", "--steps", "1", "--warmup", "0", "--max-tokens", "12"], 29691)
+    assert d["config"]["name"] == "BASELINE config 4" and d["scaling"] == "strong"
+    assert d["config"]["model"].startswith("2x llama-tiny-tp4 TP=2 responders")
+    _tokens_ok(d, 12)
+
+
+def test_config5_mixed_fleet_tp4_judge():
+    d = _run(4, ["--config", "5", "--shapes", "tiny", "--steps", "1", "--warmup", "0", "--max-tokens", "12"], 29692)
+    assert "mixtral-tiny" in d["config"]["model"] and "phi3-tiny" in d["config"]["model"]
+    assert d["extra"]["judge_tp"] == 4
+    _tokens_ok(d, 12)
+
+
+def test_config_too_big_is_skipped_not_shrunk():
+    for cfg in ("4", "5"):
+        d = _run(1, ["--config", cfg, "--steps", "1", "--warmup", "0"], 0)
+        assert d["value"] is None and "needs" in d["skipped"]

@@ -57,6 +57,11 @@ int llmc_ipc_handle_size();
 int llmc_ipc_open(const void*, void**);
 int llmc_ipc_close(void*);
 int llmc_car_timed_out(void*, int*);
+size_t llmc_car_timeout_off();
+size_t llmc_gemv_ar_timeout_off();
+int llmc_car_reset(void*);
+int llmc_can_access_peer(int, int, int*);
+int llmc_car_twoshot(const void* const*, int, int, size_t, int, const void*, void*, long, int, int, hipStream_t);
 int llmc_car_allreduce(const void* const*, int, int, size_t, void*, size_t, hipStream_t);
 int llmc_car_allgather(const void* const*, int, int, size_t, const void*, void*, size_t, hipStream_t);
 }
@@ -184,6 +189,20 @@ PYBIND11_MODULE(_llmc_hip, m) {
     int v = 0;
     check(llmc_car_timed_out(P(own), &v), "car_timed_out");
     return v;
+  });
+  m.def("car_timeout_off", []() { return llmc_car_timeout_off(); });
+  m.def("gemv_ar_timeout_off", []() { return llmc_gemv_ar_timeout_off(); });
+  m.def("car_reset", [](ptr own) { check(llmc_car_reset(P(own)), "car_reset"); });
+  m.def("can_access_peer", [](int dev, int peer) {
+    int v = 0;
+    check(llmc_can_access_peer(dev, peer, &v), "can_access_peer");
+    return v;
+  });
+  m.def("car_twoshot", [](const std::vector<ptr>& bases, int rank, int world, size_t cap, int mode, ptr in, ptr out,
+                          long seg_stride, int seg16, int nv, ptr s) {
+    std::vector<const void*> b(bases.size());
+    for (size_t i = 0; i < bases.size(); ++i) b[i] = P(bases[i]);
+    check(llmc_car_twoshot(b.data(), rank, world, cap, mode, P(in), P(out), seg_stride, seg16, nv, S(s)), "car_twoshot");
   });
   m.def("car_allreduce", [](const std::vector<ptr>& bases, int rank, int world, size_t cap, ptr x, size_t nbytes,
                             ptr s) {

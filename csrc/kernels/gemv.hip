@@ -182,6 +182,8 @@ static int moe_gemv_geom(int npairs, const void* x, int x_stride, const void* nw
 // the TP group of x_rank @ W_rank^T (+ residual, folded by rank 0). 16-wave blocks, one row per
 // wave; the grid must be resident at once (checked: <= 256 blocks, one per CU), and every rank launches
 // the same shape. bases: every rank's fused-AR buffer (kArSigBytes + 2 * cap).
+extern "C" size_t llmc_gemv_ar_timeout_off() { return kArTimeoutOff; }
+
 extern "C" int llmc_gemv_rowpar_ar(int M, const void* x, int x_stride, const void* W, void* h, int h_stride, int N,
                                    int K, const void* const* bases, int rank, int world, long cap, hipStream_t s) {
   constexpr int NT = 1024, WAVES = NT / kWave;

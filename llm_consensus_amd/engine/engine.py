@@ -395,10 +395,6 @@ class Engine:
 
     def _row_parallel(self, x: torch.Tensor, W: torch.Tensor, h: torch.Tensor) -> None:
         """h += x @ W^T across the TP group (residual folded into rank 0's partial)."""
-        rp = self.tp.rowpar
-        if rp is not None and x.is_cuda and x.shape[0] <= ops.GEMV_MAX_M and W.shape[0] <= 4096:
-            rp.gemv_rowpar_ar(x, W, h)  # decode: the all-reduce runs in the GEMV's epilogue
-            return
         ops.linear(x, W, EPI_RESADD if self.tp.rank == 0 else EPI_BF16, out=h)
         self.tp.all_reduce_(h)
 
@@ -708,23 +704,30 @@ class Engine:
                     consume(self.out_count, self.out_tokens)
                     if all(done):
                         break
-                    if ctx is not None:
-                        ctx.check()
+                    if self._stop_requested(ctx):
+                        raise ContextError(self._stop_reason(ctx))
                     self._decode_step(B)
+                self._check_collectives()
                 self._finish(seqs, results)
                 return results
 
             base_len = max(s.length for s in seqs)
             pending_ev: Optional[torch.cuda.Event] = None
 
-            def launch_copy():
-                self.host_count.copy_(self.out_count, non_blocking=True)
-                self.host_tokens.copy_(self.out_tokens, non_blocking=True)
+            def launch_copy(upto: int):
+                # only the token window produced since the last snapshot travels (columns
+                # [lo, upto) of every row; earlier columns are already in the host copy)
+                lo = min(produced) if produced else 0
+                hi = min(self.cap, upto)
+                self.host_count[:B].copy_(self.out_count[:B], non_blocking=True)
+                if hi > lo:  # per row: contiguous spans, so the copies stay asynchronous
+                    for r in range(B):
+                        self.host_tokens[r, lo:hi].copy_(self.out_tokens[r, lo:hi], non_blocking=True)
                 ev = torch.cuda.Event()
                 ev.record(self.stream)
                 return ev
 
-            pending_ev = launch_copy()
+            pending_ev = launch_copy(issued)
             while True:
                 need_more = issued < max_new
                 if need_more:
@@ -742,17 +745,41 @@ class Engine:
                 consume(self.host_count, self.host_tokens)
                 if all(done):
                     break
-                if ctx is not None and ctx.done():
+                # every TP rank takes this decision identically (the leader's), at the same
+                # replay: one rank running an extra replay would desynchronise the collectives
+                if self._stop_requested(ctx):
                     self.stream.synchronize()
-                    raise ContextError(ctx.err())
-                pending_ev = launch_copy()
+                    self._check_collectives()
+                    raise ContextError(self._stop_reason(ctx))
+                pending_ev = launch_copy(issued)
                 if not need_more:
                     pending_ev.synchronize()
                     consume(self.host_count, self.host_tokens)
                     break
             self.stream.synchronize()
+            self._check_collectives()
             self._finish(seqs, results)
             return results
+
+    # -- TP control plane -------------------------------------------------------------------------
+    def _stop_requested(self, ctx: Optional[Context]) -> bool:
+        """Cancellation / deadline between replays. Under TP with a control group the TP leader's
+        context decides for every rank (a follower's own cancel arrives at its own time)."""
+        local = ctx is not None and ctx.done()
+        if self.tp.size > 1 and self.tp.ctrl is not None:
+            return bool(self.tp.leader_decides(int(local)))
+        return local
+
+    @staticmethod
+    def _stop_reason(ctx: Optional[Context]) -> str:
+        return (ctx.err() if ctx is not None else None) or "context canceled"
+
+    def _check_collectives(self) -> None:
+        """TP engines with a control group: fail the request (on every rank) if a custom-collective
+        spin timed out since the last check; the group re-synchronises its protocol state first, so
+        the next request runs on consistent epochs."""
+        if self.tp.size > 1 and self.tp.ctrl is not None and not self.tp.check_collectives():
+            raise EngineError("custom all-reduce timed out (a TP peer stalled): this request's tokens are invalid")
 
     def _finish(self, seqs, results) -> None:
         for s, r in zip(seqs, results):

@@ -6,10 +6,17 @@ trick: rank 0 adds its partial product onto the residual stream, the other ranks
 partial product into the same buffer, and ONE in-place all-reduce yields
 ``h + sum_r partial_r`` — no separate residual-add kernel and no extra buffer per layer.
 
-On GPUs the decode-sized collectives go through the custom one-shot xGMI kernels
-(``custom_ar.py``, K13) once ``enable_custom()`` has mapped the peers: no RCCL call and no host
-work per collective, so a TP engine's decode step is capturable in one HIP graph. Larger messages
-(prefill) and CPU/gloo groups use torch.distributed.
+On GPUs the collectives go through the custom xGMI kernels (``custom_ar.py``, K13) once
+``enable_custom()`` has mapped the peers: one-shot for decode-sized messages (no RCCL call and no
+host work per collective, so a TP engine's decode step is capturable in one HIP graph) and
+two-shot (reduce-scatter + all-gather phases over peer reads) for prefill-sized ones. RCCL is the
+fallback when a group cannot map its peers; CPU/gloo groups use torch.distributed.
+
+Control plane: TP ranks must take every control decision identically (which requests form a
+batch, when a decode stops on cancellation or deadline), or their collectives desynchronise. A
+TP group therefore carries a host-side ``ctrl`` group (gloo) over the same ranks: the leader's
+decision is broadcast (``leader_decides``), and fault checks are agreed by all ranks
+(``any_rank``).
 
 Prefill under TP can run Megatron-style SEQUENCE PARALLEL (engine ``EngineConfig.sequence_parallel``):
 the residual stream is sharded by token rows between the layers, so each row-parallel output is a
@@ -22,7 +29,6 @@ token shards the tokens travel to their experts' ranks and back by all-to-all (`
 
 from __future__ import annotations
 
-import os
 import warnings
 
 from typing import List, Optional
@@ -34,33 +40,68 @@ import torch.distributed as dist
 class TPGroup:
     """Rank/size of a model's tensor-parallel group (size 1 = no communication)."""
 
-    def __init__(self, group: Optional["dist.ProcessGroup"] = None, rank: int = 0, size: int = 1):
+    def __init__(self, group: Optional["dist.ProcessGroup"] = None, rank: int = 0, size: int = 1,
+                 ctrl: Optional["dist.ProcessGroup"] = None):
         self.group = group
         self.rank = rank
         self.size = size
-        self.custom = None  # CustomAllReduce once enable_custom() ran
-        self.rowpar = None  # its twin for the row-parallel GEMVs with a fused all-reduce (LLMC_FUSED_AR=1)
+        self.ctrl = ctrl      # host control group (gloo) over the same ranks, or None
+        self.custom = None    # one-shot CustomAllReduce once enable_custom() ran
+        self.custom2 = None   # its two-shot twin for prefill-sized messages
 
-    def enable_custom(self, device, cap: Optional[int] = None) -> bool:
+    def enable_custom(self, device, cap: Optional[int] = None, cap2: Optional[int] = None) -> bool:
         """Map the group's IPC buffers for the custom collectives (GPU groups of 2..8 ranks).
         Collective; returns False on every rank (RCCL stays in charge) when any rank failed."""
         if self.size == 1 or self.custom is not None:
             return self.custom is not None
-        from .custom_ar import DEFAULT_CAP, CustomAllReduce, CustomAllReduceUnavailable
+        from .custom_ar import DEFAULT_CAP, TWOSHOT_CAP, CustomAllReduce, CustomAllReduceUnavailable
 
         try:
             self.custom = CustomAllReduce(self.group, self.rank, self.size, device, cap or DEFAULT_CAP)
-            if os.environ.get("LLMC_FUSED_AR", "0") == "1":
-                # a second buffer, dedicated to the row-parallel GEMVs with the all-reduce in
-                # their epilogue (block epochs of their own, so no all-reduce self-test on it)
-                self.rowpar = CustomAllReduce(self.group, self.rank, self.size, device, 128 * 1024, selftest=False)
+            self.custom2 = CustomAllReduce(self.group, self.rank, self.size, device, cap2 or TWOSHOT_CAP)
         except CustomAllReduceUnavailable as e:
             warnings.warn(f"custom all-reduce disabled, using RCCL: {e}")
             if self.custom is not None:
                 self.custom.close()
-            self.custom = self.rowpar = None
+            self.custom = self.custom2 = None
             return False
         return True
+
+    # -- control plane ----------------------------------------------------------------------------
+    def leader_decides(self, value: int) -> int:
+        """The leader's ``value`` on every rank (host broadcast over ``ctrl``); identity without one."""
+        if self.size == 1 or self.ctrl is None:
+            return value
+        t = torch.tensor([int(value)], dtype=torch.int64)
+        dist.broadcast(t, src=dist.get_global_rank(self.ctrl, 0), group=self.ctrl)
+        return int(t.item())
+
+    def any_rank(self, flag: bool) -> bool:
+        """True on every rank if ``flag`` is True on any rank (host all-reduce over ``ctrl``)."""
+        if self.size == 1 or self.ctrl is None:
+            return bool(flag)
+        t = torch.tensor([1 if flag else 0], dtype=torch.int32)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX, group=self.ctrl)
+        return bool(t.item())
+
+    def custom_timed_out(self) -> bool:
+        """Local: did a custom-collective spin give up since the last resync (reads device memory,
+        after the caller synchronised its stream)?"""
+        return any(c is not None and c.timed_out() for c in (self.custom, self.custom2))
+
+    def check_collectives(self) -> bool:
+        """Collective over ``ctrl`` (every rank calls it at the same point): True when every rank's
+        custom collectives completed; otherwise every rank re-synchronises the protocol state
+        (epochs, flags) and False is returned everywhere, so the caller fails the work done since
+        the last check instead of serving sums that read stale peer data."""
+        if self.size == 1 or self.custom is None:
+            return True
+        if not self.any_rank(self.custom_timed_out()):
+            return True
+        for c in (self.custom, self.custom2):
+            if c is not None:
+                c.resync()
+        return False
 
     @staticmethod
     def single() -> "TPGroup":
@@ -77,8 +118,13 @@ class TPGroup:
     def all_reduce_(self, t: torch.Tensor) -> torch.Tensor:
         if self.size > 1:
             c = self.custom
-            if c is not None and t.is_cuda and t.dtype == torch.bfloat16 and t.is_contiguous() and c.fits(t.numel() * 2):
-                return c.all_reduce_(t)
+            nbytes = t.numel() * t.element_size()
+            if c is not None and t.is_cuda and t.dtype == torch.bfloat16 and t.is_contiguous() and nbytes % 16 == 0:
+                return c.all_reduce_(t) if c.fits(nbytes) else self.custom2.all_reduce_large_(t)
+            if self._bounce(t):
+                f = t.cpu()
+                dist.all_reduce(f, group=self.group)
+                return t.copy_(f)
             dist.all_reduce(t, group=self.group)
         return t
 
@@ -89,8 +135,8 @@ class TPGroup:
             return out
         c = self.custom
         nbytes = t.numel() * t.element_size()
-        if c is not None and t.is_cuda and t.is_contiguous() and out.is_contiguous() and c.fits(nbytes):
-            return c.all_gather(t, out)
+        if c is not None and t.is_cuda and t.is_contiguous() and out.is_contiguous() and nbytes % 16 == 0:
+            return c.all_gather(t, out) if c.fits(nbytes) else self.custom2.all_gather_large(t, out)
         flat = out.view(self.size * t.shape[0], *t.shape[1:])  # gloo wants dim-0 concatenation
         if self._bounce(t):
             f = flat.cpu()
@@ -110,6 +156,10 @@ class TPGroup:
         if self.size == 1:
             return out.copy_(full)
         n = out.shape[0]
+        c = self.custom2
+        if (c is not None and full.is_cuda and full.dtype == torch.bfloat16 and full.is_contiguous()
+                and out.is_contiguous() and (out.numel() * 2) % 16 == 0):
+            return c.reduce_scatter(full, out)
         if full.is_cuda and not self._bounce(full):
             dist.reduce_scatter_tensor(out, full.contiguous(), group=self.group)
             return out

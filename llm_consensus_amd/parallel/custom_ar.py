@@ -1,11 +1,19 @@
-"""K13: custom one-shot all-reduce / all-gather for decode-sized TP collectives.
+"""K13: custom all-reduce / reduce-scatter / all-gather over IPC-mapped peer buffers.
 
 Each rank allocates one uncached device buffer (signals + two data parities, see
-``csrc/kernels/allreduce.hip``), exports it with hipIpc, and maps every peer's buffer; the
-collective is then ONE kernel that stages the local slice, signals each peer over xGMI, waits
-for theirs (bounded spin) and reads every peer's copy directly. No host involvement per call, so
-it is capturable in the decode HIP graph (RCCL is used for bootstrap and for messages larger
-than the buffer).
+``csrc/kernels/allreduce.hip``), exports it with hipIpc, and maps every peer's buffer; a
+collective is then ONE kernel that stages the local data, signals each peer over xGMI, waits for
+theirs (bounded spin) and reads the peers' copies directly. No host involvement per call, so it
+is capturable in the decode HIP graph.
+
+Two buffer classes per TP group (``TPGroup.enable_custom``):
+  * one-shot (decode: <= 1 MiB, e.g. a [B, H] hidden state or a vocab-shard logits gather): every
+    rank reads every peer's whole message — one link round trip;
+  * two-shot (prefill: > 1 MiB, sequence-parallel reduce-scatter / all-gather): reduce-scatter +
+    all-gather phases inside one launch, each rank pulling only 1/world of every peer's message per
+    phase over all of its xGMI links at once; messages larger than the buffer run as pieces.
+Setup is collective and self-checking: a rank that cannot map a peer (no P2P access between the
+devices, IPC failure) or whose self-test sum is wrong makes EVERY rank fall back to RCCL together.
 """
 
 from __future__ import annotations
@@ -18,6 +26,8 @@ import torch
 from ..utils.native import kernels
 
 DEFAULT_CAP = 1 << 20  # bytes per parity: [4, 8192] bf16 hidden = 64 KiB; logits gather [4, 32064] f32 = 512 KiB
+TWOSHOT_CAP = 64 << 20  # bytes per parity of the two-shot buffer (larger messages run in pieces)
+MODE_AR, MODE_RS, MODE_AG = 0, 1, 2
 
 
 def _on(device: torch.device):
@@ -27,6 +37,11 @@ def _on(device: torch.device):
 class CustomAllReduceUnavailable(RuntimeError):
     """Raised on EVERY rank of the group when any rank could not map the peers or the self-test
     failed: the group agrees before anyone raises, so the callers fall back together (RCCL)."""
+
+
+class CustomAllReduceTimeout(RuntimeError):
+    """A bounded spin gave up (a peer stalled): the results of the collectives since the last
+    check are invalid; ``resync()`` restores a consistent protocol state."""
 
 
 class CustomAllReduce:
@@ -43,30 +58,41 @@ class CustomAllReduce:
         self.bases: List[int] = []
         self._opened: List[int] = []
         err: Optional[BaseException] = None
-        handle: Optional[bytes] = None
+        mine = None
         k = None
-        try:
-            k = kernels()
-            with _on(self.device):
-                self.own = k.car_alloc(self.cap)
-                handle = k.ipc_handle(self.own)
-        except Exception as e:  # noqa: BLE001 - reported collectively below
-            err = e
+        if self.cap < 16 * world or self.cap % 16:
+            err = ValueError(f"custom all-reduce cap {self.cap} too small / not a multiple of 16")
+        else:
+            try:
+                k = kernels()
+                with _on(self.device):
+                    self.own = k.car_alloc(self.cap)
+                    if self.device.type == "cuda":
+                        dev_index = self.device.index if self.device.index is not None else torch.cuda.current_device()
+                    else:
+                        dev_index = -1  # CPU fakes in tests
+                    mine = (k.ipc_handle(self.own), int(dev_index))
+            except Exception as e:  # noqa: BLE001 - reported collectively below
+                err = e
         # every rank reaches every collective below, whatever failed locally (no mismatched calls)
-        handles: List[Optional[bytes]] = [None] * world
-        dist.all_gather_object(handles, handle, group=group)
-        if err is None and any(h is None for h in handles):
+        peers: List[Optional[tuple]] = [None] * world
+        dist.all_gather_object(peers, mine, group=group)
+        if err is None and any(p is None for p in peers):
             err = RuntimeError("a peer could not export its buffer")
         if err is None:
             try:
                 with _on(self.device):
-                    for r, h in enumerate(handles):
+                    my_dev = peers[rank][1]
+                    for r, (h, d) in enumerate(peers):
                         if r == rank:
                             self.bases.append(self.own)
-                        else:
-                            p = k.ipc_open(h)
-                            self.bases.append(p)
-                            self._opened.append(p)
+                            continue
+                        # a node whose GPUs cannot map each other's memory fails over cleanly
+                        if my_dev >= 0 and not k.can_access_peer(my_dev, d):
+                            raise RuntimeError(f"device {my_dev} has no peer access to device {d} (rank {r})")
+                        p = k.ipc_open(h)
+                        self.bases.append(p)
+                        self._opened.append(p)
             except Exception as e:  # noqa: BLE001
                 err = e
         ok = self._agree(err is None)
@@ -92,9 +118,12 @@ class CustomAllReduce:
         """One real collective through the mapped peers before anything depends on it: a wrong
         sum or a spin that gave up (peer writes not visible over the link) disables the path."""
         try:
-            n = 8192  # 16 KiB: the decode hidden state of an 8B model
+            n = max(8, min(8192, self.cap // 2) // 8 * 8)  # <= 16 KiB: the decode hidden state of an 8B model
             x = torch.full((n,), float(self.rank + 1), dtype=torch.bfloat16, device=self.device)
-            self.all_reduce_(x)
+            if self.cap > DEFAULT_CAP:
+                self.all_reduce_large_(x)
+            else:
+                self.all_reduce_(x)
             if x.is_cuda:
                 torch.cuda.synchronize(self.device)
             want = self.world * (self.world + 1) // 2
@@ -105,14 +134,17 @@ class CustomAllReduce:
     def fits(self, nbytes: int) -> bool:
         return nbytes % 16 == 0 and nbytes <= self.cap
 
+    @staticmethod
+    def _stream(t: torch.Tensor) -> int:
+        return torch.cuda.current_stream(t.device).cuda_stream if t.is_cuda else 0
+
+    # -- one-shot (decode) ----------------------------------------------------------------------
     def all_reduce_(self, t: torch.Tensor) -> torch.Tensor:
         """In-place bf16 sum over the group (f32 accumulation in rank order: every rank gets the
         same bits)."""
         if t.dtype != torch.bfloat16 or not t.is_contiguous():
             raise TypeError("custom all-reduce: contiguous bf16 only")
-        nbytes = t.numel() * 2
-        stream = torch.cuda.current_stream(t.device).cuda_stream if t.is_cuda else 0
-        kernels().car_allreduce(self.bases, self.rank, self.world, self.cap, t.data_ptr(), nbytes, stream)
+        kernels().car_allreduce(self.bases, self.rank, self.world, self.cap, t.data_ptr(), t.numel() * 2, self._stream(t))
         return t
 
     def all_gather(self, x: torch.Tensor, out: torch.Tensor) -> torch.Tensor:
@@ -121,16 +153,76 @@ class CustomAllReduce:
         if out.numel() * out.element_size() != nbytes * self.world:
             raise ValueError("custom all-gather: out must hold world * x")
         kernels().car_allgather(self.bases, self.rank, self.world, self.cap, x.data_ptr(), out.data_ptr(), nbytes,
-                                torch.cuda.current_stream(x.device).cuda_stream)
+                                self._stream(x))
         return out
 
+    # -- two-shot (prefill) -----------------------------------------------------------------------
+    def all_reduce_large_(self, t: torch.Tensor) -> torch.Tensor:
+        """In-place bf16 sum, two-shot, in pieces of at most ``cap`` bytes (a multiple of 16 B)."""
+        if t.dtype != torch.bfloat16 or not t.is_contiguous() or (t.numel() * 2) % 16:
+            raise TypeError("two-shot all-reduce: contiguous bf16, multiple of 16 bytes")
+        k, st = kernels(), self._stream(t)
+        total = t.numel() * 2
+        piece = self.cap // (16 * self.world) * 16 * self.world
+        for o in range(0, total, piece):
+            nb = min(piece, total - o)
+            nv = nb // 16
+            seg16 = (nv + self.world - 1) // self.world
+            p = t.data_ptr() + o
+            k.car_twoshot(self.bases, self.rank, self.world, self.cap, MODE_AR, p, p, seg16 * 16, seg16, nv, st)
+        return t
+
+    def reduce_scatter(self, full: torch.Tensor, out: torch.Tensor) -> torch.Tensor:
+        """out = rows [rank * n, (rank + 1) * n) of the bf16 sum of ``full`` [world * n, ...]."""
+        seg = out.numel() * 2
+        if (full.dtype != torch.bfloat16 or out.dtype != torch.bfloat16 or not full.is_contiguous()
+                or not out.is_contiguous() or full.numel() != out.numel() * self.world or seg % 16):
+            raise TypeError("two-shot reduce-scatter: contiguous bf16 [world*n] -> [n], 16-byte rows blocks")
+        k, st = kernels(), self._stream(out)
+        piece = self.cap // (16 * self.world) * 16
+        for o in range(0, seg, piece):
+            nb = min(piece, seg - o)
+            k.car_twoshot(self.bases, self.rank, self.world, self.cap, MODE_RS, full.data_ptr() + o, out.data_ptr() + o,
+                          seg, nb // 16, self.world * (nb // 16), st)
+        return out
+
+    def all_gather_large(self, x: torch.Tensor, out: torch.Tensor) -> torch.Tensor:
+        """out.view(world, -1)[r] = x of rank r (any dtype), two-shot pieces."""
+        seg = x.numel() * x.element_size()
+        if out.numel() * out.element_size() != seg * self.world or seg % 16 or not x.is_contiguous():
+            raise ValueError("two-shot all-gather: out must hold world * x, 16-byte multiple")
+        k, st = kernels(), self._stream(x)
+        piece = self.cap // (16 * self.world) * 16
+        for o in range(0, seg, piece):
+            nb = min(piece, seg - o)
+            k.car_twoshot(self.bases, self.rank, self.world, self.cap, MODE_AG, x.data_ptr() + o, out.data_ptr() + o,
+                          seg, nb // 16, self.world * (nb // 16), st)
+        return out
+
+    # -- fault handling ---------------------------------------------------------------------------
     def timed_out(self) -> bool:
         return bool(kernels().car_timed_out(self.own))
 
+    def resync(self) -> None:
+        """Collective: after a spin timeout, every rank drains its device, then the protocol state
+        (epochs, flags, timeout word) is zeroed on every rank between two group barriers."""
+        import torch.distributed as dist
+
+        if self.device.type == "cuda":
+            torch.cuda.synchronize(self.device)
+        dist.barrier(group=self.group)
+        with _on(self.device):
+            kernels().car_reset(self.own)
+        dist.barrier(group=self.group)
+
+    # -- EPI_AR: row-parallel GEMV with the all-reduce in its epilogue -----------------------------
+    # Multi-GPU only and unmeasured there: on ranks sharing one GPU it measured slower than GEMV +
+    # the one-shot kernel, so the engine does not use it; kept with its exactness tests
+    # (tests/test_custom_ar_gpu.py) for a multi-GPU evaluation.
     def rowpar_timed_out(self) -> bool:
-        """Timeout word of a buffer used by gemv_rowpar_ar (its signal layout: ctr[1024] | flags
-        [1024][8] | timeout at 36864; car_timed_out reads at the all-reduce layout's 3072)."""
-        return bool(kernels().car_timed_out(self.own + (4 * 1024 + 1024 * 8 * 4) - (1024 + 64 * 8 * 4)))
+        """Timeout word of a buffer used by gemv_rowpar_ar (its own signal layout)."""
+        k = kernels()
+        return bool(k.car_timed_out(self.own + k.gemv_ar_timeout_off() - k.car_timeout_off()))
 
     def gemv_rowpar_ar(self, x: torch.Tensor, W: torch.Tensor, h: torch.Tensor) -> torch.Tensor:
         """Row-parallel decode projection with the all-reduce in the GEMV epilogue (EPI_AR):
@@ -138,8 +230,7 @@ class CustomAllReduce:
         object's buffer must be dedicated to it (block epochs of its own, cap >= 128 KiB)."""
         M, K = x.shape
         kernels().gemv_rowpar_ar(M, x.data_ptr(), x.stride(0), W.data_ptr(), h.data_ptr(), h.stride(0), W.shape[0], K,
-                                 self.bases, self.rank, self.world, self.cap,
-                                 torch.cuda.current_stream(x.device).cuda_stream)
+                                 self.bases, self.rank, self.world, self.cap, self._stream(x))
         return h
 
     def close(self) -> None:

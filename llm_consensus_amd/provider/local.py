@@ -112,6 +112,7 @@ class LocalBackend:
         self._queues: Dict[int, "queue.Queue"] = {}
         self._rid_model: Dict[int, str] = {}
         self._qlock = threading.Lock()
+        self._bcast_lock = threading.Lock()
         self._ids = itertools.count(1)
         self.closed = False
 
@@ -220,10 +221,14 @@ class LocalBackend:
             q.put(("error", rid, w.fatal or "worker died"))
 
     def broadcast(self, model: str, msg) -> None:
-        for w in self._workers_for(model):
-            if w.fatal:
-                raise LocalError(w.fatal.splitlines()[0])
-            w.send(msg)
+        """Send ``msg`` to every worker hosting ``model``. Atomic across workers: concurrent
+        callers (the runner's per-model threads, the judge session) must reach every rank of a TP
+        group in ONE order, or the ranks would batch / prefill different requests."""
+        with self._bcast_lock:
+            for w in self._workers_for(model):
+                if w.fatal:
+                    raise LocalError(w.fatal.splitlines()[0])
+                w.send(msg)
 
     def provider(self, name: str) -> "LocalProvider":
         return LocalProvider(self, name)

@@ -144,11 +144,27 @@ class _EngineHost:
     def _gather(self, first, kind: str) -> list:
         """``first`` plus the queued items of the same kind, up to the engine's decode rows; waits
         up to the batching window (LLMC_BATCH_WINDOW_MS, default 5 ms, engines with > 1 row only)
-        for items still arriving. A different kind ends the batch and is processed next."""
+        for items still arriving. A different kind ends the batch and is processed next.
+
+        TP engines: the window is timing-dependent, so only the leader applies it; it broadcasts
+        the batch size over the group's control channel and every follower takes exactly that
+        many items (the driver sends every command to all ranks in one order, so they are the
+        same requests) — identical batch compositions on every rank."""
         items = [first]
         cap = self.engine.ecfg.max_batch
-        if cap <= 1:
+        tp = self.engine.tp
+        if tp.size > 1 and tp.ctrl is not None and not tp.is_leader:
+            n = tp.leader_decides(0)
+            while len(items) < n:
+                items.append(self.q.get())
             return items
+        if cap > 1:
+            self._window(items, kind, cap)
+        if tp.size > 1 and tp.ctrl is not None:
+            tp.leader_decides(len(items))
+        return items
+
+    def _window(self, items: list, kind: str, cap: int) -> None:
         deadline = time.monotonic() + BATCH_WINDOW_S
         while len(items) < cap:
             try:
@@ -159,7 +175,6 @@ class _EngineHost:
                 self._stash = nxt  # next in line: keeps the queue's order
                 break
             items.append(nxt)
-        return items
 
     # -- continuous batching -------------------------------------------------------------------
     def _loop_continuous(self) -> None:
@@ -398,8 +413,10 @@ def worker_main(gpu: int, conn, models: List[dict], dist_info: Optional[dict], t
                                     rank=dist_info["rank"], world_size=dist_info["world"], **kw)
             for gname, ranks in dist_info["groups"]:  # every worker creates every group, same order
                 g = dist.new_group(ranks)
+                # host control channel of the TP group (leader decisions, fault agreement)
+                ctrl = g if on_cpu else dist.new_group(ranks, backend="gloo")
                 if dist_info["rank"] in ranks:
-                    groups[gname] = (g, ranks.index(dist_info["rank"]), len(ranks))
+                    groups[gname] = (g, ranks.index(dist_info["rank"]), len(ranks), ctrl)
         hosts: Dict[str, _EngineHost] = {}
         ctxs: Dict[int, Context] = {}  # live requests' contexts (cancel); dropped when they finish
         faults = parse_faults(os.environ.get("LLMC_FAULT", ""))
@@ -411,13 +428,15 @@ def worker_main(gpu: int, conn, models: List[dict], dist_info: Optional[dict], t
                 register_dir(m["checkpoint"])
                 cfg = FAMILIES[m["family"]]
             if m["name"] in groups:
-                g, r, n = groups[m["name"]]
-                tp = TPGroup(g, r, n)
+                g, r, n, ctrl = groups[m["name"]]
+                tp = TPGroup(g, r, n, ctrl=ctrl)
                 if not on_cpu and os.environ.get("LLMC_CUSTOM_AR", "1") != "0":
                     tp.enable_custom(f"cuda:{gpu}")  # collective over the group: same order on every rank
             else:
                 tp = TPGroup.single()
-            # TP decode is graph-captured when its collectives are the custom xGMI kernels
+            # TP decode is graph-captured when its collectives are the custom xGMI kernels; a group
+            # whose peers could not be mapped decodes eagerly over RCCL (LLMC_TP_GRAPHS=1 captures
+            # the RCCL collectives instead — needs >= 2 GPUs, unverified on the 1-GPU test box)
             graphs = tp.size == 1 or tp.custom is not None or os.environ.get("LLMC_TP_GRAPHS") == "1"
             ecfg = EngineConfig(device="cpu" if on_cpu else f"cuda:{gpu}", max_context=m["max_context"],
                                 max_batch=m.get("max_batch", 1), max_seqs=m.get("max_seqs", 0), seed=m["seed"],

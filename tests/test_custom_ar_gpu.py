@@ -192,3 +192,138 @@ def test_rowpar_fused_allreduce(cuda, world):
         assert not isinstance(bad, str), bad
         assert bad == 0, f"rank {rank}: {bad} elements differ from GEMV + separate all-reduce"
         assert not tmo, f"rank {rank}: a spin timed out"
+
+
+def _twoshot_worker(rank, world, port, q):
+    """Two-shot all-reduce / reduce-scatter / all-gather (prefill-sized messages, run in pieces
+    when larger than the buffer) against f32 sums of every rank's input."""
+    try:
+        import torch.distributed as dist
+
+        from llm_consensus_amd.parallel.comm import TPGroup
+
+        torch.cuda.set_device(0)
+        dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world)
+        tp = TPGroup(dist.group.WORLD, rank, world)
+        # a 16 MiB two-shot buffer: the 64 MiB case runs as pieces
+        assert tp.enable_custom("cuda:0", cap=1 << 20, cap2=16 << 20)
+        errs = []
+        for mib in (4, 64):
+            n = mib * (1 << 20) // 2 + 8 * 37  # ragged: last segment shorter
+            x = _inp(rank, n, mib).cuda()
+            tp.all_reduce_(x)
+            torch.cuda.synchronize()
+            ref = sum(_inp(r, n, mib).float() for r in range(world))
+            errs.append(float((x.float().cpu() - ref).abs().max() / ref.abs().max()))
+        # sequence-parallel shapes: [world * Ts, H] -> [Ts, H] and back
+        Ts, H = 1500, 4096
+        full = [(_inp(r, world * Ts * H, 7).view(world * Ts, H)) for r in range(world)]
+        out = torch.empty(Ts, H, dtype=torch.bfloat16, device="cuda")
+        tp.reduce_scatter_rows(full[rank].cuda(), out)
+        torch.cuda.synchronize()
+        ref = sum(f.float() for f in full)[rank * Ts:(rank + 1) * Ts]
+        errs.append(float((out.float().cpu() - ref).abs().max() / ref.abs().max()))
+        mine = _inp(rank, Ts * H, 11).view(Ts, H).cuda()
+        g = torch.empty(world, Ts, H, dtype=torch.bfloat16, device="cuda")
+        tp.all_gather_rows(mine, g)
+        torch.cuda.synchronize()
+        gat_ok = all(bool(torch.equal(g[r].cpu(), _inp(r, Ts * H, 11).view(Ts, H))) for r in range(world))
+        q.put((rank, max(errs), gat_ok, tp.custom_timed_out()))
+        dist.barrier()
+        tp.custom.close()
+        tp.custom2.close()
+        dist.destroy_process_group()
+    except Exception as e:  # noqa: BLE001
+        import traceback
+
+        q.put((rank, repr(e) + traceback.format_exc(), False, True))
+
+
+@pytest.mark.parametrize("world", [2, 4])
+def test_twoshot_collectives_ipc(cuda, world):
+    import socket
+
+    with socket.socket() as sk:
+        sk.bind(("127.0.0.1", 0))
+        port = sk.getsockname()[1]
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_twoshot_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=300) for _ in range(world)]
+    for p in procs:
+        p.join(timeout=60)
+    for rank, err, gat_ok, tmo in res:
+        assert not isinstance(err, str), err
+        assert not tmo, f"rank {rank}: a spin timed out"
+        assert err < 1e-2, (rank, err)
+        assert gat_ok, rank
+
+
+def _cancel_tp_worker(rank, world, port, q):
+    """A TP=2 engine (custom one-shot collectives in captured decode graphs, gloo control group)
+    whose ranks see the cancel one replay apart: both stop at the leader's replay, the protocol
+    stays in step (no spin timeout) and the next request is bit-identical to a clean run."""
+    try:
+        import torch.distributed as dist
+
+        from llm_consensus_amd.context import ContextError
+        from llm_consensus_amd.engine import Engine, EngineConfig
+        from llm_consensus_amd.models.config import FAMILIES
+        from llm_consensus_amd.parallel.comm import TPGroup
+
+        torch.cuda.set_device(0)
+        dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world)
+        tp = TPGroup(dist.group.WORLD, rank, world, ctrl=dist.group.WORLD)
+        assert tp.enable_custom("cuda:0")
+        e = Engine(FAMILIES["llama-small"], EngineConfig(device="cuda:0", max_context=512, seed=3), tp=tp)
+        e.warmup_graphs()
+        p = [(i * 131) % 30000 + 256 for i in range(40)]
+        ref = e.generate_ids(p, 48, temperature=0.0, stop_on_eos=False)
+
+        class Late:
+            def __init__(self, n):
+                self.n, self.calls = n, 0
+
+            def done(self):
+                self.calls += 1
+                return self.calls >= self.n
+
+            def err(self):
+                return "context canceled"
+
+        err = None
+        try:
+            e.generate_ids(p, 400, temperature=0.0, stop_on_eos=False, ctx=Late(3 + rank))
+        except ContextError as ex:
+            err = str(ex)
+        again = e.generate_ids(p, 48, temperature=0.0, stop_on_eos=False)
+        torch.cuda.synchronize()
+        q.put((rank, err, again == ref, tp.custom_timed_out()))
+        dist.barrier()
+        dist.destroy_process_group()
+    except Exception as ex:  # noqa: BLE001
+        import traceback
+
+        q.put((rank, repr(ex) + traceback.format_exc(), False, True))
+
+
+def test_tp_cancel_mid_decode_keeps_protocol_in_step(cuda):
+    import socket
+
+    with socket.socket() as sk:
+        sk.bind(("127.0.0.1", 0))
+        port = sk.getsockname()[1]
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_cancel_tp_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=300) for _ in range(2)]
+    for p in procs:
+        p.join(timeout=60)
+    for rank, err, same, tmo in res:
+        assert err == "context canceled", (rank, err)
+        assert same, f"rank {rank}: the request after the cancel differs from the clean run"
+        assert not tmo, f"rank {rank}: a spin timed out"

@@ -129,10 +129,13 @@ class _FakeCarKernels:
     """Stand-in for the HIP module: mapping succeeds or fails per rank, and the all-reduce
     writes the right sum only where told to (exercises the group agreement, not the kernel)."""
 
-    def __init__(self, rank, fail_open_rank=-1, correct_ranks=()):
+    def __init__(self, rank, fail_open_rank=-1, correct_ranks=(), fail_alloc_rank=-1, timeout_rank=-1):
         self.rank, self.fail_open_rank, self.correct = rank, fail_open_rank, set(correct_ranks)
+        self.fail_alloc_rank, self.timeout_rank = fail_alloc_rank, timeout_rank
 
     def car_alloc(self, cap):
+        if self.rank == self.fail_alloc_rank:
+            raise RuntimeError("car_alloc: out of memory")
         return 4096 * (self.rank + 1)
 
     def ipc_handle(self, p):
@@ -150,7 +153,7 @@ class _FakeCarKernels:
         pass
 
     def car_timed_out(self, own):
-        return 0
+        return 1 if self.rank == self.timeout_rank else 0
 
     def car_allreduce(self, bases, rank, world, cap, ptr, nbytes, stream):
         import ctypes
@@ -158,6 +161,10 @@ class _FakeCarKernels:
         if rank in self.correct:
             want = torch.full((nbytes // 2,), float(world * (world + 1) // 2), dtype=torch.bfloat16)
             ctypes.memmove(ptr, want.data_ptr(), nbytes)
+
+    def car_twoshot(self, bases, rank, world, cap, mode, src, dst, seg_stride, seg16, nv, stream):
+        assert mode == 0 and src == dst  # the self-test is an in-place all-reduce
+        self.car_allreduce(bases, rank, world, cap, dst, nv * 16, stream)
 
 
 def _car_agree_worker(rank, world, port, case, q):
@@ -172,6 +179,8 @@ def _car_agree_worker(rank, world, port, case, q):
 
         fake = {"open_fails": _FakeCarKernels(rank, fail_open_rank=1, correct_ranks=(0, 1)),
                 "selftest_wrong": _FakeCarKernels(rank, correct_ranks=(0,)),
+                "alloc_fails": _FakeCarKernels(rank, correct_ranks=(0, 1), fail_alloc_rank=1),
+                "selftest_timeout": _FakeCarKernels(rank, correct_ranks=(0, 1), timeout_rank=1),
                 "ok": _FakeCarKernels(rank, correct_ranks=(0, 1))}[case]
         custom_ar.kernels = lambda: fake
         tp = TPGroup(dist.group.WORLD, rank, world)
@@ -188,7 +197,8 @@ def _car_agree_worker(rank, world, port, case, q):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("case,want", [("open_fails", False), ("selftest_wrong", False), ("ok", True)])
+@pytest.mark.parametrize("case,want", [("open_fails", False), ("selftest_wrong", False), ("alloc_fails", False),
+                                       ("selftest_timeout", False), ("ok", True)])
 def test_custom_ar_enable_is_collective(case, want):
     """One rank failing to map a peer (or a self-test sum that is wrong on one rank) disables the
     custom all-reduce on EVERY rank, with no mismatched collectives: RCCL keeps the group."""

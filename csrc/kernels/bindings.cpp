@@ -25,11 +25,9 @@ int llmc_gemm(const void*, int, const void*, int, void*, int, int, int, int, int
 int llmc_rope_kv_write(const void*, int, void*, int, const void*, const void*, const void*, void*, void*, const void*,
                        int, int, int, int, int, hipStream_t);
 int llmc_attn_decode(const void*, int, const void*, const void*, const void*, int, const void*, void*, void*, void*,
-                     int, int, int, int, int, int, int, int, int, float, int, hipStream_t);
+                     int, int, int, int, int, int, int, int, int, int, float, int, hipStream_t);
 int llmc_gemv_qkv_rope(int, const void*, int, const void*, float, const void*, int, int, void*, int, void*, void*,
                        const void*, const void*, const void*, const void*, int, int, int, int, hipStream_t);
-int llmc_gemv_attn_merge(int, const void*, int, const void*, const void*, int, int, int, int, int, int, const void*,
-                         void*, int, int, int, int, hipStream_t);
 int llmc_attn_prefill(const void*, int, const void*, const void*, const void*, int, const void*, const void*,
                       const void*, void*, int, int, int, int, int, int, int, float, hipStream_t);
 int llmc_sample(const void*, int64_t, int, int, const void*, const void*, const void*, const void*, const void*, void*,
@@ -100,10 +98,10 @@ PYBIND11_MODULE(_llmc_hip, m) {
           "rope_kv_write");
   });
   m.def("attn_decode", [](ptr q, int qs, ptr kc, ptr vc, ptr bt, int bts, ptr sl, ptr part, ptr ctr, ptr out, int os,
-                          int B, int nh, int nkv, int D, int bs, int chunk, int grid_chunks, int max_chunks,
-                          float scale, int mode, ptr s) {
+                          int B, int nh, int nkv, int D, int bs, int nblocks, int chunk, int grid_chunks,
+                          int max_chunks, float scale, int fused, ptr s) {
     check(llmc_attn_decode(P(q), qs, P(kc), P(vc), P(bt), bts, P(sl), P(part), P(ctr), P(out), os, B, nh, nkv, D, bs,
-                           chunk, grid_chunks, max_chunks, scale, mode, S(s)),
+                           nblocks, chunk, grid_chunks, max_chunks, scale, fused, S(s)),
           "attn_decode");
   });
   m.def("gemv_qkv_rope", [](int M, ptr x, int xs, ptr nw, float eps, ptr W, int N, int K, ptr qo, int qos, ptr kc,
@@ -111,12 +109,6 @@ PYBIND11_MODULE(_llmc_hip, m) {
     check(llmc_gemv_qkv_rope(M, P(x), xs, P(nw), eps, P(W), N, K, P(qo), qos, P(kc), P(vc), P(pos), P(slots),
                              P(cos_t), P(sin_t), nh, nkv, D, bs, S(s)),
           "gemv_qkv_rope");
-  });
-  m.def("gemv_attn_merge", [](int M, ptr x, int xs, ptr part, ptr sl, int nkv, int G, int D, int gc, int min_chunk,
-                              int max_chunks, ptr W, ptr out, int os, int N, int K, int epi, ptr s) {
-    check(llmc_gemv_attn_merge(M, P(x), xs, P(part), P(sl), nkv, G, D, gc, min_chunk, max_chunks, P(W), P(out), os, N,
-                               K, epi, S(s)),
-          "gemv_attn_merge");
   });
   m.def("attn_prefill", [](ptr q, int qs, ptr kc, ptr vc, ptr bt, int bts, ptr qst, ptr ql, ptr cl, ptr out, int os,
                            int B, int max_qlen, int nh, int nkv, int D, int bs, float scale, ptr s) {

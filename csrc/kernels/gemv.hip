@@ -13,7 +13,7 @@ namespace llmc {
 
 template <int M, int NT, int RPW, int PRO, int EPI, int UNROLL_OVERRIDE = 0>
 static int launch_gemv_g(const void* x, int x_stride, const void* nw, float eps, const void* W, void* out,
-                         int out_stride, int N, int K, const RopeEpi& rope, const MergePro& mp, hipStream_t s) {
+                         int out_stride, int N, int K, const RopeEpi& rope, hipStream_t s) {
   constexpr int UNROLL = UNROLL_OVERRIDE ? UNROLL_OVERRIDE : (RPW == 1 ? 4 : (RPW == 2 ? 4 : (M <= 2 ? 4 : 2)));
   constexpr int WAVES = NT / kWave;
   auto kern = gemv_kernel<M, NT, RPW, UNROLL, PRO, EPI, false>;
@@ -29,7 +29,7 @@ static int launch_gemv_g(const void* x, int x_stride, const void* nw, float eps,
   const int rows_per_block = WAVES * RPW;
   const int grid = (N + rows_per_block - 1) / rows_per_block;
   kern<<<grid, NT, lds, s>>>((const bf16_t*)x, x_stride, (const bf16_t*)nw, eps, (const bf16_t*)W, out, out_stride, N,
-                             K, nullptr, 1, rope, mp, ArEpi{});
+                             K, nullptr, 1, rope, ArEpi{});
   return static_cast<int>(hipGetLastError());
 }
 
@@ -58,31 +58,31 @@ static int pick_waves(int N, bool paired) {
 
 template <int M, int PRO, int EPI>
 static int launch_gemv(const void* x, int x_stride, const void* nw, float eps, const void* W, void* out,
-                       int out_stride, int N, int K, const RopeEpi& rope, const MergePro& mp, hipStream_t s) {
+                       int out_stride, int N, int K, const RopeEpi& rope, hipStream_t s) {
   constexpr bool paired = EPI == EPI_SILU || EPI == EPI_ROPE;
   const int w = pick_waves(N, paired);
   // long rows on few blocks (a 70B TP=4 rank's qkv: 2560 x 8192 = 160 fat blocks): 8 loads per
   // lane in flight instead of 4 (9.67 vs 10.99 us, profiles/r1_attn_decode_tp_shapes.md)
   if (w == 16 && K >= 8192 && N <= 4096)
-    return launch_gemv_g<M, 1024, 1, PRO, EPI, 8>(x, x_stride, nw, eps, W, out, out_stride, N, K, rope, mp, s);
+    return launch_gemv_g<M, 1024, 1, PRO, EPI, 8>(x, x_stride, nw, eps, W, out, out_stride, N, K, rope, s);
   switch (w) {
-    case 16: return launch_gemv_g<M, 1024, 1, PRO, EPI>(x, x_stride, nw, eps, W, out, out_stride, N, K, rope, mp, s);
-    case 12: return launch_gemv_g<M, 768, 1, PRO, EPI>(x, x_stride, nw, eps, W, out, out_stride, N, K, rope, mp, s);
-    case 8: return launch_gemv_g<M, 512, 1, PRO, EPI>(x, x_stride, nw, eps, W, out, out_stride, N, K, rope, mp, s);
-    case 4: return launch_gemv_g<M, 256, 1, PRO, EPI, 8>(x, x_stride, nw, eps, W, out, out_stride, N, K, rope, mp, s);
+    case 16: return launch_gemv_g<M, 1024, 1, PRO, EPI>(x, x_stride, nw, eps, W, out, out_stride, N, K, rope, s);
+    case 12: return launch_gemv_g<M, 768, 1, PRO, EPI>(x, x_stride, nw, eps, W, out, out_stride, N, K, rope, s);
+    case 8: return launch_gemv_g<M, 512, 1, PRO, EPI>(x, x_stride, nw, eps, W, out, out_stride, N, K, rope, s);
+    case 4: return launch_gemv_g<M, 256, 1, PRO, EPI, 8>(x, x_stride, nw, eps, W, out, out_stride, N, K, rope, s);
     default:  // paired rows that do not tile by 16-32 rows: pairs inside one wave
-      return launch_gemv_g<M, 256, 2, PRO, EPI>(x, x_stride, nw, eps, W, out, out_stride, N, K, rope, mp, s);
+      return launch_gemv_g<M, 256, 2, PRO, EPI>(x, x_stride, nw, eps, W, out, out_stride, N, K, rope, s);
   }
 }
 
 template <int PRO, int EPI>
 static int dispatch_m(int M, const void* x, int x_stride, const void* nw, float eps, const void* W, void* out,
-                      int out_stride, int N, int K, const RopeEpi& rope, hipStream_t s, const MergePro& mp = {}) {
+                      int out_stride, int N, int K, const RopeEpi& rope, hipStream_t s) {
   switch (M) {
-    case 1: return launch_gemv<1, PRO, EPI>(x, x_stride, nw, eps, W, out, out_stride, N, K, rope, mp, s);
-    case 2: return launch_gemv<2, PRO, EPI>(x, x_stride, nw, eps, W, out, out_stride, N, K, rope, mp, s);
-    case 3: return launch_gemv<3, PRO, EPI>(x, x_stride, nw, eps, W, out, out_stride, N, K, rope, mp, s);
-    case 4: return launch_gemv<4, PRO, EPI>(x, x_stride, nw, eps, W, out, out_stride, N, K, rope, mp, s);
+    case 1: return launch_gemv<1, PRO, EPI>(x, x_stride, nw, eps, W, out, out_stride, N, K, rope, s);
+    case 2: return launch_gemv<2, PRO, EPI>(x, x_stride, nw, eps, W, out, out_stride, N, K, rope, s);
+    case 3: return launch_gemv<3, PRO, EPI>(x, x_stride, nw, eps, W, out, out_stride, N, K, rope, s);
+    case 4: return launch_gemv<4, PRO, EPI>(x, x_stride, nw, eps, W, out, out_stride, N, K, rope, s);
     default: return -3;
   }
 }
@@ -131,22 +131,6 @@ extern "C" int llmc_gemv_qkv_rope(int M, const void* x, int x_stride, const void
   return gemv_dispatch(M, x, x_stride, norm_w, eps, W, nullptr, 0, N, K, EPI_ROPE, rope, s);
 }
 
-// o_proj for decode with the split-KV attention merge fused into the prologue (PRO_MERGE): x is
-// the attention output buffer (rows of single-chunk sequences), part/seq_lens the attention's
-// partials. epi: EPI_RESADD (TP rank 0 / TP=1: h += W.x) or EPI_BF16 (other TP ranks).
-extern "C" int llmc_gemv_attn_merge(int M, const void* x, int x_stride, const void* part, const void* seq_lens,
-                                    int nkv, int G, int D, int gc, int min_chunk, int max_chunks, const void* W,
-                                    void* out, int out_stride, int N, int K, int epi, hipStream_t s) {
-  if (K != nkv * G * D || D % 8 != 0 || K % 8 != 0 || gc > max_chunks || min_chunk <= 0) return -1;
-  MergePro mp{(const float*)part, (const int32_t*)seq_lens, nkv, G, D, gc, min_chunk, max_chunks};
-  RopeEpi rope{};
-  switch (epi) {
-    case EPI_RESADD: return dispatch_m<PRO_MERGE, EPI_RESADD>(M, x, x_stride, nullptr, 0.f, W, out, out_stride, N, K, rope, s, mp);
-    case EPI_BF16: return dispatch_m<PRO_MERGE, EPI_BF16>(M, x, x_stride, nullptr, 0.f, W, out, out_stride, N, K, rope, s, mp);
-    default: return -4;
-  }
-}
-
 // MoE decode (K11 at batch 1): one GEMV per (token, top-k slot) pair against the selected
 // expert's weights; expert ids are read on device, so the launch is graph-replayable.
 namespace llmc {
@@ -159,7 +143,7 @@ static int launch_moe_gemv(int npairs, const void* x, int x_stride, const void* 
   dim3 grid((N + WAVES * RPW - 1) / (WAVES * RPW), npairs);
   gemv_kernel<1, NT, RPW, 4, PRO, EPI, true><<<grid, NT, lds, s>>>(
       (const bf16_t*)x, x_stride, (const bf16_t*)nw, eps, (const bf16_t*)W, out, out_stride, N, K,
-      (const int32_t*)ids, x_div, RopeEpi{}, MergePro{}, ArEpi{});
+      (const int32_t*)ids, x_div, RopeEpi{}, ArEpi{});
   return static_cast<int>(hipGetLastError());
 }
 
@@ -202,7 +186,7 @@ extern "C" int llmc_gemv_rowpar_ar(int M, const void* x, int x_stride, const voi
   case MM:                                                                                                       \
     gemv_kernel<MM, NT, 1, 4, PRO_NONE, EPI_AR, false><<<grid, NT, lds, s>>>(                                    \
         (const bf16_t*)x, x_stride, nullptr, 0.f, (const bf16_t*)W, h, h_stride, N, K, nullptr, 1, RopeEpi{},    \
-        MergePro{}, ar);                                                                                         \
+        ar);                                                                                         \
     break;
   switch (M) {
     LLMC_AR_CASE(1)
@@ -234,7 +218,7 @@ extern "C" int llmc_moe_down_combine(int T, const void* act, int act_stride, con
   wts.cos_t = static_cast<const float*>(w);
   dim3 grid((N + WAVES - 1) / WAVES, T);
   kern<<<grid, NT, lds, s>>>((const bf16_t*)act, act_stride, nullptr, 0.f, (const bf16_t*)W, h, h_stride, N, K,
-                             (const int32_t*)ids, 1, wts, MergePro{}, ArEpi{});
+                             (const int32_t*)ids, 1, wts, ArEpi{});
   return static_cast<int>(hipGetLastError());
 }
 
@@ -264,7 +248,7 @@ static int launch_sweep(const void* x, const void* nw, const void* W, void* out,
   const size_t lds = static_cast<size_t>(K) * sizeof(bf16_t) + WAVES * sizeof(float);
   const int grid = (N + WAVES * RPW - 1) / (WAVES * RPW);
   gemv_kernel<1, NT, RPW, UNROLL, PRO_NORM, EPI_BF16, false><<<grid, NT, lds, s>>>(
-      (const bf16_t*)x, K, (const bf16_t*)nw, 1e-5f, (const bf16_t*)W, out, N, N, K, nullptr, 1, RopeEpi{}, MergePro{}, ArEpi{});
+      (const bf16_t*)x, K, (const bf16_t*)nw, 1e-5f, (const bf16_t*)W, out, N, N, K, nullptr, 1, RopeEpi{}, ArEpi{});
   return static_cast<int>(hipGetLastError());
 }
 }  // namespace llmc

@@ -17,9 +17,6 @@
 //    ROPE: qkv projection with pair-interleaved Q/K head rows -> rotate-half RoPE from the f32
 //    accumulators, q to the q buffer, k/v straight into the paged KV cache at the device slot
 //    (replaces the separate RoPE + KV-write launch of the decode step).
-//  * Fused prologue  PRO_MERGE (o_proj only): x <- the split-KV decode attention output, merged
-//    here from the attention kernel's per-chunk partials (O, m, l) instead of by a separate
-//    reduce launch; rows whose sequence got a single chunk read the attention's direct output.
 #pragma once
 #include <type_traits>
 
@@ -27,7 +24,7 @@
 
 namespace llmc {
 
-enum { PRO_NONE = 0, PRO_NORM = 1, PRO_MERGE = 2 };
+enum { PRO_NONE = 0, PRO_NORM = 1 };
 enum { EPI_BF16 = 0, EPI_F32 = 1, EPI_RESADD = 2, EPI_SILU = 3, EPI_ROPE = 4, EPI_COMBINE = 5, EPI_AR = 6 };
 
 struct RopeEpi {
@@ -40,15 +37,6 @@ struct RopeEpi {
   const float* cos_t;       // [max_pos][D/2]
   const float* sin_t;
   int nh, nkv, D, bs;
-};
-
-// PRO_MERGE operands: partials of attn_decode_mfma (layout [M][nkv][max_chunks][G][D + 2] f32 =
-// unnormalised O, m (natural-log domain), l) and the balanced-split parameters that decide how
-// many chunks each row's sequence was split into (common.h decode_nsplit).
-struct MergePro {
-  const float* part;
-  const int32_t* seq_lens;  // [M]
-  int nkv, G, D, gc, min_chunk, max_chunks;
 };
 
 // EPI_AR operands: a row-parallel projection (TP o_proj / down_proj at decode) whose all-reduce
@@ -74,7 +62,7 @@ __global__ __launch_bounds__(NT) void gemv_kernel(const bf16_t* __restrict__ x, 
                                                   const bf16_t* __restrict__ norm_w, float eps,
                                                   const bf16_t* __restrict__ W, void* __restrict__ out,
                                                   int out_stride, int N, int K, const int32_t* __restrict__ expert_ids,
-                                                  int x_div, RopeEpi rope, MergePro mp, ArEpi ar) {
+                                                  int x_div, RopeEpi rope, ArEpi ar) {
   constexpr int WAVES = NT / kWave;
   constexpr bool PAIR_LDS = (EPI == EPI_SILU || EPI == EPI_ROPE) && RPW == 1;  // host: N % (2 * WAVES) == 0
   // EXPERT (MoE decode): blockIdx.y = (token, slot) pair; weights of expert expert_ids[pair],
@@ -266,61 +254,6 @@ __global__ __launch_bounds__(NT) void gemv_kernel(const bf16_t* __restrict__ x, 
           for (int j = 0; j < 8; ++j) f[j] = f[j] * inv[m] * g[j];
           reinterpret_cast<u32x4*>(xs + m * K)[c] = pack8(f);
         }
-      }
-    }
-  } else if constexpr (PRO == PRO_MERGE) {
-    // thread <-> 8 consecutive dims of one head; merge that head's chunks 4 at a time with all
-    // 4 x (m, l, 8 O) loads in flight (online rescale between groups). The partial rows are
-    // (D + 2) floats apart, so O is read as 8-B float2 (rows are only 8-B aligned).
-    const int stride = mp.D + 2;
-    const int64_t cstride = static_cast<int64_t>(mp.G) * stride;
-#pragma unroll
-    for (int m = 0; m < M; ++m) {
-      const int n = decode_nsplit(mp.seq_lens[m], mp.gc, -mp.min_chunk);
-      for (int c = tid; c < nchunk; c += NT) {
-        if (n == 1) {  // the attention kernel wrote this row's output directly
-          reinterpret_cast<u32x4*>(xs + m * K)[c] = reinterpret_cast<const u32x4*>(x + static_cast<int64_t>(m) * x_stride)[c];
-          continue;
-        }
-        const int k0 = c * 8, h = k0 / mp.D, d0 = k0 - h * mp.D;
-        const int kvh = h / mp.G, g = h - kvh * mp.G;
-        const float* pb = mp.part + (static_cast<int64_t>(m * mp.nkv + kvh) * mp.max_chunks * mp.G + g) * stride;
-        float mx = -1e30f, l = 0.f, o[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-        for (int c0 = 0; c0 < n; c0 += 4) {
-          float mm[4], ll[4];
-          float2 ov[4][4];
-#pragma unroll
-          for (int j = 0; j < 4; ++j) {
-            const float* pc = pb + min(c0 + j, n - 1) * cstride;  // clamped: loads stay batched
-            mm[j] = pc[mp.D];
-            ll[j] = pc[mp.D + 1];
-#pragma unroll
-            for (int e = 0; e < 4; ++e) ov[j][e] = reinterpret_cast<const float2*>(pc + d0)[e];
-          }
-          float gm = mx;
-#pragma unroll
-          for (int j = 0; j < 4; ++j)
-            if (c0 + j < n) gm = fmaxf(gm, mm[j]);
-          const float a = __expf(mx - gm);
-          l *= a;
-#pragma unroll
-          for (int e = 0; e < 8; ++e) o[e] *= a;
-#pragma unroll
-          for (int j = 0; j < 4; ++j) {
-            const float sc = c0 + j < n ? __expf(mm[j] - gm) : 0.f;
-            l += ll[j] * sc;
-#pragma unroll
-            for (int e = 0; e < 4; ++e) {
-              o[2 * e] += ov[j][e].x * sc;
-              o[2 * e + 1] += ov[j][e].y * sc;
-            }
-          }
-          mx = gm;
-        }
-        const float inv = 1.f / l;
-#pragma unroll
-        for (int e = 0; e < 8; ++e) o[e] *= inv;
-        reinterpret_cast<u32x4*>(xs + m * K)[c] = pack8(o);
       }
     }
   } else if (x_fast) {

@@ -21,7 +21,6 @@ from __future__ import annotations
 
 import dataclasses
 import math
-import os
 import time
 from typing import Callable, Dict, List, Optional, Sequence as Seq
 
@@ -49,7 +48,6 @@ class EngineConfig:
     steps_per_graph: int = 8
     use_graphs: bool = True
     prefill_chunk: int = 8192
-    attn_chunk: int = 0  # 0 = balanced MFMA split (>= 128 keys per block); > 0 = fixed chunk size
     init_scale: float = 1.0
     stream_priority: int = 0
     # TP prefill: shard the residual stream by token rows between layers (reduce-scatter +
@@ -60,26 +58,31 @@ class EngineConfig:
     expert_parallel: bool = False
 
 
-def attn_buckets(ctxmax: int, fixed_chunk: int = 0, blocks_per_head: int = 64) -> List[tuple]:
-    """Decode-attention shapes per context bucket: [(capacity_tokens, chunk, grid_chunks)].
+FUSED_CHUNK_SMALL, FUSED_CHUNK_LARGE = 128, 256
 
-    Default (MFMA kernel, balanced split): ``chunk`` is the minimum of 128 keys per split-KV block
-    and the kernel spreads a sequence's keys evenly over ``grid_chunks`` blocks, so the grid only
-    grows with the context until ``blocks_per_head`` (~1 block per CU over the kv heads of one
-    row, measured on MI355X: profiles/r1_attn_decode_microbench.md) and one bucket then covers
-    every longer context. ``fixed_chunk`` > 0 selects fixed-size chunks (VALU kernel when not a
-    multiple of 128): capacities double from 1024 and grid_chunks * chunk covers the bucket."""
+
+def attn_buckets(ctxmax: int, blocks_per_head: int = 64, fused_max: int = 4096) -> List[tuple]:
+    """Decode-attention shapes per context bucket: [(capacity_tokens, chunk, grid_chunks, fused)].
+
+    Capacities double from 1024. Buckets up to ``fused_max`` keys use the fused single-launch form
+    (fixed 128-key chunks up to 2048 keys, 256-key chunks above: at most 16 partials for the
+    in-launch merge; grid_chunks = capacity / chunk). Longer ones use the
+    balanced split: ``chunk`` is the minimum of 128 keys per block, the kernel spreads a
+    sequence's keys evenly over ``grid_chunks`` blocks, and the grid grows with the context until
+    ``blocks_per_head`` (~1 block per CU over the kv heads of one row, measured on MI355X:
+    profiles/r1_attn_decode_microbench.md); one bucket then covers every longer context."""
     out, cap = [], 1024
     while True:
         c = min(cap, ctxmax)
-        if fixed_chunk:
-            out.append((c, fixed_chunk, (c + fixed_chunk - 1) // fixed_chunk))
+        if c <= fused_max:
+            ch = FUSED_CHUNK_SMALL if c <= 2048 else FUSED_CHUNK_LARGE
+            out.append((c, ch, (c + ch - 1) // ch, True))
         else:
             gc = min((c + 127) // 128, blocks_per_head)
-            if out and out[-1][2] == gc:
-                out[-1] = (c, 128, gc)  # same grid: widen the previous bucket
+            if out and not out[-1][3] and out[-1][2] == gc:
+                out[-1] = (c, 128, gc, False)  # same grid: widen the previous bucket
             else:
-                out.append((c, 128, gc))
+                out.append((c, 128, gc, False))
         if cap >= ctxmax:
             return out
         cap *= 2
@@ -185,21 +188,16 @@ class Engine:
                             torch.zeros(self.tp.size, B, self.w.vocab_local, dtype=torch.float32, device=dev))
         # split-KV decode attention: one (chunk, grid) shape per context bucket
         ctxmax = self.ecfg.max_context + self.ecfg.steps_per_graph + 2
-        # target blocks per decode row: ~1 per CU; without GQA (Phi-3: one query head per kv head)
-        # a block's key range costs less, and 2 per CU measured faster (9.45 vs 9.85 us at 2k keys,
-        # 14.9 vs 15.9 at 4k: profiles/r1_attn_decode_tp_shapes.md)
-        blocks = int(os.environ.get("LLMC_ATTN_BLOCKS", "512" if self.nh == self.nkv else "256"))
-        fixed = self.ecfg.attn_chunk or (0 if ops.ATTN_DECODE_MODE >= 2 else 128)  # VALU modes: fixed chunks
-        self.attn_buckets = attn_buckets(ctxmax, fixed, max(1, blocks // self.nkv))
-        self.max_chunks = max(gc for _, _, gc in self.attn_buckets)
-        # LLMC_ATTN_MERGE=1: merge the split-KV partials in o_proj's prologue instead of the reduce
-        # launch. Measured SLOWER on MI355X (8B decode 2.95 vs 2.90 ms/token at 2k context, 3.72
-        # vs 3.61 at 33k: every o_proj block re-reads all partials and the chunk groups are
-        # dependent L2 round trips before its weight stream resumes), so it is off by default.
-        self._attn_merge = (self.on_gpu and ops.ATTN_DECODE_MODE == 2 and fixed == 0
-                            and os.environ.get("LLMC_ATTN_MERGE", "0") == "1")
-        self.attn_part, self.attn_counters = ops.decode_attn_workspace(B, self.nh, self.nkv, self.D,
-                                                                        self.max_chunks, dev)
+        # target blocks per decode row (split form): ~1 per CU; without GQA (Phi-3: one query head
+        # per kv head) a block's key range costs less, and 2 per CU measured faster (9.45 vs 9.85 us
+        # at 2k keys, 14.9 vs 15.9 at 4k: profiles/r1_attn_decode_tp_shapes.md)
+        blocks = 512 if self.nh == self.nkv else 256
+        fused_max = ops.FUSED_ATTN_MAX_KEYS if self.bs % 32 == 0 else 0
+        self.attn_buckets = attn_buckets(ctxmax, max(1, blocks // self.nkv), fused_max)
+        split_chunks = max([gc for _, _, gc, f in self.attn_buckets if not f] or [1])
+        fused_chunks = max([gc for _, _, gc, f in self.attn_buckets if f] or [1])
+        self.attn_part, self.attn_counters = ops.decode_attn_workspace(B, self.nh, self.nkv, self.D, split_chunks, dev)
+        self.attn_part_f, _ = ops.decode_attn_workspace(B, self.nh, self.nkv, self.D, fused_chunks, dev, fused=True)
         if self.on_gpu:
             P = ops.sample_parts()
             self.ws_v = torch.zeros(B, P, dtype=torch.float32, device=dev)
@@ -492,26 +490,17 @@ class Engine:
     def _decode_step(self, B: int, bucket: Optional[int] = None) -> None:
         """One token for rows 0..B-1. ``bucket`` indexes ``attn_buckets`` (default: the largest)."""
         c = self.cfg
-        _, chunk, grid_chunks = self.attn_buckets[-1 if bucket is None else bucket]
+        _, chunk, grid_chunks, fused = self.attn_buckets[-1 if bucket is None else bucket]
+        part = self.attn_part_f if fused else self.attn_part
         h, q, attn, act = self.h[:B], self.q[:B], self.attn[:B], self.act[:B]
         ops.embedding(self.tokens_in[:B], self.w.embed, out=h)
         for li, Lw in enumerate(self.w.layers):
             ops.qkv_rope(h, Lw.w_qkv, Lw.ln1, c.rms_eps, q, self.k_cache[li], self.v_cache[li], self.positions[:B],
                          self.slots[:B], self.cos_t, self.sin_t, self.nh, self.nkv, self.D, self.bs)
-            if self._attn_merge:
-                # split-KV partials merged inside the o_proj GEMV's prologue (no reduce launch)
-                ops.attn_decode(q, self.k_cache[li], self.v_cache[li], self.block_tables[:B], self.seq_lens[:B], attn,
-                                self.attn_part[:B], self.attn_counters[:B], self.nh, self.nkv, self.D, self.bs,
-                                chunk, self.scale, grid_chunks, mode=4)
-                ops.attn_o_proj(attn, self.attn_part[:B], self.seq_lens[:B], Lw.w_o, h,
-                                EPI_RESADD if self.tp.rank == 0 else EPI_BF16, self.nh, self.nkv, self.D, chunk,
-                                grid_chunks)
-                self.tp.all_reduce_(h)
-            else:
-                ops.attn_decode(q, self.k_cache[li], self.v_cache[li], self.block_tables[:B], self.seq_lens[:B], attn,
-                                self.attn_part[:B], self.attn_counters[:B], self.nh, self.nkv, self.D, self.bs,
-                                chunk, self.scale, grid_chunks)
-                self._row_parallel(attn, Lw.w_o, h)
+            ops.attn_decode(q, self.k_cache[li], self.v_cache[li], self.block_tables[:B], self.seq_lens[:B], attn,
+                            part[:B], self.attn_counters[:B], self.nh, self.nkv, self.D, self.bs, chunk, self.scale,
+                            grid_chunks, fused=fused)
+            self._row_parallel(attn, Lw.w_o, h)
             if c.is_moe:
                 self._moe_decode(h, Lw, B)
             else:
@@ -582,7 +571,7 @@ class Engine:
     def _bucket(self, ctx_tokens: int) -> int:
         """Smallest attention bucket covering ``ctx_tokens`` (so a short context's graph does not
         launch thousands of empty blocks)."""
-        for i, (cap, _, _) in enumerate(self.attn_buckets):
+        for i, (cap, _, _, _) in enumerate(self.attn_buckets):
             if cap >= ctx_tokens:
                 return i
         return len(self.attn_buckets) - 1

@@ -165,49 +165,36 @@ def qkv_rope(x, W, norm_w, eps, q_out, k_cache, v_cache, positions, slots, cos_t
                             nh, nkv, D, bs, _s(x))
 
 
-def decode_attn_workspace(B, nh, nkv, D, max_chunks, device):
-    """(part, counters) for attn_decode: f32 partials [B, nkv, max_chunks, G, D+2] and zeroed tickets."""
+FUSED_ATTN_MAX_KEYS = 4096  # decode attention: fused single-launch form up to this bucket capacity
+FUSED_CHUNK = 128           # keys per block of the fused form
+
+
+def decode_attn_workspace(B, nh, nkv, D, max_chunks, device, fused: bool = False):
+    """(part, counters) for attn_decode: f32 partials [B, nkv, max_chunks, G, D + 2] (split form)
+    or [B, nkv, max_chunks, G, D + 4] (fused form: 16-B rows), and zeroed merge tickets [B, nkv]."""
     G = nh // nkv
-    part = torch.zeros(B, nkv, max_chunks, G, D + 2, dtype=torch.float32, device=device)
+    part = torch.zeros(B, nkv, max_chunks, G, D + (4 if fused else 2), dtype=torch.float32, device=device)
     counters = torch.zeros(B, nkv, dtype=torch.int32, device=device)
     return part, counters
 
 
-# decode attention kernel: 2 = MFMA balanced split + reduce kernel (default), 3 = MFMA with the
-# in-launch last-arriver reduce, 0 = VALU fixed chunks + reduce kernel, 1 = VALU + in-launch
-# reduce, 4 = MFMA leaving the partials to the o_proj GEMV's merge prologue (attn_o_proj; the
-# engine's decode step uses it with LLMC_ATTN_MERGE=1; measured slower, off by default). MFMA modes need chunk % 128 == 0 (else
-# mode 0 runs).
-ATTN_DECODE_MODE = int(os.environ.get("LLMC_ATTN_MODE", "2"))
-
-
 def attn_decode(q, k_cache, v_cache, block_tables, seq_lens, out, part, counters, nh, nkv, D, bs, chunk, scale,
-                grid_chunks: Optional[int] = None, mode: Optional[int] = None):
+                grid_chunks: Optional[int] = None, fused: bool = False):
+    """Decode attention (K5). ``fused``: fixed 128-key chunks (``grid_chunks`` = bucket capacity /
+    128) merged in the same launch — short contexts; else the balanced split over <= grid_chunks
+    blocks of >= ``chunk`` keys + the reduce launch — long contexts. ``part`` must come from
+    ``decode_attn_workspace(..., fused=fused)``."""
     if not q.is_cuda:
         out.copy_(oracle.attn_decode(q, k_cache, v_cache, block_tables, seq_lens, nh, nkv, D, bs, scale))
         return out
     B = q.shape[0]
     max_chunks = part.shape[2]
     gc = max_chunks if grid_chunks is None else min(grid_chunks, max_chunks)
-    if mode is None:
-        mode = ATTN_DECODE_MODE if (ATTN_DECODE_MODE < 2 or chunk % 128 == 0) else 0
+    if part.shape[-1] != D + (4 if fused else 2):
+        raise ValueError("attn_decode: workspace layout does not match the kernel form")
     kernels().attn_decode(_p(q), q.stride(0), _p(k_cache), _p(v_cache), _p(block_tables), block_tables.stride(0),
-                          _p(seq_lens), _p(part), _p(counters), _p(out), out.stride(0), B, nh, nkv, D, bs, chunk, gc,
-                          max_chunks, float(scale), mode, _s(q))
-    return out
-
-
-def attn_o_proj(attn, part, seq_lens, W, out, epi, nh, nkv, D, chunk, grid_chunks):
-    """Decode o_proj with the split-KV merge fused in: ``attn`` holds the attention output of rows
-    whose sequence took one chunk, ``part`` the per-chunk partials of an ``attn_decode(...,
-    mode=4)`` launch with the same ``chunk``/``grid_chunks``; ``out`` (+)= merge(...) @ W^T."""
-    if not attn.is_cuda:
-        return oracle.linear(attn, W, epi, out)
-    M, K = attn.shape
-    max_chunks = part.shape[2]
-    gc = min(grid_chunks, max_chunks)
-    kernels().gemv_attn_merge(M, _p(attn), attn.stride(0), _p(part), _p(seq_lens), nkv, nh // nkv, D, gc, chunk,
-                              max_chunks, _p(W), _p(out), out.stride(0), W.shape[0], K, epi, _s(attn))
+                          _p(seq_lens), _p(part), _p(counters), _p(out), out.stride(0), B, nh, nkv, D, bs,
+                          k_cache.shape[0], chunk, gc, max_chunks, float(scale), 1 if fused else 0, _s(q))
     return out
 
 

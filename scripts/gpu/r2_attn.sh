@@ -1,0 +1,5 @@
+set -o pipefail
+cd $GRAFT_REPO_ROOT
+mkdir -p gpurun_out
+timeout -k 10 600 python -u -m pytest tests/test_kernels_gpu.py tests/test_engine_gpu.py tests/test_batcher.py -x -q --timeout 300 --timeout-method thread > gpurun_out/r2_attn_tests.log 2>&1 && \
+timeout -k 10 300 python scripts/microbench_kernels.py attn > gpurun_out/r2_attn_microbench.log 2>&1

@@ -37,97 +37,51 @@ def timeit(fn, iters=50, warm=5):
     return a.elapsed_time(b) * 1000 / (10 * iters)  # us
 
 
-def bench_attn():
-    """VALU fixed chunks (mode 0) vs the MFMA balanced split (mode 2, min 128 keys per block) at
-    several grid sizes (blocks per kv head)."""
-    nh, nkv, D, bs = 32, 8, 128, 64
-    for L in [128, 600, 2048, 4096, 16384, 33000, 65000]:
-        nb = (L + bs - 1) // bs + 2
-        kc = torch.randn(nb, nkv, bs, D, device="cuda").to(BF)
-        vc = torch.randn_like(kc)
-        bt = torch.arange(nb, dtype=torch.int32, device="cuda").view(1, -1)
-        sl = torch.tensor([L], dtype=torch.int32, device="cuda")
-        q = torch.randn(1, nh * D, device="cuda").to(BF)
-        out = torch.empty(1, nh * D, dtype=BF, device="cuda")
-        gb = L * nkv * D * 2 * 2 / 1e9
-        line = []
-        for chunk in [64, 256]:
-            mc = (L + chunk - 1) // chunk
-            part, ctr = ops.decode_attn_workspace(1, nh, nkv, D, max(mc, 1), "cuda")
-            us = timeit(lambda: ops.attn_decode(q, kc, vc, bt, sl, out, part, ctr, nh, nkv, D, bs, chunk,
-                                                1 / math.sqrt(D), mode=0))
-            line.append(f"valu c{chunk} {us:6.2f}")
-        best = 1e9
-        for mode in (2, 3):
-            for gc in [16, 24, 32, 48, 64]:
-                gc_eff = min(gc, (L + 127) // 128)
-                part, ctr = ops.decode_attn_workspace(1, nh, nkv, D, gc_eff, "cuda")
-                us = timeit(lambda: ops.attn_decode(q, kc, vc, bt, sl, out, part, ctr, nh, nkv, D, bs, 128,
-                                                    1 / math.sqrt(D), grid_chunks=gc_eff, mode=mode))
-                best = min(best, us)
-                line.append(f"m{mode} g{gc} {us:6.2f}")
-        print(f"attn L={L:6d}: " + "  ".join(line) + f"  | best {gb / best * 1e6 / 1e3:5.2f} TB/s")
+def _attn_case(L, nh, nkv, D, bs=64, B=1):
+    nb = B * ((L + bs - 1) // bs) + 2
+    kc = torch.randn(nb, nkv, bs, D, device="cuda").to(BF)
+    vc = torch.randn_like(kc)
+    per = (L + bs - 1) // bs
+    bt = torch.randperm(nb, device="cuda")[: B * per].view(B, per).to(torch.int32)
+    sl = torch.full((B,), L, dtype=torch.int32, device="cuda")
+    q = torch.randn(B, nh * D, device="cuda").to(BF)
+    out = torch.empty(B, nh * D, dtype=BF, device="cuda")
+    return kc, vc, bt, sl, q, out
 
 
-def bench_attn_phi3():
-    """Phi-3-mini decode attention (32 heads = 32 kv heads, D = 96, no GQA) over the grid size."""
-    nh = nkv = 32
-    D, bs = 96, 64
-    for L in [512, 1024, 2048, 4096]:
-        nb = (L + bs - 1) // bs + 2
-        kc = torch.randn(nb, nkv, bs, D, device="cuda").to(BF)
-        vc = torch.randn_like(kc)
-        bt = torch.arange(nb, dtype=torch.int32, device="cuda").view(1, -1)
-        sl = torch.tensor([L], dtype=torch.int32, device="cuda")
-        q = torch.randn(1, nh * D, device="cuda").to(BF)
-        out = torch.empty(1, nh * D, dtype=BF, device="cuda")
-        line = []
-        for gc in [1, 2, 4, 8, 16, 32]:
-            gc_eff = min(gc, (L + 127) // 128)
-            if gc_eff < gc:
-                continue
-            part, ctr = ops.decode_attn_workspace(1, nh, nkv, D, gc_eff, "cuda")
-            t2 = timeit(lambda: ops.attn_decode(q, kc, vc, bt, sl, out, part, ctr, nh, nkv, D, bs, 128,
-                                                1 / math.sqrt(D), grid_chunks=gc_eff, mode=2))
-            t4 = timeit(lambda: ops.attn_decode(q, kc, vc, bt, sl, out, part, ctr, nh, nkv, D, bs, 128,
-                                                1 / math.sqrt(D), grid_chunks=gc_eff, mode=4))
-            line.append(f"g{gc_eff}: {t2:5.2f} (attn {t4:5.2f})")
-        for chunk in (64, 128, 256):  # VALU split-KV kernel, fixed chunks (mode 0)
-            mc = (L + chunk - 1) // chunk
-            part, ctr = ops.decode_attn_workspace(1, nh, nkv, D, mc, "cuda")
-            t0 = timeit(lambda: ops.attn_decode(q, kc, vc, bt, sl, out, part, ctr, nh, nkv, D, bs, chunk,
-                                                1 / math.sqrt(D), mode=0))
-            line.append(f"valu c{chunk}: {t0:5.2f}")
-        print(f"phi3 attn L={L:6d}: " + "  ".join(line), flush=True)
-
-
-def bench_attn_tp():
-    """Decode attention at the per-rank head counts of a tensor-parallel Llama-3-8B (TP = 1, 2, 4,
-    8 -> 8, 4, 2, 1 kv heads, GQA group 4): attention alone (mode 4 = MFMA partials, no merge)
-    and attention + reduce kernel (mode 2) over the grid size (blocks per kv head)."""
-    D, bs = 128, 64
-    for nkv in [8, 4, 2, 1]:
-        nh = 4 * nkv
-        for L in [2048, 8192, 33000]:
-            nb = (L + bs - 1) // bs + 2
-            kc = torch.randn(nb, nkv, bs, D, device="cuda").to(BF)
-            vc = torch.randn_like(kc)
-            bt = torch.arange(nb, dtype=torch.int32, device="cuda").view(1, -1)
-            sl = torch.tensor([L], dtype=torch.int32, device="cuda")
-            q = torch.randn(1, nh * D, device="cuda").to(BF)
-            out = torch.empty(1, nh * D, dtype=BF, device="cuda")
+def bench_attn(shapes=((32, 8, 128), (32, 32, 96), (16, 2, 128), (8, 1, 128))):
+    """Decode attention per layer (graph-timed, random paged K/V): the fused single-launch form
+    (fixed 128-key chunks, in-launch merge; the engine's form for buckets <= 4096 keys) vs the
+    balanced split + reduce launch over its grid sizes (blocks per kv head)."""
+    for nh, nkv, D in shapes:
+        for L in [128, 600, 1024, 2048, 4096, 8192, 16384, 33000]:
+            kc, vc, bt, sl, q, out = _attn_case(L, nh, nkv, D)
+            sc = 1 / math.sqrt(D)
+            gb = L * nkv * D * 2 * 2 / 1e9
             line = []
-            for gc in [16, 32, 64, 128, 256, 512]:
+            best = 1e9
+            if L <= 4096:
+                cap = 1024
+                while cap < L:
+                    cap *= 2
+                for ch in (128, 256):
+                    gc = cap // ch
+                    part, ctr = ops.decode_attn_workspace(1, nh, nkv, D, gc, "cuda", fused=True)
+                    us = timeit(lambda: ops.attn_decode(q, kc, vc, bt, sl, out, part, ctr, nh, nkv, D, 64, ch, sc,
+                                                        grid_chunks=gc, fused=True))
+                    best = min(best, us)
+                    line.append(f"fused c{ch} {us:6.2f}")
+            for gc in [16, 32, 64, 128, 256]:
                 gc_eff = min(gc, (L + 127) // 128)
                 if gc_eff < gc and gc > 16:
                     continue
                 part, ctr = ops.decode_attn_workspace(1, nh, nkv, D, gc_eff, "cuda")
-                t2 = timeit(lambda: ops.attn_decode(q, kc, vc, bt, sl, out, part, ctr, nh, nkv, D, bs, 128,
-                                                    1 / math.sqrt(D), grid_chunks=gc_eff, mode=2))
-                t4 = timeit(lambda: ops.attn_decode(q, kc, vc, bt, sl, out, part, ctr, nh, nkv, D, bs, 128,
-                                                    1 / math.sqrt(D), grid_chunks=gc_eff, mode=4))
-                line.append(f"g{gc_eff}: {t2:5.2f} (attn {t4:5.2f})")
-            print(f"attn nkv={nkv} L={L:6d}: " + "  ".join(line), flush=True)
+                us = timeit(lambda: ops.attn_decode(q, kc, vc, bt, sl, out, part, ctr, nh, nkv, D, 64, 128, sc,
+                                                    grid_chunks=gc_eff))
+                best = min(best, us)
+                line.append(f"split g{gc_eff} {us:6.2f}")
+            print(f"attn nh={nh} nkv={nkv} D={D} L={L:6d}: " + "  ".join(line)
+                  + f"  | best {gb / best * 1e6 / 1e3:5.2f} TB/s", flush=True)
 
 
 def bench_gemv():
@@ -259,10 +213,6 @@ if __name__ == "__main__":
         bench_attn()
     if what in ("gemv", "all"):
         bench_gemv()
-    if what in ("attn-phi3",):
-        bench_attn_phi3()
-    if what in ("attn-tp",):
-        bench_attn_tp()
     if what in ("sweep",):
         bench_gemv_sweep()
     if what in ("sweep-phi3",):  # Phi-3-mini shapes (K = 3072 / 8192)

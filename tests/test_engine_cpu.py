@@ -106,10 +106,14 @@ def test_attn_buckets_cover_context():
     for ctxmax in [100, 1024, 4106, 16394, 131082]:
         bks = attn_buckets(ctxmax)
         assert bks[-1][0] == ctxmax
-        for cap, chunk, gc in bks:
-            assert chunk == 128 and 1 <= gc <= 64
+        for cap, chunk, gc, fused in bks:
+            if fused:  # fixed 128/256-key chunks cover the bucket, <= 16 partials to merge
+                assert cap <= 4096 and gc * chunk >= cap and gc <= 16 and chunk in (128, 256)
+            else:
+                assert chunk == 128 and cap > 4096 and 1 <= gc <= 64
         assert [b[0] for b in bks] == sorted(b[0] for b in bks)
-        assert len({b[2] for b in bks}) == len(bks)  # one graph per distinct grid
-    assert attn_buckets(131082, 0, 32)[-1] == (131082, 128, 32)
-    fixed = attn_buckets(4106, 64)
-    assert {c for _, c, _ in fixed} == {64} and all(gc * 64 >= cap for cap, _, gc in fixed)
+        split = [b[2] for b in bks if not b[3]]
+        assert len(set(split)) == len(split)  # one graph per distinct split grid
+    assert attn_buckets(131082, 32)[-1] == (131082, 128, 32, False)
+    assert [b[3] for b in attn_buckets(4106)] == [True, True, True, False]
+    assert all(not b[3] for b in attn_buckets(4106, fused_max=0))

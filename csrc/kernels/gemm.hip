@@ -149,18 +149,267 @@ __global__ __launch_bounds__(256, 2) void gemm_kernel(const bf16_t* __restrict__
     }
 }
 
+// ---------------------------------------------------------------------------------------------
+// Dense prefill GEMM (K6, M >= 5): the 256 x 256 tile, 8-wave, 4-phase-per-K-step template
+// (cdna_hip_programming.md §5 "The 256² 8-phase template", T1-T5), re-derived for C = A . W^T with
+// both operands K-contiguous:
+//  * waves 2 (M) x 4 (N), each owning a 128 x 64 output block = 8 x 4 tiles of
+//    mfma_f32_16x16x32_bf16 with the operands SWAPPED (W fragment as A, activation fragment as B:
+//    D[n][m]) so each lane ends with 4 consecutive output columns of one row -> 8-B/16-B stores.
+//  * each K-step (64) is consumed in 4 phases by output quadrant of the wave's block:
+//      P1 A rows 0-63 + W cols 0-31 -> q(0,0);  P2 W cols 32-63 -> q(0,1);
+//      P3 A rows 64-127             -> q(1,1);  P4 (no reads)   -> q(1,0)
+//    so every operand byte of the K-step is read from LDS exactly once, and each "quarter" of a
+//    K-step's operands (A0 / W0 / W1 / A1: 128 rows x 64 K = 16 KiB, the rows the 8 waves read in
+//    one phase) has a single last-read phase.
+//  * LDS is a RING of 10 quarter slots (160 KiB, one block per CU): quarter n (= 4 * kstep + j)
+//    lives in slot n % 10 and is fetched by global_load_lds_dwordx4 (2 per thread) FOUR phases
+//    after the quarter it replaces was last read, and waited for (counted `s_waitcnt vmcnt(8)`,
+//    never 0 in the main loop) four phases before its first read: ~4 phases of MFMA work hide
+//    every fetch, and no barrier drains the load queue.
+//  * ping-pong: the two wave rows run one barrier apart (waves 4-7 take one extra barrier up
+//    front), so one row's LDS reads + load issue overlap the other row's MFMA cluster on the same
+//    SIMD; s_setprio(1) around each MFMA cluster keeps hipcc from scattering it (T5).
+//  * LDS XOR swizzle chunk ^ ((row >> 1) & 7) (128-B rows): applied to the per-lane SOURCE address
+//    of the lane-linear LDS-DMA and again on the ds_read_b128 address (rule 21): conflict-free.
+//  * grid: bijective XCD remap (T1) then grouped tile order (8 M-tiles x all N per group) so the
+//    ~32 tiles an XCD runs at once share 8 activation panels and 4 weight panels in its L2.
+//  * fused epilogues: bf16 | f32 | residual add (C += A.W^T) | SiLU-mul of interleaved gate/up
+//    columns (C[m][n/2] = silu(g) * u) — the same f32-accumulate, one-rounding numerics.
+constexpr int kT = 256, kTK = 64;
+constexpr int kQuarter = 128 * kTK * 2;  // bytes
+constexpr int kSlots = 10;
+constexpr int kGroupM = 8;
+
+template <int EPI>
+__global__ __launch_bounds__(512, 1) void gemm256_kernel(const bf16_t* __restrict__ A, int lda,
+                                                        const bf16_t* __restrict__ W, int ldw, void* __restrict__ C,
+                                                        int ldc, int M, int N, int K) {
+  __shared__ __attribute__((aligned(16))) char smem[kSlots * kQuarter];
+  const int num_m = (M + kT - 1) / kT, num_n = (N + kT - 1) / kT;
+  const int id = xcd_remap(blockIdx.x, num_m * num_n);
+  const int group = id / (kGroupM * num_n);
+  const int first_m = group * kGroupM;
+  const int gsz = min(num_m - first_m, kGroupM);
+  const int in_group = id - group * kGroupM * num_n;
+  const int m0 = (first_m + in_group % gsz) * kT, n0 = (in_group / gsz) * kT;
+
+  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+  const int wr = wave >> 2, wc = wave & 3;
+  const int l16 = lane & 15, lg = lane >> 4;
+
+  // per-thread LDS-DMA sources: quarter j (0 A0, 1 W0, 2 W1, 3 A1) x 2 instructions
+  const bf16_t* src[4][2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int s = i * 512 + tid;
+    const int r = s >> 3, c = (s & 7) ^ ((r >> 1) & 7);
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const int ar = min(m0 + (r >> 6) * 128 + h * 64 + (r & 63), M - 1);
+      const int wrow = min(n0 + (r >> 5) * 64 + h * 32 + (r & 31), N - 1);
+      src[h == 0 ? 0 : 3][i] = A + static_cast<int64_t>(ar) * lda + c * 8;
+      src[1 + h][i] = W + static_cast<int64_t>(wrow) * ldw + c * 8;
+    }
+  }
+  const int nk = K / kTK, nq = 4 * nk;
+  auto stage = [&](int n) {  // quarter n -> ring slot n % 10 (wave-uniform LDS base + lane * 16)
+    const int j = n & 3, k0 = (n >> 2) * kTK;
+    char* q = smem + (n % kSlots) * kQuarter;
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+      __builtin_amdgcn_global_load_lds((const void*)(src[j][i] + k0),
+                                       (__attribute__((address_space(3))) void*)(q + (i * 512 + wave * 64) * 16), 16, 0, 0);
+  };
+  auto lds_off = [&](int r, int c) { return r * 128 + ((c ^ ((r >> 1) & 7)) << 4); };
+
+  f32x4 acc[8][4];
+#pragma unroll
+  for (int a = 0; a < 8; ++a)
+#pragma unroll
+    for (int b = 0; b < 4; ++b) acc[a][b] = f32x4{0.f, 0.f, 0.f, 0.f};
+  bf16x8 af[4][2], bw0[2][2], bw1[2][2];
+
+  // prologue: quarters 0..5 (k-step 0 and the first half of k-step 1) in flight, step 0 landed
+  for (int n = 0; n < 6 && n < nq; ++n) stage(n);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  asm volatile("s_barrier" ::: "memory");
+  __builtin_amdgcn_sched_barrier(0);
+  if (wr == 1) asm volatile("s_barrier" ::: "memory");  // ping-pong: wave row 1 runs one barrier behind
+  __builtin_amdgcn_sched_barrier(0);
+
+  // one phase: [reads] [LDS-DMA of quarter n] counted wait | barrier | MFMA cluster | barrier
+  // the "memory" clobbers keep LDS reads from moving across the barriers (the intrinsic alone
+  // is not a memory barrier for the compiler); sched_barrier(0) pins the MFMA clusters
+  auto sync_wait = [&](int n_issue) {
+    if (n_issue < nq) {
+      stage(n_issue);
+      asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+    } else {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    __builtin_amdgcn_sched_barrier(0);
+    asm volatile("s_barrier" ::: "memory");
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_sched_barrier(0);
+  };
+  auto end_phase = [&]() {
+    __builtin_amdgcn_sched_barrier(0);
+    asm volatile("s_barrier" ::: "memory");
+    __builtin_amdgcn_sched_barrier(0);
+  };
+
+  for (int t = 0; t < nk; ++t) {
+    const char* qa0 = smem + ((4 * t + 0) % kSlots) * kQuarter;
+    const char* qw0 = smem + ((4 * t + 1) % kSlots) * kQuarter;
+    const char* qw1 = smem + ((4 * t + 2) % kSlots) * kQuarter;
+    const char* qa1 = smem + ((4 * t + 3) % kSlots) * kQuarter;
+    // ---- P1: A rows 0-63, W cols 0-31 -> q(0,0)
+#pragma unroll
+    for (int ni = 0; ni < 2; ++ni)
+#pragma unroll
+      for (int kk = 0; kk < 2; ++kk)
+        bw0[ni][kk] = *reinterpret_cast<const bf16x8*>(qw0 + lds_off(wc * 32 + ni * 16 + l16, kk * 4 + lg));
+#pragma unroll
+    for (int mi = 0; mi < 4; ++mi)
+#pragma unroll
+      for (int kk = 0; kk < 2; ++kk)
+        af[mi][kk] = *reinterpret_cast<const bf16x8*>(qa0 + lds_off(wr * 64 + mi * 16 + l16, kk * 4 + lg));
+    sync_wait(4 * t + 6);
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int mi = 0; mi < 4; ++mi)
+#pragma unroll
+      for (int ni = 0; ni < 2; ++ni)
+#pragma unroll
+        for (int kk = 0; kk < 2; ++kk)
+          acc[mi][ni] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bw0[ni][kk], af[mi][kk], acc[mi][ni], 0, 0, 0);
+    __builtin_amdgcn_s_setprio(0);
+    end_phase();
+    // ---- P2: W cols 32-63 -> q(0,1)
+#pragma unroll
+    for (int ni = 0; ni < 2; ++ni)
+#pragma unroll
+      for (int kk = 0; kk < 2; ++kk)
+        bw1[ni][kk] = *reinterpret_cast<const bf16x8*>(qw1 + lds_off(wc * 32 + ni * 16 + l16, kk * 4 + lg));
+    sync_wait(4 * t + 7);
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int mi = 0; mi < 4; ++mi)
+#pragma unroll
+      for (int ni = 0; ni < 2; ++ni)
+#pragma unroll
+        for (int kk = 0; kk < 2; ++kk)
+          acc[mi][2 + ni] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bw1[ni][kk], af[mi][kk], acc[mi][2 + ni], 0, 0, 0);
+    __builtin_amdgcn_s_setprio(0);
+    end_phase();
+    // ---- P3: A rows 64-127 -> q(1,1)
+#pragma unroll
+    for (int mi = 0; mi < 4; ++mi)
+#pragma unroll
+      for (int kk = 0; kk < 2; ++kk)
+        af[mi][kk] = *reinterpret_cast<const bf16x8*>(qa1 + lds_off(wr * 64 + mi * 16 + l16, kk * 4 + lg));
+    sync_wait(4 * t + 8);
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int mi = 0; mi < 4; ++mi)
+#pragma unroll
+      for (int ni = 0; ni < 2; ++ni)
+#pragma unroll
+        for (int kk = 0; kk < 2; ++kk)
+          acc[4 + mi][2 + ni] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bw1[ni][kk], af[mi][kk], acc[4 + mi][2 + ni], 0, 0, 0);
+    __builtin_amdgcn_s_setprio(0);
+    end_phase();
+    // ---- P4: no reads -> q(1,0)
+    sync_wait(4 * t + 9);
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int mi = 0; mi < 4; ++mi)
+#pragma unroll
+      for (int ni = 0; ni < 2; ++ni)
+#pragma unroll
+        for (int kk = 0; kk < 2; ++kk)
+          acc[4 + mi][ni] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bw0[ni][kk], af[mi][kk], acc[4 + mi][ni], 0, 0, 0);
+    __builtin_amdgcn_s_setprio(0);
+    end_phase();
+  }
+  if (wr == 0) asm volatile("s_barrier" ::: "memory");  // balance the ping-pong offset
+
+  // ---- epilogue: lane holds C[m][n .. n + 3], m = row of l16, n = 4 * lg within each 16x16 tile
+  const bool vec_ok = (N % 4 == 0) && (ldc % 4 == 0);
+#pragma unroll
+  for (int mi = 0; mi < 8; ++mi) {
+    const int m = m0 + wr * 128 + mi * 16 + l16;
+    if (m >= M) continue;
+#pragma unroll
+    for (int ni = 0; ni < 4; ++ni) {
+      const int n = n0 + wc * 64 + ni * 16 + 4 * lg;
+      const f32x4 v = acc[mi][ni];
+      if constexpr (EPI == 3) {  // SiLU(gate) * up over interleaved (gate, up) column pairs
+        float o[2];
+#pragma unroll
+        for (int p = 0; p < 2; ++p) {
+          const float g = v[2 * p], u = v[2 * p + 1];
+          o[p] = g / (1.f + __expf(-g)) * u;
+        }
+        bf16_t* crow = reinterpret_cast<bf16_t*>(C) + static_cast<int64_t>(m) * ldc;
+        if (vec_ok && n + 3 < N) {
+          *reinterpret_cast<uint32_t*>(crow + n / 2) = pack_bf16x2(o[0], o[1]);
+        } else {
+#pragma unroll
+          for (int p = 0; p < 2; ++p)
+            if (n + 2 * p + 1 < N) crow[n / 2 + p] = f32_to_bf16(o[p]);
+        }
+      } else if constexpr (EPI == 1) {
+        float* crow = reinterpret_cast<float*>(C) + static_cast<int64_t>(m) * ldc;
+        if (vec_ok && n + 3 < N) {
+          *reinterpret_cast<f32x4*>(crow + n) = v;
+        } else {
+#pragma unroll
+          for (int e = 0; e < 4; ++e)
+            if (n + e < N) crow[n + e] = v[e];
+        }
+      } else {
+        bf16_t* crow = reinterpret_cast<bf16_t*>(C) + static_cast<int64_t>(m) * ldc;
+        if (vec_ok && n + 3 < N) {
+          float o[4] = {v[0], v[1], v[2], v[3]};
+          if constexpr (EPI == 2) {
+            const u32x2 old = *reinterpret_cast<const u32x2*>(crow + n);
+            o[0] += bf16_lo(old[0]);
+            o[1] += bf16_hi(old[0]);
+            o[2] += bf16_lo(old[1]);
+            o[3] += bf16_hi(old[1]);
+          }
+          *reinterpret_cast<u32x2*>(crow + n) = u32x2{pack_bf16x2(o[0], o[1]), pack_bf16x2(o[2], o[3])};
+        } else {
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            if (n + e >= N) continue;
+            const float x = EPI == 2 ? bf16_to_f32(crow[n + e]) + v[e] : v[e];
+            crow[n + e] = f32_to_bf16(x);
+          }
+        }
+      }
+    }
+  }
+}
+
 }  // namespace llmc
 
 using namespace llmc;
 
+// C[M, N] (+)= A[M, K] . W[N, K]^T. epi: 0 bf16, 1 f32, 2 C += (bf16), 3 SiLU-mul of interleaved
+// gate/up columns into C[M, N / 2] (bf16). K must be a multiple of 64.
 extern "C" int llmc_gemm(const void* A, int lda, const void* W, int ldw, void* C, int ldc, int M, int N, int K,
                          int epi, hipStream_t s) {
-  if (K % kBK != 0 || M <= 0 || N <= 0) return -1;
-  const int nwg = ((M + kBM - 1) / kBM) * ((N + kBN - 1) / kBN);
+  if (K % kTK != 0 || M <= 0 || N <= 0 || K <= 0 || (epi == 3 && N % 2 != 0)) return -1;
+  if (lda % 8 != 0 || ldw % 8 != 0) return -1;  // 16-B aligned rows for the LDS-DMA
+  const int nwg = ((M + kT - 1) / kT) * ((N + kT - 1) / kT);
   switch (epi) {
-    case 0: gemm_kernel<0, false><<<nwg, 256, 0, s>>>((const bf16_t*)A, lda, (const bf16_t*)W, ldw, C, ldc, M, N, K); break;
-    case 1: gemm_kernel<1, false><<<nwg, 256, 0, s>>>((const bf16_t*)A, lda, (const bf16_t*)W, ldw, C, ldc, M, N, K); break;
-    case 2: gemm_kernel<2, false><<<nwg, 256, 0, s>>>((const bf16_t*)A, lda, (const bf16_t*)W, ldw, C, ldc, M, N, K); break;
+    case 0: gemm256_kernel<0><<<nwg, 512, 0, s>>>((const bf16_t*)A, lda, (const bf16_t*)W, ldw, C, ldc, M, N, K); break;
+    case 1: gemm256_kernel<1><<<nwg, 512, 0, s>>>((const bf16_t*)A, lda, (const bf16_t*)W, ldw, C, ldc, M, N, K); break;
+    case 2: gemm256_kernel<2><<<nwg, 512, 0, s>>>((const bf16_t*)A, lda, (const bf16_t*)W, ldw, C, ldc, M, N, K); break;
+    case 3: gemm256_kernel<3><<<nwg, 512, 0, s>>>((const bf16_t*)A, lda, (const bf16_t*)W, ldw, C, ldc, M, N, K); break;
     default: return -2;
   }
   return static_cast<int>(hipGetLastError());

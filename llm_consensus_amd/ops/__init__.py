@@ -8,7 +8,6 @@ stream, so every op is capturable in a HIP graph.
 
 from __future__ import annotations
 
-import os
 from typing import Optional
 
 import torch
@@ -18,8 +17,6 @@ from . import oracle
 
 EPI_BF16, EPI_F32, EPI_RESADD, EPI_SILU, EPI_ROPE = 0, 1, 2, 3, 4
 GEMV_MAX_M = 4
-PREFILL_GEMM = os.environ.get("LLMC_PREFILL_GEMM", "blas")  # "blas" (hipBLASLt) | "hip" (ours)
-PREFILL_BLAS_MIN_M = 64
 
 
 def _p(t: Optional[torch.Tensor]) -> int:
@@ -75,14 +72,10 @@ def linear(x: torch.Tensor, W: torch.Tensor, epi: int = EPI_BF16, out: Optional[
            norm_w: Optional[torch.Tensor] = None, eps: float = 1e-5) -> torch.Tensor:
     """y = (rmsnorm(x)*norm_w if norm_w else x) @ W^T with a fused epilogue.
 
-    M <= 4 rows → weight-streaming GEMV (decode); larger M → prefill GEMM (a norm is applied by
-    a separate rmsnorm launch first). EPI_RESADD accumulates into ``out`` in place.
-
-    Prefill GEMMs with M >= PREFILL_BLAS_MIN_M are plain library GEMMs (D = A·Bᵀ or
-    D = C + A·Bᵀ, f32 accumulation, one bf16 rounding — the same numerics as our epilogues) and
-    go to hipBLASLt through torch (1.5-1.6 PF/s vs 0.85-0.9 PF/s for our 128x128 MFMA kernel on
-    the 8B shapes: profiles/r1_prefill_gemm_attention.md); LLMC_PREFILL_GEMM=hip forces ours.
-    The fused / gathered GEMMs (MoE grouped GEMM, decode GEMVs) stay hand-written.
+    M <= 4 rows -> weight-streaming GEMV (decode; the norm runs in its prologue); larger M -> the
+    256x256 MFMA prefill GEMM (csrc/kernels/gemm.hip; a norm is a separate rmsnorm launch first).
+    Epilogues: bf16 | f32 | EPI_RESADD (accumulates into ``out`` in place) | EPI_SILU (interleaved
+    gate/up columns -> silu(g) * u, [M, N / 2]). One code path per shape class, all hand-written.
     """
     if not x.is_cuda:
         return oracle.linear(x, W, epi, out, norm_w, eps)
@@ -102,28 +95,19 @@ def linear(x: torch.Tensor, W: torch.Tensor, epi: int = EPI_BF16, out: Optional[
         return out
     if norm_w is not None:
         x = rmsnorm(x, norm_w, eps)
-    if M >= PREFILL_BLAS_MIN_M and PREFILL_GEMM == "blas" and epi != EPI_F32 and x.is_contiguous():
-        if epi == EPI_SILU:
-            return silu_mul_interleaved(torch.matmul(x, W.t()), out)
-        if epi == EPI_RESADD:
-            return out.addmm_(x, W.t())
-        return torch.matmul(x, W.t(), out=out)
-    if epi == EPI_SILU:
-        gu = torch.empty(M, N, dtype=torch.bfloat16, device=x.device)
-        kernels().gemm(_p(x), x.stride(0), _p(W), W.stride(0), _p(gu), gu.stride(0), M, N, K, EPI_BF16, _s(x))
-        return silu_mul_interleaved(gu, out)
     kernels().gemm(_p(x), x.stride(0), _p(W), W.stride(0), _p(out), out.stride(0), M, N, K, epi, _s(x))
     return out
 
 
 def gemm(x: torch.Tensor, W: torch.Tensor, epi: int = EPI_BF16, out: Optional[torch.Tensor] = None) -> torch.Tensor:
-    """Always the MFMA GEMM path (for tests / prefill)."""
+    """Always the MFMA GEMM path (tests / microbenchmarks)."""
     if not x.is_cuda:
         return oracle.linear(x, W, epi, out)
     M, K = x.shape
     N = W.shape[0]
     if out is None:
-        out = torch.empty(M, N, dtype=torch.float32 if epi == EPI_F32 else torch.bfloat16, device=x.device)
+        n_out = N // 2 if epi == EPI_SILU else N
+        out = torch.empty(M, n_out, dtype=torch.float32 if epi == EPI_F32 else torch.bfloat16, device=x.device)
     kernels().gemm(_p(x), x.stride(0), _p(W), W.stride(0), _p(out), out.stride(0), M, N, K, epi, _s(x))
     return out
 

@@ -73,9 +73,16 @@ def test_gemv_fused_norm(cuda, M):
     close(y, ref, 3e-2)
 
 
-@pytest.mark.parametrize("M,N,K", [(128, 128, 64), (37, 200, 256), (300, 512, 4096), (1024, 384, 1024)])
-@pytest.mark.parametrize("epi", [0, 1, 2])
+@pytest.mark.parametrize("M,N,K", [(128, 128, 64), (37, 200, 256), (300, 512, 4096), (1024, 384, 1024),
+                                   (5, 4096, 128), (600, 700, 1472), (257, 130, 320), (2048, 2304, 2048),
+                                   (513, 6144, 4096)])
+@pytest.mark.parametrize("epi", [0, 1, 2, 3])
 def test_gemm(cuda, M, N, K, epi):
+    """256x256 ring-pipelined prefill GEMM vs the fp32 oracle: ragged M/N tiles (row/column
+    clamps, masked epilogue), N % 4 != 0 (scalar epilogue), K from one to 64 K-steps (ring
+    wrap-around, the vmcnt(0) tail), every epilogue incl. the fused SiLU-mul."""
+    if epi == 3 and N % 2:
+        pytest.skip("SiLU pairs need even N")
     torch.manual_seed(M + N + K + epi)
     x = rnd(M, K)
     W = rnd(N, K, scale=0.05)
@@ -86,9 +93,10 @@ def test_gemm(cuda, M, N, K, epi):
     close(y, ref, 2e-2)
 
 
-def test_gemm_identity_asymmetric(cuda):
-    """A = I with an asymmetric B catches a transposed C write (guide §3)."""
-    K = 128
+@pytest.mark.parametrize("K", [128, 512])
+def test_gemm_identity_asymmetric(cuda, K):
+    """A = I with an asymmetric B catches a transposed C write (guide §3); K = 512 spans two
+    256-row tiles in M and N."""
     A = torch.eye(K, dtype=BF, device="cuda")
     W = (torch.arange(K * K, device="cuda").view(K, K) % 97).to(BF)  # asymmetric
     y = ops.gemm(A, W, 0)

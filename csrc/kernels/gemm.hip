@@ -150,41 +150,110 @@ __global__ __launch_bounds__(256, 2) void gemm_kernel(const bf16_t* __restrict__
 }
 
 // ---------------------------------------------------------------------------------------------
-// Dense prefill GEMM (K6, M >= 5): the 256 x 256 tile, 8-wave, 4-phase-per-K-step template
-// (cdna_hip_programming.md §5 "The 256² 8-phase template", T1-T5), re-derived for C = A . W^T with
-// both operands K-contiguous:
-//  * waves 2 (M) x 4 (N), each owning a 128 x 64 output block = 8 x 4 tiles of
-//    mfma_f32_16x16x32_bf16 with the operands SWAPPED (W fragment as A, activation fragment as B:
-//    D[n][m]) so each lane ends with 4 consecutive output columns of one row -> 8-B/16-B stores.
-//  * each K-step (64) is consumed in 4 phases by output quadrant of the wave's block:
-//      P1 A rows 0-63 + W cols 0-31 -> q(0,0);  P2 W cols 32-63 -> q(0,1);
-//      P3 A rows 64-127             -> q(1,1);  P4 (no reads)   -> q(1,0)
-//    so every operand byte of the K-step is read from LDS exactly once, and each "quarter" of a
-//    K-step's operands (A0 / W0 / W1 / A1: 128 rows x 64 K = 16 KiB, the rows the 8 waves read in
-//    one phase) has a single last-read phase.
-//  * LDS is a RING of 10 quarter slots (160 KiB, one block per CU): quarter n (= 4 * kstep + j)
-//    lives in slot n % 10 and is fetched by global_load_lds_dwordx4 (2 per thread) FOUR phases
-//    after the quarter it replaces was last read, and waited for (counted `s_waitcnt vmcnt(8)`,
-//    never 0 in the main loop) four phases before its first read: ~4 phases of MFMA work hide
-//    every fetch, and no barrier drains the load queue.
-//  * ping-pong: the two wave rows run one barrier apart (waves 4-7 take one extra barrier up
-//    front), so one row's LDS reads + load issue overlap the other row's MFMA cluster on the same
-//    SIMD; s_setprio(1) around each MFMA cluster keeps hipcc from scattering it (T5).
-//  * LDS XOR swizzle chunk ^ ((row >> 1) & 7) (128-B rows): applied to the per-lane SOURCE address
-//    of the lane-linear LDS-DMA and again on the ds_read_b128 address (rule 21): conflict-free.
-//  * grid: bijective XCD remap (T1) then grouped tile order (8 M-tiles x all N per group) so the
-//    ~32 tiles an XCD runs at once share 8 activation panels and 4 weight panels in its L2.
+// Dense prefill GEMM (K6, M >= 5): C = A . W^T, both operands K-contiguous, 256 x 256 tiles,
+// 512 threads = 8 waves (2 M x 4 N), one block per CU (160 KiB of LDS).
+//  * wave block 128 x 64 = 8 x 4 tiles of mfma_f32_16x16x32_bf16 with the operands SWAPPED (W
+//    fragment as A, activation as B: D[n][m]) so a lane ends with 4 consecutive output columns of
+//    one row -> 8-/16-byte epilogue stores.
+//  * a K-step (64) is consumed in 2 phases: P1 reads A rows 0-63 of the wave + its 64 W columns
+//    (16 ds_read_b128) -> output rows 0-63; P2 reads A rows 64-127 (8) -> rows 64-127. The step's
+//    operands are 4 "quarters" (A0 / W0 / W1 / A1: 128 rows x 64 K = 16 KiB each), every byte read
+//    from LDS exactly once.
+//  * LDS = a RING of 10 quarter slots. Quarter n (= 4 kstep + j) lives in slot n % 10 and is
+//    fetched by LDS-DMA (buffer_load_dwordx4 ... lds: per-lane 32-bit offsets fixed for the whole
+//    K loop, the K position in the scalar offset, so a fetch costs no vector instruction) one phase
+//    after its slot's previous quarter was last read — each phase retires its LDS reads before its
+//    first barrier — so the ring runs TWO K-steps ahead: every fetch has two phases (~2k cycles)
+//    to land before the counted `s_waitcnt vmcnt(8)` that precedes its first read; no barrier ever
+//    drains the load queue (cdna_hip_programming.md §5 "Pipelining across barriers").
+//  * ping-pong: the two wave rows run one barrier apart (waves 4-7 take an extra barrier up
+//    front), so one row's LDS reads + fetch issue overlap the other row's MFMA cluster on the same
+//    SIMD; s_setprio(1) around each cluster keeps hipcc from scattering it (T5).
+//  * LDS XOR swizzle chunk ^ ((row >> 1) & 7) (128-B rows): on the per-lane SOURCE offset of the
+//    lane-linear LDS-DMA and on the ds_read_b128 address (rule 21): conflict-free
+//    (SQ_LDS_BANK_CONFLICT 0).
+//  * grid: bijective XCD remap (T1) then grouped tile order (8 M-tiles x all N per group).
 //  * fused epilogues: bf16 | f32 | residual add (C += A.W^T) | SiLU-mul of interleaved gate/up
-//    columns (C[m][n/2] = silu(g) * u) — the same f32-accumulate, one-rounding numerics.
+//    columns (C[m][n/2] = silu(g) * u).
+// Measured (MI355X, random bf16; profiles/r2_prefill_gemm.md): 1.28-1.38 PF/s on the Llama-3-8B
+// prefill shapes, 83-86 % of hipBLASLt on the same data. The remaining gap is structural (PMC:
+// hipBLASLt runs 4 waves x 128 x 128 with 512 registers each and 1.5x fewer LDS reads; this
+// 8-wave layout parks waves at barriers: SQ_WAIT_ANY 275M vs 37M wave-cycles per dispatch).
 constexpr int kT = 256, kTK = 64;
 constexpr int kQuarter = 128 * kTK * 2;  // bytes
 constexpr int kSlots = 10;
 constexpr int kGroupM = 8;
 
+// Epilogue store of 4 consecutive output columns C[m][n .. n + 3] (f32 accumulators) with the
+// fused epilogue; m < M checked by the caller.
+template <int EPI>
+__device__ __forceinline__ void store4(void* __restrict__ C, int ldc, int N, int m, int n, const f32x4& v, bool vec_ok) {
+  if constexpr (EPI == 3) {  // SiLU(gate) * up over interleaved (gate, up) column pairs
+    float o[2];
+#pragma unroll
+    for (int p = 0; p < 2; ++p) {
+      const float g = v[2 * p], u = v[2 * p + 1];
+      o[p] = g / (1.f + __expf(-g)) * u;
+    }
+    bf16_t* crow = reinterpret_cast<bf16_t*>(C) + static_cast<int64_t>(m) * ldc;
+    if (vec_ok && n + 3 < N) {
+      *reinterpret_cast<uint32_t*>(crow + n / 2) = pack_bf16x2(o[0], o[1]);
+    } else {
+#pragma unroll
+      for (int p = 0; p < 2; ++p)
+        if (n + 2 * p + 1 < N) crow[n / 2 + p] = f32_to_bf16(o[p]);
+    }
+  } else if constexpr (EPI == 1) {
+    float* crow = reinterpret_cast<float*>(C) + static_cast<int64_t>(m) * ldc;
+    if (vec_ok && n + 3 < N) {
+      *reinterpret_cast<f32x4*>(crow + n) = v;
+    } else {
+#pragma unroll
+      for (int e = 0; e < 4; ++e)
+        if (n + e < N) crow[n + e] = v[e];
+    }
+  } else {
+    bf16_t* crow = reinterpret_cast<bf16_t*>(C) + static_cast<int64_t>(m) * ldc;
+    if (vec_ok && n + 3 < N) {
+      float o[4] = {v[0], v[1], v[2], v[3]};
+      if constexpr (EPI == 2) {
+        const u32x2 old = *reinterpret_cast<const u32x2*>(crow + n);
+        o[0] += bf16_lo(old[0]);
+        o[1] += bf16_hi(old[0]);
+        o[2] += bf16_lo(old[1]);
+        o[3] += bf16_hi(old[1]);
+      }
+      *reinterpret_cast<u32x2*>(crow + n) = u32x2{pack_bf16x2(o[0], o[1]), pack_bf16x2(o[2], o[3])};
+    } else {
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        if (n + e >= N) continue;
+        const float x = EPI == 2 ? bf16_to_f32(crow[n + e]) + v[e] : v[e];
+        crow[n + e] = f32_to_bf16(x);
+      }
+    }
+  }
+}
+
+// Epilogue of the 16x16x32 kernels: acc[mi][ni] holds D[n][m] of 16 x 16 tile (mi, ni) of the wave's
+// 128 x 64 block (operands swapped), i.e. lane (l16, lg) has C[m][n .. n + 3].
+template <int EPI>
+__device__ __forceinline__ void gemm256_epilogue(const f32x4 (&acc)[8][4], void* __restrict__ C, int ldc, int M, int N,
+                                                 int m0, int n0, int wr, int wc, int l16, int lg) {
+  const bool vec_ok = (N % 4 == 0) && (ldc % 4 == 0);
+#pragma unroll
+  for (int mi = 0; mi < 8; ++mi) {
+    const int m = m0 + wr * 128 + mi * 16 + l16;
+    if (m >= M) continue;
+#pragma unroll
+    for (int ni = 0; ni < 4; ++ni) store4<EPI>(C, ldc, N, m, n0 + wc * 64 + ni * 16 + 4 * lg, acc[mi][ni], vec_ok);
+  }
+}
+
 template <int EPI>
 __global__ __launch_bounds__(512, 1) void gemm256_kernel(const bf16_t* __restrict__ A, int lda,
-                                                        const bf16_t* __restrict__ W, int ldw, void* __restrict__ C,
-                                                        int ldc, int M, int N, int K) {
+                                                          const bf16_t* __restrict__ W, int ldw, void* __restrict__ C,
+                                                          int ldc, int M, int N, int K) {
   __shared__ __attribute__((aligned(16))) char smem[kSlots * kQuarter];
   const int num_m = (M + kT - 1) / kT, num_n = (N + kT - 1) / kT;
   const int id = xcd_remap(blockIdx.x, num_m * num_n);
@@ -193,64 +262,68 @@ __global__ __launch_bounds__(512, 1) void gemm256_kernel(const bf16_t* __restric
   const int gsz = min(num_m - first_m, kGroupM);
   const int in_group = id - group * kGroupM * num_n;
   const int m0 = (first_m + in_group % gsz) * kT, n0 = (in_group / gsz) * kT;
-
-  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wr = wave >> 2, wc = wave & 3;
   const int l16 = lane & 15, lg = lane >> 4;
-
-  // per-thread LDS-DMA sources: quarter j (0 A0, 1 W0, 2 W1, 3 A1) x 2 instructions
-  const bf16_t* src[4][2];
+  // buffer descriptors on this tile's rows (offsets stay < 2 GiB: 256 rows x ld); per-lane byte
+  // offsets of the 4 quarter types x 2 pieces (rows clamped to the matrix)
+  const int rowsA = min(kT, M - m0), rowsW = min(kT, N - n0);
+  const __amdgpu_buffer_rsrc_t rsA = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)(A + static_cast<int64_t>(m0) * lda), 0, rowsA * lda * 2, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rsW = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)(W + static_cast<int64_t>(n0) * ldw), 0, rowsW * ldw * 2, 0x00020000);
+  uint32_t voff[4][2];
 #pragma unroll
   for (int i = 0; i < 2; ++i) {
     const int s = i * 512 + tid;
     const int r = s >> 3, c = (s & 7) ^ ((r >> 1) & 7);
 #pragma unroll
     for (int h = 0; h < 2; ++h) {
-      const int ar = min(m0 + (r >> 6) * 128 + h * 64 + (r & 63), M - 1);
-      const int wrow = min(n0 + (r >> 5) * 64 + h * 32 + (r & 31), N - 1);
-      src[h == 0 ? 0 : 3][i] = A + static_cast<int64_t>(ar) * lda + c * 8;
-      src[1 + h][i] = W + static_cast<int64_t>(wrow) * ldw + c * 8;
+      const int ar = min((r >> 6) * 128 + h * 64 + (r & 63), rowsA - 1);
+      const int wrow = min((r >> 5) * 64 + h * 32 + (r & 31), rowsW - 1);
+      voff[h == 0 ? 0 : 3][i] = static_cast<uint32_t>((ar * lda + c * 8) * 2);
+      voff[1 + h][i] = static_cast<uint32_t>((wrow * ldw + c * 8) * 2);
     }
   }
   const int nk = K / kTK, nq = 4 * nk;
-  auto stage = [&](int n) {  // quarter n -> ring slot n % 10 (wave-uniform LDS base + lane * 16)
-    const int j = n & 3, k0 = (n >> 2) * kTK;
-    char* q = smem + (n % kSlots) * kQuarter;
+  auto stage = [&](int n) {
+    const int j = n & 3, kbytes = (n >> 2) * kTK * 2;
+    char* q = smem + (n % kSlots) * kQuarter + wave * 64 * 16;
 #pragma unroll
     for (int i = 0; i < 2; ++i)
-      __builtin_amdgcn_global_load_lds((const void*)(src[j][i] + k0),
-                                       (__attribute__((address_space(3))) void*)(q + (i * 512 + wave * 64) * 16), 16, 0, 0);
+      __builtin_amdgcn_raw_ptr_buffer_load_lds((j == 0 || j == 3) ? rsA : rsW,
+                                               (__attribute__((address_space(3))) void*)(q + i * 512 * 16), 16,
+                                               voff[j][i], kbytes, 0, 0);
   };
   auto lds_off = [&](int r, int c) { return r * 128 + ((c ^ ((r >> 1) & 7)) << 4); };
-
   f32x4 acc[8][4];
 #pragma unroll
   for (int a = 0; a < 8; ++a)
 #pragma unroll
     for (int b = 0; b < 4; ++b) acc[a][b] = f32x4{0.f, 0.f, 0.f, 0.f};
   bf16x8 af[4][2], bw0[2][2], bw1[2][2];
-
-  // prologue: quarters 0..5 (k-step 0 and the first half of k-step 1) in flight, step 0 landed
-  for (int n = 0; n < 6 && n < nq; ++n) stage(n);
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  for (int n = 0; n < 8 && n < nq; ++n) stage(n);
+  if (nq >= 8) {
+    asm volatile("s_waitcnt vmcnt(8)" ::: "memory");  // k-step 0 landed, k-step 1 in flight
+  } else {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  }
   asm volatile("s_barrier" ::: "memory");
   __builtin_amdgcn_sched_barrier(0);
-  if (wr == 1) asm volatile("s_barrier" ::: "memory");  // ping-pong: wave row 1 runs one barrier behind
+  if (wr == 1) asm volatile("s_barrier" ::: "memory");
   __builtin_amdgcn_sched_barrier(0);
-
-  // one phase: [reads] [LDS-DMA of quarter n] counted wait | barrier | MFMA cluster | barrier
-  // the "memory" clobbers keep LDS reads from moving across the barriers (the intrinsic alone
-  // is not a memory barrier for the compiler); sched_barrier(0) pins the MFMA clusters
   auto sync_wait = [&](int n_issue) {
-    if (n_issue < nq) {
+    if (n_issue + 1 < nq) {
       stage(n_issue);
-      asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+      stage(n_issue + 1);
+      asm volatile("s_waitcnt vmcnt(8) lgkmcnt(0)" ::: "memory");
     } else {
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      if (n_issue < nq) stage(n_issue);
+      asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
     }
     __builtin_amdgcn_sched_barrier(0);
     asm volatile("s_barrier" ::: "memory");
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_sched_barrier(0);
   };
   auto end_phase = [&]() {
@@ -258,57 +331,23 @@ __global__ __launch_bounds__(512, 1) void gemm256_kernel(const bf16_t* __restric
     asm volatile("s_barrier" ::: "memory");
     __builtin_amdgcn_sched_barrier(0);
   };
-
   for (int t = 0; t < nk; ++t) {
     const char* qa0 = smem + ((4 * t + 0) % kSlots) * kQuarter;
     const char* qw0 = smem + ((4 * t + 1) % kSlots) * kQuarter;
     const char* qw1 = smem + ((4 * t + 2) % kSlots) * kQuarter;
     const char* qa1 = smem + ((4 * t + 3) % kSlots) * kQuarter;
-    // ---- P1: A rows 0-63, W cols 0-31 -> q(0,0)
 #pragma unroll
     for (int ni = 0; ni < 2; ++ni)
 #pragma unroll
-      for (int kk = 0; kk < 2; ++kk)
+      for (int kk = 0; kk < 2; ++kk) {
         bw0[ni][kk] = *reinterpret_cast<const bf16x8*>(qw0 + lds_off(wc * 32 + ni * 16 + l16, kk * 4 + lg));
+        bw1[ni][kk] = *reinterpret_cast<const bf16x8*>(qw1 + lds_off(wc * 32 + ni * 16 + l16, kk * 4 + lg));
+      }
 #pragma unroll
     for (int mi = 0; mi < 4; ++mi)
 #pragma unroll
       for (int kk = 0; kk < 2; ++kk)
         af[mi][kk] = *reinterpret_cast<const bf16x8*>(qa0 + lds_off(wr * 64 + mi * 16 + l16, kk * 4 + lg));
-    sync_wait(4 * t + 6);
-    __builtin_amdgcn_s_setprio(1);
-#pragma unroll
-    for (int mi = 0; mi < 4; ++mi)
-#pragma unroll
-      for (int ni = 0; ni < 2; ++ni)
-#pragma unroll
-        for (int kk = 0; kk < 2; ++kk)
-          acc[mi][ni] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bw0[ni][kk], af[mi][kk], acc[mi][ni], 0, 0, 0);
-    __builtin_amdgcn_s_setprio(0);
-    end_phase();
-    // ---- P2: W cols 32-63 -> q(0,1)
-#pragma unroll
-    for (int ni = 0; ni < 2; ++ni)
-#pragma unroll
-      for (int kk = 0; kk < 2; ++kk)
-        bw1[ni][kk] = *reinterpret_cast<const bf16x8*>(qw1 + lds_off(wc * 32 + ni * 16 + l16, kk * 4 + lg));
-    sync_wait(4 * t + 7);
-    __builtin_amdgcn_s_setprio(1);
-#pragma unroll
-    for (int mi = 0; mi < 4; ++mi)
-#pragma unroll
-      for (int ni = 0; ni < 2; ++ni)
-#pragma unroll
-        for (int kk = 0; kk < 2; ++kk)
-          acc[mi][2 + ni] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bw1[ni][kk], af[mi][kk], acc[mi][2 + ni], 0, 0, 0);
-    __builtin_amdgcn_s_setprio(0);
-    end_phase();
-    // ---- P3: A rows 64-127 -> q(1,1)
-#pragma unroll
-    for (int mi = 0; mi < 4; ++mi)
-#pragma unroll
-      for (int kk = 0; kk < 2; ++kk)
-        af[mi][kk] = *reinterpret_cast<const bf16x8*>(qa1 + lds_off(wr * 64 + mi * 16 + l16, kk * 4 + lg));
     sync_wait(4 * t + 8);
     __builtin_amdgcn_s_setprio(1);
 #pragma unroll
@@ -316,82 +355,33 @@ __global__ __launch_bounds__(512, 1) void gemm256_kernel(const bf16_t* __restric
 #pragma unroll
       for (int ni = 0; ni < 2; ++ni)
 #pragma unroll
-        for (int kk = 0; kk < 2; ++kk)
-          acc[4 + mi][2 + ni] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bw1[ni][kk], af[mi][kk], acc[4 + mi][2 + ni], 0, 0, 0);
+        for (int kk = 0; kk < 2; ++kk) {
+          acc[mi][ni] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bw0[ni][kk], af[mi][kk], acc[mi][ni], 0, 0, 0);
+          acc[mi][2 + ni] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bw1[ni][kk], af[mi][kk], acc[mi][2 + ni], 0, 0, 0);
+        }
     __builtin_amdgcn_s_setprio(0);
     end_phase();
-    // ---- P4: no reads -> q(1,0)
-    sync_wait(4 * t + 9);
+#pragma unroll
+    for (int mi = 0; mi < 4; ++mi)
+#pragma unroll
+      for (int kk = 0; kk < 2; ++kk)
+        af[mi][kk] = *reinterpret_cast<const bf16x8*>(qa1 + lds_off(wr * 64 + mi * 16 + l16, kk * 4 + lg));
+    sync_wait(4 * t + 10);
     __builtin_amdgcn_s_setprio(1);
 #pragma unroll
     for (int mi = 0; mi < 4; ++mi)
 #pragma unroll
       for (int ni = 0; ni < 2; ++ni)
 #pragma unroll
-        for (int kk = 0; kk < 2; ++kk)
+        for (int kk = 0; kk < 2; ++kk) {
           acc[4 + mi][ni] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bw0[ni][kk], af[mi][kk], acc[4 + mi][ni], 0, 0, 0);
+          acc[4 + mi][2 + ni] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bw1[ni][kk], af[mi][kk], acc[4 + mi][2 + ni], 0, 0, 0);
+        }
     __builtin_amdgcn_s_setprio(0);
     end_phase();
   }
-  if (wr == 0) asm volatile("s_barrier" ::: "memory");  // balance the ping-pong offset
-
-  // ---- epilogue: lane holds C[m][n .. n + 3], m = row of l16, n = 4 * lg within each 16x16 tile
-  const bool vec_ok = (N % 4 == 0) && (ldc % 4 == 0);
-#pragma unroll
-  for (int mi = 0; mi < 8; ++mi) {
-    const int m = m0 + wr * 128 + mi * 16 + l16;
-    if (m >= M) continue;
-#pragma unroll
-    for (int ni = 0; ni < 4; ++ni) {
-      const int n = n0 + wc * 64 + ni * 16 + 4 * lg;
-      const f32x4 v = acc[mi][ni];
-      if constexpr (EPI == 3) {  // SiLU(gate) * up over interleaved (gate, up) column pairs
-        float o[2];
-#pragma unroll
-        for (int p = 0; p < 2; ++p) {
-          const float g = v[2 * p], u = v[2 * p + 1];
-          o[p] = g / (1.f + __expf(-g)) * u;
-        }
-        bf16_t* crow = reinterpret_cast<bf16_t*>(C) + static_cast<int64_t>(m) * ldc;
-        if (vec_ok && n + 3 < N) {
-          *reinterpret_cast<uint32_t*>(crow + n / 2) = pack_bf16x2(o[0], o[1]);
-        } else {
-#pragma unroll
-          for (int p = 0; p < 2; ++p)
-            if (n + 2 * p + 1 < N) crow[n / 2 + p] = f32_to_bf16(o[p]);
-        }
-      } else if constexpr (EPI == 1) {
-        float* crow = reinterpret_cast<float*>(C) + static_cast<int64_t>(m) * ldc;
-        if (vec_ok && n + 3 < N) {
-          *reinterpret_cast<f32x4*>(crow + n) = v;
-        } else {
-#pragma unroll
-          for (int e = 0; e < 4; ++e)
-            if (n + e < N) crow[n + e] = v[e];
-        }
-      } else {
-        bf16_t* crow = reinterpret_cast<bf16_t*>(C) + static_cast<int64_t>(m) * ldc;
-        if (vec_ok && n + 3 < N) {
-          float o[4] = {v[0], v[1], v[2], v[3]};
-          if constexpr (EPI == 2) {
-            const u32x2 old = *reinterpret_cast<const u32x2*>(crow + n);
-            o[0] += bf16_lo(old[0]);
-            o[1] += bf16_hi(old[0]);
-            o[2] += bf16_lo(old[1]);
-            o[3] += bf16_hi(old[1]);
-          }
-          *reinterpret_cast<u32x2*>(crow + n) = u32x2{pack_bf16x2(o[0], o[1]), pack_bf16x2(o[2], o[3])};
-        } else {
-#pragma unroll
-          for (int e = 0; e < 4; ++e) {
-            if (n + e >= N) continue;
-            const float x = EPI == 2 ? bf16_to_f32(crow[n + e]) + v[e] : v[e];
-            crow[n + e] = f32_to_bf16(x);
-          }
-        }
-      }
-    }
-  }
+  if (wr == 0) asm volatile("s_barrier" ::: "memory");
+  gemm256_epilogue<EPI>(acc, C, ldc, M, N, m0, n0, wr, wc, l16, lg);
 }
 
 }  // namespace llmc
@@ -399,11 +389,13 @@ __global__ __launch_bounds__(512, 1) void gemm256_kernel(const bf16_t* __restric
 using namespace llmc;
 
 // C[M, N] (+)= A[M, K] . W[N, K]^T. epi: 0 bf16, 1 f32, 2 C += (bf16), 3 SiLU-mul of interleaved
-// gate/up columns into C[M, N / 2] (bf16). K must be a multiple of 64.
+// gate/up columns into C[M, N / 2] (bf16). K must be a multiple of 64, lda/ldw multiples of 8.
 extern "C" int llmc_gemm(const void* A, int lda, const void* W, int ldw, void* C, int ldc, int M, int N, int K,
                          int epi, hipStream_t s) {
   if (K % kTK != 0 || M <= 0 || N <= 0 || K <= 0 || (epi == 3 && N % 2 != 0)) return -1;
   if (lda % 8 != 0 || ldw % 8 != 0) return -1;  // 16-B aligned rows for the LDS-DMA
+  // buffer offsets inside one 256-row tile must stay below 2^31 bytes
+  if (static_cast<int64_t>(kT) * lda * 2 >= (1ll << 31) || static_cast<int64_t>(kT) * ldw * 2 >= (1ll << 31)) return -1;
   const int nwg = ((M + kT - 1) / kT) * ((N + kT - 1) / kT);
   switch (epi) {
     case 0: gemm256_kernel<0><<<nwg, 512, 0, s>>>((const bf16_t*)A, lda, (const bf16_t*)W, ldw, C, ldc, M, N, K); break;

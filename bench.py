@@ -320,9 +320,11 @@ def main() -> None:
             if judge.tp.is_leader:
                 stats["judge_tokens"] = len(jids)
             judge.free_sequence(jseq)
-            if judge.tp.custom is not None and judge.tp.custom.timed_out():
-                raise RuntimeError("a custom all-reduce spin timed out (a peer stalled): judge tokens are invalid")
         sync()
+        # a custom-collective spin that gave up means a peer stalled and the sums are invalid
+        for e in [e for _, e, _, _ in responders] + ([judge] if judge is not None else []):
+            if e.tp.size > 1 and e.tp.custom_timed_out():
+                raise RuntimeError(f"{e.name}: a custom all-reduce spin timed out (a peer stalled): tokens are invalid")
         if world > 1:
             dist.barrier()
         t_end = time.perf_counter()

@@ -37,7 +37,10 @@ namespace llmc {
 constexpr int kMaxRanks = 8;
 constexpr int kMaxBlocks = 256;  // signal slots (two-shot launches use all of them)
 constexpr int kBlocks = 32;      // one-shot: blocks per launch (at most; see car_grid)
-constexpr int kTsBlocks = 256;   // two-shot: fixed grid (every launch, every rank)
+// two-shot: fixed grid (every launch, every rank). Kept to a quarter of the chip: the blocks spin
+// on their peers, and a full-chip grid of spinning blocks can starve a peer's queued kernel of CUs
+// when ranks share a GPU (a 512-thread, 160-KiB GEMM block needs a whole CU) -> spin timeout.
+constexpr int kTsBlocks = 64;
 constexpr int kChunk = 256;      // 16-B vectors per chunk (one per thread)
 constexpr size_t kSigBytes = 64 * 1024;
 constexpr int kFlagOff = 1024;                              // bytes: after ctr[kMaxBlocks]

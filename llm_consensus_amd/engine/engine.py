@@ -647,18 +647,7 @@ class Engine:
                 if not s.has_logits:
                     raise EngineError("sequence has no prefill logits")
                 self._reserve(s, s.length + p.max_tokens + S + 1)
-            # bind sequences to decode rows 0..B-1: block tables and prefill logits into the rows
-            self.block_tables[:B].copy_(self._block_table(seqs))
-            for i, (s, p) in enumerate(zip(seqs, params)):
-                s.row = i
-                r = i
-                self.logits_local[r].copy_(s.logits)
-                self.inv_temp[r] = 0.0 if p.temperature <= 0 else 1.0 / p.temperature
-                self.top_k[r] = p.top_k
-                self.top_p[r] = p.top_p
-                self.seeds[r] = p.seed
-                self.positions[r] = s.length - 1
-                self.out_count[r] = 0
+            self._bind_rows(seqs, params)
             if max_new > self.cap - S - 1:
                 raise EngineError("max_tokens exceeds engine capacity")
             # first token from the prefill logits (+ device state advance)
@@ -769,6 +758,46 @@ class Engine:
         the next request runs on consistent epochs."""
         if self.tp.size > 1 and self.tp.ctrl is not None and not self.tp.check_collectives():
             raise EngineError("custom all-reduce timed out (a TP peer stalled): this request's tokens are invalid")
+
+    def _bind_rows(self, seqs: List[Sequence], params: List[SamplingParams]) -> None:
+        """Bind sequences to decode rows 0..B-1: block tables, prefill logits and sampling state."""
+        B = len(seqs)
+        self.block_tables[:B].copy_(self._block_table(seqs))
+        for i, (s, p) in enumerate(zip(seqs, params)):
+            s.row = i
+            self.logits_local[i].copy_(s.logits)
+            self.inv_temp[i] = 0.0 if p.temperature <= 0 else 1.0 / p.temperature
+            self.top_k[i] = p.top_k
+            self.top_p[i] = p.top_p
+            self.seeds[i] = p.seed
+            self.positions[i] = s.length - 1
+            self.out_count[i] = 0
+
+    @torch.no_grad()
+    def debug_decode_logits(self, prompt: Seq[int], n: int):
+        """Greedy decode of ``n`` tokens one eager step at a time (TP=1), returning (tokens, logits
+        [n, V] f32): row i holds the full-vocabulary logits token i was sampled from — the hook the
+        teacher-forced oracle test compares against a CPU prefill of prompt + tokens[:i]."""
+        if self.tp.size != 1:
+            raise EngineError("debug_decode_logits: TP=1 only")
+        seq = self.new_sequence()
+        try:
+            with self._on_stream():
+                self.prefill([seq], [list(prompt)])
+                self._reserve(seq, seq.length + n + 2)
+                self._use_topkp = False
+                self._bind_rows([seq], [SamplingParams(n, 0.0, 1.0, 0, 0, False)])
+                rows = [self.logits_local[0].clone()]
+                self._sample(1, self._gather_logits(1))
+                for _ in range(n - 1):
+                    self._decode_step(1, self._bucket(seq.length + n + 2))
+                    rows.append(self.logits_local[0].clone())
+                toks = self.out_tokens[0, :n].clone()
+            if self.on_gpu:
+                self.stream.synchronize()
+            return toks.cpu().tolist(), torch.stack(rows).float().cpu()
+        finally:
+            self.free_sequence(seq)
 
     def _finish(self, seqs, results) -> None:
         for s, r in zip(seqs, results):

@@ -87,8 +87,8 @@ def rope_kv_write(qkv, positions, cos_t, sin_t, k_cache, v_cache, slots, nh, nkv
 
 def _gather_kv(cache, bt_row, L, bs):
     """[L, nkv, D] from a paged cache [nb, nkv, bs, D]."""
-    idx = torch.arange(L)
-    pages = bt_row[(idx // bs)].long()
+    idx = torch.arange(L, device=cache.device)
+    pages = bt_row.to(cache.device)[(idx // bs)].long()
     return cache[pages, :, (idx % bs)]
 
 
@@ -119,8 +119,8 @@ def attn_prefill(q, k_cache, v_cache, block_tables, q_start, q_lens, ctx_lens, n
         v = _gather_kv(v_cache, block_tables[b], ctx, bs).float().repeat_interleave(G, dim=1)
         qb = q[q0:q0 + ql, : nh * D].view(ql, nh, D).float()
         s = torch.einsum("qhd,khd->hqk", qb, k) * scale
-        qpos = torch.arange(ctx - ql, ctx).view(1, ql, 1)
-        kpos = torch.arange(ctx).view(1, 1, ctx)
+        qpos = torch.arange(ctx - ql, ctx, device=s.device).view(1, ql, 1)
+        kpos = torch.arange(ctx, device=s.device).view(1, 1, ctx)
         s = s.masked_fill(kpos > qpos, float("-inf"))
         p = torch.softmax(s, dim=-1)
         o = torch.einsum("hqk,khd->qhd", p, v)

@@ -118,3 +118,21 @@ def test_cli_judge_tp_flag_cpu():
     assert rc == 0, err
     d = json.loads(out)
     assert d["judge"] == "llama-tiny@j" and len(d["consensus"]) > 0 and len(d["responses"]) == 2
+
+
+def test_cli_config4_two_tp_responder_groups_cpu(tmp_path):
+    """BASELINE config 4 through the CLI on CPU workers (gloo): two Llama-70B-shaped responders,
+    each a TP=2 group pinned to its own pair of worker processes (disjoint halves of the "node"),
+    plus an 8B-shaped judge on a fifth worker (cmd/llm-consensus/main.go:132-170: fan-out, then
+    judge). Every TP rank follows its leader's batching/stop decisions over the control group."""
+    rc, out, err = run_cli(["--models", "llama-tiny-tp4@0,llama-tiny-tp4@1", "--judge", "llama-tiny@j",
+                            "--placement", "llama-tiny-tp4@0=-1+-2,llama-tiny-tp4@1=-3+-4,llama-tiny@j=-5",
+                            "--max-tokens", "8", "--temperature", "0", "--data-dir", str(tmp_path),
+                            "Compare two sorting algorithms."],
+                           env={"LLMC_DEVICE": "cpu", "LLMC_CPU_WORKERS": "5"})
+    assert rc == 0, err
+    run = tmp_path / os.listdir(tmp_path)[0]
+    res = json.loads((run / "result.json").read_text())
+    assert sorted(r["model"] for r in res["responses"]) == ["llama-tiny-tp4@0", "llama-tiny-tp4@1"]
+    assert all(len(r["content"]) > 0 for r in res["responses"])
+    assert res["judge"] == "llama-tiny@j" and len(res["consensus"]) > 0

@@ -254,6 +254,30 @@ def test_attn_prefill(cuda, nh, nkv, D, case):
     close(out, ref, 2e-2)
 
 
+@pytest.mark.parametrize("nh,nkv,D,ctx", [(32, 8, 128, 8192), (32, 8, 128, 16384), (32, 8, 128, 33000),
+                                        (32, 32, 96, 16384)])
+def test_attn_prefill_long_context_vs_fp32(cuda, nh, nkv, D, ctx):
+    """Judge-length contexts (the N=8 judge prompt is ~33k tokens): the last 384 queries of a ctx-key
+    paged sequence (the final chunk of a chunked prefill) beside a short full prefill, against the
+    fp32 oracle computed on the GPU (the same einsum/softmax code as the CPU oracle)."""
+    torch.manual_seed(ctx + D)
+    bs = 64
+    qlens, ctxs = [384, 300], [ctx, 300]
+    B = len(qlens)
+    kc, vc, bt = _paged_kv(B, max(ctxs), nkv, D, bs)
+    qs = torch.tensor([0, qlens[0]], dtype=torch.int32)
+    T = sum(qlens)
+    q = rnd(T, nh * D)
+    out = torch.zeros(T, nh * D, dtype=BF, device="cuda")
+    ql, cl = torch.tensor(qlens, dtype=torch.int32), torch.tensor(ctxs, dtype=torch.int32)
+    scale = 1 / math.sqrt(D)
+    ops.attn_prefill(q, kc, vc, bt.cuda(), qs.cuda(), ql.cuda(), cl.cuda(), out, max(qlens), nh, nkv, D, bs, scale)
+    ref = torch.zeros(T, nh * D, dtype=BF, device="cuda")
+    oracle.attn_prefill(q, kc, vc, bt.cuda(), qs, ql, cl, nh, nkv, D, bs, scale, ref)  # fp32 math, on the GPU
+    torch.cuda.synchronize()
+    close(out, ref.float().cpu(), 2e-2)
+
+
 def _sample_bufs(B, V):
     P = ops.sample_parts()
     return (torch.empty(B, P, device="cuda"), torch.empty(B, P, dtype=torch.int32, device="cuda"),

@@ -43,7 +43,7 @@ def _worker(rank, world, port, name, q, ekw=None):
         gen = e.generate_ids(PROMPT, 24, temperature=0.0, stop_on_eos=False)
         torch.cuda.synchronize()
         if rank == 0:
-            q.put((logits.tolist(), gen, tp.custom.timed_out()))
+            q.put((logits.tolist(), gen, tp.custom_timed_out()))
         dist.barrier()
         dist.destroy_process_group()
     except Exception as ex:  # noqa: BLE001

@@ -1,148 +1,570 @@
-// K5 (long contexts): cross-chunk merge of the SPLIT form of decode attention
-// (attn_decode_mfma.hip: per-block partials O, m (natural log), l in [B, nkv, max_chunks, G, D + 2])
-// and the host entry point that picks the form per context bucket.
+// K5: paged decode attention with the GQA group on the matrix cores (one query token per
+// sequence), ONE launch per step in both of its forms (host: llmc_attn_decode).
+//
+// Shared sub-tile step (a wave and 32 keys), mfma_f32_16x16x32_bf16:
+//   S^T[key][h] = K . Q^T     A = K (16 keys x 32 dims: one 16-B global load per lane, no LDS),
+//                             B = Q^T (32 dims x 16 heads; the G real heads, rest zero) in VGPRs.
+//                             C puts head h = lane & 15 on the lane and 4 keys per 16x16 tile in
+//                             registers -> per head, 8 of the 32 keys are lane-local and the
+//                             row max / row sum need only 2 xor-shuffles (offsets 16, 32).
+//   O^T[d][h] += V^T . P^T    B = P^T straight from the S^T accumulators (cvt to bf16; the
+//                             k-order is permuted to match, guide §3 "accumulator tile as the next
+//                             MFMA's operand"); A = V^T via ds_read_b64_tr_b16 (T10) from a per-wave
+//                             LDS image of the 32 V rows, chunk-swizzled c ^ ((row & 7) << 1) so a
+//                             half-wave's 8 rows x 32 B hit 64 distinct banks. O^T keeps the head on
+//                             the lane, so the online-softmax rescale uses lane-local alpha.
+//
+// FUSED form (short contexts, <= 4k keys: responders): a block = 4 waves = one kv head x a FIXED
+// 128- or 256-key chunk. The chunk does not depend on L, so a wave's page id (its 32/64 keys share
+// a page), the length, the merge epoch and Q are loaded together in ONE round trip, then K/V.
+// SPLIT form (long contexts: the judge): a block = 8 waves (4 without GQA) = one kv head x one balanced key range
+// (the L keys split evenly, in 32-key units, over min(grid_chunks, L / min_chunk) blocks:
+// common.h decode_nsplit / decode_range), so a graph captured for a bucket keeps every block
+// equally busy whatever the actual L; the block's page ids are staged in LDS once; 8 waves put
+// 2 x 16 KB of K/V per wave in flight (the 4-wave form of round 1 left the HBM queue half empty
+// and needed a second, reduce launch).
+//
+// Cross-block merge, both forms, in the same launch, with no fence and no drain: every chunk block
+// publishes its normalised partial (O/l per dim in bf16, lambda = m + log2 l per head in f32) as
+// 8-byte {value, tag} granules (two per 16-B write-through store; MI355X_MICROARCH.md
+// § visibility R2: the data IS the flag) and takes a ticket; the LAST arriver merges every
+// partial with an online log-sum-exp, re-polling any granule whose tag is not yet this launch's
+// (a store still in flight from a block that has already arrived — never a block that is not yet
+// running, so nothing waits on scheduling and no CU is held while co-located engines need it;
+// polling mergers that waited on unscheduled producers cost the 3-engine bench 8-20 %). The tag is
+// a per-(row, kv head) epoch in device memory the merger advances (tag = epoch + 1: never 0,
+// never reused), so a granule left by any earlier launch can never match. Spins are bounded.
 #include "common.h"
 
 namespace llmc {
 
-constexpr float kNegBig = -1e30f;
+typedef __attribute__((ext_vector_type(4))) short s16x4m;
+typedef __attribute__((address_space(3))) s16x4m lds_s16x4m;
 
-// grid (nkv * G, B, ceil(D / DB)), 256 threads: one query head x DB dims per block; the 256
-// threads are DB dims x (256 / DB) chunk groups. ONE memory round trip for up to 16 * 256 / DB
-// chunks: every thread issues its (up to 16) partial-value loads and the block its m / l loads
-// together — the values do not depend on the softmax max — then the max, the scale factors and
-// the weighted sums are formed from registers and LDS; chunk groups meet in LDS. The host picks
-// DB from the grid's chunk count (64 / 32 / 16 for <= 64 / 128 / 256 chunks) so a wide split
-// (a TP rank's single kv head spread over 256 blocks) still merges in one round trip, on 4x the
-// blocks, instead of 4 dependent batches.
-template <int G, int DB>
-__global__ __launch_bounds__(256) void attn_decode_reduce_kernel(const float* __restrict__ part,
-                                                                 const int32_t* __restrict__ seq_lens,
-                                                                 bf16_t* __restrict__ out, int out_stride, int nkv,
-                                                                 int D, int chunk_arg, int gc, int max_chunks) {
-  static_assert(DB == 16 || DB == 32 || DB == 64, "DB");
-  constexpr int CG = 256 / DB;  // chunk groups
-  const int kvh = blockIdx.x / G, g = blockIdx.x % G, b = blockIdx.y;
-  extern __shared__ __attribute__((aligned(16))) char smem[];
-  float* sc = reinterpret_cast<float*>(smem);  // [max_chunks]: m, then exp(m - M)
-  float* lv = sc + max_chunks;                 // [max_chunks]: l
-  float* red = lv + max_chunks;                // [CG][DB] + 8 scratch
-  const int tid = threadIdx.x, stride = D + 2;
-  const float* pb = part + ((static_cast<int64_t>(b) * nkv + kvh) * max_chunks * G + g) * stride;
-  const int64_t cstride = static_cast<int64_t>(G) * stride;  // between consecutive chunks
-  const int dl = tid % DB, cg = tid / DB;
-  const int d = blockIdx.z * DB + dl;
-  const bool live = d < D;
-  // The partial values and this thread's (m, l) words are loaded for the GRID's chunk count gc
-  // before the sequence length arrives: they do not depend on it, so the length's round trip
-  // and theirs overlap. Slots past the sequence's own chunk count hold finite stale partials
-  // (the workspace starts zeroed) and are masked below, never multiplied in.
-  float v[16];
+constexpr float kNegInfM = -1e30f;
+constexpr int kVRowBytes = 256;              // LDS pitch of one V row (D <= 128)
+constexpr unsigned kSpinLimit = 1u << 22;    // polls before a merger gives up (never in practice)
+
+__device__ __forceinline__ int vswz(int row, int chunk) { return row * kVRowBytes + ((chunk ^ ((row & 7) << 1)) << 4); }
+
+// Per-wave attention state over 32-key sub-tiles (head h = lane & 15 of the wave's kv head).
+template <int G, int D>
+struct SubTile {
+  static constexpr int KS = D / 32;  // dim slabs for Q.K
+  static constexpr int DT = D / 16;  // 16-dim tiles of O^T
+  static constexpr int VCH = D / 8;  // 16-B chunks per V row
+  static constexpr int NV = (32 * VCH + 63) / 64;  // 16-B V chunks per lane per sub-tile
+
+  bf16x8 qf[KS];
+  f32x4 acc[DT];
+  float m_run, l_run;
+
+  __device__ __forceinline__ void init(const bf16_t* qrow_kvh, int lane) {
+    const int h = lane & 15, g4 = lane >> 4;
+    const bool real = h < G;
+    const bf16_t* qrow = qrow_kvh + (real ? h : 0) * D;
 #pragma unroll
-  for (int j = 0; j < 16; ++j) {
-    const int c = min(cg + CG * j, gc - 1);  // clamped: all loads in flight, masked below
-    v[j] = live ? pb[c * cstride + d] : 0.f;
-  }
-  float m0 = kNegBig, l0 = 0.f;
-  if (tid < gc) {
-    m0 = pb[tid * cstride + D];
-    l0 = pb[tid * cstride + D + 1];
-  }
-  const int L = seq_lens[b];
-  const int nchunks = decode_nsplit(L, gc, chunk_arg);
-  if (nchunks <= 1) return;
-  float mx = kNegBig;
-  for (int c = tid; c < nchunks; c += 256) {
-    const float m = c == tid ? m0 : pb[c * cstride + D];
-    sc[c] = m;
-    lv[c] = c == tid ? l0 : pb[c * cstride + D + 1];
-    mx = fmaxf(mx, m);
-  }
-  mx = wave_max(mx);
-  if ((tid & 63) == 0) red[256 + tid / 64] = mx;
-  __syncthreads();
-  mx = fmaxf(fmaxf(red[256], red[257]), fmaxf(red[258], red[259]));
-  float ls = 0.f;
-  for (int c = tid; c < nchunks; c += 256) {
-    const float e = __expf(sc[c] - mx);
-    sc[c] = e;
-    ls += lv[c] * e;
-  }
-  ls = wave_sum(ls);
-  if ((tid & 63) == 0) red[260 + tid / 64] = ls;
-  __syncthreads();
-  const float lsum = red[260] + red[261] + red[262] + red[263];
-  float o = 0.f;
-#pragma unroll
-  for (int j = 0; j < 16; ++j) o += (cg + CG * j < nchunks) ? v[j] * sc[cg + CG * j] : 0.f;
-  for (int c0 = cg + 16 * CG; c0 < nchunks; c0 += 16 * CG) {  // beyond one round trip: further batches
-    float w[16];
-#pragma unroll
-    for (int j = 0; j < 16; ++j) {
-      const int c = min(c0 + CG * j, nchunks - 1);
-      w[j] = live ? pb[c * cstride + d] : 0.f;
+    for (int ks = 0; ks < KS; ++ks) {
+      bf16x8 v = *reinterpret_cast<const bf16x8*>(qrow + ks * 32 + 8 * g4);
+      qf[ks] = real ? v : bf16x8{0, 0, 0, 0, 0, 0, 0, 0};
     }
 #pragma unroll
-    for (int j = 0; j < 16; ++j) o += (c0 + CG * j < nchunks) ? w[j] * sc[c0 + CG * j] : 0.f;
+    for (int dt = 0; dt < DT; ++dt) acc[dt] = f32x4{0.f, 0.f, 0.f, 0.f};
+    m_run = kNegInfM;
+    l_run = 0.f;
   }
-  red[cg * DB + dl] = o;
-  __syncthreads();
-  if (cg == 0 && live) {
-    float tot = 0.f;
+
+  // K (A operand, registers) and V (staged for LDS) loads of keys [kbase, kbase + 32), clamped
+  // to `end`; row(key) -> the key's K (or V) row.
+  template <typename RowFn>
+  __device__ __forceinline__ void issue(int kbase, int end, int lane, RowFn row, const bf16_t* kc, const bf16_t* vc,
+                                        bf16x8 (&kf)[2][KS], u32x4 (&vst)[NV]) {
+    const int h = lane & 15, g4 = lane >> 4;
 #pragma unroll
-    for (int i = 0; i < CG; ++i) tot += red[i * DB + dl];
-    out[static_cast<int64_t>(b) * out_stride + (kvh * G + g) * D + d] = f32_to_bf16(tot / lsum);
+    for (int kt = 0; kt < 2; ++kt) {
+      int key = kbase + kt * 16 + h;
+      key = key < end ? key : end - 1;
+      const bf16_t* kr = row(kc, key);
+#pragma unroll
+      for (int ks = 0; ks < KS; ++ks) kf[kt][ks] = *reinterpret_cast<const bf16x8*>(kr + ks * 32 + 8 * g4);
+    }
+#pragma unroll
+    for (int u = 0; u < NV; ++u) {
+      const int flat = u * 64 + lane;
+      const int r = flat / VCH, ch = flat % VCH;
+      if (r < 32) {
+        int key = kbase + r;
+        key = key < end ? key : end - 1;
+        vst[u] = *reinterpret_cast<const u32x4*>(row(vc, key) + ch * 8);
+      }
+    }
+  }
+
+  __device__ __forceinline__ void compute(int kbase, int end, int lane, char* vbuf, float scale_log2,
+                                          bf16x8 (&kf)[2][KS], u32x4 (&vst)[NV]) {
+    const int g4 = lane >> 4;
+    // ---- S^T = K . Q^T ----
+    f32x4 s[2];
+#pragma unroll
+    for (int kt = 0; kt < 2; ++kt) {
+      s[kt] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int ks = 0; ks < KS; ++ks) s[kt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kf[kt][ks], qf[ks], s[kt], 0, 0, 0);
+    }
+    // V rows -> LDS (swizzled), visible to this wave's tr reads after lgkmcnt(0)
+#pragma unroll
+    for (int u = 0; u < NV; ++u) {
+      const int flat = u * 64 + lane;
+      const int r = flat / VCH, ch = flat % VCH;
+      if (r < 32) *reinterpret_cast<u32x4*>(vbuf + vswz(r, ch)) = vst[u];
+    }
+    // ---- online softmax over this sub-tile (keys 4*g4+i and 16+4*g4+i of the lane's head) ----
+    float mx = kNegInfM;
+#pragma unroll
+    for (int kt = 0; kt < 2; ++kt)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int key = kbase + kt * 16 + 4 * g4 + i;
+        const float v = key < end ? s[kt][i] * scale_log2 : kNegInfM;
+        s[kt][i] = v;
+        mx = fmaxf(mx, v);
+      }
+    mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
+    mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+    const float m_new = fmaxf(m_run, mx);
+    const float alpha = exp2f(m_run - m_new);
+    float rs = 0.f;
+#pragma unroll
+    for (int kt = 0; kt < 2; ++kt)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const float p = s[kt][i] <= -1e29f ? 0.f : exp2f(s[kt][i] - m_new);
+        s[kt][i] = p;
+        rs += p;
+      }
+    rs += __shfl_xor(rs, 16, 64);
+    rs += __shfl_xor(rs, 32, 64);
+    l_run = l_run * alpha + rs;
+    m_run = m_new;
+    // P^T fragment: k = 8*g4 + j  <->  key 4*g4 + j (j < 4), 16 + 4*g4 + (j - 4) (j >= 4)
+    bf16x8 pf;
+    {
+      u32x4 pk;
+      pk[0] = pack_bf16x2(s[0][0], s[0][1]);
+      pk[1] = pack_bf16x2(s[0][2], s[0][3]);
+      pk[2] = pack_bf16x2(s[1][0], s[1][1]);
+      pk[3] = pack_bf16x2(s[1][2], s[1][3]);
+      pf = __builtin_bit_cast(bf16x8, pk);
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // this wave's V rows are in LDS
+    // ---- O^T += V^T . P^T ; A = V^T rows d = dt*16 + (lane & 15), keys via two tr reads ----
+    const int qq = (lane & 15) >> 2, p4 = lane & 3;
+#pragma unroll
+    for (int dt = 0; dt < DT; ++dt) {
+      const int ch = 2 * dt + (p4 >> 1);
+      const int sub = (p4 & 1) * 8;
+      const s16x4m lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4m*)(vbuf + vswz(4 * g4 + qq, ch) + sub));
+      const s16x4m hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4m*)(vbuf + vswz(16 + 4 * g4 + qq, ch) + sub));
+      bf16x8 a;
+      a[0] = lo[0]; a[1] = lo[1]; a[2] = lo[2]; a[3] = lo[3];
+      a[4] = hi[0]; a[5] = hi[1]; a[6] = hi[2]; a[7] = hi[3];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) acc[dt][i] *= alpha;
+      acc[dt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, pf, acc[dt], 0, 0, 0);
+    }
+    // the next sub-tile overwrites vbuf: make sure every tr read of this one has returned
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  }
+
+  // wave state -> red[wave][h][D + 2] (O^T column h, then m, l; only lanes with h < G)
+  __device__ __forceinline__ void to_lds(float* red, int wave, int lane) const {
+    const int h = lane & 15, g4 = lane >> 4;
+    if (h < G) {
+      float* r = red + (wave * G + h) * (D + 2);
+#pragma unroll
+      for (int dt = 0; dt < DT; ++dt)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) r[dt * 16 + 4 * g4 + i] = acc[dt][i];
+      if (g4 == 0) {
+        r[D] = m_run;
+        r[D + 1] = l_run;
+      }
+    }
+  }
+};
+
+// Merge the NW waves' states of head hh at dim d (log2 domain): o (unnormalised), m, l.
+template <int G, int D, int NW>
+__device__ __forceinline__ void merge_waves(const float* red, int hh, int d, float& o, float& m, float& l) {
+  constexpr int stride = D + 2;
+  float mx = kNegInfM;
+#pragma unroll
+  for (int w = 0; w < NW; ++w) mx = fmaxf(mx, red[(w * G + hh) * stride + D]);
+  float ls = 0.f, oo = 0.f;
+#pragma unroll
+  for (int w = 0; w < NW; ++w) {
+    const float* r = red + (w * G + hh) * stride;
+    const float sc = exp2f(r[D] - mx);
+    ls += r[D + 1] * sc;
+    oo += r[d] * sc;
+  }
+  o = oo;
+  m = mx;
+  l = ls;
+}
+
+// The block's own result when it is the sequence's only chunk.
+template <int G, int D, int NW>
+__device__ __forceinline__ void store_direct(const float* red, bf16_t* out_row, int tid) {
+  for (int idx = tid; idx < G * D; idx += NW * 64) {
+    const int hh = idx / D, d = idx % D;
+    float o, m, l;
+    merge_waves<G, D, NW>(red, hh, d, o, m, l);
+    out_row[hh * D + d] = f32_to_bf16(o / l);
   }
 }
 
-static size_t reduce_lds(int max_chunks) { return (2 * static_cast<size_t>(max_chunks) + 256 + 8) * sizeof(float); }
+// ---- partial granules -------------------------------------------------------------------------
+// Per (row, kv head) slab: [max_chunks][G][D/4 + 1] 16-B units. Unit u < D/4 = {bf16x2 O[4u..4u+1]/l,
+// tag, bf16x2 O[4u+2..4u+3]/l, tag}; unit D/4 = {lambda, tag, lambda, tag}. Every 8-B half is ONE
+// granule of one write-through (sc1) store (MI355X_MICROARCH.md § visibility R2: 16-B sc1 halves
+// untorn), so a reader needs no ordering: it checks every tag. Normalised partials in bf16 (as the
+// output; the weights and lambda stay f32).
+__device__ __forceinline__ void st16_sc1(__amdgpu_buffer_rsrc_t rsrc, int byte_off, u32x4 v) {
+  __builtin_amdgcn_raw_buffer_store_b128(v, rsrc, byte_off, 0, 16);
+}
+__device__ __forceinline__ u32x4 ld16_sc1(__amdgpu_buffer_rsrc_t rsrc, int byte_off) {
+  return __builtin_amdgcn_raw_buffer_load_b128(rsrc, byte_off, 0, 16);
+}
+// lambda granule: an 8-B relaxed agent-scope atomic load (global_load_dwordx2 sc1). Being an
+// ordered load it also keeps the compiler from hoisting the O-unit buffer loads out of a re-poll
+// (a loop with no ordered access looks loop-invariant to it).
+__device__ __forceinline__ u32x2 ld8_atomic(const char* base, int byte_off) {
+  const uint64_t v = __hip_atomic_load(reinterpret_cast<const uint64_t*>(base + byte_off), __ATOMIC_RELAXED,
+                                       __HIP_MEMORY_SCOPE_AGENT);
+  return u32x2{static_cast<uint32_t>(v), static_cast<uint32_t>(v >> 32)};
+}
 
-// One reduce launch; DB (dims per block) from the largest chunk count this grid can produce, so
-// even a 256-way split merges in one round trip.
-template <int G>
-static int launch_reduce(int B, int nkv, int D, int chunk_arg, int gc, int max_chunks, hipStream_t s, const void* part,
-                         const void* sl, void* out, int out_stride) {
-  const size_t lds = reduce_lds(max_chunks);
-  if (gc <= 64) {
-    attn_decode_reduce_kernel<G, 64><<<dim3(nkv * G, B, (D + 63) / 64), 256, lds, s>>>(
-        (const float*)part, (const int32_t*)sl, (bf16_t*)out, out_stride, nkv, D, chunk_arg, gc, max_chunks);
-  } else if (gc <= 128) {
-    attn_decode_reduce_kernel<G, 32><<<dim3(nkv * G, B, (D + 31) / 32), 256, lds, s>>>(
-        (const float*)part, (const int32_t*)sl, (bf16_t*)out, out_stride, nkv, D, chunk_arg, gc, max_chunks);
-  } else {
-    attn_decode_reduce_kernel<G, 16><<<dim3(nkv * G, B, (D + 15) / 16), 256, lds, s>>>(
-        (const float*)part, (const int32_t*)sl, (bf16_t*)out, out_stride, nkv, D, chunk_arg, gc, max_chunks);
+template <int G, int D, int NW>
+__device__ __forceinline__ void publish_partial(const float* red, __amdgpu_buffer_rsrc_t rsrc, int c, uint32_t tag,
+                                                int tid) {
+  constexpr int HQ = D / 4, RU = HQ + 1;
+  for (int p = tid; p < G * HQ; p += NW * 64) {
+    const int g = p / HQ, u = p % HQ;
+    float o[4], m, l;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) merge_waves<G, D, NW>(red, g, 4 * u + e, o[e], m, l);
+    const float inv = 1.f / l;
+    const int row = (c * G + g) * RU;
+    st16_sc1(rsrc, (row + u) * 16, u32x4{pack_bf16x2(o[0] * inv, o[1] * inv), tag, pack_bf16x2(o[2] * inv, o[3] * inv), tag});
+    if (u == 0) {
+      const uint32_t lam = __float_as_uint(m + __log2f(l));
+      st16_sc1(rsrc, (row + HQ) * 16, u32x4{lam, tag, lam, tag});
+    }
   }
+}
+
+// The last-arriving chunk block merges all nchunks partials: thread = (output quad, chunk group),
+// up to 8 chunks' {O quad, lambda} loads in flight per thread, re-polled until every tag matches
+// (a straggler is a store already issued by a block that has arrived: no wait on any block that
+// is not running), folded with an online log-sum-exp; chunk groups meet in LDS.
+template <int G, int D, int NT>
+__device__ __forceinline__ void merge_all(float* slab, int max_chunks, int nchunks, uint32_t tag, bf16_t* out_row,
+                                          f32x4* scratch, int tid) {
+  constexpr int HQ = D / 4, RU = HQ + 1, Q = G * HQ;
+  static_assert(Q <= NT, "one pass");
+  const __amdgpu_buffer_rsrc_t rsrc = __builtin_amdgcn_make_buffer_rsrc(slab, 0, max_chunks * G * RU * 16, 0x00020000);
+  const char* base = reinterpret_cast<const char*>(slab);
+  const int ngr = max(1, min(NT / Q, nchunks));
+  const int gr = tid / Q;
+  float M = kNegInfM, S = 0.f, a[4] = {0.f, 0.f, 0.f, 0.f};
+  if (gr < ngr) {
+    const int g = (tid % Q) / HQ, u = (tid % Q) % HQ;
+    for (int c0 = gr; c0 < nchunks; c0 += 8 * ngr) {
+      u32x4 ov[8];
+      u32x2 lv[8];
+      for (unsigned spins = 0;; ++spins) {
+        bool ok = true;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const int cc = min(c0 + j * ngr, nchunks - 1);  // clamped: every load in flight, masked below
+          const int row = (cc * G + g) * RU;
+          ov[j] = ld16_sc1(rsrc, (row + u) * 16);
+          lv[j] = ld8_atomic(base, (row + HQ) * 16);
+        }
+#pragma unroll
+        for (int j = 0; j < 8; ++j)
+          if (c0 + j * ngr < nchunks) ok = ok && ov[j][1] == tag && ov[j][3] == tag && lv[j][1] == tag;
+        if (__all(ok) || spins >= kSpinLimit) break;
+        __builtin_amdgcn_s_sleep(2);
+      }
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        if (c0 + j * ngr < nchunks) {
+          const float lam = __uint_as_float(lv[j][0]);
+          const float mn = fmaxf(M, lam);
+          const float so = exp2f(M - mn), sn = exp2f(lam - mn);
+          S = S * so + sn;
+          a[0] = a[0] * so + bf16_lo(ov[j][0]) * sn;
+          a[1] = a[1] * so + bf16_hi(ov[j][0]) * sn;
+          a[2] = a[2] * so + bf16_lo(ov[j][2]) * sn;
+          a[3] = a[3] * so + bf16_hi(ov[j][2]) * sn;
+          M = mn;
+        }
+      }
+    }
+  }
+  scratch[2 * tid] = f32x4{M, S, 0.f, 0.f};
+  scratch[2 * tid + 1] = f32x4{a[0], a[1], a[2], a[3]};
+  __syncthreads();
+  if (tid < Q) {
+    f32x4 ms = scratch[2 * tid], acc = scratch[2 * tid + 1];
+    for (int k = 1; k < ngr; ++k) {
+      const f32x4 ms2 = scratch[2 * (tid + k * Q)], acc2 = scratch[2 * (tid + k * Q) + 1];
+      const float mn = fmaxf(ms[0], ms2[0]);
+      const float so = exp2f(ms[0] - mn), sn = exp2f(ms2[0] - mn);
+      ms = f32x4{mn, ms[1] * so + ms2[1] * sn, 0.f, 0.f};
+      acc = acc * so + acc2 * sn;
+    }
+    const int g = tid / HQ, u = tid % HQ;
+    const float inv = 1.f / ms[1];
+    *reinterpret_cast<u32x2*>(out_row + g * D + 4 * u) =
+        u32x2{pack_bf16x2(acc[0] * inv, acc[1] * inv), pack_bf16x2(acc[2] * inv, acc[3] * inv)};
+  }
+}
+
+// Publish this chunk's partial, take a ticket; the last arriver merges, then re-arms the ticket and
+// advances the epoch (every block of this launch read the epoch before it arrived). `flag` is one
+// LDS word. Returns nothing: every block but the last exits inside.
+template <int G, int D, int NW>
+__device__ __forceinline__ void publish_and_merge(const float* red, float* part, int* ctr, int b, int nkv, int kvh,
+                                                  int c, int nchunks, int max_chunks, uint32_t tag, bf16_t* out_row,
+                                                  char* smem, int* flag, int tid) {
+  constexpr int RU = D / 4 + 1;
+  float* slab = part + (static_cast<int64_t>(b) * nkv + kvh) * max_chunks * G * RU * 4;
+  publish_partial<G, D, NW>(red, __builtin_amdgcn_make_buffer_rsrc(slab, 0, max_chunks * G * RU * 16, 0x00020000), c,
+                            tag, tid);
+  __syncthreads();  // every wave's stores are issued (not drained: the merger checks tags)
+  if (tid == 0) *flag = __hip_atomic_fetch_add(ctr, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == nchunks - 1;
+  __syncthreads();
+  if (*flag == 0) return;
+  merge_all<G, D, NW * 64>(slab, max_chunks, nchunks, tag, out_row, reinterpret_cast<f32x4*>(smem), tid);
+  if (tid == 0) {
+    __hip_atomic_store(ctr, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);                     // re-arm
+    __hip_atomic_store(ctr + 1, static_cast<int>(tag), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // epoch
+  }
+}
+
+// ---------------------------------------------------------------------------------------------
+template <int G, int D, int NW>
+__global__ __launch_bounds__(NW * 64) void attn_decode_split_kernel(
+    const bf16_t* __restrict__ q, int q_stride, const bf16_t* __restrict__ k_cache,
+    const bf16_t* __restrict__ v_cache, const int32_t* __restrict__ block_tables, int bt_stride,
+    const int32_t* __restrict__ seq_lens, float* __restrict__ part, int* __restrict__ counters, bf16_t* __restrict__ out,
+    int out_stride, int nkv, int bs, int nblocks, int min_chunk, int max_chunks, float scale_log2) {
+  static_assert(G <= 16 && D % 32 == 0 && D <= 128, "shape");
+  using ST = SubTile<G, D>;
+  constexpr int NT = NW * 64;
+  const int c = blockIdx.x, kvh = blockIdx.y, b = blockIdx.z;
+  int* ctr = counters + 2 * (b * nkv + kvh);  // {ticket, epoch}
+  const uint32_t tag = static_cast<uint32_t>(__hip_atomic_load(ctr + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) + 1u;
+  const int L = seq_lens[b];
+  const int nchunks = decode_nsplit(L, gridDim.x, -min_chunk);
+  if (c >= nchunks) return;
+  int start, end;
+  decode_range(L, nchunks, c, -min_chunk, start, end);
+
+  const int tid = threadIdx.x, wave = tid / 64, lane = tid % 64;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  char* vbuf = smem + wave * 32 * kVRowBytes;  // per-wave V image [32][256 B]
+  float* red = reinterpret_cast<float*>(smem + NW * 32 * kVRowBytes);
+  int* pages = reinterpret_cast<int*>(red + NW * G * (D + 2));  // this block's page ids
+
+  ST st;
+  st.init(q + static_cast<int64_t>(b) * q_stride + kvh * G * D, lane);
+  // stage the block's page ids once (no dependent block-table load per key)
+  const int32_t* bt = block_tables + static_cast<int64_t>(b) * bt_stride;
+  const int p0 = start / bs;
+  const int npages = (end - 1) / bs - p0 + 1;
+  // page ids clamped into the cache: a corrupt block table reads a wrong page, never a wild address
+  for (int i = tid; i < npages; i += NT) pages[i] = min(max(bt[min(p0 + i, bt_stride - 1)], 0), nblocks - 1);
+  __syncthreads();
+  const int64_t head_stride = static_cast<int64_t>(bs) * D;
+  auto row = [&](const bf16_t* cache, int key) {
+    const int64_t page = pages[key / bs - p0];
+    return cache + (page * nkv + kvh) * head_stride + static_cast<int64_t>(key % bs) * D;
+  };
+
+  const int per_wave = (((end - start + NW - 1) / NW) + 31) & ~31;  // 32-key sub-tiles per wave
+  const int wbase = start + wave * per_wave;
+  bf16x8 kfA[2][ST::KS], kfB[2][ST::KS];
+  u32x4 vsA[ST::NV], vsB[ST::NV];
+  auto valid = [&](int k) { return k - wbase < per_wave && k < end; };  // wave-uniform
+  // two named register sets, hand-unrolled (no runtime-indexed register arrays, guide rule 20):
+  // the next sub-tile's loads are in flight while the current one computes
+  if (valid(wbase)) st.issue(wbase, end, lane, row, k_cache, v_cache, kfA, vsA);
+  for (int k0 = wbase;; k0 += 64) {
+    if (!valid(k0)) break;
+    if (valid(k0 + 32)) st.issue(k0 + 32, end, lane, row, k_cache, v_cache, kfB, vsB);
+    st.compute(k0, end, lane, vbuf, scale_log2, kfA, vsA);
+    if (!valid(k0 + 32)) break;
+    if (valid(k0 + 64)) st.issue(k0 + 64, end, lane, row, k_cache, v_cache, kfA, vsA);
+    st.compute(k0 + 32, end, lane, vbuf, scale_log2, kfB, vsB);
+  }
+  st.to_lds(red, wave, lane);
+  __syncthreads();
+  bf16_t* out_row = out + static_cast<int64_t>(b) * out_stride + kvh * G * D;
+  if (nchunks == 1) {
+    store_direct<G, D, NW>(red, out_row, tid);
+    return;
+  }
+  publish_and_merge<G, D, NW>(red, part, ctr, b, nkv, kvh, c, nchunks, max_chunks, tag, out_row, smem,
+                              reinterpret_cast<int*>(pages), tid);
+}
+
+// ---------------------------------------------------------------------------------------------
+template <int G, int D>
+__global__ __launch_bounds__(256) void attn_decode_fused_kernel(
+    const bf16_t* __restrict__ q, int q_stride, const bf16_t* __restrict__ k_cache,
+    const bf16_t* __restrict__ v_cache, const int32_t* __restrict__ block_tables, int bt_stride,
+    const int32_t* __restrict__ seq_lens, float* __restrict__ part, int* __restrict__ counters,
+    bf16_t* __restrict__ out, int out_stride, int nkv, int bs, int nblocks, int chunk, int max_chunks,
+    float scale_log2) {
+  static_assert(G <= 16 && D % 32 == 0 && D <= 128, "shape");
+  using ST = SubTile<G, D>;
+  const int c = blockIdx.x, kvh = blockIdx.y, b = blockIdx.z;
+  const int tid = threadIdx.x, wave = tid / 64, lane = tid % 64;
+  const int per_wave = chunk / 4;  // keys per wave (32 or 64): inside one page (host-checked)
+  // ONE round trip for everything that does not depend on the sequence length: the length, this
+  // wave's page id (wave-uniform: scalar cache), the merge epoch and Q (vector)
+  const int key0 = c * chunk + wave * per_wave;
+  const int32_t* bt = block_tables + static_cast<int64_t>(b) * bt_stride;
+  const int pidx = __builtin_amdgcn_readfirstlane(min(key0 / bs, bt_stride - 1));
+  const int page = min(max(ld_scalar(bt + pidx), 0), nblocks - 1);  // clamped into the cache
+  const int L = ld_scalar(seq_lens + b);
+  int* ctr = counters + 2 * (b * nkv + kvh);  // {ticket, epoch}
+  const uint32_t tag = static_cast<uint32_t>(__hip_atomic_load(ctr + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) + 1u;
+  ST st;
+  st.init(q + static_cast<int64_t>(b) * q_stride + kvh * G * D, lane);
+  if (c * chunk >= L) return;  // block-uniform
+  const int nchunks = (L + chunk - 1) / chunk;
+  const int end = min(L, key0 + per_wave);
+
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  char* vbuf = smem + wave * 32 * kVRowBytes;
+  float* red = reinterpret_cast<float*>(smem + 4 * 32 * kVRowBytes);
+  if (key0 < L) {  // wave-uniform
+    const int64_t base = (static_cast<int64_t>(page) * nkv + kvh) * bs * D;
+    auto row = [&](const bf16_t* cache, int key) { return cache + base + static_cast<int64_t>(key % bs) * D; };
+    bf16x8 kfA[2][ST::KS], kfB[2][ST::KS];
+    u32x4 vsA[ST::NV], vsB[ST::NV];
+    st.issue(key0, end, lane, row, k_cache, v_cache, kfA, vsA);
+    if (key0 + 32 < end) st.issue(key0 + 32, end, lane, row, k_cache, v_cache, kfB, vsB);
+    st.compute(key0, end, lane, vbuf, scale_log2, kfA, vsA);
+    if (key0 + 32 < end) st.compute(key0 + 32, end, lane, vbuf, scale_log2, kfB, vsB);
+  }
+  st.to_lds(red, wave, lane);
+  __syncthreads();
+  bf16_t* out_row = out + static_cast<int64_t>(b) * out_stride + kvh * G * D;
+  if (nchunks == 1) {
+    store_direct<G, D, 4>(red, out_row, tid);
+    return;
+  }
+  publish_and_merge<G, D, 4>(red, part, ctr, b, nkv, kvh, c, nchunks, max_chunks, tag, out_row, smem,
+                             reinterpret_cast<int*>(red + 4 * G * (D + 2)), tid);
+}
+
+// Waves per split block: 8 with GQA; 4 without (G = 1: one head per kv head, Phi-3's 32 kv heads
+// already give 512 blocks, and 8-wave blocks at 212 VGPRs would halve the blocks resident per CU).
+template <int G>
+constexpr int split_waves() { return G == 1 ? 4 : 8; }
+
+template <int G, int D>
+static int launch_split(dim3 grid, hipStream_t s, const void* q, int q_stride, const void* kc, const void* vc,
+                        const void* bt, int bt_stride, const void* sl, void* part, void* ctr, void* out, int out_stride,
+                        int nkv, int bs, int nblocks, int chunk, int max_chunks, float scale) {
+  constexpr int NW = split_waves<G>();
+  // page-id staging sized for the largest balanced range any sequence of this table can get
+  const int grid_chunks = static_cast<int>(grid.x);
+  const int units = (bt_stride * bs + 31) / 32;
+  const int bal = 32 * ((units + grid_chunks - 1) / grid_chunks) + 32;
+  const int max_chunk = bal > 2 * chunk ? bal : 2 * chunk;
+  const size_t lds = NW * 32 * kVRowBytes + static_cast<size_t>(NW) * G * (D + 2) * sizeof(float) +
+                     static_cast<size_t>((max_chunk + bs - 1) / bs + 2) * sizeof(int);
+  if (lds > 160 * 1024) return -4;
+  auto kern = attn_decode_split_kernel<G, D, NW>;
+  static bool attr_set = false;
+  if (!attr_set) {
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize,
+                              160 * 1024);
+    attr_set = true;
+  }
+  kern<<<grid, NW * 64, lds, s>>>((const bf16_t*)q, q_stride, (const bf16_t*)kc, (const bf16_t*)vc,
+                                  (const int32_t*)bt, bt_stride, (const int32_t*)sl, (float*)part, (int*)ctr,
+                                  (bf16_t*)out, out_stride, nkv, bs, nblocks, chunk, max_chunks,
+                                  scale * 1.4426950408889634f);
   return static_cast<int>(hipGetLastError());
+}
+
+template <int G, int D>
+static int launch_fused(dim3 grid, hipStream_t s, const void* q, int q_stride, const void* kc, const void* vc,
+                        const void* bt, int bt_stride, const void* sl, void* part, void* ctr, void* out, int out_stride,
+                        int nkv, int bs, int nblocks, int chunk, int max_chunks, float scale) {
+  const size_t lds = 4 * 32 * kVRowBytes + static_cast<size_t>(4) * G * (D + 2) * sizeof(float) + 16;  // + flag
+  if (lds > 64 * 1024) return -4;
+  attn_decode_fused_kernel<G, D><<<grid, 256, lds, s>>>(
+      (const bf16_t*)q, q_stride, (const bf16_t*)kc, (const bf16_t*)vc, (const int32_t*)bt, bt_stride,
+      (const int32_t*)sl, (float*)part, (int*)ctr, (bf16_t*)out, out_stride, nkv, bs, nblocks, chunk, max_chunks,
+      scale * 1.4426950408889634f);
+  return static_cast<int>(hipGetLastError());
+}
+
+template <int G>
+static int launch_g(bool fused, int D, dim3 grid, hipStream_t s, const void* q, int q_stride, const void* kc,
+                    const void* vc, const void* bt, int bt_stride, const void* sl, void* part, void* ctr, void* out,
+                    int out_stride, int nkv, int bs, int nblocks, int chunk, int max_chunks, float scale) {
+#define LLMC_ATTN_D(DD)                                                                                          \
+  case DD:                                                                                                       \
+    return fused ? launch_fused<G, DD>(grid, s, q, q_stride, kc, vc, bt, bt_stride, sl, part, ctr, out, out_stride, \
+                                       nkv, bs, nblocks, chunk, max_chunks, scale)                               \
+                 : launch_split<G, DD>(grid, s, q, q_stride, kc, vc, bt, bt_stride, sl, part, ctr, out, out_stride, \
+                                       nkv, bs, nblocks, chunk, max_chunks, scale);
+  switch (D) {
+    LLMC_ATTN_D(64)
+    LLMC_ATTN_D(96)
+    LLMC_ATTN_D(128)
+    default: return -2;
+  }
+#undef LLMC_ATTN_D
 }
 
 }  // namespace llmc
 
 using namespace llmc;
 
-extern "C" int llmc_attn_decode_mfma(const void*, int, const void*, const void*, const void*, int, const void*, void*,
-                                     void*, void*, int, int, int, int, int, int, int, int, int, int, float, int,
-                                     hipStream_t);
-
-// One decode step's attention for rows 0..B-1. fused = 1 (short contexts): fixed 128-key chunks,
-// grid_chunks = bucket capacity / 128, merged in the same launch (part [B, nkv, max_chunks, G, D + 4],
-// counters [B, nkv] int32 zeroed once). fused = 0 (long contexts): balanced split over <= grid_chunks
-// blocks of >= chunk keys (a multiple of 128) + the reduce launch (part [B, nkv, max_chunks, G, D + 2]).
+// Attention of one decode step for rows 0..B-1, one launch.
+// part: f32 [B, nkv, max_chunks, G, D + 4] partial granules (zeroed once); counters: int32
+// [B, nkv, 2] {ticket, epoch} (zeroed once; the kernel re-arms the ticket and advances the epoch).
+// fused = 1 (short contexts): grid_chunks fixed chunk-key blocks (chunk 128 or 256; bs % (chunk/4) == 0).
+// fused = 0 (long contexts): balanced split over <= grid_chunks blocks of >= chunk keys (multiple of 128).
 extern "C" int llmc_attn_decode(const void* q, int q_stride, const void* k_cache, const void* v_cache,
                                 const void* block_tables, int bt_stride, const void* seq_lens, void* part,
                                 void* counters, void* out, int out_stride, int B, int nh, int nkv, int D, int bs,
                                 int nblocks, int chunk, int grid_chunks, int max_chunks, float scale, int fused,
                                 hipStream_t s) {
-  if (D % 32 != 0 || D > 128 || nh % nkv != 0 || grid_chunks > max_chunks) return -1;
-  int rc = llmc_attn_decode_mfma(q, q_stride, k_cache, v_cache, block_tables, bt_stride, seq_lens, part, counters,
-                                 out, out_stride, B, nh, nkv, D, bs, nblocks, chunk, grid_chunks, max_chunks, scale,
-                                 fused, s);
-  if (rc != 0 || fused || grid_chunks <= 1) return rc;
-  switch (nh / nkv) {
-    case 1: return launch_reduce<1>(B, nkv, D, -chunk, grid_chunks, max_chunks, s, part, seq_lens, out, out_stride);
-    case 2: return launch_reduce<2>(B, nkv, D, -chunk, grid_chunks, max_chunks, s, part, seq_lens, out, out_stride);
-    case 4: return launch_reduce<4>(B, nkv, D, -chunk, grid_chunks, max_chunks, s, part, seq_lens, out, out_stride);
-    case 8: return launch_reduce<8>(B, nkv, D, -chunk, grid_chunks, max_chunks, s, part, seq_lens, out, out_stride);
-    default: return -2;
+  if (nh % nkv != 0 || grid_chunks > max_chunks || grid_chunks < 1 || nblocks < 1 || counters == nullptr ||
+      bt_stride < 1)
+    return -1;
+  if (fused ? ((chunk != 128 && chunk != 256) || bs % (chunk / 4) != 0) : (chunk % 128 != 0)) return -1;
+  const int G = nh / nkv;
+  if (static_cast<int64_t>(max_chunks) * G * (D / 4 + 1) * 16 >= (1ll << 31)) return -4;
+  dim3 grid(grid_chunks, nkv, B);
+  const bool f = fused != 0;
+  switch (G) {
+    case 1: return launch_g<1>(f, D, grid, s, q, q_stride, k_cache, v_cache, block_tables, bt_stride, seq_lens, part, counters, out, out_stride, nkv, bs, nblocks, chunk, max_chunks, scale);
+    case 2: return launch_g<2>(f, D, grid, s, q, q_stride, k_cache, v_cache, block_tables, bt_stride, seq_lens, part, counters, out, out_stride, nkv, bs, nblocks, chunk, max_chunks, scale);
+    case 4: return launch_g<4>(f, D, grid, s, q, q_stride, k_cache, v_cache, block_tables, bt_stride, seq_lens, part, counters, out, out_stride, nkv, bs, nblocks, chunk, max_chunks, scale);
+    case 8: return launch_g<8>(f, D, grid, s, q, q_stride, k_cache, v_cache, block_tables, bt_stride, seq_lens, part, counters, out, out_stride, nkv, bs, nblocks, chunk, max_chunks, scale);
+    default: return -3;
   }
 }

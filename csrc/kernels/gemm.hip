@@ -175,10 +175,12 @@ __global__ __launch_bounds__(256, 2) void gemm_kernel(const bf16_t* __restrict__
 //  * grid: bijective XCD remap (T1) then grouped tile order (8 M-tiles x all N per group).
 //  * fused epilogues: bf16 | f32 | residual add (C += A.W^T) | SiLU-mul of interleaved gate/up
 //    columns (C[m][n/2] = silu(g) * u).
-// Measured (MI355X, random bf16; profiles/r2_prefill_gemm.md): 1.28-1.38 PF/s on the Llama-3-8B
-// prefill shapes, 83-86 % of hipBLASLt on the same data. The remaining gap is structural (PMC:
-// hipBLASLt runs 4 waves x 128 x 128 with 512 registers each and 1.5x fewer LDS reads; this
-// 8-wave layout parks waves at barriers: SQ_WAIT_ANY 275M vs 37M wave-cycles per dispatch).
+// Measured (MI355X, random bf16; profiles/r2_prefill_gemm.md): 1.26-1.40 PF/s on the Llama-3-8B
+// prefill shapes, 83-87 % of hipBLASLt on the same data (PMC: hipBLASLt runs 4 waves x 128 x 128
+// with 512 registers each and 1.5x fewer LDS reads; this 8-wave layout parks waves at barriers).
+// A 4-wave 128 x 128-per-wave form of this kernel (5-slice 32-K LDS-DMA ring, one barrier per
+// slice, fragments double-buffered, accumulators split over VGPRs/AGPRs by hipcc) measured
+// 0.92-1.00 PF/s on the same shapes and was dropped.
 constexpr int kT = 256, kTK = 64;
 constexpr int kQuarter = 128 * kTK * 2;  // bytes
 constexpr int kSlots = 10;

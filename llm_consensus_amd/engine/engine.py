@@ -61,12 +61,14 @@ class EngineConfig:
 FUSED_CHUNK_SMALL, FUSED_CHUNK_LARGE = 128, 256
 
 
-def attn_buckets(ctxmax: int, blocks_per_head: int = 64, fused_max: int = 4096) -> List[tuple]:
+def attn_buckets(ctxmax: int, blocks_per_head: int = 64, fused_max: int = 4096, group: int = 4) -> List[tuple]:
     """Decode-attention shapes per context bucket: [(capacity_tokens, chunk, grid_chunks, fused)].
 
-    Capacities double from 1024. Buckets up to ``fused_max`` keys use the fused single-launch form
-    (fixed 128-key chunks up to 2048 keys, 256-key chunks above: at most 16 partials for the
-    in-launch merge; grid_chunks = capacity / chunk). Longer ones use the
+    Capacities double from 1024. Buckets up to ``fused_max`` keys use the fused form (fixed-chunk
+    blocks, grid_chunks = capacity / chunk): 128-key chunks up to 2048 keys with GQA (``group``
+    query heads per kv head >= 2; 8.8 vs 9.9 us at 2k) and up to 1024 without (Phi-3), 256-key
+    chunks above (10.9 vs 11.9 us at 4k; Phi-3 14.5 vs 23.3: 32 kv heads already fill the chip;
+    profiles/r2_attn_decode.md). Longer ones use the
     balanced split: ``chunk`` is the minimum of 128 keys per block, the kernel spreads a
     sequence's keys evenly over ``grid_chunks`` blocks, and the grid grows with the context until
     ``blocks_per_head`` (~1 block per CU over the kv heads of one row, measured on MI355X:
@@ -75,7 +77,7 @@ def attn_buckets(ctxmax: int, blocks_per_head: int = 64, fused_max: int = 4096) 
     while True:
         c = min(cap, ctxmax)
         if c <= fused_max:
-            ch = FUSED_CHUNK_SMALL if c <= 2048 else FUSED_CHUNK_LARGE
+            ch = FUSED_CHUNK_SMALL if c <= (2048 if group >= 2 else 1024) else FUSED_CHUNK_LARGE
             out.append((c, ch, (c + ch - 1) // ch, True))
         else:
             gc = min((c + 127) // 128, blocks_per_head)
@@ -86,6 +88,16 @@ def attn_buckets(ctxmax: int, blocks_per_head: int = 64, fused_max: int = 4096) 
         if cap >= ctxmax:
             return out
         cap *= 2
+
+
+def split_blocks_per_head(nh: int, nkv: int) -> int:
+    """Grid of the split (long-context) attention form per kv head: ~1 8-wave block per CU over the
+    row's kv heads (256 blocks; 512 without GQA, where a block's range costs less), capped so the
+    in-launch merge reads at most ~64 partial granule rows of 4 heads per merger
+    (chunks x G <= 256) and never more than 64 partials."""
+    G = max(1, nh // nkv)
+    blocks = 512 if G == 1 else 256
+    return max(1, min(blocks // nkv, 256 // G, 64))
 
 
 @dataclasses.dataclass
@@ -188,16 +200,10 @@ class Engine:
                             torch.zeros(self.tp.size, B, self.w.vocab_local, dtype=torch.float32, device=dev))
         # split-KV decode attention: one (chunk, grid) shape per context bucket
         ctxmax = self.ecfg.max_context + self.ecfg.steps_per_graph + 2
-        # target blocks per decode row (split form): ~1 per CU; without GQA (Phi-3: one query head
-        # per kv head) a block's key range costs less, and 2 per CU measured faster (9.45 vs 9.85 us
-        # at 2k keys, 14.9 vs 15.9 at 4k: profiles/r1_attn_decode_tp_shapes.md)
-        blocks = 512 if self.nh == self.nkv else 256
-        fused_max = ops.FUSED_ATTN_MAX_KEYS if self.bs % 32 == 0 else 0
-        self.attn_buckets = attn_buckets(ctxmax, max(1, blocks // self.nkv), fused_max)
-        split_chunks = max([gc for _, _, gc, f in self.attn_buckets if not f] or [1])
-        fused_chunks = max([gc for _, _, gc, f in self.attn_buckets if f] or [1])
-        self.attn_part, self.attn_counters = ops.decode_attn_workspace(B, self.nh, self.nkv, self.D, split_chunks, dev)
-        self.attn_part_f, _ = ops.decode_attn_workspace(B, self.nh, self.nkv, self.D, fused_chunks, dev, fused=True)
+        self.attn_buckets = attn_buckets(ctxmax, split_blocks_per_head(self.nh, self.nkv),
+                                         ops.FUSED_ATTN_MAX_KEYS if self.bs % 32 == 0 else 0, self.nh // self.nkv)
+        max_chunks = max(gc for _, _, gc, _ in self.attn_buckets)
+        self.attn_part, self.attn_counters = ops.decode_attn_workspace(B, self.nh, self.nkv, self.D, max_chunks, dev)
         if self.on_gpu:
             P = ops.sample_parts()
             self.ws_v = torch.zeros(B, P, dtype=torch.float32, device=dev)
@@ -491,7 +497,7 @@ class Engine:
         """One token for rows 0..B-1. ``bucket`` indexes ``attn_buckets`` (default: the largest)."""
         c = self.cfg
         _, chunk, grid_chunks, fused = self.attn_buckets[-1 if bucket is None else bucket]
-        part = self.attn_part_f if fused else self.attn_part
+        part = self.attn_part
         h, q, attn, act = self.h[:B], self.q[:B], self.attn[:B], self.act[:B]
         ops.embedding(self.tokens_in[:B], self.w.embed, out=h)
         for li, Lw in enumerate(self.w.layers):

@@ -154,28 +154,30 @@ FUSED_CHUNK = 128           # keys per block of the fused form
 
 
 def decode_attn_workspace(B, nh, nkv, D, max_chunks, device, fused: bool = False):
-    """(part, counters) for attn_decode: f32 partials [B, nkv, max_chunks, G, D + 2] (split form)
-    or [B, nkv, max_chunks, G, D + 4] (fused form: 16-B rows), and zeroed merge tickets [B, nkv]."""
+    """(part, counters) for attn_decode, either form: partial granules f32 [B, nkv, max_chunks, G,
+    D + 4] (bf16 {value pair, tag} granules merged in-launch) and the per-(row, kv head) {ticket,
+    epoch} int32 [B, nkv, 2], both zeroed once and never reset (the kernel re-arms the tickets and
+    advances the epochs). ``fused`` is accepted for call-site symmetry; the layout is the same."""
     G = nh // nkv
-    part = torch.zeros(B, nkv, max_chunks, G, D + (4 if fused else 2), dtype=torch.float32, device=device)
-    counters = torch.zeros(B, nkv, dtype=torch.int32, device=device)
+    part = torch.zeros(B, nkv, max_chunks, G, D + 4, dtype=torch.float32, device=device)
+    counters = torch.zeros(B, nkv, 2, dtype=torch.int32, device=device)
     return part, counters
 
 
 def attn_decode(q, k_cache, v_cache, block_tables, seq_lens, out, part, counters, nh, nkv, D, bs, chunk, scale,
                 grid_chunks: Optional[int] = None, fused: bool = False):
-    """Decode attention (K5). ``fused``: fixed 128-key chunks (``grid_chunks`` = bucket capacity /
-    128) merged in the same launch — short contexts; else the balanced split over <= grid_chunks
-    blocks of >= ``chunk`` keys + the reduce launch — long contexts. ``part`` must come from
-    ``decode_attn_workspace(..., fused=fused)``."""
+    """Decode attention (K5), one launch. ``fused``: fixed ``chunk``-key blocks (128 or 256;
+    ``grid_chunks`` = bucket capacity / chunk) — short contexts; else the balanced split over <=
+    grid_chunks 8-wave blocks of >= ``chunk`` keys — long contexts. Both merge their partials in
+    the same launch. ``part``/``counters`` come from ``decode_attn_workspace``."""
     if not q.is_cuda:
         out.copy_(oracle.attn_decode(q, k_cache, v_cache, block_tables, seq_lens, nh, nkv, D, bs, scale))
         return out
     B = q.shape[0]
     max_chunks = part.shape[2]
     gc = max_chunks if grid_chunks is None else min(grid_chunks, max_chunks)
-    if part.shape[-1] != D + (4 if fused else 2):
-        raise ValueError("attn_decode: workspace layout does not match the kernel form")
+    if part.shape[-1] != D + 4 or counters.shape[0] < B or counters.shape[-1] != 2:
+        raise ValueError("attn_decode: workspace does not match (use decode_attn_workspace)")
     kernels().attn_decode(_p(q), q.stride(0), _p(k_cache), _p(v_cache), _p(block_tables), block_tables.stride(0),
                           _p(seq_lens), _p(part), _p(counters), _p(out), out.stride(0), B, nh, nkv, D, bs,
                           k_cache.shape[0], chunk, gc, max_chunks, float(scale), 1 if fused else 0, _s(q))

@@ -60,11 +60,11 @@ def bench_attn(shapes=((32, 8, 128), (32, 32, 96), (16, 2, 128), (8, 1, 128))):
             gb = L * nkv * D * 2 * 2 / 1e9
             line = []
             best = 1e9
-            if L <= 4096:
+            if L <= 16384:
                 cap = 1024
                 while cap < L:
                     cap *= 2
-                for ch in (128, 256):
+                for ch in ((128, 256) if L <= 4096 else (128,)):
                     gc = cap // ch
                     part, ctr = ops.decode_attn_workspace(1, nh, nkv, D, gc, "cuda", fused=True)
                     us = timeit(lambda: ops.attn_decode(q, kc, vc, bt, sl, out, part, ctr, nh, nkv, D, 64, ch, sc,
@@ -99,7 +99,83 @@ SWEEP = ["256x1u8", "256x2u4", "256x4u4", "512x1u8", "512x2u4", "128x1u8", "64x1
          "256x2u8", "512x4u2", "128x2u4", "1024x1u8", "1024x2u4", "1024x2u2", "1024x1u2", "768x1u4", "1024x4u2", "1024x1u6"]
 
 
-ALL_def bench_prefill():
+ALL_VARIANTS = os.environ.get("SWEEP_ALL") == "1"
+
+
+def bench_gemv_sweep(shapes=None):
+    """GEMV geometry sweep on COLD weights: the graph cycles through enough copies of W to exceed
+    the 256 MB MALL, as in a real decode step (16 GB streamed per token)."""
+    from llm_consensus_amd.utils.native import kernels
+
+    k = kernels()
+    for (N, K) in shapes or [(6144, 4096), (4096, 4096), (28672, 4096), (4096, 14336), (128256, 4096)]:
+        if K * 2 > 64 * 1024:
+            continue
+        copies = max(2, (1 << 30) // (N * K * 2))
+        Ws = [(torch.randn(N, K, device="cuda") * 0.02).to(BF) for _ in range(copies)]
+        x = torch.randn(1, K, device="cuda").to(BF)
+        nw = torch.ones(K, dtype=BF, device="cuda")
+        out = torch.zeros(1, N, dtype=BF, device="cuda")
+        res = []
+        for v, name in enumerate(SWEEP):
+            if not ALL_VARIANTS and name not in ("256x2u4", "512x1u8", "1024x1u4", "1024x1u6", "1024x1u8", "768x1u4",
+                                                 "1024x1u2"):
+                continue
+            st = torch.cuda.current_stream().cuda_stream
+
+            def run():
+                for W in Ws:
+                    k.gemv_sweep(v, x.data_ptr(), nw.data_ptr(), W.data_ptr(), out.data_ptr(), N, K,
+                                 torch.cuda.current_stream().cuda_stream)
+            us = timeit(run, iters=2, warm=1) / copies
+            res.append(f"{name} {us:6.2f}")
+        del Ws
+        torch.cuda.empty_cache()
+        print(f"sweep N={N} K={K} ({N * K * 2 / 1e6:.0f} MB, {copies} copies): " + "  ".join(res), flush=True)
+
+
+def bench_qkv_rope():
+    """qkv GEMV with the RoPE + paged-KV-write epilogue vs the same GEMV with a plain bf16
+    epilogue (both with the fused RMSNorm prologue), cold weights: what the epilogue costs."""
+    from llm_consensus_amd.ops import oracle
+
+    for (nh, nkv, D, H) in [(32, 8, 128, 4096), (32, 32, 96, 3072), (4, 1, 128, 4096)]:
+        N = (nh + 2 * nkv) * D
+        copies = max(2, (1 << 30) // (N * H * 2))
+        Ws = [(torch.randn(N, H, device="cuda") * 0.02).to(BF) for _ in range(copies)]
+        x = torch.randn(1, H, device="cuda").to(BF)
+        nw = torch.ones(H, dtype=BF, device="cuda")
+        bs, nb = 64, 64
+        kc = torch.zeros(nb, nkv, bs, D, dtype=BF, device="cuda")
+        vc = torch.zeros_like(kc)
+        cos_t, sin_t = oracle.rope_tables([1.0 / (10000 ** (2 * i / D)) for i in range(D // 2)], 4096)
+        cos_t, sin_t = cos_t.cuda(), sin_t.cuda()
+        pos = torch.tensor([1000], dtype=torch.int32, device="cuda")
+        slots = torch.tensor([1000], dtype=torch.int32, device="cuda")
+        q = torch.zeros(1, nh * D, dtype=BF, device="cuda")
+        out = torch.zeros(1, N, dtype=BF, device="cuda")
+
+        def rope():
+            for W in Ws:
+                ops.qkv_rope(x, W, nw, 1e-5, q, kc, vc, pos, slots, cos_t, sin_t, nh, nkv, D, bs)
+
+        def plain():
+            for W in Ws:
+                ops.gemv(x, W, 0, out=out, norm_w=nw)
+        tr = timeit(rope, iters=2, warm=1) / copies
+        tp = timeit(plain, iters=2, warm=1) / copies
+        print(f"qkv nh={nh} nkv={nkv} D={D} H={H} (N={N}): rope+kv epilogue {tr:6.2f} us, plain {tp:6.2f} us",
+              flush=True)
+
+
+def bench_launch():
+    x = torch.zeros(1, 4096, dtype=BF, device="cuda")
+    w = torch.ones(4096, dtype=BF, device="cuda")
+    us = timeit(lambda: ops.rmsnorm(x, w, 1e-5, out=x))
+    print(f"rmsnorm [1,4096] (launch-bound floor): {us:.2f} us")
+
+
+def bench_prefill():
     """Prefill GEMM (ours vs torch.matmul = hipBLASLt) and flash prefill attention throughput."""
     for (M, N, K) in [(8192, 28672, 4096), (8192, 6144, 4096), (8192, 4096, 4096), (8192, 4096, 14336),
                       (13463, 28672, 4096), (2048, 6144, 4096)]:
@@ -109,8 +185,9 @@ ALL_def bench_prefill():
         t_ours = timeit(lambda: ops.gemm(x, W, 0, out=out), iters=10)
         t_ref = timeit(lambda: torch.matmul(x, W.t(), out=out), iters=10)  # hipBLASLt: reference only
         fl = 2 * M * N * K
-        print(f"gemm M={M} N={N} K={K}: ours {t_ours:8.1f} us {fl / t_ours / 1e6:6.0f} TF/s | torch {t_ref:8.1f} us "
-              f"{fl / t_ref / 1e6:6.0f} TF/s", flush=True)
+        line = (f"gemm M={M} N={N} K={K}: ours {t_ours:8.1f} us {fl / t_ours / 1e6:6.0f} TF/s | torch {t_ref:8.1f} us "
+                f"{fl / t_ref / 1e6:6.0f} TF/s")
+        print(line, flush=True)
     nh, nkv, D, bs = 32, 8, 128, 64
     for (T, ctx) in [(2048, 2048), (8192, 8192), (8192, 32768)]:
         nb = (ctx + bs - 1) // bs + 1

@@ -53,3 +53,12 @@ def test_config_too_big_is_skipped_not_shrunk():
     for cfg in ("4", "5"):
         d = _run(1, ["--config", cfg, "--steps", "1", "--warmup", "0"], 0)
         assert d["value"] is None and "needs" in d["skipped"]
+
+
+def test_fanout_eight_ranks_like_the_scale_run():
+    """The driver's N=8 scaling run, rehearsed on 8 gloo ranks: one responder per rank, the judge
+    tensor-parallel over the first ranks its head count allows, value = whole-job tokens/s."""
+    d = _run(8, ["--shapes", "tiny", "--steps", "1", "--warmup", "0", "--max-tokens", "12"], 29693)
+    assert d["n_gpus"] == 8 and d["config"]["global_batch"] == 8 and d["scaling"] == "weak"
+    assert d["extra"]["judge_tp"] >= 2
+    _tokens_ok(d, 12)

@@ -117,3 +117,14 @@ def test_attn_buckets_cover_context():
     assert attn_buckets(131082, 32)[-1] == (131082, 128, 32, False)
     assert [b[3] for b in attn_buckets(4106)] == [True, True, True, False]
     assert all(not b[3] for b in attn_buckets(4106, fused_max=0))
+    # without GQA (Phi-3) buckets above 1k keys use 256-key chunks
+    assert [b[1] for b in attn_buckets(4106, group=1) if b[3]] == [128, 256, 256]
+
+
+def test_split_blocks_per_head():
+    from llm_consensus_amd.engine.engine import split_blocks_per_head
+
+    assert split_blocks_per_head(32, 8) == 32   # Llama-3-8B: 256 8-wave blocks per row
+    assert split_blocks_per_head(32, 32) == 16  # Phi-3: 512 4-wave blocks
+    assert split_blocks_per_head(4, 1) == 64    # a TP=8 rank: capped at 64 partials
+    assert split_blocks_per_head(16, 2) == 32   # a 70B TP=4 rank (G = 8): chunks x G <= 256

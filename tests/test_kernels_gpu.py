@@ -167,8 +167,8 @@ def _paged_kv(B, L_max, nkv, D, bs):
 @pytest.mark.parametrize("chunk", [128, 256])
 def test_attn_decode_fused(cuda, nh, nkv, D, lens, chunk):
     """Short-context form: fixed 128/256-key chunks (a 4096-key bucket = 32/16 blocks per kv head),
-    merged in-launch by the last-arriving block (write-through partials); the tickets must be
-    re-armed after every launch."""
+    merged in the same launch by the last-arriving block from tagged granules; the ticket must be
+    re-armed and the epoch of every (row, kv head) that merged advanced once per launch."""
     torch.manual_seed(3)
     B, bs = len(lens), 64
     kc, vc, bt = _paged_kv(B, max(lens), nkv, D, bs)
@@ -184,25 +184,30 @@ def test_attn_decode_fused(cuda, nh, nkv, D, lens, chunk):
         ops.attn_decode(q, kc, vc, bt.cuda(), sl.cuda(), out, part, ctr, nh, nkv, D, bs, chunk, scale, grid_chunks=gc,
                         fused=True)
         close(out, ref, 2e-2)
-    assert int(ctr.abs().sum()) == 0
+    # tickets re-armed, epochs advanced once per launch where a merge ran
+    epochs = torch.tensor([3 if n > chunk else 0 for n in lens], dtype=torch.int32).view(-1, 1).expand(B, nkv)
+    assert int(ctr[..., 0].abs().sum()) == 0 and torch.equal(ctr[..., 1].cpu(), epochs), ctr
 
 
 @pytest.mark.parametrize("nh,nkv,D", [(32, 8, 128), (32, 32, 96), (16, 2, 128)])
 @pytest.mark.parametrize("gc", [1, 3, 7, 64])
 def test_attn_decode_balanced_split(cuda, nh, nkv, D, gc):
-    """Long-context form with a fixed grid: each sequence's keys spread evenly over gc blocks (>= 128
-    keys each) + the reduce launch."""
+    """Long-context form with a fixed grid: each sequence's keys spread evenly over gc 8-wave blocks
+    (>= 128 keys each), merged in the same launch. The lengths change between launches on the same
+    workspace (a row's chunk count shrinks and grows back), so a granule left by an earlier launch
+    must never be taken for this one's."""
     torch.manual_seed(5)
-    lens, bs = [5000, 130, 1], 64
-    B = len(lens)
-    kc, vc, bt = _paged_kv(B, max(lens), nkv, D, bs)
+    bs = 64
+    rounds = [[5000, 130, 1], [5000, 130, 1], [300, 4999, 2], [4097, 3000, 700], [5000, 130, 1]]
+    B = 3
+    kc, vc, bt = _paged_kv(B, 5000, nkv, D, bs)
     q = rnd(B, nh * D)
-    sl = torch.tensor(lens, dtype=torch.int32)
     part, ctr = ops.decode_attn_workspace(B, nh, nkv, D, gc, "cuda")
     out = torch.empty(B, nh * D, dtype=BF, device="cuda")
     scale = 1 / math.sqrt(D)
-    ref = oracle.attn_decode(q.cpu(), kc.cpu(), vc.cpu(), bt, sl, nh, nkv, D, bs, scale)
-    for _ in range(2):
+    for lens in rounds:
+        sl = torch.tensor(lens, dtype=torch.int32)
+        ref = oracle.attn_decode(q.cpu(), kc.cpu(), vc.cpu(), bt, sl, nh, nkv, D, bs, scale)
         out.zero_()
         ops.attn_decode(q, kc, vc, bt.cuda(), sl.cuda(), out, part, ctr, nh, nkv, D, bs, 128, scale, grid_chunks=gc)
         close(out, ref, 2e-2)
@@ -211,8 +216,8 @@ def test_attn_decode_balanced_split(cuda, nh, nkv, D, gc):
 @pytest.mark.parametrize("gc", [100, 256, 300])
 def test_attn_decode_wide_split(cuda, gc):
     """A TP=8 rank of Llama-3-8B (4 query heads, ONE kv head) at a judge-length context: the keys
-    spread over up to 300 blocks, so the reduce kernel runs its 32- and 16-dim block forms (one
-    round trip for <= 128 / 256 chunks) and, past 256 chunks, a second batch."""
+    spread over up to 300 blocks, so the last arriver folds the granules of many chunk groups in
+    batches of 8 per thread."""
     torch.manual_seed(6)
     nh, nkv, D, bs = 4, 1, 128, 64
     lens = [40000, 9000, 130]

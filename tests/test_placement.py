@@ -49,7 +49,7 @@ def test_config5_mixed_fleet_with_70b_tp4_judge():
 
 
 def test_memory_is_checked_per_gpu():
-    # 70B unsharded (141 GB) + 120 GB of KV does not fit one 288 GB GPU's usable 92 %
+    # 70B unsharded (141 GB) + 130 GB of KV = 271 GB does not fit one 288 GB GPU's usable 92 % (265 GB)
     with pytest.raises(PlacementError, match="no GPU has that free"):
         solve([ModelDemand("llama-3-70b", W70B, 130 * G)], [0])
     # fits once it is TP=2 (135.5 GB per GPU)

@@ -264,43 +264,42 @@ __device__ __forceinline__ void publish_partial(const float* red, __amdgpu_buffe
   }
 }
 
-// The last-arriving chunk block merges all nchunks partials: thread = (output quad, chunk group),
-// up to 8 chunks' {O quad, lambda} loads in flight per thread, re-polled until every tag matches
-// (a straggler is a store already issued by a block that has arrived: no wait on any block that
-// is not running), folded with an online log-sum-exp; chunk groups meet in LDS.
+// Merge the partial rows [r0, r0 + n) of a granule slab: thread = (output quad, row group), up to 8
+// rows' {O quad, lambda} loads in flight per thread, re-polled until every tag matches (a
+// straggler is a store already issued by a block that has arrived: no wait on any block that is
+// not running), folded with an online log-sum-exp; row groups meet in LDS. On return threads
+// tid < G * D / 4 hold their quad's (M, S) in ms[0..1] and the unnormalised sums in acc.
 template <int G, int D, int NT>
-__device__ __forceinline__ void merge_all(float* slab, int max_chunks, int nchunks, uint32_t tag, bf16_t* out_row,
-                                          f32x4* scratch, int tid) {
+__device__ __forceinline__ void merge_rows(__amdgpu_buffer_rsrc_t rsrc, const char* base, int r0, int n, uint32_t tag,
+                                           f32x4* scratch, int tid, f32x4& ms, f32x4& acc) {
   constexpr int HQ = D / 4, RU = HQ + 1, Q = G * HQ;
   static_assert(Q <= NT, "one pass");
-  const __amdgpu_buffer_rsrc_t rsrc = __builtin_amdgcn_make_buffer_rsrc(slab, 0, max_chunks * G * RU * 16, 0x00020000);
-  const char* base = reinterpret_cast<const char*>(slab);
-  const int ngr = max(1, min(NT / Q, nchunks));
+  const int ngr = max(1, min(NT / Q, n));
   const int gr = tid / Q;
   float M = kNegInfM, S = 0.f, a[4] = {0.f, 0.f, 0.f, 0.f};
   if (gr < ngr) {
     const int g = (tid % Q) / HQ, u = (tid % Q) % HQ;
-    for (int c0 = gr; c0 < nchunks; c0 += 8 * ngr) {
+    for (int c0 = gr; c0 < n; c0 += 8 * ngr) {
       u32x4 ov[8];
       u32x2 lv[8];
       for (unsigned spins = 0;; ++spins) {
         bool ok = true;
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
-          const int cc = min(c0 + j * ngr, nchunks - 1);  // clamped: every load in flight, masked below
+          const int cc = r0 + min(c0 + j * ngr, n - 1);  // clamped: every load in flight, masked below
           const int row = (cc * G + g) * RU;
           ov[j] = ld16_sc1(rsrc, (row + u) * 16);
           lv[j] = ld8_atomic(base, (row + HQ) * 16);
         }
 #pragma unroll
         for (int j = 0; j < 8; ++j)
-          if (c0 + j * ngr < nchunks) ok = ok && ov[j][1] == tag && ov[j][3] == tag && lv[j][1] == tag;
+          if (c0 + j * ngr < n) ok = ok && ov[j][1] == tag && ov[j][3] == tag && lv[j][1] == tag;
         if (__all(ok) || spins >= kSpinLimit) break;
         __builtin_amdgcn_s_sleep(2);
       }
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
-        if (c0 + j * ngr < nchunks) {
+        if (c0 + j * ngr < n) {
           const float lam = __uint_as_float(lv[j][0]);
           const float mn = fmaxf(M, lam);
           const float so = exp2f(M - mn), sn = exp2f(lam - mn);
@@ -318,7 +317,8 @@ __device__ __forceinline__ void merge_all(float* slab, int max_chunks, int nchun
   scratch[2 * tid + 1] = f32x4{a[0], a[1], a[2], a[3]};
   __syncthreads();
   if (tid < Q) {
-    f32x4 ms = scratch[2 * tid], acc = scratch[2 * tid + 1];
+    ms = scratch[2 * tid];
+    acc = scratch[2 * tid + 1];
     for (int k = 1; k < ngr; ++k) {
       const f32x4 ms2 = scratch[2 * (tid + k * Q)], acc2 = scratch[2 * (tid + k * Q) + 1];
       const float mn = fmaxf(ms[0], ms2[0]);
@@ -326,31 +326,67 @@ __device__ __forceinline__ void merge_all(float* slab, int max_chunks, int nchun
       ms = f32x4{mn, ms[1] * so + ms2[1] * sn, 0.f, 0.f};
       acc = acc * so + acc2 * sn;
     }
+  }
+  __syncthreads();  // scratch is reused by the caller's next merge
+}
+
+// Publish this chunk's partial and take a ticket in its GROUP of `gsize` consecutive chunks; the
+// group's last arriver merges the group. With one group that is the output; otherwise the group
+// result is published as one more granule row (slab row max_chunks + group) and the last group
+// merger merges those (two levels: a 256-block split merges 16 rows twice instead of 256 rows in
+// one block). The last merger re-arms the tickets it took and advances the epoch (every block of
+// this launch read the epoch before it arrived). ctr = {top ticket, epoch, group tickets...};
+// `flag` is one LDS word. Every block but the last returns inside.
+template <int G, int D, int NW>
+__device__ __forceinline__ void publish_and_merge(const float* red, float* part, int* ctr, int b, int nkv, int kvh,
+                                                  int c, int nchunks, int gsize, int max_chunks, int max_groups,
+                                                  uint32_t tag, bf16_t* out_row, char* smem, int* flag, int tid) {
+  constexpr int HQ = D / 4, RU = HQ + 1, Q = G * HQ;
+  const int rows = max_chunks + max_groups;
+  float* slab = part + (static_cast<int64_t>(b) * nkv + kvh) * rows * G * RU * 4;
+  const __amdgpu_buffer_rsrc_t rsrc = __builtin_amdgcn_make_buffer_rsrc(slab, 0, rows * G * RU * 16, 0x00020000);
+  const char* base = reinterpret_cast<const char*>(slab);
+  f32x4* scratch = reinterpret_cast<f32x4*>(smem);
+  publish_partial<G, D, NW>(red, rsrc, c, tag, tid);
+  const int grp = c / gsize, ngroups = (nchunks + gsize - 1) / gsize;
+  const int g0 = grp * gsize, gn = min(gsize, nchunks - g0);
+  int* gctr = ngroups == 1 ? ctr : ctr + 2 + grp;
+  __syncthreads();  // every wave's stores are issued (not drained: the merger checks tags)
+  if (tid == 0) *flag = __hip_atomic_fetch_add(gctr, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == gn - 1;
+  __syncthreads();
+  if (*flag == 0) return;
+  f32x4 ms, acc;
+  merge_rows<G, D, NW * 64>(rsrc, base, g0, gn, tag, scratch, tid, ms, acc);
+  if (ngroups > 1) {
+    // publish the group result as a granule row, then the top-level ticket
+    if (tid < Q) {
+      const int g = tid / HQ, u = tid % HQ;
+      const float inv = 1.f / ms[1];
+      const int row = ((max_chunks + grp) * G + g) * RU;
+      st16_sc1(rsrc, (row + u) * 16,
+               u32x4{pack_bf16x2(acc[0] * inv, acc[1] * inv), tag, pack_bf16x2(acc[2] * inv, acc[3] * inv), tag});
+      if (u == 0) {
+        const uint32_t lam = __float_as_uint(ms[0] + __log2f(ms[1]));
+        st16_sc1(rsrc, (row + HQ) * 16, u32x4{lam, tag, lam, tag});
+      }
+    }
+    __syncthreads();
+    if (tid == 0) {
+      __hip_atomic_store(gctr, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // re-arm the group ticket
+      *flag = __hip_atomic_fetch_add(ctr, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == ngroups - 1;
+    }
+    __syncthreads();
+    if (*flag == 0) return;
+    merge_rows<G, D, NW * 64>(rsrc, base, max_chunks, ngroups, tag, scratch, tid, ms, acc);
+  }
+  if (tid < Q) {
     const int g = tid / HQ, u = tid % HQ;
     const float inv = 1.f / ms[1];
     *reinterpret_cast<u32x2*>(out_row + g * D + 4 * u) =
         u32x2{pack_bf16x2(acc[0] * inv, acc[1] * inv), pack_bf16x2(acc[2] * inv, acc[3] * inv)};
   }
-}
-
-// Publish this chunk's partial, take a ticket; the last arriver merges, then re-arms the ticket and
-// advances the epoch (every block of this launch read the epoch before it arrived). `flag` is one
-// LDS word. Returns nothing: every block but the last exits inside.
-template <int G, int D, int NW>
-__device__ __forceinline__ void publish_and_merge(const float* red, float* part, int* ctr, int b, int nkv, int kvh,
-                                                  int c, int nchunks, int max_chunks, uint32_t tag, bf16_t* out_row,
-                                                  char* smem, int* flag, int tid) {
-  constexpr int RU = D / 4 + 1;
-  float* slab = part + (static_cast<int64_t>(b) * nkv + kvh) * max_chunks * G * RU * 4;
-  publish_partial<G, D, NW>(red, __builtin_amdgcn_make_buffer_rsrc(slab, 0, max_chunks * G * RU * 16, 0x00020000), c,
-                            tag, tid);
-  __syncthreads();  // every wave's stores are issued (not drained: the merger checks tags)
-  if (tid == 0) *flag = __hip_atomic_fetch_add(ctr, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == nchunks - 1;
-  __syncthreads();
-  if (*flag == 0) return;
-  merge_all<G, D, NW * 64>(slab, max_chunks, nchunks, tag, out_row, reinterpret_cast<f32x4*>(smem), tid);
   if (tid == 0) {
-    __hip_atomic_store(ctr, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);                     // re-arm
+    __hip_atomic_store(ctr, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);                          // re-arm
     __hip_atomic_store(ctr + 1, static_cast<int>(tag), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // epoch
   }
 }
@@ -361,12 +397,13 @@ __global__ __launch_bounds__(NW * 64) void attn_decode_split_kernel(
     const bf16_t* __restrict__ q, int q_stride, const bf16_t* __restrict__ k_cache,
     const bf16_t* __restrict__ v_cache, const int32_t* __restrict__ block_tables, int bt_stride,
     const int32_t* __restrict__ seq_lens, float* __restrict__ part, int* __restrict__ counters, bf16_t* __restrict__ out,
-    int out_stride, int nkv, int bs, int nblocks, int min_chunk, int max_chunks, float scale_log2) {
+    int out_stride, int nkv, int bs, int nblocks, int min_chunk, int max_chunks, int gsize, int max_groups,
+    float scale_log2) {
   static_assert(G <= 16 && D % 32 == 0 && D <= 128, "shape");
   using ST = SubTile<G, D>;
   constexpr int NT = NW * 64;
   const int c = blockIdx.x, kvh = blockIdx.y, b = blockIdx.z;
-  int* ctr = counters + 2 * (b * nkv + kvh);  // {ticket, epoch}
+  int* ctr = counters + (b * nkv + kvh) * (2 + max_groups);  // {ticket, epoch, group tickets}
   const uint32_t tag = static_cast<uint32_t>(__hip_atomic_load(ctr + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) + 1u;
   const int L = seq_lens[b];
   const int nchunks = decode_nsplit(L, gridDim.x, -min_chunk);
@@ -418,7 +455,7 @@ __global__ __launch_bounds__(NW * 64) void attn_decode_split_kernel(
     store_direct<G, D, NW>(red, out_row, tid);
     return;
   }
-  publish_and_merge<G, D, NW>(red, part, ctr, b, nkv, kvh, c, nchunks, max_chunks, tag, out_row, smem,
+  publish_and_merge<G, D, NW>(red, part, ctr, b, nkv, kvh, c, nchunks, gsize, max_chunks, max_groups, tag, out_row, smem,
                               reinterpret_cast<int*>(pages), tid);
 }
 
@@ -428,8 +465,8 @@ __global__ __launch_bounds__(256) void attn_decode_fused_kernel(
     const bf16_t* __restrict__ q, int q_stride, const bf16_t* __restrict__ k_cache,
     const bf16_t* __restrict__ v_cache, const int32_t* __restrict__ block_tables, int bt_stride,
     const int32_t* __restrict__ seq_lens, float* __restrict__ part, int* __restrict__ counters,
-    bf16_t* __restrict__ out, int out_stride, int nkv, int bs, int nblocks, int chunk, int max_chunks,
-    float scale_log2) {
+    bf16_t* __restrict__ out, int out_stride, int nkv, int bs, int nblocks, int chunk, int max_chunks, int gsize,
+    int max_groups, float scale_log2) {
   static_assert(G <= 16 && D % 32 == 0 && D <= 128, "shape");
   using ST = SubTile<G, D>;
   const int c = blockIdx.x, kvh = blockIdx.y, b = blockIdx.z;
@@ -442,7 +479,7 @@ __global__ __launch_bounds__(256) void attn_decode_fused_kernel(
   const int pidx = __builtin_amdgcn_readfirstlane(min(key0 / bs, bt_stride - 1));
   const int page = min(max(ld_scalar(bt + pidx), 0), nblocks - 1);  // clamped into the cache
   const int L = ld_scalar(seq_lens + b);
-  int* ctr = counters + 2 * (b * nkv + kvh);  // {ticket, epoch}
+  int* ctr = counters + (b * nkv + kvh) * (2 + max_groups);  // {ticket, epoch, group tickets}
   const uint32_t tag = static_cast<uint32_t>(__hip_atomic_load(ctr + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) + 1u;
   ST st;
   st.init(q + static_cast<int64_t>(b) * q_stride + kvh * G * D, lane);
@@ -470,27 +507,21 @@ __global__ __launch_bounds__(256) void attn_decode_fused_kernel(
     store_direct<G, D, 4>(red, out_row, tid);
     return;
   }
-  publish_and_merge<G, D, 4>(red, part, ctr, b, nkv, kvh, c, nchunks, max_chunks, tag, out_row, smem,
+  publish_and_merge<G, D, 4>(red, part, ctr, b, nkv, kvh, c, nchunks, gsize, max_chunks, max_groups, tag, out_row, smem,
                              reinterpret_cast<int*>(red + 4 * G * (D + 2)), tid);
 }
 
-// Waves per split block: 8 with GQA; 4 without (G = 1: one head per kv head, Phi-3's 32 kv heads
+// Split blocks: 8 waves when a block's balanced range at the table's full length is >= 512 keys
+// (2 x 16 KB of K/V in flight per wave), 4 otherwise (wide TP grids: a TP=8 rank's one kv head
+// over 256 blocks has ~130 keys per block) and always without GQA (G = 1: Phi-3's 32 kv heads
 // already give 512 blocks, and 8-wave blocks at 212 VGPRs would halve the blocks resident per CU).
-template <int G>
-constexpr int split_waves() { return G == 1 ? 4 : 8; }
-
-template <int G, int D>
-static int launch_split(dim3 grid, hipStream_t s, const void* q, int q_stride, const void* kc, const void* vc,
-                        const void* bt, int bt_stride, const void* sl, void* part, void* ctr, void* out, int out_stride,
-                        int nkv, int bs, int nblocks, int chunk, int max_chunks, float scale) {
-  constexpr int NW = split_waves<G>();
-  // page-id staging sized for the largest balanced range any sequence of this table can get
-  const int grid_chunks = static_cast<int>(grid.x);
-  const int units = (bt_stride * bs + 31) / 32;
-  const int bal = 32 * ((units + grid_chunks - 1) / grid_chunks) + 32;
-  const int max_chunk = bal > 2 * chunk ? bal : 2 * chunk;
+template <int G, int D, int NW>
+static int launch_split_nw(dim3 grid, hipStream_t s, const void* q, int q_stride, const void* kc, const void* vc,
+                           const void* bt, int bt_stride, const void* sl, void* part, void* ctr, void* out,
+                           int out_stride, int nkv, int bs, int nblocks, int chunk, int max_chunks, int gsize,
+                           int max_groups, int max_chunk_keys, float scale) {
   const size_t lds = NW * 32 * kVRowBytes + static_cast<size_t>(NW) * G * (D + 2) * sizeof(float) +
-                     static_cast<size_t>((max_chunk + bs - 1) / bs + 2) * sizeof(int);
+                     static_cast<size_t>((max_chunk_keys + bs - 1) / bs + 2) * sizeof(int);
   if (lds > 160 * 1024) return -4;
   auto kern = attn_decode_split_kernel<G, D, NW>;
   static bool attr_set = false;
@@ -501,34 +532,53 @@ static int launch_split(dim3 grid, hipStream_t s, const void* q, int q_stride, c
   }
   kern<<<grid, NW * 64, lds, s>>>((const bf16_t*)q, q_stride, (const bf16_t*)kc, (const bf16_t*)vc,
                                   (const int32_t*)bt, bt_stride, (const int32_t*)sl, (float*)part, (int*)ctr,
-                                  (bf16_t*)out, out_stride, nkv, bs, nblocks, chunk, max_chunks,
+                                  (bf16_t*)out, out_stride, nkv, bs, nblocks, chunk, max_chunks, gsize, max_groups,
                                   scale * 1.4426950408889634f);
   return static_cast<int>(hipGetLastError());
 }
 
 template <int G, int D>
+static int launch_split(dim3 grid, hipStream_t s, const void* q, int q_stride, const void* kc, const void* vc,
+                        const void* bt, int bt_stride, const void* sl, void* part, void* ctr, void* out, int out_stride,
+                        int nkv, int bs, int nblocks, int chunk, int max_chunks, int gsize, int max_groups,
+                        float scale) {
+  // page-id staging sized for the largest balanced range any sequence of this table can get
+  const int grid_chunks = static_cast<int>(grid.x);
+  const int units = (bt_stride * bs + 31) / 32;
+  const int bal = 32 * ((units + grid_chunks - 1) / grid_chunks) + 32;
+  const int max_chunk = bal > 2 * chunk ? bal : 2 * chunk;
+  if (G > 1 && bal >= 512)
+    return launch_split_nw<G, D, 8>(grid, s, q, q_stride, kc, vc, bt, bt_stride, sl, part, ctr, out, out_stride, nkv,
+                                    bs, nblocks, chunk, max_chunks, gsize, max_groups, max_chunk, scale);
+  return launch_split_nw<G, D, 4>(grid, s, q, q_stride, kc, vc, bt, bt_stride, sl, part, ctr, out, out_stride, nkv, bs,
+                                  nblocks, chunk, max_chunks, gsize, max_groups, max_chunk, scale);
+}
+
+template <int G, int D>
 static int launch_fused(dim3 grid, hipStream_t s, const void* q, int q_stride, const void* kc, const void* vc,
                         const void* bt, int bt_stride, const void* sl, void* part, void* ctr, void* out, int out_stride,
-                        int nkv, int bs, int nblocks, int chunk, int max_chunks, float scale) {
+                        int nkv, int bs, int nblocks, int chunk, int max_chunks, int gsize, int max_groups,
+                        float scale) {
   const size_t lds = 4 * 32 * kVRowBytes + static_cast<size_t>(4) * G * (D + 2) * sizeof(float) + 16;  // + flag
   if (lds > 64 * 1024) return -4;
   attn_decode_fused_kernel<G, D><<<grid, 256, lds, s>>>(
       (const bf16_t*)q, q_stride, (const bf16_t*)kc, (const bf16_t*)vc, (const int32_t*)bt, bt_stride,
-      (const int32_t*)sl, (float*)part, (int*)ctr, (bf16_t*)out, out_stride, nkv, bs, nblocks, chunk, max_chunks,
-      scale * 1.4426950408889634f);
+      (const int32_t*)sl, (float*)part, (int*)ctr, (bf16_t*)out, out_stride, nkv, bs, nblocks, chunk, max_chunks, gsize,
+      max_groups, scale * 1.4426950408889634f);
   return static_cast<int>(hipGetLastError());
 }
 
 template <int G>
 static int launch_g(bool fused, int D, dim3 grid, hipStream_t s, const void* q, int q_stride, const void* kc,
                     const void* vc, const void* bt, int bt_stride, const void* sl, void* part, void* ctr, void* out,
-                    int out_stride, int nkv, int bs, int nblocks, int chunk, int max_chunks, float scale) {
+                    int out_stride, int nkv, int bs, int nblocks, int chunk, int max_chunks, int gsize,
+                    int max_groups, float scale) {
 #define LLMC_ATTN_D(DD)                                                                                          \
   case DD:                                                                                                       \
     return fused ? launch_fused<G, DD>(grid, s, q, q_stride, kc, vc, bt, bt_stride, sl, part, ctr, out, out_stride, \
-                                       nkv, bs, nblocks, chunk, max_chunks, scale)                               \
+                                       nkv, bs, nblocks, chunk, max_chunks, gsize, max_groups, scale)            \
                  : launch_split<G, DD>(grid, s, q, q_stride, kc, vc, bt, bt_stride, sl, part, ctr, out, out_stride, \
-                                       nkv, bs, nblocks, chunk, max_chunks, scale);
+                                       nkv, bs, nblocks, chunk, max_chunks, gsize, max_groups, scale);
   switch (D) {
     LLMC_ATTN_D(64)
     LLMC_ATTN_D(96)
@@ -543,10 +593,18 @@ static int launch_g(bool fused, int D, dim3 grid, hipStream_t s, const void* q, 
 using namespace llmc;
 
 // Attention of one decode step for rows 0..B-1, one launch.
-// part: f32 [B, nkv, max_chunks, G, D + 4] partial granules (zeroed once); counters: int32
-// [B, nkv, 2] {ticket, epoch} (zeroed once; the kernel re-arms the ticket and advances the epoch).
+// part: f32 [B, nkv, max_chunks + max_groups, G, D + 4] partial granules (zeroed once); counters:
+// int32 [B, nkv, 2 + max_groups] {top ticket, epoch, group tickets} (zeroed once; the kernel re-arms
+// the tickets and advances the epoch); max_groups = attn_decode_groups(max_chunks).
 // fused = 1 (short contexts): grid_chunks fixed chunk-key blocks (chunk 128 or 256; bs % (chunk/4) == 0).
 // fused = 0 (long contexts): balanced split over <= grid_chunks blocks of >= chunk keys (multiple of 128).
+// Chunk partials are merged in one level up to kAttnOneLevel chunks, else in groups of kAttnGroup.
+constexpr int kAttnOneLevel = 32, kAttnGroup = 16;  // one-level merges of 64 rows measured 1.3-1.5x slower
+
+extern "C" int llmc_attn_decode_groups(int max_chunks) {
+  return max_chunks > kAttnOneLevel ? (max_chunks + kAttnGroup - 1) / kAttnGroup : 0;
+}
+
 extern "C" int llmc_attn_decode(const void* q, int q_stride, const void* k_cache, const void* v_cache,
                                 const void* block_tables, int bt_stride, const void* seq_lens, void* part,
                                 void* counters, void* out, int out_stride, int B, int nh, int nkv, int D, int bs,
@@ -557,14 +615,16 @@ extern "C" int llmc_attn_decode(const void* q, int q_stride, const void* k_cache
     return -1;
   if (fused ? ((chunk != 128 && chunk != 256) || bs % (chunk / 4) != 0) : (chunk % 128 != 0)) return -1;
   const int G = nh / nkv;
-  if (static_cast<int64_t>(max_chunks) * G * (D / 4 + 1) * 16 >= (1ll << 31)) return -4;
+  const int max_groups = llmc_attn_decode_groups(max_chunks);
+  const int gsize = grid_chunks > kAttnOneLevel ? kAttnGroup : grid_chunks;
+  if (static_cast<int64_t>(max_chunks + max_groups) * G * (D / 4 + 1) * 16 >= (1ll << 31)) return -4;
   dim3 grid(grid_chunks, nkv, B);
   const bool f = fused != 0;
   switch (G) {
-    case 1: return launch_g<1>(f, D, grid, s, q, q_stride, k_cache, v_cache, block_tables, bt_stride, seq_lens, part, counters, out, out_stride, nkv, bs, nblocks, chunk, max_chunks, scale);
-    case 2: return launch_g<2>(f, D, grid, s, q, q_stride, k_cache, v_cache, block_tables, bt_stride, seq_lens, part, counters, out, out_stride, nkv, bs, nblocks, chunk, max_chunks, scale);
-    case 4: return launch_g<4>(f, D, grid, s, q, q_stride, k_cache, v_cache, block_tables, bt_stride, seq_lens, part, counters, out, out_stride, nkv, bs, nblocks, chunk, max_chunks, scale);
-    case 8: return launch_g<8>(f, D, grid, s, q, q_stride, k_cache, v_cache, block_tables, bt_stride, seq_lens, part, counters, out, out_stride, nkv, bs, nblocks, chunk, max_chunks, scale);
+    case 1: return launch_g<1>(f, D, grid, s, q, q_stride, k_cache, v_cache, block_tables, bt_stride, seq_lens, part, counters, out, out_stride, nkv, bs, nblocks, chunk, max_chunks, gsize, max_groups, scale);
+    case 2: return launch_g<2>(f, D, grid, s, q, q_stride, k_cache, v_cache, block_tables, bt_stride, seq_lens, part, counters, out, out_stride, nkv, bs, nblocks, chunk, max_chunks, gsize, max_groups, scale);
+    case 4: return launch_g<4>(f, D, grid, s, q, q_stride, k_cache, v_cache, block_tables, bt_stride, seq_lens, part, counters, out, out_stride, nkv, bs, nblocks, chunk, max_chunks, gsize, max_groups, scale);
+    case 8: return launch_g<8>(f, D, grid, s, q, q_stride, k_cache, v_cache, block_tables, bt_stride, seq_lens, part, counters, out, out_stride, nkv, bs, nblocks, chunk, max_chunks, gsize, max_groups, scale);
     default: return -3;
   }
 }

@@ -24,6 +24,7 @@ int llmc_gemv(int, const void*, int, const void*, float, const void*, void*, int
 int llmc_gemm(const void*, int, const void*, int, void*, int, int, int, int, int, hipStream_t);
 int llmc_rope_kv_write(const void*, int, void*, int, const void*, const void*, const void*, void*, void*, const void*,
                        int, int, int, int, int, hipStream_t);
+int llmc_attn_decode_groups(int);
 int llmc_attn_decode(const void*, int, const void*, const void*, const void*, int, const void*, void*, void*, void*,
                      int, int, int, int, int, int, int, int, int, int, float, int, hipStream_t);
 int llmc_gemv_qkv_rope(int, const void*, int, const void*, float, const void*, int, int, void*, int, void*, void*,
@@ -97,6 +98,7 @@ PYBIND11_MODULE(_llmc_hip, m) {
                              bs, S(s)),
           "rope_kv_write");
   });
+  m.def("attn_decode_groups", [](int max_chunks) { return llmc_attn_decode_groups(max_chunks); });
   m.def("attn_decode", [](ptr q, int qs, ptr kc, ptr vc, ptr bt, int bts, ptr sl, ptr part, ptr ctr, ptr out, int os,
                           int B, int nh, int nkv, int D, int bs, int nblocks, int chunk, int grid_chunks,
                           int max_chunks, float scale, int fused, ptr s) {

@@ -61,24 +61,31 @@ class EngineConfig:
 FUSED_CHUNK_SMALL, FUSED_CHUNK_LARGE = 128, 256
 
 
-def attn_buckets(ctxmax: int, blocks_per_head: int = 64, fused_max: int = 4096, group: int = 4) -> List[tuple]:
+def attn_buckets(ctxmax: int, blocks_per_head: int = 32, fused_max: int = 4096, group: int = 4,
+                 nkv: int = 8) -> List[tuple]:
     """Decode-attention shapes per context bucket: [(capacity_tokens, chunk, grid_chunks, fused)].
 
-    Capacities double from 1024. Buckets up to ``fused_max`` keys use the fused form (fixed-chunk
-    blocks, grid_chunks = capacity / chunk): 128-key chunks up to 2048 keys with GQA (``group``
-    query heads per kv head >= 2; 8.8 vs 9.9 us at 2k) and up to 1024 without (Phi-3), 256-key
-    chunks above (10.9 vs 11.9 us at 4k; Phi-3 14.5 vs 23.3: 32 kv heads already fill the chip;
-    profiles/r2_attn_decode.md). Longer ones use the
-    balanced split: ``chunk`` is the minimum of 128 keys per block, the kernel spreads a
-    sequence's keys evenly over ``grid_chunks`` blocks, and the grid grows with the context until
-    ``blocks_per_head`` (~1 block per CU over the kv heads of one row, measured on MI355X:
-    profiles/r1_attn_decode_microbench.md); one bucket then covers every longer context."""
+    Capacities double from 1024. A bucket uses the fused form (fixed-chunk blocks over the bucket
+    capacity, grid_chunks = capacity / chunk; no length-dependent page-table round trip) up to
+    ``fused_max`` keys — 128-key chunks up to 2048 keys with GQA (``group`` query heads per kv
+    head >= 2) and up to 1024 without (Phi-3), 256-key chunks above — and, beyond it, while the
+    grid stays within ~one block per CU: 128-key chunks if capacity / 128 x ``nkv`` <= 256, else
+    256-key chunks if capacity / 256 x ``nkv`` <= 256 (TP ranks, whose one or two kv heads leave
+    the chip idle under a per-head split). Otherwise the balanced split: ``chunk`` is the minimum
+    of 128 keys per block, the kernel spreads a sequence's keys evenly over ``grid_chunks`` blocks,
+    and the grid grows with the context until ``blocks_per_head``; one bucket then covers every
+    longer context. Measured per shape: profiles/r2_attn_decode.md. ``fused_max`` = 0 disables
+    the fused form (page size not a multiple of 32 keys)."""
     out, cap = [], 1024
     while True:
         c = min(cap, ctxmax)
-        if c <= fused_max:
+        if fused_max > 0 and c <= fused_max:
             ch = FUSED_CHUNK_SMALL if c <= (2048 if group >= 2 else 1024) else FUSED_CHUNK_LARGE
             out.append((c, ch, (c + ch - 1) // ch, True))
+        elif fused_max > 0 and (c + 127) // 128 * nkv <= 256:
+            out.append((c, 128, (c + 127) // 128, True))
+        elif fused_max > 0 and (c + 255) // 256 * nkv <= 256:
+            out.append((c, 256, (c + 255) // 256, True))
         else:
             gc = min((c + 127) // 128, blocks_per_head)
             if out and not out[-1][3] and out[-1][2] == gc:
@@ -91,13 +98,11 @@ def attn_buckets(ctxmax: int, blocks_per_head: int = 64, fused_max: int = 4096, 
 
 
 def split_blocks_per_head(nh: int, nkv: int) -> int:
-    """Grid of the split (long-context) attention form per kv head: ~1 8-wave block per CU over the
-    row's kv heads (256 blocks; 512 without GQA, where a block's range costs less), capped so the
-    in-launch merge reads at most ~64 partial granule rows of 4 heads per merger
-    (chunks x G <= 256) and never more than 64 partials."""
-    G = max(1, nh // nkv)
-    blocks = 512 if G == 1 else 256
-    return max(1, min(blocks // nkv, 256 // G, 64))
+    """Grid of the split (long-context) attention form per kv head: ~one block per CU over the row's
+    kv heads (256; 512 without GQA, where a block's range costs less). A TP=8 rank's single kv
+    head gets all 256 (its partials merge in two levels of 16)."""
+    blocks = 512 if nh == nkv else 256
+    return max(1, min(blocks // nkv, 256))
 
 
 @dataclasses.dataclass
@@ -201,7 +206,8 @@ class Engine:
         # split-KV decode attention: one (chunk, grid) shape per context bucket
         ctxmax = self.ecfg.max_context + self.ecfg.steps_per_graph + 2
         self.attn_buckets = attn_buckets(ctxmax, split_blocks_per_head(self.nh, self.nkv),
-                                         ops.FUSED_ATTN_MAX_KEYS if self.bs % 32 == 0 else 0, self.nh // self.nkv)
+                                         ops.FUSED_ATTN_MAX_KEYS if self.bs % 32 == 0 else 0, self.nh // self.nkv,
+                                         self.nkv)
         max_chunks = max(gc for _, _, gc, _ in self.attn_buckets)
         self.attn_part, self.attn_counters = ops.decode_attn_workspace(B, self.nh, self.nkv, self.D, max_chunks, dev)
         if self.on_gpu:

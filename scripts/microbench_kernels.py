@@ -49,10 +49,10 @@ def _attn_case(L, nh, nkv, D, bs=64, B=1):
     return kc, vc, bt, sl, q, out
 
 
-def bench_attn(shapes=((32, 8, 128), (32, 32, 96), (16, 2, 128), (8, 1, 128))):
-    """Decode attention per layer (graph-timed, random paged K/V): the fused single-launch form
-    (fixed 128-key chunks, in-launch merge; the engine's form for buckets <= 4096 keys) vs the
-    balanced split + reduce launch over its grid sizes (blocks per kv head)."""
+def bench_attn(shapes=((32, 8, 128), (32, 32, 96), (16, 2, 128), (8, 1, 128), (4, 1, 128))):
+    """Decode attention per layer (graph-timed, random paged K/V): the fused form (fixed 128/256-key
+    chunk blocks over the power-of-two bucket capacity) vs the balanced split over its grid sizes
+    (blocks per kv head); both merge in-launch."""
     for nh, nkv, D in shapes:
         for L in [128, 600, 1024, 2048, 4096, 8192, 16384, 33000]:
             kc, vc, bt, sl, q, out = _attn_case(L, nh, nkv, D)
@@ -60,17 +60,18 @@ def bench_attn(shapes=((32, 8, 128), (32, 32, 96), (16, 2, 128), (8, 1, 128))):
             gb = L * nkv * D * 2 * 2 / 1e9
             line = []
             best = 1e9
-            if L <= 16384:
-                cap = 1024
-                while cap < L:
-                    cap *= 2
-                for ch in ((128, 256) if L <= 4096 else (128,)):
-                    gc = cap // ch
-                    part, ctr = ops.decode_attn_workspace(1, nh, nkv, D, gc, "cuda", fused=True)
-                    us = timeit(lambda: ops.attn_decode(q, kc, vc, bt, sl, out, part, ctr, nh, nkv, D, 64, ch, sc,
-                                                        grid_chunks=gc, fused=True))
-                    best = min(best, us)
-                    line.append(f"fused c{ch} {us:6.2f}")
+            cap = 1024
+            while cap < L:
+                cap *= 2
+            for ch in (128, 256):
+                if (cap // ch) * nkv > 1024:  # beyond two residency rounds: not a candidate
+                    continue
+                gc = cap // ch
+                part, ctr = ops.decode_attn_workspace(1, nh, nkv, D, gc, "cuda", fused=True)
+                us = timeit(lambda: ops.attn_decode(q, kc, vc, bt, sl, out, part, ctr, nh, nkv, D, 64, ch, sc,
+                                                    grid_chunks=gc, fused=True))
+                best = min(best, us)
+                line.append(f"fused c{ch} {us:6.2f}")
             for gc in [16, 32, 64, 128, 256]:
                 gc_eff = min(gc, (L + 127) // 128)
                 if gc_eff < gc and gc > 16:
@@ -212,6 +213,8 @@ if __name__ == "__main__":
         bench_launch()
     if what in ("attn", "all"):
         bench_attn()
+    if what in ("attn-tp",):  # TP ranks' shapes only (G = 8 / 4 on one or two kv heads)
+        bench_attn(((16, 2, 128), (8, 1, 128), (4, 1, 128)))
     if what in ("gemv", "all"):
         bench_gemv()
     if what in ("sweep",):

@@ -103,28 +103,35 @@ def test_weights_param_counts():
 def test_attn_buckets_cover_context():
     from llm_consensus_amd.engine.engine import attn_buckets
 
-    for ctxmax in [100, 1024, 4106, 16394, 131082]:
-        bks = attn_buckets(ctxmax)
-        assert bks[-1][0] == ctxmax
-        for cap, chunk, gc, fused in bks:
-            if fused:  # fixed 128/256-key chunks cover the bucket, <= 16 partials to merge
-                assert cap <= 4096 and gc * chunk >= cap and gc <= 16 and chunk in (128, 256)
-            else:
-                assert chunk == 128 and cap > 4096 and 1 <= gc <= 64
-        assert [b[0] for b in bks] == sorted(b[0] for b in bks)
-        split = [b[2] for b in bks if not b[3]]
-        assert len(set(split)) == len(split)  # one graph per distinct split grid
+    for nkv, bph in [(8, 32), (2, 128), (1, 256)]:
+        for ctxmax in [100, 1024, 4106, 16394, 131082]:
+            bks = attn_buckets(ctxmax, bph, nkv=nkv)
+            assert bks[-1][0] == ctxmax
+            for cap, chunk, gc, fused in bks:
+                if fused:  # fixed 128/256-key chunks cover the bucket; beyond 4k only while <= 256 blocks
+                    assert gc * chunk >= cap and chunk in (128, 256)
+                    assert cap <= 4096 or gc * nkv <= 256
+                else:
+                    assert chunk == 128 and cap > 4096 and 1 <= gc <= bph
+            assert [b[0] for b in bks] == sorted(b[0] for b in bks)
+            split = [b[2] for b in bks if not b[3]]
+            assert len(set(split)) == len(split)  # one graph per distinct split grid
     assert attn_buckets(131082, 32)[-1] == (131082, 128, 32, False)
-    assert [b[3] for b in attn_buckets(4106)] == [True, True, True, False]
+    # Llama-3-8B (8 kv heads): fused up to 8k (256-key chunks at 4k-8k), split above
+    assert [(b[1], b[3]) for b in attn_buckets(16394)] == [(128, True), (128, True), (256, True), (256, True),
+                                                           (128, False)]
+    # a TP=8 rank (one kv head): fused up to 64k keys
+    assert all(b[3] for b in attn_buckets(65536, 256, nkv=1))
     assert all(not b[3] for b in attn_buckets(4106, fused_max=0))
-    # without GQA (Phi-3) buckets above 1k keys use 256-key chunks
-    assert [b[1] for b in attn_buckets(4106, group=1) if b[3]] == [128, 256, 256]
+    # without GQA (Phi-3: 32 kv heads) buckets above 1k keys use 256-key chunks, split beyond 4k
+    assert [(b[1], b[3]) for b in attn_buckets(8200, 16, group=1, nkv=32)] == [(128, True), (256, True), (256, True),
+                                                                              (128, False)]
 
 
 def test_split_blocks_per_head():
     from llm_consensus_amd.engine.engine import split_blocks_per_head
 
-    assert split_blocks_per_head(32, 8) == 32   # Llama-3-8B: 256 8-wave blocks per row
-    assert split_blocks_per_head(32, 32) == 16  # Phi-3: 512 4-wave blocks
-    assert split_blocks_per_head(4, 1) == 64    # a TP=8 rank: capped at 64 partials
-    assert split_blocks_per_head(16, 2) == 32   # a 70B TP=4 rank (G = 8): chunks x G <= 256
+    assert split_blocks_per_head(32, 8) == 32    # Llama-3-8B: 256 blocks per row
+    assert split_blocks_per_head(32, 32) == 16   # Phi-3: 512 4-wave blocks
+    assert split_blocks_per_head(4, 1) == 256    # a TP=8 rank: every CU, two-level merge
+    assert split_blocks_per_head(16, 2) == 128   # a 70B TP=4 rank

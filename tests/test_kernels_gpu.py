@@ -213,24 +213,29 @@ def test_attn_decode_balanced_split(cuda, nh, nkv, D, gc):
         close(out, ref, 2e-2)
 
 
+@pytest.mark.parametrize("nh,nkv", [(4, 1), (8, 1), (16, 2)])
 @pytest.mark.parametrize("gc", [100, 256, 300])
-def test_attn_decode_wide_split(cuda, gc):
-    """A TP=8 rank of Llama-3-8B (4 query heads, ONE kv head) at a judge-length context: the keys
-    spread over up to 300 blocks, so the last arriver folds the granules of many chunk groups in
-    batches of 8 per thread."""
+def test_attn_decode_wide_split(cuda, nh, nkv, gc):
+    """TP ranks at judge-length contexts (a TP=8 rank of Llama-3-8B: 4 query heads on ONE kv head;
+    Llama-3-70B TP=8 / TP=4 ranks: G = 8): the keys spread over up to 300 blocks, so the partials
+    merge in two levels (groups of 16, then the group results). Lengths change between launches on
+    the same workspace; every ticket must be re-armed."""
     torch.manual_seed(6)
-    nh, nkv, D, bs = 4, 1, 128, 64
-    lens = [40000, 9000, 130]
-    B = len(lens)
-    kc, vc, bt = _paged_kv(B, max(lens), nkv, D, bs)
+    D, bs = 128, 64
+    B = 3
+    kc, vc, bt = _paged_kv(B, 40000, nkv, D, bs)
     q = rnd(B, nh * D)
-    sl = torch.tensor(lens, dtype=torch.int32)
     part, ctr = ops.decode_attn_workspace(B, nh, nkv, D, gc, "cuda")
     out = torch.empty(B, nh * D, dtype=BF, device="cuda")
     scale = 1 / math.sqrt(D)
-    ref = oracle.attn_decode(q.cpu(), kc.cpu(), vc.cpu(), bt, sl, nh, nkv, D, bs, scale)
-    ops.attn_decode(q, kc, vc, bt.cuda(), sl.cuda(), out, part, ctr, nh, nkv, D, bs, 128, scale, grid_chunks=gc)
-    close(out, ref, 2e-2)
+    for lens in ([40000, 9000, 130], [2100, 39999, 17000], [40000, 9000, 130]):
+        sl = torch.tensor(lens, dtype=torch.int32)
+        ref = oracle.attn_decode(q.cpu(), kc.cpu(), vc.cpu(), bt, sl, nh, nkv, D, bs, scale)
+        out.zero_()
+        ops.attn_decode(q, kc, vc, bt.cuda(), sl.cuda(), out, part, ctr, nh, nkv, D, bs, 128, scale, grid_chunks=gc)
+        close(out, ref, 2e-2)
+    tickets = torch.cat([ctr[..., :1], ctr[..., 2:]], dim=-1)
+    assert int(tickets.abs().sum()) == 0, ctr
 
 
 @pytest.mark.parametrize("nh,nkv,D", [(32, 8, 128), (32, 32, 96), (16, 2, 128), (4, 2, 64)])

@@ -226,7 +226,8 @@ def main() -> None:
         tok = get_tokenizer(cfg.vocab)
         ids = tok.encode(prompt_text, add_bos=True)
         ctx = len(ids) + args.max_tokens + 64
-        graphs = not args.no_graphs and (tp.size == 1 or tp.custom is not None)
+        graphs = not args.no_graphs and (tp.size == 1 or tp.custom is not None
+                                         or (not on_cpu and tp.graph_capture_ok(dev)))
         eng = Engine(cfg, EngineConfig(device=dev, max_context=ctx, seed=e["seed"], steps_per_graph=args.steps_per_graph,
                                        use_graphs=graphs), tp=tp, name=e["name"])
         responders.append((i, eng, ids, tok))
@@ -238,7 +239,8 @@ def main() -> None:
         # expand (invalid UTF-8 -> U+FFFD -> 3 byte tokens), so budget 2x per response
         fixed = len(jtok.encode(build_judge_prompt(prompt_text, []), add_bos=True))
         judge_ctx = min(jcfg.max_position, fixed + n_resp * (2 * args.max_tokens + 64) + jmax + 64)
-        graphs = not args.no_graphs and (jtp_grp.size == 1 or jtp_grp.custom is not None)
+        graphs = not args.no_graphs and (jtp_grp.size == 1 or jtp_grp.custom is not None
+                                         or (not on_cpu and jtp_grp.graph_capture_ok(dev)))
         judge = Engine(jcfg, EngineConfig(device=dev, max_context=judge_ctx, seed=judge_plan["seed"],
                                           steps_per_graph=args.steps_per_graph, use_graphs=graphs),
                        tp=jtp_grp, name=judge_plan["name"])

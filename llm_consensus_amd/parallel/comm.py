@@ -10,7 +10,8 @@ On GPUs the collectives go through the custom xGMI kernels (``custom_ar.py``, K1
 ``enable_custom()`` has mapped the peers: one-shot for decode-sized messages (no RCCL call and no
 host work per collective, so a TP engine's decode step is capturable in one HIP graph) and
 two-shot (reduce-scatter + all-gather phases over peer reads) for prefill-sized ones. RCCL is the
-fallback when a group cannot map its peers; CPU/gloo groups use torch.distributed.
+fallback when a group cannot map its peers (its collectives are then captured in the decode graphs
+too, after a collective self-check: ``graph_capture_ok``); CPU/gloo groups use torch.distributed.
 
 Control plane: TP ranks must take every control decision identically (which requests form a
 batch, when a decode stops on cancellation or deadline), or their collectives desynchronise. A
@@ -66,6 +67,29 @@ class TPGroup:
             self.custom = self.custom2 = None
             return False
         return True
+
+    def graph_capture_ok(self, device) -> bool:
+        """Can this group's RCCL collectives run inside the engine's decode HIP graphs? The
+        fallback when the custom kernels are unavailable: instead of decoding eagerly (~320
+        launches + 64 host-issued RCCL calls per token), capture RCCL too. Collective: every rank
+        captures an all-reduce + all-gather, the group agrees before anyone replays (a rank that
+        failed to capture never leaves peers waiting in a replayed collective), then checks the
+        sums and agrees again. False on every rank if anything failed; gloo groups are never
+        capturable."""
+        if self.size == 1:
+            return True
+        if self.group is None or dist.get_backend(self.group) != "nccl":
+            return False
+
+        def agree(ok: bool) -> bool:  # MIN over the group, eager RCCL on a one-element tensor
+            t = torch.tensor([1 if ok else 0], dtype=torch.int32, device=device)
+            dist.all_reduce(t, op=dist.ReduceOp.MIN, group=self.group)
+            return bool(t.item())
+
+        cap = rccl_graph_capture(self.group, self.rank, self.size, device)
+        if not agree(cap is not None):
+            return False
+        return agree(rccl_graph_replay_check(cap, self.rank, self.size, device))
 
     # -- control plane ----------------------------------------------------------------------------
     def leader_decides(self, value: int) -> int:
@@ -203,6 +227,39 @@ class TPGroup:
     def barrier(self) -> None:
         if self.size > 1:
             dist.barrier(group=self.group)
+
+
+def rccl_graph_capture(group, rank: int, size: int, device):
+    """Capture an all-reduce and an all-gather of small fp32 buffers over ``group`` in one HIP
+    graph (after an eager warm-up collective); (graph, x, y) or None if capture failed."""
+    try:
+        x = torch.full((256,), float(rank + 1), dtype=torch.float32, device=device)
+        y = torch.empty(size * 256, dtype=torch.float32, device=device)
+        dist.all_reduce(x.clone(), group=group)  # communicator ready before the capture
+        torch.cuda.synchronize(device)
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g, stream=torch.cuda.Stream(device)):
+            dist.all_reduce(x, group=group)
+            dist.all_gather_into_tensor(y, x, group=group)
+        return g, x, y
+    except Exception as e:  # noqa: BLE001
+        warnings.warn(f"RCCL graph capture failed ({type(e).__name__}: {e}); TP decode stays eager")
+        return None
+
+
+def rccl_graph_replay_check(cap, rank: int, size: int, device) -> bool:
+    """Replay a ``rccl_graph_capture`` graph twice from fresh inputs and check the sums."""
+    g, x, y = cap
+    try:
+        total = size * (size + 1) / 2
+        for _ in range(2):
+            x.fill_(float(rank + 1))
+            g.replay()
+        torch.cuda.synchronize(device)
+        return bool((x == total).all()) and bool((y == total).all())
+    except Exception as e:  # noqa: BLE001
+        warnings.warn(f"RCCL graph replay failed ({type(e).__name__}: {e}); TP decode stays eager")
+        return False
 
 
 def shard_range(n: int, rank: int, size: int):

@@ -434,10 +434,10 @@ def worker_main(gpu: int, conn, models: List[dict], dist_info: Optional[dict], t
                     tp.enable_custom(f"cuda:{gpu}")  # collective over the group: same order on every rank
             else:
                 tp = TPGroup.single()
-            # TP decode is graph-captured when its collectives are the custom xGMI kernels; a group
-            # whose peers could not be mapped decodes eagerly over RCCL (LLMC_TP_GRAPHS=1 captures
-            # the RCCL collectives instead — needs >= 2 GPUs, unverified on the 1-GPU test box)
-            graphs = tp.size == 1 or tp.custom is not None or os.environ.get("LLMC_TP_GRAPHS") == "1"
+            # TP decode is graph-captured: over the custom xGMI kernels, or — for a group whose peers
+            # could not be mapped — over RCCL if the group's capture self-check passes on every rank
+            # (collective, same order on every rank); eager only if that fails too
+            graphs = tp.size == 1 or tp.custom is not None or (not on_cpu and tp.graph_capture_ok(f"cuda:{gpu}"))
             ecfg = EngineConfig(device="cpu" if on_cpu else f"cuda:{gpu}", max_context=m["max_context"],
                                 max_batch=m.get("max_batch", 1), max_seqs=m.get("max_seqs", 0), seed=m["seed"],
                                 use_graphs=graphs,

@@ -99,3 +99,37 @@ def test_tp2_gpu_matches_tp1(cuda, name, ekw):
         lt = ref.full_logits(s).float().cpu()
         gap = float(lt.max() - lt[gen[agree]])
         assert gap < 0.01 * float(lt.abs().max()), (agree, gap, gen, ref_gen)
+
+
+def _rccl_capture_worker(port, q):
+    import torch.distributed as dist
+
+    try:
+        torch.cuda.set_device(0)
+        dist.init_process_group("nccl", init_method=f"tcp://127.0.0.1:{port}", rank=0, world_size=1,
+                                device_id=torch.device("cuda", 0))
+        from llm_consensus_amd.parallel.comm import TPGroup, rccl_graph_capture, rccl_graph_replay_check
+
+        cap = rccl_graph_capture(dist.group.WORLD, 0, 1, "cuda:0")
+        ok = cap is not None and rccl_graph_replay_check(cap, 0, 1, "cuda:0")
+        # the collective wrapper on a gloo group is never capturable
+        g = dist.new_group([0], backend="gloo")
+        gloo_ok = TPGroup(g, 0, 2).graph_capture_ok("cuda:0")
+        dist.destroy_process_group()
+        q.put((ok, gloo_ok))
+    except Exception as e:  # noqa: BLE001
+        q.put((f"{type(e).__name__}: {e}", None))
+
+
+def test_rccl_collectives_capture_in_hip_graph():
+    """The RCCL fallback of TP decode (peers not mappable) captures its collectives in the decode
+    graph after a self-check: an all-reduce + all-gather captured in a HIP graph and replayed give
+    the right sums on this torch/RCCL build (one rank: more need more GPUs than the test box has)."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    p = ctx.Process(target=_rccl_capture_worker, args=(_free_port(), q))
+    p.start()
+    ok, gloo_ok = q.get(timeout=300)
+    p.join(timeout=60)
+    assert ok is True, ok
+    assert gloo_ok is False

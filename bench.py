@@ -56,6 +56,22 @@ def log(*a):
     print(f"[bench r{os.environ.get('RANK', '0')}]", *a, file=sys.stderr, flush=True)
 
 
+class Progress:
+    """on_tokens callback that logs a token count every ``every`` seconds (rank 0): long phases
+    (a judge decode on ranks time-sharing one GPU) keep writing instead of looking hung."""
+
+    def __init__(self, what: str, every: float = 30.0):
+        self.what, self.every, self.n = what, every, 0
+        self.t0 = self.last = time.perf_counter()
+
+    def __call__(self, *args) -> None:
+        self.n += len(args[-1])
+        now = time.perf_counter()
+        if now - self.last >= self.every:
+            self.last = now
+            log(f"{self.what}: {self.n} tokens after {now - self.t0:.0f}s")
+
+
 def judge_tp_degree(cfg, world: int, requested: int) -> int:
     """TP degree of the judge: ``requested`` if > 0, else the largest t <= min(world, 8) that
     shards the judge's heads, kv heads, FFN and vocab evenly (8 = custom all-reduce limit)."""
@@ -272,8 +288,9 @@ def main() -> None:
         def run_one(j):
             try:
                 i, e, ids, _ = responders[j]
+                prog = Progress(f"round {step}: responder {i}") if (rank == 0 and j == 0) else None
                 outs[i] = e.generate_ids(ids, args.max_tokens, temperature=args.temperature,
-                                         seed=1000 * step + i + 1, stop_on_eos=False)
+                                         seed=1000 * step + i + 1, stop_on_eos=False, on_tokens=prog)
             except BaseException as ex:  # noqa: BLE001
                 errs.append(ex)
 
@@ -315,7 +332,8 @@ def main() -> None:
             t_jp = time.perf_counter()
             if rank == 0:
                 log(f"round {step}: judge prefill of {len(rest_ids)} tokens in {t_jp - t_resp:.2f}s (TP={judge.tp.size})")
-            jids = judge.decode([jseq], [SamplingParams(jmax, args.temperature, 1.0, 0, 99 + step, False)])[0]
+            jids = judge.decode([jseq], [SamplingParams(jmax, args.temperature, 1.0, 0, 99 + step, False)],
+                                on_tokens=Progress(f"round {step}: judge") if rank == 0 else None)[0]
             stats["judge_prompt_tokens"] = jseq.length - len(jids)
             stats["judge_prefill_s"] = t_jp - t_resp
             stats["judge_decode_s"] = time.perf_counter() - t_jp

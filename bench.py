@@ -92,7 +92,19 @@ def make_plan(args, world: int):
     if args.config == "fanout":
         n = args.n_models or max(3, world)
         rf = fam(args.model)
-        resp = [{"name": f"{args.model}@{i}", "family": rf, "ranks": [i % world], "seed": 1000 + i} for i in range(n)]
+        # whole models round-robin over the GPUs; when n is not a multiple of N the remainder would
+        # pile onto the first GPUs (N=2: GPU 0 decoding two models, GPU 1 one, the round waiting
+        # on GPU 0), so each leftover responder is tensor-parallel over an equal share of the GPUs
+        # instead: every GPU then streams the same bytes per step
+        whole = n - n % world if world > 1 else n
+        rest = n - whole
+        tp = world // rest if rest else 1
+        if rest and (world % rest or judge_tp_degree(FAMILIES[rf], tp, 0) != tp):
+            whole, rest = n, 0  # no even sharding: round-robin all of them
+        resp = [{"name": f"{args.model}@{i}", "family": rf, "ranks": [i % world], "seed": 1000 + i}
+                for i in range(whole)]
+        resp += [{"name": f"{args.model}@{whole + j}", "family": rf, "ranks": list(range(j * tp, (j + 1) * tp)),
+                  "seed": 1000 + whole + j} for j in range(rest)]
         jf = fam(args.judge)
         jtp = judge_tp_degree(FAMILIES[jf], world, args.judge_tp)
         judge = {"name": f"{args.judge}@judge", "family": jf, "ranks": list(range(jtp)), "seed": 777}
@@ -389,8 +401,9 @@ def main() -> None:
         value = tot_tokens / elapsed
         resp_tok_s = n_resp * args.max_tokens * args.steps / sum(p["responders_s"] for p in per_step)
         jtp = len(judge_plan["ranks"])
-        par = {"fanout": f"fanout{n_resp}", "4": f"fanout2-tp{len(resp_plan[0]['ranks'])}",
-               "5": "fanout3-mixed"}[args.config]
+        rtp = sorted({len(e["ranks"]) for e in resp_plan if len(e["ranks"]) > 1})
+        par = {"fanout": f"fanout{n_resp}" + "".join(f"-resp_tp{t}" for t in rtp),
+               "4": f"fanout2-tp{len(resp_plan[0]['ranks'])}", "5": "fanout3-mixed"}[args.config]
         out = {
             "metric": METRIC,
             "value": round(value, 2),

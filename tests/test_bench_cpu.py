@@ -62,3 +62,13 @@ def test_fanout_eight_ranks_like_the_scale_run():
     assert d["n_gpus"] == 8 and d["config"]["global_batch"] == 8 and d["scaling"] == "weak"
     assert d["extra"]["judge_tp"] >= 2
     _tokens_ok(d, 12)
+
+
+def test_fanout_two_ranks_balances_the_third_responder():
+    """N=2: two whole responders (one per rank) and the third tensor-parallel over both ranks, so
+    both GPUs stream the same bytes per step; the judge is TP=2."""
+    d = _run(2, ["--shapes", "tiny", "--steps", "1", "--warmup", "0", "--max-tokens", "12"], 29694)
+    assert d["config"]["global_batch"] == 3
+    assert "2x llama-tiny + 1x llama-tiny TP=2 responders" in d["config"]["model"]
+    assert d["config"]["parallelism"] == "fanout3-resp_tp2-over2gpus-judge_tp2"
+    _tokens_ok(d, 12)

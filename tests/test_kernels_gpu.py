@@ -213,6 +213,31 @@ def test_attn_decode_balanced_split(cuda, nh, nkv, D, gc):
         close(out, ref, 2e-2)
 
 
+@pytest.mark.parametrize("nh,nkv,chunk,cap", [(4, 1, 128, 32768), (4, 1, 256, 65536), (16, 2, 256, 32768)])
+def test_attn_decode_fused_long_context(cuda, nh, nkv, chunk, cap):
+    """The fixed-chunk form on TP ranks at judge lengths (engine.attn_buckets: one or two kv heads
+    over up to 256 chunk blocks, merged in two levels of 16), lengths changing between launches on
+    one workspace."""
+    torch.manual_seed(8)
+    D, bs, B = 128, 64, 3
+    Lmax = min(cap, 40000)
+    kc, vc, bt = _paged_kv(B, Lmax, nkv, D, bs)
+    q = rnd(B, nh * D)
+    gc = cap // chunk
+    part, ctr = ops.decode_attn_workspace(B, nh, nkv, D, gc, "cuda", fused=True)
+    out = torch.empty(B, nh * D, dtype=BF, device="cuda")
+    scale = 1 / math.sqrt(D)
+    for lens in ([Lmax, 9000, 130], [2100, Lmax - 1, 17000], [Lmax, 9000, 130]):
+        sl = torch.tensor(lens, dtype=torch.int32)
+        ref = oracle.attn_decode(q.cpu(), kc.cpu(), vc.cpu(), bt, sl, nh, nkv, D, bs, scale)
+        out.zero_()
+        ops.attn_decode(q, kc, vc, bt.cuda(), sl.cuda(), out, part, ctr, nh, nkv, D, bs, chunk, scale,
+                        grid_chunks=gc, fused=True)
+        close(out, ref, 2e-2)
+    tickets = torch.cat([ctr[..., :1], ctr[..., 2:]], dim=-1)
+    assert int(tickets.abs().sum()) == 0, ctr
+
+
 @pytest.mark.parametrize("nh,nkv", [(4, 1), (8, 1), (16, 2)])
 @pytest.mark.parametrize("gc", [100, 256, 300])
 def test_attn_decode_wide_split(cuda, nh, nkv, gc):

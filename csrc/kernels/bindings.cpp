@@ -20,7 +20,8 @@ extern "C" {
 int llmc_rmsnorm(const void*, const void*, void*, int, int, int, int, float, hipStream_t);
 int llmc_embedding(const void*, const void*, void*, int, int, int, hipStream_t);
 int llmc_silu_mul_interleaved(const void*, void*, int, int, hipStream_t);
-int llmc_gemv(int, const void*, int, const void*, float, const void*, void*, int, int, int, int, hipStream_t);
+int llmc_gemv(int, const void*, int, const void*, float, const void*, void*, int, int, int, int, int, hipStream_t);
+int llmc_gemvm(int, const void*, int, const void*, float, const void*, void*, int, int, int, int, hipStream_t);
 int llmc_gemm(const void*, int, const void*, int, void*, int, int, int, int, int, hipStream_t);
 int llmc_rope_kv_write(const void*, int, void*, int, const void*, const void*, const void*, void*, void*, const void*,
                        int, int, int, int, int, hipStream_t);
@@ -28,7 +29,7 @@ int llmc_attn_decode_groups(int);
 int llmc_attn_decode(const void*, int, const void*, const void*, const void*, int, const void*, void*, void*, void*,
                      int, int, int, int, int, int, int, int, int, int, float, int, hipStream_t);
 int llmc_gemv_qkv_rope(int, const void*, int, const void*, float, const void*, int, int, void*, int, void*, void*,
-                       const void*, const void*, const void*, const void*, int, int, int, int, hipStream_t);
+                       const void*, const void*, const void*, const void*, int, int, int, int, int, hipStream_t);
 int llmc_attn_prefill(const void*, int, const void*, const void*, const void*, int, const void*, const void*,
                       const void*, void*, int, int, int, int, int, int, int, float, hipStream_t);
 int llmc_sample(const void*, int64_t, int, int, const void*, const void*, const void*, const void*, const void*, void*,
@@ -86,8 +87,12 @@ PYBIND11_MODULE(_llmc_hip, m) {
   m.def("silu_mul_interleaved", [](ptr gu, ptr y, int T, int I, ptr s) {
     check(llmc_silu_mul_interleaved(P(gu), P(y), T, I, S(s)), "silu_mul");
   });
-  m.def("gemv", [](int M, ptr x, int xs, ptr nw, float eps, ptr W, ptr out, int os, int N, int K, int epi, ptr s) {
-    check(llmc_gemv(M, P(x), xs, P(nw), eps, P(W), P(out), os, N, K, epi, S(s)), "gemv");
+  m.def("gemv", [](int M, ptr x, int xs, ptr nw, float eps, ptr W, ptr out, int os, int N, int K, int epi, int mfma,
+                   ptr s) {
+    check(llmc_gemv(M, P(x), xs, P(nw), eps, P(W), P(out), os, N, K, epi, mfma, S(s)), "gemv");
+  });
+  m.def("gemvm", [](int M, ptr x, int xs, ptr nw, float eps, ptr W, ptr out, int os, int N, int K, int epi, ptr s) {
+    check(llmc_gemvm(M, P(x), xs, P(nw), eps, P(W), P(out), os, N, K, epi, S(s)), "gemvm");
   });
   m.def("gemm", [](ptr A, int lda, ptr W, int ldw, ptr C, int ldc, int M, int N, int K, int epi, ptr s) {
     check(llmc_gemm(P(A), lda, P(W), ldw, P(C), ldc, M, N, K, epi, S(s)), "gemm");
@@ -107,9 +112,10 @@ PYBIND11_MODULE(_llmc_hip, m) {
           "attn_decode");
   });
   m.def("gemv_qkv_rope", [](int M, ptr x, int xs, ptr nw, float eps, ptr W, int N, int K, ptr qo, int qos, ptr kc,
-                            ptr vc, ptr pos, ptr slots, ptr cos_t, ptr sin_t, int nh, int nkv, int D, int bs, ptr s) {
+                            ptr vc, ptr pos, ptr slots, ptr cos_t, ptr sin_t, int nh, int nkv, int D, int bs,
+                            int mfma, ptr s) {
     check(llmc_gemv_qkv_rope(M, P(x), xs, P(nw), eps, P(W), N, K, P(qo), qos, P(kc), P(vc), P(pos), P(slots),
-                             P(cos_t), P(sin_t), nh, nkv, D, bs, S(s)),
+                             P(cos_t), P(sin_t), nh, nkv, D, bs, mfma, S(s)),
           "gemv_qkv_rope");
   });
   m.def("attn_prefill", [](ptr q, int qs, ptr kc, ptr vc, ptr bt, int bts, ptr qst, ptr ql, ptr cl, ptr out, int os,

@@ -88,9 +88,15 @@ static int dispatch_m(int M, const void* x, int x_stride, const void* nw, float 
 }
 
 static int gemv_dispatch(int M, const void* x, int x_stride, const void* norm_w, float eps, const void* W, void* out,
-                         int out_stride, int N, int K, int epi, const RopeEpi& rope, hipStream_t s) {
+                         int out_stride, int N, int K, int epi, const RopeEpi& rope, bool mfma, hipStream_t s) {
   if (K % 8 != 0) return -1;
   if ((epi == EPI_SILU || epi == EPI_ROPE) && (N % 2 != 0)) return -1;
+  // 3-16 rows: the MFMA form (profiles/r2_batched_decode.md: from 3 rows on the VALU dot products,
+  // not the weight stream, set this kernel's time); 1-2 rows, or K off the 128-k tiles: VALU GEMV.
+  // `mfma` pins the MFMA form at every row count: an engine that batches >= 3 rows decodes all its
+  // steps on one form, so a request's tokens do not depend on how many rows shared its steps.
+  if ((M > kGemvMaxM || mfma) && K % 128 == 0 && x_stride % 8 == 0)
+    return gemvm_dispatch(M, x, x_stride, norm_w, eps, W, out, out_stride, N, K, epi, rope, s);
   const bool norm = norm_w != nullptr;
 #define LLMC_GEMV_CASE(E)                                                                                   \
   case E:                                                                                                   \
@@ -114,21 +120,21 @@ static int gemv_dispatch(int M, const void* x, int x_stride, const void* norm_w,
 using namespace llmc;
 
 extern "C" int llmc_gemv(int M, const void* x, int x_stride, const void* norm_w, float eps, const void* W, void* out,
-                         int out_stride, int N, int K, int epi, hipStream_t s) {
+                         int out_stride, int N, int K, int epi, int mfma, hipStream_t s) {
   if (epi == EPI_ROPE) return -5;
   RopeEpi rope{};
-  return gemv_dispatch(M, x, x_stride, norm_w, eps, W, out, out_stride, N, K, epi, rope, s);
+  return gemv_dispatch(M, x, x_stride, norm_w, eps, W, out, out_stride, N, K, epi, rope, mfma != 0, s);
 }
 
 // qkv projection for decode with fused RMSNorm prologue and RoPE + paged-KV-write epilogue.
 extern "C" int llmc_gemv_qkv_rope(int M, const void* x, int x_stride, const void* norm_w, float eps, const void* W,
                                   int N, int K, void* q_out, int q_stride, void* k_cache, void* v_cache,
                                   const void* positions, const void* slots, const void* cos_t, const void* sin_t,
-                                  int nh, int nkv, int D, int bs, hipStream_t s) {
+                                  int nh, int nkv, int D, int bs, int mfma, hipStream_t s) {
   if (N != (nh + 2 * nkv) * D || D % 2 != 0) return -1;
   RopeEpi rope{(bf16_t*)q_out, q_stride, (bf16_t*)k_cache, (bf16_t*)v_cache, (const int32_t*)positions,
                (const int32_t*)slots, (const float*)cos_t, (const float*)sin_t, nh, nkv, D, bs};
-  return gemv_dispatch(M, x, x_stride, norm_w, eps, W, nullptr, 0, N, K, EPI_ROPE, rope, s);
+  return gemv_dispatch(M, x, x_stride, norm_w, eps, W, nullptr, 0, N, K, EPI_ROPE, rope, mfma != 0, s);
 }
 
 // MoE decode (K11 at batch 1): one GEMV per (token, top-k slot) pair against the selected

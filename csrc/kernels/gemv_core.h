@@ -57,6 +57,12 @@ struct ArEpi {
   long cap;       // bytes per data parity
 };
 
+// Batched decode (3 <= M <= 16 rows): the MFMA form in gemv_mfma.hip, same prologue/epilogues.
+// This kernel serves M <= kGemvMaxM (and M <= 4 when K is not a multiple of 128).
+constexpr int kGemvMaxM = 2, kGemvmMaxM = 16;
+int gemvm_dispatch(int M, const void* x, int x_stride, const void* norm_w, float eps, const void* W, void* out,
+                   int out_stride, int N, int K, int epi, const RopeEpi& rope, hipStream_t st);
+
 template <int M, int NT, int RPW, int UNROLL, int PRO, int EPI, bool EXPERT = false>
 __global__ __launch_bounds__(NT) void gemv_kernel(const bf16_t* __restrict__ x, int x_stride,
                                                   const bf16_t* __restrict__ norm_w, float eps,

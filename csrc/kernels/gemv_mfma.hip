@@ -1,0 +1,271 @@
+// K6 (batched-decode class): y[m, n] = sum_k x[m, k] * W[n, k] for M = 5..16 rows on the matrix
+// cores — the decode step of a continuous batch of up to 16 sequences per engine.
+//
+// Why a third GEMM shape: the VALU GEMV (gemv_core.h) does 8 v_dot2 per 16-B weight chunk per row,
+// so past ~4 rows it turns VALU- and LDS-bound, and the 256 x 256 prefill GEMM launches only
+// N / 256 blocks (16 for a 4096-row projection). Here the weight stream stays the whole cost:
+//  * one block = 16 weight rows x all of K; its S waves split K (S = 4-8 on model shapes, so the
+//    grid holds ~8 waves per CU), wave w owns tiles [w*ntile, (w+1)*ntile) of 128 k.
+//  * a tile = 16 rows x 256 B, loaded as four whole 256-B row segments per instruction (lane
+//    -> row 4i + lane/16, chunk lane%16; non-temporal), one tile in flight behind the one being
+//    computed. The MFMA A fragment wants 16 rows x 64 B per instruction instead (lane -> row
+//    lane%16, k 8*(lane/16)): loaded that way the same bytes streamed 1.35x slower, so the tile
+//    goes through the wave's own 4 KiB of LDS (chunk c of row q at 16-B slot c ^ q: conflict-free
+//    for the 8-lane b128 write groups and the 4 fragment-read groups) — no barrier, one wave.
+//  * B fragment = x[lane%16][32j + 8*(lane/16) ..] (x is tiny and L2-resident), 4 per tile.
+//  * D[n][m] lands as 4 consecutive rows n (= 4*(lane/16) + t) of one token m (= lane%16) per lane:
+//    the (2i, 2i+1) row pairs of the SiLU gate/up and RoPE epilogues meet inside one lane.
+//  * PRO_NORM: rmsnorm(x)*w factorises as inv_rms[m] * (x * w): the MFMA takes bf16(x * w) and the
+//    epilogue scales by inv_rms[m], whose sum of squares every wave gathers from the x chunks it
+//    already loaded (no extra pass over x).
+//  * split-K partials meet in LDS (S x 1 KiB); wave 0 runs the fused epilogue: bf16 | f32 |
+//    residual add | SiLU-mul | RoPE + paged-KV write (same semantics as the GEMV's).
+// K % 128 == 0 (every model shape); other K take the GEMM path (ops.linear / ops.qkv_rope).
+#include "gemv_core.h"
+
+namespace llmc {
+
+template <int S, int PRO, int EPI>
+__global__ __launch_bounds__(S * 64) void gemvm_kernel(const bf16_t* __restrict__ x, int x_stride,
+                                                       const bf16_t* __restrict__ norm_w, float eps,
+                                                       const bf16_t* __restrict__ W, void* __restrict__ out,
+                                                       int out_stride, int M, int N, int K, RopeEpi rope) {
+  constexpr int TK = 128;  // k per tile: 16 rows x 256 B = one LDS bank row per weight row
+  __shared__ __attribute__((aligned(16))) char wt[S][16 * TK * 2];  // per-wave transposition tile
+  __shared__ f32x4 red[S][64];
+  __shared__ float ssr[S][16];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int r = lane & 15, g = lane >> 4;
+  const int n0 = blockIdx.x * 16;
+  const int ntile = K / TK / S;  // tiles of this wave (host: K % (TK * S) == 0)
+  const int kw = wave * ntile * TK;
+  // weight tile loads: instruction i covers rows 4i + lane/16, 16-B chunk lane%16 — four whole
+  // 256-B row segments per instruction (the MFMA fragment order, 16 rows x 64 B per instruction,
+  // measured 1.35x slower on the same bytes)
+  const u32x4* wsrc[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+    wsrc[i] = reinterpret_cast<const u32x4*>(W + static_cast<int64_t>(min(n0 + 4 * i + g, N - 1)) * K + kw + r * 8);
+  const u32x4* xp = reinterpret_cast<const u32x4*>(x + static_cast<int64_t>(min(r, M - 1)) * x_stride + kw + g * 8);
+  const u32x4* gp = reinterpret_cast<const u32x4*>(norm_w + kw + g * 8);  // PRO_NORM only
+  char* tile = wt[wave];
+
+  // one tile = 4 weight loads + 4 x fragments (k-steps of 32: lane (r, g) holds x[r][32j + 8g ..])
+  auto issue = [&](u32x4 (&wv)[4], u32x4 (&xv)[4], u32x4 (&gv)[4], int t) {
+    const int tu = min(t, ntile - 1) * (TK / 8);  // 16-B units
+#pragma unroll
+    for (int i = 0; i < 4; ++i) wv[i] = load16<true>(wsrc[i] + tu);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      xv[j] = xp[tu + 4 * j];
+      if constexpr (PRO == PRO_NORM) gv[j] = gp[tu + 4 * j];
+    }
+  };
+  f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+  float ss = 0.f;
+  auto consume = [&](const u32x4 (&wv)[4], const u32x4 (&xv)[4], const u32x4 (&gv)[4]) {
+    // row-major tile -> this wave's LDS (chunk c of row q at slot c ^ q: the b128 write groups of
+    // 8 lanes and the 4 fragment-read groups are conflict-free) -> A fragments (row r, chunk 4j + g)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int q = 4 * i + g;
+      *reinterpret_cast<u32x4*>(tile + q * 256 + ((r ^ q) << 4)) = wv[i];
+    }
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const u32x4 a = *reinterpret_cast<const u32x4*>(tile + r * 256 + (((4 * j + g) ^ r) << 4));
+      u32x4 xb = xv[j];
+      if constexpr (PRO == PRO_NORM) {
+        float f[8], w8[8];
+        unpack8(xv[j], f);
+        unpack8(gv[j], w8);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          ss += f[e] * f[e];
+          f[e] *= w8[e];
+        }
+        xb = pack8(f);
+      }
+      acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, a), __builtin_bit_cast(bf16x8, xb), acc,
+                                                    0, 0, 0);
+    }
+  };
+  u32x4 wc[4], xc[4], gc[4];
+  issue(wc, xc, gc, 0);
+  for (int t = 0; t + 1 < ntile; ++t) {
+    u32x4 wn[4], xn[4], gn[4];
+    issue(wn, xn, gn, t + 1);
+    consume(wc, xc, gc);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      wc[i] = wn[i];
+      xc[i] = xn[i];
+      if constexpr (PRO == PRO_NORM) gc[i] = gn[i];
+    }
+  }
+  consume(wc, xc, gc);
+
+  // ---- split-K reduction over the block's waves ----
+  red[wave][lane] = acc;
+  if constexpr (PRO == PRO_NORM) {
+    ss += __shfl_xor(ss, 16, 64);
+    ss += __shfl_xor(ss, 32, 64);
+    if (g == 0) ssr[wave][r] = ss;
+  }
+  __syncthreads();
+  if (wave != 0) return;
+  f32x4 v = red[0][lane];
+#pragma unroll
+  for (int w = 1; w < S; ++w) v += red[w][lane];
+  const int m = r;
+  if (m >= M) return;
+  if constexpr (PRO == PRO_NORM) {
+    float t = 0.f;
+#pragma unroll
+    for (int w = 0; w < S; ++w) t += ssr[w][m];
+    v *= rsqrtf(t / K + eps);
+  }
+  const int nb = n0 + 4 * g;  // this lane's rows nb .. nb + 3 of token m
+  if (nb >= N) return;
+  const bool full = nb + 3 < N;
+
+  // ---- fused epilogue ----
+  if constexpr (EPI == EPI_F32) {
+    float* o = reinterpret_cast<float*>(out) + static_cast<int64_t>(m) * out_stride + nb;
+    if (full && (out_stride % 4 == 0)) {
+      *reinterpret_cast<f32x4*>(o) = v;
+    } else {
+#pragma unroll
+      for (int t = 0; t < 4; ++t)
+        if (nb + t < N) o[t] = v[t];
+    }
+  } else if constexpr (EPI == EPI_BF16 || EPI == EPI_RESADD) {
+    bf16_t* o = reinterpret_cast<bf16_t*>(out) + static_cast<int64_t>(m) * out_stride + nb;
+    if (full && (out_stride % 4 == 0)) {
+      float f[4] = {v[0], v[1], v[2], v[3]};
+      if constexpr (EPI == EPI_RESADD) {
+        const u32x2 old = *reinterpret_cast<const u32x2*>(o);
+        f[0] += bf16_lo(old[0]);
+        f[1] += bf16_hi(old[0]);
+        f[2] += bf16_lo(old[1]);
+        f[3] += bf16_hi(old[1]);
+      }
+      *reinterpret_cast<u32x2*>(o) = u32x2{pack_bf16x2(f[0], f[1]), pack_bf16x2(f[2], f[3])};
+    } else {
+#pragma unroll
+      for (int t = 0; t < 4; ++t) {
+        if (nb + t >= N) continue;
+        o[t] = f32_to_bf16(EPI == EPI_RESADD ? bf16_to_f32(o[t]) + v[t] : v[t]);
+      }
+    }
+  } else if constexpr (EPI == EPI_SILU) {  // rows (2j, 2j + 1) = (gate_j, up_j) -> column j
+    bf16_t* o = reinterpret_cast<bf16_t*>(out) + static_cast<int64_t>(m) * out_stride + nb / 2;
+    if (full) {
+      *reinterpret_cast<uint32_t*>(o) = pack_bf16x2(silu(v[0]) * v[1], silu(v[2]) * v[3]);
+    } else {
+      if (nb + 1 < N) o[0] = f32_to_bf16(silu(v[0]) * v[1]);
+    }
+  } else if constexpr (EPI == EPI_ROPE) {
+    // rows (2i, 2i + 1) of a Q/K head = dims (i, i + D/2) (pair-interleaved on the host); V rows
+    // keep canonical order. The token's position and KV slot are per lane (token m).
+    const int D = rope.D, half = D / 2;
+    const int slot = rope.slots[m];
+    const int pos = rope.positions[m];
+    const int64_t page = slot >= 0 ? slot / rope.bs : 0;
+    const int off = slot >= 0 ? slot % rope.bs : 0;
+#pragma unroll
+    for (int p = 0; p < 2; ++p) {
+      const int n = nb + 2 * p;
+      if (n + 1 >= N) continue;
+      const float a = v[2 * p], b = v[2 * p + 1];
+      const int head = n / D;
+      if (head < rope.nh + rope.nkv) {
+        const int i = (n % D) / 2;
+        const int64_t t = static_cast<int64_t>(pos) * half + i;
+        const float c = rope.cos_t[t], sn = rope.sin_t[t];
+        const float o1 = a * c - b * sn, o2 = b * c + a * sn;
+        if (head < rope.nh) {
+          bf16_t* qo = rope.q_out + static_cast<int64_t>(m) * rope.q_stride + head * D;
+          qo[i] = f32_to_bf16(o1);
+          qo[i + half] = f32_to_bf16(o2);
+        } else if (slot >= 0) {
+          bf16_t* ko = rope.k_cache + ((page * rope.nkv + (head - rope.nh)) * rope.bs + off) * D;
+          ko[i] = f32_to_bf16(o1);
+          ko[i + half] = f32_to_bf16(o2);
+        }
+      } else if (slot >= 0) {
+        const int vh = head - rope.nh - rope.nkv, d = n % D;
+        bf16_t* vv = rope.v_cache + ((page * rope.nkv + vh) * rope.bs + off) * D;
+        *reinterpret_cast<uint32_t*>(vv + d) = pack_bf16x2(a, b);
+      }
+    }
+  }
+}
+
+template <int S, int PRO, int EPI>
+static int launch_gemvm_s(const void* x, int x_stride, const void* nw, float eps, const void* W, void* out,
+                          int out_stride, int M, int N, int K, const RopeEpi& rope, hipStream_t st) {
+  const int grid = (N + 15) / 16;
+  gemvm_kernel<S, PRO, EPI><<<grid, S * 64, 0, st>>>((const bf16_t*)x, x_stride, (const bf16_t*)nw, eps,
+                                                     (const bf16_t*)W, out, out_stride, M, N, K, rope);
+  return static_cast<int>(hipGetLastError());
+}
+
+// Waves per block: enough split-K that the grid holds ~8 waves per CU (2048), while every wave
+// keeps >= 2 tiles of 128 k (one in flight behind the one it computes) and the tiles divide
+// evenly (at least 4 waves when K allows it; at most 8: 16 x 64 threads would cap a lane at 128
+// VGPRs and spill).
+static int pick_split(int N, int K) {
+  const int blocks = (N + 15) / 16, tiles = K / 128;
+  int S = 1;
+  while (S < 8 && tiles % (2 * S) == 0 &&
+         (S < 4 || (static_cast<long>(blocks) * S < 2048 && tiles / (2 * S) >= 2)))
+    S *= 2;
+  return S;
+}
+
+template <int PRO, int EPI>
+static int launch_gemvm(const void* x, int x_stride, const void* nw, float eps, const void* W, void* out,
+                        int out_stride, int M, int N, int K, const RopeEpi& rope, hipStream_t st) {
+  switch (pick_split(N, K)) {
+    case 1: return launch_gemvm_s<1, PRO, EPI>(x, x_stride, nw, eps, W, out, out_stride, M, N, K, rope, st);
+    case 2: return launch_gemvm_s<2, PRO, EPI>(x, x_stride, nw, eps, W, out, out_stride, M, N, K, rope, st);
+    case 4: return launch_gemvm_s<4, PRO, EPI>(x, x_stride, nw, eps, W, out, out_stride, M, N, K, rope, st);
+    case 8: return launch_gemvm_s<8, PRO, EPI>(x, x_stride, nw, eps, W, out, out_stride, M, N, K, rope, st);
+    default: return -1;
+  }
+}
+
+int gemvm_dispatch(int M, const void* x, int x_stride, const void* norm_w, float eps, const void* W, void* out,
+                   int out_stride, int N, int K, int epi, const RopeEpi& rope, hipStream_t st) {
+  if (M < 1 || M > kGemvmMaxM || K % 128 != 0 || x_stride % 8 != 0) return -1;
+  if ((epi == EPI_SILU || epi == EPI_ROPE) && N % 4 != 0) return -1;
+  const bool norm = norm_w != nullptr;
+#define LLMC_GEMVM_CASE(E)                                                                                    \
+  case E:                                                                                                     \
+    return norm ? launch_gemvm<PRO_NORM, E>(x, x_stride, norm_w, eps, W, out, out_stride, M, N, K, rope, st) \
+                : launch_gemvm<PRO_NONE, E>(x, x_stride, norm_w, eps, W, out, out_stride, M, N, K, rope, st);
+  switch (epi) {
+    LLMC_GEMVM_CASE(EPI_BF16)
+    LLMC_GEMVM_CASE(EPI_F32)
+    LLMC_GEMVM_CASE(EPI_RESADD)
+    LLMC_GEMVM_CASE(EPI_SILU)
+    case EPI_ROPE:
+      if (!norm) return -5;
+      return launch_gemvm<PRO_NORM, EPI_ROPE>(x, x_stride, norm_w, eps, W, out, out_stride, M, N, K, rope, st);
+    default: return -4;
+  }
+#undef LLMC_GEMVM_CASE
+}
+
+}  // namespace llmc
+
+// Direct entry (tests / microbenchmarks: the MFMA form at any M <= 16).
+extern "C" int llmc_gemvm(int M, const void* x, int x_stride, const void* norm_w, float eps, const void* W, void* out,
+                          int out_stride, int N, int K, int epi, hipStream_t s) {
+  if (epi == llmc::EPI_ROPE) return -5;
+  llmc::RopeEpi rope{};
+  return llmc::gemvm_dispatch(M, x, x_stride, norm_w, eps, W, out, out_stride, N, K, epi, rope, s);
+}
+

@@ -40,7 +40,7 @@ from ..utils.native import runtime
 class EngineConfig:
     device: str = "cuda:0"
     max_context: int = 8192
-    max_batch: int = 1   # decode rows per step (GEMV M <= 4)
+    max_batch: int = 1   # decode rows per step (weight-streaming GEMV/MFMA form: M <= 16)
     max_seqs: int = 0    # live sequences the KV pool is sized for (0 = max_batch)
     block_size: int = 64
     kv_blocks: int = 0
@@ -140,6 +140,10 @@ class Engine:
         self.name = name or cfg.name
         self.device = torch.device(self.ecfg.device)
         self.on_gpu = self.device.type == "cuda"
+        # decode projections of an engine that batches >= 3 rows run on the MFMA form at every row
+        # count (ops.linear ``mfma``): one numeric form per engine, so a request's tokens do not
+        # depend on how many rows shared its steps; 1-2 row engines keep the faster VALU GEMV
+        self.mfma_decode = self.on_gpu and self.ecfg.max_batch >= 3
         if self.on_gpu:
             torch.cuda.set_device(self.device)
             self.stream = torch.cuda.Stream(self.device, priority=self.ecfg.stream_priority)
@@ -368,7 +372,8 @@ class Engine:
             last_d = torch.tensor([q_start[i] + q_lens[i] - 1 for i in part], dtype=torch.long).to(dev)
             hl = h.index_select(0, last_d)
             lg = torch.empty(len(part), self.w.vocab_local, dtype=torch.float32, device=dev)
-            ops.linear(hl, self.w.lm_head, EPI_F32, out=lg, norm_w=self.w.final_norm, eps=c.rms_eps)
+            ops.linear(hl, self.w.lm_head, EPI_F32, out=lg, norm_w=self.w.final_norm, eps=c.rms_eps,
+                       mfma=self.mfma_decode)
             for j, i in enumerate(part):
                 s = batch[i][0]
                 s.logits = lg[j]
@@ -405,7 +410,7 @@ class Engine:
 
     def _row_parallel(self, x: torch.Tensor, W: torch.Tensor, h: torch.Tensor) -> None:
         """h += x @ W^T across the TP group (residual folded into rank 0's partial)."""
-        ops.linear(x, W, EPI_RESADD if self.tp.rank == 0 else EPI_BF16, out=h)
+        ops.linear(x, W, EPI_RESADD if self.tp.rank == 0 else EPI_BF16, out=h, mfma=self.mfma_decode)
         self.tp.all_reduce_(h)
 
     def _expert_ffn(self, A: torch.Tensor, ids: torch.Tensor, Lw) -> torch.Tensor:
@@ -424,7 +429,7 @@ class Engine:
                 gu = (A[p // k:p // k + 1].float() @ Lw.w_gu[e].float().t()).to(torch.bfloat16)
                 y[p] = (oracle.silu_mul_interleaved(gu).float() @ Lw.w_down[e].float().t()).to(torch.bfloat16)[0]
             return y
-        if n <= ops.GEMV_MAX_M:
+        if n <= ops.MOE_GEMV_MAX_M:
             act = torch.empty(n * k, I_l, dtype=torch.bfloat16, device=A.device)
             ops.moe_gemv(A, Lw.w_gu, ids, k, act, 2 * I_l, H, EPI_SILU)
             ops.moe_gemv(act, Lw.w_down, ids, 1, y, H, I_l, EPI_BF16)
@@ -508,7 +513,8 @@ class Engine:
         ops.embedding(self.tokens_in[:B], self.w.embed, out=h)
         for li, Lw in enumerate(self.w.layers):
             ops.qkv_rope(h, Lw.w_qkv, Lw.ln1, c.rms_eps, q, self.k_cache[li], self.v_cache[li], self.positions[:B],
-                         self.slots[:B], self.cos_t, self.sin_t, self.nh, self.nkv, self.D, self.bs)
+                         self.slots[:B], self.cos_t, self.sin_t, self.nh, self.nkv, self.D, self.bs,
+                         mfma=self.mfma_decode)
             ops.attn_decode(q, self.k_cache[li], self.v_cache[li], self.block_tables[:B], self.seq_lens[:B], attn,
                             part[:B], self.attn_counters[:B], self.nh, self.nkv, self.D, self.bs, chunk, self.scale,
                             grid_chunks, fused=fused)
@@ -516,10 +522,10 @@ class Engine:
             if c.is_moe:
                 self._moe_decode(h, Lw, B)
             else:
-                ops.linear(h, Lw.w_gu, EPI_SILU, out=act, norm_w=Lw.ln2, eps=c.rms_eps)
+                ops.linear(h, Lw.w_gu, EPI_SILU, out=act, norm_w=Lw.ln2, eps=c.rms_eps, mfma=self.mfma_decode)
                 self._row_parallel(act, Lw.w_down, h)
         lg = self.logits_local[:B]
-        ops.linear(h, self.w.lm_head, EPI_F32, out=lg, norm_w=self.w.final_norm, eps=c.rms_eps)
+        ops.linear(h, self.w.lm_head, EPI_F32, out=lg, norm_w=self.w.final_norm, eps=c.rms_eps, mfma=self.mfma_decode)
         logits = self._gather_logits(B)
         self._sample(B, logits)
 
@@ -790,26 +796,39 @@ class Engine:
         """Greedy decode of ``n`` tokens one eager step at a time (TP=1), returning (tokens, logits
         [n, V] f32): row i holds the full-vocabulary logits token i was sampled from — the hook the
         teacher-forced oracle test compares against a CPU prefill of prompt + tokens[:i]."""
+        toks, lg = self.debug_decode_logits_batch([prompt], n)
+        return toks[0], lg[0]
+
+    @torch.no_grad()
+    def debug_decode_logits_batch(self, prompts: List[Seq[int]], n: int):
+        """``debug_decode_logits`` for B = len(prompts) rows decoded together (the batched decode
+        GEMV forms: VALU rows <= 4, MFMA 5-16): (tokens [B][n], logits [B, n, V] f32)."""
         if self.tp.size != 1:
             raise EngineError("debug_decode_logits: TP=1 only")
-        seq = self.new_sequence()
+        B = len(prompts)
+        if B > self.ecfg.max_batch:
+            raise EngineError(f"{B} rows > max_batch {self.ecfg.max_batch}")
+        seqs = [self.new_sequence() for _ in range(B)]
         try:
             with self._on_stream():
-                self.prefill([seq], [list(prompt)])
-                self._reserve(seq, seq.length + n + 2)
+                self.prefill(seqs, [list(p) for p in prompts])
+                for s in seqs:
+                    self._reserve(s, s.length + n + 2)
                 self._use_topkp = False
-                self._bind_rows([seq], [SamplingParams(n, 0.0, 1.0, 0, 0, False)])
-                rows = [self.logits_local[0].clone()]
-                self._sample(1, self._gather_logits(1))
+                self._bind_rows(seqs, [SamplingParams(n, 0.0, 1.0, 0, 0, False)] * B)
+                rows = [self.logits_local[:B].clone()]
+                self._sample(B, self._gather_logits(B))
+                bucket = self._bucket(max(s.length for s in seqs) + n + 2)
                 for _ in range(n - 1):
-                    self._decode_step(1, self._bucket(seq.length + n + 2))
-                    rows.append(self.logits_local[0].clone())
-                toks = self.out_tokens[0, :n].clone()
+                    self._decode_step(B, bucket)
+                    rows.append(self.logits_local[:B].clone())
+                toks = self.out_tokens[:B, :n].clone()
             if self.on_gpu:
                 self.stream.synchronize()
-            return toks.cpu().tolist(), torch.stack(rows).float().cpu()
+            return toks.cpu().tolist(), torch.stack(rows, 1).float().cpu()
         finally:
-            self.free_sequence(seq)
+            for s in seqs:
+                self.free_sequence(s)
 
     def _finish(self, seqs, results) -> None:
         for s, r in zip(seqs, results):

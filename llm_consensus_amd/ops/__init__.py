@@ -16,7 +16,8 @@ from ..utils.native import kernels
 from . import oracle
 
 EPI_BF16, EPI_F32, EPI_RESADD, EPI_SILU, EPI_ROPE = 0, 1, 2, 3, 4
-GEMV_MAX_M = 4
+GEMV_MAX_M = 16      # decode rows on the weight-streaming path (VALU GEMV 1-2, MFMA form 3-16)
+MOE_GEMV_MAX_M = 4   # MoE: per-(row, expert) GEMVs up to this many rows, then the grouped GEMM
 
 
 def _p(t: Optional[torch.Tensor]) -> int:
@@ -69,11 +70,13 @@ def silu_mul_interleaved(gu: torch.Tensor, out: Optional[torch.Tensor] = None) -
 
 
 def linear(x: torch.Tensor, W: torch.Tensor, epi: int = EPI_BF16, out: Optional[torch.Tensor] = None,
-           norm_w: Optional[torch.Tensor] = None, eps: float = 1e-5) -> torch.Tensor:
+           norm_w: Optional[torch.Tensor] = None, eps: float = 1e-5, mfma: bool = False) -> torch.Tensor:
     """y = (rmsnorm(x)*norm_w if norm_w else x) @ W^T with a fused epilogue.
 
-    M <= 4 rows -> weight-streaming GEMV (decode; the norm runs in its prologue); larger M -> the
-    256x256 MFMA prefill GEMM (csrc/kernels/gemm.hip; a norm is a separate rmsnorm launch first).
+    M <= 16 rows -> weight streaming (decode; the norm runs in its prologue): the VALU GEMV for 1-2
+    rows, the MFMA form for 3-16 (``mfma`` pins the MFMA form at every row count: a batching
+    engine's decode stays batch-invariant); larger M -> the 256x256 MFMA prefill GEMM
+    (csrc/kernels/gemm.hip; a norm is a separate rmsnorm launch first).
     Epilogues: bf16 | f32 | EPI_RESADD (accumulates into ``out`` in place) | EPI_SILU (interleaved
     gate/up columns -> silu(g) * u, [M, N / 2]). One code path per shape class, all hand-written.
     """
@@ -90,8 +93,9 @@ def linear(x: torch.Tensor, W: torch.Tensor, epi: int = EPI_BF16, out: Optional[
             raise ValueError("EPI_RESADD needs out")
         n_out = N // 2 if epi == EPI_SILU else N
         out = torch.empty(M, n_out, dtype=torch.float32 if epi == EPI_F32 else torch.bfloat16, device=x.device)
-    if M <= GEMV_MAX_M:
-        kernels().gemv(M, _p(x), x.stride(0), _p(norm_w), float(eps), _p(W), _p(out), out.stride(0), N, K, epi, _s(x))
+    if M <= 4 or (M <= GEMV_MAX_M and K % 128 == 0 and x.stride(0) % 8 == 0):
+        kernels().gemv(M, _p(x), x.stride(0), _p(norm_w), float(eps), _p(W), _p(out), out.stride(0), N, K, epi,
+                       int(mfma), _s(x))
         return out
     if norm_w is not None:
         x = rmsnorm(x, norm_w, eps)
@@ -113,8 +117,8 @@ def gemm(x: torch.Tensor, W: torch.Tensor, epi: int = EPI_BF16, out: Optional[to
 
 
 def gemv(x: torch.Tensor, W: torch.Tensor, epi: int = EPI_BF16, out: Optional[torch.Tensor] = None,
-         norm_w: Optional[torch.Tensor] = None, eps: float = 1e-5) -> torch.Tensor:
-    """Always the GEMV path (M <= 4)."""
+         norm_w: Optional[torch.Tensor] = None, eps: float = 1e-5, mfma: bool = False) -> torch.Tensor:
+    """Always the weight-streaming path (M <= 16; the kernel library picks VALU / MFMA form)."""
     if not x.is_cuda:
         return oracle.linear(x, W, epi, out, norm_w, eps)
     M, K = x.shape
@@ -122,7 +126,23 @@ def gemv(x: torch.Tensor, W: torch.Tensor, epi: int = EPI_BF16, out: Optional[to
     if out is None:
         n_out = N // 2 if epi == EPI_SILU else N
         out = torch.empty(M, n_out, dtype=torch.float32 if epi == EPI_F32 else torch.bfloat16, device=x.device)
-    kernels().gemv(M, _p(x), x.stride(0), _p(norm_w), float(eps), _p(W), _p(out), out.stride(0), N, K, epi, _s(x))
+    kernels().gemv(M, _p(x), x.stride(0), _p(norm_w), float(eps), _p(W), _p(out), out.stride(0), N, K, epi, int(mfma),
+                   _s(x))
+    return out
+
+
+def gemvm(x: torch.Tensor, W: torch.Tensor, epi: int = EPI_BF16, out: Optional[torch.Tensor] = None,
+          norm_w: Optional[torch.Tensor] = None, eps: float = 1e-5) -> torch.Tensor:
+    """Always the MFMA weight-streaming form (gemv_mfma.hip; M <= 16) — tests / microbenchmarks
+    (``linear``/``gemv`` take it by themselves for 5 <= M <= 16)."""
+    if not x.is_cuda:
+        return oracle.linear(x, W, epi, out, norm_w, eps)
+    M, K = x.shape
+    N = W.shape[0]
+    if out is None:
+        n_out = N // 2 if epi == EPI_SILU else N
+        out = torch.empty(M, n_out, dtype=torch.float32 if epi == EPI_F32 else torch.bfloat16, device=x.device)
+    kernels().gemvm(M, _p(x), x.stride(0), _p(norm_w), float(eps), _p(W), _p(out), out.stride(0), N, K, epi, _s(x))
     return out
 
 
@@ -137,16 +157,22 @@ def rope_kv_write(qkv, positions, cos_t, sin_t, k_cache, v_cache, slots, nh, nkv
                             _p(k_cache), _p(v_cache), _p(slots), T, nh, nkv, D, bs, _s(qkv))
 
 
-def qkv_rope(x, W, norm_w, eps, q_out, k_cache, v_cache, positions, slots, cos_t, sin_t, nh, nkv, D, bs) -> None:
-    """Decode qkv projection: fused RMSNorm prologue + RoPE/KV-write epilogue (one launch)."""
+def qkv_rope(x, W, norm_w, eps, q_out, k_cache, v_cache, positions, slots, cos_t, sin_t, nh, nkv, D, bs,
+             mfma: bool = False) -> None:
+    """Decode qkv projection: fused RMSNorm prologue + RoPE/KV-write epilogue (one launch; form as
+    ``linear``)."""
     if not x.is_cuda:
         qkv = oracle.linear(x, W, EPI_BF16, None, norm_w, eps)
         oracle.rope_kv_write(qkv, positions, cos_t, sin_t, k_cache, v_cache, slots, nh, nkv, D, bs, q_out)
         return
     M, K = x.shape
+    if M > 4 and (K % 128 != 0 or x.stride(0) % 8 != 0):  # outside the MFMA decode form: prefill's path
+        qkv = linear(x, W, EPI_BF16, norm_w=norm_w, eps=eps)
+        rope_kv_write(qkv, positions, cos_t, sin_t, k_cache, v_cache, slots, nh, nkv, D, bs, q_out)
+        return
     kernels().gemv_qkv_rope(M, _p(x), x.stride(0), _p(norm_w), float(eps), _p(W), W.shape[0], K, _p(q_out),
                             q_out.stride(0), _p(k_cache), _p(v_cache), _p(positions), _p(slots), _p(cos_t), _p(sin_t),
-                            nh, nkv, D, bs, _s(x))
+                            nh, nkv, D, bs, int(mfma), _s(x))
 
 
 FUSED_ATTN_MAX_KEYS = 4096  # decode attention: fused single-launch form up to this bucket capacity

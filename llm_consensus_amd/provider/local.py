@@ -28,7 +28,7 @@ from typing import Dict, List, Optional
 
 from ..catalog import PROVIDER_LOCAL, ModelSpec
 from ..context import Context, ContextError
-from ..parallel.placement import ModelDemand, default_gpus, describe, solve
+from ..parallel.placement import HBM_BYTES, USABLE_FRACTION, ModelDemand, default_gpus, describe, solve
 from ..utils import trace as tracing
 from ..utils.tokenizer import tokenizer_for
 from .base import Request, Response, StreamCallback
@@ -36,6 +36,34 @@ from .base import Request, Response, StreamCallback
 DEFAULT_MAX_TOKENS = 4096
 RESPONDER_CONTEXT = 16384
 JUDGE_CONTEXT = 131072
+KV_BLOCK = 64  # tokens per paged-KV block (EngineConfig.block_size)
+
+
+def kv_pool_blocks(placement, specs, ctx: Dict[str, int], seqs: Dict[str, int],
+                   hbm_bytes: int = HBM_BYTES) -> Dict[str, int]:
+    """Paged-KV pool per engine, in blocks. An engine asks for ``seqs[m]`` full contexts (every live
+    sequence at max_context); when the engines of a GPU ask for more than its HBM left after their
+    weights, each gets a share proportional to its ask but never less than one full context (what
+    placement reserved). Sequences take blocks as they grow, so a pool smaller than the ask only
+    limits how many LONG sequences can be live at once (a request that cannot reserve its blocks
+    fails with an engine error) — e.g. 16 judge sessions at a 131k context would ask for 290 GB."""
+    free = {}
+    for m, gs in placement.gpus.items():
+        for g in gs:
+            free.setdefault(g, hbm_bytes * USABLE_FRACTION)
+            free[g] -= specs[m].config.weight_bytes() / len(gs)
+    per_tok = {m: specs[m].config.kv_bytes_per_token() / len(gs) for m, gs in placement.gpus.items()}
+    out = {}
+    for m, gs in placement.gpus.items():
+        ask = seqs[m] * ctx[m] * per_tok[m]
+        floor = ctx[m] * per_tok[m]
+        scale = 1.0
+        for g in gs:
+            asks = sum(seqs[o] * ctx[o] * per_tok[o] for o, og in placement.gpus.items() if g in og)
+            scale = min(scale, max(0.0, free[g]) / asks if asks > 0 else 1.0)
+        tokens = max(floor, ask * min(1.0, scale)) / per_tok[m] if per_tok[m] else ctx[m] * seqs[m]
+        out[m] = int(tokens) // KV_BLOCK + 2 * seqs[m] + 2
+    return out
 
 
 class LocalError(Exception):
@@ -153,19 +181,27 @@ class LocalBackend:
         self.workers: Dict[int, _Worker] = {}
         from ..runtime.worker import worker_main
 
+        conc = max(1, concurrency)
+        seqs = {}
+        for m in self.placement.gpus:
+            # responder rows: one per --models entry per request in flight; a judge-only engine
+            # needs a session per request (and a row for plain queries)
+            n = (counts or {}).get(m, 0 if m == judge else 1) * conc
+            sess = conc if m == judge else 0
+            seqs[m] = (n, sess)
+        kv_blocks = kv_pool_blocks(self.placement, self.specs, self._ctx,
+                                   {m: max(1, n) + sess for m, (n, sess) in seqs.items()})
         for g in used:
             models = []
             for m, gs in self.placement.gpus.items():
                 if g in gs:
                     s = self.specs[m]
-                    conc = max(1, concurrency)
-                    # responder rows: one per --models entry per request in flight; a judge-only
-                    # engine needs a session per request (and a row for plain queries)
-                    n = (counts or {}).get(m, 0 if m == judge else 1) * conc
-                    sess = conc if m == judge else 0
+                    n, sess = seqs[m]
                     models.append({"name": m, "family": s.family, "seed": s.seed, "max_context": self._ctx[m],
-                                   "checkpoint": s.config.checkpoint,
-                                   "max_batch": max(1, min(4, max(n, sess))),
+                                   "checkpoint": s.config.checkpoint, "kv_blocks": kv_blocks[m],
+                                   # decode rows per step: up to 16 on the weight-streaming
+                                   # GEMV / MFMA form; MoE keeps 4 (per-(row, expert) GEMVs)
+                                   "max_batch": max(1, min(4 if s.config.is_moe else 16, max(n, sess))),
                                    "max_seqs": max(1, n) + sess})
             if groups:
                 dist_info = {"port": port, "rank": rank_of[g], "world": len(used),

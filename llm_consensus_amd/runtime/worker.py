@@ -440,6 +440,7 @@ def worker_main(gpu: int, conn, models: List[dict], dist_info: Optional[dict], t
             graphs = tp.size == 1 or tp.custom is not None or (not on_cpu and tp.graph_capture_ok(f"cuda:{gpu}"))
             ecfg = EngineConfig(device="cpu" if on_cpu else f"cuda:{gpu}", max_context=m["max_context"],
                                 max_batch=m.get("max_batch", 1), max_seqs=m.get("max_seqs", 0), seed=m["seed"],
+                                kv_blocks=m.get("kv_blocks", 0),
                                 use_graphs=graphs,
                                 # MoE under TP: whole experts per rank (LLMC_EXPERT_PARALLEL=1)
                                 expert_parallel=os.environ.get("LLMC_EXPERT_PARALLEL", "0") == "1")

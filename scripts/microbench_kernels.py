@@ -135,6 +135,39 @@ def bench_gemv_sweep(shapes=None):
         print(f"sweep N={N} K={K} ({N * K * 2 / 1e6:.0f} MB, {copies} copies): " + "  ".join(res), flush=True)
 
 
+def bench_batched_decode(shapes=None, rows=(1, 2, 3, 4, 5, 8, 12, 16)):
+    """Batched decode projections on COLD weights: the dispatcher's form per row count (VALU GEMV
+    for M <= 2, MFMA form 3-16) and the MFMA form forced at every M, with the fused norm prologue
+    where the layer has one (qkv, gate_up, lm_head) and the residual add elsewhere."""
+    from llm_consensus_amd import ops
+
+    for (N, K, epi, norm) in shapes or [(6144, 4096, 0, True), (4096, 4096, 2, False), (28672, 4096, 3, True),
+                                        (4096, 14336, 2, False), (128256, 4096, 1, True)]:
+        copies = max(2, (1 << 30) // (N * K * 2))
+        Ws = [(torch.randn(N, K, device="cuda") * 0.02).to(BF) for _ in range(copies)]
+        nw = torch.ones(K, dtype=BF, device="cuda") if norm else None
+        line = []
+        for M in rows:
+            x = torch.randn(M, K, device="cuda").to(BF)
+            n_out = N // 2 if epi == 3 else N
+            out = torch.zeros(M, n_out, dtype=torch.float32 if epi == 1 else BF, device="cuda")
+            t = {}
+            for form, fn in (("auto", ops.linear), ("mfma", ops.gemvm)):
+                if form == "mfma" and M > 2 and "auto" in t:
+                    continue  # the dispatcher already ran the MFMA form
+
+                def run():
+                    for W in Ws:
+                        fn(x, W, epi, out=out, norm_w=nw)
+                t[form] = timeit(run, iters=2, warm=1) / copies
+            tbs = N * K * 2 / t["auto"] / 1e6
+            extra = f"/{t['mfma']:.2f}" if "mfma" in t else ""
+            line.append(f"M={M} {t['auto']:6.2f}{extra} ({tbs:4.2f} TB/s)")
+        del Ws
+        torch.cuda.empty_cache()
+        print(f"batched N={N} K={K} epi={epi}{' +norm' if norm else ''}: " + "  ".join(line), flush=True)
+
+
 def bench_qkv_rope():
     """qkv GEMV with the RoPE + paged-KV-write epilogue vs the same GEMV with a plain bf16
     epilogue (both with the fused RMSNorm prologue), cold weights: what the epilogue costs."""
@@ -225,6 +258,8 @@ if __name__ == "__main__":
         bench_gemv_sweep([(768, 4096), (1536, 4096), (3584, 4096), (4096, 512), (4096, 1792)])
     if what in ("sweep-70b-tp4",):  # one TP=4 rank of Llama-3-70B: qkv, gate_up, o, down
         bench_gemv_sweep([(2560, 8192), (14336, 8192), (8192, 2048), (8192, 7168)])
+    if what in ("batched",):  # decode projections at continuous-batching row counts
+        bench_batched_decode()
     if what in ("qkv-rope",):
         bench_qkv_rope()
     if what in ("prefill",):

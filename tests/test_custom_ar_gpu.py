@@ -105,7 +105,8 @@ def test_custom_allreduce_ipc(cuda, world):
 
 def _rowpar_worker(rank, world, port, q):
     """EPI_AR: the row-parallel GEMV with its all-reduce in the epilogue must give exactly the bits
-    of GEMV (rank 0 residual-folded) + separate custom all-reduce, eagerly and from a HIP graph."""
+    of GEMV (rank 0 residual-folded) + separate custom all-reduce, eagerly and from a HIP graph
+    (1-2 rows; 3-4 rows within bf16 tolerance: the separate path's projection is the MFMA form)."""
     try:
         import torch.distributed as dist
 
@@ -134,7 +135,11 @@ def _rowpar_worker(rank, world, port, q):
                 got = h0.clone()
                 rp.gemv_rowpar_ar(x, W, got)
                 torch.cuda.synchronize()
-                errs.append(int((got != ref).sum()))
+                if M <= 2:  # same VALU GEMV form on both sides: bit-exact
+                    errs.append(int((got != ref).sum()))
+                else:  # ops.linear takes the MFMA form from 3 rows on (EPI_AR stays on the VALU GEMV)
+                    d = (got.float() - ref.float()).abs()
+                    errs.append(int((d > 2e-2 + 2e-2 * ref.float().abs()).sum()))
         # graph replay with changing inputs
         M, N, K = 1, 1024, 512
         x = torch.zeros(M, K, dtype=torch.bfloat16, device="cuda")

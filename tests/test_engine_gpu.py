@@ -103,6 +103,29 @@ def test_batched_rows_equal_single(cuda):
     assert both[0] == one and both[1] == two
 
 
+@pytest.mark.parametrize("name,B", [("llama-tiny", 8), ("phi3-tiny", 16), ("llama-small", 5)])
+def test_batched_decode_rows_match_oracle(cuda, name, B):
+    """Continuous batching past 4 rows (the MFMA decode form): B different prompts decoded in ONE
+    batch, teacher-forced at every step against the CPU oracle's prefill of each row's prompt +
+    tokens so far (fused norm / RoPE / KV-write / SiLU / residual epilogues at M = B)."""
+    cfg, ecpu, egpu = _pair(name, max_batch=16)
+    prompts = [[(i * (53 + 2 * r)) % (cfg.vocab - 300) + 256 for i in range(20 + 3 * r)] for r in range(B)]
+    n = 5
+    toks, lg = egpu.debug_decode_logits_batch(prompts, n)
+    assert lg.shape == (B, n, cfg.vocab)
+    for r in range(B):
+        for i in range(n):
+            s = ecpu.new_sequence()
+            ecpu.prefill([s], [prompts[r] + toks[r][:i]])
+            lc = s.logits.float()
+            ecpu.free_sequence(s)
+            err = (lc - lg[r, i]).abs().max().item()
+            assert err < 0.03 * max(1.0, lc.abs().max().item()), (r, i, err)
+            top2 = torch.topk(lc, 2).values
+            if (top2[0] - top2[1]).item() > 2 * err:
+                assert int(lc.argmax()) == toks[r][i], (r, i)
+
+
 def test_topk_topp_decode(cuda):
     cfg = FAMILIES["llama-tiny"]
     e = Engine(cfg, EngineConfig(device="cuda:0", max_context=512, seed=1))

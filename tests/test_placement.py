@@ -66,3 +66,29 @@ def test_tp_larger_than_node_and_no_gpus():
         solve([ModelDemand("llama-3-70b", W70B, 0, tp=8)], list(range(4)))
     with pytest.raises(PlacementError, match="no GPUs"):
         solve([ModelDemand("x", 1, 0)], [])
+
+
+def test_kv_pool_blocks_fit_the_gpu():
+    """16 requests in flight on one GPU: 2 x 8B responders (16 rows each) + an 8B judge (17
+    sessions at a 131k context would ask for ~290 GB of KV): every pool shrinks to the GPU's HBM
+    left after the weights, pro rata, never below one full context; small asks stay whole."""
+    from llm_consensus_amd.catalog import resolve as resolve_model
+    from llm_consensus_amd.parallel.placement import HBM_BYTES, USABLE_FRACTION, Placement
+    from llm_consensus_amd.provider.local import JUDGE_CONTEXT, KV_BLOCK, RESPONDER_CONTEXT, kv_pool_blocks
+
+    names = ["llama-3-8b@0", "llama-3-8b@1", "llama-3-8b@judge"]
+    specs = {n: resolve_model(n) for n in names}
+    ctx = {"llama-3-8b@0": RESPONDER_CONTEXT, "llama-3-8b@1": RESPONDER_CONTEXT, "llama-3-8b@judge": JUDGE_CONTEXT}
+    pl = Placement({n: [0] for n in names})
+    seqs = {"llama-3-8b@0": 16, "llama-3-8b@1": 16, "llama-3-8b@judge": 17}
+    blocks = kv_pool_blocks(pl, specs, ctx, seqs)
+    per_tok = specs["llama-3-8b@0"].config.kv_bytes_per_token()
+    weights = sum(specs[n].config.weight_bytes() for n in names)
+    kv = sum(b * KV_BLOCK * per_tok for b in blocks.values())
+    assert weights + kv <= HBM_BYTES * USABLE_FRACTION * 1.01
+    for n in names:
+        assert blocks[n] * KV_BLOCK >= ctx[n]  # at least one full context
+    assert blocks["llama-3-8b@judge"] < seqs["llama-3-8b@judge"] * JUDGE_CONTEXT // KV_BLOCK
+    # one request in flight: the asks fit, every engine gets all it asked for
+    one = kv_pool_blocks(pl, specs, ctx, {"llama-3-8b@0": 1, "llama-3-8b@1": 1, "llama-3-8b@judge": 2})
+    assert one["llama-3-8b@judge"] * KV_BLOCK >= 2 * JUDGE_CONTEXT

@@ -21,7 +21,7 @@ int llmc_rmsnorm(const void*, const void*, void*, int, int, int, int, float, hip
 int llmc_embedding(const void*, const void*, void*, int, int, int, hipStream_t);
 int llmc_silu_mul_interleaved(const void*, void*, int, int, hipStream_t);
 int llmc_gemv(int, const void*, int, const void*, float, const void*, void*, int, int, int, int, int, hipStream_t);
-int llmc_gemvm(int, const void*, int, const void*, float, const void*, void*, int, int, int, int, hipStream_t);
+int llmc_gemvm(int, const void*, int, const void*, float, const void*, void*, int, int, int, int, int, hipStream_t);
 int llmc_gemm(const void*, int, const void*, int, void*, int, int, int, int, int, hipStream_t);
 int llmc_rope_kv_write(const void*, int, void*, int, const void*, const void*, const void*, void*, void*, const void*,
                        int, int, int, int, int, hipStream_t);
@@ -91,8 +91,9 @@ PYBIND11_MODULE(_llmc_hip, m) {
                    ptr s) {
     check(llmc_gemv(M, P(x), xs, P(nw), eps, P(W), P(out), os, N, K, epi, mfma, S(s)), "gemv");
   });
-  m.def("gemvm", [](int M, ptr x, int xs, ptr nw, float eps, ptr W, ptr out, int os, int N, int K, int epi, ptr s) {
-    check(llmc_gemvm(M, P(x), xs, P(nw), eps, P(W), P(out), os, N, K, epi, S(s)), "gemvm");
+  m.def("gemvm", [](int M, ptr x, int xs, ptr nw, float eps, ptr W, ptr out, int os, int N, int K, int epi, int form,
+                    ptr s) {
+    check(llmc_gemvm(M, P(x), xs, P(nw), eps, P(W), P(out), os, N, K, epi, form, S(s)), "gemvm");
   });
   m.def("gemm", [](ptr A, int lda, ptr W, int ldw, ptr C, int ldc, int M, int N, int K, int epi, ptr s) {
     check(llmc_gemm(P(A), lda, P(W), ldw, P(C), ldc, M, N, K, epi, S(s)), "gemm");

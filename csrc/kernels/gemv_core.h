@@ -61,7 +61,7 @@ struct ArEpi {
 // This kernel serves M <= kGemvMaxM (and M <= 4 when K is not a multiple of 128).
 constexpr int kGemvMaxM = 2, kGemvmMaxM = 16;
 int gemvm_dispatch(int M, const void* x, int x_stride, const void* norm_w, float eps, const void* W, void* out,
-                   int out_stride, int N, int K, int epi, const RopeEpi& rope, hipStream_t st);
+                   int out_stride, int N, int K, int epi, const RopeEpi& rope, hipStream_t st, int form = 0);
 
 template <int M, int NT, int RPW, int UNROLL, int PRO, int EPI, bool EXPERT = false>
 __global__ __launch_bounds__(NT) void gemv_kernel(const bf16_t* __restrict__ x, int x_stride,

@@ -25,112 +25,12 @@
 
 namespace llmc {
 
-template <int S, int PRO, int EPI>
-__global__ __launch_bounds__(S * 64) void gemvm_kernel(const bf16_t* __restrict__ x, int x_stride,
-                                                       const bf16_t* __restrict__ norm_w, float eps,
-                                                       const bf16_t* __restrict__ W, void* __restrict__ out,
-                                                       int out_stride, int M, int N, int K, RopeEpi rope) {
-  constexpr int TK = 128;  // k per tile: 16 rows x 256 B = one LDS bank row per weight row
-  __shared__ __attribute__((aligned(16))) char wt[S][16 * TK * 2];  // per-wave transposition tile
-  __shared__ f32x4 red[S][64];
-  __shared__ float ssr[S][16];
-  const int tid = threadIdx.x, lane = tid & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int r = lane & 15, g = lane >> 4;
-  const int n0 = blockIdx.x * 16;
-  const int ntile = K / TK / S;  // tiles of this wave (host: K % (TK * S) == 0)
-  const int kw = wave * ntile * TK;
-  // weight tile loads: instruction i covers rows 4i + lane/16, 16-B chunk lane%16 — four whole
-  // 256-B row segments per instruction (the MFMA fragment order, 16 rows x 64 B per instruction,
-  // measured 1.35x slower on the same bytes)
-  const u32x4* wsrc[4];
-#pragma unroll
-  for (int i = 0; i < 4; ++i)
-    wsrc[i] = reinterpret_cast<const u32x4*>(W + static_cast<int64_t>(min(n0 + 4 * i + g, N - 1)) * K + kw + r * 8);
-  const u32x4* xp = reinterpret_cast<const u32x4*>(x + static_cast<int64_t>(min(r, M - 1)) * x_stride + kw + g * 8);
-  const u32x4* gp = reinterpret_cast<const u32x4*>(norm_w + kw + g * 8);  // PRO_NORM only
-  char* tile = wt[wave];
-
-  // one tile = 4 weight loads + 4 x fragments (k-steps of 32: lane (r, g) holds x[r][32j + 8g ..])
-  auto issue = [&](u32x4 (&wv)[4], u32x4 (&xv)[4], u32x4 (&gv)[4], int t) {
-    const int tu = min(t, ntile - 1) * (TK / 8);  // 16-B units
-#pragma unroll
-    for (int i = 0; i < 4; ++i) wv[i] = load16<true>(wsrc[i] + tu);
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      xv[j] = xp[tu + 4 * j];
-      if constexpr (PRO == PRO_NORM) gv[j] = gp[tu + 4 * j];
-    }
-  };
-  f32x4 acc = {0.f, 0.f, 0.f, 0.f};
-  float ss = 0.f;
-  auto consume = [&](const u32x4 (&wv)[4], const u32x4 (&xv)[4], const u32x4 (&gv)[4]) {
-    // row-major tile -> this wave's LDS (chunk c of row q at slot c ^ q: the b128 write groups of
-    // 8 lanes and the 4 fragment-read groups are conflict-free) -> A fragments (row r, chunk 4j + g)
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int q = 4 * i + g;
-      *reinterpret_cast<u32x4*>(tile + q * 256 + ((r ^ q) << 4)) = wv[i];
-    }
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const u32x4 a = *reinterpret_cast<const u32x4*>(tile + r * 256 + (((4 * j + g) ^ r) << 4));
-      u32x4 xb = xv[j];
-      if constexpr (PRO == PRO_NORM) {
-        float f[8], w8[8];
-        unpack8(xv[j], f);
-        unpack8(gv[j], w8);
-#pragma unroll
-        for (int e = 0; e < 8; ++e) {
-          ss += f[e] * f[e];
-          f[e] *= w8[e];
-        }
-        xb = pack8(f);
-      }
-      acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, a), __builtin_bit_cast(bf16x8, xb), acc,
-                                                    0, 0, 0);
-    }
-  };
-  u32x4 wc[4], xc[4], gc[4];
-  issue(wc, xc, gc, 0);
-  for (int t = 0; t + 1 < ntile; ++t) {
-    u32x4 wn[4], xn[4], gn[4];
-    issue(wn, xn, gn, t + 1);
-    consume(wc, xc, gc);
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      wc[i] = wn[i];
-      xc[i] = xn[i];
-      if constexpr (PRO == PRO_NORM) gc[i] = gn[i];
-    }
-  }
-  consume(wc, xc, gc);
-
-  // ---- split-K reduction over the block's waves ----
-  red[wave][lane] = acc;
-  if constexpr (PRO == PRO_NORM) {
-    ss += __shfl_xor(ss, 16, 64);
-    ss += __shfl_xor(ss, 32, 64);
-    if (g == 0) ssr[wave][r] = ss;
-  }
-  __syncthreads();
-  if (wave != 0) return;
-  f32x4 v = red[0][lane];
-#pragma unroll
-  for (int w = 1; w < S; ++w) v += red[w][lane];
-  const int m = r;
-  if (m >= M) return;
-  if constexpr (PRO == PRO_NORM) {
-    float t = 0.f;
-#pragma unroll
-    for (int w = 0; w < S; ++w) t += ssr[w][m];
-    v *= rsqrtf(t / K + eps);
-  }
-  const int nb = n0 + 4 * g;  // this lane's rows nb .. nb + 3 of token m
+// Fused epilogue of one lane: rows nb .. nb + 3 (f32 accumulators v) of token m.
+template <int EPI>
+__device__ __forceinline__ void gemvm_epilogue(const f32x4& v, int nb, int m, int N, void* __restrict__ out,
+                                               int out_stride, const RopeEpi& rope) {
   if (nb >= N) return;
   const bool full = nb + 3 < N;
-
-  // ---- fused epilogue ----
   if constexpr (EPI == EPI_F32) {
     float* o = reinterpret_cast<float*>(out) + static_cast<int64_t>(m) * out_stride + nb;
     if (full && (out_stride % 4 == 0)) {
@@ -203,12 +103,160 @@ __global__ __launch_bounds__(S * 64) void gemvm_kernel(const bf16_t* __restrict_
   }
 }
 
-template <int S, int PRO, int EPI>
+
+template <int S, int RB, int XL, int PRO, int EPI>
+__global__ __launch_bounds__(S * 64) void gemvm_kernel(const bf16_t* __restrict__ x, int x_stride,
+                                                       const bf16_t* __restrict__ norm_w, float eps,
+                                                       const bf16_t* __restrict__ W, void* __restrict__ out,
+                                                       int out_stride, int M, int N, int K, RopeEpi rope) {
+  constexpr int TK = 128;       // k per tile: one 256-B LDS bank row per matrix row
+  constexpr int WR = 16 * RB;   // weight rows per block (RB 16-row groups share every x fragment)
+  constexpr int TB = 16 * TK * 2;
+  // per-wave transposition tiles: RB weight row groups (+ the 16 token rows of x when XL)
+  __shared__ __attribute__((aligned(16))) char lds_t[S][(RB + XL) * TB];
+  __shared__ f32x4 red[S][RB][64];
+  __shared__ float ssr[S][16];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int r = lane & 15, g = lane >> 4;
+  const int n0 = blockIdx.x * WR;
+  const int ntile = K / TK / S;  // tiles of this wave (host: K % (TK * S) == 0)
+  const int kw = wave * ntile * TK;
+  // tile loads: instruction i covers rows 4i + lane/16, 16-B chunk lane%16 — four whole 256-B
+  // row segments per instruction (the MFMA fragment order, 16 rows x 64 B per instruction, streamed
+  // the same weight bytes 1.35x slower; x, L2-resident, the same way)
+  const u32x4* wsrc[4 * RB];
+#pragma unroll
+  for (int i = 0; i < 4 * RB; ++i)
+    wsrc[i] = reinterpret_cast<const u32x4*>(W + static_cast<int64_t>(min(n0 + 4 * i + g, N - 1)) * K + kw + r * 8);
+  // x: XL = 1 -> row-contiguous loads transposed through LDS like the weights; XL = 0 -> the B
+  // fragments straight from L2 (lane (r, g) loads x[r][32j + 8g ..]; few distinct token rows are
+  // mostly broadcasts, cheaper than the LDS round trip)
+  const u32x4* xsrc[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+    xsrc[i] = XL ? reinterpret_cast<const u32x4*>(x + static_cast<int64_t>(min(4 * i + g, M - 1)) * x_stride + kw + r * 8)
+                 : reinterpret_cast<const u32x4*>(x + static_cast<int64_t>(min(r, M - 1)) * x_stride + kw + g * 8) + 4 * i;
+  const u32x4* gp = reinterpret_cast<const u32x4*>(norm_w + kw + g * 8);  // PRO_NORM only
+  char* tw = lds_t[wave];
+  char* tx = tw + RB * TB;
+
+  auto issue = [&](u32x4 (&wv)[4 * RB], u32x4 (&xv)[4], u32x4 (&gv)[4], int t) {
+    const int tu = min(t, ntile - 1) * (TK / 8);  // 16-B units
+#pragma unroll
+    for (int i = 0; i < 4 * RB; ++i) wv[i] = load16<true>(wsrc[i] + tu);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) xv[i] = XL ? xsrc[i][tu] : xsrc[0][tu + 4 * i];
+    if constexpr (PRO == PRO_NORM) {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) gv[j] = gp[tu + 4 * j];
+    }
+  };
+  f32x4 acc[RB];
+#pragma unroll
+  for (int b = 0; b < RB; ++b) acc[b] = f32x4{0.f, 0.f, 0.f, 0.f};
+  float ss = 0.f;
+  // row-major tiles -> this wave's LDS (chunk c of row q at 16-B slot c ^ q: conflict-free for the
+  // 8-lane b128 write groups and the four 16-lane fragment-read groups) -> fragments (row r,
+  // chunk 4j + g): A = weights of each row group, B = x (normalised on the way when PRO_NORM)
+  auto consume = [&](const u32x4 (&wv)[4 * RB], const u32x4 (&xv)[4], const u32x4 (&gv)[4]) {
+#pragma unroll
+    for (int i = 0; i < 4 * RB; ++i) {
+      const int q = 4 * i + g;  // weight row within the block
+      *reinterpret_cast<u32x4*>(tw + (q >> 4) * TB + (q & 15) * 256 + ((r ^ (q & 15)) << 4)) = wv[i];
+    }
+    if constexpr (XL) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int q = 4 * i + g;
+        *reinterpret_cast<u32x4*>(tx + q * 256 + ((r ^ q) << 4)) = xv[i];
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int slot = ((4 * j + g) ^ r) << 4;
+      u32x4 xb = XL ? *reinterpret_cast<const u32x4*>(tx + r * 256 + slot) : xv[j];
+      if constexpr (PRO == PRO_NORM) {
+        float f[8], w8[8];
+        unpack8(xb, f);
+        unpack8(gv[j], w8);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          ss += f[e] * f[e];
+          f[e] *= w8[e];
+        }
+        xb = pack8(f);
+      }
+#pragma unroll
+      for (int b = 0; b < RB; ++b) {
+        const u32x4 a = *reinterpret_cast<const u32x4*>(tw + b * TB + r * 256 + slot);
+        acc[b] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, a), __builtin_bit_cast(bf16x8, xb),
+                                                         acc[b], 0, 0, 0);
+      }
+    }
+  };
+  u32x4 wc[4 * RB], xc[4], gc[4];
+  issue(wc, xc, gc, 0);
+  for (int t = 0; t + 1 < ntile; ++t) {
+    u32x4 wn[4 * RB], xn[4], gn[4];
+    issue(wn, xn, gn, t + 1);
+    consume(wc, xc, gc);
+#pragma unroll
+    for (int i = 0; i < 4 * RB; ++i) wc[i] = wn[i];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      xc[i] = xn[i];
+      if constexpr (PRO == PRO_NORM) gc[i] = gn[i];
+    }
+  }
+  consume(wc, xc, gc);
+
+  // ---- split-K reduction over the block's waves ----
+#pragma unroll
+  for (int b = 0; b < RB; ++b) red[wave][b][lane] = acc[b];
+  if constexpr (PRO == PRO_NORM) {
+    ss += __shfl_xor(ss, 16, 64);
+    ss += __shfl_xor(ss, 32, 64);
+    if (g == 0) ssr[wave][r] = ss;
+  }
+  __syncthreads();
+  if (wave != 0) return;
+  const int m = r;
+  if (m >= M) return;
+  float inv = 1.f;
+  if constexpr (PRO == PRO_NORM) {
+    float t = 0.f;
+#pragma unroll
+    for (int w = 0; w < S; ++w) t += ssr[w][m];
+    inv = rsqrtf(t / K + eps);
+  }
+#pragma unroll
+  for (int b = 0; b < RB; ++b) {
+    f32x4 v = red[0][b][lane];
+#pragma unroll
+    for (int w = 1; w < S; ++w) v += red[w][b][lane];
+    if constexpr (PRO == PRO_NORM) v *= inv;
+    gemvm_epilogue<EPI>(v, n0 + 16 * b + 4 * g, m, N, out, out_stride, rope);
+  }
+}
+
+// Form per shape (profiles/r2_batched_decode.md, `microbench_kernels.py gemvm-forms`): two 16-row
+// weight groups per wave from 6144 output rows (8B qkv / gate_up / lm_head: 3-8 % faster; the
+// 4096-row o_proj / down lose 25-45 % with half the blocks), x through LDS once the distinct token
+// rows make its fragment loads cost (12+ rows; 8+ with one group per wave).
+static int gemvm_form(int M, int N, int K) {
+  (void)K;
+  const bool rb2 = N >= 6144;
+  const bool xl = rb2 ? M >= 12 : M >= 8;
+  return 1 + (xl ? 1 : 0) + (rb2 ? 2 : 0);
+}
+
+template <int S, int RB, int XL, int PRO, int EPI>
 static int launch_gemvm_s(const void* x, int x_stride, const void* nw, float eps, const void* W, void* out,
                           int out_stride, int M, int N, int K, const RopeEpi& rope, hipStream_t st) {
-  const int grid = (N + 15) / 16;
-  gemvm_kernel<S, PRO, EPI><<<grid, S * 64, 0, st>>>((const bf16_t*)x, x_stride, (const bf16_t*)nw, eps,
-                                                     (const bf16_t*)W, out, out_stride, M, N, K, rope);
+  const int grid = (N + 16 * RB - 1) / (16 * RB);
+  gemvm_kernel<S, RB, XL, PRO, EPI><<<grid, S * 64, 0, st>>>((const bf16_t*)x, x_stride, (const bf16_t*)nw, eps,
+                                                             (const bf16_t*)W, out, out_stride, M, N, K, rope);
   return static_cast<int>(hipGetLastError());
 }
 
@@ -216,8 +264,8 @@ static int launch_gemvm_s(const void* x, int x_stride, const void* nw, float eps
 // keeps >= 2 tiles of 128 k (one in flight behind the one it computes) and the tiles divide
 // evenly (at least 4 waves when K allows it; at most 8: 16 x 64 threads would cap a lane at 128
 // VGPRs and spill).
-static int pick_split(int N, int K) {
-  const int blocks = (N + 15) / 16, tiles = K / 128;
+static int pick_split(int blocks, int K) {
+  const int tiles = K / 128;
   int S = 1;
   while (S < 8 && tiles % (2 * S) == 0 &&
          (S < 4 || (static_cast<long>(blocks) * S < 2048 && tiles / (2 * S) >= 2)))
@@ -225,27 +273,42 @@ static int pick_split(int N, int K) {
   return S;
 }
 
+template <int RB, int XL, int PRO, int EPI>
+static int launch_gemvm_rb(const void* x, int x_stride, const void* nw, float eps, const void* W, void* out,
+                           int out_stride, int M, int N, int K, const RopeEpi& rope, hipStream_t st) {
+  switch (pick_split((N + 16 * RB - 1) / (16 * RB), K)) {
+    case 1: return launch_gemvm_s<1, RB, XL, PRO, EPI>(x, x_stride, nw, eps, W, out, out_stride, M, N, K, rope, st);
+    case 2: return launch_gemvm_s<2, RB, XL, PRO, EPI>(x, x_stride, nw, eps, W, out, out_stride, M, N, K, rope, st);
+    case 4: return launch_gemvm_s<4, RB, XL, PRO, EPI>(x, x_stride, nw, eps, W, out, out_stride, M, N, K, rope, st);
+    case 8: return launch_gemvm_s<8, RB, XL, PRO, EPI>(x, x_stride, nw, eps, W, out, out_stride, M, N, K, rope, st);
+    default: return -1;
+  }
+}
+
+// form: 0 = by shape (below); 1-4 = (row groups, x path) = (1, L2), (1, LDS), (2, L2), (2, LDS)
+// (microbenchmarks / tests pin one)
 template <int PRO, int EPI>
 static int launch_gemvm(const void* x, int x_stride, const void* nw, float eps, const void* W, void* out,
-                        int out_stride, int M, int N, int K, const RopeEpi& rope, hipStream_t st) {
-  switch (pick_split(N, K)) {
-    case 1: return launch_gemvm_s<1, PRO, EPI>(x, x_stride, nw, eps, W, out, out_stride, M, N, K, rope, st);
-    case 2: return launch_gemvm_s<2, PRO, EPI>(x, x_stride, nw, eps, W, out, out_stride, M, N, K, rope, st);
-    case 4: return launch_gemvm_s<4, PRO, EPI>(x, x_stride, nw, eps, W, out, out_stride, M, N, K, rope, st);
-    case 8: return launch_gemvm_s<8, PRO, EPI>(x, x_stride, nw, eps, W, out, out_stride, M, N, K, rope, st);
+                        int out_stride, int M, int N, int K, const RopeEpi& rope, int form, hipStream_t st) {
+  if (form == 0) form = gemvm_form(M, N, K);
+  switch (form) {
+    case 1: return launch_gemvm_rb<1, 0, PRO, EPI>(x, x_stride, nw, eps, W, out, out_stride, M, N, K, rope, st);
+    case 2: return launch_gemvm_rb<1, 1, PRO, EPI>(x, x_stride, nw, eps, W, out, out_stride, M, N, K, rope, st);
+    case 3: return launch_gemvm_rb<2, 0, PRO, EPI>(x, x_stride, nw, eps, W, out, out_stride, M, N, K, rope, st);
+    case 4: return launch_gemvm_rb<2, 1, PRO, EPI>(x, x_stride, nw, eps, W, out, out_stride, M, N, K, rope, st);
     default: return -1;
   }
 }
 
 int gemvm_dispatch(int M, const void* x, int x_stride, const void* norm_w, float eps, const void* W, void* out,
-                   int out_stride, int N, int K, int epi, const RopeEpi& rope, hipStream_t st) {
+                   int out_stride, int N, int K, int epi, const RopeEpi& rope, hipStream_t st, int form) {
   if (M < 1 || M > kGemvmMaxM || K % 128 != 0 || x_stride % 8 != 0) return -1;
   if ((epi == EPI_SILU || epi == EPI_ROPE) && N % 4 != 0) return -1;
   const bool norm = norm_w != nullptr;
 #define LLMC_GEMVM_CASE(E)                                                                                    \
   case E:                                                                                                     \
-    return norm ? launch_gemvm<PRO_NORM, E>(x, x_stride, norm_w, eps, W, out, out_stride, M, N, K, rope, st) \
-                : launch_gemvm<PRO_NONE, E>(x, x_stride, norm_w, eps, W, out, out_stride, M, N, K, rope, st);
+    return norm ? launch_gemvm<PRO_NORM, E>(x, x_stride, norm_w, eps, W, out, out_stride, M, N, K, rope, form, st) \
+                : launch_gemvm<PRO_NONE, E>(x, x_stride, norm_w, eps, W, out, out_stride, M, N, K, rope, form, st);
   switch (epi) {
     LLMC_GEMVM_CASE(EPI_BF16)
     LLMC_GEMVM_CASE(EPI_F32)
@@ -253,7 +316,7 @@ int gemvm_dispatch(int M, const void* x, int x_stride, const void* norm_w, float
     LLMC_GEMVM_CASE(EPI_SILU)
     case EPI_ROPE:
       if (!norm) return -5;
-      return launch_gemvm<PRO_NORM, EPI_ROPE>(x, x_stride, norm_w, eps, W, out, out_stride, M, N, K, rope, st);
+      return launch_gemvm<PRO_NORM, EPI_ROPE>(x, x_stride, norm_w, eps, W, out, out_stride, M, N, K, rope, form, st);
     default: return -4;
   }
 #undef LLMC_GEMVM_CASE
@@ -263,9 +326,8 @@ int gemvm_dispatch(int M, const void* x, int x_stride, const void* norm_w, float
 
 // Direct entry (tests / microbenchmarks: the MFMA form at any M <= 16).
 extern "C" int llmc_gemvm(int M, const void* x, int x_stride, const void* norm_w, float eps, const void* W, void* out,
-                          int out_stride, int N, int K, int epi, hipStream_t s) {
+                          int out_stride, int N, int K, int epi, int form, hipStream_t s) {
   if (epi == llmc::EPI_ROPE) return -5;
   llmc::RopeEpi rope{};
-  return llmc::gemvm_dispatch(M, x, x_stride, norm_w, eps, W, out, out_stride, N, K, epi, rope, s);
+  return llmc::gemvm_dispatch(M, x, x_stride, norm_w, eps, W, out, out_stride, N, K, epi, rope, s, form);
 }
-

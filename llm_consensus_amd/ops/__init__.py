@@ -132,9 +132,10 @@ def gemv(x: torch.Tensor, W: torch.Tensor, epi: int = EPI_BF16, out: Optional[to
 
 
 def gemvm(x: torch.Tensor, W: torch.Tensor, epi: int = EPI_BF16, out: Optional[torch.Tensor] = None,
-          norm_w: Optional[torch.Tensor] = None, eps: float = 1e-5) -> torch.Tensor:
+          norm_w: Optional[torch.Tensor] = None, eps: float = 1e-5, form: int = 0) -> torch.Tensor:
     """Always the MFMA weight-streaming form (gemv_mfma.hip; M <= 16) — tests / microbenchmarks
-    (``linear``/``gemv`` take it by themselves for 5 <= M <= 16)."""
+    (``linear``/``gemv`` take it by themselves for 3 <= M <= 16). ``form`` 0 = by shape, 1-4 pin
+    (row groups per wave, x path) = (1, L2), (1, LDS), (2, L2), (2, LDS)."""
     if not x.is_cuda:
         return oracle.linear(x, W, epi, out, norm_w, eps)
     M, K = x.shape
@@ -142,7 +143,8 @@ def gemvm(x: torch.Tensor, W: torch.Tensor, epi: int = EPI_BF16, out: Optional[t
     if out is None:
         n_out = N // 2 if epi == EPI_SILU else N
         out = torch.empty(M, n_out, dtype=torch.float32 if epi == EPI_F32 else torch.bfloat16, device=x.device)
-    kernels().gemvm(M, _p(x), x.stride(0), _p(norm_w), float(eps), _p(W), _p(out), out.stride(0), N, K, epi, _s(x))
+    kernels().gemvm(M, _p(x), x.stride(0), _p(norm_w), float(eps), _p(W), _p(out), out.stride(0), N, K, epi, form,
+                    _s(x))
     return out
 
 

@@ -168,6 +168,31 @@ def bench_batched_decode(shapes=None, rows=(1, 2, 3, 4, 5, 8, 12, 16)):
         print(f"batched N={N} K={K} epi={epi}{' +norm' if norm else ''}: " + "  ".join(line), flush=True)
 
 
+def bench_gemvm_forms(shapes=None, rows=(3, 4, 5, 8, 12, 16)):
+    """The MFMA decode form's four variants per shape and row count (cold weights): (row groups per
+    wave, x path) = 1: (1, L2)  2: (1, LDS)  3: (2, L2)  4: (2, LDS); 'auto' = the shape rule."""
+    from llm_consensus_amd import ops
+
+    for (N, K, epi, norm) in shapes or [(6144, 4096, 0, True), (4096, 4096, 2, False), (28672, 4096, 3, True),
+                                        (4096, 14336, 2, False), (128256, 4096, 1, True), (14336, 4096, 3, True)]:
+        copies = max(2, (1 << 30) // (N * K * 2))
+        Ws = [(torch.randn(N, K, device="cuda") * 0.02).to(BF) for _ in range(copies)]
+        nw = torch.ones(K, dtype=BF, device="cuda") if norm else None
+        for M in rows:
+            x = torch.randn(M, K, device="cuda").to(BF)
+            n_out = N // 2 if epi == 3 else N
+            out = torch.zeros(M, n_out, dtype=torch.float32 if epi == 1 else BF, device="cuda")
+            res = []
+            for form in (0, 1, 2, 3, 4):
+                def run():
+                    for W in Ws:
+                        ops.gemvm(x, W, epi, out=out, norm_w=nw, form=form)
+                res.append(f"{'auto' if form == 0 else form}:{timeit(run, iters=2, warm=1) / copies:6.2f}")
+            print(f"forms N={N} K={K} epi={epi} M={M}: " + "  ".join(res), flush=True)
+        del Ws
+        torch.cuda.empty_cache()
+
+
 def bench_qkv_rope():
     """qkv GEMV with the RoPE + paged-KV-write epilogue vs the same GEMV with a plain bf16
     epilogue (both with the fused RMSNorm prologue), cold weights: what the epilogue costs."""
@@ -258,6 +283,8 @@ if __name__ == "__main__":
         bench_gemv_sweep([(768, 4096), (1536, 4096), (3584, 4096), (4096, 512), (4096, 1792)])
     if what in ("sweep-70b-tp4",):  # one TP=4 rank of Llama-3-70B: qkv, gate_up, o, down
         bench_gemv_sweep([(2560, 8192), (14336, 8192), (8192, 2048), (8192, 7168)])
+    if what in ("gemvm-forms",):  # the MFMA decode form's variants
+        bench_gemvm_forms()
     if what in ("batched",):  # decode projections at continuous-batching row counts
         bench_batched_decode()
     if what in ("qkv-rope",):

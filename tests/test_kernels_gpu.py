@@ -108,6 +108,22 @@ def test_gemvm(cuda, M, N, K, epi):
     close(y, ref, 2e-2)
 
 
+@pytest.mark.parametrize("form", [1, 2, 3, 4])
+@pytest.mark.parametrize("M", [3, 16])
+@pytest.mark.parametrize("N,K", [(1000, 4096), (8200, 1024), (4096, 14336)])
+@pytest.mark.parametrize("epi", [0, 2, 3])
+def test_gemvm_forms(cuda, form, M, N, K, epi):
+    """Every variant of the MFMA form pinned (one / two 16-row weight groups per wave, x fragments
+    from L2 / through LDS): ragged N for the 32-row blocks (1000, 8200), split-K 4-8 waves."""
+    torch.manual_seed(form * 13 + M + N + epi)
+    x = rnd(M, K)
+    W = rnd(N, K, scale=0.05)
+    out = rnd(M, N) if epi == 2 else None
+    ref_out = out.cpu().clone() if out is not None else None
+    y = ops.gemvm(x, W, epi, out=out, form=form)
+    close(y, oracle.linear(x.cpu(), W.cpu(), epi, ref_out), 2e-2)
+
+
 @pytest.mark.parametrize("M", [3, 5, 7, 12, 16])
 @pytest.mark.parametrize("N,K,epi", [(6144, 4096, 0), (28672, 4096, 3), (4096, 14336, 2), (128256, 4096, 1),
                                      (9216, 3072, 0)])

@@ -22,6 +22,8 @@ int llmc_embedding(const void*, const void*, void*, int, int, int, hipStream_t);
 int llmc_silu_mul_interleaved(const void*, void*, int, int, hipStream_t);
 int llmc_gemv(int, const void*, int, const void*, float, const void*, void*, int, int, int, int, int, hipStream_t);
 int llmc_gemvm(int, const void*, int, const void*, float, const void*, void*, int, int, int, int, int, hipStream_t);
+int llmc_moe_gemvm(int, const void*, int, const void*, float, const void*, const void*, int, int, void*, int, int, int,
+                   int, hipStream_t);
 int llmc_gemm(const void*, int, const void*, int, void*, int, int, int, int, int, hipStream_t);
 int llmc_rope_kv_write(const void*, int, void*, int, const void*, const void*, const void*, void*, void*, const void*,
                        int, int, int, int, int, hipStream_t);
@@ -90,6 +92,10 @@ PYBIND11_MODULE(_llmc_hip, m) {
   m.def("gemv", [](int M, ptr x, int xs, ptr nw, float eps, ptr W, ptr out, int os, int N, int K, int epi, int mfma,
                    ptr s) {
     check(llmc_gemv(M, P(x), xs, P(nw), eps, P(W), P(out), os, N, K, epi, mfma, S(s)), "gemv");
+  });
+  m.def("moe_gemvm", [](int P, ptr x, int xs, ptr nw, float eps, ptr W, ptr ids, int x_div, int E, ptr out, int os,
+                        int N, int K, int epi, ptr s) {
+    check(llmc_moe_gemvm(P, P(x), xs, P(nw), eps, P(W), P(ids), x_div, E, P(out), os, N, K, epi, S(s)), "moe_gemvm");
   });
   m.def("gemvm", [](int M, ptr x, int xs, ptr nw, float eps, ptr W, ptr out, int os, int N, int K, int epi, int form,
                     ptr s) {

@@ -25,6 +25,14 @@
 
 namespace llmc {
 
+// MoE decode (EXP): the (token, slot) pairs of `ids` [P] (local expert ids, -1 = another rank's)
+// grouped by expert: block (n, e) streams expert e's rows n once for every pair routed to e (at
+// most one per token, so <= 16 for <= 16 tokens); x row of pair p = p / x_div, output row p.
+struct ExpertMap {
+  const int32_t* ids = nullptr;
+  int P = 0, x_div = 1, E = 1;
+};
+
 // Fused epilogue of one lane: rows nb .. nb + 3 (f32 accumulators v) of token m.
 template <int EPI>
 __device__ __forceinline__ void gemvm_epilogue(const f32x4& v, int nb, int m, int N, void* __restrict__ out,
@@ -61,10 +69,11 @@ __device__ __forceinline__ void gemvm_epilogue(const f32x4& v, int nb, int m, in
     }
   } else if constexpr (EPI == EPI_SILU) {  // rows (2j, 2j + 1) = (gate_j, up_j) -> column j
     bf16_t* o = reinterpret_cast<bf16_t*>(out) + static_cast<int64_t>(m) * out_stride + nb / 2;
-    if (full) {
+    if (full && out_stride % 2 == 0) {  // 4-B aligned pair
       *reinterpret_cast<uint32_t*>(o) = pack_bf16x2(silu(v[0]) * v[1], silu(v[2]) * v[3]);
     } else {
       if (nb + 1 < N) o[0] = f32_to_bf16(silu(v[0]) * v[1]);
+      if (nb + 3 < N) o[1] = f32_to_bf16(silu(v[2]) * v[3]);
     }
   } else if constexpr (EPI == EPI_ROPE) {
     // rows (2i, 2i + 1) of a Q/K head = dims (i, i + D/2) (pair-interleaved on the host); V rows
@@ -104,11 +113,12 @@ __device__ __forceinline__ void gemvm_epilogue(const f32x4& v, int nb, int m, in
 }
 
 
-template <int S, int RB, int XL, int PRO, int EPI>
+template <int S, int RB, int XL, int PRO, int EPI, bool EXP>
 __global__ __launch_bounds__(S * 64) void gemvm_kernel(const bf16_t* __restrict__ x, int x_stride,
                                                        const bf16_t* __restrict__ norm_w, float eps,
                                                        const bf16_t* __restrict__ W, void* __restrict__ out,
-                                                       int out_stride, int M, int N, int K, RopeEpi rope) {
+                                                       int out_stride, int M, int N, int K, RopeEpi rope,
+                                                       ExpertMap ex) {
   constexpr int TK = 128;       // k per tile: one 256-B LDS bank row per matrix row
   constexpr int WR = 16 * RB;   // weight rows per block (RB 16-row groups share every x fragment)
   constexpr int TB = 16 * TK * 2;
@@ -120,6 +130,24 @@ __global__ __launch_bounds__(S * 64) void gemvm_kernel(const bf16_t* __restrict_
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int r = lane & 15, g = lane >> 4;
   const int n0 = blockIdx.x * WR;
+  // token column m -> x row / output row (identity; MoE: the pairs routed to this block's expert)
+  __shared__ int pmap[16];
+  if constexpr (EXP) {
+    __shared__ int pcnt;
+    const int e = blockIdx.y;
+    if (wave == 0) {
+      const bool hit = lane < ex.P && ex.ids[lane] == e;
+      const uint64_t mask = __ballot(hit);
+      const int j = __popcll(mask & ((1ull << lane) - 1));
+      if (hit && j < 16) pmap[j] = lane;
+      if (lane == 0) pcnt = min(__popcll(mask), 16);
+    }
+    __syncthreads();
+    M = pcnt;
+    if (M == 0) return;  // no pair routed here: this expert's rows are not streamed
+    W += static_cast<int64_t>(e) * N * K;
+  }
+  auto xrow = [&](int m) { return EXP ? pmap[min(m, M - 1)] / ex.x_div : min(m, M - 1); };
   const int ntile = K / TK / S;  // tiles of this wave (host: K % (TK * S) == 0)
   const int kw = wave * ntile * TK;
   // tile loads: instruction i covers rows 4i + lane/16, 16-B chunk lane%16 — four whole 256-B
@@ -135,8 +163,8 @@ __global__ __launch_bounds__(S * 64) void gemvm_kernel(const bf16_t* __restrict_
   const u32x4* xsrc[4];
 #pragma unroll
   for (int i = 0; i < 4; ++i)
-    xsrc[i] = XL ? reinterpret_cast<const u32x4*>(x + static_cast<int64_t>(min(4 * i + g, M - 1)) * x_stride + kw + r * 8)
-                 : reinterpret_cast<const u32x4*>(x + static_cast<int64_t>(min(r, M - 1)) * x_stride + kw + g * 8) + 4 * i;
+    xsrc[i] = XL ? reinterpret_cast<const u32x4*>(x + static_cast<int64_t>(xrow(4 * i + g)) * x_stride + kw + r * 8)
+                 : reinterpret_cast<const u32x4*>(x + static_cast<int64_t>(xrow(r)) * x_stride + kw + g * 8) + 4 * i;
   const u32x4* gp = reinterpret_cast<const u32x4*>(norm_w + kw + g * 8);  // PRO_NORM only
   char* tw = lds_t[wave];
   char* tx = tw + RB * TB;
@@ -236,7 +264,7 @@ __global__ __launch_bounds__(S * 64) void gemvm_kernel(const bf16_t* __restrict_
 #pragma unroll
     for (int w = 1; w < S; ++w) v += red[w][b][lane];
     if constexpr (PRO == PRO_NORM) v *= inv;
-    gemvm_epilogue<EPI>(v, n0 + 16 * b + 4 * g, m, N, out, out_stride, rope);
+    gemvm_epilogue<EPI>(v, n0 + 16 * b + 4 * g, EXP ? pmap[m] : m, N, out, out_stride, rope);
   }
 }
 
@@ -251,12 +279,13 @@ static int gemvm_form(int M, int N, int K) {
   return 1 + (xl ? 1 : 0) + (rb2 ? 2 : 0);
 }
 
-template <int S, int RB, int XL, int PRO, int EPI>
+template <int S, int RB, int XL, int PRO, int EPI, bool EXP>
 static int launch_gemvm_s(const void* x, int x_stride, const void* nw, float eps, const void* W, void* out,
-                          int out_stride, int M, int N, int K, const RopeEpi& rope, hipStream_t st) {
-  const int grid = (N + 16 * RB - 1) / (16 * RB);
-  gemvm_kernel<S, RB, XL, PRO, EPI><<<grid, S * 64, 0, st>>>((const bf16_t*)x, x_stride, (const bf16_t*)nw, eps,
-                                                             (const bf16_t*)W, out, out_stride, M, N, K, rope);
+                          int out_stride, int M, int N, int K, const RopeEpi& rope, const ExpertMap& ex,
+                          hipStream_t st) {
+  const dim3 grid((N + 16 * RB - 1) / (16 * RB), EXP ? ex.E : 1);
+  gemvm_kernel<S, RB, XL, PRO, EPI, EXP><<<grid, S * 64, 0, st>>>(
+      (const bf16_t*)x, x_stride, (const bf16_t*)nw, eps, (const bf16_t*)W, out, out_stride, M, N, K, rope, ex);
   return static_cast<int>(hipGetLastError());
 }
 
@@ -273,31 +302,39 @@ static int pick_split(int blocks, int K) {
   return S;
 }
 
-template <int RB, int XL, int PRO, int EPI>
+template <int RB, int XL, int PRO, int EPI, bool EXP>
 static int launch_gemvm_rb(const void* x, int x_stride, const void* nw, float eps, const void* W, void* out,
-                           int out_stride, int M, int N, int K, const RopeEpi& rope, hipStream_t st) {
+                           int out_stride, int M, int N, int K, const RopeEpi& rope, const ExpertMap& ex,
+                           hipStream_t st) {
+#define LLMC_S(SS) \
+  return launch_gemvm_s<SS, RB, XL, PRO, EPI, EXP>(x, x_stride, nw, eps, W, out, out_stride, M, N, K, rope, ex, st)
   switch (pick_split((N + 16 * RB - 1) / (16 * RB), K)) {
-    case 1: return launch_gemvm_s<1, RB, XL, PRO, EPI>(x, x_stride, nw, eps, W, out, out_stride, M, N, K, rope, st);
-    case 2: return launch_gemvm_s<2, RB, XL, PRO, EPI>(x, x_stride, nw, eps, W, out, out_stride, M, N, K, rope, st);
-    case 4: return launch_gemvm_s<4, RB, XL, PRO, EPI>(x, x_stride, nw, eps, W, out, out_stride, M, N, K, rope, st);
-    case 8: return launch_gemvm_s<8, RB, XL, PRO, EPI>(x, x_stride, nw, eps, W, out, out_stride, M, N, K, rope, st);
+    case 1: LLMC_S(1);
+    case 2: LLMC_S(2);
+    case 4: LLMC_S(4);
+    case 8: LLMC_S(8);
     default: return -1;
   }
+#undef LLMC_S
 }
 
-// form: 0 = by shape (below); 1-4 = (row groups, x path) = (1, L2), (1, LDS), (2, L2), (2, LDS)
-// (microbenchmarks / tests pin one)
-template <int PRO, int EPI>
+// form: 0 = by shape (gemvm_form); 1-4 pin (row groups, x path) = (1, L2), (1, LDS), (2, L2),
+// (2, LDS) (microbenchmarks / tests)
+template <int PRO, int EPI, bool EXP = false>
 static int launch_gemvm(const void* x, int x_stride, const void* nw, float eps, const void* W, void* out,
-                        int out_stride, int M, int N, int K, const RopeEpi& rope, int form, hipStream_t st) {
+                        int out_stride, int M, int N, int K, const RopeEpi& rope, int form, hipStream_t st,
+                        const ExpertMap& ex = ExpertMap{}) {
   if (form == 0) form = gemvm_form(M, N, K);
+#define LLMC_F(RB, XL) \
+  return launch_gemvm_rb<RB, XL, PRO, EPI, EXP>(x, x_stride, nw, eps, W, out, out_stride, M, N, K, rope, ex, st)
   switch (form) {
-    case 1: return launch_gemvm_rb<1, 0, PRO, EPI>(x, x_stride, nw, eps, W, out, out_stride, M, N, K, rope, st);
-    case 2: return launch_gemvm_rb<1, 1, PRO, EPI>(x, x_stride, nw, eps, W, out, out_stride, M, N, K, rope, st);
-    case 3: return launch_gemvm_rb<2, 0, PRO, EPI>(x, x_stride, nw, eps, W, out, out_stride, M, N, K, rope, st);
-    case 4: return launch_gemvm_rb<2, 1, PRO, EPI>(x, x_stride, nw, eps, W, out, out_stride, M, N, K, rope, st);
+    case 1: LLMC_F(1, 0);
+    case 2: LLMC_F(1, 1);
+    case 3: LLMC_F(2, 0);
+    case 4: LLMC_F(2, 1);
     default: return -1;
   }
+#undef LLMC_F
 }
 
 int gemvm_dispatch(int M, const void* x, int x_stride, const void* norm_w, float eps, const void* W, void* out,
@@ -330,4 +367,34 @@ extern "C" int llmc_gemvm(int M, const void* x, int x_stride, const void* norm_w
   if (epi == llmc::EPI_ROPE) return -5;
   llmc::RopeEpi rope{};
   return llmc::gemvm_dispatch(M, x, x_stride, norm_w, eps, W, out, out_stride, N, K, epi, rope, s, form);
+}
+
+// MoE decode, pairs grouped by expert (see ExpertMap): out[p] = W[ids[p]] . x[p / x_div] (+ fused
+// norm on x / SiLU), for P <= 64 pairs of <= 16 tokens. Rows of other ranks' pairs (id -1) are
+// not written.
+extern "C" int llmc_moe_gemvm(int P, const void* x, int x_stride, const void* norm_w, float eps, const void* W,
+                              const void* ids, int x_div, int E, void* out, int out_stride, int N, int K, int epi,
+                              hipStream_t s) {
+  using namespace llmc;
+  // P <= 64: one wave's ballot maps the pairs; <= 16 pairs per expert holds for <= 16 tokens with
+  // distinct experts per token (the caller's contract: ops.moe_gemvm checks the token count)
+  if (P < 1 || P > 64 || x_div < 1 || E < 1 || K % 128 != 0 || x_stride % 8 != 0) return -1;
+  if (epi == EPI_SILU && N % 4 != 0) return -1;
+  ExpertMap ex{static_cast<const int32_t*>(ids), P, x_div, E};
+  const int form = 1 + (N >= 6144 ? 2 : 0);  // few pairs per expert: x fragments from L2
+  RopeEpi rope{};
+  const bool norm = norm_w != nullptr;
+  switch (epi) {
+    case EPI_BF16:
+      return norm ? launch_gemvm<PRO_NORM, EPI_BF16, true>(x, x_stride, norm_w, eps, W, out, out_stride, kGemvmMaxM, N, K,
+                                                           rope, form, s, ex)
+                  : launch_gemvm<PRO_NONE, EPI_BF16, true>(x, x_stride, norm_w, eps, W, out, out_stride, kGemvmMaxM, N, K,
+                                                           rope, form, s, ex);
+    case EPI_SILU:
+      return norm ? launch_gemvm<PRO_NORM, EPI_SILU, true>(x, x_stride, norm_w, eps, W, out, out_stride, kGemvmMaxM, N, K,
+                                                           rope, form, s, ex)
+                  : launch_gemvm<PRO_NONE, EPI_SILU, true>(x, x_stride, norm_w, eps, W, out, out_stride, kGemvmMaxM, N, K,
+                                                           rope, form, s, ex);
+    default: return -4;
+  }
 }

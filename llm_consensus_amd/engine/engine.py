@@ -546,6 +546,16 @@ class Engine:
             w, ids = self.moe_lw[:B], self.moe_lids[:B]
         I_l, H = self.w.inter, c.hidden
         act, y = self.moe_act[: B * k], self.moe_y[: B * k]
+        if self.mfma_decode and H % 128 == 0 and I_l % 128 == 0:
+            # a batching engine (see mfma_decode): the pairs grouped by expert on the MFMA form, each
+            # routed expert streamed once for all its rows, then the combine
+            ops.moe_gemvm(h, Lw.w_gu, ids, k, act, 2 * I_l, H, EPI_SILU, norm_w=Lw.ln2, eps=c.rms_eps)
+            ops.moe_gemvm(act, Lw.w_down, ids, 1, y, H, I_l, EPI_BF16)
+            if self.tp.rank != 0:
+                h.zero_()
+            ops.moe_combine(y, w, ids, h)
+            self.tp.all_reduce_(h)
+            return
         ops.moe_gemv(h, Lw.w_gu, ids, k, act, 2 * I_l, H, EPI_SILU, norm_w=Lw.ln2, eps=c.rms_eps)
         if self.tp.rank != 0:  # row-parallel partial: only rank 0 carries the residual
             h.zero_()

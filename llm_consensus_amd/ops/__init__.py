@@ -321,6 +321,20 @@ def moe_gemv(x, W_experts, ids, x_div, out, N, K, epi, norm_w=None, eps: float =
     return out
 
 
+def moe_gemvm(x, W_experts, ids, x_div, out, N, K, epi, norm_w=None, eps: float = 1e-5):
+    """Batched MoE decode (<= 16 tokens) on the MFMA form with the pairs grouped by expert: every
+    routed expert's weights stream once for all its pairs (``moe_gemv`` streams them once per pair).
+    out[p] = W[ids[p]] . x[p // x_div]; pairs with id -1 (another rank's expert) are not written."""
+    if not x.is_cuda:
+        raise ValueError("moe_gemvm: GPU only (the CPU path is moe_gemv's oracle)")
+    P, E = ids.numel(), W_experts.shape[0]
+    if ids.dim() != 2 or ids.shape[0] > GEMV_MAX_M:
+        raise ValueError(f"moe_gemvm: ids [tokens <= {GEMV_MAX_M}, k], got {tuple(ids.shape)}")
+    kernels().moe_gemvm(P, _p(x), x.stride(0), _p(norm_w) if norm_w is not None else 0, float(eps), _p(W_experts),
+                        _p(ids), x_div, E, _p(out), out.stride(0), N, K, epi, _s(x))
+    return out
+
+
 def moe_down_combine(act, W_down, ids, w, h, N, K):
     """Decode MoE down projection fused with the combine (top-2): h[t] += sum_j w[t, j] *
     (W_down[ids[t, j]] . act[t*2 + j]), fixed order, f32."""

@@ -200,8 +200,8 @@ class LocalBackend:
                     models.append({"name": m, "family": s.family, "seed": s.seed, "max_context": self._ctx[m],
                                    "checkpoint": s.config.checkpoint, "kv_blocks": kv_blocks[m],
                                    # decode rows per step: up to 16 on the weight-streaming
-                                   # GEMV / MFMA form; MoE keeps 4 (per-(row, expert) GEMVs)
-                                   "max_batch": max(1, min(4 if s.config.is_moe else 16, max(n, sess))),
+                                   # GEMV / MFMA form (MoE: pairs grouped by expert)
+                                   "max_batch": max(1, min(16, max(n, sess))),
                                    "max_seqs": max(1, n) + sess})
             if groups:
                 dist_info = {"port": port, "rank": rank_of[g], "world": len(used),

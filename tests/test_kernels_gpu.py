@@ -108,6 +108,36 @@ def test_gemvm(cuda, M, N, K, epi):
     close(y, ref, 2e-2)
 
 
+@pytest.mark.parametrize("B", [3, 8, 16])
+@pytest.mark.parametrize("ep", [False, True])
+def test_moe_gemvm(cuda, B, ep):
+    """Batched MoE decode with the (token, slot) pairs grouped by expert (MFMA form): gate_up with
+    the fused norm + SiLU and the down projection, per pair against the fp32 oracle; expert-parallel
+    ids (-1 = another rank's expert) leave their rows untouched."""
+    torch.manual_seed(B * 3 + ep)
+    E, H, I, k = 8, 512, 384, 2
+    ids = torch.stack([torch.randperm(E)[:k] for _ in range(B)]).to(torch.int32)
+    if ep:
+        ids[ids >= 4] = -1
+    x = rnd(B, H)
+    nw = rnd(H)
+    Wgu = rnd(E, 2 * I, H, scale=0.05)
+    Wd = rnd(E, H, I, scale=0.05)
+    act = torch.full((B * k, I), 7.0, dtype=BF, device="cuda")
+    y = torch.full((B * k, H), 7.0, dtype=BF, device="cuda")
+    ops.moe_gemvm(x, Wgu, ids.cuda(), k, act, 2 * I, H, ops.EPI_SILU, norm_w=nw, eps=1e-5)
+    ops.moe_gemvm(act, Wd, ids.cuda(), 1, y, H, I, ops.EPI_BF16)
+    xn = _normed_exact(x, nw)
+    for p, e in enumerate(ids.view(-1).tolist()):
+        if e < 0:
+            assert bool((act[p] == 7.0).all()) and bool((y[p] == 7.0).all()), p
+            continue
+        ref = oracle.linear(x[p // k:p // k + 1].cpu(), Wgu[e].cpu(), ops.EPI_SILU, None, nw.cpu(), 1e-5)
+        g = xn[p // k:p // k + 1] @ Wgu[e].cpu().float().t()
+        no_worse_than_oracle(act[p:p + 1], ref, torch.nn.functional.silu(g[:, 0::2]) * g[:, 1::2])
+        close(y[p:p + 1], oracle.linear(act[p:p + 1].cpu(), Wd[e].cpu(), ops.EPI_BF16), 2e-2)
+
+
 @pytest.mark.parametrize("form", [1, 2, 3, 4])
 @pytest.mark.parametrize("M", [3, 16])
 @pytest.mark.parametrize("N,K", [(1000, 4096), (8200, 1024), (4096, 14336)])

@@ -62,7 +62,7 @@ FUSED_CHUNK_SMALL, FUSED_CHUNK_LARGE = 128, 256
 
 
 def attn_buckets(ctxmax: int, blocks_per_head: int = 32, fused_max: int = 4096, group: int = 4,
-                 nkv: int = 8) -> List[tuple]:
+                 nkv: int = 8, rows: int = 1) -> List[tuple]:
     """Decode-attention shapes per context bucket: [(capacity_tokens, chunk, grid_chunks, fused)].
 
     Capacities double from 1024. A bucket uses the fused form (fixed-chunk blocks over the bucket
@@ -75,8 +75,26 @@ def attn_buckets(ctxmax: int, blocks_per_head: int = 32, fused_max: int = 4096, 
     of 128 keys per block, the kernel spreads a sequence's keys evenly over ``grid_chunks`` blocks,
     and the grid grows with the context until ``blocks_per_head``; one bucket then covers every
     longer context. Measured per shape: profiles/r2_attn_decode.md. ``fused_max`` = 0 disables
-    the fused form (page size not a multiple of 32 keys)."""
+    the fused form (page size not a multiple of 32 keys).
+
+    An engine batching ``rows`` >= 3 decode rows whose rows x kv heads give >= 32 independent
+    (row, head) units takes its parallelism from the rows: every bucket is the balanced split at
+    256 / (rows x nkv) blocks per kv head (16 rows of the 8B: 2 blocks, 31 vs 44-79 µs for the
+    fused forms at 2.5k keys; profiles/r2_batched_decode.md). The partition of a row's keys then
+    depends on its own length only, not on the bucket the batch's longest row selects."""
     out, cap = [], 1024
+    if rows >= 3 and rows * nkv >= 32:
+        per_head = max(1, 256 // (rows * nkv))
+        while True:
+            c = min(cap, ctxmax)
+            gc = min((c + 127) // 128, per_head)
+            if out and out[-1][2] == gc:
+                out[-1] = (c, 128, gc, False)
+            else:
+                out.append((c, 128, gc, False))
+            if cap >= ctxmax:
+                return out
+            cap *= 2
     while True:
         c = min(cap, ctxmax)
         if fused_max > 0 and c <= fused_max:
@@ -211,7 +229,7 @@ class Engine:
         ctxmax = self.ecfg.max_context + self.ecfg.steps_per_graph + 2
         self.attn_buckets = attn_buckets(ctxmax, split_blocks_per_head(self.nh, self.nkv),
                                          ops.FUSED_ATTN_MAX_KEYS if self.bs % 32 == 0 else 0, self.nh // self.nkv,
-                                         self.nkv)
+                                         self.nkv, rows=self.ecfg.max_batch)
         max_chunks = max(gc for _, _, gc, _ in self.attn_buckets)
         self.attn_part, self.attn_counters = ops.decode_attn_workspace(B, self.nh, self.nkv, self.D, max_chunks, dev)
         if self.on_gpu:

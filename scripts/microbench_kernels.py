@@ -85,6 +85,37 @@ def bench_attn(shapes=((32, 8, 128), (32, 32, 96), (16, 2, 128), (8, 1, 128), (4
                   + f"  | best {gb / best * 1e6 / 1e3:5.2f} TB/s", flush=True)
 
 
+def bench_attn_batched(shapes=((32, 8, 128),), rows=(1, 4, 16), lens=(2048, 2560, 8192)):
+    """Decode attention for B rows per launch (continuous batching): the fused form over the
+    engine's bucket (capacity = next power of two >= L, 128/256-key chunks) vs the balanced split
+    at several blocks per kv head."""
+    for nh, nkv, D in shapes:
+        for B in rows:
+            for L in lens:
+                kc, vc, bt, sl, q, out = _attn_case(L, nh, nkv, D, B=B)
+                sc = 1 / math.sqrt(D)
+                gb = B * L * nkv * D * 2 * 2 / 1e9
+                cap = 1024
+                while cap < L:
+                    cap *= 2
+                line, best = [], 1e9
+                for ch in (128, 256):
+                    gc = cap // ch
+                    part, ctr = ops.decode_attn_workspace(B, nh, nkv, D, gc, "cuda", fused=True)
+                    us = timeit(lambda: ops.attn_decode(q, kc, vc, bt, sl, out, part, ctr, nh, nkv, D, 64, ch, sc,
+                                                        grid_chunks=gc, fused=True))
+                    best = min(best, us)
+                    line.append(f"fused c{ch} {us:6.2f}")
+                for gc in (2, 4, 8, 16, 32):
+                    part, ctr = ops.decode_attn_workspace(B, nh, nkv, D, gc, "cuda")
+                    us = timeit(lambda: ops.attn_decode(q, kc, vc, bt, sl, out, part, ctr, nh, nkv, D, 64, 128, sc,
+                                                        grid_chunks=gc))
+                    best = min(best, us)
+                    line.append(f"split g{gc} {us:6.2f}")
+                print(f"attn B={B:2d} nh={nh} nkv={nkv} D={D} L={L:6d}: " + "  ".join(line)
+                      + f"  | best {gb / best * 1e6 / 1e3:5.2f} TB/s", flush=True)
+
+
 def bench_gemv():
     for (N, K, epi, norm) in [(6144, 4096, 0, True), (4096, 4096, 2, False), (28672, 4096, 3, True),
                               (4096, 14336, 2, False), (128256, 4096, 1, True)]:
@@ -283,6 +314,8 @@ if __name__ == "__main__":
         bench_gemv_sweep([(768, 4096), (1536, 4096), (3584, 4096), (4096, 512), (4096, 1792)])
     if what in ("sweep-70b-tp4",):  # one TP=4 rank of Llama-3-70B: qkv, gate_up, o, down
         bench_gemv_sweep([(2560, 8192), (14336, 8192), (8192, 2048), (8192, 7168)])
+    if what in ("attn-batched",):  # decode attention with many rows per launch
+        bench_attn_batched()
     if what in ("gemvm-forms",):  # the MFMA decode form's variants
         bench_gemvm_forms()
     if what in ("batched",):  # decode projections at continuous-batching row counts

@@ -12,10 +12,27 @@ ap.add_argument("--tokens", type=int, default=128)
 ap.add_argument("--prompt", type=int, default=512)
 ap.add_argument("--no-graphs", action="store_true")
 ap.add_argument("--ctx", type=int, default=8192)
+ap.add_argument("--batch", type=int, default=1, help="decode rows per step (continuous-batching engine)")
 a = ap.parse_args()
 cfg = FAMILIES[a.model]
-e = Engine(cfg, EngineConfig(device="cuda:0", max_context=a.ctx, seed=1, use_graphs=not a.no_graphs))
+e = Engine(cfg, EngineConfig(device="cuda:0", max_context=a.ctx, seed=1, use_graphs=not a.no_graphs,
+                             max_batch=a.batch))
 prompt = [(i * 7919) % 30000 + 256 for i in range(a.prompt)]
+if a.batch > 1:
+    from llm_consensus_amd.engine import SamplingParams
+
+    prompts = [[(i * (7919 + 2 * r)) % 30000 + 256 for i in range(a.prompt)] for r in range(a.batch)]
+    sp = [SamplingParams(a.tokens, 1.0, 1.0, 0, 100 + r, False) for r in range(a.batch)]
+    e.generate_batch(prompts, [SamplingParams(16, 1.0, 1.0, 0, r, False) for r in range(a.batch)])  # warm
+    torch.cuda.synchronize()
+    t = time.perf_counter()
+    outs = e.generate_batch(prompts, sp)
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t
+    n = sum(len(o) for o in outs)
+    print(f"{a.model}: {a.batch} rows x {a.tokens} tokens in {dt:.3f}s incl prefill of {a.batch} x {a.prompt} -> "
+          f"{1000 * dt / a.tokens:.3f} ms/step, {n / dt:.0f} tokens/s", flush=True)
+    sys.exit(0)
 e.generate_ids(prompt, 16, stop_on_eos=False)  # warm (graph capture)
 torch.cuda.synchronize()
 t = time.perf_counter()

@@ -128,6 +128,21 @@ def test_attn_buckets_cover_context():
                                                                               (128, False)]
 
 
+def test_attn_buckets_batching_engine():
+    """A 16-row (or 4-row) 8B engine takes its attention parallelism from the rows: the balanced
+    split at 256 / (rows x kv heads) blocks per head in every bucket, i.e. one bucket / graph per
+    batch size; engines of 1-2 rows, or rows x kv heads < 32, keep the per-context forms."""
+    from llm_consensus_amd.engine.engine import attn_buckets
+
+    assert attn_buckets(16394, 32, rows=16) == [(16394, 128, 2, False)]
+    assert attn_buckets(16394, 32, rows=4) == [(16394, 128, 8, False)]
+    assert attn_buckets(16394, 32, rows=2) == attn_buckets(16394, 32)
+    assert attn_buckets(16394, 32, nkv=2, rows=8) == attn_buckets(16394, 32, nkv=2)   # 16 units
+    assert attn_buckets(4106, 16, group=1, nkv=32, rows=4) == [(4106, 128, 2, False)]  # Phi-3
+    # short contexts: never more blocks than 128-key ranges
+    assert attn_buckets(200, 32, rows=4) == [(200, 128, 2, False)]
+
+
 def test_split_blocks_per_head():
     from llm_consensus_amd.engine.engine import split_blocks_per_head
 

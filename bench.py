@@ -28,6 +28,10 @@ smaller config under the same name.
 rehearsals of the multi-rank flows: ``LLMC_BENCH_DEVICE=cpu`` or ``LLMC_BENCH_SAME_GPU=1`` with
 ``LLMC_BENCH_BACKEND=gloo``).
 
+Warmup: the first of ``--warmup`` rounds is a full round; the others decode ``--warmup-tokens``
+(default 512) tokens per engine — every kernel, graph and bucket of a round has run by then, and a
+20-step x 40-s driver run stays within its wall-clock. The K timed rounds are always full rounds.
+
 Reported ``value`` = total generated tokens (responders + judge) per second of wall time over the
 whole job (max over ranks); ``ms_per_step`` = mean round latency; p50/p90 are in ``extra``.
 Data: synthetic prompt (seeded synthetic-tokenizer text), random-init weights, bf16.
@@ -158,6 +162,8 @@ def main() -> None:
     ap.add_argument("--n-models", type=int, default=0, help="fanout: responders (0 = max(3, N))")
     ap.add_argument("--max-tokens", type=int, default=4096)
     ap.add_argument("--judge-max-tokens", type=int, default=0, help="0 = same as --max-tokens")
+    ap.add_argument("--warmup-tokens", type=int, default=512,
+                    help="tokens per engine in warmup rounds after the first (untimed; 0 = full rounds)")
     ap.add_argument("--prompt-tokens", type=int, default=128)
     ap.add_argument("--temperature", type=float, default=1.0)
     ap.add_argument("--judge-tp", type=int, default=0, help="0 = auto (config 5: 4)")
@@ -284,7 +290,9 @@ def main() -> None:
     log(f"engines ready in {time.time() - t0:.1f}s: {[e.name for _, e, _, _ in responders]}"
         + (f" + {judge.name} (TP={judge.tp.size}, ctx {judge_ctx})" if judge else ""))
 
-    def one_round(step: int):
+    def one_round(step: int, max_tokens: int = 0):
+        max_tokens = max_tokens or args.max_tokens
+        jmax_r = jmax if max_tokens == args.max_tokens else min(jmax, max_tokens)
         stats = {}
         t_start = time.perf_counter()
         # judge header prefill can start before any response exists
@@ -301,7 +309,7 @@ def main() -> None:
             try:
                 i, e, ids, _ = responders[j]
                 prog = Progress(f"round {step}: responder {i}") if (rank == 0 and j == 0) else None
-                outs[i] = e.generate_ids(ids, args.max_tokens, temperature=args.temperature,
+                outs[i] = e.generate_ids(ids, max_tokens, temperature=args.temperature,
                                          seed=1000 * step + i + 1, stop_on_eos=False, on_tokens=prog)
             except BaseException as ex:  # noqa: BLE001
                 errs.append(ex)
@@ -318,7 +326,7 @@ def main() -> None:
             log(f"round {step}: responders done in {t_resp - t_start:.2f}s")
         # gather every response to every rank: the leader of each responder writes its row
         # (token + 1; 0 = empty) and one SUM all-reduce assembles the table
-        table = torch.zeros((n_resp, args.max_tokens), dtype=torch.int32)
+        table = torch.zeros((n_resp, max_tokens), dtype=torch.int32)
         for i, e, _, _ in responders:
             if e.tp.is_leader:
                 r = torch.tensor(outs[i], dtype=torch.int32) + 1
@@ -327,7 +335,7 @@ def main() -> None:
             tt = table.to(cdev)
             dist.all_reduce(tt)
             table = tt.cpu()
-        n_tokens = n_resp * args.max_tokens
+        n_tokens = n_resp * max_tokens
         if judge is not None:
             # every judge rank renders the same prompt from the gathered rows (deterministic), so
             # the TP shards prefill/decode in lockstep; rank 0 accounts the judge tokens
@@ -344,7 +352,7 @@ def main() -> None:
             t_jp = time.perf_counter()
             if rank == 0:
                 log(f"round {step}: judge prefill of {len(rest_ids)} tokens in {t_jp - t_resp:.2f}s (TP={judge.tp.size})")
-            jids = judge.decode([jseq], [SamplingParams(jmax, args.temperature, 1.0, 0, 99 + step, False)],
+            jids = judge.decode([jseq], [SamplingParams(jmax_r, args.temperature, 1.0, 0, 99 + step, False)],
                                 on_tokens=Progress(f"round {step}: judge") if rank == 0 else None)[0]
             stats["judge_prompt_tokens"] = jseq.length - len(jids)
             stats["judge_prefill_s"] = t_jp - t_resp
@@ -362,11 +370,11 @@ def main() -> None:
         t_end = time.perf_counter()
         stats["responders_s"] = t_resp - t_start
         stats["e2e_s"] = t_end - t_start
-        stats["tokens"] = n_tokens + (jmax if judge_plan else 0)
+        stats["tokens"] = n_tokens + (jmax_r if judge_plan else 0)
         return stats
 
     for w in range(args.warmup):
-        st = one_round(w)
+        st = one_round(w, 0 if w == 0 else args.warmup_tokens)
         log(f"warmup {w}: {st}")
 
     sync()
@@ -437,6 +445,7 @@ def main() -> None:
                 "judge_prefill_s": round(judge_stats.get("judge_prefill_s", 0.0), 3),
                 "judge_decode_s": round(judge_stats.get("judge_decode_s", 0.0), 3),
                 "judge_tp": jtp,
+                "warmup_rounds_tokens": [args.max_tokens] + [args.warmup_tokens or args.max_tokens] * max(0, args.warmup - 1),
                 "custom_allreduce": {e.name: e.tp.custom is not None for _, e, _, _ in responders if e.tp.size > 1}
                 | ({judge.name: judge.tp.custom is not None} if judge is not None and judge.tp.size > 1 else {}),
             },

@@ -72,3 +72,11 @@ def test_fanout_two_ranks_balances_the_third_responder():
     assert "2x llama-tiny + 1x llama-tiny TP=2 responders" in d["config"]["model"]
     assert d["config"]["parallelism"] == "fanout3-resp_tp2-over2gpus-judge_tp2"
     _tokens_ok(d, 12)
+
+
+def test_warmup_rounds_after_the_first_are_short_timed_rounds_full():
+    """Warmup: the first round is full length, later ones decode --warmup-tokens; the timed rounds
+    (and the reported tokens) are full rounds."""
+    d = _run(1, ["--shapes", "tiny", "--steps", "1", "--warmup", "2", "--max-tokens", "12", "--warmup-tokens", "4"], 0)
+    assert d["extra"]["warmup_rounds_tokens"] == [12, 4]
+    _tokens_ok(d, 12)

@@ -305,12 +305,23 @@ def main() -> None:
         outs: Dict[int, List[int]] = {}
         errs = []
 
+        # per responder: [time to first token, latency] in s from the round start (its leader's clock)
+        times = torch.zeros((n_resp, 2), dtype=torch.float64)
+
         def run_one(j):
             try:
                 i, e, ids, _ = responders[j]
                 prog = Progress(f"round {step}: responder {i}") if (rank == 0 and j == 0) else None
+
+                def on_tokens(new, i=i, prog=prog):
+                    if times[i, 0] == 0:
+                        times[i, 0] = time.perf_counter() - t_start
+                    if prog is not None:
+                        prog(new)
+
                 outs[i] = e.generate_ids(ids, max_tokens, temperature=args.temperature,
-                                         seed=1000 * step + i + 1, stop_on_eos=False, on_tokens=prog)
+                                         seed=1000 * step + i + 1, stop_on_eos=False, on_tokens=on_tokens)
+                times[i, 1] = time.perf_counter() - t_start
             except BaseException as ex:  # noqa: BLE001
                 errs.append(ex)
 
@@ -331,10 +342,17 @@ def main() -> None:
             if e.tp.is_leader:
                 r = torch.tensor(outs[i], dtype=torch.int32) + 1
                 table[i, : r.numel()] = r
+            else:
+                times[i] = 0.0  # the leader's clock reports this responder
         if world > 1:
             tt = table.to(cdev)
             dist.all_reduce(tt)
             table = tt.cpu()
+            ts = times.to(cdev)
+            dist.all_reduce(ts)
+            times = ts.cpu()
+        stats["per_model"] = {e["name"]: {"ttft_s": float(times[i, 0]), "latency_s": float(times[i, 1])}
+                              for i, e in enumerate(resp_plan)}
         n_tokens = n_resp * max_tokens
         if judge is not None:
             # every judge rank renders the same prompt from the gathered rows (deterministic), so
@@ -352,8 +370,18 @@ def main() -> None:
             t_jp = time.perf_counter()
             if rank == 0:
                 log(f"round {step}: judge prefill of {len(rest_ids)} tokens in {t_jp - t_resp:.2f}s (TP={judge.tp.size})")
+            jprog = Progress(f"round {step}: judge") if rank == 0 else None
+            jfirst = []
+
+            def on_judge_tokens(i, new):
+                if not jfirst:
+                    jfirst.append(time.perf_counter())
+                if jprog is not None:
+                    jprog(i, new)
+
             jids = judge.decode([jseq], [SamplingParams(jmax_r, args.temperature, 1.0, 0, 99 + step, False)],
-                                on_tokens=Progress(f"round {step}: judge") if rank == 0 else None)[0]
+                                on_tokens=on_judge_tokens)[0]
+            stats["judge_ttft_s"] = (jfirst[0] if jfirst else time.perf_counter()) - t_resp
             stats["judge_prompt_tokens"] = jseq.length - len(jids)
             stats["judge_prefill_s"] = t_jp - t_resp
             stats["judge_decode_s"] = time.perf_counter() - t_jp
@@ -401,11 +429,13 @@ def main() -> None:
         elapsed = float(tt.item())
         # judge timings live on the judge's ranks: rank 0 is not one of them in config 5 at N > 4
         jt = torch.tensor([judge_stats.get(k, 0.0) for k in ("judge_prompt_tokens", "judge_prefill_s",
-                                                             "judge_decode_s")], dtype=torch.float64, device=cdev)
+                                                             "judge_decode_s", "judge_ttft_s")],
+                          dtype=torch.float64, device=cdev)
         dist.all_reduce(jt, op=dist.ReduceOp.MAX)
         judge_stats = dict(judge_stats, judge_prompt_tokens=int(jt[0].item()), judge_prefill_s=float(jt[1].item()),
-                           judge_decode_s=float(jt[2].item()))
+                           judge_decode_s=float(jt[2].item()), judge_ttft_s=float(jt[3].item()))
     if rank == 0:
+        names = [e["name"] for e in resp_plan]
         value = tot_tokens / elapsed
         resp_tok_s = n_resp * args.max_tokens * args.steps / sum(p["responders_s"] for p in per_step)
         jtp = len(judge_plan["ranks"])
@@ -444,6 +474,16 @@ def main() -> None:
                 "judge_prompt_tokens": judge_stats.get("judge_prompt_tokens", 0),
                 "judge_prefill_s": round(judge_stats.get("judge_prefill_s", 0.0), 3),
                 "judge_decode_s": round(judge_stats.get("judge_decode_s", 0.0), 3),
+                # the judge's first token after the last response (incremental prefill + one sample)
+                "judge_ttft_s": round(judge_stats.get("judge_ttft_s", 0.0), 3),
+                # per responder, median over the timed rounds (reference result.json latency_ms;
+                # raw ns as the reference's time.Duration would hold it)
+                "per_model_latency_ms": {m: round(1000 * statistics.median(p["per_model"][m]["latency_s"]
+                                                                          for p in per_step), 1) for m in names},
+                "per_model_latency_ns": {m: int(1e9 * statistics.median(p["per_model"][m]["latency_s"]
+                                                                       for p in per_step)) for m in names},
+                "per_model_ttft_ms": {m: round(1000 * statistics.median(p["per_model"][m]["ttft_s"] for p in per_step), 1)
+                                      for m in names},
                 "judge_tp": jtp,
                 "warmup_rounds_tokens": [args.max_tokens] + [args.warmup_tokens or args.max_tokens] * max(0, args.warmup - 1),
                 "custom_allreduce": {e.name: e.tp.custom is not None for _, e, _, _ in responders if e.tp.size > 1}

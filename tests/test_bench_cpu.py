@@ -27,6 +27,11 @@ def _tokens_ok(d, max_tokens):
     tokens = (d["config"]["global_batch"] + 1) * max_tokens
     assert abs(d["value"] - tokens / (d["ms_per_step"] / 1000)) < 0.02 * d["value"]
     assert d["extra"]["judge_prompt_tokens"] > 0 and d["extra"]["judge_decode_s"] > 0
+    # per-model latency / TTFT of every responder, whichever rank ran it
+    lat, ttft = d["extra"]["per_model_latency_ms"], d["extra"]["per_model_ttft_ms"]
+    assert len(lat) == d["config"]["global_batch"] and set(lat) == set(ttft)
+    assert all(0 < ttft[m] <= lat[m] for m in lat)
+    assert 0 < d["extra"]["judge_ttft_s"] < d["ms_per_step"] / 1000
 
 
 def test_fanout_one_rank_runs_judge():

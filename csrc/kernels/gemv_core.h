@@ -57,9 +57,10 @@ struct ArEpi {
   long cap;       // bytes per data parity
 };
 
-// Batched decode (3 <= M <= 16 rows): the MFMA form in gemv_mfma.hip, same prologue/epilogues.
-// This kernel serves M <= kGemvMaxM (and M <= 4 when K is not a multiple of 128).
-constexpr int kGemvMaxM = 2, kGemvmMaxM = 16;
+// Batched decode (3 <= M <= 32 rows): the MFMA form in gemv_mfma.hip, same prologue/epilogues
+// (one 16-token MFMA column group up to 16 rows, two above). This kernel serves M <= kGemvMaxM
+// (and M <= 4 when K is not a multiple of 128). MoE pairs stay within one token group.
+constexpr int kGemvMaxM = 2, kGemvmMaxM = 32, kMoeGemvmMaxTokens = 16;
 int gemvm_dispatch(int M, const void* x, int x_stride, const void* norm_w, float eps, const void* W, void* out,
                    int out_stride, int N, int K, int epi, const RopeEpi& rope, hipStream_t st, int form = 0);
 

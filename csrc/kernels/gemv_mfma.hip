@@ -1,5 +1,5 @@
-// K6 (batched-decode class): y[m, n] = sum_k x[m, k] * W[n, k] for M = 5..16 rows on the matrix
-// cores — the decode step of a continuous batch of up to 16 sequences per engine.
+// K6 (batched-decode class): y[m, n] = sum_k x[m, k] * W[n, k] for M = 3..32 rows on the matrix
+// cores — the decode step of a continuous batch of up to 32 sequences per engine.
 //
 // Why a third GEMM shape: the VALU GEMV (gemv_core.h) does 8 v_dot2 per 16-B weight chunk per row,
 // so past ~4 rows it turns VALU- and LDS-bound, and the 256 x 256 prefill GEMM launches only
@@ -20,6 +20,9 @@
 //    already loaded (no extra pass over x).
 //  * split-K partials meet in LDS (S x 1 KiB); wave 0 runs the fused epilogue: bf16 | f32 |
 //    residual add | SiLU-mul | RoPE + paged-KV write (same semantics as the GEMV's).
+//  * 17-32 rows (TG = 2 token groups): every A fragment feeds two MFMAs, one per 16-token column
+//    group, so the weights still stream once for all rows; each group has its own B fragments,
+//    accumulators and norm sums.
 // K % 128 == 0 (every model shape); other K take the GEMM path (ops.linear / ops.qkv_rope).
 #include "gemv_core.h"
 
@@ -113,19 +116,20 @@ __device__ __forceinline__ void gemvm_epilogue(const f32x4& v, int nb, int m, in
 }
 
 
-template <int S, int RB, int XL, int PRO, int EPI, bool EXP>
+template <int S, int RB, int XL, int PRO, int EPI, bool EXP, int TG>
 __global__ __launch_bounds__(S * 64) void gemvm_kernel(const bf16_t* __restrict__ x, int x_stride,
                                                        const bf16_t* __restrict__ norm_w, float eps,
                                                        const bf16_t* __restrict__ W, void* __restrict__ out,
                                                        int out_stride, int M, int N, int K, RopeEpi rope,
                                                        ExpertMap ex) {
+  static_assert(TG == 1 || (TG == 2 && !EXP), "MoE pairs fit one token group");
   constexpr int TK = 128;       // k per tile: one 256-B LDS bank row per matrix row
   constexpr int WR = 16 * RB;   // weight rows per block (RB 16-row groups share every x fragment)
   constexpr int TB = 16 * TK * 2;
-  // per-wave transposition tiles: RB weight row groups (+ the 16 token rows of x when XL)
-  __shared__ __attribute__((aligned(16))) char lds_t[S][(RB + XL) * TB];
-  __shared__ f32x4 red[S][RB][64];
-  __shared__ float ssr[S][16];
+  // per-wave transposition tiles: RB weight row groups (+ the 16 * TG token rows of x when XL)
+  __shared__ __attribute__((aligned(16))) char lds_t[S][(RB + XL * TG) * TB];
+  __shared__ f32x4 red[S][RB * TG][64];
+  __shared__ float ssr[S][16 * TG];
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int r = lane & 15, g = lane >> 4;
@@ -160,34 +164,42 @@ __global__ __launch_bounds__(S * 64) void gemvm_kernel(const bf16_t* __restrict_
   // x: XL = 1 -> row-contiguous loads transposed through LDS like the weights; XL = 0 -> the B
   // fragments straight from L2 (lane (r, g) loads x[r][32j + 8g ..]; few distinct token rows are
   // mostly broadcasts, cheaper than the LDS round trip)
-  const u32x4* xsrc[4];
+  const u32x4* xsrc[TG][4];
 #pragma unroll
-  for (int i = 0; i < 4; ++i)
-    xsrc[i] = XL ? reinterpret_cast<const u32x4*>(x + static_cast<int64_t>(xrow(4 * i + g)) * x_stride + kw + r * 8)
-                 : reinterpret_cast<const u32x4*>(x + static_cast<int64_t>(xrow(r)) * x_stride + kw + g * 8) + 4 * i;
+  for (int t = 0; t < TG; ++t)
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+      xsrc[t][i] = XL ? reinterpret_cast<const u32x4*>(x + static_cast<int64_t>(xrow(16 * t + 4 * i + g)) * x_stride + kw + r * 8)
+                      : reinterpret_cast<const u32x4*>(x + static_cast<int64_t>(xrow(16 * t + r)) * x_stride + kw + g * 8) + 4 * i;
   const u32x4* gp = reinterpret_cast<const u32x4*>(norm_w + kw + g * 8);  // PRO_NORM only
   char* tw = lds_t[wave];
   char* tx = tw + RB * TB;
 
-  auto issue = [&](u32x4 (&wv)[4 * RB], u32x4 (&xv)[4], u32x4 (&gv)[4], int t) {
+  auto issue = [&](u32x4 (&wv)[4 * RB], u32x4 (&xv)[TG][4], u32x4 (&gv)[4], int t) {
     const int tu = min(t, ntile - 1) * (TK / 8);  // 16-B units
 #pragma unroll
     for (int i = 0; i < 4 * RB; ++i) wv[i] = load16<true>(wsrc[i] + tu);
 #pragma unroll
-    for (int i = 0; i < 4; ++i) xv[i] = XL ? xsrc[i][tu] : xsrc[0][tu + 4 * i];
+    for (int q = 0; q < TG; ++q)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) xv[q][i] = XL ? xsrc[q][i][tu] : xsrc[q][0][tu + 4 * i];
     if constexpr (PRO == PRO_NORM) {
 #pragma unroll
       for (int j = 0; j < 4; ++j) gv[j] = gp[tu + 4 * j];
     }
   };
-  f32x4 acc[RB];
+  f32x4 acc[RB][TG];
 #pragma unroll
-  for (int b = 0; b < RB; ++b) acc[b] = f32x4{0.f, 0.f, 0.f, 0.f};
-  float ss = 0.f;
+  for (int b = 0; b < RB; ++b)
+#pragma unroll
+    for (int q = 0; q < TG; ++q) acc[b][q] = f32x4{0.f, 0.f, 0.f, 0.f};
+  float ss[TG];
+#pragma unroll
+  for (int q = 0; q < TG; ++q) ss[q] = 0.f;
   // row-major tiles -> this wave's LDS (chunk c of row q at 16-B slot c ^ q: conflict-free for the
   // 8-lane b128 write groups and the four 16-lane fragment-read groups) -> fragments (row r,
   // chunk 4j + g): A = weights of each row group, B = x (normalised on the way when PRO_NORM)
-  auto consume = [&](const u32x4 (&wv)[4 * RB], const u32x4 (&xv)[4], const u32x4 (&gv)[4]) {
+  auto consume = [&](const u32x4 (&wv)[4 * RB], const u32x4 (&xv)[TG][4], const u32x4 (&gv)[4]) {
 #pragma unroll
     for (int i = 0; i < 4 * RB; ++i) {
       const int q = 4 * i + g;  // weight row within the block
@@ -195,45 +207,54 @@ __global__ __launch_bounds__(S * 64) void gemvm_kernel(const bf16_t* __restrict_
     }
     if constexpr (XL) {
 #pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const int q = 4 * i + g;
-        *reinterpret_cast<u32x4*>(tx + q * 256 + ((r ^ q) << 4)) = xv[i];
-      }
+      for (int t = 0; t < TG; ++t)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const int q = 4 * i + g;
+          *reinterpret_cast<u32x4*>(tx + t * TB + q * 256 + ((r ^ q) << 4)) = xv[t][i];
+        }
     }
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
       const int slot = ((4 * j + g) ^ r) << 4;
-      u32x4 xb = XL ? *reinterpret_cast<const u32x4*>(tx + r * 256 + slot) : xv[j];
-      if constexpr (PRO == PRO_NORM) {
-        float f[8], w8[8];
-        unpack8(xb, f);
-        unpack8(gv[j], w8);
+      u32x4 xb[TG];
 #pragma unroll
-        for (int e = 0; e < 8; ++e) {
-          ss += f[e] * f[e];
-          f[e] *= w8[e];
+      for (int t = 0; t < TG; ++t) {
+        xb[t] = XL ? *reinterpret_cast<const u32x4*>(tx + t * TB + r * 256 + slot) : xv[t][j];
+        if constexpr (PRO == PRO_NORM) {
+          float f[8], w8[8];
+          unpack8(xb[t], f);
+          unpack8(gv[j], w8);
+#pragma unroll
+          for (int e = 0; e < 8; ++e) {
+            ss[t] += f[e] * f[e];
+            f[e] *= w8[e];
+          }
+          xb[t] = pack8(f);
         }
-        xb = pack8(f);
       }
 #pragma unroll
       for (int b = 0; b < RB; ++b) {
         const u32x4 a = *reinterpret_cast<const u32x4*>(tw + b * TB + r * 256 + slot);
-        acc[b] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, a), __builtin_bit_cast(bf16x8, xb),
-                                                         acc[b], 0, 0, 0);
+#pragma unroll
+        for (int t = 0; t < TG; ++t)
+          acc[b][t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, a),
+                                                              __builtin_bit_cast(bf16x8, xb[t]), acc[b][t], 0, 0, 0);
       }
     }
   };
-  u32x4 wc[4 * RB], xc[4], gc[4];
+  u32x4 wc[4 * RB], xc[TG][4], gc[4];
   issue(wc, xc, gc, 0);
   for (int t = 0; t + 1 < ntile; ++t) {
-    u32x4 wn[4 * RB], xn[4], gn[4];
+    u32x4 wn[4 * RB], xn[TG][4], gn[4];
     issue(wn, xn, gn, t + 1);
     consume(wc, xc, gc);
 #pragma unroll
     for (int i = 0; i < 4 * RB; ++i) wc[i] = wn[i];
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
-      xc[i] = xn[i];
+#pragma unroll
+      for (int q = 0; q < TG; ++q) xc[q][i] = xn[q][i];
       if constexpr (PRO == PRO_NORM) gc[i] = gn[i];
     }
   }
@@ -241,30 +262,39 @@ __global__ __launch_bounds__(S * 64) void gemvm_kernel(const bf16_t* __restrict_
 
   // ---- split-K reduction over the block's waves ----
 #pragma unroll
-  for (int b = 0; b < RB; ++b) red[wave][b][lane] = acc[b];
+  for (int b = 0; b < RB; ++b)
+#pragma unroll
+    for (int t = 0; t < TG; ++t) red[wave][b * TG + t][lane] = acc[b][t];
   if constexpr (PRO == PRO_NORM) {
-    ss += __shfl_xor(ss, 16, 64);
-    ss += __shfl_xor(ss, 32, 64);
-    if (g == 0) ssr[wave][r] = ss;
+#pragma unroll
+    for (int t = 0; t < TG; ++t) {
+      float v = ss[t];
+      v += __shfl_xor(v, 16, 64);
+      v += __shfl_xor(v, 32, 64);
+      if (g == 0) ssr[wave][16 * t + r] = v;
+    }
   }
   __syncthreads();
   if (wave != 0) return;
-  const int m = r;
-  if (m >= M) return;
-  float inv = 1.f;
-  if constexpr (PRO == PRO_NORM) {
-    float t = 0.f;
 #pragma unroll
-    for (int w = 0; w < S; ++w) t += ssr[w][m];
-    inv = rsqrtf(t / K + eps);
-  }
+  for (int t = 0; t < TG; ++t) {
+    const int m = 16 * t + r;
+    if (m >= M) continue;
+    float inv = 1.f;
+    if constexpr (PRO == PRO_NORM) {
+      float sum = 0.f;
 #pragma unroll
-  for (int b = 0; b < RB; ++b) {
-    f32x4 v = red[0][b][lane];
+      for (int w = 0; w < S; ++w) sum += ssr[w][m];
+      inv = rsqrtf(sum / K + eps);
+    }
 #pragma unroll
-    for (int w = 1; w < S; ++w) v += red[w][b][lane];
-    if constexpr (PRO == PRO_NORM) v *= inv;
-    gemvm_epilogue<EPI>(v, n0 + 16 * b + 4 * g, EXP ? pmap[m] : m, N, out, out_stride, rope);
+    for (int b = 0; b < RB; ++b) {
+      f32x4 v = red[0][b * TG + t][lane];
+#pragma unroll
+      for (int w = 1; w < S; ++w) v += red[w][b * TG + t][lane];
+      if constexpr (PRO == PRO_NORM) v *= inv;
+      gemvm_epilogue<EPI>(v, n0 + 16 * b + 4 * g, EXP ? pmap[m] : m, N, out, out_stride, rope);
+    }
   }
 }
 
@@ -272,9 +302,12 @@ __global__ __launch_bounds__(S * 64) void gemvm_kernel(const bf16_t* __restrict_
 // weight groups per wave from 6144 output rows (8B qkv / gate_up / lm_head: 3-8 % faster; the
 // 4096-row o_proj / down lose 25-45 % with half the blocks), x through LDS once the distinct token
 // rows make its fragment loads cost (12+ rows; 8+ with one group per wave).
+// Two token groups (17-32 rows): x from L2 with two row groups per wave (the LDS x tiles of both
+// token groups beside two weight groups would not fit 160 KiB at 8 waves), x through LDS with one.
 static int gemvm_form(int M, int N, int K) {
   (void)K;
   const bool rb2 = N >= 6144;
+  if (M > 16) return rb2 ? 3 : 2;
   const bool xl = rb2 ? M >= 12 : M >= 8;
   return 1 + (xl ? 1 : 0) + (rb2 ? 2 : 0);
 }
@@ -284,7 +317,15 @@ static int launch_gemvm_s(const void* x, int x_stride, const void* nw, float eps
                           int out_stride, int M, int N, int K, const RopeEpi& rope, const ExpertMap& ex,
                           hipStream_t st) {
   const dim3 grid((N + 16 * RB - 1) / (16 * RB), EXP ? ex.E : 1);
-  gemvm_kernel<S, RB, XL, PRO, EPI, EXP><<<grid, S * 64, 0, st>>>(
+  if constexpr (!EXP && !(RB == 2 && XL == 1)) {
+    if (M > 16) {
+      gemvm_kernel<S, RB, XL, PRO, EPI, EXP, 2><<<grid, S * 64, 0, st>>>(
+          (const bf16_t*)x, x_stride, (const bf16_t*)nw, eps, (const bf16_t*)W, out, out_stride, M, N, K, rope, ex);
+      return static_cast<int>(hipGetLastError());
+    }
+  }
+  if (M > 16) return -6;  // two token groups: not with two LDS x tiles beside two weight groups
+  gemvm_kernel<S, RB, XL, PRO, EPI, EXP, 1><<<grid, S * 64, 0, st>>>(
       (const bf16_t*)x, x_stride, (const bf16_t*)nw, eps, (const bf16_t*)W, out, out_stride, M, N, K, rope, ex);
   return static_cast<int>(hipGetLastError());
 }
@@ -361,7 +402,7 @@ int gemvm_dispatch(int M, const void* x, int x_stride, const void* norm_w, float
 
 }  // namespace llmc
 
-// Direct entry (tests / microbenchmarks: the MFMA form at any M <= 16).
+// Direct entry (tests / microbenchmarks: the MFMA form at any M <= 32).
 extern "C" int llmc_gemvm(int M, const void* x, int x_stride, const void* norm_w, float eps, const void* W, void* out,
                           int out_stride, int N, int K, int epi, int form, hipStream_t s) {
   if (epi == llmc::EPI_ROPE) return -5;
@@ -386,14 +427,14 @@ extern "C" int llmc_moe_gemvm(int P, const void* x, int x_stride, const void* no
   const bool norm = norm_w != nullptr;
   switch (epi) {
     case EPI_BF16:
-      return norm ? launch_gemvm<PRO_NORM, EPI_BF16, true>(x, x_stride, norm_w, eps, W, out, out_stride, kGemvmMaxM, N, K,
+      return norm ? launch_gemvm<PRO_NORM, EPI_BF16, true>(x, x_stride, norm_w, eps, W, out, out_stride, kMoeGemvmMaxTokens, N, K,
                                                            rope, form, s, ex)
-                  : launch_gemvm<PRO_NONE, EPI_BF16, true>(x, x_stride, norm_w, eps, W, out, out_stride, kGemvmMaxM, N, K,
+                  : launch_gemvm<PRO_NONE, EPI_BF16, true>(x, x_stride, norm_w, eps, W, out, out_stride, kMoeGemvmMaxTokens, N, K,
                                                            rope, form, s, ex);
     case EPI_SILU:
-      return norm ? launch_gemvm<PRO_NORM, EPI_SILU, true>(x, x_stride, norm_w, eps, W, out, out_stride, kGemvmMaxM, N, K,
+      return norm ? launch_gemvm<PRO_NORM, EPI_SILU, true>(x, x_stride, norm_w, eps, W, out, out_stride, kMoeGemvmMaxTokens, N, K,
                                                            rope, form, s, ex)
-                  : launch_gemvm<PRO_NONE, EPI_SILU, true>(x, x_stride, norm_w, eps, W, out, out_stride, kGemvmMaxM, N, K,
+                  : launch_gemvm<PRO_NONE, EPI_SILU, true>(x, x_stride, norm_w, eps, W, out, out_stride, kMoeGemvmMaxTokens, N, K,
                                                            rope, form, s, ex);
     default: return -4;
   }

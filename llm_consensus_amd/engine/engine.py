@@ -40,7 +40,7 @@ from ..utils.native import runtime
 class EngineConfig:
     device: str = "cuda:0"
     max_context: int = 8192
-    max_batch: int = 1   # decode rows per step (weight-streaming GEMV/MFMA form: M <= 16)
+    max_batch: int = 1   # decode rows per step (weight-streaming GEMV/MFMA form: M <= 32; MoE <= 16)
     max_seqs: int = 0    # live sequences the KV pool is sized for (0 = max_batch)
     block_size: int = 64
     kv_blocks: int = 0
@@ -830,7 +830,7 @@ class Engine:
     @torch.no_grad()
     def debug_decode_logits_batch(self, prompts: List[Seq[int]], n: int):
         """``debug_decode_logits`` for B = len(prompts) rows decoded together (the batched decode
-        GEMV forms: VALU rows <= 4, MFMA 5-16): (tokens [B][n], logits [B, n, V] f32)."""
+        GEMV forms: VALU rows <= 2, MFMA 3-32): (tokens [B][n], logits [B, n, V] f32)."""
         if self.tp.size != 1:
             raise EngineError("debug_decode_logits: TP=1 only")
         B = len(prompts)

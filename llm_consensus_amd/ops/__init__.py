@@ -16,7 +16,8 @@ from ..utils.native import kernels
 from . import oracle
 
 EPI_BF16, EPI_F32, EPI_RESADD, EPI_SILU, EPI_ROPE = 0, 1, 2, 3, 4
-GEMV_MAX_M = 16      # decode rows on the weight-streaming path (VALU GEMV 1-2, MFMA form 3-16)
+GEMV_MAX_M = 32      # decode rows on the weight-streaming path (VALU GEMV 1-2, MFMA form 3-32)
+MOE_GEMVM_MAX_TOKENS = 16  # batched MoE decode: (token, expert) pairs of <= 16 tokens per launch
 MOE_GEMV_MAX_M = 4   # MoE: per-(row, expert) GEMVs up to this many rows, then the grouped GEMM
 
 
@@ -73,8 +74,8 @@ def linear(x: torch.Tensor, W: torch.Tensor, epi: int = EPI_BF16, out: Optional[
            norm_w: Optional[torch.Tensor] = None, eps: float = 1e-5, mfma: bool = False) -> torch.Tensor:
     """y = (rmsnorm(x)*norm_w if norm_w else x) @ W^T with a fused epilogue.
 
-    M <= 16 rows -> weight streaming (decode; the norm runs in its prologue): the VALU GEMV for 1-2
-    rows, the MFMA form for 3-16 (``mfma`` pins the MFMA form at every row count: a batching
+    M <= 32 rows -> weight streaming (decode; the norm runs in its prologue): the VALU GEMV for 1-2
+    rows, the MFMA form for 3-32 (one 16-token column group up to 16 rows, two above) (``mfma`` pins the MFMA form at every row count: a batching
     engine's decode stays batch-invariant); larger M -> the 256x256 MFMA prefill GEMM
     (csrc/kernels/gemm.hip; a norm is a separate rmsnorm launch first).
     Epilogues: bf16 | f32 | EPI_RESADD (accumulates into ``out`` in place) | EPI_SILU (interleaved
@@ -118,7 +119,7 @@ def gemm(x: torch.Tensor, W: torch.Tensor, epi: int = EPI_BF16, out: Optional[to
 
 def gemv(x: torch.Tensor, W: torch.Tensor, epi: int = EPI_BF16, out: Optional[torch.Tensor] = None,
          norm_w: Optional[torch.Tensor] = None, eps: float = 1e-5, mfma: bool = False) -> torch.Tensor:
-    """Always the weight-streaming path (M <= 16; the kernel library picks VALU / MFMA form)."""
+    """Always the weight-streaming path (M <= 32; the kernel library picks VALU / MFMA form)."""
     if not x.is_cuda:
         return oracle.linear(x, W, epi, out, norm_w, eps)
     M, K = x.shape
@@ -133,8 +134,8 @@ def gemv(x: torch.Tensor, W: torch.Tensor, epi: int = EPI_BF16, out: Optional[to
 
 def gemvm(x: torch.Tensor, W: torch.Tensor, epi: int = EPI_BF16, out: Optional[torch.Tensor] = None,
           norm_w: Optional[torch.Tensor] = None, eps: float = 1e-5, form: int = 0) -> torch.Tensor:
-    """Always the MFMA weight-streaming form (gemv_mfma.hip; M <= 16) — tests / microbenchmarks
-    (``linear``/``gemv`` take it by themselves for 3 <= M <= 16). ``form`` 0 = by shape, 1-4 pin
+    """Always the MFMA weight-streaming form (gemv_mfma.hip; M <= 32) — tests / microbenchmarks
+    (``linear``/``gemv`` take it by themselves for 3 <= M <= 32). ``form`` 0 = by shape, 1-4 pin
     (row groups per wave, x path) = (1, L2), (1, LDS), (2, L2), (2, LDS)."""
     if not x.is_cuda:
         return oracle.linear(x, W, epi, out, norm_w, eps)
@@ -322,14 +323,14 @@ def moe_gemv(x, W_experts, ids, x_div, out, N, K, epi, norm_w=None, eps: float =
 
 
 def moe_gemvm(x, W_experts, ids, x_div, out, N, K, epi, norm_w=None, eps: float = 1e-5):
-    """Batched MoE decode (<= 16 tokens) on the MFMA form with the pairs grouped by expert: every
+    """Batched MoE decode (<= MOE_GEMVM_MAX_TOKENS tokens) on the MFMA form with the pairs grouped by expert: every
     routed expert's weights stream once for all its pairs (``moe_gemv`` streams them once per pair).
     out[p] = W[ids[p]] . x[p // x_div]; pairs with id -1 (another rank's expert) are not written."""
     if not x.is_cuda:
         raise ValueError("moe_gemvm: GPU only (the CPU path is moe_gemv's oracle)")
     P, E = ids.numel(), W_experts.shape[0]
-    if ids.dim() != 2 or ids.shape[0] > GEMV_MAX_M:
-        raise ValueError(f"moe_gemvm: ids [tokens <= {GEMV_MAX_M}, k], got {tuple(ids.shape)}")
+    if ids.dim() != 2 or ids.shape[0] > MOE_GEMVM_MAX_TOKENS:
+        raise ValueError(f"moe_gemvm: ids [tokens <= {MOE_GEMVM_MAX_TOKENS}, k], got {tuple(ids.shape)}")
     kernels().moe_gemvm(P, _p(x), x.stride(0), _p(norm_w) if norm_w is not None else 0, float(eps), _p(W_experts),
                         _p(ids), x_div, E, _p(out), out.stride(0), N, K, epi, _s(x))
     return out

@@ -117,6 +117,17 @@ class _Worker:
                 self.backend._deliver(msg)
 
 
+# = ops.GEMV_MAX_M / ops.MOE_GEMVM_MAX_TOKENS (not imported: the driver process stays torch-free;
+# tests/test_placement.py checks they agree)
+DECODE_ROWS_MAX, MOE_DECODE_ROWS_MAX = 32, 16
+
+
+def max_decode_rows(cfg) -> int:
+    """Decode rows one engine batches per step: the MFMA weight-streaming form takes 32 token rows
+    (two 16-token column groups); batched MoE decode groups (row, expert) pairs of <= 16 tokens."""
+    return MOE_DECODE_ROWS_MAX if cfg.is_moe else DECODE_ROWS_MAX
+
+
 class LocalBackend:
     """Owns the worker processes of one run and routes requests to them."""
 
@@ -199,9 +210,9 @@ class LocalBackend:
                     n, sess = seqs[m]
                     models.append({"name": m, "family": s.family, "seed": s.seed, "max_context": self._ctx[m],
                                    "checkpoint": s.config.checkpoint, "kv_blocks": kv_blocks[m],
-                                   # decode rows per step: up to 16 on the weight-streaming
-                                   # GEMV / MFMA form (MoE: pairs grouped by expert)
-                                   "max_batch": max(1, min(16, max(n, sess))),
+                                   # decode rows per step: up to 32 on the weight-streaming
+                                   # GEMV / MFMA form (MoE: 16, pairs grouped by expert)
+                                   "max_batch": max(1, min(max_decode_rows(s.config), max(n, sess))),
                                    "max_seqs": max(1, n) + sess})
             if groups:
                 dist_info = {"port": port, "rank": rank_of[g], "world": len(used),

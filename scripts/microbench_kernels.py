@@ -168,7 +168,7 @@ def bench_gemv_sweep(shapes=None):
 
 def bench_batched_decode(shapes=None, rows=(1, 2, 3, 4, 5, 8, 12, 16)):
     """Batched decode projections on COLD weights: the dispatcher's form per row count (VALU GEMV
-    for M <= 2, MFMA form 3-16) and the MFMA form forced at every M, with the fused norm prologue
+    for M <= 2, MFMA form 3-32) and the MFMA form forced at every M, with the fused norm prologue
     where the layer has one (qkv, gate_up, lm_head) and the residual add elsewhere."""
     from llm_consensus_amd import ops
 
@@ -214,7 +214,7 @@ def bench_gemvm_forms(shapes=None, rows=(3, 4, 5, 8, 12, 16)):
             n_out = N // 2 if epi == 3 else N
             out = torch.zeros(M, n_out, dtype=torch.float32 if epi == 1 else BF, device="cuda")
             res = []
-            for form in (0, 1, 2, 3, 4):
+            for form in (0, 1, 2, 3, 4) if M <= 16 else (0, 1, 2, 3):  # 17-32 rows: no form 4 (LDS)
                 def run():
                     for W in Ws:
                         ops.gemvm(x, W, epi, out=out, norm_w=nw, form=form)
@@ -320,6 +320,9 @@ if __name__ == "__main__":
         bench_gemvm_forms()
     if what in ("batched",):  # decode projections at continuous-batching row counts
         bench_batched_decode()
+    if what in ("batched32",):  # two 16-token column groups (17-32 rows) against 16
+        bench_batched_decode(rows=(8, 16, 17, 24, 32))
+        bench_gemvm_forms(rows=(24, 32))
     if what in ("qkv-rope",):
         bench_qkv_rope()
     if what in ("prefill",):

@@ -103,13 +103,14 @@ def test_batched_rows_equal_single(cuda):
     assert both[0] == one and both[1] == two
 
 
-@pytest.mark.parametrize("name,B", [("llama-tiny", 8), ("phi3-tiny", 16), ("llama-small", 5), ("mixtral-tiny", 12)])
+@pytest.mark.parametrize("name,B", [("llama-tiny", 8), ("phi3-tiny", 16), ("llama-small", 5), ("mixtral-tiny", 12),
+                                    ("llama-tiny", 32), ("phi3-tiny", 21)])
 def test_batched_decode_rows_match_oracle(cuda, name, B):
     """Continuous batching past 4 rows (the MFMA decode form): B different prompts decoded in ONE
     batch, teacher-forced at every step against the CPU oracle's prefill of each row's prompt +
     tokens so far (fused norm / RoPE / KV-write / SiLU / residual epilogues at M = B; Mixtral: the
     pairs grouped by expert)."""
-    cfg, ecpu, egpu = _pair(name, max_batch=16)
+    cfg, ecpu, egpu = _pair(name, max_batch=max(16, B))
     prompts = [[(i * (53 + 2 * r)) % (cfg.vocab - 300) + 256 for i in range(20 + 3 * r)] for r in range(B)]
     n = 5
     toks, lg = egpu.debug_decode_logits_batch(prompts, n)

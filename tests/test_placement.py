@@ -92,3 +92,29 @@ def test_kv_pool_blocks_fit_the_gpu():
     # one request in flight: the asks fit, every engine gets all it asked for
     one = kv_pool_blocks(pl, specs, ctx, {"llama-3-8b@0": 1, "llama-3-8b@1": 1, "llama-3-8b@judge": 2})
     assert one["llama-3-8b@judge"] * KV_BLOCK >= 2 * JUDGE_CONTEXT
+
+
+def test_decode_row_caps_match_the_kernels():
+    """The driver's per-engine decode-row cap (torch-free) equals the op layer's limits."""
+    from llm_consensus_amd import ops
+    from llm_consensus_amd.models.config import FAMILIES
+    from llm_consensus_amd.provider import local
+
+    assert local.DECODE_ROWS_MAX == ops.GEMV_MAX_M
+    assert local.MOE_DECODE_ROWS_MAX == ops.MOE_GEMVM_MAX_TOKENS
+    assert local.max_decode_rows(FAMILIES["mixtral-8x7b"]) == 16
+    assert local.max_decode_rows(FAMILIES["llama-3-8b"]) == 32
+
+
+def test_driver_process_stays_torch_free():
+    """The CLI / server driver plans placement and spawns the GPU workers without importing torch
+    (its ~2 s import would sit on the startup path before any worker starts)."""
+    import subprocess
+    import sys
+
+    code = ("import sys, llm_consensus_amd.cli, llm_consensus_amd.provider.local, "
+            "llm_consensus_amd.runtime.worker, llm_consensus_amd.server, llm_consensus_amd.parallel.placement; "
+            "print('torch' in sys.modules)")
+    r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stderr
+    assert r.stdout.strip() == "False"

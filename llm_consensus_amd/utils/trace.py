@@ -11,6 +11,7 @@ from __future__ import annotations
 import contextlib
 import json
 import os
+import sys
 import threading
 import time
 from typing import Dict, List
@@ -18,7 +19,12 @@ from typing import Dict, List
 _enabled = os.environ.get("LLMC_TRACE", "0") == "1"
 _lock = threading.Lock()
 _events: List[Dict] = []
-_t0 = time.perf_counter_ns()
+# Timestamps: CLOCK_MONOTONIC, which is system-wide on Linux, so the driver's and every worker's
+# events share one time axis in the merged trace (a per-process origin would shift them apart).
+
+
+def _now_us() -> float:
+    return time.clock_gettime_ns(time.CLOCK_MONOTONIC) / 1000.0
 
 
 def enable(on: bool = True) -> None:
@@ -31,9 +37,12 @@ def enabled() -> bool:
 
 
 def _roctx():
+    """roctx in processes that already run torch (the GPU workers); the torch-free driver never
+    imports it for a trace span (a ~2 s import inside a query's span)."""
+    torch = sys.modules.get("torch")
+    if torch is None:
+        return None
     try:
-        import torch
-
         if torch.cuda.is_available() and hasattr(torch.cuda, "nvtx"):
             return torch.cuda.nvtx
     except Exception:  # noqa: BLE001
@@ -52,14 +61,14 @@ def span(name: str, cat: str = "engine", **args):
             rx.range_push(name)
         except Exception:  # noqa: BLE001
             rx = None
-    t = time.perf_counter_ns()
+    t = _now_us()
     try:
         yield
     finally:
-        d = time.perf_counter_ns() - t
+        d = _now_us() - t
         if rx is not None:
             rx.range_pop()
-        ev = {"name": name, "cat": cat, "ph": "X", "ts": (t - _t0) / 1000.0, "dur": d / 1000.0,
+        ev = {"name": name, "cat": cat, "ph": "X", "ts": t, "dur": d,
               "pid": os.getpid(), "tid": threading.get_ident() % 100000, "args": args}
         with _lock:
             _events.append(ev)
@@ -68,7 +77,7 @@ def span(name: str, cat: str = "engine", **args):
 def instant(name: str, cat: str = "engine", **args) -> None:
     if not _enabled:
         return
-    ev = {"name": name, "cat": cat, "ph": "i", "s": "p", "ts": (time.perf_counter_ns() - _t0) / 1000.0,
+    ev = {"name": name, "cat": cat, "ph": "i", "s": "p", "ts": _now_us(),
           "pid": os.getpid(), "tid": threading.get_ident() % 100000, "args": args}
     with _lock:
         _events.append(ev)

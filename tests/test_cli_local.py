@@ -33,6 +33,14 @@ def test_cli_local_models_cpu_workers(tmp_path):
     tr = json.loads((run / "trace.json").read_text())
     names = {e["name"] for e in tr["traceEvents"]}
     assert {"prefill", "decode", "query"} <= names
+    # one time axis for the driver and the workers: every worker decode span of a responder lies
+    # inside the driver's query span of that model
+    q = [e for e in tr["traceEvents"] if e["name"] == "query"]
+    dec = [e for e in tr["traceEvents"] if e["name"] == "decode"]
+    assert {e["pid"] for e in q}.isdisjoint({e["pid"] for e in dec})
+    q0, q1 = min(e["ts"] for e in q), max(e["ts"] + e["dur"] for e in q)
+    first_dec = min(e["ts"] for e in dec)
+    assert q0 <= first_dec <= q1, (q0, first_dec, q1)
 
 
 def test_cli_duplicate_local_model_batched_cpu():

@@ -59,6 +59,7 @@ class EngineConfig:
 
 
 FUSED_CHUNK_SMALL, FUSED_CHUNK_LARGE = 128, 256
+BATCHING_MIN_KEYS = 2048  # batching engines: minimum keys per split block (see attn_buckets)
 
 
 def attn_buckets(ctxmax: int, blocks_per_head: int = 32, fused_max: int = 4096, group: int = 4,
@@ -78,20 +79,22 @@ def attn_buckets(ctxmax: int, blocks_per_head: int = 32, fused_max: int = 4096, 
     the fused form (page size not a multiple of 32 keys).
 
     An engine batching ``rows`` >= 3 decode rows whose rows x kv heads give >= 32 independent
-    (row, head) units takes its parallelism from the rows: every bucket is the balanced split at
-    256 / (rows x nkv) blocks per kv head (16 rows of the 8B: 2 blocks, 31 vs 44-79 µs for the
-    fused forms at 2.5k keys; profiles/r2_batched_decode.md). The partition of a row's keys then
-    depends on its own length only, not on the bucket the batch's longest row selects."""
+    (row, head) units uses the balanced split with a BATCHING_MIN_KEYS (2048) minimum per block
+    over min(32, capacity / 2048) blocks per kv head: a row of L keys is split into min(32,
+    ceil(L / 2048)) ranges whatever the bucket and whatever else is batched (batch-invariant
+    tokens), so a lone long row still spreads over the chip (8B at 13.5k keys: 30 µs vs 141 for
+    one block per (row, head)) while 32 rows stay within 1.2x of it
+    (profiles/r2_batched_decode.md, `microbench_kernels.py attn-rows`)."""
     out, cap = [], 1024
     if rows >= 3 and rows * nkv >= 32:
-        per_head = max(1, 256 // (rows * nkv))
+        mk = BATCHING_MIN_KEYS
         while True:
             c = min(cap, ctxmax)
-            gc = min((c + 127) // 128, per_head)
+            gc = min(32, (c + mk - 1) // mk)
             if out and out[-1][2] == gc:
-                out[-1] = (c, 128, gc, False)
+                out[-1] = (c, mk, gc, False)
             else:
-                out.append((c, 128, gc, False))
+                out.append((c, mk, gc, False))
             if cap >= ctxmax:
                 return out
             cap *= 2

@@ -296,6 +296,36 @@ def bench_prefill():
         print(f"attn_prefill T={T} ctx={ctx}: {us:8.1f} us {fl / us / 1e6:6.0f} TF/s", flush=True)
 
 
+def bench_attn_rows_policy(rows=(1, 2, 4, 8, 16, 32), lens=(700, 2560, 8192, 13500)):
+    """Batching engines' decode attention: the grid a batch-invariant policy can use. 'rowsN' = the
+    balanced split at max(1, 256 / (N x nkv)) blocks per kv head for an engine sized for N rows
+    (every B); 'mcK' = the split with a K-key minimum per block over min(32, capacity / K) blocks
+    per head for the power-of-two bucket capacity (a row's partition then depends on its own
+    length only). us per launch."""
+    nh, nkv, D = 32, 8, 128
+    sc = 1 / math.sqrt(D)
+    for L in lens:
+        for B in rows:
+            kc, vc, bt, sl, q, out = _attn_case(L, nh, nkv, D, B=B)
+            line = []
+            for eng_rows in (16, 32):
+                gc = max(1, 256 // (eng_rows * nkv))
+                part, ctr = ops.decode_attn_workspace(B, nh, nkv, D, gc, "cuda")
+                us = timeit(lambda: ops.attn_decode(q, kc, vc, bt, sl, out, part, ctr, nh, nkv, D, 64, 128, sc,
+                                                    grid_chunks=gc))
+                line.append(f"rows{eng_rows}(g{gc}) {us:7.2f}")
+            cap = 1024
+            while cap < L:
+                cap *= 2
+            for mc in (512, 1024, 2048):
+                gc = min(32, -(-cap // mc))  # the bucket's grid: no block beyond the capacity
+                part, ctr = ops.decode_attn_workspace(B, nh, nkv, D, gc, "cuda")
+                us = timeit(lambda: ops.attn_decode(q, kc, vc, bt, sl, out, part, ctr, nh, nkv, D, 64, mc, sc,
+                                                    grid_chunks=gc))
+                line.append(f"mc{mc}(g{gc}) {us:7.2f}")
+            print(f"attn-rows L={L:6d} B={B:2d}: " + "  ".join(line), flush=True)
+
+
 if __name__ == "__main__":
     what = sys.argv[1] if len(sys.argv) > 1 else "all"
     if what in ("launch", "all"):
@@ -320,6 +350,8 @@ if __name__ == "__main__":
         bench_gemvm_forms()
     if what in ("batched",):  # decode projections at continuous-batching row counts
         bench_batched_decode()
+    if what in ("attn-rows",):  # batching engines' attention grid policy
+        bench_attn_rows_policy()
     if what in ("batched32",):  # two 16-token column groups (17-32 rows) against 16
         bench_batched_decode(rows=(8, 16, 17, 24, 32))
         bench_gemvm_forms(rows=(24, 32))

@@ -13,10 +13,11 @@ ap.add_argument("--prompt", type=int, default=512)
 ap.add_argument("--no-graphs", action="store_true")
 ap.add_argument("--ctx", type=int, default=8192)
 ap.add_argument("--batch", type=int, default=1, help="decode rows per step (continuous-batching engine)")
+ap.add_argument("--engine-rows", type=int, default=0, help="engine max_batch (0 = --batch): e.g. one row on a serving engine")
 a = ap.parse_args()
 cfg = FAMILIES[a.model]
 e = Engine(cfg, EngineConfig(device="cuda:0", max_context=a.ctx, seed=1, use_graphs=not a.no_graphs,
-                             max_batch=a.batch))
+                             max_batch=max(a.batch, a.engine_rows)))
 prompt = [(i * 7919) % 30000 + 256 for i in range(a.prompt)]
 if a.batch > 1:
     from llm_consensus_amd.engine import SamplingParams

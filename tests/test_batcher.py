@@ -98,3 +98,24 @@ def test_continuous_batching_cancelled_row_cpu():
     assert isinstance(done[0].error, ContextError)
     for i in (1, 2):
         assert done[i].error is None and done[i].tokens == ref[i]
+
+
+@pytest.mark.gpu
+def test_batching_engine_long_rows_batch_invariant(cuda):
+    """A batching engine (16 rows x 2 kv heads: the length-only attention split, min 2048 keys per
+    block) over rows of very different lengths: a 3000-key row (two split ranges) decoded beside
+    short rows, whose batch selects larger buckets than they would alone, still gets exactly its
+    solo tokens, and so do they."""
+    eng = Engine(FAMILIES["llama-tiny"], EngineConfig(device="cuda:0", max_context=4000, max_batch=16, max_seqs=6,
+                                                      seed=13))
+    reqs = [
+        ([(7 * i) % 900 + 100 for i in range(3000)], SamplingParams(max_tokens=24, temperature=0.0, stop_on_eos=False)),
+        ([500 + i for i in range(9)], SamplingParams(max_tokens=20, temperature=0.0, stop_on_eos=False)),
+        ([(11 * i) % 800 + 150 for i in range(2100)], SamplingParams(max_tokens=16, temperature=1.0, seed=3,
+                                                                     stop_on_eos=False)),
+        ([100 + i for i in range(5)], SamplingParams(max_tokens=12, temperature=0.0, stop_on_eos=False)),
+    ]
+    ref = [_alone(eng, p, sp) for p, sp in reqs]
+    got = _run_schedule(eng, reqs, admit_at=[0, 0, 1, 2])
+    for i, (g, r) in enumerate(zip(got, ref)):
+        assert g == r, (i, g, r)

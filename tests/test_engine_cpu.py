@@ -129,18 +129,29 @@ def test_attn_buckets_cover_context():
 
 
 def test_attn_buckets_batching_engine():
-    """A 16-row (or 4-row) 8B engine takes its attention parallelism from the rows: the balanced
-    split at 256 / (rows x kv heads) blocks per head in every bucket, i.e. one bucket / graph per
-    batch size; engines of 1-2 rows, or rows x kv heads < 32, keep the per-context forms."""
+    """A batching 8B engine (>= 3 rows, rows x kv heads >= 32) splits a row of L keys into
+    min(32, ceil(L / 2048)) ranges whatever its bucket and batch: the grid per head is min(32,
+    capacity / 2048), so the kernel's min(grid, ceil(L / 2048)) never depends on the bucket;
+    engines of 1-2 rows, or rows x kv heads < 32, keep the per-context forms."""
+    import math
+
+    from llm_consensus_amd.engine.engine import BATCHING_MIN_KEYS as MK
     from llm_consensus_amd.engine.engine import attn_buckets
 
-    assert attn_buckets(16394, 32, rows=16) == [(16394, 128, 2, False)]
-    assert attn_buckets(16394, 32, rows=4) == [(16394, 128, 8, False)]
+    b16 = attn_buckets(131082, 32, rows=16)
+    assert all(ch == MK and not fused for _, ch, _, fused in b16)
+    assert [(c, g) for c, _, g, _ in b16] == [(2048, 1), (4096, 2), (8192, 4), (16384, 8), (32768, 16),
+                                              (131082, 32)]
+    assert attn_buckets(131082, 32, rows=4) == b16 == attn_buckets(131082, 32, rows=32)
+    # batch invariance: the split a row gets is a function of its own length only
+    for L in (1, 700, 2048, 2049, 5000, 13500, 40000, 131000):
+        splits = {min(g, math.ceil(L / MK)) for c, _, g, _ in b16 if c >= L}
+        assert len(splits) == 1 and splits.pop() == min(32, math.ceil(L / MK)), L
     assert attn_buckets(16394, 32, rows=2) == attn_buckets(16394, 32)
     assert attn_buckets(16394, 32, nkv=2, rows=8) == attn_buckets(16394, 32, nkv=2)   # 16 units
-    assert attn_buckets(4106, 16, group=1, nkv=32, rows=4) == [(4106, 128, 2, False)]  # Phi-3
-    # short contexts: never more blocks than 128-key ranges
-    assert attn_buckets(200, 32, rows=4) == [(200, 128, 2, False)]
+    assert attn_buckets(4106, 16, group=1, nkv=32, rows=4) == [(2048, MK, 1, False), (4096, MK, 2, False),
+                                                               (4106, MK, 3, False)]  # Phi-3
+    assert attn_buckets(200, 32, rows=4) == [(200, MK, 1, False)]
 
 
 def test_split_blocks_per_head():

@@ -239,6 +239,7 @@ def run(argv: List[str], stdout: TextIO = sys.stdout, stderr: TextIO = sys.stder
         from .utils import trace
 
         trace.enable(True)
+        trace.instant("cli_start", cat="startup")
     ctx = root_ctx or Context.background()
     show_ui = ui.is_terminal(stderr) and not cfg.quiet and not cfg.json
     start = time.monotonic()

@@ -223,6 +223,7 @@ class LocalBackend:
             p.start()
             b.close()
             self.workers[g] = _Worker(self, g, a, p)
+        tracing.instant("workers_spawned", cat="startup", n=len(self.workers))
         deadline = time.monotonic() + start_timeout
         for w in self.workers.values():
             if not w.ready.wait(max(0.0, deadline - time.monotonic())):

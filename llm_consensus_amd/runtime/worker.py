@@ -392,18 +392,22 @@ def worker_main(gpu: int, conn, models: List[dict], dist_info: Optional[dict], t
             conn.send(msg)
 
     try:
-        import torch
-
-        from ..context import Context
-        from ..engine import Engine, EngineConfig
-        from ..models.config import FAMILIES
-        from ..parallel.comm import TPGroup
         from ..utils import trace
 
         trace.enable(trace_on)
+        with trace.span("worker_import", cat="startup", gpu=gpu):
+            import torch
+
+            from ..context import Context
+            from ..engine import Engine, EngineConfig
+            from ..models.config import FAMILIES
+            from ..parallel.comm import TPGroup
+
         on_cpu = gpu < 0  # CPU worker (tests / no-GPU hosts): oracle op path, gloo collectives
         if not on_cpu:
-            torch.cuda.set_device(gpu)
+            with trace.span("device_init", cat="startup", gpu=gpu):
+                torch.cuda.set_device(gpu)
+                torch.zeros(1, device=f"cuda:{gpu}")  # HIP context + allocator up front
         groups = {}
         if dist_info:
             import torch.distributed as dist
@@ -444,7 +448,8 @@ def worker_main(gpu: int, conn, models: List[dict], dist_info: Optional[dict], t
                                 use_graphs=graphs,
                                 # MoE under TP: whole experts per rank (LLMC_EXPERT_PARALLEL=1)
                                 expert_parallel=os.environ.get("LLMC_EXPERT_PARALLEL", "0") == "1")
-            eng = Engine(cfg, ecfg, tp=tp, name=m["name"])
+            with trace.span("engine_init", cat="startup", engine=m["name"]):
+                eng = Engine(cfg, ecfg, tp=tp, name=m["name"])
             hosts[m["name"]] = _EngineHost(m["name"], eng, send, tp.is_leader, faults.get(m["name"]),
                                            on_finished=lambda rid: ctxs.pop(rid, None))
         if not on_cpu:

@@ -14,6 +14,7 @@ each with a TP degree, and the node's GPUs (288 GB HBM3E each). Rules:
 from __future__ import annotations
 
 import dataclasses
+import os
 from typing import Dict, List, Optional, Sequence
 
 HBM_BYTES = 288 * 10**9
@@ -126,13 +127,52 @@ def describe(p: Placement) -> str:
     return "; ".join(f"{m}->{','.join(map(str, g))}" for m, g in sorted(p.gpus.items()))
 
 
+_KFD_NODES = "/sys/class/kfd/kfd/topology/nodes"
+
+
+def visible_gpu_count() -> int:
+    """GPUs this process can open, without importing torch (the driver process stays torch-free;
+    the import alone is ~1.5 s on the CLI's startup path): KFD topology nodes with a GPU whose
+    render node is accessible, narrowed by HIP/ROCR/CUDA_VISIBLE_DEVICES as the HIP runtime
+    narrows them. -1 when the topology is unreadable (the caller asks torch instead)."""
+    try:
+        nodes = sorted(os.listdir(_KFD_NODES), key=lambda d: int(d) if d.isdigit() else 1 << 30)
+    except OSError:
+        return -1
+    n = 0
+    for d in nodes:
+        try:
+            with open(os.path.join(_KFD_NODES, d, "gpu_id")) as f:
+                if int(f.read().strip() or "0") == 0:
+                    continue  # a CPU node
+            minor = None
+            with open(os.path.join(_KFD_NODES, d, "properties")) as f:
+                for line in f:
+                    k, _, v = line.partition(" ")
+                    if k == "drm_render_minor":
+                        minor = int(v)
+            if minor is None or not os.access(f"/dev/dri/renderD{minor}", os.R_OK | os.W_OK):
+                continue
+            n += 1
+        except (OSError, ValueError):
+            continue
+    for var in ("ROCR_VISIBLE_DEVICES", "HIP_VISIBLE_DEVICES", "CUDA_VISIBLE_DEVICES"):
+        v = os.environ.get(var)
+        if v is not None:
+            ids = [x for x in v.split(",") if x.strip() != ""]
+            n = min(n, len(ids))
+    return n
+
+
 def default_gpus(requested: Optional[List[int]] = None) -> List[int]:
     if requested:
         return list(requested)
-    try:
-        import torch
+    n = visible_gpu_count()
+    if n < 0:
+        try:
+            import torch
 
-        n = torch.cuda.device_count()  # does not initialise the GPU on this image
-    except Exception:  # noqa: BLE001
-        n = 0
+            n = torch.cuda.device_count()  # does not initialise the GPU on this image
+        except Exception:  # noqa: BLE001
+            n = 0
     return list(range(n))

@@ -118,3 +118,40 @@ def test_driver_process_stays_torch_free():
     r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=120)
     assert r.returncode == 0, r.stderr
     assert r.stdout.strip() == "False"
+
+
+@pytest.mark.gpu
+def test_visible_gpu_count_matches_the_hip_runtime():
+    """The driver's torch-free GPU count (KFD topology + accessible render nodes + visibility
+    env) equals what the HIP runtime enumerates."""
+    import torch
+
+    from llm_consensus_amd.parallel.placement import visible_gpu_count
+
+    assert visible_gpu_count() == torch.cuda.device_count()
+
+
+def test_visible_gpu_count_from_kfd_topology(tmp_path, monkeypatch):
+    """CPU nodes (gpu_id 0) and GPUs whose render node this process cannot open are not counted;
+    a visibility variable narrows the count; no topology -> -1 (torch decides)."""
+    import os
+
+    from llm_consensus_amd.parallel import placement
+
+    for i, (gid, minor) in enumerate([(0, None), (4242, 128), (5151, 129), (6363, 130)]):
+        d = tmp_path / str(i)
+        d.mkdir()
+        (d / "gpu_id").write_text(f"{gid}\n")
+        (d / "properties").write_text("cpu_cores_count 0\n" + (f"drm_render_minor {minor}\n" if minor else ""))
+    monkeypatch.setattr(placement, "_KFD_NODES", str(tmp_path))
+    real_access = os.access
+    monkeypatch.setattr(placement.os, "access",
+                        lambda p, m: p in ("/dev/dri/renderD128", "/dev/dri/renderD129") or real_access(p, m) and False)
+    for var in ("ROCR_VISIBLE_DEVICES", "HIP_VISIBLE_DEVICES", "CUDA_VISIBLE_DEVICES"):
+        monkeypatch.delenv(var, raising=False)
+    assert placement.visible_gpu_count() == 2
+    assert placement.default_gpus() == [0, 1]
+    monkeypatch.setenv("HIP_VISIBLE_DEVICES", "1")
+    assert placement.visible_gpu_count() == 1
+    monkeypatch.setattr(placement, "_KFD_NODES", str(tmp_path / "missing"))
+    assert placement.visible_gpu_count() == -1

@@ -157,6 +157,9 @@ class Engine:
                  name: str = "", weights: Optional[TransformerWeights] = None):
         self.cfg = cfg
         self.ecfg = ecfg or EngineConfig()
+        rows_max = ops.MOE_GEMVM_MAX_TOKENS if cfg.is_moe else ops.GEMV_MAX_M
+        if not 1 <= self.ecfg.max_batch <= rows_max:
+            raise EngineError(f"{cfg.name}: max_batch {self.ecfg.max_batch} outside 1..{rows_max} decode rows")
         self.tp = tp or TPGroup.single()
         self.name = name or cfg.name
         self.device = torch.device(self.ecfg.device)

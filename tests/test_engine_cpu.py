@@ -161,3 +161,18 @@ def test_split_blocks_per_head():
     assert split_blocks_per_head(32, 32) == 16   # Phi-3: 512 4-wave blocks
     assert split_blocks_per_head(4, 1) == 256    # a TP=8 rank: every CU, two-level merge
     assert split_blocks_per_head(16, 2) == 128   # a 70B TP=4 rank
+
+def test_engine_rejects_more_rows_than_the_decode_forms_take():
+    """32 decode rows per engine (the MFMA form's two token groups), 16 for MoE engines (pairs of
+    <= 16 tokens per batched MoE launch): larger engines fail at construction, not mid-decode."""
+    import pytest
+
+    from llm_consensus_amd.engine import Engine, EngineConfig
+    from llm_consensus_amd.engine.engine import EngineError
+    from llm_consensus_amd.models.config import FAMILIES
+
+    with pytest.raises(EngineError):
+        Engine(FAMILIES["mixtral-tiny"], EngineConfig(device="cpu", max_context=64, max_batch=17))
+    with pytest.raises(EngineError):
+        Engine(FAMILIES["llama-tiny"], EngineConfig(device="cpu", max_context=64, max_batch=33))
+    Engine(FAMILIES["llama-tiny"], EngineConfig(device="cpu", max_context=64, max_batch=32))

@@ -168,7 +168,7 @@ def default_gpus(requested: Optional[List[int]] = None) -> List[int]:
     if requested:
         return list(requested)
     n = visible_gpu_count()
-    if n < 0:
+    if n <= 0:  # unreadable topology, or no render node passed the access check: ask the runtime
         try:
             import torch
 

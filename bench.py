@@ -2,20 +2,26 @@
 """Consensus-round benchmark (BASELINE.json metric: p50 end-to-end consensus latency + aggregate
 output tokens/sec, N-model fan-out) for the BASELINE.json configs on N GPUs of one node.
 
-One process per GPU (torchrun; RCCL over xGMI). One timed step = one full consensus round as
-``llm-consensus`` runs it (reference ``internal/runner/runner.go:62-115`` fan-out, then
-``internal/consensus/judge.go:81-104`` judge): every responder prefills the prompt and decodes
-``--max-tokens`` tokens, the responses are gathered, the judge prompt is rendered with the
-reference template and the judge prefills it (header first, incrementally) and
-decodes ``--max-tokens`` tokens.
+One process per GPU (RCCL over xGMI). Under ``torchrun`` the ranks come from the environment;
+``python bench.py --gpus N`` without a launcher starts its own N rank processes (GPU i = rank i)
+before anything touches the GPU, and rank 0 prints the one JSON line. One timed step = one full
+consensus round as ``llm-consensus`` runs it (reference ``internal/runner/runner.go:62-115``
+fan-out, then ``internal/consensus/judge.go:81-104`` judge): every responder prefills the prompt
+and decodes ``--max-tokens`` tokens, the responses are gathered, the judge prompt is rendered with
+the reference template and the judge prefills it (header first, incrementally)
+and decodes ``--max-tokens`` tokens.
 
-``--config`` presets (the engines named in the JSON ``config.model`` are exactly the ones that run):
+``--config`` presets (the engines named in the JSON ``config.model`` are exactly the ones that run;
+``config.name`` says which BASELINE config it is and, for a variant, how it differs):
 
 * ``fanout`` (default; configs 2/3): ``max(3, N)`` Llama-3-8B responders (distinct random-init
   replicas ``llama-3-8b@i``) placed round-robin over the N GPUs, plus a Llama-3-8B judge
   tensor-parallel over the GPUs (``--judge-tp``, auto = largest valid degree <= N) on its own
-  hipStreams beside the responders. N=1: 3 co-located responders + judge (config-2 shape);
-  N=4: 4 responders + TP=4 judge; N=8: config 3 (one responder per GPU, judge shares GPU 0..).
+  hipStreams beside the responders. N=1: 3 co-located responders + judge (config 2 on one GPU);
+  N=4: 4 responders + TP=4 judge (variant of config 2); N=8: 8 responders + TP=8 judge (variant
+  of config 3). ``--judge-tp 1`` puts the judge on the least-loaded GPU instead:
+  ``--gpus 4 --n-models 3 --judge-tp 1`` is config 2 and ``--gpus 8 --judge-tp 1`` config 3 as
+  BASELINE.json words them.
 * ``4``: 2 x Llama-3-70B responders, each TP=N/2 over its half of the node (RCCL + custom xGMI
   all-reduce), + Llama-3-8B judge. Needs an even N >= 2.
 * ``5``: mixed fleet — Mixtral-8x7B (MoE grouped GEMM) + Llama-3-8B + Phi-3-mini responders, one
@@ -24,13 +30,16 @@ decodes ``--max-tokens`` tokens.
 A config that does not fit N prints ONE JSON line with ``"skipped"`` and ``value`` null — never a
 smaller config under the same name.
 
+Round size: ``--max-tokens`` defaults to 2048 so that the driver's fixed ``--steps 20 --warmup 5``
+finishes inside its 600-s limit at every N (N=1 measured: see BASELINE.md §2.0); 4096-token rounds
+are the ``--max-tokens 4096`` secondary. Warmup rounds decode ``--warmup-tokens`` (default 64)
+tokens per engine: every decode graph is captured when the engines are built and the judge's
+prefill path is warmed once at full prompt length, so a short round exercises everything a timed
+round does. The K timed rounds are always full rounds.
+
 ``--shapes tiny`` swaps every family for its tiny twin (same code paths; CPU / same-GPU
 rehearsals of the multi-rank flows: ``LLMC_BENCH_DEVICE=cpu`` or ``LLMC_BENCH_SAME_GPU=1`` with
 ``LLMC_BENCH_BACKEND=gloo``).
-
-Warmup: the first of ``--warmup`` rounds is a full round; the others decode ``--warmup-tokens``
-(default 512) tokens per engine — every kernel, graph and bucket of a round has run by then, and a
-20-step x 40-s driver run stays within its wall-clock. The K timed rounds are always full rounds.
 
 Reported ``value`` = total generated tokens (responders + judge) per second of wall time over the
 whole job (max over ranks); ``ms_per_step`` = mean round latency; p50/p90 are in ``extra``.
@@ -58,6 +67,49 @@ TINY = {"llama-3-8b": "llama-tiny", "llama-3-70b": "llama-tiny-tp4", "mixtral-8x
 
 def log(*a):
     print(f"[bench r{os.environ.get('RANK', '0')}]", *a, file=sys.stderr, flush=True)
+
+
+def self_launch(n: int) -> int:
+    """Run this script as N rank processes (RANK = LOCAL_RANK = i binds GPU i; rendezvous on
+    127.0.0.1) and return the first failing exit status, else 0. Called before anything imports
+    torch, so the parent never initialises HIP; a rank that fails takes the others down (they
+    would wait forever in a collective), and SIGTERM/SIGINT are forwarded."""
+    import signal
+    import socket
+    import subprocess
+
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   GROUP_RANK="0", MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:], env=env))
+
+    def stop(*_):
+        for p in procs:
+            if p.poll() is None:
+                p.terminate()
+
+    signal.signal(signal.SIGTERM, lambda *a: (stop(), sys.exit(143)))
+    signal.signal(signal.SIGINT, lambda *a: (stop(), sys.exit(130)))
+    status, kill_at = 0, None
+    while any(p.poll() is None for p in procs):
+        bad = [p.returncode for p in procs if p.returncode not in (None, 0)]
+        if bad and not status:
+            status = bad[0]
+            log(f"a rank exited with status {status}: stopping the others")
+            stop()
+            kill_at = time.time() + 15
+        if kill_at is not None and time.time() > kill_at:
+            for p in procs:
+                if p.poll() is None:
+                    p.kill()
+        time.sleep(0.2)
+    if not status:
+        status = next((p.returncode for p in procs if p.returncode), 0)
+    return status
 
 
 class Progress:
@@ -111,7 +163,14 @@ def make_plan(args, world: int):
                   "seed": 1000 + whole + j} for j in range(rest)]
         jf = fam(args.judge)
         jtp = judge_tp_degree(FAMILIES[jf], world, args.judge_tp)
-        judge = {"name": f"{args.judge}@judge", "family": jf, "ranks": list(range(jtp)), "seed": 777}
+        if jtp == 1:
+            # a single-GPU judge time-shares the least-loaded GPU (config 2: the 4th GPU beside 3
+            # responders; config 3: GPU 0 with one responder per GPU)
+            load = [sum(g in e["ranks"] for e in resp) for g in range(world)]
+            jranks = [min(range(world), key=lambda g: (load[g], g))]
+        else:
+            jranks = list(range(jtp))
+        judge = {"name": f"{args.judge}@judge", "family": jf, "ranks": jranks, "seed": 777}
         return resp, judge, None
     if args.config == "4":
         if world < 2 or world % 2:
@@ -133,6 +192,25 @@ def make_plan(args, world: int):
         return resp, {"name": "llama-3-70b@judge", "family": fam("llama-3-70b"),
                       "ranks": list(range(world - jtp, world)), "seed": 777}, None
     raise SystemExit(f"unknown --config {args.config}")
+
+
+def config_name(args, world: int, resp, judge) -> str:
+    """Which BASELINE.json config this run is, and how a variant differs from its wording."""
+    if args.config != "fanout":
+        return f"BASELINE config {args.config}"
+    n, jtp = len(resp), len(judge["ranks"])
+    whole = all(len(e["ranks"]) == 1 for e in resp)
+    if world == 4 and n == 3 and jtp == 1 and whole:
+        return "BASELINE config 2"
+    if world == 8 and n == 8 and jtp == 1 and judge["ranks"] == [0] and whole:
+        return "BASELINE config 3"
+    if world == 1:
+        return "BASELINE config 2 on one GPU (3 responders + judge co-located on their own streams)"
+    base = "config 3" if world == 8 else "config 2"
+    how = [f"{n} responders" + ("" if whole else " (some tensor-parallel)")]
+    how.append(f"judge TP={jtp} over GPUs {judge['ranks'][0]}-{judge['ranks'][-1]}" if jtp > 1
+               else f"judge on GPU {judge['ranks'][0]}")
+    return f"variant of BASELINE {base} on {world} GPUs: " + ", ".join(how)
 
 
 def describe(resp, judge) -> str:
@@ -160,10 +238,11 @@ def main() -> None:
     ap.add_argument("--model", default="llama-3-8b", help="fanout: responder family")
     ap.add_argument("--judge", default="llama-3-8b", help="fanout: judge family")
     ap.add_argument("--n-models", type=int, default=0, help="fanout: responders (0 = max(3, N))")
-    ap.add_argument("--max-tokens", type=int, default=4096)
+    ap.add_argument("--max-tokens", type=int, default=2048,
+                    help="tokens per response and for the judge (2048: 20 driver steps fit its 600-s limit)")
     ap.add_argument("--judge-max-tokens", type=int, default=0, help="0 = same as --max-tokens")
-    ap.add_argument("--warmup-tokens", type=int, default=512,
-                    help="tokens per engine in warmup rounds after the first (untimed; 0 = full rounds)")
+    ap.add_argument("--warmup-tokens", type=int, default=64,
+                    help="tokens per engine in the (untimed) warmup rounds (0 = full rounds)")
     ap.add_argument("--prompt-tokens", type=int, default=128)
     ap.add_argument("--temperature", type=float, default=1.0)
     ap.add_argument("--judge-tp", type=int, default=0, help="0 = auto (config 5: 4)")
@@ -173,6 +252,11 @@ def main() -> None:
                     help="rank 0 also writes the full record (per-step stats, p50/p90) here ('' = off)")
     args = ap.parse_args()
 
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        # no launcher: start the N ranks here, before this process touches the GPU (it never
+        # imports torch), and exit with their status
+        sys.exit(self_launch(args.gpus))
+
     import torch
     import torch.distributed as dist
 
@@ -180,7 +264,7 @@ def main() -> None:
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus:
-        log(f"warning: --gpus {args.gpus} but WORLD_SIZE {world}; using WORLD_SIZE")
+        raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE {world}: one rank per GPU is the contract")
     n_gpus = world
 
     resp_plan, judge_plan, skip = make_plan(args, world)
@@ -284,6 +368,12 @@ def main() -> None:
         e.warmup_graphs()
     if judge is not None:
         judge.warmup_graphs()
+        # the judge's prefill path at full prompt length once (allocator growth, every chunk
+        # shape), so that short warmup rounds leave nothing for the first timed round to warm
+        n_warm = min(judge_ctx - jmax - 64, fixed + n_resp * (args.max_tokens + 64))
+        ws = judge.new_sequence()
+        judge.prefill([ws], [[(7 * i) % 30000 + 300 for i in range(n_warm)]])
+        judge.free_sequence(ws)
     sync()
     if world > 1:
         dist.barrier()
@@ -402,7 +492,7 @@ def main() -> None:
         return stats
 
     for w in range(args.warmup):
-        st = one_round(w, 0 if w == 0 else args.warmup_tokens)
+        st = one_round(w, args.warmup_tokens)
         log(f"warmup {w}: {st}")
 
     sync()
@@ -457,8 +547,7 @@ def main() -> None:
             "dtype": "bf16",
             "data": "synthetic prompt (synthetic tokenizer), random-init weights",
             "config": {
-                "name": {"fanout": "fanout (BASELINE configs 2/3)", "4": "BASELINE config 4",
-                         "5": "BASELINE config 5"}[args.config],
+                "name": config_name(args, n_gpus, resp_plan, judge_plan),
                 "model": describe(resp_plan, judge_plan),
                 "global_batch": n_resp,
                 "seq_len": args.prompt_tokens + args.max_tokens,
@@ -485,7 +574,7 @@ def main() -> None:
                 "per_model_ttft_ms": {m: round(1000 * statistics.median(p["per_model"][m]["ttft_s"] for p in per_step), 1)
                                       for m in names},
                 "judge_tp": jtp,
-                "warmup_rounds_tokens": [args.max_tokens] + [args.warmup_tokens or args.max_tokens] * max(0, args.warmup - 1),
+                "warmup_rounds_tokens": [args.warmup_tokens or args.max_tokens] * args.warmup,
                 "custom_allreduce": {e.name: e.tp.custom is not None for _, e, _, _ in responders if e.tp.size > 1}
                 | ({judge.name: judge.tp.custom is not None} if judge is not None and judge.tp.size > 1 else {}),
             },

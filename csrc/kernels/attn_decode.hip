@@ -271,7 +271,7 @@ __device__ __forceinline__ void publish_partial(const float* red, __amdgpu_buffe
 // tid < G * D / 4 hold their quad's (M, S) in ms[0..1] and the unnormalised sums in acc.
 template <int G, int D, int NT>
 __device__ __forceinline__ void merge_rows(__amdgpu_buffer_rsrc_t rsrc, const char* base, int r0, int n, uint32_t tag,
-                                           f32x4* scratch, int tid, f32x4& ms, f32x4& acc) {
+                                           f32x4* scratch, int tid, f32x4& ms, f32x4& acc, int* fault) {
   constexpr int HQ = D / 4, RU = HQ + 1, Q = G * HQ;
   static_assert(Q <= NT, "one pass");
   const int ngr = max(1, min(NT / Q, n));
@@ -294,7 +294,13 @@ __device__ __forceinline__ void merge_rows(__amdgpu_buffer_rsrc_t rsrc, const ch
 #pragma unroll
         for (int j = 0; j < 8; ++j)
           if (c0 + j * ngr < n) ok = ok && ov[j][1] == tag && ov[j][3] == tag && lv[j][1] == tag;
-        if (__all(ok) || spins >= kSpinLimit) break;
+        if (__all(ok)) break;
+        if (spins >= kSpinLimit) {
+          // gave up on a granule that never arrived: the output is wrong, so say so (the
+          // engine reads this word after its sync points and fails the request)
+          if (fault != nullptr && (tid & 63) == 0) __hip_atomic_store(fault, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          break;
+        }
         __builtin_amdgcn_s_sleep(2);
       }
 #pragma unroll
@@ -340,7 +346,8 @@ __device__ __forceinline__ void merge_rows(__amdgpu_buffer_rsrc_t rsrc, const ch
 template <int G, int D, int NW>
 __device__ __forceinline__ void publish_and_merge(const float* red, float* part, int* ctr, int b, int nkv, int kvh,
                                                   int c, int nchunks, int gsize, int max_chunks, int max_groups,
-                                                  uint32_t tag, bf16_t* out_row, char* smem, int* flag, int tid) {
+                                                  uint32_t tag, bf16_t* out_row, char* smem, int* flag, int tid,
+                                                  int* fault) {
   constexpr int HQ = D / 4, RU = HQ + 1, Q = G * HQ;
   const int rows = max_chunks + max_groups;
   float* slab = part + (static_cast<int64_t>(b) * nkv + kvh) * rows * G * RU * 4;
@@ -356,7 +363,7 @@ __device__ __forceinline__ void publish_and_merge(const float* red, float* part,
   __syncthreads();
   if (*flag == 0) return;
   f32x4 ms, acc;
-  merge_rows<G, D, NW * 64>(rsrc, base, g0, gn, tag, scratch, tid, ms, acc);
+  merge_rows<G, D, NW * 64>(rsrc, base, g0, gn, tag, scratch, tid, ms, acc, fault);
   if (ngroups > 1) {
     // publish the group result as a granule row, then the top-level ticket
     if (tid < Q) {
@@ -377,7 +384,7 @@ __device__ __forceinline__ void publish_and_merge(const float* red, float* part,
     }
     __syncthreads();
     if (*flag == 0) return;
-    merge_rows<G, D, NW * 64>(rsrc, base, max_chunks, ngroups, tag, scratch, tid, ms, acc);
+    merge_rows<G, D, NW * 64>(rsrc, base, max_chunks, ngroups, tag, scratch, tid, ms, acc, fault);
   }
   if (tid < Q) {
     const int g = tid / HQ, u = tid % HQ;
@@ -398,7 +405,7 @@ __global__ __launch_bounds__(NW * 64) void attn_decode_split_kernel(
     const bf16_t* __restrict__ v_cache, const int32_t* __restrict__ block_tables, int bt_stride,
     const int32_t* __restrict__ seq_lens, float* __restrict__ part, int* __restrict__ counters, bf16_t* __restrict__ out,
     int out_stride, int nkv, int bs, int nblocks, int min_chunk, int max_chunks, int gsize, int max_groups,
-    float scale_log2) {
+    float scale_log2, int* __restrict__ fault) {
   static_assert(G <= 16 && D % 32 == 0 && D <= 128, "shape");
   using ST = SubTile<G, D>;
   constexpr int NT = NW * 64;
@@ -456,7 +463,7 @@ __global__ __launch_bounds__(NW * 64) void attn_decode_split_kernel(
     return;
   }
   publish_and_merge<G, D, NW>(red, part, ctr, b, nkv, kvh, c, nchunks, gsize, max_chunks, max_groups, tag, out_row, smem,
-                              reinterpret_cast<int*>(pages), tid);
+                              reinterpret_cast<int*>(pages), tid, fault);
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -466,7 +473,7 @@ __global__ __launch_bounds__(256) void attn_decode_fused_kernel(
     const bf16_t* __restrict__ v_cache, const int32_t* __restrict__ block_tables, int bt_stride,
     const int32_t* __restrict__ seq_lens, float* __restrict__ part, int* __restrict__ counters,
     bf16_t* __restrict__ out, int out_stride, int nkv, int bs, int nblocks, int chunk, int max_chunks, int gsize,
-    int max_groups, float scale_log2) {
+    int max_groups, float scale_log2, int* __restrict__ fault) {
   static_assert(G <= 16 && D % 32 == 0 && D <= 128, "shape");
   using ST = SubTile<G, D>;
   const int c = blockIdx.x, kvh = blockIdx.y, b = blockIdx.z;
@@ -508,7 +515,7 @@ __global__ __launch_bounds__(256) void attn_decode_fused_kernel(
     return;
   }
   publish_and_merge<G, D, 4>(red, part, ctr, b, nkv, kvh, c, nchunks, gsize, max_chunks, max_groups, tag, out_row, smem,
-                             reinterpret_cast<int*>(red + 4 * G * (D + 2)), tid);
+                             reinterpret_cast<int*>(red + 4 * G * (D + 2)), tid, fault);
 }
 
 // Split blocks: 8 waves when a block's balanced range at the table's full length is >= 512 keys
@@ -519,7 +526,7 @@ template <int G, int D, int NW>
 static int launch_split_nw(dim3 grid, hipStream_t s, const void* q, int q_stride, const void* kc, const void* vc,
                            const void* bt, int bt_stride, const void* sl, void* part, void* ctr, void* out,
                            int out_stride, int nkv, int bs, int nblocks, int chunk, int max_chunks, int gsize,
-                           int max_groups, int max_chunk_keys, float scale) {
+                           int max_groups, int max_chunk_keys, float scale, int* fault) {
   const size_t lds = NW * 32 * kVRowBytes + static_cast<size_t>(NW) * G * (D + 2) * sizeof(float) +
                      static_cast<size_t>((max_chunk_keys + bs - 1) / bs + 2) * sizeof(int);
   if (lds > 160 * 1024) return -4;
@@ -533,7 +540,7 @@ static int launch_split_nw(dim3 grid, hipStream_t s, const void* q, int q_stride
   kern<<<grid, NW * 64, lds, s>>>((const bf16_t*)q, q_stride, (const bf16_t*)kc, (const bf16_t*)vc,
                                   (const int32_t*)bt, bt_stride, (const int32_t*)sl, (float*)part, (int*)ctr,
                                   (bf16_t*)out, out_stride, nkv, bs, nblocks, chunk, max_chunks, gsize, max_groups,
-                                  scale * 1.4426950408889634f);
+                                  scale * 1.4426950408889634f, fault);
   return static_cast<int>(hipGetLastError());
 }
 
@@ -541,30 +548,32 @@ template <int G, int D>
 static int launch_split(dim3 grid, hipStream_t s, const void* q, int q_stride, const void* kc, const void* vc,
                         const void* bt, int bt_stride, const void* sl, void* part, void* ctr, void* out, int out_stride,
                         int nkv, int bs, int nblocks, int chunk, int max_chunks, int gsize, int max_groups,
-                        float scale) {
+                        float scale, int* fault) {
   // page-id staging sized for the largest balanced range any sequence of this table can get
   const int grid_chunks = static_cast<int>(grid.x);
   const int units = (bt_stride * bs + 31) / 32;
   const int bal = 32 * ((units + grid_chunks - 1) / grid_chunks) + 32;
   const int max_chunk = bal > 2 * chunk ? bal : 2 * chunk;
-  if (G > 1 && bal >= 512)
+  // a minimum block range of >= 512 keys (the length-only split of batching engines) always takes
+  // 8 waves, so a row's per-wave key partition never depends on the bucket its batch selected
+  if (G > 1 && (bal >= 512 || chunk >= 512))
     return launch_split_nw<G, D, 8>(grid, s, q, q_stride, kc, vc, bt, bt_stride, sl, part, ctr, out, out_stride, nkv,
-                                    bs, nblocks, chunk, max_chunks, gsize, max_groups, max_chunk, scale);
+                                    bs, nblocks, chunk, max_chunks, gsize, max_groups, max_chunk, scale, fault);
   return launch_split_nw<G, D, 4>(grid, s, q, q_stride, kc, vc, bt, bt_stride, sl, part, ctr, out, out_stride, nkv, bs,
-                                  nblocks, chunk, max_chunks, gsize, max_groups, max_chunk, scale);
+                                  nblocks, chunk, max_chunks, gsize, max_groups, max_chunk, scale, fault);
 }
 
 template <int G, int D>
 static int launch_fused(dim3 grid, hipStream_t s, const void* q, int q_stride, const void* kc, const void* vc,
                         const void* bt, int bt_stride, const void* sl, void* part, void* ctr, void* out, int out_stride,
                         int nkv, int bs, int nblocks, int chunk, int max_chunks, int gsize, int max_groups,
-                        float scale) {
+                        float scale, int* fault) {
   const size_t lds = 4 * 32 * kVRowBytes + static_cast<size_t>(4) * G * (D + 2) * sizeof(float) + 16;  // + flag
   if (lds > 64 * 1024) return -4;
   attn_decode_fused_kernel<G, D><<<grid, 256, lds, s>>>(
       (const bf16_t*)q, q_stride, (const bf16_t*)kc, (const bf16_t*)vc, (const int32_t*)bt, bt_stride,
       (const int32_t*)sl, (float*)part, (int*)ctr, (bf16_t*)out, out_stride, nkv, bs, nblocks, chunk, max_chunks, gsize,
-      max_groups, scale * 1.4426950408889634f);
+      max_groups, scale * 1.4426950408889634f, fault);
   return static_cast<int>(hipGetLastError());
 }
 
@@ -572,13 +581,13 @@ template <int G>
 static int launch_g(bool fused, int D, dim3 grid, hipStream_t s, const void* q, int q_stride, const void* kc,
                     const void* vc, const void* bt, int bt_stride, const void* sl, void* part, void* ctr, void* out,
                     int out_stride, int nkv, int bs, int nblocks, int chunk, int max_chunks, int gsize,
-                    int max_groups, float scale) {
+                    int max_groups, float scale, int* fault) {
 #define LLMC_ATTN_D(DD)                                                                                          \
   case DD:                                                                                                       \
     return fused ? launch_fused<G, DD>(grid, s, q, q_stride, kc, vc, bt, bt_stride, sl, part, ctr, out, out_stride, \
-                                       nkv, bs, nblocks, chunk, max_chunks, gsize, max_groups, scale)            \
+                                       nkv, bs, nblocks, chunk, max_chunks, gsize, max_groups, scale, fault)     \
                  : launch_split<G, DD>(grid, s, q, q_stride, kc, vc, bt, bt_stride, sl, part, ctr, out, out_stride, \
-                                       nkv, bs, nblocks, chunk, max_chunks, gsize, max_groups, scale);
+                                       nkv, bs, nblocks, chunk, max_chunks, gsize, max_groups, scale, fault);
   switch (D) {
     LLMC_ATTN_D(64)
     LLMC_ATTN_D(96)
@@ -599,6 +608,8 @@ using namespace llmc;
 // fused = 1 (short contexts): grid_chunks fixed chunk-key blocks (chunk 128 or 256; bs % (chunk/4) == 0).
 // fused = 0 (long contexts): balanced split over <= grid_chunks blocks of >= chunk keys (multiple of 128).
 // Chunk partials are merged in one level up to kAttnOneLevel chunks, else in groups of kAttnGroup.
+// fault (nullable int32): set to 1 when a merger gave up waiting for a partial (bounded spin): the
+// step's attention output is then invalid and the caller must fail the request.
 constexpr int kAttnOneLevel = 32, kAttnGroup = 16;  // one-level merges of 64 rows measured 1.3-1.5x slower
 
 extern "C" int llmc_attn_decode_groups(int max_chunks) {
@@ -609,7 +620,7 @@ extern "C" int llmc_attn_decode(const void* q, int q_stride, const void* k_cache
                                 const void* block_tables, int bt_stride, const void* seq_lens, void* part,
                                 void* counters, void* out, int out_stride, int B, int nh, int nkv, int D, int bs,
                                 int nblocks, int chunk, int grid_chunks, int max_chunks, float scale, int fused,
-                                hipStream_t s) {
+                                void* fault, hipStream_t s) {
   if (nh % nkv != 0 || grid_chunks > max_chunks || grid_chunks < 1 || nblocks < 1 || counters == nullptr ||
       bt_stride < 1)
     return -1;
@@ -621,10 +632,10 @@ extern "C" int llmc_attn_decode(const void* q, int q_stride, const void* k_cache
   dim3 grid(grid_chunks, nkv, B);
   const bool f = fused != 0;
   switch (G) {
-    case 1: return launch_g<1>(f, D, grid, s, q, q_stride, k_cache, v_cache, block_tables, bt_stride, seq_lens, part, counters, out, out_stride, nkv, bs, nblocks, chunk, max_chunks, gsize, max_groups, scale);
-    case 2: return launch_g<2>(f, D, grid, s, q, q_stride, k_cache, v_cache, block_tables, bt_stride, seq_lens, part, counters, out, out_stride, nkv, bs, nblocks, chunk, max_chunks, gsize, max_groups, scale);
-    case 4: return launch_g<4>(f, D, grid, s, q, q_stride, k_cache, v_cache, block_tables, bt_stride, seq_lens, part, counters, out, out_stride, nkv, bs, nblocks, chunk, max_chunks, gsize, max_groups, scale);
-    case 8: return launch_g<8>(f, D, grid, s, q, q_stride, k_cache, v_cache, block_tables, bt_stride, seq_lens, part, counters, out, out_stride, nkv, bs, nblocks, chunk, max_chunks, gsize, max_groups, scale);
+    case 1: return launch_g<1>(f, D, grid, s, q, q_stride, k_cache, v_cache, block_tables, bt_stride, seq_lens, part, counters, out, out_stride, nkv, bs, nblocks, chunk, max_chunks, gsize, max_groups, scale, static_cast<int*>(fault));
+    case 2: return launch_g<2>(f, D, grid, s, q, q_stride, k_cache, v_cache, block_tables, bt_stride, seq_lens, part, counters, out, out_stride, nkv, bs, nblocks, chunk, max_chunks, gsize, max_groups, scale, static_cast<int*>(fault));
+    case 4: return launch_g<4>(f, D, grid, s, q, q_stride, k_cache, v_cache, block_tables, bt_stride, seq_lens, part, counters, out, out_stride, nkv, bs, nblocks, chunk, max_chunks, gsize, max_groups, scale, static_cast<int*>(fault));
+    case 8: return launch_g<8>(f, D, grid, s, q, q_stride, k_cache, v_cache, block_tables, bt_stride, seq_lens, part, counters, out, out_stride, nkv, bs, nblocks, chunk, max_chunks, gsize, max_groups, scale, static_cast<int*>(fault));
     default: return -3;
   }
 }

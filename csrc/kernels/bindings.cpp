@@ -29,7 +29,7 @@ int llmc_rope_kv_write(const void*, int, void*, int, const void*, const void*, c
                        int, int, int, int, int, hipStream_t);
 int llmc_attn_decode_groups(int);
 int llmc_attn_decode(const void*, int, const void*, const void*, const void*, int, const void*, void*, void*, void*,
-                     int, int, int, int, int, int, int, int, int, int, float, int, hipStream_t);
+                     int, int, int, int, int, int, int, int, int, int, float, int, void*, hipStream_t);
 int llmc_gemv_qkv_rope(int, const void*, int, const void*, float, const void*, int, int, void*, int, void*, void*,
                        const void*, const void*, const void*, const void*, int, int, int, int, int, hipStream_t);
 int llmc_attn_prefill(const void*, int, const void*, const void*, const void*, int, const void*, const void*,
@@ -113,9 +113,9 @@ PYBIND11_MODULE(_llmc_hip, m) {
   m.def("attn_decode_groups", [](int max_chunks) { return llmc_attn_decode_groups(max_chunks); });
   m.def("attn_decode", [](ptr q, int qs, ptr kc, ptr vc, ptr bt, int bts, ptr sl, ptr part, ptr ctr, ptr out, int os,
                           int B, int nh, int nkv, int D, int bs, int nblocks, int chunk, int grid_chunks,
-                          int max_chunks, float scale, int fused, ptr s) {
+                          int max_chunks, float scale, int fused, ptr fault, ptr s) {
     check(llmc_attn_decode(P(q), qs, P(kc), P(vc), P(bt), bts, P(sl), P(part), P(ctr), P(out), os, B, nh, nkv, D, bs,
-                           nblocks, chunk, grid_chunks, max_chunks, scale, fused, S(s)),
+                           nblocks, chunk, grid_chunks, max_chunks, scale, fused, P(fault), S(s)),
           "attn_decode");
   });
   m.def("gemv_qkv_rope", [](int M, ptr x, int xs, ptr nw, float eps, ptr W, int N, int K, ptr qo, int qos, ptr kc,

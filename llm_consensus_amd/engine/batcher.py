@@ -54,6 +54,9 @@ class ContinuousBatcher:
         self.rows: List[Row] = []
         self._pending = None          # event of the in-flight host snapshot
         self._snap: List[Row] = []    # row layout the snapshot was taken with
+        # host copy of the engine's decode-attention fault word, taken with every snapshot
+        self._host_fault = (torch.zeros(1, dtype=torch.int32, pin_memory=True) if engine.on_gpu
+                            else torch.zeros(1, dtype=torch.int32))
         self._eos = set(engine.cfg.eos)
         e = engine
         self._row_state = [e.tokens_in, e.positions, e.seq_lens, e.slots, e.block_tables, e.out_tokens,
@@ -172,11 +175,23 @@ class ContinuousBatcher:
                 return self._compact()
             if self._pending is not None:
                 self._pending.synchronize()
+                if int(self._host_fault[0]):
+                    # a decode-attention merge gave up during the replays behind this snapshot:
+                    # the rows it covered carry invalid tokens — fail them instead of streaming
+                    from .engine import EngineError
+
+                    e.attn_fault.zero_()
+                    self._host_fault.zero_()
+                    for row in self._snap:
+                        if not row.done:
+                            row.error, row.done = EngineError("decode attention: a partial merge timed out: "
+                                                              "this request's tokens are invalid"), True
                 self._consume(e.host_count, e.host_tokens, self._snap)
             gone = self._compact()
             # snapshot of the state after this replay (and the compaction), read next call
             e.host_count.copy_(e.out_count, non_blocking=True)
             e.host_tokens.copy_(e.out_tokens, non_blocking=True)
+            self._host_fault.copy_(e.attn_fault, non_blocking=True)
             ev = torch.cuda.Event()
             ev.record(e.stream)
             self._pending, self._snap = ev, list(self.rows)

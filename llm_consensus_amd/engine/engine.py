@@ -59,7 +59,10 @@ class EngineConfig:
 
 
 FUSED_CHUNK_SMALL, FUSED_CHUNK_LARGE = 128, 256
-BATCHING_MIN_KEYS = 2048  # batching engines: minimum keys per split block (see attn_buckets)
+# batching engines: minimum keys per split block (see attn_buckets) when rows x kv heads fill the
+# chip with >= 32 (row, head) units, and below that (3 duplicate 8B responders = 24 units, TP
+# ranks holding 1-2 kv heads) where a row needs more blocks of its own
+BATCHING_MIN_KEYS, BATCHING_MIN_KEYS_FEW = 2048, 512
 
 
 def attn_buckets(ctxmax: int, blocks_per_head: int = 32, fused_max: int = 4096, group: int = 4,
@@ -78,16 +81,18 @@ def attn_buckets(ctxmax: int, blocks_per_head: int = 32, fused_max: int = 4096, 
     longer context. Measured per shape: profiles/r2_attn_decode.md. ``fused_max`` = 0 disables
     the fused form (page size not a multiple of 32 keys).
 
-    An engine batching ``rows`` >= 3 decode rows whose rows x kv heads give >= 32 independent
-    (row, head) units uses the balanced split with a BATCHING_MIN_KEYS (2048) minimum per block
-    over min(32, capacity / 2048) blocks per kv head: a row of L keys is split into min(32,
-    ceil(L / 2048)) ranges whatever the bucket and whatever else is batched (batch-invariant
-    tokens), so a lone long row still spreads over the chip (8B at 13.5k keys: 30 µs vs 141 for
-    one block per (row, head)) while 32 rows stay within 1.2x of it
-    (profiles/r2_batched_decode.md, `microbench_kernels.py attn-rows`)."""
+    An engine batching ``rows`` >= 3 decode rows uses the balanced split with a minimum of ``mk``
+    keys per block over min(32, capacity / mk) blocks per kv head — mk = BATCHING_MIN_KEYS (2048)
+    when rows x kv heads give >= 32 independent (row, head) units, BATCHING_MIN_KEYS_FEW (512)
+    below — always on 8-wave blocks: a row of L keys is split into min(32, ceil(L / mk)) ranges
+    whatever the bucket and whatever else is batched, so its tokens are batch-invariant (the fused
+    form's chunk and the split grid would follow the bucket the longest row selects); a lone long
+    row still spreads over the chip (8B at 13.5k keys: 30 µs vs 141 for one block per (row,
+    head)) while 32 rows stay within 1.2x of it (profiles/r2_batched_decode.md,
+    `microbench_kernels.py attn-rows`)."""
     out, cap = [], 1024
-    if rows >= 3 and rows * nkv >= 32:
-        mk = BATCHING_MIN_KEYS
+    if rows >= 3:
+        mk = BATCHING_MIN_KEYS if rows * nkv >= 32 else BATCHING_MIN_KEYS_FEW
         while True:
             c = min(cap, ctxmax)
             gc = min(32, (c + mk - 1) // mk)
@@ -238,6 +243,8 @@ class Engine:
                                          self.nkv, rows=self.ecfg.max_batch)
         max_chunks = max(gc for _, _, gc, _ in self.attn_buckets)
         self.attn_part, self.attn_counters = ops.decode_attn_workspace(B, self.nh, self.nkv, self.D, max_chunks, dev)
+        # set by a decode-attention merger that gave up on a partial (checked after every decode)
+        self.attn_fault = torch.zeros(1, dtype=torch.int32, device=dev) if self.on_gpu else None
         if self.on_gpu:
             P = ops.sample_parts()
             self.ws_v = torch.zeros(B, P, dtype=torch.float32, device=dev)
@@ -541,7 +548,7 @@ class Engine:
                          mfma=self.mfma_decode)
             ops.attn_decode(q, self.k_cache[li], self.v_cache[li], self.block_tables[:B], self.seq_lens[:B], attn,
                             part[:B], self.attn_counters[:B], self.nh, self.nkv, self.D, self.bs, chunk, self.scale,
-                            grid_chunks, fused=fused)
+                            grid_chunks, fused=fused, fault=self.attn_fault)
             self._row_parallel(attn, Lw.w_o, h)
             if c.is_moe:
                 self._moe_decode(h, Lw, B)
@@ -797,7 +804,7 @@ class Engine:
         context decides for every rank (a follower's own cancel arrives at its own time)."""
         local = ctx is not None and ctx.done()
         if self.tp.size > 1 and self.tp.ctrl is not None:
-            return bool(self.tp.leader_decides(int(local)))
+            return bool(self.tp.leader_decides(int(local), "stop"))
         return local
 
     @staticmethod
@@ -805,11 +812,26 @@ class Engine:
         return (ctx.err() if ctx is not None else None) or "context canceled"
 
     def _check_collectives(self) -> None:
-        """TP engines with a control group: fail the request (on every rank) if a custom-collective
-        spin timed out since the last check; the group re-synchronises its protocol state first, so
-        the next request runs on consistent epochs."""
-        if self.tp.size > 1 and self.tp.ctrl is not None and not self.tp.check_collectives():
-            raise EngineError("custom all-reduce timed out (a TP peer stalled): this request's tokens are invalid")
+        """After a decode (stream synchronised): fail the request if a bounded device spin gave up
+        since the last check, on every rank of a TP group with a control group.
+
+        * custom-collective spins: the group re-synchronises its protocol state first, so the next
+          request runs on consistent epochs;
+        * decode-attention merges (``attn_fault``): a merger that gave up merged a partial that
+          never arrived, so the tokens sampled from it are wrong — reported, never streamed on
+          silently (reference ``runner.go:100-107`` reports failures)."""
+        attn_bad = False
+        if self.attn_fault is not None:
+            attn_bad = bool(self.attn_fault.item())
+            if attn_bad:
+                self.attn_fault.zero_()
+        if self.tp.size > 1 and self.tp.ctrl is not None:
+            if not self.tp.check_collectives():
+                raise EngineError("custom all-reduce timed out (a TP peer stalled): this request's tokens are invalid")
+            attn_bad = self.tp.any_rank(attn_bad)
+        if attn_bad:
+            raise EngineError("decode attention: a partial merge timed out (a block never published its "
+                              "partial): this request's tokens are invalid")
 
     def _bind_rows(self, seqs: List[Sequence], params: List[SamplingParams]) -> None:
         """Bind sequences to decode rows 0..B-1: block tables, prefill logits and sampling state."""

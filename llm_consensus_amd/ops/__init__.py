@@ -198,11 +198,13 @@ def decode_attn_workspace(B, nh, nkv, D, max_chunks, device, fused: bool = False
 
 
 def attn_decode(q, k_cache, v_cache, block_tables, seq_lens, out, part, counters, nh, nkv, D, bs, chunk, scale,
-                grid_chunks: Optional[int] = None, fused: bool = False):
+                grid_chunks: Optional[int] = None, fused: bool = False, fault: Optional[torch.Tensor] = None):
     """Decode attention (K5), one launch. ``fused``: fixed ``chunk``-key blocks (128 or 256;
     ``grid_chunks`` = bucket capacity / chunk) — short contexts; else the balanced split over <=
     grid_chunks 8-wave blocks of >= ``chunk`` keys — long contexts. Both merge their partials in
-    the same launch. ``part``/``counters`` come from ``decode_attn_workspace``."""
+    the same launch. ``part``/``counters`` come from ``decode_attn_workspace``. ``fault`` (int32
+    [1], optional) is set to 1 by a merger that gave up waiting for a partial (bounded spin): the
+    output is then invalid (``Engine`` checks it after every decode and fails the request)."""
     if not q.is_cuda:
         out.copy_(oracle.attn_decode(q, k_cache, v_cache, block_tables, seq_lens, nh, nkv, D, bs, scale))
         return out
@@ -215,7 +217,7 @@ def attn_decode(q, k_cache, v_cache, block_tables, seq_lens, out, part, counters
         raise ValueError("attn_decode: workspace does not match (use decode_attn_workspace)")
     kernels().attn_decode(_p(q), q.stride(0), _p(k_cache), _p(v_cache), _p(block_tables), block_tables.stride(0),
                           _p(seq_lens), _p(part), _p(counters), _p(out), out.stride(0), B, nh, nkv, D, bs,
-                          k_cache.shape[0], chunk, gc, max_chunks, float(scale), 1 if fused else 0, _s(q))
+                          k_cache.shape[0], chunk, gc, max_chunks, float(scale), 1 if fused else 0, _p(fault), _s(q))
     return out
 
 

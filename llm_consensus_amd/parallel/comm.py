@@ -38,6 +38,13 @@ import torch
 import torch.distributed as dist
 
 
+CTRL_KINDS = {"value": 1, "batch": 2, "stop": 3}
+
+
+class ControlDesync(RuntimeError):
+    """The TP ranks' control decisions no longer pair up (see ``TPGroup.leader_decides``)."""
+
+
 class TPGroup:
     """Rank/size of a model's tensor-parallel group (size 1 = no communication)."""
 
@@ -92,13 +99,26 @@ class TPGroup:
         return agree(rccl_graph_replay_check(cap, self.rank, self.size, device))
 
     # -- control plane ----------------------------------------------------------------------------
-    def leader_decides(self, value: int) -> int:
-        """The leader's ``value`` on every rank (host broadcast over ``ctrl``); identity without one."""
+    def leader_decides(self, value: int, kind: str = "value") -> int:
+        """The leader's ``value`` on every rank (host broadcast over ``ctrl``); identity without one.
+
+        Each decision travels as (kind, sequence number, value): every rank counts its calls, and
+        a follower whose call does not meet the leader's same-kind call of the same number (one
+        rank left a decode early and the ranks' call sequences shifted, e.g. a batch size read as
+        a stop flag) raises ``ControlDesync`` instead of acting on a value meant for another
+        decision."""
         if self.size == 1 or self.ctrl is None:
             return value
-        t = torch.tensor([int(value)], dtype=torch.int64)
+        code = CTRL_KINDS[kind]
+        self._ctrl_seq = getattr(self, "_ctrl_seq", 0) + 1
+        t = torch.tensor([code, self._ctrl_seq, int(value)], dtype=torch.int64)
         dist.broadcast(t, src=dist.get_global_rank(self.ctrl, 0), group=self.ctrl)
-        return int(t.item())
+        got_kind, got_seq = int(t[0]), int(t[1])
+        if got_kind != code or got_seq != self._ctrl_seq:
+            names = {v: k for k, v in CTRL_KINDS.items()}
+            raise ControlDesync(f"TP control channel out of step on rank {self.rank}: expected {kind} "
+                                f"#{self._ctrl_seq}, leader sent {names.get(got_kind, got_kind)} #{got_seq}")
+        return int(t[2])
 
     def any_rank(self, flag: bool) -> bool:
         """True on every rank if ``flag`` is True on any rank (host all-reduce over ``ctrl``)."""

@@ -89,6 +89,9 @@ class _EngineHost:
             if item is None:
                 return
             kind = item[0]
+            # the requests this item answers for: the first one until the batch is gathered, so a
+            # failure while gathering still replies to it (and never to a previous batch)
+            batch = [item[1]] if kind == "gen" else [item[2]] if kind == "sess_generate" else []
             try:
                 if kind == "gen":
                     # replica batching: gather the generate requests for this engine that arrive
@@ -128,9 +131,7 @@ class _EngineHost:
                     if seq is not None:
                         self.engine.free_sequence(seq)
             except Exception as e:  # noqa: BLE001 - engine-level failure = that request's error
-                rids = []
-                if kind in ("gen", "sess_generate"):
-                    rids = [r.rid for r in batch]
+                rids = [r.rid for r in batch]
                 msg = f"{type(e).__name__}: {e}"
                 if os.environ.get("LLMC_DEBUG"):
                     msg += "\n" + traceback.format_exc()
@@ -154,14 +155,14 @@ class _EngineHost:
         cap = self.engine.ecfg.max_batch
         tp = self.engine.tp
         if tp.size > 1 and tp.ctrl is not None and not tp.is_leader:
-            n = tp.leader_decides(0)
+            n = tp.leader_decides(0, "batch")
             while len(items) < n:
                 items.append(self.q.get())
             return items
         if cap > 1:
             self._window(items, kind, cap)
         if tp.size > 1 and tp.ctrl is not None:
-            tp.leader_decides(len(items))
+            tp.leader_decides(len(items), "batch")
         return items
 
     def _window(self, items: list, kind: str, cap: int) -> None:

@@ -119,3 +119,45 @@ def test_batching_engine_long_rows_batch_invariant(cuda):
     got = _run_schedule(eng, reqs, admit_at=[0, 0, 1, 2])
     for i, (g, r) in enumerate(zip(got, ref)):
         assert g == r, (i, g, r)
+
+
+@pytest.mark.gpu
+def test_three_rows_eight_kv_heads_batch_invariant(cuda):
+    """3 rows x 8 kv heads (3 duplicate 8B responders batched in one engine: 24 (row, head)
+    units, the length-only split with a 512-key minimum): rows of 2900, 9 and 1300 keys, whose
+    batch selects larger attention buckets than the short rows would alone, get exactly their
+    solo tokens (the bucket-dependent fused chunk used to change their rounding)."""
+    cfg = FAMILIES["llama-tiny"].with_(name="llama-tiny-kv8", hidden=1024, n_heads=16, n_kv_heads=8, head_dim=64,
+                                       intermediate=1024)
+    eng = Engine(cfg, EngineConfig(device="cuda:0", max_context=4000, max_batch=3, max_seqs=6, seed=21))
+    reqs = [
+        ([(7 * i) % 900 + 100 for i in range(2900)], SamplingParams(max_tokens=24, temperature=0.0, stop_on_eos=False)),
+        ([500 + i for i in range(9)], SamplingParams(max_tokens=20, temperature=1.0, seed=5, stop_on_eos=False)),
+        ([(11 * i) % 800 + 150 for i in range(1300)], SamplingParams(max_tokens=16, temperature=0.0,
+                                                                     stop_on_eos=False)),
+    ]
+    ref = [_alone(eng, p, sp) for p, sp in reqs]
+    got = _run_schedule(eng, reqs, admit_at=[0, 0, 1])
+    for i, (g, r) in enumerate(zip(got, ref)):
+        assert g == r, (i, g, r)
+
+
+@pytest.mark.gpu
+def test_attention_fault_fails_batched_rows(cuda):
+    """A decode-attention merge that gave up (the kernel's fault word) fails the rows whose
+    replays it covered, with an error, instead of streaming their tokens on."""
+    eng = _engine("cuda:0")
+    bat = ContinuousBatcher(eng)
+    s = eng.new_sequence()
+    eng.prefill([s], [[100 + i for i in range(20)]])
+    row = bat.admit(s, SamplingParams(max_tokens=64, temperature=0.0, stop_on_eos=False))
+    bat.step()
+    eng.attn_fault.fill_(1)  # what a merger that gave up writes
+    torch.cuda.synchronize()
+    gone = []
+    for _ in range(4):
+        gone += bat.step()
+        if gone:
+            break
+    assert gone == [row] and row.error is not None and "merge timed out" in str(row.error)
+    assert int(eng.attn_fault.item()) == 0

@@ -79,9 +79,66 @@ def test_fanout_two_ranks_balances_the_third_responder():
     _tokens_ok(d, 12)
 
 
-def test_warmup_rounds_after_the_first_are_short_timed_rounds_full():
-    """Warmup: the first round is full length, later ones decode --warmup-tokens; the timed rounds
-    (and the reported tokens) are full rounds."""
+def test_warmup_rounds_are_short_timed_rounds_full():
+    """Warmup rounds decode --warmup-tokens per engine; the timed rounds (and the reported tokens)
+    are full rounds."""
     d = _run(1, ["--shapes", "tiny", "--steps", "1", "--warmup", "2", "--max-tokens", "12", "--warmup-tokens", "4"], 0)
-    assert d["extra"]["warmup_rounds_tokens"] == [12, 4]
+    assert d["extra"]["warmup_rounds_tokens"] == [4, 4]
     _tokens_ok(d, 12)
+
+
+def _self_launched(n, extra=()):
+    """``python bench.py --gpus N`` with no launcher in the environment: bench.py starts the N
+    rank processes itself."""
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_PORT")}
+    env.update(LLMC_BENCH_DEVICE="cpu", OMP_NUM_THREADS="1")
+    r = subprocess.run([sys.executable, "bench.py", "--gpus", str(n), "--shapes", "tiny", "--steps", "1", "--warmup",
+                        "1", "--max-tokens", "8", "--warmup-tokens", "4", "--results-dir", "", *extra],
+                       cwd=ROOT, capture_output=True, timeout=600, env=env)
+    assert r.returncode == 0, r.stderr.decode()[-3000:]
+    lines = [ln for ln in r.stdout.decode().splitlines() if ln.strip().startswith("{")]
+    assert len(lines) == 1, r.stdout.decode()
+    return json.loads(lines[0])
+
+
+def test_self_launch_n_ranks_without_a_launcher():
+    for n in (2, 4, 8):
+        d = _self_launched(n)
+        assert d["n_gpus"] == n and d["steps"] == 1 and d["warmup"] == 1
+        assert d["config"]["global_batch"] == max(3, n)
+        _tokens_ok(d, 8)
+
+
+def test_self_launch_failing_rank_fails_the_job():
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    env.update(LLMC_BENCH_DEVICE="cpu", OMP_NUM_THREADS="1")
+    r = subprocess.run([sys.executable, "bench.py", "--gpus", "2", "--shapes", "tiny", "--model", "no-such-family",
+                        "--steps", "1", "--warmup", "0", "--results-dir", ""],
+                       cwd=ROOT, capture_output=True, timeout=300, env=env)
+    assert r.returncode != 0
+    assert not [ln for ln in r.stdout.decode().splitlines() if ln.startswith("{")]
+
+
+def test_config_names_are_honest():
+    """Config 2 / 3 as BASELINE.json words them with --judge-tp 1; the TP-judge defaults are
+    labelled variants."""
+    import argparse
+
+    import bench
+
+    def plan(n, **kw):
+        a = argparse.Namespace(config="fanout", shapes="full", model="llama-3-8b", judge="llama-3-8b",
+                               n_models=kw.get("n_models", 0), judge_tp=kw.get("judge_tp", 0))
+        r, j, _ = bench.make_plan(a, n)
+        return bench.config_name(a, n, r, j), r, j
+
+    name, r, j = plan(4, n_models=3, judge_tp=1)
+    assert name == "BASELINE config 2" and j["ranks"] == [3] and [e["ranks"] for e in r] == [[0], [1], [2]]
+    name, r, j = plan(8, judge_tp=1)
+    assert name == "BASELINE config 3" and j["ranks"] == [0] and len(r) == 8
+    name, _, j = plan(8)
+    assert name.startswith("variant of BASELINE config 3") and "TP=8" in name and len(j["ranks"]) == 8
+    name, _, _ = plan(4)
+    assert name.startswith("variant of BASELINE config 2") and "4 responders" in name
+    name, _, j = plan(1)
+    assert name.startswith("BASELINE config 2 on one GPU") and j["ranks"] == [0]

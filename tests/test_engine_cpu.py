@@ -132,7 +132,7 @@ def test_attn_buckets_batching_engine():
     """A batching 8B engine (>= 3 rows, rows x kv heads >= 32) splits a row of L keys into
     min(32, ceil(L / 2048)) ranges whatever its bucket and batch: the grid per head is min(32,
     capacity / 2048), so the kernel's min(grid, ceil(L / 2048)) never depends on the bucket;
-    engines of 1-2 rows, or rows x kv heads < 32, keep the per-context forms."""
+    engines of 1-2 rows keep the per-context forms."""
     import math
 
     from llm_consensus_amd.engine.engine import BATCHING_MIN_KEYS as MK
@@ -148,7 +148,16 @@ def test_attn_buckets_batching_engine():
         splits = {min(g, math.ceil(L / MK)) for c, _, g, _ in b16 if c >= L}
         assert len(splits) == 1 and splits.pop() == min(32, math.ceil(L / MK)), L
     assert attn_buckets(16394, 32, rows=2) == attn_buckets(16394, 32)
-    assert attn_buckets(16394, 32, nkv=2, rows=8) == attn_buckets(16394, 32, nkv=2)   # 16 units
+    # fewer than 32 (row, kv head) units (3 duplicate 8B responders: 24; TP ranks with 2 kv
+    # heads): still a length-only split, with a 512-key minimum so a row spreads further
+    from llm_consensus_amd.engine.engine import BATCHING_MIN_KEYS_FEW as MKF
+
+    for rows, nkv in ((3, 8), (8, 2), (3, 1)):
+        bf = attn_buckets(16394, 32, nkv=nkv, rows=rows)
+        assert all(ch == MKF and not fused for _, ch, _, fused in bf)
+        for L in (1, 511, 513, 2048, 5000, 13500, 16390):
+            splits = {min(g, math.ceil(L / MKF)) for c, _, g, _ in bf if c >= L}
+            assert len(splits) == 1 and splits.pop() == min(32, math.ceil(L / MKF)), (rows, nkv, L)
     assert attn_buckets(4106, 16, group=1, nkv=32, rows=4) == [(2048, MK, 1, False), (4096, MK, 2, False),
                                                                (4106, MK, 3, False)]  # Phi-3
     assert attn_buckets(200, 32, rows=4) == [(200, MK, 1, False)]

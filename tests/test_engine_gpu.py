@@ -149,3 +149,17 @@ def test_long_context_chunked_prefill(cuda):
     torch.cuda.synchronize()
     err = (sa.logits - sb.logits).abs().max().item()
     assert err < 0.05 * sa.logits.abs().max().item()
+
+
+def test_attention_merge_timeout_fails_the_request(cuda):
+    """The decode-attention fault word (set by a merger whose bounded spin gave up) fails the
+    request with an error; the word is re-armed and the next request decodes normally."""
+    from llm_consensus_amd.engine.engine import EngineError
+
+    eng = Engine(FAMILIES["llama-tiny"], EngineConfig(device="cuda:0", max_context=512, seed=1))
+    eng.attn_fault.fill_(1)  # what a merger that gave up writes
+    torch.cuda.synchronize()
+    with pytest.raises(EngineError, match="partial merge timed out"):
+        eng.generate_ids(list(range(100, 120)), 8, stop_on_eos=False)
+    assert int(eng.attn_fault.item()) == 0
+    assert len(eng.generate_ids(list(range(100, 120)), 8, stop_on_eos=False)) == 8

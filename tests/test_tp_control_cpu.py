@@ -118,10 +118,10 @@ class _FakeTP:
     def is_leader(self):
         return self.rank == 0
 
-    def leader_decides(self, v):
+    def leader_decides(self, v, kind="value"):
         from llm_consensus_amd.parallel.comm import TPGroup
 
-        return TPGroup.leader_decides(self, v)
+        return TPGroup.leader_decides(self, v, kind)
 
 
 class _FakeEngine:
@@ -221,3 +221,54 @@ def test_custom_timeout_fails_request_on_every_rank_then_resyncs():
     for rank, err, resyncs, ok in res:
         assert err and "timed out" in err, res
         assert resyncs == 1 and ok is not None and len(ok) == 4, res
+
+
+def _desync_worker(rank, world, port, q):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from llm_consensus_amd.parallel.comm import ControlDesync, TPGroup
+
+        tp = TPGroup(dist.group.WORLD, rank, world, ctrl=dist.group.WORLD)
+        assert tp.leader_decides(3 if rank == 0 else 0, "batch") == 3
+        # the follower left its decode early: it asks for the next batch size while the leader
+        # is still broadcasting a per-replay stop flag
+        try:
+            got = tp.leader_decides(0, "stop" if rank == 0 else "batch")
+            q.put((rank, "value", got))
+        except ControlDesync as ex:
+            q.put((rank, "desync", str(ex)))
+    except Exception as ex:  # noqa: BLE001
+        q.put((rank, "error", repr(ex)))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_control_decisions_of_different_kinds_never_pair_up():
+    (_, k0, v0), (_, k1, v1) = _spawn(_desync_worker, 2)
+    assert k0 == "value" and v0 == 0  # the leader's own value
+    assert k1 == "desync" and "expected batch" in v1 and "leader sent stop" in v1, (k1, v1)
+
+
+def test_gather_failure_replies_to_the_request_it_was_gathering_for():
+    """A TP engine host whose batch-size broadcast fails (a peer is gone) answers the request it
+    was gathering for with an error and finishes it — not a previous batch's requests."""
+    from types import SimpleNamespace
+
+    from llm_consensus_amd.runtime import worker as W
+
+    class BrokenTP:
+        size, rank, is_leader, ctrl = 2, 0, True, object()
+
+        def leader_decides(self, v, kind="value"):
+            raise RuntimeError("peer gone")
+
+    sent, finished = [], []
+    eng = SimpleNamespace(ecfg=SimpleNamespace(max_batch=1), tp=BrokenTP())
+    h = W._EngineHost("m", eng, sent.append, leader=True, on_finished=finished.append)
+    h.q.put(("gen", W._Req("r7", [1, 2], None, None)))
+    h.q.put(None)
+    h.t.join(timeout=10)
+    assert [m[:2] for m in sent] == [("error", "r7")] and "peer gone" in sent[0][2]
+    assert finished == ["r7"]

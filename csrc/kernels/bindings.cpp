@@ -38,14 +38,12 @@ int llmc_sample(const void*, int64_t, int, int, const void*, const void*, const 
                 void*, void*, void*, void*, void*, const void*, int, int, void*, void*, int, int, hipStream_t);
 int llmc_sample_parts();
 int llmc_moe_route(const void*, int, int, int, void*, void*, hipStream_t);
-int llmc_gemv_rowpar_ar(int, const void*, int, const void*, void*, int, int, int, const void* const*, int, int, long,
-                        hipStream_t);
 int llmc_moe_down_combine(int, const void*, int, const void*, const void*, const void*, void*, int, int, int, int,
                           hipStream_t);
 int llmc_moe_router(const void*, int, const void*, float, const void*, int, int, int, int, void*, void*, hipStream_t);
 int llmc_moe_align(const void*, int, int, int, int, void*, void*, void*, void*, hipStream_t);
-int llmc_moe_gemm(const void*, int, const void*, const void*, const void*, const void*, void*, int, int, int, int, int,
-                  int, hipStream_t);
+int llmc_moe_gemm(const void*, int, int, const void*, const void*, const void*, const void*, void*, int, int, int, int,
+                  int, int, int, hipStream_t);
 int llmc_moe_combine(const void*, const void*, const void*, void*, int, int, int, hipStream_t);
 int llmc_moe_gemv(int, const void*, int, const void*, float, const void*, const void*, int, void*, int, int, int, int,
                   hipStream_t);
@@ -60,7 +58,6 @@ int llmc_ipc_open(const void*, void**);
 int llmc_ipc_close(void*);
 int llmc_car_timed_out(void*, int*);
 size_t llmc_car_timeout_off();
-size_t llmc_gemv_ar_timeout_off();
 int llmc_car_reset(void*);
 int llmc_can_access_peer(int, int, int*);
 int llmc_car_twoshot(const void* const*, int, int, size_t, int, const void*, void*, long, int, int, hipStream_t);
@@ -154,10 +151,10 @@ PYBIND11_MODULE(_llmc_hip, m) {
     check(llmc_moe_align(P(ids), T, k, E, tile, P(sorted_rows), P(tile_expert), P(tile_count), P(counts), S(s)),
           "moe_align");
   });
-  m.def("moe_gemm", [](ptr A, int lda, ptr W, ptr sorted_rows, ptr tile_expert, ptr tile_count, ptr C, int ldc,
-                       int N, int K, int max_tiles, int a_row_div, int epi, ptr s) {
-    check(llmc_moe_gemm(P(A), lda, P(W), P(sorted_rows), P(tile_expert), P(tile_count), P(C), ldc, N, K, max_tiles,
-                        a_row_div, epi, S(s)),
+  m.def("moe_gemm", [](ptr A, int lda, int a_rows, ptr W, ptr sorted_rows, ptr tile_expert, ptr tile_count, ptr C,
+                       int ldc, int N, int K, int max_tiles, int a_row_div, int epi, int tile, ptr s) {
+    check(llmc_moe_gemm(P(A), lda, a_rows, P(W), P(sorted_rows), P(tile_expert), P(tile_count), P(C), ldc, N, K,
+                        max_tiles, a_row_div, epi, tile, S(s)),
           "moe_gemm");
   });
   m.def("moe_combine", [](ptr y, ptr w, ptr ids, ptr out, int T, int k, int H, ptr s) {
@@ -198,7 +195,6 @@ PYBIND11_MODULE(_llmc_hip, m) {
     return v;
   });
   m.def("car_timeout_off", []() { return llmc_car_timeout_off(); });
-  m.def("gemv_ar_timeout_off", []() { return llmc_gemv_ar_timeout_off(); });
   m.def("car_reset", [](ptr own) { check(llmc_car_reset(P(own)), "car_reset"); });
   m.def("can_access_peer", [](int dev, int peer) {
     int v = 0;
@@ -216,12 +212,6 @@ PYBIND11_MODULE(_llmc_hip, m) {
     std::vector<const void*> b(bases.size());
     for (size_t i = 0; i < bases.size(); ++i) b[i] = P(bases[i]);
     check(llmc_car_allreduce(b.data(), rank, world, cap, P(x), nbytes, S(s)), "car_allreduce");
-  });
-  m.def("gemv_rowpar_ar", [](int M, ptr x, int xs, ptr W, ptr h, int hs, int N, int K, const std::vector<ptr>& bases,
-                             int rank, int world, long cap, ptr s) {
-    std::vector<const void*> b(bases.size());
-    for (size_t i = 0; i < bases.size(); ++i) b[i] = P(bases[i]);
-    check(llmc_gemv_rowpar_ar(M, P(x), xs, P(W), P(h), hs, N, K, b.data(), rank, world, cap, S(s)), "gemv_rowpar_ar");
   });
   m.def("car_allgather", [](const std::vector<ptr>& bases, int rank, int world, size_t cap, ptr x, ptr out,
                             size_t nbytes, ptr s) {

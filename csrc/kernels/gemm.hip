@@ -26,9 +26,11 @@ __device__ __forceinline__ int xcd_remap(int bid, int nwg) {
   return base + bid / 8;
 }
 
-// GATHER = MoE grouped GEMM (K11): the M axis is a list of expert-sorted rows padded to 128-row
-// tiles (moe_align); tile t multiplies by expert tile_expert[t]'s weights, gathers A rows
-// sorted_rows[i] / a_row_div and scatters C rows sorted_rows[i] (-1 = padding).
+// GATHER = MoE grouped GEMM (K11) for small expert groups (< 256 rows per expert on average;
+// larger ones take gemm256_kernel<EPI, true>): the M axis is a list of expert-sorted rows padded to
+// 128-row tiles (moe_align); tile t multiplies by expert tile_expert[t]'s weights, gathers A rows
+// sorted_rows[i] / a_row_div and scatters C rows sorted_rows[i] (-1 = padding). EPI 3 = SiLU-mul of
+// interleaved gate/up columns, as the dense kernel's.
 template <int EPI, bool GATHER>
 __global__ __launch_bounds__(256, 2) void gemm_kernel(const bf16_t* __restrict__ A, int lda,
                                                       const bf16_t* __restrict__ W, int ldw, void* __restrict__ C,
@@ -41,11 +43,13 @@ __global__ __launch_bounds__(256, 2) void gemm_kernel(const bf16_t* __restrict__
   const int num_n = (N + kBN - 1) / kBN;
   int m0, n0;
   if constexpr (GATHER) {
+    // bijective XCD remap: consecutive tiles of one expert share an N panel on one XCD's L2
     const int max_tiles = M / kBM;  // M = padded row capacity
-    const int tile = blockIdx.x % max_tiles;
+    const int id = xcd_remap(blockIdx.x, max_tiles * num_n);
+    const int tile = id % max_tiles;
     if (tile >= tile_count[0]) return;
     m0 = tile * kBM;
-    n0 = (blockIdx.x / max_tiles) * kBN;
+    n0 = (id / max_tiles) * kBN;
     W += static_cast<int64_t>(tile_expert[tile]) * N * ldw;
   } else {
     const int num_m = (M + kBM - 1) / kBM;
@@ -126,9 +130,13 @@ __global__ __launch_bounds__(256, 2) void gemm_kernel(const bf16_t* __restrict__
 #pragma unroll
     for (int b = 0; b < 2; ++b) {
       const int n = n0 + wc * 64 + b * 32 + r;
-      if (n >= N) continue;
 #pragma unroll
       for (int i = 0; i < 16; ++i) {
+        const float v = acc[a][b][i];
+        // EPI 3: interleaved (gate, up) columns n, n + 1 sit in lanes r, r ^ 1 (N even: both or
+        // neither in range), exchanged before any lane leaves the loop body
+        const float pv = EPI == 3 ? __shfl_xor(v, 1, 64) : 0.f;
+        if (n >= N) continue;
         int m = m0 + wr * 64 + a * 32 + (i & 3) + 8 * (i >> 2) + 4 * hh;
         if constexpr (GATHER) {
           m = sorted_rows[m];
@@ -136,9 +144,10 @@ __global__ __launch_bounds__(256, 2) void gemm_kernel(const bf16_t* __restrict__
         } else {
           if (m >= M) continue;
         }
-        const float v = acc[a][b][i];
         if constexpr (EPI == 0) {
           reinterpret_cast<bf16_t*>(C)[static_cast<int64_t>(m) * ldc + n] = f32_to_bf16(v);
+        } else if constexpr (EPI == 3) {
+          if ((n & 1) == 0) reinterpret_cast<bf16_t*>(C)[static_cast<int64_t>(m) * ldc + n / 2] = f32_to_bf16(silu(v) * pv);
         } else if constexpr (EPI == 1) {
           reinterpret_cast<float*>(C)[static_cast<int64_t>(m) * ldc + n] = v;
         } else {
@@ -252,10 +261,19 @@ __device__ __forceinline__ void gemm256_epilogue(const f32x4 (&acc)[8][4], void*
   }
 }
 
-template <int EPI>
+// GATHER = the MoE grouped GEMM (K11) on this pipeline: M = max_tiles x 256 rows of moe_align's
+// expert-sorted, 256-row-padded pair list; tile t multiplies by expert tile_expert[t]'s [N, K]
+// weights, its A rows are gathered (sorted_rows[i] / a_row_div of the a_rows-row matrix A: the
+// per-lane LDS-DMA offsets simply point at the gathered rows) and its C rows scattered to
+// sorted_rows[i] (-1 = padding, not stored). Tiles beyond tile_count[0] exit at once.
+template <int EPI, bool GATHER = false>
 __global__ __launch_bounds__(512, 1) void gemm256_kernel(const bf16_t* __restrict__ A, int lda,
                                                           const bf16_t* __restrict__ W, int ldw, void* __restrict__ C,
-                                                          int ldc, int M, int N, int K) {
+                                                          int ldc, int M, int N, int K,
+                                                          const int32_t* __restrict__ sorted_rows = nullptr,
+                                                          const int32_t* __restrict__ tile_expert = nullptr,
+                                                          const int32_t* __restrict__ tile_count = nullptr,
+                                                          int a_row_div = 1, int a_rows = 0) {
   __shared__ __attribute__((aligned(16))) char smem[kSlots * kQuarter];
   const int num_m = (M + kT - 1) / kT, num_n = (N + kT - 1) / kT;
   const int id = xcd_remap(blockIdx.x, num_m * num_n);
@@ -264,15 +282,20 @@ __global__ __launch_bounds__(512, 1) void gemm256_kernel(const bf16_t* __restric
   const int gsz = min(num_m - first_m, kGroupM);
   const int in_group = id - group * kGroupM * num_n;
   const int m0 = (first_m + in_group % gsz) * kT, n0 = (in_group / gsz) * kT;
+  if constexpr (GATHER) {
+    const int tile = m0 / kT;
+    if (tile >= tile_count[0]) return;  // block-uniform, before any barrier
+    W += static_cast<int64_t>(tile_expert[tile]) * N * ldw;
+  }
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wr = wave >> 2, wc = wave & 3;
   const int l16 = lane & 15, lg = lane >> 4;
-  // buffer descriptors on this tile's rows (offsets stay < 2 GiB: 256 rows x ld); per-lane byte
-  // offsets of the 4 quarter types x 2 pieces (rows clamped to the matrix)
+  // buffer descriptors on this tile's rows (offsets stay < 2 GiB: 256 rows x ld; GATHER: the whole
+  // A, host-checked); per-lane byte offsets of the 4 quarter types x 2 pieces (rows clamped)
   const int rowsA = min(kT, M - m0), rowsW = min(kT, N - n0);
   const __amdgpu_buffer_rsrc_t rsA = __builtin_amdgcn_make_buffer_rsrc(
-      (void*)(A + static_cast<int64_t>(m0) * lda), 0, rowsA * lda * 2, 0x00020000);
+      (void*)(GATHER ? A : A + static_cast<int64_t>(m0) * lda), 0, (GATHER ? a_rows : rowsA) * lda * 2, 0x00020000);
   const __amdgpu_buffer_rsrc_t rsW = __builtin_amdgcn_make_buffer_rsrc(
       (void*)(W + static_cast<int64_t>(n0) * ldw), 0, rowsW * ldw * 2, 0x00020000);
   uint32_t voff[4][2];
@@ -282,7 +305,11 @@ __global__ __launch_bounds__(512, 1) void gemm256_kernel(const bf16_t* __restric
     const int r = s >> 3, c = (s & 7) ^ ((r >> 1) & 7);
 #pragma unroll
     for (int h = 0; h < 2; ++h) {
-      const int ar = min((r >> 6) * 128 + h * 64 + (r & 63), rowsA - 1);
+      int ar = min((r >> 6) * 128 + h * 64 + (r & 63), rowsA - 1);
+      if constexpr (GATHER) {
+        const int sr = sorted_rows[m0 + ar];
+        ar = sr < 0 ? 0 : sr / a_row_div;
+      }
       const int wrow = min((r >> 5) * 64 + h * 32 + (r & 31), rowsW - 1);
       voff[h == 0 ? 0 : 3][i] = static_cast<uint32_t>((ar * lda + c * 8) * 2);
       voff[1 + h][i] = static_cast<uint32_t>((wrow * ldw + c * 8) * 2);
@@ -383,7 +410,18 @@ __global__ __launch_bounds__(512, 1) void gemm256_kernel(const bf16_t* __restric
     end_phase();
   }
   if (wr == 0) asm volatile("s_barrier" ::: "memory");
-  gemm256_epilogue<EPI>(acc, C, ldc, M, N, m0, n0, wr, wc, l16, lg);
+  if constexpr (GATHER) {
+    const bool vec_ok = (N % 4 == 0) && (ldc % 4 == 0);
+#pragma unroll
+    for (int mi = 0; mi < 8; ++mi) {
+      const int m = sorted_rows[m0 + wr * 128 + mi * 16 + l16];
+      if (m < 0) continue;
+#pragma unroll
+      for (int ni = 0; ni < 4; ++ni) store4<EPI>(C, ldc, N, m, n0 + wc * 64 + ni * 16 + 4 * lg, acc[mi][ni], vec_ok);
+    }
+  } else {
+    gemm256_epilogue<EPI>(acc, C, ldc, M, N, m0, n0, wr, wc, l16, lg);
+  }
 }
 
 }  // namespace llmc
@@ -409,20 +447,39 @@ extern "C" int llmc_gemm(const void* A, int lda, const void* W, int ldw, void* C
   return static_cast<int>(hipGetLastError());
 }
 
-// Grouped expert GEMM over moe_align's padded row list (max_tiles * 128 rows of capacity).
-extern "C" int llmc_moe_gemm(const void* A, int lda, const void* W, const void* sorted_rows, const void* tile_expert,
-                             const void* tile_count, void* C, int ldc, int N, int K, int max_tiles, int a_row_div,
-                             int epi, hipStream_t s) {
-  if (K % kBK != 0) return -1;
-  const int nwg = max_tiles * ((N + kBN - 1) / kBN);
-  const int M = max_tiles * kBM;
+// Grouped expert GEMM over moe_align's padded row list (max_tiles * tile rows of capacity; tile =
+// 256: the 256 x 256 LDS-DMA pipeline, 128: the two-buffer 128 x 128 kernel for small groups).
+// A: a_rows rows (gathered by sorted_rows / a_row_div); epi 0 bf16, 1 f32, 3 SiLU-mul of
+// interleaved gate/up columns into C[., N / 2].
+extern "C" int llmc_moe_gemm(const void* A, int lda, int a_rows, const void* W, const void* sorted_rows,
+                             const void* tile_expert, const void* tile_count, void* C, int ldc, int N, int K,
+                             int max_tiles, int a_row_div, int epi, int tile, hipStream_t s) {
+  if (K % kTK != 0 || lda % 8 != 0 || K % 8 != 0 || a_rows < 1 || (epi == 3 && N % 2 != 0)) return -1;
+  if (epi != 0 && epi != 1 && epi != 3) return -2;
   const int32_t* sr = (const int32_t*)sorted_rows;
   const int32_t* te = (const int32_t*)tile_expert;
   const int32_t* tc = (const int32_t*)tile_count;
+  const bf16_t* a = (const bf16_t*)A;
+  const bf16_t* w = (const bf16_t*)W;
+  if (tile == kT) {
+    // gathered-row offsets are 32-bit byte offsets into the whole A
+    if (static_cast<int64_t>(a_rows) * lda * 2 >= (1ll << 31) || static_cast<int64_t>(kT) * K * 2 >= (1ll << 31))
+      return -1;
+    const int M = max_tiles * kT, nwg = max_tiles * ((N + kT - 1) / kT);
+    switch (epi) {
+      case 0: gemm256_kernel<0, true><<<nwg, 512, 0, s>>>(a, lda, w, K, C, ldc, M, N, K, sr, te, tc, a_row_div, a_rows); break;
+      case 1: gemm256_kernel<1, true><<<nwg, 512, 0, s>>>(a, lda, w, K, C, ldc, M, N, K, sr, te, tc, a_row_div, a_rows); break;
+      default: gemm256_kernel<3, true><<<nwg, 512, 0, s>>>(a, lda, w, K, C, ldc, M, N, K, sr, te, tc, a_row_div, a_rows); break;
+    }
+    return static_cast<int>(hipGetLastError());
+  }
+  if (tile != kBM) return -1;
+  const int nwg = max_tiles * ((N + kBN - 1) / kBN);
+  const int M = max_tiles * kBM;
   switch (epi) {
-    case 0: gemm_kernel<0, true><<<nwg, 256, 0, s>>>((const bf16_t*)A, lda, (const bf16_t*)W, K, C, ldc, M, N, K, sr, te, tc, a_row_div); break;
-    case 1: gemm_kernel<1, true><<<nwg, 256, 0, s>>>((const bf16_t*)A, lda, (const bf16_t*)W, K, C, ldc, M, N, K, sr, te, tc, a_row_div); break;
-    default: return -2;
+    case 0: gemm_kernel<0, true><<<nwg, 256, 0, s>>>(a, lda, w, K, C, ldc, M, N, K, sr, te, tc, a_row_div); break;
+    case 1: gemm_kernel<1, true><<<nwg, 256, 0, s>>>(a, lda, w, K, C, ldc, M, N, K, sr, te, tc, a_row_div); break;
+    default: gemm_kernel<3, true><<<nwg, 256, 0, s>>>(a, lda, w, K, C, ldc, M, N, K, sr, te, tc, a_row_div); break;
   }
   return static_cast<int>(hipGetLastError());
 }

@@ -29,7 +29,7 @@ static int launch_gemv_g(const void* x, int x_stride, const void* nw, float eps,
   const int rows_per_block = WAVES * RPW;
   const int grid = (N + rows_per_block - 1) / rows_per_block;
   kern<<<grid, NT, lds, s>>>((const bf16_t*)x, x_stride, (const bf16_t*)nw, eps, (const bf16_t*)W, out, out_stride, N,
-                             K, nullptr, 1, rope, ArEpi{});
+                             K, nullptr, 1, rope);
   return static_cast<int>(hipGetLastError());
 }
 
@@ -149,7 +149,7 @@ static int launch_moe_gemv(int npairs, const void* x, int x_stride, const void* 
   dim3 grid((N + WAVES * RPW - 1) / (WAVES * RPW), npairs);
   gemv_kernel<1, NT, RPW, 4, PRO, EPI, true><<<grid, NT, lds, s>>>(
       (const bf16_t*)x, x_stride, (const bf16_t*)nw, eps, (const bf16_t*)W, out, out_stride, N, K,
-      (const int32_t*)ids, x_div, RopeEpi{}, ArEpi{});
+      (const int32_t*)ids, x_div, RopeEpi{});
   return static_cast<int>(hipGetLastError());
 }
 
@@ -167,42 +167,6 @@ static int moe_gemv_geom(int npairs, const void* x, int x_stride, const void* nw
   }
 }
 }  // namespace llmc
-
-// Row-parallel decode projection with its all-reduce fused into the epilogue (EPI_AR): h = sum over
-// the TP group of x_rank @ W_rank^T (+ residual, folded by rank 0). 16-wave blocks, one row per
-// wave; the grid must be resident at once (checked: <= 256 blocks, one per CU), and every rank launches
-// the same shape. bases: every rank's fused-AR buffer (kArSigBytes + 2 * cap).
-extern "C" size_t llmc_gemv_ar_timeout_off() { return kArTimeoutOff; }
-
-extern "C" int llmc_gemv_rowpar_ar(int M, const void* x, int x_stride, const void* W, void* h, int h_stride, int N,
-                                   int K, const void* const* bases, int rank, int world, long cap, hipStream_t s) {
-  constexpr int NT = 1024, WAVES = NT / kWave;
-  if (M < 1 || M > 4 || K % 8 != 0 || world < 2 || world > 8 || rank < 0 || rank >= world) return -1;
-  const int grid = (N + WAVES - 1) / WAVES;
-  // every block must be resident at once (one 16-wave block per CU): blocks spin on their peers
-  if (grid > kArMaxBlocks || grid > 256 || static_cast<long>(grid) * WAVES * M * 2 > cap) return -2;
-  ArEpi ar{};
-  for (int r = 0; r < 8; ++r) ar.base[r] = r < world ? static_cast<char*>(const_cast<void*>(bases[r])) : nullptr;
-  ar.rank = rank;
-  ar.world = world;
-  ar.cap = cap;
-  const size_t lds = static_cast<size_t>(M) * K * sizeof(bf16_t) + 2 * M * WAVES * sizeof(float);
-  if (lds > 64 * 1024) return -3;
-#define LLMC_AR_CASE(MM)                                                                                         \
-  case MM:                                                                                                       \
-    gemv_kernel<MM, NT, 1, 4, PRO_NONE, EPI_AR, false><<<grid, NT, lds, s>>>(                                    \
-        (const bf16_t*)x, x_stride, nullptr, 0.f, (const bf16_t*)W, h, h_stride, N, K, nullptr, 1, RopeEpi{},    \
-        ar);                                                                                         \
-    break;
-  switch (M) {
-    LLMC_AR_CASE(1)
-    LLMC_AR_CASE(2)
-    LLMC_AR_CASE(3)
-    LLMC_AR_CASE(4)
-  }
-#undef LLMC_AR_CASE
-  return static_cast<int>(hipGetLastError());
-}
 
 // MoE decode down projection fused with the combine: h[t] += sum_j w[t, j] * (W_down[ids[t, j]] . act[t*k + j])
 // for top-2 routing (k == 2), one block per 16 output rows per token, each wave streaming its row
@@ -224,7 +188,7 @@ extern "C" int llmc_moe_down_combine(int T, const void* act, int act_stride, con
   wts.cos_t = static_cast<const float*>(w);
   dim3 grid((N + WAVES - 1) / WAVES, T);
   kern<<<grid, NT, lds, s>>>((const bf16_t*)act, act_stride, nullptr, 0.f, (const bf16_t*)W, h, h_stride, N, K,
-                             (const int32_t*)ids, 1, wts, ArEpi{});
+                             (const int32_t*)ids, 1, wts);
   return static_cast<int>(hipGetLastError());
 }
 
@@ -254,7 +218,7 @@ static int launch_sweep(const void* x, const void* nw, const void* W, void* out,
   const size_t lds = static_cast<size_t>(K) * sizeof(bf16_t) + WAVES * sizeof(float);
   const int grid = (N + WAVES * RPW - 1) / (WAVES * RPW);
   gemv_kernel<1, NT, RPW, UNROLL, PRO_NORM, EPI_BF16, false><<<grid, NT, lds, s>>>(
-      (const bf16_t*)x, K, (const bf16_t*)nw, 1e-5f, (const bf16_t*)W, out, N, N, K, nullptr, 1, RopeEpi{}, ArEpi{});
+      (const bf16_t*)x, K, (const bf16_t*)nw, 1e-5f, (const bf16_t*)W, out, N, N, K, nullptr, 1, RopeEpi{});
   return static_cast<int>(hipGetLastError());
 }
 }  // namespace llmc

@@ -25,7 +25,7 @@
 namespace llmc {
 
 enum { PRO_NONE = 0, PRO_NORM = 1 };
-enum { EPI_BF16 = 0, EPI_F32 = 1, EPI_RESADD = 2, EPI_SILU = 3, EPI_ROPE = 4, EPI_COMBINE = 5, EPI_AR = 6 };
+enum { EPI_BF16 = 0, EPI_F32 = 1, EPI_RESADD = 2, EPI_SILU = 3, EPI_ROPE = 4, EPI_COMBINE = 5 };
 
 struct RopeEpi {
   bf16_t* q_out;            // [M, q_stride], canonical head-major layout
@@ -37,24 +37,6 @@ struct RopeEpi {
   const float* cos_t;       // [max_pos][D/2]
   const float* sin_t;
   int nh, nkv, D, bs;
-};
-
-// EPI_AR operands: a row-parallel projection (TP o_proj / down_proj at decode) whose all-reduce
-// runs in the GEMV's own epilogue, block by block, over the one-shot IPC protocol of
-// allreduce.hip (its own buffer: signals | data parity 0 | data parity 1). Block b of every rank
-// owns the same rows, so block b only waits for block b of the peers: rank 0 folds the residual,
-// every rank stages bf16 partials, flags its peers (system-scope release), waits for theirs,
-// sums all ranks' partials in rank order (bitwise-identical on every rank, as the separate
-// all-reduce kernel) and writes h. Saves that kernel's launch and boundary per row-parallel
-// projection. Needs every block resident at once (grid <= one round of the chip).
-constexpr int kArSigBytes = 64 * 1024;
-constexpr int kArMaxBlocks = 1024;
-constexpr int kArFlagOff = 4 * kArMaxBlocks;                    // after ctr[kArMaxBlocks]
-constexpr int kArTimeoutOff = kArFlagOff + kArMaxBlocks * 8 * 4;  // flags [blocks][8 ranks]
-struct ArEpi {
-  char* base[8];  // every rank's buffer, mapped in this process (own one included)
-  int rank, world;
-  long cap;       // bytes per data parity
 };
 
 // Batched decode (3 <= M <= 32 rows): the MFMA form in gemv_mfma.hip, same prologue/epilogues
@@ -69,7 +51,7 @@ __global__ __launch_bounds__(NT) void gemv_kernel(const bf16_t* __restrict__ x, 
                                                   const bf16_t* __restrict__ norm_w, float eps,
                                                   const bf16_t* __restrict__ W, void* __restrict__ out,
                                                   int out_stride, int N, int K, const int32_t* __restrict__ expert_ids,
-                                                  int x_div, RopeEpi rope, ArEpi ar) {
+                                                  int x_div, RopeEpi rope) {
   constexpr int WAVES = NT / kWave;
   constexpr bool PAIR_LDS = (EPI == EPI_SILU || EPI == EPI_ROPE) && RPW == 1;  // host: N % (2 * WAVES) == 0
   // EXPERT (MoE decode): blockIdx.y = (token, slot) pair; weights of expert expert_ids[pair],
@@ -150,14 +132,6 @@ __global__ __launch_bounds__(NT) void gemv_kernel(const bf16_t* __restrict__ x, 
   issue(cur, lane);
   __builtin_amdgcn_sched_barrier(0);
 
-
-  // EPI_AR: this block's epoch, read now (behind the first weight batch) and used in the epilogue
-  uint32_t ar_epoch = 0;
-  if constexpr (EPI == EPI_AR) {
-    if (threadIdx.x == 0)
-      ar_epoch = __hip_atomic_load(reinterpret_cast<uint32_t*>(ar.base[ar.rank]) + blockIdx.x, __ATOMIC_RELAXED,
-                                   __HIP_MEMORY_SCOPE_SYSTEM) + 1;
-  }
 
   // RoPE epilogue operands (PAIR_LDS: one row per even wave) are wave-uniform, so they come
   // through the SCALAR cache (s_load, counted by lgkmcnt): as vector loads they queued behind the
@@ -281,7 +255,7 @@ __global__ __launch_bounds__(NT) void gemv_kernel(const bf16_t* __restrict__ x, 
     }
   }
   __syncthreads();
-  if (!PAIR_LDS && EPI != EPI_AR && row0 >= N) return;  // PAIR_LDS / EPI_AR: every wave reaches the barriers
+  if (!PAIR_LDS && row0 >= N) return;  // PAIR_LDS: every wave reaches the pair barrier
   if constexpr (PAIR_LDS && EPI == EPI_ROPE) {
     const int w_u = __builtin_amdgcn_readfirstlane(wave);
     const int r_u = (blockIdx.x * WAVES + w_u) * RPW;
@@ -413,64 +387,6 @@ __global__ __launch_bounds__(NT) void gemv_kernel(const bf16_t* __restrict__ x, 
           }
         }
     }
-    return;
-  }
-  if constexpr (EPI == EPI_AR) {
-    static_assert(RPW == 1, "EPI_AR: one row per wave");
-    __shared__ uint32_t ar_ep;
-    if (threadIdx.x == 0) ar_ep = ar_epoch;
-    // 1. stage this rank's bf16 partial (rank 0: + residual) for its (row, token) pairs
-    const int b = blockIdx.x;
-    const int bf_slots = WAVES * M;  // bf16 values per block
-    char* own = ar.base[ar.rank] + kArSigBytes;
-    __syncthreads();
-    const uint32_t epoch = ar_ep;
-    const long doff = static_cast<long>(epoch & 1) * ar.cap;
-    if (lane < M && row0 < N) {
-      float v = 0.f;
-#pragma unroll
-      for (int m = 0; m < M; ++m)
-        if (lane == m) v = acc[0][m];  // wave_sum left every lane holding every token's sum
-      if (ar.rank == 0) v += bf16_to_f32(reinterpret_cast<const bf16_t*>(out)[static_cast<int64_t>(lane) * out_stride + row0]);
-      reinterpret_cast<bf16_t*>(own + doff)[b * bf_slots + wave * M + lane] = f32_to_bf16(v);
-    }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    // 2. flag every peer, wait for every peer's flag of this block (bounded), acquire
-    const int tid = threadIdx.x;
-    if (tid < ar.world) {
-      uint32_t* f = reinterpret_cast<uint32_t*>(ar.base[tid] + kArFlagOff) + b * 8 + ar.rank;
-      __hip_atomic_store(f, epoch, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
-    }
-    if (tid < ar.world) {
-      uint32_t* f = reinterpret_cast<uint32_t*>(ar.base[ar.rank] + kArFlagOff) + b * 8 + tid;
-      unsigned spins = 0;
-      while (__hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) < epoch) {
-        __builtin_amdgcn_s_sleep(2);
-        if (++spins > (1u << 24)) {  // ~seconds: give up instead of hanging the GPU
-          __hip_atomic_store(reinterpret_cast<uint32_t*>(ar.base[ar.rank] + kArTimeoutOff), 1u, __ATOMIC_RELAXED,
-                             __HIP_MEMORY_SCOPE_SYSTEM);
-          break;
-        }
-      }
-      __atomic_thread_fence(__ATOMIC_ACQUIRE);
-    }
-    __syncthreads();
-    // 3. sum every rank's partial in rank order, write h
-    if (lane < M && row0 < N) {
-      float sum = 0.f;
-      bf16_t in[8];
-#pragma unroll
-      for (int r = 0; r < 8; ++r)
-        if (r < ar.world) in[r] = reinterpret_cast<const bf16_t*>(ar.base[r] + kArSigBytes + doff)[b * bf_slots + wave * M + lane];
-#pragma unroll
-      for (int r = 0; r < 8; ++r)
-        if (r < ar.world) sum += bf16_to_f32(in[r]);
-      reinterpret_cast<bf16_t*>(out)[static_cast<int64_t>(lane) * out_stride + row0] = f32_to_bf16(sum);
-    }
-    if (tid == 0)
-      __hip_atomic_store(reinterpret_cast<uint32_t*>(ar.base[ar.rank]) + b, epoch, __ATOMIC_RELAXED,
-                         __HIP_MEMORY_SCOPE_SYSTEM);
     return;
   }
   if constexpr (COMBINE) {

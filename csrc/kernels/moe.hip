@@ -5,8 +5,8 @@
 // Data flow (prefill, T tokens, top-k):
 //   router logits [T, E] f32 --moe_route--> w [T, k] f32, ids [T, k] i32
 //   ids --moe_align--> sorted_rows [cap] (pair index t*k+j grouped by expert, each expert padded
-//                      to 128-row tiles, -1 = pad), tile_expert [max_tiles], tile_count [1]
-//   x [T, H] --gemm<GATHER>(a_row_div = k)--> gu [T*k, 2I] --silu_mul--> act [T*k, I]
+//                      to 128- or 256-row tiles, -1 = pad), tile_expert [max_tiles], tile_count [1]
+//   x [T, H] --gemm<GATHER, EPI_SILU>(a_row_div = k)--> act [T*k, I]   (SiLU-mul in the epilogue)
 //   act --gemm<GATHER>(a_row_div = 1)--> y [T*k, H] --moe_combine--> h[t] += sum_j w[t,j] y[t*k+j]
 // The combine is a fixed-order sum in f32 (no float atomics: bitwise reproducible,
 // MI355X_MICROARCH.md "Global float atomics" pitfall). Expert parallel: moe_ep_localize maps the
@@ -135,10 +135,9 @@ __global__ __launch_bounds__(kRouterThreads) void moe_router_kernel(
 }
 
 constexpr int kAlignThreads = 1024;
-constexpr int kMoeTile = 128;
 
 __global__ __launch_bounds__(kAlignThreads) void moe_align_kernel(const int32_t* __restrict__ ids, int npairs, int E,
-                                                                  int cap, int max_tiles,
+                                                                  int cap, int max_tiles, int tile,
                                                                   int32_t* __restrict__ sorted_rows,
                                                                   int32_t* __restrict__ tile_expert,
                                                                   int32_t* __restrict__ tile_count,
@@ -158,14 +157,14 @@ __global__ __launch_bounds__(kAlignThreads) void moe_align_kernel(const int32_t*
     int o = 0;
     for (int e = 0; e < E; ++e) {
       off[e] = o;
-      const int nt = (cnt[e] + kMoeTile - 1) / kMoeTile;
-      for (int tt = 0; tt < nt; ++tt) tile_expert[o / kMoeTile + tt] = e;
-      o += nt * kMoeTile;
+      const int nt = (cnt[e] + tile - 1) / tile;
+      for (int tt = 0; tt < nt; ++tt) tile_expert[o / tile + tt] = e;
+      o += nt * tile;
       if (counts_out) counts_out[e] = cnt[e];
     }
     off[E] = o;
-    tile_count[0] = o / kMoeTile;
-    for (int tt = o / kMoeTile; tt < max_tiles; ++tt) tile_expert[tt] = 0;
+    tile_count[0] = o / tile;
+    for (int tt = o / tile; tt < max_tiles; ++tt) tile_expert[tt] = 0;
   }
   __syncthreads();
   for (int i = threadIdx.x; i < npairs; i += kAlignThreads) {
@@ -231,10 +230,10 @@ int llmc_moe_router(const void* x, int x_stride, const void* norm_w, float eps, 
 // tile must be 128 (the grouped GEMM's M tile); max_tiles = ceil(npairs/128) + E
 int llmc_moe_align(const void* ids, int T, int k, int E, int tile, void* sorted_rows, void* tile_expert,
                    void* tile_count, void* counts, hipStream_t s) {
-  if (tile != kMoeTile || E > 64) return -1;
+  if ((tile != 128 && tile != 256) || E > 64) return -1;
   const int npairs = T * k;
-  const int max_tiles = (npairs + kMoeTile - 1) / kMoeTile + E;
-  moe_align_kernel<<<1, kAlignThreads, 0, s>>>((const int32_t*)ids, npairs, E, max_tiles * kMoeTile, max_tiles,
+  const int max_tiles = (npairs + tile - 1) / tile + E;
+  moe_align_kernel<<<1, kAlignThreads, 0, s>>>((const int32_t*)ids, npairs, E, max_tiles * tile, max_tiles, tile,
                                                (int32_t*)sorted_rows, (int32_t*)tile_expert, (int32_t*)tile_count,
                                                (int32_t*)counts);
   return static_cast<int>(hipGetLastError());

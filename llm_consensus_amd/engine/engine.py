@@ -447,7 +447,9 @@ class Engine:
     def _expert_ffn(self, A: torch.Tensor, ids: torch.Tensor, Lw) -> torch.Tensor:
         """y[p] = down_e(silu(gate_up_e(A[p // k]))) for every (row, slot) pair p of ``ids`` [n, k]
         (expert ids index this rank's expert tensors): expert GEMVs for <= 4 rows, else expert
-        alignment + the gathered-row grouped MFMA GEMM (K10/K11)."""
+        alignment + the gathered-row grouped MFMA GEMM (K10/K11: the 256 x 256 LDS-DMA pipeline
+        once the pairs average >= 256 rows per expert, 128-row tiles below), SiLU fused into the
+        gate_up epilogue."""
         c = self.cfg
         n, k = ids.shape
         E_l, I_l, H = Lw.w_gu.shape[0], self.w.inter, c.hidden
@@ -465,15 +467,16 @@ class Engine:
             ops.moe_gemv(A, Lw.w_gu, ids, k, act, 2 * I_l, H, EPI_SILU)
             ops.moe_gemv(act, Lw.w_down, ids, 1, y, H, I_l, EPI_BF16)
             return y
-        mt = ops.moe_max_tiles(n * k, E_l)
-        sr = torch.empty(mt * ops.MOE_TILE, dtype=torch.int32, device=A.device)
+        tile = ops.moe_tile(n * k, E_l)
+        mt = ops.moe_max_tiles(n * k, E_l, tile)
+        sr = torch.empty(mt * tile, dtype=torch.int32, device=A.device)
         te = torch.empty(mt, dtype=torch.int32, device=A.device)
         tc = torch.empty(1, dtype=torch.int32, device=A.device)
-        ops.moe_align(ids, E_l, sr, te, tc)
-        gu = torch.empty(n * k, 2 * I_l, dtype=torch.bfloat16, device=A.device)
-        ops.moe_gemm(A, Lw.w_gu, sr, te, tc, gu, 2 * I_l, H, mt, k)
-        act = ops.silu_mul_interleaved(gu)
-        ops.moe_gemm(act, Lw.w_down, sr, te, tc, y, H, I_l, mt, 1)
+        ops.moe_align(ids, E_l, sr, te, tc, tile=tile)
+        # gate_up with the SiLU-mul in its epilogue: the [pairs, 2I] product never reaches memory
+        act = torch.empty(n * k, I_l, dtype=torch.bfloat16, device=A.device)
+        ops.moe_gemm(A, Lw.w_gu, sr, te, tc, act, 2 * I_l, H, mt, k, epi=EPI_SILU, tile=tile)
+        ops.moe_gemm(act, Lw.w_down, sr, te, tc, y, H, I_l, mt, 1, tile=tile)
         return y
 
     def _route(self, xn: torch.Tensor, Lw):

@@ -277,7 +277,14 @@ def _advance_cpu(tok, tokens_in, positions, seq_lens, slots, block_tables, bs, o
 
 
 # -- MoE -----------------------------------------------------------------------------------------
-MOE_TILE = 128
+MOE_TILE = 128       # row tile of the small-group grouped GEMM (128 x 128 kernel)
+MOE_TILE_LARGE = 256  # ... and of the 256 x 256 LDS-DMA pipeline
+
+
+def moe_tile(npairs: int, E: int) -> int:
+    """Row tile of the grouped expert GEMM: the 256 x 256 pipeline once the (token, slot) pairs
+    average >= 256 rows per expert (padding stays < 1/2 tile per expert), else 128-row tiles."""
+    return MOE_TILE_LARGE if npairs >= MOE_TILE_LARGE * E else MOE_TILE
 
 
 def moe_route(logits: torch.Tensor, k: int, w_out: torch.Tensor, ids_out: torch.Tensor):
@@ -291,19 +298,23 @@ def moe_route(logits: torch.Tensor, k: int, w_out: torch.Tensor, ids_out: torch.
     return w_out, ids_out
 
 
-def moe_max_tiles(npairs: int, E: int) -> int:
-    return (npairs + MOE_TILE - 1) // MOE_TILE + E
+def moe_max_tiles(npairs: int, E: int, tile: int = MOE_TILE) -> int:
+    return (npairs + tile - 1) // tile + E
 
 
-def moe_align(ids: torch.Tensor, E: int, sorted_rows, tile_expert, tile_count, counts=None):
+def moe_align(ids: torch.Tensor, E: int, sorted_rows, tile_expert, tile_count, counts=None, tile: int = MOE_TILE):
     T, k = ids.shape
-    kernels().moe_align(_p(ids), T, k, E, MOE_TILE, _p(sorted_rows), _p(tile_expert), _p(tile_count), _p(counts),
+    kernels().moe_align(_p(ids), T, k, E, tile, _p(sorted_rows), _p(tile_expert), _p(tile_count), _p(counts),
                         _s(ids))
 
 
-def moe_gemm(A, W_experts, sorted_rows, tile_expert, tile_count, out, N, K, max_tiles, a_row_div, epi=EPI_BF16):
-    kernels().moe_gemm(_p(A), A.stride(0), _p(W_experts), _p(sorted_rows), _p(tile_expert), _p(tile_count), _p(out),
-                       out.stride(0), N, K, max_tiles, a_row_div, epi, _s(A))
+def moe_gemm(A, W_experts, sorted_rows, tile_expert, tile_count, out, N, K, max_tiles, a_row_div, epi=EPI_BF16,
+             tile: int = MOE_TILE):
+    """Grouped expert GEMM (K11) over moe_align's list (same ``tile``): out[sorted_rows[i]] =
+    epi(A[sorted_rows[i] // a_row_div] . W[tile_expert[i // tile]]^T); EPI_SILU writes silu(gate) *
+    up of the interleaved gate/up columns ([., N / 2])."""
+    kernels().moe_gemm(_p(A), A.stride(0), A.shape[0], _p(W_experts), _p(sorted_rows), _p(tile_expert),
+                       _p(tile_count), _p(out), out.stride(0), N, K, max_tiles, a_row_div, epi, tile, _s(A))
     return out
 
 

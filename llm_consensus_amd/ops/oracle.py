@@ -238,3 +238,77 @@ def moe_ep_localize(ids: torch.Tensor, w: torch.Tensor, e0: int, n_local: int):
 
 def softmax_scale(D: int) -> float:
     return 1.0 / math.sqrt(D)
+
+
+# -- whole-model reference forward (tests) ------------------------------------------------------
+@torch.no_grad()
+def reference_logits(w, cfg, ids, out_pos, cos_t: torch.Tensor, sin_t: torch.Tensor, chunk: int = 1024,
+                     attn_chunk: int = 512) -> torch.Tensor:
+    """fp32 PyTorch forward of a ``TransformerWeights`` model (one TP=1 model or one rank's shard
+    standing alone) over the token sequence ``ids``: the last-layer logits [len(out_pos), V_local]
+    f32 at positions ``out_pos``. Every matmul, norm, RoPE, softmax and SiLU is fp32; activations
+    are rounded to bf16 exactly where the engine stores them (normed rows, q/k/v, attention
+    output, residual stream, SiLU product, expert outputs), so it is the engine's semantics at
+    full precision — the oracle of the full-depth teacher-forced decode tests. Runs on the
+    weights' device (the GPU for full-size models: fp32 copies are made one weight at a time),
+    in ``chunk``-token slices for the projections and ``attn_chunk``-query slices for causal
+    attention over the whole sequence."""
+    dev = w.embed.device
+    bf, f32 = torch.bfloat16, torch.float32
+    T = len(ids)
+    nh, nkv, D = w.nh, w.nkv, cfg.head_dim
+    G, half = nh // nkv, D // 2
+    idx = torch.as_tensor(ids, dtype=torch.long, device=dev)
+    pos = torch.arange(T, device=dev)
+    cos, sin = cos_t.to(dev)[pos].unsqueeze(1), sin_t.to(dev)[pos].unsqueeze(1)  # [T, 1, half]
+    h = w.embed[idx.clamp(0, w.embed.shape[0] - 1)].clone()
+    scale = 1.0 / math.sqrt(D)
+
+    def lin(x, W):  # fp32 x @ W^T in token slices -> fp32
+        Wf = W.float()
+        return torch.cat([x[i:i + chunk].float() @ Wf.t() for i in range(0, x.shape[0], chunk)])
+
+    for L in w.layers:
+        xn = rmsnorm(h, L.ln1, cfg.rms_eps)
+        qkv = lin(xn, L.w_qkv).to(bf)
+        qk = qkv[:, : (nh + nkv) * D].view(T, nh + nkv, half, 2).float()
+        x1, x2 = qk[..., 0], qk[..., 1]
+        rot = torch.cat([x1 * cos - x2 * sin, x2 * cos + x1 * sin], dim=-1).to(bf)  # [T, nh + nkv, D]
+        q, k = rot[:, :nh].float(), rot[:, nh:].float()
+        v = qkv[:, (nh + nkv) * D:(nh + 2 * nkv) * D].view(T, nkv, D).float()
+        attn = torch.empty(T, nh * D, dtype=bf, device=dev)
+        for q0 in range(0, T, attn_chunk):
+            q1 = min(T, q0 + attn_chunk)
+            qc = q[q0:q1].view(q1 - q0, nkv, G, D)                        # [q, kv, G, D]
+            s = torch.einsum("qkgd,tkd->kgqt", qc, k[:q1]) * scale         # keys 0..q1-1
+            mask = torch.arange(q1, device=dev).view(1, -1) > torch.arange(q0, q1, device=dev).view(-1, 1)
+            s.masked_fill_(mask, float("-inf"))
+            p = torch.softmax(s, dim=-1)
+            o = torch.einsum("kgqt,tkd->qkgd", p, v[:q1])
+            attn[q0:q1] = o.reshape(q1 - q0, nh * D).to(bf)
+            del s, p, o
+        h = (h.float() + lin(attn, L.w_o)).to(bf)
+        xn = rmsnorm(h, L.ln2, cfg.rms_eps)
+        if cfg.is_moe:
+            rw, rid = moe_route(lin(xn, L.w_router), cfg.top_k_experts)
+            k_ = cfg.top_k_experts
+            y = torch.zeros(T * k_, cfg.hidden, dtype=bf, device=dev)
+            flat = rid.view(-1).long()
+            for e in range(L.w_gu.shape[0]):
+                sel = (flat == e).nonzero().view(-1)
+                if sel.numel() == 0:
+                    continue
+                xe = xn[sel // k_]
+                gu = lin(xe, L.w_gu[e])
+                act = (torch.nn.functional.silu(gu[:, 0::2]) * gu[:, 1::2]).to(bf)
+                y[sel] = lin(act, L.w_down[e]).to(bf)
+            s = (rw.float().unsqueeze(-1) * y.view(T, k_, -1).float()).sum(1)
+            h = (h.float() + s).to(bf)
+        else:
+            gu = lin(xn, L.w_gu)
+            act = (torch.nn.functional.silu(gu[:, 0::2]) * gu[:, 1::2]).to(bf)
+            del gu
+            h = (h.float() + lin(act, L.w_down)).to(bf)
+    sel = torch.as_tensor(out_pos, dtype=torch.long, device=dev)
+    hn = rmsnorm(h[sel], w.final_norm, cfg.rms_eps)
+    return hn.float() @ w.lm_head.float().t()

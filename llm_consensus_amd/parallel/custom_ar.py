@@ -215,24 +215,6 @@ class CustomAllReduce:
             kernels().car_reset(self.own)
         dist.barrier(group=self.group)
 
-    # -- EPI_AR: row-parallel GEMV with the all-reduce in its epilogue -----------------------------
-    # Multi-GPU only and unmeasured there: on ranks sharing one GPU it measured slower than GEMV +
-    # the one-shot kernel, so the engine does not use it; kept with its exactness tests
-    # (tests/test_custom_ar_gpu.py) for a multi-GPU evaluation.
-    def rowpar_timed_out(self) -> bool:
-        """Timeout word of a buffer used by gemv_rowpar_ar (its own signal layout)."""
-        k = kernels()
-        return bool(k.car_timed_out(self.own + k.gemv_ar_timeout_off() - k.car_timeout_off()))
-
-    def gemv_rowpar_ar(self, x: torch.Tensor, W: torch.Tensor, h: torch.Tensor) -> torch.Tensor:
-        """Row-parallel decode projection with the all-reduce in the GEMV epilogue (EPI_AR):
-        h = sum over ranks of x_r @ W_r^T, rank 0 folding the residual already in h. This
-        object's buffer must be dedicated to it (block epochs of its own, cap >= 128 KiB)."""
-        M, K = x.shape
-        kernels().gemv_rowpar_ar(M, x.data_ptr(), x.stride(0), W.data_ptr(), h.data_ptr(), h.stride(0), W.shape[0], K,
-                                 self.bases, self.rank, self.world, self.cap, self._stream(x))
-        return h
-
     def close(self) -> None:
         if not self.own and not self._opened:
             return

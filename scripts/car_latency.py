@@ -4,12 +4,6 @@ captures 200 all-reduces of a [1, 4096] bf16 hidden row in a HIP graph and times
 A lower bound for the per-all-reduce cost of a TP decode step (64 per token for Llama-3-8B).
 
   python scripts/car_latency.py --world 2,4
-  python scripts/car_latency.py --world 2 --fused 2048x7168   # row-parallel GEMV + AR: separate vs EPI_AR
-
-With ``--fused NxK`` each rank instead times a row-parallel decode projection (x[1, K] @ W[N, K]^T
-into the residual row) both ways: the GEMV kernel followed by the custom all-reduce, and the one
-GEMV kernel with the all-reduce in its epilogue (LLMC_FUSED_AR's path). Keep N <= 2048 here: every
-block of every rank sharing the GPU must be resident at once.
 """
 import argparse
 import os
@@ -19,66 +13,6 @@ import time
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import torch  # noqa: E402
 import torch.multiprocessing as mp  # noqa: E402
-
-
-def _time_graph(fn, reps, s):
-    import torch.distributed as dist
-
-    with torch.cuda.stream(s):
-        for _ in range(4):
-            fn()
-    torch.cuda.synchronize()
-    dist.barrier()
-    g = torch.cuda.CUDAGraph()
-    with torch.cuda.graph(g, stream=s):
-        for _ in range(reps):
-            fn()
-    dist.barrier()
-    times = []
-    for _ in range(5):
-        torch.cuda.synchronize()
-        dist.barrier()
-        t = time.perf_counter()
-        g.replay()
-        torch.cuda.synchronize()
-        times.append(time.perf_counter() - t)
-    return min(times) / reps * 1e6
-
-
-def _fused_worker(rank, world, port, nk, reps, q):
-    import torch.distributed as dist
-
-    from llm_consensus_amd import ops
-    from llm_consensus_amd.ops import EPI_BF16, EPI_RESADD
-    from llm_consensus_amd.parallel.comm import TPGroup
-    from llm_consensus_amd.parallel.custom_ar import CustomAllReduce
-
-    N, K = nk
-    torch.cuda.set_device(0)
-    dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world)
-    tp = TPGroup(dist.group.WORLD, rank, world)
-    tp.enable_custom("cuda:0", cap=1 << 20)
-    rp = CustomAllReduce(tp.group, rank, world, "cuda:0", 128 * 1024, selftest=False)
-    g = torch.Generator(device="cpu").manual_seed(rank)
-    x = (torch.randn(1, K, generator=g) * 0.5).to("cuda", torch.bfloat16)
-    W = (torch.randn(N, K, generator=g) * 0.02).to("cuda", torch.bfloat16)
-    h = torch.zeros(1, N, device="cuda", dtype=torch.bfloat16)
-    s = torch.cuda.Stream()
-
-    def separate():
-        ops.linear(x, W, EPI_RESADD if rank == 0 else EPI_BF16, out=h)
-        tp.all_reduce_(h)
-
-    def fused():
-        rp.gemv_rowpar_ar(x, W, h)
-
-    t_sep = _time_graph(separate, reps, s)
-    t_fus = _time_graph(fused, reps, s)
-    q.put((rank, t_sep, t_fus, tp.custom.timed_out() or rp.rowpar_timed_out()))
-    dist.barrier()
-    rp.close()
-    tp.custom.close()
-    dist.destroy_process_group()
 
 
 def _worker(rank, world, port, n, reps, q):
@@ -121,23 +55,8 @@ def main():
     ap.add_argument("--world", default="2,4")
     ap.add_argument("--elems", type=int, default=4096)
     ap.add_argument("--reps", type=int, default=200)
-    ap.add_argument("--fused", default="", help="NxK: time a row-parallel GEMV + all-reduce, separate vs fused")
     a = ap.parse_args()
     ctx = mp.get_context("spawn")
-    if a.fused:
-        nk = tuple(int(v) for v in a.fused.lower().split("x"))
-        for w in [int(x) for x in a.world.split(",")]:
-            q = ctx.Queue()
-            ps = [ctx.Process(target=_fused_worker, args=(r, w, 29750 + w, nk, a.reps, q)) for r in range(w)]
-            for p in ps:
-                p.start()
-            res = [q.get(timeout=300) for _ in ps]
-            for p in ps:
-                p.join(timeout=60)
-            print(f"row-parallel GEMV {nk[0]}x{nk[1]} per rank + all-reduce, {w} ranks on one GPU: separate "
-                  f"{max(r[1] for r in res):.2f} us, fused epilogue {max(r[2] for r in res):.2f} us per projection "
-                  f"(graph-replayed, max over ranks; timed out: {any(r[3] for r in res)})", flush=True)
-        return
     for w in [int(x) for x in a.world.split(",")]:
         q = ctx.Queue()
         port = 29700 + w

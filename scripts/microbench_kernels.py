@@ -296,6 +296,34 @@ def bench_prefill():
         print(f"attn_prefill T={T} ctx={ctx}: {us:8.1f} us {fl / us / 1e6:6.0f} TF/s", flush=True)
 
 
+def bench_moe(tokens=(2048, 8192, 16384)):
+    """Mixtral-8x7B grouped expert GEMMs (top-2 of 8, hidden 4096, FFN 14336), routed by random
+    router logits: gate_up (SiLU-mul epilogue) and down over moe_align's list; TF/s on the routed
+    pairs' FLOPs (padding rows excluded)."""
+    E, k, H, I = 8, 2, 4096, 14336
+    wgu = ((torch.rand(E, 2 * I, H, device="cuda") * 2 - 1) * 0.05).to(BF)
+    wd = ((torch.rand(E, H, I, device="cuda") * 2 - 1) * 0.05).to(BF)
+    for T in tokens:
+        x = (torch.rand(T, H, device="cuda") * 2 - 1).to(BF)
+        w = torch.empty(T, k, device="cuda")
+        ids = torch.empty(T, k, dtype=torch.int32, device="cuda")
+        ops.moe_route(torch.randn(T, E, device="cuda"), k, w, ids)
+        tile = ops.moe_tile(T * k, E)
+        mt = ops.moe_max_tiles(T * k, E, tile)
+        sr = torch.empty(mt * tile, dtype=torch.int32, device="cuda")
+        te = torch.empty(mt, dtype=torch.int32, device="cuda")
+        tc = torch.empty(1, dtype=torch.int32, device="cuda")
+        ops.moe_align(ids, E, sr, te, tc, tile=tile)
+        act = torch.empty(T * k, I, dtype=BF, device="cuda")
+        y = torch.empty(T * k, H, dtype=BF, device="cuda")
+        t_gu = timeit(lambda: ops.moe_gemm(x, wgu, sr, te, tc, act, 2 * I, H, mt, k, epi=ops.EPI_SILU, tile=tile),
+                      iters=10)
+        t_dn = timeit(lambda: ops.moe_gemm(act, wd, sr, te, tc, y, H, I, mt, 1, tile=tile), iters=10)
+        f_gu, f_dn = 2 * T * k * 2 * I * H, 2 * T * k * H * I
+        print(f"moe T={T} tile={tile}: gate_up+silu {t_gu:8.1f} us {f_gu / t_gu / 1e6:6.0f} TF/s | down {t_dn:8.1f} us "
+              f"{f_dn / t_dn / 1e6:6.0f} TF/s", flush=True)
+
+
 def bench_attn_rows_policy(rows=(1, 2, 4, 8, 16, 32), lens=(700, 2560, 8192, 13500)):
     """Batching engines' decode attention: the grid a batch-invariant policy can use. 'rowsN' = the
     balanced split at max(1, 256 / (N x nkv)) blocks per kv head for an engine sized for N rows
@@ -357,5 +385,7 @@ if __name__ == "__main__":
         bench_gemvm_forms(rows=(24, 32))
     if what in ("qkv-rope",):
         bench_qkv_rope()
+    if what in ("moe",):  # Mixtral grouped expert GEMMs
+        bench_moe()
     if what in ("prefill",):
         bench_prefill()

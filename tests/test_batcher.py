@@ -160,4 +160,5 @@ def test_attention_fault_fails_batched_rows(cuda):
         if gone:
             break
     assert gone == [row] and row.error is not None and "merge timed out" in str(row.error)
+    torch.cuda.synchronize()  # the re-arm is queued on the engine's stream
     assert int(eng.attn_fault.item()) == 0

@@ -103,102 +103,6 @@ def test_custom_allreduce_ipc(cuda, world):
         assert gather_ok, rank
 
 
-def _rowpar_worker(rank, world, port, q):
-    """EPI_AR: the row-parallel GEMV with its all-reduce in the epilogue must give exactly the bits
-    of GEMV (rank 0 residual-folded) + separate custom all-reduce, eagerly and from a HIP graph
-    (1-2 rows; 3-4 rows within bf16 tolerance: the separate path's projection is the MFMA form)."""
-    try:
-        import torch.distributed as dist
-
-        from llm_consensus_amd import ops
-        from llm_consensus_amd.parallel.comm import TPGroup
-        from llm_consensus_amd.parallel.custom_ar import CustomAllReduce
-
-        torch.cuda.set_device(0)
-        dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world)
-        tp = TPGroup(dist.group.WORLD, rank, world)
-        tp.enable_custom("cuda:0", cap=1 << 20)
-        rp = CustomAllReduce(dist.group.WORLD, rank, world, "cuda:0", 128 * 1024, selftest=False)
-        errs = []
-        # per-rank grids stay small (<= 64 blocks): the ranks share this one GPU and every block of every
-        # rank must be resident at once (on a node each rank has a GPU of its own)
-        for M, N, K in [(1, 1024, 512), (2, 1024, 1792), (4, 1000, 256), (3, 1024, 1024)]:
-            for rep in range(3):
-                g = torch.Generator().manual_seed(7 * rank + rep + M * 1000 + K)
-                x = torch.randn(M, K, generator=g).to(torch.bfloat16).cuda()
-                W = (torch.randn(N, K, generator=g) * 0.05).to(torch.bfloat16).cuda()
-                g0 = torch.Generator().manual_seed(99 + rep + M)
-                h0 = torch.randn(M, N, generator=g0).to(torch.bfloat16).cuda()  # same residual on all ranks
-                ref = h0.clone()
-                ops.linear(x, W, ops.EPI_RESADD if rank == 0 else ops.EPI_BF16, out=ref)
-                tp.all_reduce_(ref)
-                got = h0.clone()
-                rp.gemv_rowpar_ar(x, W, got)
-                torch.cuda.synchronize()
-                if M <= 2:  # same VALU GEMV form on both sides: bit-exact
-                    errs.append(int((got != ref).sum()))
-                else:  # ops.linear takes the MFMA form from 3 rows on (EPI_AR stays on the VALU GEMV)
-                    d = (got.float() - ref.float()).abs()
-                    errs.append(int((d > 2e-2 + 2e-2 * ref.float().abs()).sum()))
-        # graph replay with changing inputs
-        M, N, K = 1, 1024, 512
-        x = torch.zeros(M, K, dtype=torch.bfloat16, device="cuda")
-        W = (torch.randn(N, K) * 0.05).to(torch.bfloat16).cuda()
-        h = torch.zeros(M, N, dtype=torch.bfloat16, device="cuda")
-        s = torch.cuda.Stream()
-        with torch.cuda.stream(s):
-            rp.gemv_rowpar_ar(x, W, h)
-        torch.cuda.synchronize()
-        dist.barrier()
-        gr = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(gr, stream=s):
-            rp.gemv_rowpar_ar(x, W, h)
-            rp.gemv_rowpar_ar(x, W, h)
-        dist.barrier()
-        for rep in range(3):
-            x.copy_(torch.randn(M, K, generator=torch.Generator().manual_seed(rank * 31 + rep)).to(torch.bfloat16))
-            h.copy_(torch.randn(M, N, generator=torch.Generator().manual_seed(500 + rep)).to(torch.bfloat16))
-            ref = h.clone()
-            for _ in range(2):
-                ops.linear(x, W, ops.EPI_RESADD if rank == 0 else ops.EPI_BF16, out=ref)
-                tp.all_reduce_(ref)
-            torch.cuda.synchronize()
-            dist.barrier()
-            gr.replay()
-            torch.cuda.synchronize()
-            errs.append(int((h != ref).sum()))
-        q.put((rank, max(errs) if max(errs) == 0 else str(errs), rp.rowpar_timed_out() or tp.custom.timed_out()))
-        dist.barrier()
-        rp.close()
-        tp.custom.close()
-        dist.destroy_process_group()
-    except Exception as e:  # noqa: BLE001
-        import traceback
-
-        q.put((rank, repr(e) + traceback.format_exc(), True))
-
-
-@pytest.mark.parametrize("world", [2, 4])
-def test_rowpar_fused_allreduce(cuda, world):
-    import socket
-
-    with socket.socket() as sk:
-        sk.bind(("127.0.0.1", 0))
-        port = sk.getsockname()[1]
-    ctx = mp.get_context("spawn")
-    q = ctx.Queue()
-    procs = [ctx.Process(target=_rowpar_worker, args=(r, world, port, q)) for r in range(world)]
-    for p in procs:
-        p.start()
-    res = [q.get(timeout=240) for _ in range(world)]
-    for p in procs:
-        p.join(timeout=60)
-    for rank, bad, tmo in res:
-        assert not isinstance(bad, str), bad
-        assert bad == 0, f"rank {rank}: {bad} elements differ from GEMV + separate all-reduce"
-        assert not tmo, f"rank {rank}: a spin timed out"
-
-
 def _twoshot_worker(rank, world, port, q):
     """Two-shot all-reduce / reduce-scatter / all-gather (prefill-sized messages, run in pieces
     when larger than the buffer) against f32 sums of every rank's input."""

@@ -486,7 +486,7 @@ def test_sample_topk_topp_and_advance(cuda):
     assert oc.cpu().tolist() == [1, 1] and ot[:, 0].cpu().tolist() == n.tolist() and tin.cpu().tolist() == n.tolist()
 
 
-@pytest.mark.parametrize("T", [1, 3, 300])
+@pytest.mark.parametrize("T", [1, 3, 300, 1100])
 def test_moe(cuda, T):
     torch.manual_seed(7)
     E, k, H, I = 8, 2, 256, 384
@@ -509,18 +509,58 @@ def test_moe(cuda, T):
         y = torch.empty(T * k, H, dtype=BF, device="cuda")
         ops.moe_gemv(act, wd, ids, 1, y, H, I, ops.EPI_BF16)
     else:
-        mt = ops.moe_max_tiles(T * k, E)
-        sr = torch.empty(mt * 128, dtype=torch.int32, device="cuda")
+        tile = ops.moe_tile(T * k, E)
+        assert tile == (256 if T * k >= 256 * E else 128)
+        mt = ops.moe_max_tiles(T * k, E, tile)
+        sr = torch.empty(mt * tile, dtype=torch.int32, device="cuda")
         te = torch.empty(mt, dtype=torch.int32, device="cuda")
         tc = torch.empty(1, dtype=torch.int32, device="cuda")
-        ops.moe_align(ids, E, sr, te, tc)
-        gu = torch.empty(T * k, 2 * I, dtype=BF, device="cuda")
-        ops.moe_gemm(x, wgu, sr, te, tc, gu, 2 * I, H, mt, k)
-        act = ops.silu_mul_interleaved(gu)
+        ops.moe_align(ids, E, sr, te, tc, tile=tile)
+        act = torch.empty(T * k, I, dtype=BF, device="cuda")
+        ops.moe_gemm(x, wgu, sr, te, tc, act, 2 * I, H, mt, k, epi=ops.EPI_SILU, tile=tile)
         y = torch.empty(T * k, H, dtype=BF, device="cuda")
-        ops.moe_gemm(act, wd, sr, te, tc, y, H, I, mt, 1)
+        ops.moe_gemm(act, wd, sr, te, tc, y, H, I, mt, 1, tile=tile)
     ops.moe_combine(y, w, ids, h)
     close(h, href, 3e-2)
+
+
+@pytest.mark.parametrize("T,tile", [(700, 128), (1500, 256), (2600, 256)])
+def test_moe_grouped_gemm_ragged(cuda, T, tile):
+    """The grouped expert GEMM on ragged groups: the router is skewed so two experts take most
+    pairs (hundreds of rows each, several 256-row tiles, a partial last tile) and others a few;
+    gate_up (SiLU-mul in the epilogue) and down per pair vs an fp32 per-expert oracle."""
+    torch.manual_seed(11)
+    E, k, H, I = 8, 2, 512, 640
+    x = rnd(T, H)
+    wgu = rnd(E, 2 * I, H, scale=0.05)
+    wd = rnd(E, H, I, scale=0.05)
+    logits = torch.randn(T, E, device="cuda") + torch.tensor([3.0, 2.5, 0, 0, -1, -2, -3, -4], device="cuda")
+    w = torch.empty(T, k, device="cuda")
+    ids = torch.empty(T, k, dtype=torch.int32, device="cuda")
+    ops.moe_route(logits, k, w, ids)
+    counts = torch.bincount(ids.view(-1).long().cpu(), minlength=E)
+    assert counts.max() > 2 * 128 and counts.min() < 128, counts  # ragged: big groups and small ones
+    assert ops.moe_tile(T * k, E) == tile
+    mt = ops.moe_max_tiles(T * k, E, tile)
+    sr = torch.empty(mt * tile, dtype=torch.int32, device="cuda")
+    te = torch.empty(mt, dtype=torch.int32, device="cuda")
+    tc = torch.empty(1, dtype=torch.int32, device="cuda")
+    ops.moe_align(ids, E, sr, te, tc, tile=tile)
+    act = torch.full((T * k, I), float("nan"), dtype=BF, device="cuda")
+    ops.moe_gemm(x, wgu, sr, te, tc, act, 2 * I, H, mt, k, epi=ops.EPI_SILU, tile=tile)
+    y = torch.full((T * k, H), float("nan"), dtype=BF, device="cuda")
+    ops.moe_gemm(act, wd, sr, te, tc, y, H, I, mt, 1, tile=tile)
+    # fp32 oracle per expert group (every pair written: NaN poison would show a missed row)
+    xr, idc = x.float().repeat_interleave(k, 0), ids.view(-1).long()
+    aref = torch.empty(T * k, I, device="cuda")
+    yref = torch.empty(T * k, H, device="cuda")
+    for e in range(E):
+        sel = (idc == e).nonzero().view(-1)
+        g = xr[sel] @ wgu[e].float().t()
+        aref[sel] = torch.nn.functional.silu(g[:, 0::2]) * g[:, 1::2]
+        yref[sel] = act[sel].float() @ wd[e].float().t()
+    close(act, aref, 3e-2)
+    close(y, yref, 3e-2)
 
 
 @pytest.mark.parametrize("T,E,H", [(1, 8, 4096), (4, 8, 256), (2, 16, 1024), (3, 4, 192)])

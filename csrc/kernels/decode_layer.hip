@@ -1,0 +1,515 @@
+// Fused batch-1 decode layer: the five dependent steps of one transformer layer's decode token in
+// ONE launch, as a dataflow over dispatch-ordered tasks (host: llmc_decode_layer).
+//
+//   qkv   rows of [Wq|Wk|Wv] . rmsnorm(h)   RoPE epilogue: q -> scratch, k/v -> paged cache
+//   attn  split-KV decode attention over the cache (attn_core.h), last-arriver merge
+//   o     rows of Wo . attn                 residual epilogue: h += ...
+//   gu    rows of [Wg|Wu] . rmsnorm(h)      SiLU-mul epilogue: act
+//   down  rows of Wd . act                  residual epilogue: h += ...
+//
+// Why: as five launches, every step pays a kernel boundary plus its own ramp — the first weight
+// batch of the next GEMV is only requested once the previous kernel has drained (batch-1 decode of
+// Llama-3-8B: qkv 10.5 us for 50 MB, o 7.2 us for 34 MB, attention 10.6 us for 10 MB of K/V:
+// profiles/r2_dec2k_kernel_stats.md). Here a task of the next step is dispatched as soon as a slot
+// frees up, issues its weight loads (they do not depend on the activations), and only then waits
+// for the step it depends on (MI355X_MICROARCH.md price list rows prefetch-credit, phase-in-launch).
+//
+// Deadlock freedom without residency assumptions: every block takes its task index from a
+// dispatch counter (agent-scope atomic) when it starts, and tasks are numbered in dependency order
+// (all qkv tasks, then all attention tasks, ...). A task only ever waits for tasks with SMALLER
+// indices, which were taken by blocks that had already started — resident blocks that never wait
+// on anything later — so the wait always ends, however many blocks of this launch (or of engines
+// co-located on the GPU) fit on the chip. Every spin is bounded (fault word, never a hang).
+//
+// Hand-offs inside the launch (MI355X_MICROARCH.md § visibility, "Valid forms" table, row 1): every
+// byte a later step reads — q, the new token's k/v cache rows, the attention output, h, act — is
+// stored write-through (sc1, 4-16 B) and read with sc1 loads (L1 bypass); each storing wave drains
+// (`s_waitcnt vmcnt(0)`), the block meets at a barrier and ONE lane adds to the step's done counter;
+// a consumer block polls that counter from one lane (relaxed, sc1) and releases its waves at a
+// barrier. The counters are reset by the last down task, so every launch starts from zero.
+//
+// Scope: one decode row, no tensor parallelism, dense MLP (the engines of the bench's responders
+// and judge); the engine keeps the five-kernel path for everything else.
+#include "attn_core.h"
+
+namespace llmc {
+
+constexpr int kDlThreads = 512, kDlWaves = kDlThreads / kWave;
+constexpr int kDlRows = 2 * kDlWaves;  // GEMV output rows per task: 2 per wave
+constexpr int kDlUnroll = 4;           // 16-B weight chunks per row per lane per batch
+constexpr unsigned kDlSpinLimit = 1u << 22;
+enum { DL_DISPATCH = 0, DL_QKV = 1, DL_ATTN = 2, DL_O = 3, DL_GU = 4, DL_DOWN = 5, DL_WORDS = 8 };
+
+struct DecodeLayerArgs {
+  const bf16_t *ln1, *w_qkv, *w_o, *ln2, *w_gu, *w_down;
+  bf16_t *k_cache, *v_cache;  // this layer: [nblocks][nkv][bs][D]
+  const int32_t *positions, *slots, *seq_lens, *block_table;
+  const float *cos_t, *sin_t;
+  bf16_t *h, *q, *attn, *act;  // residual row [H]; scratch q / attention output [nh D]; act [I]
+  float* part;                 // attention partial granules (attn_decode workspace, row 0)
+  int* attn_ctr;               // its {ticket, epoch, group tickets} per kv head
+  uint32_t* sync;              // DL_WORDS counters, zero between launches
+  int* fault;                  // 1: attention merge gave up, 2: a step's wait gave up
+  uint64_t* stamps;            // diagnostics (nullptr = off): 5 s_memrealtime stamps per task
+  int bt_stride, H, nh, nkv, I, bs, nblocks, min_chunk, gc, max_chunks, max_groups;
+  float eps, scale_log2;
+  int n_qkv, n_attn, n_o, n_gu, n_down;
+};
+
+// Diagnostics: task timeline stamps (100 MHz real-time counter), thread 0 only.
+__device__ __forceinline__ void dl_stamp(uint64_t* st, int k) {
+  if (st != nullptr && threadIdx.x == 0) st[k] = __builtin_amdgcn_s_memrealtime();
+}
+
+// Write-through (sc1) 16-B accesses of one buffer through a buffer descriptor.
+struct WtBuf {
+  __amdgpu_buffer_rsrc_t r;
+  const char* base;
+  __device__ __forceinline__ WtBuf(const void* p, uint32_t bytes)
+      : r(__builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), 0, bytes, 0x00020000)),
+        base(static_cast<const char*>(p)) {}
+  __device__ __forceinline__ u32x4 ld16(const void* p) const {
+    return __builtin_amdgcn_raw_buffer_load_b128(r, static_cast<int>(static_cast<const char*>(p) - base), 0, 16);
+  }
+  __device__ __forceinline__ void st16(void* p, u32x4 v) const {
+    __builtin_amdgcn_raw_buffer_store_b128(v, r, static_cast<int>(static_cast<const char*>(p) - base), 0, 16);
+  }
+  __device__ __forceinline__ u32x4 operator()(const bf16_t* p) const { return ld16(p); }
+};
+
+// One lane polls `ctr` (relaxed agent-scope = sc1 load) until it reaches `target`; the block meets
+// at the barrier behind it. ctr == nullptr: barrier only.
+__device__ __forceinline__ void dl_wait(uint32_t* ctr, uint32_t target, int* fault) {
+  if (ctr != nullptr && threadIdx.x == 0) {
+    for (unsigned spins = 0; __hip_atomic_load(ctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target; ++spins) {
+      if (spins >= kDlSpinLimit) {
+        __hip_atomic_store(fault, 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        break;
+      }
+      __builtin_amdgcn_s_sleep(1);
+    }
+  }
+  __syncthreads();
+}
+
+// Every wave's write-through stores have landed; one lane counts the task done. Returns the
+// counter's previous value on thread 0. Block-uniform call.
+__device__ __forceinline__ uint32_t dl_signal(uint32_t* ctr) {
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  uint32_t old = 0;
+  if (threadIdx.x == 0) old = __hip_atomic_fetch_add(ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  return old;
+}
+
+// Rows [r0, r0 + 16) of W[N, K] (2 per wave) against x = NORM ? bf16(rmsnorm(src) * norm_w) : src,
+// src written in this launch (K bf16). The first weight batch is requested BEFORE the wait on
+// `dep`. On return every lane of wave w holds rows r0 + 2w, r0 + 2w + 1 in y[0], y[1].
+template <bool NORM>
+__device__ __forceinline__ void dl_gemv(const bf16_t* __restrict__ W, int N, int K, int r0, const WtBuf& xb,
+                                        const bf16_t* src, const bf16_t* __restrict__ norm_w, float eps, uint32_t* dep,
+                                        uint32_t target, int* fault, char* smem, float (&y)[2], uint64_t* stp) {
+  const int tid = threadIdx.x, wave = tid / kWave, lane = tid % kWave;
+  const int nchunk = K / 8;
+  const u32x4* w0 = reinterpret_cast<const u32x4*>(W + static_cast<int64_t>(min(r0 + 2 * wave, N - 1)) * K);
+  const u32x4* w1 = reinterpret_cast<const u32x4*>(W + static_cast<int64_t>(min(r0 + 2 * wave + 1, N - 1)) * K);
+  constexpr int U = kDlUnroll, STEP = kWave * U;
+  const int iters = (nchunk + STEP - 1) / STEP;
+  auto issue = [&](u32x4 (&d)[2][U], int cb) {
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int c = min(cb + u * kWave, nchunk - 1);
+      d[0][u] = load16<true>(w0 + c);
+      d[1][u] = load16<true>(w1 + c);
+    }
+  };
+  u32x4 cur[2][U];
+  issue(cur, lane);
+  dl_wait(dep, target, fault);
+  dl_stamp(stp, 2);
+
+  // x -> LDS (normalised if NORM)
+  bf16_t* xs = reinterpret_cast<bf16_t*>(smem);
+  float* red = reinterpret_cast<float*>(smem + static_cast<size_t>(K) * 2);
+  if constexpr (NORM) {
+    float ss = 0.f;
+    for (int c = tid; c < nchunk; c += kDlThreads) {
+      const u32x4 v = xb.ld16(src + 8 * c);
+      float f[8];
+      unpack8(v, f);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) ss += f[e] * f[e];
+      reinterpret_cast<u32x4*>(xs)[c] = v;
+    }
+    ss = wave_sum(ss);
+    if (lane == 0) red[wave] = ss;
+    __syncthreads();
+    float t = 0.f;
+#pragma unroll
+    for (int w = 0; w < kDlWaves; ++w) t += red[w];
+    const float inv = rsqrtf(t / K + eps);
+    for (int c = tid; c < nchunk; c += kDlThreads) {
+      float f[8], g[8];
+      unpack8(reinterpret_cast<const u32x4*>(xs)[c], f);
+      unpack8(reinterpret_cast<const u32x4*>(norm_w)[c], g);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) f[e] = f[e] * inv * g[e];
+      reinterpret_cast<u32x4*>(xs)[c] = pack8(f);
+    }
+  } else {
+    for (int c = tid; c < nchunk; c += kDlThreads) reinterpret_cast<u32x4*>(xs)[c] = xb.ld16(src + 8 * c);
+  }
+  __syncthreads();
+
+  const u32x4* xv = reinterpret_cast<const u32x4*>(xs);
+  float a0 = 0.f, a1 = 0.f;
+  int c0 = lane;
+  for (int it = 0; it + 1 < iters; ++it, c0 += STEP) {
+    u32x4 nxt[2][U];
+    issue(nxt, c0 + STEP);
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const u32x4 xx = xv[c0 + u * kWave];
+      a0 = dot8_bf16(cur[0][u], xx, a0);
+      a1 = dot8_bf16(cur[1][u], xx, a1);
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      cur[0][u] = nxt[0][u];
+      cur[1][u] = nxt[1][u];
+    }
+  }
+#pragma unroll
+  for (int u = 0; u < U; ++u) {
+    const int c = c0 + u * kWave;
+    if (c < nchunk) {
+      const u32x4 xx = xv[c];
+      a0 = dot8_bf16(cur[0][u], xx, a0);
+      a1 = dot8_bf16(cur[1][u], xx, a1);
+    }
+  }
+  y[0] = wave_sum(a0);
+  y[1] = wave_sum(a1);
+}
+
+// Stage the 16 task outputs (2 per wave) in LDS: out16[2 * wave + j] = v[j] (after the GEMV, the
+// x image is dead: the staging area sits behind it). Block-uniform.
+__device__ __forceinline__ float* dl_stage(char* smem, int K, float v0, float v1) {
+  float* st = reinterpret_cast<float*>(smem + static_cast<size_t>(K) * 2) + kDlWaves;
+  const int wave = threadIdx.x / kWave, lane = threadIdx.x % kWave;
+  if (lane == 0) {
+    st[2 * wave] = v0;
+    st[2 * wave + 1] = v1;
+  }
+  __syncthreads();
+  return st;
+}
+
+// h[r0 .. r0 + 16) += out16 (bf16 residual stream, write-through read-modify-write by thread 0/1)
+__device__ __forceinline__ void dl_resadd(bf16_t* h, const WtBuf& hb, int r0, const float* st) {
+  const int tid = threadIdx.x;
+  if (tid < 2) {
+    bf16_t* p = h + r0 + 8 * tid;
+    float f[8];
+    unpack8(hb.ld16(p), f);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) f[e] += st[8 * tid + e];
+    hb.st16(p, pack8(f));
+  }
+}
+
+template <int G, int D>
+__device__ __forceinline__ void dl_qkv(const DecodeLayerArgs& a, int t, char* smem, uint64_t* stp) {
+  const int N = (a.nh + 2 * a.nkv) * D;
+  const int r0 = t * kDlRows;
+  const WtBuf hb(a.h, a.H * 2);
+  float y[2];
+  dl_gemv<true>(a.w_qkv, N, a.H, r0, hb, a.h, a.ln1, a.eps, nullptr, 0, a.fault, smem, y, stp);
+  // RoPE of the wave's (2i, 2i + 1) pair = dims (i, i + D/2) of a Q/K head; V rows stay in order
+  const int wave = threadIdx.x / kWave;
+  const int head = r0 / D;  // a task never straddles heads (D % 16 == 0)
+  constexpr int half = D / 2;
+  float o0 = y[0], o1 = y[1];
+  if (head < a.nh + a.nkv) {
+    const int i = (r0 % D) / 2 + wave;
+    const int pos = a.positions[0];
+    const float c = a.cos_t[static_cast<int64_t>(pos) * half + i], sn = a.sin_t[static_cast<int64_t>(pos) * half + i];
+    o0 = y[0] * c - y[1] * sn;
+    o1 = y[1] * c + y[0] * sn;
+  }
+  const float* st = dl_stage(smem, a.H, o0, o1);
+  const int tid = threadIdx.x;
+  if (tid < 2) {
+    float f[8];
+    bf16_t* dst = nullptr;
+    const int slot = a.slots[0];
+    const int64_t page = slot / a.bs, off = slot % a.bs;
+    if (head < a.nh + a.nkv) {  // piece tid: dims i0 .. i0 + 8 (first of each pair) or + D/2 (second)
+      const int i0 = (r0 % D) / 2 + tid * half;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) f[e] = st[2 * e + tid];
+      if (head < a.nh) {
+        dst = a.q + head * D + i0;
+        WtBuf(a.q, a.nh * D * 2).st16(dst, pack8(f));
+      } else if (slot >= 0) {
+        dst = a.k_cache + ((page * a.nkv + (head - a.nh)) * a.bs + off) * D + i0;
+        WtBuf(a.k_cache, static_cast<uint32_t>(static_cast<int64_t>(a.nblocks) * a.nkv * a.bs * D * 2)).st16(dst, pack8(f));
+      }
+    } else if (slot >= 0) {  // V rows r0 .. r0 + 16 = dims d0 .. d0 + 16 in order
+      const int d0 = r0 % D + 8 * tid;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) f[e] = st[8 * tid + e];
+      dst = a.v_cache + ((page * a.nkv + (head - a.nh - a.nkv)) * a.bs + off) * D + d0;
+      WtBuf(a.v_cache, static_cast<uint32_t>(static_cast<int64_t>(a.nblocks) * a.nkv * a.bs * D * 2)).st16(dst, pack8(f));
+    }
+  }
+  dl_stamp(stp, 3);
+  dl_signal(a.sync + DL_QKV);
+  dl_stamp(stp, 4);
+}
+
+// Split-KV attention of kv head kvh, balanced key range c of the gc-block grid (attn_decode.hip's
+// split form with NW = 8 waves), every input read write-through: q and the new token's k/v were
+// written by this launch's qkv tasks.
+template <int G, int D>
+__device__ __forceinline__ void dl_attn(const DecodeLayerArgs& a, int t, char* smem, uint64_t* stp) {
+  using ST = SubTile<G, D>;
+  constexpr int NW = kDlWaves, NT = kDlThreads;
+  const int kvh = t / a.gc, c = t % a.gc;
+  const int tid = threadIdx.x, wave = tid / kWave, lane = tid % kWave;
+  int* ctr = a.attn_ctr + kvh * (2 + a.max_groups);
+  const uint32_t tag = static_cast<uint32_t>(__hip_atomic_load(ctr + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) + 1u;
+  const int L = a.seq_lens[0];
+  const int nchunks = decode_nsplit(L, a.gc, -a.min_chunk);
+  if (c >= nchunks) return;  // no wait, no signal: the head's merger counts the live chunks only
+  int start, end;
+  decode_range(L, nchunks, c, -a.min_chunk, start, end);
+  char* vbuf = smem + wave * 32 * kVRowBytes;
+  int* pages = reinterpret_cast<int*>(smem + NW * 32 * kVRowBytes);
+  const int p0 = start / a.bs;
+  const int npages = (end - 1) / a.bs - p0 + 1;
+  for (int i = tid; i < npages; i += NT)
+    pages[i] = min(max(a.block_table[min(p0 + i, a.bt_stride - 1)], 0), a.nblocks - 1);
+  const uint32_t cache_bytes = static_cast<uint32_t>(static_cast<int64_t>(a.nblocks) * a.nkv * a.bs * D * 2);
+  const WtBuf kb(a.k_cache, cache_bytes), vb(a.v_cache, cache_bytes), qb(a.q, a.nh * D * 2);
+  dl_wait(a.sync + DL_QKV, a.n_qkv, a.fault);
+  dl_stamp(stp, 2);
+  ST st;
+  st.init(a.q + kvh * G * D, lane, qb);
+  const int64_t head_stride = static_cast<int64_t>(a.bs) * D;
+  auto row = [&](const bf16_t* cache, int key) {
+    const int64_t page = pages[key / a.bs - p0];
+    return cache + (page * a.nkv + kvh) * head_stride + static_cast<int64_t>(key % a.bs) * D;
+  };
+  const int per_wave = (((end - start + NW - 1) / NW) + 31) & ~31;
+  const int wbase = start + wave * per_wave;
+  // one sub-tile in flight per wave (a block's range is 256-1024 keys: 1-4 sub-tiles per wave),
+  // which keeps the fused kernel at 4 waves per SIMD
+  bf16x8 kf[2][ST::KS];
+  u32x4 vs[ST::NV];
+  for (int k0 = wbase; k0 - wbase < per_wave && k0 < end; k0 += 32) {
+    st.issue(k0, end, lane, row, a.k_cache, a.v_cache, kf, vs, kb, vb);
+    st.compute(k0, end, lane, vbuf, a.scale_log2, kf, vs);
+  }
+  __syncthreads();  // every wave is done with its V image: the wave states go where it was
+  float* red = reinterpret_cast<float*>(smem);
+  st.to_lds(red, wave, lane);
+  __syncthreads();
+  bf16_t* out_row = a.attn + kvh * G * D;
+  if (nchunks == 1) {
+    store_direct_sc1<G, D, NW>(red, out_row, tid);
+    dl_stamp(stp, 3);
+    dl_signal(a.sync + DL_ATTN);
+    dl_stamp(stp, 4);
+    return;
+  }
+  const bool wrote = publish_and_merge<G, D, NW, true>(red, a.part, ctr, 0, a.nkv, kvh, c, nchunks, a.gc, a.max_chunks,
+                                                       a.max_groups, tag, out_row, smem, pages, tid, a.fault);
+  dl_stamp(stp, 3);
+  if (wrote) dl_signal(a.sync + DL_ATTN);
+  dl_stamp(stp, 4);
+}
+
+template <int G, int D>
+__device__ __forceinline__ void dl_o(const DecodeLayerArgs& a, int t, char* smem, uint64_t* stp) {
+  const int r0 = t * kDlRows, K = a.nh * D;
+  float y[2];
+  dl_gemv<false>(a.w_o, a.H, K, r0, WtBuf(a.attn, K * 2), a.attn, nullptr, 0.f, a.sync + DL_ATTN, a.nkv, a.fault,
+                 smem, y, stp);
+  const float* st = dl_stage(smem, K, y[0], y[1]);
+  dl_resadd(a.h, WtBuf(a.h, a.H * 2), r0, st);
+  dl_stamp(stp, 3);
+  dl_signal(a.sync + DL_O);
+  dl_stamp(stp, 4);
+}
+
+__device__ __forceinline__ void dl_gu(const DecodeLayerArgs& a, int t, char* smem, uint64_t* stp) {
+  const int r0 = t * kDlRows;
+  float y[2];
+  dl_gemv<true>(a.w_gu, 2 * a.I, a.H, r0, WtBuf(a.h, a.H * 2), a.h, a.ln2, a.eps, a.sync + DL_O, a.n_o, a.fault,
+                smem, y, stp);
+  // rows (2i, 2i + 1) = (gate_i, up_i): wave w holds output column r0 / 2 + w
+  const float* st = dl_stage(smem, a.H, silu(y[0]) * y[1], 0.f);
+  if (threadIdx.x == 0) {
+    float f[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) f[e] = st[2 * e];
+    WtBuf(a.act, a.I * 2).st16(a.act + r0 / 2, pack8(f));
+  }
+  dl_stamp(stp, 3);
+  dl_signal(a.sync + DL_GU);
+  dl_stamp(stp, 4);
+}
+
+__device__ __forceinline__ void dl_down(const DecodeLayerArgs& a, int t, char* smem, uint64_t* stp) {
+  const int r0 = t * kDlRows;
+  float y[2];
+  dl_gemv<false>(a.w_down, a.H, a.I, r0, WtBuf(a.act, a.I * 2), a.act, nullptr, 0.f, a.sync + DL_GU, a.n_gu, a.fault,
+                 smem, y, stp);
+  const float* st = dl_stage(smem, a.I, y[0], y[1]);
+  dl_resadd(a.h, WtBuf(a.h, a.H * 2), r0, st);
+  dl_stamp(stp, 3);
+  const uint32_t old = dl_signal(a.sync + DL_DOWN);
+  dl_stamp(stp, 4);
+  if (threadIdx.x == 0 && old == static_cast<uint32_t>(a.n_down - 1)) {
+    // the last task of the launch: every block has taken its index and every wait is over
+#pragma unroll
+    for (int w = 0; w < DL_WORDS; ++w) __hip_atomic_store(a.sync + w, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+}
+
+template <int G, int D>
+__global__ __launch_bounds__(kDlThreads, 4) void decode_layer_kernel(DecodeLayerArgs a) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  __shared__ uint32_t s_task;
+  const uint64_t t0 = a.stamps != nullptr ? __builtin_amdgcn_s_memrealtime() : 0;
+  if (threadIdx.x == 0)
+    s_task = __hip_atomic_fetch_add(a.sync + DL_DISPATCH, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  __syncthreads();
+  int t = static_cast<int>(s_task);
+  uint64_t* stp = a.stamps != nullptr ? a.stamps + static_cast<int64_t>(t) * 8 : nullptr;
+  dl_stamp(stp, 0);
+  if (stp != nullptr && threadIdx.x == 0) {
+    stp[5] = t0;
+    stp[6] = blockIdx.x;
+    uint32_t xcc;
+    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
+    stp[7] = xcc;
+  }
+  if (t < a.n_qkv) return dl_qkv<G, D>(a, t, smem, stp);
+  t -= a.n_qkv;
+  if (t < a.n_attn) return dl_attn<G, D>(a, t, smem, stp);
+  t -= a.n_attn;
+  if (t < a.n_o) return dl_o<G, D>(a, t, smem, stp);
+  t -= a.n_o;
+  if (t < a.n_gu) return dl_gu(a, t, smem, stp);
+  t -= a.n_gu;
+  if (t < a.n_down) return dl_down(a, t, smem, stp);
+}
+
+template <int G, int D>
+static int launch_dl(const DecodeLayerArgs& a, size_t lds, hipStream_t s) {
+  auto kern = decode_layer_kernel<G, D>;
+  // two 512-thread blocks per CU (__launch_bounds__ min 4 waves per SIMD) leave 80 KiB of LDS each
+  static size_t attr_lds = 0;
+  if (lds > 64 * 1024 && lds > attr_lds) {
+    const hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(kern),
+                                             hipFuncAttributeMaxDynamicSharedMemorySize, 80 * 1024);
+    if (e != hipSuccess) return static_cast<int>(e);
+    attr_lds = 80 * 1024;
+  }
+  if (lds > 80 * 1024) return -4;
+  const int grid = a.n_qkv + a.n_attn + a.n_o + a.n_gu + a.n_down;
+  kern<<<grid, kDlThreads, lds, s>>>(a);
+  return static_cast<int>(hipGetLastError());
+}
+
+}  // namespace llmc
+
+using namespace llmc;
+
+extern "C" int llmc_attn_decode_groups(int max_chunks);
+
+// One decode layer for ONE row (see the header). gc <= 32 balanced attention blocks per kv head of
+// >= min_chunk keys (a multiple of 32); max_chunks / part / attn_ctr: the attn_decode workspace
+// (max_chunks >= gc). sync: DL_WORDS uint32 counters, zeroed once (each launch leaves them zero).
+extern "C" int llmc_decode_layer(const void* ln1, const void* w_qkv, const void* w_o, const void* ln2, const void* w_gu,
+                                 const void* w_down, void* k_cache, void* v_cache, const void* positions,
+                                 const void* slots, const void* seq_lens, const void* block_table, int bt_stride,
+                                 const void* cos_t, const void* sin_t, void* h, void* q, void* attn, void* act,
+                                 void* part, void* attn_ctr, void* sync, void* fault, void* stamps, int H, int nh,
+                                 int nkv, int D,
+                                 int I, int bs, int nblocks, int min_chunk, int gc, int max_chunks, float eps,
+                                 float scale, hipStream_t s) {
+  if (nh % nkv != 0 || H % kDlRows != 0 || I % kDlRows != 0 || ((nh + 2 * nkv) * D) % kDlRows != 0 ||
+      D % kDlRows != 0 || H % 8 != 0 || (nh * D) % 8 != 0 || gc < 1 || gc > 32 || gc > max_chunks ||
+      min_chunk % 32 != 0 || min_chunk < 32 || bt_stride < 1 || nblocks < 1 || fault == nullptr || sync == nullptr)
+    return -1;
+  if (static_cast<int64_t>(nblocks) * nkv * bs * D * 2 >= (1ll << 31)) return -4;  // 32-bit buffer offsets
+  DecodeLayerArgs a;
+  a.ln1 = (const bf16_t*)ln1;
+  a.w_qkv = (const bf16_t*)w_qkv;
+  a.w_o = (const bf16_t*)w_o;
+  a.ln2 = (const bf16_t*)ln2;
+  a.w_gu = (const bf16_t*)w_gu;
+  a.w_down = (const bf16_t*)w_down;
+  a.k_cache = (bf16_t*)k_cache;
+  a.v_cache = (bf16_t*)v_cache;
+  a.positions = (const int32_t*)positions;
+  a.slots = (const int32_t*)slots;
+  a.seq_lens = (const int32_t*)seq_lens;
+  a.block_table = (const int32_t*)block_table;
+  a.cos_t = (const float*)cos_t;
+  a.sin_t = (const float*)sin_t;
+  a.h = (bf16_t*)h;
+  a.q = (bf16_t*)q;
+  a.attn = (bf16_t*)attn;
+  a.act = (bf16_t*)act;
+  a.part = (float*)part;
+  a.attn_ctr = (int*)attn_ctr;
+  a.sync = (uint32_t*)sync;
+  a.fault = (int*)fault;
+  a.stamps = (uint64_t*)stamps;
+  a.bt_stride = bt_stride;
+  a.H = H;
+  a.nh = nh;
+  a.nkv = nkv;
+  a.I = I;
+  a.bs = bs;
+  a.nblocks = nblocks;
+  a.min_chunk = min_chunk;
+  a.gc = gc;
+  a.max_chunks = max_chunks;
+  a.max_groups = llmc_attn_decode_groups(max_chunks);
+  a.eps = eps;
+  a.scale_log2 = scale * 1.4426950408889634f;
+  a.n_qkv = (nh + 2 * nkv) * D / kDlRows;
+  a.n_attn = nkv * gc;
+  a.n_o = H / kDlRows;
+  a.n_gu = 2 * I / kDlRows;
+  a.n_down = H / kDlRows;
+  const int G = nh / nkv;
+  // LDS: the largest of a GEMV's x image (+ reduction / staging words) and attention's 8 V images
+  // + page ids of the longest balanced range (the wave states reuse the V images)
+  const int kmax = H > I ? (H > nh * D ? H : nh * D) : (I > nh * D ? I : nh * D);
+  const size_t gemv_lds = static_cast<size_t>(kmax) * 2 + (kDlWaves + kDlRows) * sizeof(float);
+  const int units = (bt_stride * bs + 31) / 32;
+  const int max_range = 32 * ((units + gc - 1) / gc) + 32;
+  const size_t attn_lds = static_cast<size_t>(kDlWaves) * 32 * kVRowBytes +
+                          static_cast<size_t>((max_range + bs - 1) / bs + 2) * sizeof(int);
+  const size_t red_lds = static_cast<size_t>(kDlWaves) * G * (D + 2) * sizeof(float);
+  // the wave states and merge_rows' scratch (2 x 16 B per thread) reuse the V images
+  const size_t lds = gemv_lds > attn_lds ? gemv_lds : attn_lds;
+  if (red_lds > static_cast<size_t>(kDlWaves) * 32 * kVRowBytes) return -4;
+  if (lds > 160 * 1024) return -4;
+  switch (G * 1000 + D) {
+    case 1128: return launch_dl<1, 128>(a, lds, s);
+    case 2128: return launch_dl<2, 128>(a, lds, s);
+    case 4128: return launch_dl<4, 128>(a, lds, s);
+    case 8128: return launch_dl<8, 128>(a, lds, s);
+    case 1096: return launch_dl<1, 96>(a, lds, s);
+    case 4064: return launch_dl<4, 64>(a, lds, s);
+    case 2064: return launch_dl<2, 64>(a, lds, s);
+    default: return -3;
+  }
+}

@@ -56,6 +56,9 @@ class EngineConfig:
     sp_min_tokens: int = 256
     # MoE under TP: each rank holds n_experts / tp whole experts instead of 1/tp of every expert
     expert_parallel: bool = False
+    # one-row engines (no TP, dense MLP): each decode layer as ONE fused launch
+    # (csrc/kernels/decode_layer.hip) instead of five kernels
+    fused_layer: bool = True
 
 
 FUSED_CHUNK_SMALL, FUSED_CHUNK_LARGE = 128, 256
@@ -242,6 +245,15 @@ class Engine:
                                          ops.FUSED_ATTN_MAX_KEYS if self.bs % 32 == 0 else 0, self.nh // self.nkv,
                                          self.nkv, rows=self.ecfg.max_batch)
         max_chunks = max(gc for _, _, gc, _ in self.attn_buckets)
+        # fused decode layer (one launch per layer) for one-row dense engines without TP
+        G = self.nh // max(1, self.nkv)
+        self.fused_layer = (self.on_gpu and self.ecfg.fused_layer and B == 1 and not c.is_moe and self.tp.size == 1
+                            and self.D in (64, 96, 128) and G in (1, 2, 4, 8) and c.hidden % 16 == 0
+                            and self.w.inter % 16 == 0 and self.D % 16 == 0)
+        if self.fused_layer:
+            self.layer_gc = [ops.decode_layer_grid(cap) for cap, _, _, _ in self.attn_buckets]
+            max_chunks = max(max_chunks, max(self.layer_gc))
+            self.dl_sync = torch.zeros(8, dtype=torch.int32, device=dev)
         self.attn_part, self.attn_counters = ops.decode_attn_workspace(B, self.nh, self.nkv, self.D, max_chunks, dev)
         # set by a decode-attention merger that gave up on a partial (checked after every decode)
         self.attn_fault = torch.zeros(1, dtype=torch.int32, device=dev) if self.on_gpu else None
@@ -545,6 +557,15 @@ class Engine:
         part = self.attn_part
         h, q, attn, act = self.h[:B], self.q[:B], self.attn[:B], self.act[:B]
         ops.embedding(self.tokens_in[:B], self.w.embed, out=h)
+        if self.fused_layer and B == 1:
+            gc = self.layer_gc[-1 if bucket is None else bucket]
+            for li, Lw in enumerate(self.w.layers):
+                ops.decode_layer(Lw, h, q, attn, act, self.k_cache[li], self.v_cache[li], self.positions[:1],
+                                 self.slots[:1], self.seq_lens[:1], self.block_tables[:1], self.cos_t, self.sin_t,
+                                 part, self.attn_counters, self.dl_sync, self.attn_fault, self.nh, self.nkv, self.D,
+                                 self.bs, gc, c.rms_eps, self.scale)
+            self._lm_head_sample(B)
+            return
         for li, Lw in enumerate(self.w.layers):
             ops.qkv_rope(h, Lw.w_qkv, Lw.ln1, c.rms_eps, q, self.k_cache[li], self.v_cache[li], self.positions[:B],
                          self.slots[:B], self.cos_t, self.sin_t, self.nh, self.nkv, self.D, self.bs,
@@ -558,8 +579,12 @@ class Engine:
             else:
                 ops.linear(h, Lw.w_gu, EPI_SILU, out=act, norm_w=Lw.ln2, eps=c.rms_eps, mfma=self.mfma_decode)
                 self._row_parallel(act, Lw.w_down, h)
+        self._lm_head_sample(B)
+
+    def _lm_head_sample(self, B: int) -> None:
         lg = self.logits_local[:B]
-        ops.linear(h, self.w.lm_head, EPI_F32, out=lg, norm_w=self.w.final_norm, eps=c.rms_eps, mfma=self.mfma_decode)
+        ops.linear(self.h[:B], self.w.lm_head, EPI_F32, out=lg, norm_w=self.w.final_norm, eps=self.cfg.rms_eps,
+                   mfma=self.mfma_decode)
         logits = self._gather_logits(B)
         self._sample(B, logits)
 
@@ -828,13 +853,15 @@ class Engine:
             attn_bad = bool(self.attn_fault.item())
             if attn_bad:
                 self.attn_fault.zero_()
+                if self.fused_layer:  # a fused layer that gave up left its step counters mid-count
+                    self.dl_sync.zero_()
         if self.tp.size > 1 and self.tp.ctrl is not None:
             if not self.tp.check_collectives():
                 raise EngineError("custom all-reduce timed out (a TP peer stalled): this request's tokens are invalid")
             attn_bad = self.tp.any_rank(attn_bad)
         if attn_bad:
             raise EngineError("decode attention: a partial merge timed out (a block never published its "
-                              "partial): this request's tokens are invalid")
+                              "partial, or a fused layer step's wait gave up): this request's tokens are invalid")
 
     def _bind_rows(self, seqs: List[Sequence], params: List[SamplingParams]) -> None:
         """Bind sequences to decode rows 0..B-1: block tables, prefill logits and sampling state."""

@@ -221,6 +221,36 @@ def attn_decode(q, k_cache, v_cache, block_tables, seq_lens, out, part, counters
     return out
 
 
+DECODE_LAYER_MIN_CHUNK = 256  # fused decode layer: keys per attention block at least (8 waves x 32)
+
+
+def decode_layer_grid(ctx_cap: int) -> int:
+    """Attention blocks per kv head of the fused decode layer for a context bucket of ``ctx_cap``
+    keys: one per 256 keys, at most 32 (one-level merge)."""
+    return max(1, min(32, -(-ctx_cap // DECODE_LAYER_MIN_CHUNK)))
+
+
+def decode_layer(Lw, h, q, attn, act, k_cache, v_cache, positions, slots, seq_lens, block_table, cos_t, sin_t,
+                 part, counters, sync, fault, nh, nkv, D, bs, gc, eps, scale, stamps=None) -> None:
+    """One decode layer for ONE row in one launch (csrc/kernels/decode_layer.hip): qkv GEMV with
+    the RMSNorm prologue and RoPE / paged-KV epilogue -> split-KV attention over ``gc`` blocks per
+    kv head -> o GEMV + residual -> gate_up GEMV with the RMSNorm prologue and SiLU-mul -> down
+    GEMV + residual, as a dataflow of dispatch-ordered tasks. ``h`` [1, H] is updated in place;
+    ``q`` / ``attn`` / ``act`` are scratch; ``part`` / ``counters``: the attn_decode workspace;
+    ``sync``: int32 [8] zeroed once; ``fault``: the engine's fault word; ``stamps`` (diagnostics):
+    int64 [tasks, 8] per-task timeline (s_memrealtime at start / task taken / wait over / before and
+    after the done signal, dispatch time, blockIdx, XCC id)."""
+    groups = counters.shape[-1] - 2
+    max_chunks = part.shape[2] - groups
+    H, I = h.shape[-1], act.shape[-1]
+    kernels().decode_layer(_p(Lw.ln1), _p(Lw.w_qkv), _p(Lw.w_o), _p(Lw.ln2), _p(Lw.w_gu), _p(Lw.w_down), _p(k_cache),
+                           _p(v_cache), _p(positions), _p(slots), _p(seq_lens), _p(block_table), block_table.stride(0),
+                           _p(cos_t), _p(sin_t), _p(h), _p(q), _p(attn), _p(act), _p(part), _p(counters), _p(sync),
+                           _p(fault), _p(stamps), H, nh, nkv, D, I, bs, k_cache.shape[0], DECODE_LAYER_MIN_CHUNK, gc,
+                           max_chunks,
+                           float(eps), float(scale), _s(h))
+
+
 def attn_prefill(q, k_cache, v_cache, block_tables, q_start, q_lens, ctx_lens, out, max_qlen, nh, nkv, D, bs, scale):
     if not q.is_cuda:
         return oracle.attn_prefill(q, k_cache, v_cache, block_tables, q_start, q_lens, ctx_lens, nh, nkv, D, bs,

@@ -57,8 +57,9 @@ class EngineConfig:
     # MoE under TP: each rank holds n_experts / tp whole experts instead of 1/tp of every expert
     expert_parallel: bool = False
     # one-row engines (no TP, dense MLP): each decode layer as ONE fused launch
-    # (csrc/kernels/decode_layer.hip) instead of five kernels
-    fused_layer: bool = True
+    # (csrc/kernels/decode_layer.hip) instead of five kernels. Off by default: measured slower
+    # than the five tuned kernels so far (docs/ARCHITECTURE.md, "Fused decode layer")
+    fused_layer: bool = False
 
 
 FUSED_CHUNK_SMALL, FUSED_CHUNK_LARGE = 128, 256

@@ -23,7 +23,7 @@ ap.add_argument("--reps", type=int, default=20)
 a = ap.parse_args()
 
 cfg = FAMILIES[a.model].with_(n_layers=2)
-e = Engine(cfg, EngineConfig(device="cuda:0", max_context=a.ctx + 64, seed=1))
+e = Engine(cfg, EngineConfig(device="cuda:0", max_context=a.ctx + 64, seed=1, fused_layer=True))
 assert e.fused_layer
 prompt = [(i * 7919) % 30000 + 256 for i in range(a.ctx)]
 s = e.new_sequence()

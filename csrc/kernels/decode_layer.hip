@@ -38,7 +38,10 @@ constexpr int kDlThreads = 512, kDlWaves = kDlThreads / kWave;
 constexpr int kDlRows = 2 * kDlWaves;  // GEMV output rows per task: 2 per wave
 constexpr int kDlUnroll = 4;           // 16-B weight chunks per row per lane per batch
 constexpr unsigned kDlSpinLimit = 1u << 22;
-enum { DL_DISPATCH = 0, DL_QKV = 1, DL_ATTN = 2, DL_O = 3, DL_GU = 4, DL_DOWN = 5, DL_WORDS = 8 };
+// counters, each on a 256-B line of its own (pollers of one never slow the atomics of another)
+constexpr int kDlLine = 64;  // uint32 words
+enum { DL_DISPATCH = 0, DL_QKV = 1 * kDlLine, DL_ATTN = 2 * kDlLine, DL_O = 3 * kDlLine, DL_GU = 4 * kDlLine,
+       DL_DOWN = 5 * kDlLine, DL_COUNTERS = 6, DL_WORDS = 8 * kDlLine };
 
 struct DecodeLayerArgs {
   const bf16_t *ln1, *w_qkv, *w_o, *ln2, *w_gu, *w_down;
@@ -48,12 +51,13 @@ struct DecodeLayerArgs {
   bf16_t *h, *q, *attn, *act;  // residual row [H]; scratch q / attention output [nh D]; act [I]
   float* part;                 // attention partial granules (attn_decode workspace, row 0)
   int* attn_ctr;               // its {ticket, epoch, group tickets} per kv head
-  uint32_t* sync;              // DL_WORDS counters, zero between launches
+  uint32_t* sync;              // DL_WORDS words (DL_COUNTERS counters, one per line), zero between launches
   int* fault;                  // 1: attention merge gave up, 2: a step's wait gave up
   uint64_t* stamps;            // diagnostics (nullptr = off): 5 s_memrealtime stamps per task
   int bt_stride, H, nh, nkv, I, bs, nblocks, min_chunk, gc, max_chunks, max_groups;
   float eps, scale_log2;
   int n_qkv, n_attn, n_o, n_gu, n_down;
+  int gu_groups;  // 16-row groups per gate_up task
 };
 
 // Diagnostics: task timeline stamps (100 MHz real-time counter), thread 0 only.
@@ -86,7 +90,7 @@ __device__ __forceinline__ void dl_wait(uint32_t* ctr, uint32_t target, int* fau
         __hip_atomic_store(fault, 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         break;
       }
-      __builtin_amdgcn_s_sleep(1);
+      __builtin_amdgcn_s_sleep(4);
     }
   }
   __syncthreads();
@@ -102,20 +106,28 @@ __device__ __forceinline__ uint32_t dl_signal(uint32_t* ctr) {
   return old;
 }
 
-// Rows [r0, r0 + 16) of W[N, K] (2 per wave) against x = NORM ? bf16(rmsnorm(src) * norm_w) : src,
-// src written in this launch (K bf16). The first weight batch is requested BEFORE the wait on
-// `dep`. On return every lane of wave w holds rows r0 + 2w, r0 + 2w + 1 in y[0], y[1].
+// Rows [r0, r0 + 16 g) of W[N, K] — g groups of 16 rows, 2 per wave per group — against
+// x = NORM ? bf16(rmsnorm(src) * norm_w) : src, src written in this launch (K bf16, K <= 16 x 512 x
+// 8). The first weight batch (and the norm weights) is requested BEFORE the wait on `dep`; the
+// weights then stream as one double-buffered sequence of (group, K batch) units. `pre` (nullable):
+// 8 bf16 per thread < 2 g loaded write-through right after the wait (the residual rows an epilogue
+// adds to). On return the staging area out[16 g] holds every row's dot product (row r0 + 16 j +
+// 2 w + k at out[16 j + 2 w + k]) and the block has met at a barrier.
 template <bool NORM>
-__device__ __forceinline__ void dl_gemv(const bf16_t* __restrict__ W, int N, int K, int r0, const WtBuf& xb,
-                                        const bf16_t* src, const bf16_t* __restrict__ norm_w, float eps, uint32_t* dep,
-                                        uint32_t target, int* fault, char* smem, float (&y)[2], uint64_t* stp) {
+__device__ __forceinline__ float* dl_gemv(const bf16_t* __restrict__ W, int N, int K, int r0, int g, const WtBuf& xb,
+                                          const bf16_t* src, const bf16_t* __restrict__ norm_w, float eps,
+                                          uint32_t* dep, uint32_t target, int* fault, char* smem, uint64_t* stp,
+                                          const WtBuf* pre_b = nullptr, const bf16_t* pre = nullptr,
+                                          u32x4* pre_v = nullptr) {
   const int tid = threadIdx.x, wave = tid / kWave, lane = tid % kWave;
   const int nchunk = K / 8;
-  const u32x4* w0 = reinterpret_cast<const u32x4*>(W + static_cast<int64_t>(min(r0 + 2 * wave, N - 1)) * K);
-  const u32x4* w1 = reinterpret_cast<const u32x4*>(W + static_cast<int64_t>(min(r0 + 2 * wave + 1, N - 1)) * K);
   constexpr int U = kDlUnroll, STEP = kWave * U;
-  const int iters = (nchunk + STEP - 1) / STEP;
-  auto issue = [&](u32x4 (&d)[2][U], int cb) {
+  const int iters = (nchunk + STEP - 1) / STEP, n_units = g * iters;
+  auto issue = [&](u32x4 (&d)[2][U], int unit) {
+    const int grp = unit / iters, cb = (unit % iters) * STEP + lane;
+    const int row = min(r0 + 16 * grp + 2 * wave, N - 2);
+    const u32x4* w0 = reinterpret_cast<const u32x4*>(W + static_cast<int64_t>(row) * K);
+    const u32x4* w1 = w0 + nchunk;
 #pragma unroll
     for (int u = 0; u < U; ++u) {
       const int c = min(cb + u * kWave, nchunk - 1);
@@ -124,22 +136,36 @@ __device__ __forceinline__ void dl_gemv(const bf16_t* __restrict__ W, int N, int
     }
   };
   u32x4 cur[2][U];
-  issue(cur, lane);
+  issue(cur, 0);
+  u32x4 gw[2];  // norm weights of this thread's x chunks (read-only: before the wait)
+  if constexpr (NORM) {
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int c = tid + j * kDlThreads;
+      if (c < nchunk) gw[j] = reinterpret_cast<const u32x4*>(norm_w)[c];
+    }
+  }
   dl_wait(dep, target, fault);
   dl_stamp(stp, 2);
+  if (pre != nullptr && tid < 2 * g) *pre_v = pre_b->ld16(pre + 8 * tid);
 
   // x -> LDS (normalised if NORM)
   bf16_t* xs = reinterpret_cast<bf16_t*>(smem);
   float* red = reinterpret_cast<float*>(smem + static_cast<size_t>(K) * 2);
+  float* out = red + kDlWaves;
   if constexpr (NORM) {
+    u32x4 xr[2];
     float ss = 0.f;
-    for (int c = tid; c < nchunk; c += kDlThreads) {
-      const u32x4 v = xb.ld16(src + 8 * c);
-      float f[8];
-      unpack8(v, f);
 #pragma unroll
-      for (int e = 0; e < 8; ++e) ss += f[e] * f[e];
-      reinterpret_cast<u32x4*>(xs)[c] = v;
+    for (int j = 0; j < 2; ++j) {
+      const int c = tid + j * kDlThreads;
+      if (c < nchunk) {
+        xr[j] = xb.ld16(src + 8 * c);
+        float f[8];
+        unpack8(xr[j], f);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) ss += f[e] * f[e];
+      }
     }
     ss = wave_sum(ss);
     if (lane == 0) red[wave] = ss;
@@ -148,13 +174,17 @@ __device__ __forceinline__ void dl_gemv(const bf16_t* __restrict__ W, int N, int
 #pragma unroll
     for (int w = 0; w < kDlWaves; ++w) t += red[w];
     const float inv = rsqrtf(t / K + eps);
-    for (int c = tid; c < nchunk; c += kDlThreads) {
-      float f[8], g[8];
-      unpack8(reinterpret_cast<const u32x4*>(xs)[c], f);
-      unpack8(reinterpret_cast<const u32x4*>(norm_w)[c], g);
 #pragma unroll
-      for (int e = 0; e < 8; ++e) f[e] = f[e] * inv * g[e];
-      reinterpret_cast<u32x4*>(xs)[c] = pack8(f);
+    for (int j = 0; j < 2; ++j) {
+      const int c = tid + j * kDlThreads;
+      if (c < nchunk) {
+        float f[8], gg[8];
+        unpack8(xr[j], f);
+        unpack8(gw[j], gg);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) f[e] = f[e] * inv * gg[e];
+        reinterpret_cast<u32x4*>(xs)[c] = pack8(f);
+      }
     }
   } else {
     for (int c = tid; c < nchunk; c += kDlThreads) reinterpret_cast<u32x4*>(xs)[c] = xb.ld16(src + 8 * c);
@@ -163,58 +193,51 @@ __device__ __forceinline__ void dl_gemv(const bf16_t* __restrict__ W, int N, int
 
   const u32x4* xv = reinterpret_cast<const u32x4*>(xs);
   float a0 = 0.f, a1 = 0.f;
-  int c0 = lane;
-  for (int it = 0; it + 1 < iters; ++it, c0 += STEP) {
+  for (int unit = 0; unit < n_units; ++unit) {
     u32x4 nxt[2][U];
-    issue(nxt, c0 + STEP);
+    if (unit + 1 < n_units) issue(nxt, unit + 1);
+    const int c0 = (unit % iters) * STEP + lane;
 #pragma unroll
     for (int u = 0; u < U; ++u) {
-      const u32x4 xx = xv[c0 + u * kWave];
-      a0 = dot8_bf16(cur[0][u], xx, a0);
-      a1 = dot8_bf16(cur[1][u], xx, a1);
+      const int c = c0 + u * kWave;
+      if (c < nchunk) {
+        const u32x4 xx = xv[c];
+        a0 = dot8_bf16(cur[0][u], xx, a0);
+        a1 = dot8_bf16(cur[1][u], xx, a1);
+      }
     }
+    if (unit % iters == iters - 1) {  // the group's rows are complete
+      const float y0 = wave_sum(a0), y1 = wave_sum(a1);
+      if (lane == 0) {
+        const int o = 16 * (unit / iters) + 2 * wave;
+        out[o] = y0;
+        out[o + 1] = y1;
+      }
+      a0 = a1 = 0.f;
+    }
+    if (unit + 1 < n_units) {
 #pragma unroll
-    for (int u = 0; u < U; ++u) {
-      cur[0][u] = nxt[0][u];
-      cur[1][u] = nxt[1][u];
+      for (int u = 0; u < U; ++u) {
+        cur[0][u] = nxt[0][u];
+        cur[1][u] = nxt[1][u];
+      }
     }
-  }
-#pragma unroll
-  for (int u = 0; u < U; ++u) {
-    const int c = c0 + u * kWave;
-    if (c < nchunk) {
-      const u32x4 xx = xv[c];
-      a0 = dot8_bf16(cur[0][u], xx, a0);
-      a1 = dot8_bf16(cur[1][u], xx, a1);
-    }
-  }
-  y[0] = wave_sum(a0);
-  y[1] = wave_sum(a1);
-}
-
-// Stage the 16 task outputs (2 per wave) in LDS: out16[2 * wave + j] = v[j] (after the GEMV, the
-// x image is dead: the staging area sits behind it). Block-uniform.
-__device__ __forceinline__ float* dl_stage(char* smem, int K, float v0, float v1) {
-  float* st = reinterpret_cast<float*>(smem + static_cast<size_t>(K) * 2) + kDlWaves;
-  const int wave = threadIdx.x / kWave, lane = threadIdx.x % kWave;
-  if (lane == 0) {
-    st[2 * wave] = v0;
-    st[2 * wave + 1] = v1;
   }
   __syncthreads();
-  return st;
+  return out;
 }
 
-// h[r0 .. r0 + 16) += out16 (bf16 residual stream, write-through read-modify-write by thread 0/1)
-__device__ __forceinline__ void dl_resadd(bf16_t* h, const WtBuf& hb, int r0, const float* st) {
+// h[r0 .. r0 + 16 g) += out (bf16 residual stream, write-through; old rows preloaded in `old` by
+// threads < 2 g)
+__device__ __forceinline__ void dl_resadd(bf16_t* h, const WtBuf& hb, int r0, int g, const float* out,
+                                          const u32x4& old) {
   const int tid = threadIdx.x;
-  if (tid < 2) {
-    bf16_t* p = h + r0 + 8 * tid;
+  if (tid < 2 * g) {
     float f[8];
-    unpack8(hb.ld16(p), f);
+    unpack8(old, f);
 #pragma unroll
-    for (int e = 0; e < 8; ++e) f[e] += st[8 * tid + e];
-    hb.st16(p, pack8(f));
+    for (int e = 0; e < 8; ++e) f[e] += out[8 * tid + e];
+    hb.st16(h + r0 + 8 * tid, pack8(f));
   }
 }
 
@@ -223,44 +246,40 @@ __device__ __forceinline__ void dl_qkv(const DecodeLayerArgs& a, int t, char* sm
   const int N = (a.nh + 2 * a.nkv) * D;
   const int r0 = t * kDlRows;
   const WtBuf hb(a.h, a.H * 2);
-  float y[2];
-  dl_gemv<true>(a.w_qkv, N, a.H, r0, hb, a.h, a.ln1, a.eps, nullptr, 0, a.fault, smem, y, stp);
-  // RoPE of the wave's (2i, 2i + 1) pair = dims (i, i + D/2) of a Q/K head; V rows stay in order
-  const int wave = threadIdx.x / kWave;
-  const int head = r0 / D;  // a task never straddles heads (D % 16 == 0)
+  const float* out = dl_gemv<true>(a.w_qkv, N, a.H, r0, 1, hb, a.h, a.ln1, a.eps, nullptr, 0, a.fault, smem, stp);
+  // RoPE of each (2i, 2i + 1) row pair = dims (i, i + D/2) of a Q/K head; V rows stay in order.
+  // A task never straddles heads (D % 16 == 0). Thread 0 stores the first dims of its 8 pairs,
+  // thread 1 the second ones (16 B each, write-through).
+  const int head = r0 / D;
   constexpr int half = D / 2;
-  float o0 = y[0], o1 = y[1];
-  if (head < a.nh + a.nkv) {
-    const int i = (r0 % D) / 2 + wave;
-    const int pos = a.positions[0];
-    const float c = a.cos_t[static_cast<int64_t>(pos) * half + i], sn = a.sin_t[static_cast<int64_t>(pos) * half + i];
-    o0 = y[0] * c - y[1] * sn;
-    o1 = y[1] * c + y[0] * sn;
-  }
-  const float* st = dl_stage(smem, a.H, o0, o1);
   const int tid = threadIdx.x;
   if (tid < 2) {
     float f[8];
-    bf16_t* dst = nullptr;
     const int slot = a.slots[0];
     const int64_t page = slot / a.bs, off = slot % a.bs;
-    if (head < a.nh + a.nkv) {  // piece tid: dims i0 .. i0 + 8 (first of each pair) or + D/2 (second)
-      const int i0 = (r0 % D) / 2 + tid * half;
+    const uint32_t cache_bytes = static_cast<uint32_t>(static_cast<int64_t>(a.nblocks) * a.nkv * a.bs * D * 2);
+    if (head < a.nh + a.nkv) {
+      const int ip = (r0 % D) / 2;  // first pair index of the task
+      const int pos = a.positions[0];
 #pragma unroll
-      for (int e = 0; e < 8; ++e) f[e] = st[2 * e + tid];
+      for (int e = 0; e < 8; ++e) {
+        const float c = a.cos_t[static_cast<int64_t>(pos) * half + ip + e];
+        const float sn = a.sin_t[static_cast<int64_t>(pos) * half + ip + e];
+        const float y0 = out[2 * e], y1 = out[2 * e + 1];
+        f[e] = tid == 0 ? y0 * c - y1 * sn : y1 * c + y0 * sn;
+      }
+      const int i0 = ip + tid * half;
       if (head < a.nh) {
-        dst = a.q + head * D + i0;
-        WtBuf(a.q, a.nh * D * 2).st16(dst, pack8(f));
+        WtBuf(a.q, a.nh * D * 2).st16(a.q + head * D + i0, pack8(f));
       } else if (slot >= 0) {
-        dst = a.k_cache + ((page * a.nkv + (head - a.nh)) * a.bs + off) * D + i0;
-        WtBuf(a.k_cache, static_cast<uint32_t>(static_cast<int64_t>(a.nblocks) * a.nkv * a.bs * D * 2)).st16(dst, pack8(f));
+        WtBuf(a.k_cache, cache_bytes).st16(a.k_cache + ((page * a.nkv + (head - a.nh)) * a.bs + off) * D + i0, pack8(f));
       }
     } else if (slot >= 0) {  // V rows r0 .. r0 + 16 = dims d0 .. d0 + 16 in order
-      const int d0 = r0 % D + 8 * tid;
 #pragma unroll
-      for (int e = 0; e < 8; ++e) f[e] = st[8 * tid + e];
-      dst = a.v_cache + ((page * a.nkv + (head - a.nh - a.nkv)) * a.bs + off) * D + d0;
-      WtBuf(a.v_cache, static_cast<uint32_t>(static_cast<int64_t>(a.nblocks) * a.nkv * a.bs * D * 2)).st16(dst, pack8(f));
+      for (int e = 0; e < 8; ++e) f[e] = out[8 * tid + e];
+      const int d0 = r0 % D + 8 * tid;
+      WtBuf(a.v_cache, cache_bytes)
+          .st16(a.v_cache + ((page * a.nkv + (head - a.nh - a.nkv)) * a.bs + off) * D + d0, pack8(f));
     }
   }
   dl_stamp(stp, 3);
@@ -333,28 +352,28 @@ __device__ __forceinline__ void dl_attn(const DecodeLayerArgs& a, int t, char* s
 template <int G, int D>
 __device__ __forceinline__ void dl_o(const DecodeLayerArgs& a, int t, char* smem, uint64_t* stp) {
   const int r0 = t * kDlRows, K = a.nh * D;
-  float y[2];
-  dl_gemv<false>(a.w_o, a.H, K, r0, WtBuf(a.attn, K * 2), a.attn, nullptr, 0.f, a.sync + DL_ATTN, a.nkv, a.fault,
-                 smem, y, stp);
-  const float* st = dl_stage(smem, K, y[0], y[1]);
-  dl_resadd(a.h, WtBuf(a.h, a.H * 2), r0, st);
+  const WtBuf hb(a.h, a.H * 2);
+  u32x4 old;
+  // the residual rows were last written by the previous layer's launch: preloaded behind the wait
+  const float* out = dl_gemv<false>(a.w_o, a.H, K, r0, 1, WtBuf(a.attn, K * 2), a.attn, nullptr, 0.f,
+                                    a.sync + DL_ATTN, a.nkv, a.fault, smem, stp, &hb, a.h + r0, &old);
+  dl_resadd(a.h, hb, r0, 1, out, old);
   dl_stamp(stp, 3);
   dl_signal(a.sync + DL_O);
   dl_stamp(stp, 4);
 }
 
 __device__ __forceinline__ void dl_gu(const DecodeLayerArgs& a, int t, char* smem, uint64_t* stp) {
-  const int r0 = t * kDlRows;
-  float y[2];
-  dl_gemv<true>(a.w_gu, 2 * a.I, a.H, r0, WtBuf(a.h, a.H * 2), a.h, a.ln2, a.eps, a.sync + DL_O, a.n_o, a.fault,
-                smem, y, stp);
-  // rows (2i, 2i + 1) = (gate_i, up_i): wave w holds output column r0 / 2 + w
-  const float* st = dl_stage(smem, a.H, silu(y[0]) * y[1], 0.f);
-  if (threadIdx.x == 0) {
+  const int g = a.gu_groups, r0 = t * kDlRows * g;
+  const float* out = dl_gemv<true>(a.w_gu, 2 * a.I, a.H, r0, g, WtBuf(a.h, a.H * 2), a.h, a.ln2, a.eps,
+                                   a.sync + DL_O, a.n_o, a.fault, smem, stp);
+  // rows (2i, 2i + 1) = (gate_i, up_i): 8 act columns per 16-row group, one 16-B store each
+  const int tid = threadIdx.x;
+  if (tid < g) {
     float f[8];
 #pragma unroll
-    for (int e = 0; e < 8; ++e) f[e] = st[2 * e];
-    WtBuf(a.act, a.I * 2).st16(a.act + r0 / 2, pack8(f));
+    for (int e = 0; e < 8; ++e) f[e] = silu(out[16 * tid + 2 * e]) * out[16 * tid + 2 * e + 1];
+    WtBuf(a.act, a.I * 2).st16(a.act + r0 / 2 + 8 * tid, pack8(f));
   }
   dl_stamp(stp, 3);
   dl_signal(a.sync + DL_GU);
@@ -363,18 +382,21 @@ __device__ __forceinline__ void dl_gu(const DecodeLayerArgs& a, int t, char* sme
 
 __device__ __forceinline__ void dl_down(const DecodeLayerArgs& a, int t, char* smem, uint64_t* stp) {
   const int r0 = t * kDlRows;
-  float y[2];
-  dl_gemv<false>(a.w_down, a.H, a.I, r0, WtBuf(a.act, a.I * 2), a.act, nullptr, 0.f, a.sync + DL_GU, a.n_gu, a.fault,
-                 smem, y, stp);
-  const float* st = dl_stage(smem, a.I, y[0], y[1]);
-  dl_resadd(a.h, WtBuf(a.h, a.H * 2), r0, st);
+  const WtBuf hb(a.h, a.H * 2);
+  u32x4 old;
+  // the residual rows were written by this launch's o tasks (done before any gu task began, so
+  // before this task's wait is over): loaded behind the wait
+  const float* out = dl_gemv<false>(a.w_down, a.H, a.I, r0, 1, WtBuf(a.act, a.I * 2), a.act, nullptr, 0.f,
+                                    a.sync + DL_GU, a.n_gu, a.fault, smem, stp, &hb, a.h + r0, &old);
+  dl_resadd(a.h, hb, r0, 1, out, old);
   dl_stamp(stp, 3);
-  const uint32_t old = dl_signal(a.sync + DL_DOWN);
+  const uint32_t prev = dl_signal(a.sync + DL_DOWN);
   dl_stamp(stp, 4);
-  if (threadIdx.x == 0 && old == static_cast<uint32_t>(a.n_down - 1)) {
+  if (threadIdx.x == 0 && prev == static_cast<uint32_t>(a.n_down - 1)) {
     // the last task of the launch: every block has taken its index and every wait is over
 #pragma unroll
-    for (int w = 0; w < DL_WORDS; ++w) __hip_atomic_store(a.sync + w, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    for (int w = 0; w < DL_COUNTERS; ++w)
+      __hip_atomic_store(a.sync + w * kDlLine, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
 }
 
@@ -432,7 +454,7 @@ extern "C" int llmc_attn_decode_groups(int max_chunks);
 
 // One decode layer for ONE row (see the header). gc <= 32 balanced attention blocks per kv head of
 // >= min_chunk keys (a multiple of 32); max_chunks / part / attn_ctr: the attn_decode workspace
-// (max_chunks >= gc). sync: DL_WORDS uint32 counters, zeroed once (each launch leaves them zero).
+// (max_chunks >= gc). sync: DL_WORDS (512) uint32 words, zeroed once (each launch leaves them zero).
 extern "C" int llmc_decode_layer(const void* ln1, const void* w_qkv, const void* w_o, const void* ln2, const void* w_gu,
                                  const void* w_down, void* k_cache, void* v_cache, const void* positions,
                                  const void* slots, const void* seq_lens, const void* block_table, int bt_stride,
@@ -441,7 +463,7 @@ extern "C" int llmc_decode_layer(const void* ln1, const void* w_qkv, const void*
                                  int nkv, int D,
                                  int I, int bs, int nblocks, int min_chunk, int gc, int max_chunks, float eps,
                                  float scale, hipStream_t s) {
-  if (nh % nkv != 0 || H % kDlRows != 0 || I % kDlRows != 0 || ((nh + 2 * nkv) * D) % kDlRows != 0 ||
+  if (H / 8 > 2 * kDlThreads || nh % nkv != 0 || H % kDlRows != 0 || I % kDlRows != 0 || ((nh + 2 * nkv) * D) % kDlRows != 0 ||
       D % kDlRows != 0 || H % 8 != 0 || (nh * D) % 8 != 0 || gc < 1 || gc > 32 || gc > max_chunks ||
       min_chunk % 32 != 0 || min_chunk < 32 || bt_stride < 1 || nblocks < 1 || fault == nullptr || sync == nullptr)
     return -1;
@@ -486,13 +508,22 @@ extern "C" int llmc_decode_layer(const void* ln1, const void* w_qkv, const void*
   a.n_qkv = (nh + 2 * nkv) * D / kDlRows;
   a.n_attn = nkv * gc;
   a.n_o = H / kDlRows;
-  a.n_gu = 2 * I / kDlRows;
+  // gate_up: several 16-row groups per task while >= 256 tasks remain (one x image and one set of
+  // per-task overheads for up to 8 groups)
+  const int gu_rows = 2 * I / kDlRows;
+  a.gu_groups = 1;
+  for (int gg = 8; gg > 1; --gg)
+    if (gu_rows % gg == 0 && gu_rows / gg >= 256) {
+      a.gu_groups = gg;
+      break;
+    }
+  a.n_gu = gu_rows / a.gu_groups;
   a.n_down = H / kDlRows;
   const int G = nh / nkv;
   // LDS: the largest of a GEMV's x image (+ reduction / staging words) and attention's 8 V images
   // + page ids of the longest balanced range (the wave states reuse the V images)
   const int kmax = H > I ? (H > nh * D ? H : nh * D) : (I > nh * D ? I : nh * D);
-  const size_t gemv_lds = static_cast<size_t>(kmax) * 2 + (kDlWaves + kDlRows) * sizeof(float);
+  const size_t gemv_lds = static_cast<size_t>(kmax) * 2 + (kDlWaves + 8 * kDlRows) * sizeof(float);
   const int units = (bt_stride * bs + 31) / 32;
   const int max_range = 32 * ((units + gc - 1) / gc) + 32;
   const size_t attn_lds = static_cast<size_t>(kDlWaves) * 32 * kVRowBytes +

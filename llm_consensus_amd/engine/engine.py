@@ -254,7 +254,7 @@ class Engine:
         if self.fused_layer:
             self.layer_gc = [ops.decode_layer_grid(cap) for cap, _, _, _ in self.attn_buckets]
             max_chunks = max(max_chunks, max(self.layer_gc))
-            self.dl_sync = torch.zeros(8, dtype=torch.int32, device=dev)
+            self.dl_sync = torch.zeros(ops.DECODE_LAYER_SYNC_WORDS, dtype=torch.int32, device=dev)
         self.attn_part, self.attn_counters = ops.decode_attn_workspace(B, self.nh, self.nkv, self.D, max_chunks, dev)
         # set by a decode-attention merger that gave up on a partial (checked after every decode)
         self.attn_fault = torch.zeros(1, dtype=torch.int32, device=dev) if self.on_gpu else None

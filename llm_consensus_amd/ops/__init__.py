@@ -222,6 +222,7 @@ def attn_decode(q, k_cache, v_cache, block_tables, seq_lens, out, part, counters
 
 
 DECODE_LAYER_MIN_CHUNK = 256  # fused decode layer: keys per attention block at least (8 waves x 32)
+DECODE_LAYER_SYNC_WORDS = 512  # its step counters, one 256-B line each
 
 
 def decode_layer_grid(ctx_cap: int) -> int:
@@ -237,7 +238,7 @@ def decode_layer(Lw, h, q, attn, act, k_cache, v_cache, positions, slots, seq_le
     kv head -> o GEMV + residual -> gate_up GEMV with the RMSNorm prologue and SiLU-mul -> down
     GEMV + residual, as a dataflow of dispatch-ordered tasks. ``h`` [1, H] is updated in place;
     ``q`` / ``attn`` / ``act`` are scratch; ``part`` / ``counters``: the attn_decode workspace;
-    ``sync``: int32 [8] zeroed once; ``fault``: the engine's fault word; ``stamps`` (diagnostics):
+    ``sync``: int32 [DECODE_LAYER_SYNC_WORDS] zeroed once; ``fault``: the engine's fault word; ``stamps`` (diagnostics):
     int64 [tasks, 8] per-task timeline (s_memrealtime at start / task taken / wait over / before and
     after the done signal, dispatch time, blockIdx, XCC id)."""
     groups = counters.shape[-1] - 2

@@ -35,7 +35,9 @@ torch.cuda.synchronize()
 bucket = e._bucket(s.length + 8)
 gc = e.layer_gc[bucket]
 nh, nkv, D, H, I = e.nh, e.nkv, e.D, cfg.hidden, e.w.inter
-counts = {"qkv": (nh + 2 * nkv) * D // 16, "attn": nkv * gc, "o": H // 16, "gu": 2 * I // 16, "down": H // 16}
+gu_rows = 2 * I // 16
+gu_g = next((g for g in range(8, 1, -1) if gu_rows % g == 0 and gu_rows // g >= 256), 1)  # as the kernel
+counts = {"qkv": (nh + 2 * nkv) * D // 16, "attn": nkv * gc, "o": H // 16, "gu": gu_rows // gu_g, "down": H // 16}
 ntask = sum(counts.values())
 st = torch.zeros(ntask, 8, dtype=torch.int64, device="cuda")
 Lw = e.w.layers[0]

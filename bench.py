@@ -59,6 +59,7 @@ from typing import Dict, List, Optional
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
+T_START = time.time()  # the wall-clock budget (--time-budget) counts from here
 
 METRIC = "consensus_aggregate_output_tokens_per_s"
 TINY = {"llama-3-8b": "llama-tiny", "llama-3-70b": "llama-tiny-tp4", "mixtral-8x7b": "mixtral-tiny",
@@ -248,6 +249,10 @@ def main() -> None:
     ap.add_argument("--judge-tp", type=int, default=0, help="0 = auto (config 5: 4)")
     ap.add_argument("--steps-per-graph", type=int, default=8)
     ap.add_argument("--no-graphs", action="store_true")
+    ap.add_argument("--time-budget", type=float, default=560.0,
+                    help="seconds the whole command may take (0 = off): the last two warmup rounds (W >= 2) are "
+                         "timed at two lengths, and if K full rounds would overrun, the timed rounds decode fewer "
+                         "tokens (recorded as config.max_tokens, with max_tokens_requested)")
     ap.add_argument("--results-dir", default=os.path.join(ROOT, "bench", "results"),
                     help="rank 0 also writes the full record (per-step stats, p50/p90) here ('' = off)")
     args = ap.parse_args()
@@ -491,9 +496,31 @@ def main() -> None:
         stats["tokens"] = n_tokens + (jmax_r if judge_plan else 0)
         return stats
 
+    wt = args.warmup_tokens or args.max_tokens
+    probe = {}
     for w in range(args.warmup):
-        st = one_round(w, args.warmup_tokens)
+        # the last two warmup rounds double as a cost probe: round time ~ c0 + c1 x tokens
+        n_w = 2 * wt if (w == args.warmup - 1 and args.warmup >= 2) else wt
+        tw = time.perf_counter()
+        st = one_round(w, min(n_w, args.max_tokens))
+        probe[min(n_w, args.max_tokens)] = time.perf_counter() - tw
         log(f"warmup {w}: {st}")
+    round_tokens = args.max_tokens
+    if args.time_budget > 0 and args.warmup >= 2 and len(probe) == 2:
+        (t1, s1), (t2, s2) = sorted(probe.items())
+        pr = torch.tensor([s1, s2], dtype=torch.float64, device=cdev)
+        if world > 1:
+            dist.all_reduce(pr, op=dist.ReduceOp.MAX)
+        s1, s2 = float(pr[0]), float(pr[1])
+        c1 = max((s2 - s1) / (t2 - t1), 1e-6)
+        c0 = max(s1 - c1 * t1, 0.0)
+        left = args.time_budget - (time.time() - T_START) - 10.0  # teardown margin
+        need = args.steps * (c0 + c1 * args.max_tokens)
+        if need > left:
+            fit = int(((left / args.steps) - c0) / c1) // 64 * 64
+            round_tokens = max(64, min(args.max_tokens, fit))
+            log(f"time budget: {args.steps} rounds of {args.max_tokens} tokens need ~{need:.0f}s, {left:.0f}s left: "
+                f"timed rounds decode {round_tokens} tokens")
 
     sync()
     if world > 1:
@@ -503,7 +530,7 @@ def main() -> None:
     t0 = time.perf_counter()
     per_step = []
     for s in range(args.steps):
-        st = one_round(100 + s)
+        st = one_round(100 + s, round_tokens)
         lat.append(st["e2e_s"])
         tot_tokens += st["tokens"]
         per_step.append(st)
@@ -527,7 +554,7 @@ def main() -> None:
     if rank == 0:
         names = [e["name"] for e in resp_plan]
         value = tot_tokens / elapsed
-        resp_tok_s = n_resp * args.max_tokens * args.steps / sum(p["responders_s"] for p in per_step)
+        resp_tok_s = n_resp * round_tokens * args.steps / sum(p["responders_s"] for p in per_step)
         jtp = len(judge_plan["ranks"])
         rtp = sorted({len(e["ranks"]) for e in resp_plan if len(e["ranks"]) > 1})
         par = {"fanout": f"fanout{n_resp}" + "".join(f"-resp_tp{t}" for t in rtp),
@@ -550,8 +577,8 @@ def main() -> None:
                 "name": config_name(args, n_gpus, resp_plan, judge_plan),
                 "model": describe(resp_plan, judge_plan),
                 "global_batch": n_resp,
-                "seq_len": args.prompt_tokens + args.max_tokens,
-                "max_tokens": args.max_tokens,
+                "seq_len": args.prompt_tokens + round_tokens,
+                "max_tokens": round_tokens,
                 "prompt_tokens": args.prompt_tokens,
                 "parallelism": par + ("" if n_gpus == 1 else f"-over{n_gpus}gpus") + (f"-judge_tp{jtp}" if jtp > 1 else ""),
             },
@@ -574,7 +601,10 @@ def main() -> None:
                 "per_model_ttft_ms": {m: round(1000 * statistics.median(p["per_model"][m]["ttft_s"] for p in per_step), 1)
                                       for m in names},
                 "judge_tp": jtp,
-                "warmup_rounds_tokens": [args.warmup_tokens or args.max_tokens] * args.warmup,
+                "warmup_rounds_tokens": [min(args.max_tokens, wt * (2 if (w == args.warmup - 1 and args.warmup >= 2)
+                                                                      else 1)) for w in range(args.warmup)],
+                "max_tokens_requested": args.max_tokens,
+                "time_budget_s": args.time_budget,
                 "custom_allreduce": {e.name: e.tp.custom is not None for _, e, _, _ in responders if e.tp.size > 1}
                 | ({judge.name: judge.tp.custom is not None} if judge is not None and judge.tp.size > 1 else {}),
             },

@@ -80,11 +80,23 @@ def test_fanout_two_ranks_balances_the_third_responder():
 
 
 def test_warmup_rounds_are_short_timed_rounds_full():
-    """Warmup rounds decode --warmup-tokens per engine; the timed rounds (and the reported tokens)
-    are full rounds."""
-    d = _run(1, ["--shapes", "tiny", "--steps", "1", "--warmup", "2", "--max-tokens", "12", "--warmup-tokens", "4"], 0)
-    assert d["extra"]["warmup_rounds_tokens"] == [4, 4]
+    """Warmup rounds decode --warmup-tokens per engine (the last one twice that: with the one
+    before it, the round-cost probe of the time budget); the timed rounds (and the reported
+    tokens) are full rounds."""
+    d = _run(1, ["--shapes", "tiny", "--steps", "1", "--warmup", "3", "--max-tokens", "12", "--warmup-tokens", "4"], 0)
+    assert d["extra"]["warmup_rounds_tokens"] == [4, 4, 8]
+    assert d["config"]["max_tokens"] == d["extra"]["max_tokens_requested"] == 12
     _tokens_ok(d, 12)
+
+
+def test_time_budget_shortens_rounds_never_steps():
+    """A budget the requested rounds cannot fit: the timed rounds decode fewer tokens (reported as
+    config.max_tokens next to max_tokens_requested), still exactly --steps of them."""
+    d = _run(1, ["--shapes", "tiny", "--steps", "2", "--warmup", "2", "--max-tokens", "4096", "--warmup-tokens", "8",
+                 "--time-budget", "1"], 0)
+    assert d["steps"] == 2 and d["extra"]["max_tokens_requested"] == 4096
+    assert 64 <= d["config"]["max_tokens"] < 4096
+    _tokens_ok(d, d["config"]["max_tokens"])
 
 
 def _self_launched(n, extra=()):

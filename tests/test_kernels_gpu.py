@@ -380,6 +380,37 @@ def test_attn_decode_wide_split(cuda, nh, nkv, gc):
     assert int(tickets.abs().sum()) == 0, ctr
 
 
+def test_attn_decode_partial_rounding_at_33k(cuda):
+    """each chunk's normalised partial O/l is published in bf16, and the two-level merge
+    (256 blocks = 16 groups of 16) rounds the group results to bf16 again. Measured against an fp32
+    attention at 33k keys on a TP=8 rank's shape (4 query heads on one kv head): the error of the
+    256-block two-level path vs that of ONE block (no published partials: f32 wave merge, one
+    bf16 rounding of the output). The extra roundings must stay within bf16's own rounding of the
+    output (recorded in the assertion message)."""
+    torch.manual_seed(12)
+    nh, nkv, D, bs, L = 4, 1, 128, 64, 33000
+    kc, vc, bt = _paged_kv(1, L, nkv, D, bs)
+    q = rnd(1, nh * D)
+    sl = torch.tensor([L], dtype=torch.int32)
+    scale = 1 / math.sqrt(D)
+    # fp32 reference on the GPU
+    idx = torch.arange(L, device="cuda")
+    pages = bt[0].cuda().long()[idx // bs]
+    k = kc[pages, 0, idx % bs].float()
+    v = vc[pages, 0, idx % bs].float()
+    p = torch.softmax((q.view(nh, D).float() @ k.t()) * scale, dim=-1)
+    ref = (p @ v).view(1, -1)
+    errs = {}
+    for gc in (1, 256):
+        part, ctr = ops.decode_attn_workspace(1, nh, nkv, D, gc, "cuda")
+        out = torch.zeros(1, nh * D, dtype=BF, device="cuda")
+        ops.attn_decode(q, kc, vc, bt.cuda(), sl.cuda(), out, part, ctr, nh, nkv, D, bs, 128, scale, grid_chunks=gc)
+        torch.cuda.synchronize()
+        errs[gc] = (out.float() - ref).abs().max().item()
+    bf16_ulp = ref.abs().max().item() * 2 ** -8
+    assert errs[256] <= errs[1] + bf16_ulp, (errs, bf16_ulp)
+
+
 @pytest.mark.parametrize("nh,nkv,D", [(32, 8, 128), (32, 32, 96), (16, 2, 128), (4, 2, 64)])
 @pytest.mark.parametrize("case", ["full", "chunk", "ragged"])
 def test_attn_prefill(cuda, nh, nkv, D, case):

@@ -38,10 +38,15 @@ constexpr int kDlThreads = 512, kDlWaves = kDlThreads / kWave;
 constexpr int kDlRows = 2 * kDlWaves;  // GEMV output rows per task: 2 per wave
 constexpr int kDlUnroll = 4;           // 16-B weight chunks per row per lane per batch
 constexpr unsigned kDlSpinLimit = 1u << 22;
-// counters, each on a 256-B line of its own (pollers of one never slow the atomics of another)
+// counters, each on a 256-B line of its own (pollers of one never slow the atomics of another):
+// the dispatch counter, per GEMV step a work queue (next 16-row group) and a done counter (groups
+// finished; attention: kv heads merged), and the exit counter whose last increment re-arms them all
 constexpr int kDlLine = 64;  // uint32 words
-enum { DL_DISPATCH = 0, DL_QKV = 1 * kDlLine, DL_ATTN = 2 * kDlLine, DL_O = 3 * kDlLine, DL_GU = 4 * kDlLine,
-       DL_DOWN = 5 * kDlLine, DL_COUNTERS = 6, DL_WORDS = 8 * kDlLine };
+enum {
+  DL_DISPATCH = 0, DL_EXIT, DL_QKV_Q, DL_QKV, DL_ATTN, DL_O_Q, DL_O, DL_GU_Q, DL_GU, DL_DOWN_Q, DL_DOWN,
+  DL_COUNTERS
+};
+constexpr int DL_WORDS = 16 * kDlLine;
 
 struct DecodeLayerArgs {
   const bf16_t *ln1, *w_qkv, *w_o, *ln2, *w_gu, *w_down;
@@ -56,8 +61,8 @@ struct DecodeLayerArgs {
   uint64_t* stamps;            // diagnostics (nullptr = off): 5 s_memrealtime stamps per task
   int bt_stride, H, nh, nkv, I, bs, nblocks, min_chunk, gc, max_chunks, max_groups;
   float eps, scale_log2;
-  int n_qkv, n_attn, n_o, n_gu, n_down;
-  int gu_groups;  // 16-row groups per gate_up task
+  int n_qkv, n_attn, n_o, n_gu, n_down;  // blocks per step (GEMV steps: workers)
+  int g_qkv, g_o, g_gu, g_down;           // 16-row groups per GEMV step
 };
 
 // Diagnostics: task timeline stamps (100 MHz real-time counter), thread 0 only.
@@ -106,28 +111,38 @@ __device__ __forceinline__ uint32_t dl_signal(uint32_t* ctr) {
   return old;
 }
 
-// Rows [r0, r0 + 16 g) of W[N, K] — g groups of 16 rows, 2 per wave per group — against
-// x = NORM ? bf16(rmsnorm(src) * norm_w) : src, src written in this launch (K bf16, K <= 16 x 512 x
-// 8). The first weight batch (and the norm weights) is requested BEFORE the wait on `dep`; the
-// weights then stream as one double-buffered sequence of (group, K batch) units. `pre` (nullable):
-// 8 bf16 per thread < 2 g loaded write-through right after the wait (the residual rows an epilogue
-// adds to). On return the staging area out[16 g] holds every row's dot product (row r0 + 16 j +
-// 2 w + k at out[16 j + 2 w + k]) and the block has met at a barrier.
-template <bool NORM>
-__device__ __forceinline__ float* dl_gemv(const bf16_t* __restrict__ W, int N, int K, int r0, int g, const WtBuf& xb,
-                                          const bf16_t* src, const bf16_t* __restrict__ norm_w, float eps,
-                                          uint32_t* dep, uint32_t target, int* fault, char* smem, uint64_t* stp,
-                                          const WtBuf* pre_b = nullptr, const bf16_t* pre = nullptr,
-                                          u32x4* pre_v = nullptr) {
+__device__ __forceinline__ uint32_t* dl_ctr(const DecodeLayerArgs& a, int c) { return a.sync + c * kDlLine; }
+
+// A worker of a GEMV step: it takes 16-row groups of W[N, K] from the step's queue (one atomic per
+// group; 2 rows per wave) until the queue is empty, against x = NORM ? bf16(rmsnorm(src) * norm_w)
+// : src (K bf16, written in this launch; staged in LDS once per worker). Its first group's first
+// weight batch (and the norm weights) is requested BEFORE the wait on `dep`, and each group's
+// next group is taken while it streams, so the weights flow as one double-buffered sequence of
+// (group, K batch) units. epi(group, out) stores a finished group (out[2 w + k] = row 16 group +
+// 2 w + k; called by every thread, block-uniformly). The worker finally adds its group count to
+// `done` (write-through stores drained first). Workers that find the queue empty return at once.
+template <bool NORM, typename Epi>
+__device__ __forceinline__ void dl_worker(const bf16_t* __restrict__ W, int K, uint32_t* queue, int n_groups,
+                                          const WtBuf& xb, const bf16_t* src, const bf16_t* __restrict__ norm_w,
+                                          float eps, uint32_t* dep, uint32_t target, uint32_t* done, int* fault,
+                                          char* smem, uint64_t* stp, Epi epi) {
   const int tid = threadIdx.x, wave = tid / kWave, lane = tid % kWave;
   const int nchunk = K / 8;
   constexpr int U = kDlUnroll, STEP = kWave * U;
-  const int iters = (nchunk + STEP - 1) / STEP, n_units = g * iters;
-  auto issue = [&](u32x4 (&d)[2][U], int unit) {
-    const int grp = unit / iters, cb = (unit % iters) * STEP + lane;
-    const int row = min(r0 + 16 * grp + 2 * wave, N - 2);
-    const u32x4* w0 = reinterpret_cast<const u32x4*>(W + static_cast<int64_t>(row) * K);
+  const int iters = (nchunk + STEP - 1) / STEP;
+  bf16_t* xs = reinterpret_cast<bf16_t*>(smem);
+  float* red = reinterpret_cast<float*>(smem + static_cast<size_t>(K) * 2);
+  float* out = red + kDlWaves;
+  int* sg = reinterpret_cast<int*>(out + kDlRows);
+  if (tid == 0) sg[0] = static_cast<int>(__hip_atomic_fetch_add(queue, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+  __syncthreads();
+  int g = sg[0];
+  if (g >= n_groups) return;  // block-uniform
+
+  auto issue = [&](u32x4 (&d)[2][U], int grp, int unit) {
+    const u32x4* w0 = reinterpret_cast<const u32x4*>(W + static_cast<int64_t>(kDlRows * grp + 2 * wave) * K);
     const u32x4* w1 = w0 + nchunk;
+    const int cb = unit * STEP + lane;
 #pragma unroll
     for (int u = 0; u < U; ++u) {
       const int c = min(cb + u * kWave, nchunk - 1);
@@ -136,7 +151,7 @@ __device__ __forceinline__ float* dl_gemv(const bf16_t* __restrict__ W, int N, i
     }
   };
   u32x4 cur[2][U];
-  issue(cur, 0);
+  issue(cur, g, 0);
   u32x4 gw[2];  // norm weights of this thread's x chunks (read-only: before the wait)
   if constexpr (NORM) {
 #pragma unroll
@@ -147,12 +162,6 @@ __device__ __forceinline__ float* dl_gemv(const bf16_t* __restrict__ W, int N, i
   }
   dl_wait(dep, target, fault);
   dl_stamp(stp, 2);
-  if (pre != nullptr && tid < 2 * g) *pre_v = pre_b->ld16(pre + 8 * tid);
-
-  // x -> LDS (normalised if NORM)
-  bf16_t* xs = reinterpret_cast<bf16_t*>(smem);
-  float* red = reinterpret_cast<float*>(smem + static_cast<size_t>(K) * 2);
-  float* out = red + kDlWaves;
   if constexpr (NORM) {
     u32x4 xr[2];
     float ss = 0.f;
@@ -192,75 +201,90 @@ __device__ __forceinline__ float* dl_gemv(const bf16_t* __restrict__ W, int N, i
   __syncthreads();
 
   const u32x4* xv = reinterpret_cast<const u32x4*>(xs);
-  float a0 = 0.f, a1 = 0.f;
-  for (int unit = 0; unit < n_units; ++unit) {
-    u32x4 nxt[2][U];
-    if (unit + 1 < n_units) issue(nxt, unit + 1);
-    const int c0 = (unit % iters) * STEP + lane;
-#pragma unroll
-    for (int u = 0; u < U; ++u) {
-      const int c = c0 + u * kWave;
-      if (c < nchunk) {
-        const u32x4 xx = xv[c];
-        a0 = dot8_bf16(cur[0][u], xx, a0);
-        a1 = dot8_bf16(cur[1][u], xx, a1);
+  int ndone = 0;
+  for (;;) {
+    if (tid == 0) sg[1] = static_cast<int>(__hip_atomic_fetch_add(queue, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+    float a0 = 0.f, a1 = 0.f;
+    int g_next = n_groups;
+    for (int unit = 0; unit < iters; ++unit) {
+      u32x4 nxt[2][U];
+      int gn = g, un = unit + 1;
+      if (unit == iters - 1) {
+        __syncthreads();  // the next group's index (thread 0's atomic has returned)
+        g_next = sg[1];
+        gn = g_next;
+        un = 0;
       }
-    }
-    if (unit % iters == iters - 1) {  // the group's rows are complete
-      const float y0 = wave_sum(a0), y1 = wave_sum(a1);
-      if (lane == 0) {
-        const int o = 16 * (unit / iters) + 2 * wave;
-        out[o] = y0;
-        out[o + 1] = y1;
-      }
-      a0 = a1 = 0.f;
-    }
-    if (unit + 1 < n_units) {
+      const bool more = un < iters || gn < n_groups;  // block-uniform
+      if (more) issue(nxt, gn, un);
+      const int c0 = unit * STEP + lane;
 #pragma unroll
       for (int u = 0; u < U; ++u) {
-        cur[0][u] = nxt[0][u];
-        cur[1][u] = nxt[1][u];
+        const int c = c0 + u * kWave;
+        if (c < nchunk) {
+          const u32x4 xx = xv[c];
+          a0 = dot8_bf16(cur[0][u], xx, a0);
+          a1 = dot8_bf16(cur[1][u], xx, a1);
+        }
+      }
+      if (more) {
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+          cur[0][u] = nxt[0][u];
+          cur[1][u] = nxt[1][u];
+        }
       }
     }
+    const float y0 = wave_sum(a0), y1 = wave_sum(a1);
+    if (lane == 0) {
+      out[2 * wave] = y0;
+      out[2 * wave + 1] = y1;
+    }
+    __syncthreads();
+    epi(g, out);
+    ++ndone;
+    if (g_next >= n_groups) break;
+    g = g_next;
   }
+  dl_stamp(stp, 3);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every storing wave: its write-through stores landed
   __syncthreads();
-  return out;
+  if (tid == 0) __hip_atomic_fetch_add(done, static_cast<uint32_t>(ndone), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  dl_stamp(stp, 4);
 }
 
-// h[r0 .. r0 + 16 g) += out (bf16 residual stream, write-through; old rows preloaded in `old` by
-// threads < 2 g)
-__device__ __forceinline__ void dl_resadd(bf16_t* h, const WtBuf& hb, int r0, int g, const float* out,
-                                          const u32x4& old) {
+// h[r0 .. r0 + 16) += out (bf16 residual stream, write-through read-modify-write by threads 0/1;
+// the rows were last written by this launch's o step or by an earlier launch)
+__device__ __forceinline__ void dl_resadd(bf16_t* h, const WtBuf& hb, int r0, const float* out) {
   const int tid = threadIdx.x;
-  if (tid < 2 * g) {
+  if (tid < 2) {
+    bf16_t* p = h + r0 + 8 * tid;
     float f[8];
-    unpack8(old, f);
+    unpack8(hb.ld16(p), f);
 #pragma unroll
     for (int e = 0; e < 8; ++e) f[e] += out[8 * tid + e];
-    hb.st16(h + r0 + 8 * tid, pack8(f));
+    hb.st16(p, pack8(f));
   }
 }
 
 template <int G, int D>
 __device__ __forceinline__ void dl_qkv(const DecodeLayerArgs& a, int t, char* smem, uint64_t* stp) {
-  const int N = (a.nh + 2 * a.nkv) * D;
-  const int r0 = t * kDlRows;
+  (void)t;
   const WtBuf hb(a.h, a.H * 2);
-  const float* out = dl_gemv<true>(a.w_qkv, N, a.H, r0, 1, hb, a.h, a.ln1, a.eps, nullptr, 0, a.fault, smem, stp);
-  // RoPE of each (2i, 2i + 1) row pair = dims (i, i + D/2) of a Q/K head; V rows stay in order.
-  // A task never straddles heads (D % 16 == 0). Thread 0 stores the first dims of its 8 pairs,
-  // thread 1 the second ones (16 B each, write-through).
-  const int head = r0 / D;
-  constexpr int half = D / 2;
-  const int tid = threadIdx.x;
-  if (tid < 2) {
+  const uint32_t cache_bytes = static_cast<uint32_t>(static_cast<int64_t>(a.nblocks) * a.nkv * a.bs * D * 2);
+  const int slot = a.slots[0], pos = a.positions[0];
+  // RoPE of each (2i, 2i + 1) row pair = dims (i, i + D/2) of a Q/K head; V rows stay in order. A
+  // group never straddles heads (D % 16 == 0). Thread 0 stores the first dims of the group's 8
+  // pairs, thread 1 the second ones (16 B each, write-through).
+  auto epi = [&](int grp, const float* out) {
+    const int r0 = grp * kDlRows, head = r0 / D;
+    constexpr int half = D / 2;
+    const int tid = threadIdx.x;
+    if (tid >= 2) return;
     float f[8];
-    const int slot = a.slots[0];
     const int64_t page = slot / a.bs, off = slot % a.bs;
-    const uint32_t cache_bytes = static_cast<uint32_t>(static_cast<int64_t>(a.nblocks) * a.nkv * a.bs * D * 2);
     if (head < a.nh + a.nkv) {
-      const int ip = (r0 % D) / 2;  // first pair index of the task
-      const int pos = a.positions[0];
+      const int ip = (r0 % D) / 2;
 #pragma unroll
       for (int e = 0; e < 8; ++e) {
         const float c = a.cos_t[static_cast<int64_t>(pos) * half + ip + e];
@@ -281,10 +305,9 @@ __device__ __forceinline__ void dl_qkv(const DecodeLayerArgs& a, int t, char* sm
       WtBuf(a.v_cache, cache_bytes)
           .st16(a.v_cache + ((page * a.nkv + (head - a.nh - a.nkv)) * a.bs + off) * D + d0, pack8(f));
     }
-  }
-  dl_stamp(stp, 3);
-  dl_signal(a.sync + DL_QKV);
-  dl_stamp(stp, 4);
+  };
+  dl_worker<true>(a.w_qkv, a.H, dl_ctr(a, DL_QKV_Q), a.g_qkv, hb, a.h, a.ln1, a.eps, nullptr, 0, dl_ctr(a, DL_QKV),
+                  a.fault, smem, stp, epi);
 }
 
 // Split-KV attention of kv head kvh, balanced key range c of the gc-block grid (attn_decode.hip's
@@ -311,7 +334,7 @@ __device__ __forceinline__ void dl_attn(const DecodeLayerArgs& a, int t, char* s
     pages[i] = min(max(a.block_table[min(p0 + i, a.bt_stride - 1)], 0), a.nblocks - 1);
   const uint32_t cache_bytes = static_cast<uint32_t>(static_cast<int64_t>(a.nblocks) * a.nkv * a.bs * D * 2);
   const WtBuf kb(a.k_cache, cache_bytes), vb(a.v_cache, cache_bytes), qb(a.q, a.nh * D * 2);
-  dl_wait(a.sync + DL_QKV, a.n_qkv, a.fault);
+  dl_wait(dl_ctr(a, DL_QKV), a.g_qkv, a.fault);
   dl_stamp(stp, 2);
   ST st;
   st.init(a.q + kvh * G * D, lane, qb);
@@ -338,66 +361,49 @@ __device__ __forceinline__ void dl_attn(const DecodeLayerArgs& a, int t, char* s
   if (nchunks == 1) {
     store_direct_sc1<G, D, NW>(red, out_row, tid);
     dl_stamp(stp, 3);
-    dl_signal(a.sync + DL_ATTN);
+    dl_signal(dl_ctr(a, DL_ATTN));
     dl_stamp(stp, 4);
     return;
   }
   const bool wrote = publish_and_merge<G, D, NW, true>(red, a.part, ctr, 0, a.nkv, kvh, c, nchunks, a.gc, a.max_chunks,
                                                        a.max_groups, tag, out_row, smem, pages, tid, a.fault);
   dl_stamp(stp, 3);
-  if (wrote) dl_signal(a.sync + DL_ATTN);
+  if (wrote) dl_signal(dl_ctr(a, DL_ATTN));
   dl_stamp(stp, 4);
 }
 
 template <int G, int D>
 __device__ __forceinline__ void dl_o(const DecodeLayerArgs& a, int t, char* smem, uint64_t* stp) {
-  const int r0 = t * kDlRows, K = a.nh * D;
+  (void)t;
+  const int K = a.nh * D;
   const WtBuf hb(a.h, a.H * 2);
-  u32x4 old;
-  // the residual rows were last written by the previous layer's launch: preloaded behind the wait
-  const float* out = dl_gemv<false>(a.w_o, a.H, K, r0, 1, WtBuf(a.attn, K * 2), a.attn, nullptr, 0.f,
-                                    a.sync + DL_ATTN, a.nkv, a.fault, smem, stp, &hb, a.h + r0, &old);
-  dl_resadd(a.h, hb, r0, 1, out, old);
-  dl_stamp(stp, 3);
-  dl_signal(a.sync + DL_O);
-  dl_stamp(stp, 4);
+  auto epi = [&](int grp, const float* out) { dl_resadd(a.h, hb, grp * kDlRows, out); };
+  dl_worker<false>(a.w_o, K, dl_ctr(a, DL_O_Q), a.g_o, WtBuf(a.attn, K * 2), a.attn, nullptr, 0.f,
+                   dl_ctr(a, DL_ATTN), a.nkv, dl_ctr(a, DL_O), a.fault, smem, stp, epi);
 }
 
 __device__ __forceinline__ void dl_gu(const DecodeLayerArgs& a, int t, char* smem, uint64_t* stp) {
-  const int g = a.gu_groups, r0 = t * kDlRows * g;
-  const float* out = dl_gemv<true>(a.w_gu, 2 * a.I, a.H, r0, g, WtBuf(a.h, a.H * 2), a.h, a.ln2, a.eps,
-                                   a.sync + DL_O, a.n_o, a.fault, smem, stp);
-  // rows (2i, 2i + 1) = (gate_i, up_i): 8 act columns per 16-row group, one 16-B store each
-  const int tid = threadIdx.x;
-  if (tid < g) {
-    float f[8];
+  (void)t;
+  const WtBuf actb(a.act, a.I * 2);
+  // rows (2i, 2i + 1) = (gate_i, up_i): 8 act columns per group, one 16-B store
+  auto epi = [&](int grp, const float* out) {
+    if (threadIdx.x == 0) {
+      float f[8];
 #pragma unroll
-    for (int e = 0; e < 8; ++e) f[e] = silu(out[16 * tid + 2 * e]) * out[16 * tid + 2 * e + 1];
-    WtBuf(a.act, a.I * 2).st16(a.act + r0 / 2 + 8 * tid, pack8(f));
-  }
-  dl_stamp(stp, 3);
-  dl_signal(a.sync + DL_GU);
-  dl_stamp(stp, 4);
+      for (int e = 0; e < 8; ++e) f[e] = silu(out[2 * e]) * out[2 * e + 1];
+      actb.st16(a.act + grp * (kDlRows / 2), pack8(f));
+    }
+  };
+  dl_worker<true>(a.w_gu, a.H, dl_ctr(a, DL_GU_Q), a.g_gu, WtBuf(a.h, a.H * 2), a.h, a.ln2, a.eps, dl_ctr(a, DL_O),
+                  a.g_o, dl_ctr(a, DL_GU), a.fault, smem, stp, epi);
 }
 
 __device__ __forceinline__ void dl_down(const DecodeLayerArgs& a, int t, char* smem, uint64_t* stp) {
-  const int r0 = t * kDlRows;
+  (void)t;
   const WtBuf hb(a.h, a.H * 2);
-  u32x4 old;
-  // the residual rows were written by this launch's o tasks (done before any gu task began, so
-  // before this task's wait is over): loaded behind the wait
-  const float* out = dl_gemv<false>(a.w_down, a.H, a.I, r0, 1, WtBuf(a.act, a.I * 2), a.act, nullptr, 0.f,
-                                    a.sync + DL_GU, a.n_gu, a.fault, smem, stp, &hb, a.h + r0, &old);
-  dl_resadd(a.h, hb, r0, 1, out, old);
-  dl_stamp(stp, 3);
-  const uint32_t prev = dl_signal(a.sync + DL_DOWN);
-  dl_stamp(stp, 4);
-  if (threadIdx.x == 0 && prev == static_cast<uint32_t>(a.n_down - 1)) {
-    // the last task of the launch: every block has taken its index and every wait is over
-#pragma unroll
-    for (int w = 0; w < DL_COUNTERS; ++w)
-      __hip_atomic_store(a.sync + w * kDlLine, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  }
+  auto epi = [&](int grp, const float* out) { dl_resadd(a.h, hb, grp * kDlRows, out); };
+  dl_worker<false>(a.w_down, a.I, dl_ctr(a, DL_DOWN_Q), a.g_down, WtBuf(a.act, a.I * 2), a.act, nullptr, 0.f,
+                   dl_ctr(a, DL_GU), a.g_gu, dl_ctr(a, DL_DOWN), a.fault, smem, stp, epi);
 }
 
 template <int G, int D>
@@ -406,7 +412,7 @@ __global__ __launch_bounds__(kDlThreads, 4) void decode_layer_kernel(DecodeLayer
   __shared__ uint32_t s_task;
   const uint64_t t0 = a.stamps != nullptr ? __builtin_amdgcn_s_memrealtime() : 0;
   if (threadIdx.x == 0)
-    s_task = __hip_atomic_fetch_add(a.sync + DL_DISPATCH, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    s_task = __hip_atomic_fetch_add(dl_ctr(a, DL_DISPATCH), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   __syncthreads();
   int t = static_cast<int>(s_task);
   uint64_t* stp = a.stamps != nullptr ? a.stamps + static_cast<int64_t>(t) * 8 : nullptr;
@@ -418,15 +424,27 @@ __global__ __launch_bounds__(kDlThreads, 4) void decode_layer_kernel(DecodeLayer
     asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
     stp[7] = xcc;
   }
-  if (t < a.n_qkv) return dl_qkv<G, D>(a, t, smem, stp);
-  t -= a.n_qkv;
-  if (t < a.n_attn) return dl_attn<G, D>(a, t, smem, stp);
-  t -= a.n_attn;
-  if (t < a.n_o) return dl_o<G, D>(a, t, smem, stp);
-  t -= a.n_o;
-  if (t < a.n_gu) return dl_gu(a, t, smem, stp);
-  t -= a.n_gu;
-  if (t < a.n_down) return dl_down(a, t, smem, stp);
+  if (t < a.n_qkv) {
+    dl_qkv<G, D>(a, t, smem, stp);
+  } else if ((t -= a.n_qkv) < a.n_attn) {
+    dl_attn<G, D>(a, t, smem, stp);
+  } else if ((t -= a.n_attn) < a.n_o) {
+    dl_o<G, D>(a, t, smem, stp);
+  } else if ((t -= a.n_o) < a.n_gu) {
+    dl_gu(a, t, smem, stp);
+  } else if ((t -= a.n_gu) < a.n_down) {
+    dl_down(a, t, smem, stp);
+  }
+  // the block's last counter access: the block whose exit is the grid's last re-arms every counter
+  // (no other block touches one afterwards) for the next launch
+  if (threadIdx.x == 0) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this block's counter adds have landed
+    const uint32_t total = static_cast<uint32_t>(a.n_qkv + a.n_attn + a.n_o + a.n_gu + a.n_down);
+    if (__hip_atomic_fetch_add(dl_ctr(a, DL_EXIT), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == total - 1) {
+#pragma unroll
+      for (int w = 0; w < DL_COUNTERS; ++w) __hip_atomic_store(dl_ctr(a, w), 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+  }
 }
 
 template <int G, int D>
@@ -454,7 +472,7 @@ extern "C" int llmc_attn_decode_groups(int max_chunks);
 
 // One decode layer for ONE row (see the header). gc <= 32 balanced attention blocks per kv head of
 // >= min_chunk keys (a multiple of 32); max_chunks / part / attn_ctr: the attn_decode workspace
-// (max_chunks >= gc). sync: DL_WORDS (512) uint32 words, zeroed once (each launch leaves them zero).
+// (max_chunks >= gc). sync: DL_WORDS (1024) uint32 words, zeroed once (each launch leaves them zero).
 extern "C" int llmc_decode_layer(const void* ln1, const void* w_qkv, const void* w_o, const void* ln2, const void* w_gu,
                                  const void* w_down, void* k_cache, void* v_cache, const void* positions,
                                  const void* slots, const void* seq_lens, const void* block_table, int bt_stride,
@@ -505,25 +523,23 @@ extern "C" int llmc_decode_layer(const void* ln1, const void* w_qkv, const void*
   a.max_groups = llmc_attn_decode_groups(max_chunks);
   a.eps = eps;
   a.scale_log2 = scale * 1.4426950408889634f;
-  a.n_qkv = (nh + 2 * nkv) * D / kDlRows;
+  a.g_qkv = (nh + 2 * nkv) * D / kDlRows;
+  a.g_o = H / kDlRows;
+  a.g_gu = 2 * I / kDlRows;
+  a.g_down = H / kDlRows;
+  // workers per GEMV step: about one per CU (the queue balances them); attention: one block per
+  // (kv head, balanced key range)
+  auto workers = [](int groups) { return groups < 256 ? groups : 256; };
+  a.n_qkv = workers(a.g_qkv);
   a.n_attn = nkv * gc;
-  a.n_o = H / kDlRows;
-  // gate_up: several 16-row groups per task while >= 256 tasks remain (one x image and one set of
-  // per-task overheads for up to 8 groups)
-  const int gu_rows = 2 * I / kDlRows;
-  a.gu_groups = 1;
-  for (int gg = 8; gg > 1; --gg)
-    if (gu_rows % gg == 0 && gu_rows / gg >= 256) {
-      a.gu_groups = gg;
-      break;
-    }
-  a.n_gu = gu_rows / a.gu_groups;
-  a.n_down = H / kDlRows;
+  a.n_o = workers(a.g_o);
+  a.n_gu = workers(a.g_gu);
+  a.n_down = workers(a.g_down);
   const int G = nh / nkv;
   // LDS: the largest of a GEMV's x image (+ reduction / staging words) and attention's 8 V images
   // + page ids of the longest balanced range (the wave states reuse the V images)
   const int kmax = H > I ? (H > nh * D ? H : nh * D) : (I > nh * D ? I : nh * D);
-  const size_t gemv_lds = static_cast<size_t>(kmax) * 2 + (kDlWaves + 8 * kDlRows) * sizeof(float);
+  const size_t gemv_lds = static_cast<size_t>(kmax) * 2 + (kDlWaves + kDlRows + 2) * sizeof(float);
   const int units = (bt_stride * bs + 31) / 32;
   const int max_range = 32 * ((units + gc - 1) / gc) + 32;
   const size_t attn_lds = static_cast<size_t>(kDlWaves) * 32 * kVRowBytes +

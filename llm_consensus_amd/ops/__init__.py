@@ -222,7 +222,7 @@ def attn_decode(q, k_cache, v_cache, block_tables, seq_lens, out, part, counters
 
 
 DECODE_LAYER_MIN_CHUNK = 256  # fused decode layer: keys per attention block at least (8 waves x 32)
-DECODE_LAYER_SYNC_WORDS = 512  # its step counters, one 256-B line each
+DECODE_LAYER_SYNC_WORDS = 1024  # its step counters, one 256-B line each
 
 
 def decode_layer_grid(ctx_cap: int) -> int:

@@ -151,16 +151,30 @@ def visible_gpu_count() -> int:
                     k, _, v = line.partition(" ")
                     if k == "drm_render_minor":
                         minor = int(v)
-            if minor is None or not os.access(f"/dev/dri/renderD{minor}", os.R_OK | os.W_OK):
+            if minor is None:
                 continue
+            # open, not os.access: a device-cgroup denial only shows when the node is opened
+            fd = os.open(f"/dev/dri/renderD{minor}", os.O_RDWR | os.O_CLOEXEC)
+            os.close(fd)
             n += 1
         except (OSError, ValueError):
             continue
     for var in ("ROCR_VISIBLE_DEVICES", "HIP_VISIBLE_DEVICES", "CUDA_VISIBLE_DEVICES"):
         v = os.environ.get(var)
-        if v is not None:
-            ids = [x for x in v.split(",") if x.strip() != ""]
-            n = min(n, len(ids))
+        if v is None:
+            continue
+        # the runtime keeps the leading valid device indices and stops at the first invalid one
+        # ("-1" hides every GPU); non-index forms (UUIDs) are the runtime's to resolve: ask it
+        kept = 0
+        for x in (t.strip() for t in v.split(",")):
+            if x == "":
+                continue
+            if not x.lstrip("-").isdigit():
+                return -1
+            if not 0 <= int(x) < n:
+                break
+            kept += 1
+        n = min(n, kept)
     return n
 
 

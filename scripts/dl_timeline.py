@@ -35,9 +35,12 @@ torch.cuda.synchronize()
 bucket = e._bucket(s.length + 8)
 gc = e.layer_gc[bucket]
 nh, nkv, D, H, I = e.nh, e.nkv, e.D, cfg.hidden, e.w.inter
-gu_rows = 2 * I // 16
-gu_g = next((g for g in range(8, 1, -1) if gu_rows % g == 0 and gu_rows // g >= 256), 1)  # as the kernel
-counts = {"qkv": (nh + 2 * nkv) * D // 16, "attn": nkv * gc, "o": H // 16, "gu": gu_rows // gu_g, "down": H // 16}
+def workers(groups):  # as the kernel: about one worker per CU per GEMV step
+    return min(groups, 256)
+
+
+counts = {"qkv": workers((nh + 2 * nkv) * D // 16), "attn": nkv * gc, "o": workers(H // 16),
+          "gu": workers(2 * I // 16), "down": workers(H // 16)}
 ntask = sum(counts.values())
 st = torch.zeros(ntask, 8, dtype=torch.int64, device="cuda")
 Lw = e.w.layers[0]

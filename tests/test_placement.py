@@ -144,14 +144,28 @@ def test_visible_gpu_count_from_kfd_topology(tmp_path, monkeypatch):
         (d / "gpu_id").write_text(f"{gid}\n")
         (d / "properties").write_text("cpu_cores_count 0\n" + (f"drm_render_minor {minor}\n" if minor else ""))
     monkeypatch.setattr(placement, "_KFD_NODES", str(tmp_path))
-    real_access = os.access
-    monkeypatch.setattr(placement.os, "access",
-                        lambda p, m: p in ("/dev/dri/renderD128", "/dev/dri/renderD129") or real_access(p, m) and False)
+    real_open = os.open
+
+    def fake_open(p, flags, *a):  # renderD130 is denied (e.g. by the device cgroup): open fails
+        if p in ("/dev/dri/renderD128", "/dev/dri/renderD129"):
+            return real_open(os.devnull, os.O_RDONLY)
+        if p.startswith("/dev/dri/"):
+            raise PermissionError(p)
+        return real_open(p, flags, *a)
+
+    monkeypatch.setattr(placement.os, "open", fake_open)
     for var in ("ROCR_VISIBLE_DEVICES", "HIP_VISIBLE_DEVICES", "CUDA_VISIBLE_DEVICES"):
         monkeypatch.delenv(var, raising=False)
     assert placement.visible_gpu_count() == 2
     assert placement.default_gpus() == [0, 1]
     monkeypatch.setenv("HIP_VISIBLE_DEVICES", "1")
     assert placement.visible_gpu_count() == 1
+    monkeypatch.setenv("HIP_VISIBLE_DEVICES", "-1")  # hides every GPU
+    assert placement.visible_gpu_count() == 0
+    monkeypatch.setenv("HIP_VISIBLE_DEVICES", "1,7,0")  # the runtime stops at the invalid index 7
+    assert placement.visible_gpu_count() == 1
+    monkeypatch.setenv("HIP_VISIBLE_DEVICES", "GPU-1234abcd")  # a UUID: the runtime resolves it
+    assert placement.visible_gpu_count() == -1
+    monkeypatch.delenv("HIP_VISIBLE_DEVICES")
     monkeypatch.setattr(placement, "_KFD_NODES", str(tmp_path / "missing"))
     assert placement.visible_gpu_count() == -1

@@ -208,14 +208,17 @@ __device__ __forceinline__ void dl_worker(const bf16_t* __restrict__ W, int K, u
     int g_next = n_groups;
     for (int unit = 0; unit < iters; ++unit) {
       u32x4 nxt[2][U];
+      const bool last = unit == iters - 1;
       int gn = g, un = unit + 1;
-      if (unit == iters - 1) {
+      if (last) {
         __syncthreads();  // the next group's index (thread 0's atomic has returned)
         g_next = sg[1];
         gn = g_next;
         un = 0;
       }
-      const bool more = un < iters || gn < n_groups;  // block-uniform
+      // within the group: the next K batch; after its last batch: the next group's first batch,
+      // only if there is one (a past-the-end group index must never become an address)
+      const bool more = !last || g_next < n_groups;  // block-uniform
       if (more) issue(nxt, gn, un);
       const int c0 = unit * STEP + lane;
 #pragma unroll

@@ -243,7 +243,7 @@ def softmax_scale(D: int) -> float:
 # -- whole-model reference forward (tests) ------------------------------------------------------
 @torch.no_grad()
 def reference_logits(w, cfg, ids, out_pos, cos_t: torch.Tensor, sin_t: torch.Tensor, chunk: int = 1024,
-                     attn_chunk: int = 512) -> torch.Tensor:
+                     attn_chunk: int = 512, p_bf16: bool = False) -> torch.Tensor:
     """fp32 PyTorch forward of a ``TransformerWeights`` model (one TP=1 model or one rank's shard
     standing alone) over the token sequence ``ids``: the last-layer logits [len(out_pos), V_local]
     f32 at positions ``out_pos``. Every matmul, norm, RoPE, softmax and SiLU is fp32; activations
@@ -252,7 +252,8 @@ def reference_logits(w, cfg, ids, out_pos, cos_t: torch.Tensor, sin_t: torch.Ten
     full precision — the oracle of the full-depth teacher-forced decode tests. Runs on the
     weights' device (the GPU for full-size models: fp32 copies are made one weight at a time),
     in ``chunk``-token slices for the projections and ``attn_chunk``-query slices for causal
-    attention over the whole sequence."""
+    attention over the whole sequence. ``p_bf16``: round the attention probabilities to bf16
+    before the P.V product, as the MFMA attention kernels do (their row sums stay f32)."""
     dev = w.embed.device
     bf, f32 = torch.bfloat16, torch.float32
     T = len(ids)
@@ -283,10 +284,16 @@ def reference_logits(w, cfg, ids, out_pos, cos_t: torch.Tensor, sin_t: torch.Ten
             s = torch.einsum("qkgd,tkd->kgqt", qc, k[:q1]) * scale         # keys 0..q1-1
             mask = torch.arange(q1, device=dev).view(1, -1) > torch.arange(q0, q1, device=dev).view(-1, 1)
             s.masked_fill_(mask, float("-inf"))
-            p = torch.softmax(s, dim=-1)
-            o = torch.einsum("kgqt,tkd->qkgd", p, v[:q1])
+            if p_bf16:
+                e = torch.exp(s - s.amax(-1, keepdim=True))
+                o = torch.einsum("kgqt,tkd->qkgd", e.to(bf).float(), v[:q1]) / e.sum(-1).permute(2, 0, 1).unsqueeze(-1)
+                del e
+            else:
+                p = torch.softmax(s, dim=-1)
+                o = torch.einsum("kgqt,tkd->qkgd", p, v[:q1])
+                del p
             attn[q0:q1] = o.reshape(q1 - q0, nh * D).to(bf)
-            del s, p, o
+            del s, o
         h = (h.float() + lin(attn, L.w_o)).to(bf)
         xn = rmsnorm(h, L.ln2, cfg.rms_eps)
         if cfg.is_moe:

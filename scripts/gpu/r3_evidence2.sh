@@ -1,0 +1,8 @@
+# Second half of scripts/gpu/r3_evidence.sh: full-size numerics, Mixtral 8k prefill profile, shard profiles.
+set -o pipefail
+cd $GRAFT_REPO_ROOT
+tag=${1:-ev}
+mkdir -p gpurun_out
+timeout -k 10 500 python -u -m pytest tests/test_numerics_full_gpu.py -v -s --timeout 400 --timeout-method thread > gpurun_out/${tag}_numerics.log 2>&1 ; \
+bash scripts/prof_decode.sh ${tag}_mixtral_8k --model mixtral-8x7b --prompt 8192 --ctx 8704 --tokens 64 && \
+bash scripts/gpu/shards.sh ${tag}

@@ -24,7 +24,7 @@ int llmc_gemv(int, const void*, int, const void*, float, const void*, void*, int
 int llmc_gemvm(int, const void*, int, const void*, float, const void*, void*, int, int, int, int, int, hipStream_t);
 int llmc_moe_gemvm(int, const void*, int, const void*, float, const void*, const void*, int, int, void*, int, int, int,
                    int, hipStream_t);
-int llmc_gemm(const void*, int, const void*, int, void*, int, int, int, int, int, int, hipStream_t);
+int llmc_gemm(const void*, int, const void*, int, void*, int, int, int, int, int, hipStream_t);
 int llmc_rope_kv_write(const void*, int, void*, int, const void*, const void*, const void*, void*, void*, const void*,
                        int, int, int, int, int, hipStream_t);
 int llmc_decode_layer(const void*, const void*, const void*, const void*, const void*, const void*, void*, void*,
@@ -102,8 +102,8 @@ PYBIND11_MODULE(_llmc_hip, m) {
                     ptr s) {
     check(llmc_gemvm(M, P(x), xs, P(nw), eps, P(W), P(out), os, N, K, epi, form, S(s)), "gemvm");
   });
-  m.def("gemm", [](ptr A, int lda, ptr W, int ldw, ptr C, int ldc, int M, int N, int K, int epi, int variant, ptr s) {
-    check(llmc_gemm(P(A), lda, P(W), ldw, P(C), ldc, M, N, K, epi, variant, S(s)), "gemm");
+  m.def("gemm", [](ptr A, int lda, ptr W, int ldw, ptr C, int ldc, int M, int N, int K, int epi, ptr s) {
+    check(llmc_gemm(P(A), lda, P(W), ldw, P(C), ldc, M, N, K, epi, S(s)), "gemm");
   });
   m.def("rope_kv_write", [](ptr qkv, int qs, ptr qo, int qos, ptr pos, ptr cos_t, ptr sin_t, ptr kc, ptr vc,
                             ptr slots, int T, int nh, int nkv, int D, int bs, ptr s) {

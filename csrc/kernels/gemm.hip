@@ -184,12 +184,11 @@ __global__ __launch_bounds__(256, 2) void gemm_kernel(const bf16_t* __restrict__
 //  * grid: bijective XCD remap (T1) then grouped tile order (8 M-tiles x all N per group).
 //  * fused epilogues: bf16 | f32 | residual add (C += A.W^T) | SiLU-mul of interleaved gate/up
 //    columns (C[m][n/2] = silu(g) * u).
-// Measured (MI355X, random bf16; profiles/r2_prefill_gemm.md): 1.26-1.40 PF/s on the Llama-3-8B
-// prefill shapes, 83-87 % of hipBLASLt on the same data (PMC: hipBLASLt runs 4 waves x 128 x 128
+// Measured (MI355X, random bf16; profiles/r3_gemm_4wave_ab.md): 1.33-1.41 PF/s on the Llama-3-8B
+// prefill shapes with the LDS-staged dwordx4 epilogue (r2: 1.26-1.40), 86-88 % of hipBLASLt (PMC: hipBLASLt runs 4 waves x 128 x 128
 // with 512 registers each and 1.5x fewer LDS reads; this 8-wave layout parks waves at barriers).
-// A 4-wave 128 x 128-per-wave form of this kernel (5-slice 32-K LDS-DMA ring, one barrier per
-// slice, fragments double-buffered, accumulators split over VGPRs/AGPRs by hipcc) measured
-// 0.92-1.00 PF/s on the same shapes and was dropped.
+// 4-wave 128 x 128-per-wave forms (AGPR accumulators, one barrier per 32- or 64-K step) measured
+// 1.09-1.19 PF/s on the same shapes and were dropped (profiles/r3_gemm_4wave_ab.md).
 constexpr int kT = 256, kTK = 64;
 constexpr int kQuarter = 128 * kTK * 2;  // bytes
 constexpr int kSlots = 10;
@@ -258,6 +257,59 @@ __device__ __forceinline__ void gemm256_epilogue(const f32x4 (&acc)[8][4], void*
     if (m >= M) continue;
 #pragma unroll
     for (int ni = 0; ni < 4; ++ni) store4<EPI>(C, ldc, N, m, n0 + wc * 64 + ni * 16 + 4 * lg, acc[mi][ni], vec_ok);
+  }
+}
+
+// bf16 epilogue through LDS (EPI 0 with N % 8 == 0, EPI 3 with N % 16 == 0; the residual add keeps the direct form, which
+// rounds acc + old once): each wave's 128 x 64 output block (128 x 32
+// for the SiLU-mul) is written to its own 16 KiB of the (drained) staging ring as 8-byte pieces
+// (4-byte for SiLU) and read back as 16-byte row chunks, so the global stores are dwordx4 covering
+// whole 128-byte (64-byte) row segments: half (a quarter of) the store instructions of the direct
+// 8-byte form. LDS image [128][OW] bf16 with the 16-byte chunk index XORed by row bits (conflict-
+// free writes and reads); only the wave's own region is touched, so one wave-local wait suffices
+// between the two passes.
+template <int EPI>
+__device__ __forceinline__ void gemm256_epilogue_lds(const f32x4 (&acc)[8][4], char* smem, void* __restrict__ C, int ldc,
+                                                     int M, int N, int m0, int n0, int wave, int wr, int wc, int lane,
+                                                     int l16, int lg) {
+  constexpr int OW = EPI == 3 ? 32 : 64;  // output columns per wave
+  constexpr int RB = OW * 2;              // bytes per LDS row
+  constexpr int CPR = RB / 16;            // 16-byte chunks per row (8 or 4)
+  char* img = smem + wave * 128 * RB;
+  auto sw = [&](int r, int chunk) { return r * RB + ((chunk ^ ((r >> 1) & (CPR - 1))) << 4); };
+  // all waves are past their last ring read (the caller's final barrier) and every LDS-DMA landed
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+#pragma unroll
+  for (int mi = 0; mi < 8; ++mi) {
+    const int r = mi * 16 + l16;
+#pragma unroll
+    for (int ni = 0; ni < 4; ++ni) {
+      const f32x4& v = acc[mi][ni];
+      if constexpr (EPI == 3) {  // columns ni * 16 + 4 lg .. + 3 -> outputs ni * 8 + 2 lg, + 1 (4 bytes)
+        const float o0 = v[0] / (1.f + __expf(-v[0])) * v[1], o1 = v[2] / (1.f + __expf(-v[2])) * v[3];
+        const int ob = (ni * 8 + 2 * lg) * 2;
+        *reinterpret_cast<uint32_t*>(img + sw(r, ob >> 4) + (ob & 15)) = pack_bf16x2(o0, o1);
+      } else {  // columns ni * 16 + 4 lg .. + 3 (8 bytes)
+        const int ob = (ni * 16 + 4 * lg) * 2;
+        *reinterpret_cast<u32x2*>(img + sw(r, ob >> 4) + (ob & 15)) =
+            u32x2{pack_bf16x2(v[0], v[1]), pack_bf16x2(v[2], v[3])};
+      }
+    }
+  }
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // this wave's writes done (wave-local image)
+  constexpr int RPI = 64 / CPR;  // rows per wave instruction
+  const int rr = lane / CPR, ch = lane % CPR;
+  const int n_out = EPI == 3 ? N / 2 : N;
+  const int col = (EPI == 3 ? n0 / 2 : n0) + wc * OW + ch * 8;
+  if (col >= n_out) return;  // n_out % 8 == 0: a chunk is all in or all out
+#pragma unroll
+  for (int it = 0; it < 128 / RPI; ++it) {
+    const int r = it * RPI + rr;
+    const int m = m0 + wr * 128 + r;
+    if (m >= M) break;
+    const uint4 d = *reinterpret_cast<const uint4*>(img + sw(r, ch));
+    *reinterpret_cast<uint4*>(reinterpret_cast<bf16_t*>(C) + static_cast<int64_t>(m) * ldc + col) = d;
   }
 }
 
@@ -419,141 +471,10 @@ __global__ __launch_bounds__(512, 1) void gemm256_kernel(const bf16_t* __restric
 #pragma unroll
       for (int ni = 0; ni < 4; ++ni) store4<EPI>(C, ldc, N, m, n0 + wc * 64 + ni * 16 + 4 * lg, acc[mi][ni], vec_ok);
     }
+  } else if ((EPI == 0 || EPI == 3) && N % (EPI == 3 ? 16 : 8) == 0 && ldc % 8 == 0) {
+    gemm256_epilogue_lds<EPI>(acc, smem, C, ldc, M, N, m0, n0, wave, wr, wc, lane, l16, lg);
   } else {
     gemm256_epilogue<EPI>(acc, C, ldc, M, N, m0, n0, wr, wc, l16, lg);
-  }
-}
-
-// ---------------------------------------------------------------------------------------------
-// 4-wave form of the dense prefill GEMM (one wave per SIMD, as hipBLASLt's MT256x256x64 kernel
-// runs): 256 x 256 tile, 2 x 2 waves of 128 x 128 = 8 x 8 tiles of mfma_f32_16x16x32_bf16 (operands
-// swapped as in gemm256_kernel: lane (l16, lg) ends with C[m][n .. n + 3]). The 256 accumulators
-// live in AGPRs and feed every MFMA directly (a[...] operands, no copies in the loop); the operand
-// fragments are read per step (double-buffering them in VGPRs spills: 256 AGPRs + 2 x 64 VGPRs of
-// fragments leave too little for addresses). K advances in 32-deep steps through a 4-slot LDS ring
-// (A 256 x 32 + W 256 x 32 per slot, 32 KiB) filled by LDS-DMA three steps ahead; ONE barrier per
-// step: it publishes step kt's slot (every wave's own pieces waited for by a counted vmcnt) and
-// retires the slot the next fill overwrites. Same XCD-bijective grouped tile order and epilogues as
-// gemm256_kernel.
-constexpr int kT4 = 256, kBK4 = 32, kSlot4 = 2 * kT4 * kBK4 * 2, kNS4 = 4;
-
-__device__ __forceinline__ int off4(int r, int c) { return r * (kBK4 * 2) + ((c ^ ((r >> 1) & 3)) << 4); }
-
-template <int EPI, bool DB>
-__global__ __launch_bounds__(256, 1) void gemm4w_kernel(const bf16_t* __restrict__ A, int lda,
-                                                        const bf16_t* __restrict__ W, int ldw, void* __restrict__ C,
-                                                        int ldc, int M, int N, int K) {
-  constexpr int NS = DB ? 5 : kNS4;  // DB: 5 x 32 KiB = all 160 KiB of LDS
-  __shared__ __attribute__((aligned(16))) char smem[NS * kSlot4];
-  const int num_m = (M + kT4 - 1) / kT4, num_n = (N + kT4 - 1) / kT4;
-  const int id = xcd_remap(blockIdx.x, num_m * num_n);
-  const int group = id / (kGroupM * num_n);
-  const int first_m = group * kGroupM;
-  const int gsz = min(num_m - first_m, kGroupM);
-  const int in_group = id - group * kGroupM * num_n;
-  const int m0 = (first_m + in_group % gsz) * kT4, n0 = (in_group / gsz) * kT4;
-  const int tid = threadIdx.x, lane = tid & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int wr = wave >> 1, wc = wave & 1;
-  const int l16 = lane & 15, lg = lane >> 4;
-  const int rowsA = min(kT4, M - m0), rowsW = min(kT4, N - n0);
-  const __amdgpu_buffer_rsrc_t rsA = __builtin_amdgcn_make_buffer_rsrc(
-      (void*)(A + static_cast<int64_t>(m0) * lda), 0, rowsA * lda * 2, 0x00020000);
-  const __amdgpu_buffer_rsrc_t rsW = __builtin_amdgcn_make_buffer_rsrc(
-      (void*)(W + static_cast<int64_t>(n0) * ldw), 0, rowsW * ldw * 2, 0x00020000);
-  // per slot and operand: 256 rows x 64 B = 1024 pieces of 16 B, 4 per thread; the LDS image is
-  // lane-linear, so the XOR swizzle goes on the per-lane SOURCE offset (rows clamped)
-  uint32_t va[4], vw[4];
-#pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    const int p = i * 256 + tid;
-    const int r = p >> 2, c = (p & 3) ^ ((r >> 1) & 3);
-    va[i] = static_cast<uint32_t>((min(r, rowsA - 1) * lda + c * 8) * 2);
-    vw[i] = static_cast<uint32_t>((min(r, rowsW - 1) * ldw + c * 8) * 2);
-  }
-  const int nk = K / kBK4;
-  auto stage = [&](int kt) {
-    char* sl = smem + (kt % NS) * kSlot4 + wave * 64 * 16;
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(rsA, (__attribute__((address_space(3))) void*)(sl + i * 256 * 16), 16,
-                                               va[i], kt * kBK4 * 2, 0, 0);
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(rsW, (__attribute__((address_space(3))) void*)(sl + kSlot4 / 2 + i * 256 * 16),
-                                               16, vw[i], kt * kBK4 * 2, 0, 0);
-    }
-  };
-  f32x4 acc[8][8];
-#pragma unroll
-  for (int a = 0; a < 8; ++a)
-#pragma unroll
-    for (int b = 0; b < 8; ++b) acc[a][b] = f32x4{0.f, 0.f, 0.f, 0.f};
-  for (int kt = 0; kt < 3 && kt < nk; ++kt) stage(kt);
-  // this wave's pieces of slot kt landed (steps kt + 1 and kt + 2 may still fly: 8 pieces each);
-  // the barrier publishes everyone's and retires slot kt - 1, which the next fill overwrites
-#define LLMC_G4_SYNC(KT)                                \
-  {                                                     \
-    if ((KT) + 2 < nk) {                                \
-      asm volatile("s_waitcnt vmcnt(16)" ::: "memory"); \
-    } else {                                            \
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  \
-    }                                                   \
-    __builtin_amdgcn_s_barrier();                       \
-    if ((KT) + 3 < nk) stage((KT) + 3);                 \
-  }
-#define LLMC_G4_READ(KT, AF, BW)                                                          \
-  {                                                                                       \
-    const char* sa_ = smem + ((KT) % NS) * kSlot4;                                        \
-    const char* sw_ = sa_ + kSlot4 / 2;                                                   \
-    _Pragma("unroll") for (int i = 0; i < 8; ++i) {                                       \
-      BW[i] = *reinterpret_cast<const bf16x8*>(sw_ + off4(wc * 128 + i * 16 + l16, lg)); \
-      AF[i] = *reinterpret_cast<const bf16x8*>(sa_ + off4(wr * 128 + i * 16 + l16, lg)); \
-    }                                                                                     \
-  }
-#define LLMC_G4_MMA(AF, BW)                                                                            \
-  _Pragma("unroll") for (int mi = 0; mi < 8; ++mi) _Pragma("unroll") for (int ni = 0; ni < 8; ++ni) \
-      acc[mi][ni] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(BW[ni], AF[mi], acc[mi][ni], 0, 0, 0);
-  if constexpr (!DB) {
-    // fragments read per step, all 16 reads issued before the first MFMA (sched_barrier: hipcc
-    // otherwise sinks each A read to its use and waits out the LDS latency 8 times a step)
-    for (int kt = 0; kt < nk; ++kt) {
-      LLMC_G4_SYNC(kt)
-      bf16x8 af[8], bw[8];
-      LLMC_G4_READ(kt, af, bw)
-      __builtin_amdgcn_sched_barrier(0);
-      LLMC_G4_MMA(af, bw)
-    }
-  } else {
-    // 64-deep steps over two ring slots: both slots' 32 fragment reads issue at once (two named
-    // sets, nothing carried across iterations), the first slot's 64 MFMAs run while the second
-    // slot's reads land. 5-slot ring: after step j's barrier, slots 2j + 3 and 2j + 4 refill the
-    // two slots step j - 1 consumed (their reads retired before this barrier).
-    bf16x8 afA[8], bwA[8], afB[8], bwB[8];
-    for (int kt = 0; kt < nk; kt += 2) {
-      if (kt + 2 < nk) {  // slots kt, kt + 1 landed; kt + 2 (8 pieces) may still fly
-        asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
-      } else {
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      }
-      __builtin_amdgcn_s_barrier();
-      if (kt + 3 < nk) stage(kt + 3);
-      if (kt + 4 < nk) stage(kt + 4);
-      LLMC_G4_READ(kt, afA, bwA)
-      LLMC_G4_READ(kt + 1, afB, bwB)
-      __builtin_amdgcn_sched_barrier(0);
-      LLMC_G4_MMA(afA, bwA)
-      LLMC_G4_MMA(afB, bwB)
-    }
-  }
-#undef LLMC_G4_MMA
-#undef LLMC_G4_READ
-#undef LLMC_G4_SYNC
-  const bool vec_ok = (N % 4 == 0) && (ldc % 4 == 0);
-#pragma unroll
-  for (int mi = 0; mi < 8; ++mi) {
-    const int m = m0 + wr * 128 + mi * 16 + l16;
-    if (m >= M) continue;
-#pragma unroll
-    for (int ni = 0; ni < 8; ++ni) store4<EPI>(C, ldc, N, m, n0 + wc * 128 + ni * 16 + 4 * lg, acc[mi][ni], vec_ok);
   }
 }
 
@@ -564,28 +485,12 @@ using namespace llmc;
 // C[M, N] (+)= A[M, K] . W[N, K]^T. epi: 0 bf16, 1 f32, 2 C += (bf16), 3 SiLU-mul of interleaved
 // gate/up columns into C[M, N / 2] (bf16). K must be a multiple of 64, lda/ldw multiples of 8.
 extern "C" int llmc_gemm(const void* A, int lda, const void* W, int ldw, void* C, int ldc, int M, int N, int K,
-                         int epi, int variant, hipStream_t s) {
+                         int epi, hipStream_t s) {
   if (K % kTK != 0 || M <= 0 || N <= 0 || K <= 0 || (epi == 3 && N % 2 != 0)) return -1;
   if (lda % 8 != 0 || ldw % 8 != 0) return -1;  // 16-B aligned rows for the LDS-DMA
   // buffer offsets inside one 256-row tile must stay below 2^31 bytes
   if (static_cast<int64_t>(kT) * lda * 2 >= (1ll << 31) || static_cast<int64_t>(kT) * ldw * 2 >= (1ll << 31)) return -1;
   const int nwg = ((M + kT - 1) / kT) * ((N + kT - 1) / kT);
-  if (variant == 1 || variant == 2) {  // the 4-wave form (2: double-buffered fragments)
-#define LLMC_G4_LAUNCH(E)                                                                                 \
-  if (variant == 1)                                                                                       \
-    gemm4w_kernel<E, false><<<nwg, 256, 0, s>>>((const bf16_t*)A, lda, (const bf16_t*)W, ldw, C, ldc, M, N, K); \
-  else                                                                                                    \
-    gemm4w_kernel<E, true><<<nwg, 256, 0, s>>>((const bf16_t*)A, lda, (const bf16_t*)W, ldw, C, ldc, M, N, K)
-    switch (epi) {
-      case 0: LLMC_G4_LAUNCH(0); break;
-      case 1: LLMC_G4_LAUNCH(1); break;
-      case 2: LLMC_G4_LAUNCH(2); break;
-      case 3: LLMC_G4_LAUNCH(3); break;
-      default: return -2;
-    }
-#undef LLMC_G4_LAUNCH
-    return static_cast<int>(hipGetLastError());
-  }
   switch (epi) {
     case 0: gemm256_kernel<0><<<nwg, 512, 0, s>>>((const bf16_t*)A, lda, (const bf16_t*)W, ldw, C, ldc, M, N, K); break;
     case 1: gemm256_kernel<1><<<nwg, 512, 0, s>>>((const bf16_t*)A, lda, (const bf16_t*)W, ldw, C, ldc, M, N, K); break;

@@ -100,16 +100,12 @@ def linear(x: torch.Tensor, W: torch.Tensor, epi: int = EPI_BF16, out: Optional[
         return out
     if norm_w is not None:
         x = rmsnorm(x, norm_w, eps)
-    kernels().gemm(_p(x), x.stride(0), _p(W), W.stride(0), _p(out), out.stride(0), M, N, K, epi, GEMM_VARIANT, _s(x))
+    kernels().gemm(_p(x), x.stride(0), _p(W), W.stride(0), _p(out), out.stride(0), M, N, K, epi, _s(x))
     return out
 
 
-GEMM_VARIANT = 0  # prefill GEMM body: 0 = 8-wave ping-pong (gemm256_kernel), 1 = 4-wave (gemm4w_kernel)
-
-
-def gemm(x: torch.Tensor, W: torch.Tensor, epi: int = EPI_BF16, out: Optional[torch.Tensor] = None,
-         variant: Optional[int] = None) -> torch.Tensor:
-    """Always the MFMA GEMM path (tests / microbenchmarks; ``variant`` pins a body)."""
+def gemm(x: torch.Tensor, W: torch.Tensor, epi: int = EPI_BF16, out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """Always the MFMA GEMM path (tests / microbenchmarks)."""
     if not x.is_cuda:
         return oracle.linear(x, W, epi, out)
     M, K = x.shape
@@ -117,8 +113,7 @@ def gemm(x: torch.Tensor, W: torch.Tensor, epi: int = EPI_BF16, out: Optional[to
     if out is None:
         n_out = N // 2 if epi == EPI_SILU else N
         out = torch.empty(M, n_out, dtype=torch.float32 if epi == EPI_F32 else torch.bfloat16, device=x.device)
-    kernels().gemm(_p(x), x.stride(0), _p(W), W.stride(0), _p(out), out.stride(0), M, N, K, epi,
-                   GEMM_VARIANT if variant is None else variant, _s(x))
+    kernels().gemm(_p(x), x.stride(0), _p(W), W.stride(0), _p(out), out.stride(0), M, N, K, epi, _s(x))
     return out
 
 

@@ -185,12 +185,10 @@ def test_linear_batched_decode_rows(cuda, M, N, K, epi):
                                    (5, 4096, 128), (600, 700, 1472), (257, 130, 320), (2048, 2304, 2048),
                                    (513, 6144, 4096)])
 @pytest.mark.parametrize("epi", [0, 1, 2, 3])
-@pytest.mark.parametrize("variant", [0, 1, 2])
-def test_gemm(cuda, M, N, K, epi, variant):
-    """256x256 ring-pipelined prefill GEMM (both bodies: 8-wave ping-pong, 4-wave AGPR) vs the
-    fp32 oracle: ragged M/N tiles (row/column clamps, masked epilogue), N % 4 != 0 (scalar
-    epilogue), K from one to 128 K-steps (ring wrap-around, the vmcnt(0) tail), every epilogue
-    incl. the fused SiLU-mul."""
+def test_gemm(cuda, M, N, K, epi):
+    """256x256 ring-pipelined prefill GEMM vs the fp32 oracle: ragged M/N tiles (row/column
+    clamps, masked epilogue), N % 4 != 0 (scalar epilogue), K from one to 64 K-steps (ring
+    wrap-around, the vmcnt(0) tail), every epilogue incl. the fused SiLU-mul."""
     if epi == 3 and N % 2:
         pytest.skip("SiLU pairs need even N")
     torch.manual_seed(M + N + K + epi)
@@ -198,19 +196,18 @@ def test_gemm(cuda, M, N, K, epi, variant):
     W = rnd(N, K, scale=0.05)
     out = rnd(M, N) if epi == 2 else None
     ref_out = out.cpu().clone() if out is not None else None
-    y = ops.gemm(x, W, epi, out=out, variant=variant)
+    y = ops.gemm(x, W, epi, out=out)
     ref = oracle.linear(x.cpu(), W.cpu(), epi, ref_out)
     close(y, ref, 2e-2)
 
 
 @pytest.mark.parametrize("K", [128, 512])
-@pytest.mark.parametrize("variant", [0, 1, 2])
-def test_gemm_identity_asymmetric(cuda, K, variant):
+def test_gemm_identity_asymmetric(cuda, K):
     """A = I with an asymmetric B catches a transposed C write (guide §3); K = 512 spans two
     256-row tiles in M and N."""
     A = torch.eye(K, dtype=BF, device="cuda")
     W = (torch.arange(K * K, device="cuda").view(K, K) % 97).to(BF)  # asymmetric
-    y = ops.gemm(A, W, 0, variant=variant)
+    y = ops.gemm(A, W, 0)
     assert torch.equal(y.cpu(), W.t().contiguous().cpu())
 
 

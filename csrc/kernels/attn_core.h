@@ -36,14 +36,13 @@ struct SubTile {
   // sc1 buffer loads for data produced inside its launch)
   template <typename Ld = PlainLd16>
   __device__ __forceinline__ void init(const bf16_t* qrow_kvh, int lane, Ld ld = Ld{}) {
+    // columns h >= G of the 16-head MFMA tile carry a copy of head 0 (finite; every column's
+    // scores, softmax state and output stay in that column and to_lds drops them). No select on
+    // the loaded value: a select would make hipcc wait for Q here, before the K/V loads issue.
     const int h = lane & 15, g4 = lane >> 4;
-    const bool real = h < G;
-    const bf16_t* qrow = qrow_kvh + (real ? h : 0) * D;
+    const bf16_t* qrow = qrow_kvh + (h < G ? h : 0) * D;
 #pragma unroll
-    for (int ks = 0; ks < KS; ++ks) {
-      bf16x8 v = __builtin_bit_cast(bf16x8, ld(qrow + ks * 32 + 8 * g4));
-      qf[ks] = real ? v : bf16x8{0, 0, 0, 0, 0, 0, 0, 0};
-    }
+    for (int ks = 0; ks < KS; ++ks) qf[ks] = __builtin_bit_cast(bf16x8, ld(qrow + ks * 32 + 8 * g4));
 #pragma unroll
     for (int dt = 0; dt < DT; ++dt) acc[dt] = f32x4{0.f, 0.f, 0.f, 0.f};
     m_run = kNegInfM;
@@ -307,8 +306,10 @@ __device__ __forceinline__ void merge_rows(__amdgpu_buffer_rsrc_t rsrc, const ch
       }
     }
   }
-  scratch[2 * tid] = f32x4{M, S, 0.f, 0.f};
-  scratch[2 * tid + 1] = f32x4{a[0], a[1], a[2], a[3]};
+  if (tid < NT) {  // tid >= NT: a thread of the block that only meets the barriers (attn_oproj.hip)
+    scratch[2 * tid] = f32x4{M, S, 0.f, 0.f};
+    scratch[2 * tid + 1] = f32x4{a[0], a[1], a[2], a[3]};
+  }
   __syncthreads();
   if (tid < Q) {
     ms = scratch[2 * tid];

@@ -1,0 +1,340 @@
+// K5 + o_proj of a batch-1 decode step in ONE launch (host: llmc_attn_oproj):
+//     h[n] += sum_k Wo[n, k] * attention(q, K/V cache)[k]
+//
+// Why (profiles/r2_dec2k_kernel_stats.md, 8B at 2k keys): as two launches the attention is a
+// latency chain (10.6 us for ~10 MB of K/V) and o_proj pays its own boundary + ramp (7.2 us for
+// 34 MB, 4.7 TB/s). Here the o_proj weights are requested right behind the K/V loads, so they
+// stream while the attention computes and merges; when the merged attention output arrives the
+// projection is arithmetic on registers.
+//
+// Grid: (nc, nkv) blocks of 8 waves; block (c, g) = kv head g x the fixed key range
+// [c * chunk, (c + 1) * chunk) (<= 256 keys: one 32-key MFMA sub-tile per wave, attn_core.h) AND
+// the o_proj tile rows [c R, (c + 1) R) x input columns of head group g (its G query heads):
+// R = H / nc rows, R / 4 per o wave (waves 0-3; waves 4-7 run the latency chain, see "Roles"),
+// each lane one 16-B column chunk per row (G D = 512).
+//
+//   1. one round trip for Q, L, the wave's page id and the two epochs; K/V of the wave's
+//      sub-tile; the block's o_proj weight tile (nt loads, in flight from here on)
+//   2. attention sub-tile -> block state -> partial granules (attn_core.h publish) and a ticket
+//      on head g's counter (EVERY block of head g takes one, keys or not)
+//   3. the last arriver of head g merges the partials and publishes head g's output (bf16) as
+//      {value, tag} granules; every block of head g polls those (the merger is running: it took
+//      the last ticket, so no wait is on a block that has not started — deadlock-free whatever
+//      the residency, safe beside co-located engines)
+//   4. o_proj partial of the tile over head g's columns (reduce-scatter across the lanes), as
+//      {f32, tag} granules; a ticket on tile c's counter; its nkv-th arriver sums the nkv
+//      partials in head order (deterministic) and adds them to the residual row h
+//   5. the last tile reducer re-arms the exit counter and advances the tile epoch (every block
+//      read it before arriving)
+//
+// Every spin is bounded: a give-up sets the fault word (checked by the engine like attn_decode's).
+#include "attn_core.h"
+
+namespace llmc {
+
+constexpr int kAoThreads = 512, kAoWaves = kAoThreads / kWave;
+constexpr int kAoLine = 16;  // int32 words per counter line (64 B)
+constexpr int kAoMaxKv = 8;  // kv heads (= head groups summed per o_proj row) at most
+
+// Diagnostics (stamps != nullptr): 8 s_memrealtime stamps (100 MHz) per block, see llmc_attn_oproj.
+__device__ __forceinline__ void ao_stamp(uint64_t* st, int k, bool who) {
+  if (st != nullptr && who) st[k] = __builtin_amdgcn_s_memrealtime();
+}
+
+template <int G, int D, int RW, bool LATE>
+__global__ __launch_bounds__(kAoThreads) void attn_oproj_kernel(
+    const bf16_t* __restrict__ q, const bf16_t* __restrict__ k_cache, const bf16_t* __restrict__ v_cache,
+    const int32_t* __restrict__ block_table, int bt_len, const int32_t* __restrict__ seq_len,
+    const bf16_t* __restrict__ w_o, int K_o, bf16_t* __restrict__ h, bf16_t* __restrict__ attn_out,
+    float* __restrict__ part, uint32_t* __restrict__ handoff, uint64_t* __restrict__ tile_part, int* __restrict__ ctr,
+    int* __restrict__ fault, int nkv, int bs, int nblocks, int chunk, float scale_log2, uint64_t* __restrict__ stamps) {
+  static_assert(G * D == 512, "one 16-B column chunk per lane per row");
+  static_assert(RW >= 1 && RW <= 32 && (RW & (RW - 1)) == 0, "rows per wave: power of two <= 32");
+  using ST = SubTile<G, D>;
+  constexpr int HQ = D / 4, RU = HQ + 1, Q = G * HQ;  // 16-B units: per head, per partial row, per group
+  constexpr int R = 4 * RW;                              // o_proj rows per block (4 o waves)
+  const int c = blockIdx.x, g = blockIdx.y, nc = gridDim.x;
+  const int tid = threadIdx.x, wave = tid / kWave, lane = tid % kWave;
+  uint64_t* stp = stamps != nullptr ? stamps + (static_cast<int64_t>(g) * nc + c) * 8 : nullptr;
+  ao_stamp(stp, 0, tid == 0);
+  int* hctr = ctr + g * kAoLine;            // {head ticket, head epoch}
+  int* tctr = ctr + (nkv + c) * kAoLine;    // {tile ticket}
+  int* xctr = ctr + (nkv + nc) * kAoLine;   // {exit count, tile epoch}
+
+  // ---- 1. one round trip: epochs, L, this wave's page id (scalar), Q (vector) ----
+  const uint32_t tag_h = static_cast<uint32_t>(__hip_atomic_load(hctr + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) + 1u;
+  const uint32_t tag_t = static_cast<uint32_t>(__hip_atomic_load(xctr + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) + 1u;
+  const int L = ld_scalar(seq_len);
+  const int key_lo = c * chunk;
+  const int wk0 = key_lo + wave * 32;  // this wave's 32-key sub-tile (one page: bs % 32 == 0)
+  const int pidx = __builtin_amdgcn_readfirstlane(min(wk0 / bs, bt_len - 1));
+  const int page = min(max(ld_scalar(block_table + pidx), 0), nblocks - 1);  // clamped into the cache
+  ST st;
+  st.init(q + g * G * D, lane);
+  const int key_hi = min(L, key_lo + chunk);
+  const bool wave_keys = wk0 < key_hi;  // wave-uniform
+  const bool block_keys = key_lo < L;   // block-uniform
+  const int nsplit = (L + chunk - 1) / chunk;  // blocks of head g with keys (host: nc * chunk >= L)
+
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  char* vbuf = smem + wave * 32 * kVRowBytes;                              // per-wave V image
+  float* red = reinterpret_cast<float*>(smem + kAoWaves * 32 * kVRowBytes);  // [8][G][D + 2]
+  u32x4* xs = reinterpret_cast<u32x4*>(red + kAoWaves * G * (D + 2));      // head g's output, 64 chunks
+  int* flag = reinterpret_cast<int*>(xs + 64);
+
+  bf16x8 kf[2][ST::KS];
+  u32x4 vs[ST::NV];
+  const int wend = min(key_hi, wk0 + 32);
+  const int64_t kvbase = (static_cast<int64_t>(page) * nkv + g) * bs * D;
+  // a wave without keys issues its loads anyway, all at one row of its page (L2 hits): loads under
+  // a branch would end in a register merge at the join that waits for them before the weights issue
+  auto row = [&](const bf16_t* cache, int key) {
+    return cache + kvbase + (wave_keys ? static_cast<int64_t>(key % bs) * D : 0);
+  };
+  // keys [wk0, wend_ld) are loaded; a wave without keys loads one (masked below: end = wk0 masks all)
+  const int wend_ld = wave_keys ? wend : wk0 + 1;
+  const int wend_c = wave_keys ? wend : wk0;
+
+  // Roles. The vector memory counter retires in order, so a wave with o_proj weights in flight
+  // cannot use any later load's result (a ticket's return value, a merge or poll load) before its
+  // weights have landed. Waves 0-3 (the "o waves") therefore carry the weights and nothing on the
+  // latency chain; waves 4-7 (the "control waves", no weights) publish the partial, take the
+  // tickets, merge, poll the hand-off and reduce the tile. Every wave computes one attention
+  // sub-tile. The o_proj tile: rows n = c R + ow RW + j (ow = o wave), columns g G D + 8 lane .. + 8.
+  const bool o_wave = wave < 4;  // wave-uniform
+  const int ct = tid - 256;      // control-thread index (waves 4-7: 0..255)
+  // tickets from wave 6: it has neither weights nor partial / hand-off stores in flight (stores
+  // count in the same counter), so the returned value is usable at once
+  constexpr int kTicketThread = 128;
+  // The attention step is written out in each role's branch: with one shared copy after the
+  // branches, hipcc's counter model at the join would make the o waves wait for their weights
+  // before the MFMAs (it assumes the fewest loads in flight over both paths).
+  u32x4 wt[RW];
+  const bf16_t* wrow = w_o + static_cast<int64_t>(c * R + wave * RW) * K_o + g * G * D + 8 * lane;
+  if (o_wave) {
+    st.issue(wk0, wend_ld, lane, row, k_cache, v_cache, kf, vs);
+    __builtin_amdgcn_sched_barrier(0);  // every K/V load issues before the first weight load
+    if constexpr (!LATE) {
+#pragma unroll
+      for (int j = 0; j < RW; ++j) wt[j] = load16<true>(wrow + static_cast<int64_t>(j) * K_o);  // nt: read once
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    // ---- 2. attention sub-tile (K/V were issued before the weights: the wait leaves them in flight).
+    // Unconditional: a wave without keys masks every score (its state stays empty); under a branch
+    // hipcc would sink the last K/V load into it, behind the weights.
+    st.compute(wk0, wend_c, lane, vbuf, scale_log2, kf, vs);
+    if constexpr (LATE) {  // weights behind the attention: the K/V loads do not queue behind them
+#pragma unroll
+      for (int j = 0; j < RW; ++j) wt[j] = load16<true>(wrow + static_cast<int64_t>(j) * K_o);
+    }
+    ao_stamp(stp, 1, tid == 0);
+  } else {
+    st.issue(wk0, wend_ld, lane, row, k_cache, v_cache, kf, vs);
+    st.compute(wk0, wend_c, lane, vbuf, scale_log2, kf, vs);
+    ao_stamp(stp, 2, ct == 0);
+  }
+  // ---- ... -> block state -> partial -> head ticket ----
+  st.to_lds(red, wave, lane);
+  __syncthreads();
+  const int slab_rows = nc;
+  float* slab = part + static_cast<int64_t>(g) * slab_rows * G * RU * 4;
+  const __amdgpu_buffer_rsrc_t rsrc = __builtin_amdgcn_make_buffer_rsrc(slab, 0, slab_rows * G * RU * 16, 0x00020000);
+  if (block_keys) publish_partial<G, D, kAoWaves>(red, rsrc, c, tag_h, o_wave ? Q : ct);
+  __syncthreads();  // every wave's stores are issued (the merger checks tags)
+  if (ct == kTicketThread) *flag = __hip_atomic_fetch_add(hctr, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == nc - 1;
+  __syncthreads();
+  ao_stamp(stp, 3, tid == 0);
+
+  // ---- 3. the last arriver of head g merges (control waves) and publishes head g's output ----
+  uint32_t* hoff = handoff + static_cast<int64_t>(g) * Q * 4;  // Q 16-B units {bf16x2, tag, bf16x2, tag}
+  const __amdgpu_buffer_rsrc_t hr = __builtin_amdgcn_make_buffer_rsrc(hoff, 0, Q * 16, 0x00020000);
+  if (*flag) {
+    f32x4 ms, acc;
+    merge_rows<G, D, 256>(rsrc, reinterpret_cast<const char*>(slab), 0, nsplit, tag_h, reinterpret_cast<f32x4*>(smem),
+                          o_wave ? 256 + tid : ct, ms, acc, fault);
+    if (!o_wave && ct < Q) {
+      const float inv = 1.f / ms[1];
+      const uint32_t lo = pack_bf16x2(acc[0] * inv, acc[1] * inv), hi = pack_bf16x2(acc[2] * inv, acc[3] * inv);
+      __builtin_amdgcn_raw_buffer_store_b128(u32x4{lo, tag_h, hi, tag_h}, hr, ct * 16, 0, 16);
+      const int gq = ct / HQ, u = ct % HQ;
+      *reinterpret_cast<u32x2*>(attn_out + (g * G + gq) * D + 4 * u) = u32x2{lo, hi};
+    }
+    if (ct == 0) {
+      __hip_atomic_store(hctr, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);                            // re-arm
+      __hip_atomic_store(hctr + 1, static_cast<int>(tag_h), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // epoch
+    }
+  }
+
+  // every block of head g: wave 4 polls head g's output granules into LDS (2 units per lane)
+  if (wave == 4) {
+    // 8-B relaxed atomic loads, one granule each: ordered loads are re-issued on every poll (plain
+    // buffer loads in this loop would look loop-invariant to hipcc and be hoisted out of it)
+    const char* hb = reinterpret_cast<const char*>(hoff) + 32 * lane;
+    u32x2 a0, a1, b0, b1;
+    // one lane polls one granule (256 blocks polling every granule flooded the memory path the
+    // weights stream through); once it has landed the wave reads them all (re-read if any lags)
+    if (lane == 0) {
+      for (unsigned spins = 0; ld8_atomic(reinterpret_cast<const char*>(hoff), 0)[1] != tag_h && spins < kSpinLimit;
+           ++spins)
+        __builtin_amdgcn_s_sleep(2);
+    }
+    for (unsigned spins = 0;; ++spins) {
+      a0 = ld8_atomic(hb, 0);
+      a1 = ld8_atomic(hb, 8);
+      b0 = ld8_atomic(hb, 16);
+      b1 = ld8_atomic(hb, 24);
+      if (__all(a0[1] == tag_h && a1[1] == tag_h && b0[1] == tag_h && b1[1] == tag_h)) break;
+      if (spins >= kSpinLimit) {
+        if (lane == 0 && fault != nullptr) __hip_atomic_store(fault, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        break;
+      }
+      __builtin_amdgcn_s_sleep(1);
+    }
+    xs[lane] = u32x4{a0[0], a1[0], b0[0], b1[0]};  // dims 8 lane .. 8 lane + 7 of head group g
+  }
+  __syncthreads();
+  ao_stamp(stp, 4, tid == 0);
+
+  // ---- 4. o_proj partial over head g's columns (o waves); reduce-scatter the RW row sums ----
+  uint64_t* tp = tile_part + (static_cast<int64_t>(c) * nkv) * R;
+  if (o_wave) {
+    float s[RW];
+    const u32x4 x = xs[lane];
+#pragma unroll
+    for (int j = 0; j < RW; ++j) s[j] = dot8_bf16(wt[j], x, 0.f);
+    // stage m: lanes with bit m keep the upper half of the live rows, the others the lower half
+#pragma unroll
+    for (int m = 32, n = RW; n > 1; m >>= 1, n >>= 1) {
+      const bool up = (lane & m) != 0;
+#pragma unroll
+      for (int i = 0; i < n / 2; ++i) {
+        const float send = up ? s[i] : s[i + n / 2];
+        const float keep = up ? s[i + n / 2] : s[i];
+        s[i] = keep + __shfl_xor(send, m, 64);
+      }
+    }
+    constexpr int LPR = 64 / RW;  // lanes sharing one row after the stages (the low log2(LPR) bits)
+#pragma unroll
+    for (int m = LPR / 2; m >= 1; m >>= 1) s[0] += __shfl_xor(s[0], m, 64);
+    if ((lane % LPR) == 0) {
+      const int my_row = wave * RW + lane / LPR;  // row within the tile
+      const uint64_t gv = static_cast<uint64_t>(__float_as_uint(s[0])) | (static_cast<uint64_t>(tag_t) << 32);
+      __hip_atomic_store(tp + g * R + my_row, gv, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // 8-B sc1 store
+    }
+    ao_stamp(stp, 5, tid == 0);
+  }
+  __syncthreads();
+  if (ct == kTicketThread) *flag = __hip_atomic_fetch_add(tctr, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == nkv - 1;
+  __syncthreads();
+  ao_stamp(stp, 6, tid == 0);
+  if (*flag == 0) return;
+
+  // ---- the tile's nkv-th arriver (control waves): h[rows] += sum over heads, fixed order ----
+  if (ct >= 0 && ct < R) {
+    // every head's granule of this row in flight at once (nkv <= kAoMaxKv), re-polled until all
+    // tags match; summed in head order
+    uint64_t v[kAoMaxKv];
+    for (unsigned spins = 0;; ++spins) {
+      bool ok = true;
+#pragma unroll
+      for (int gg = 0; gg < kAoMaxKv; ++gg)
+        if (gg < nkv) v[gg] = __hip_atomic_load(tp + gg * R + ct, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+#pragma unroll
+      for (int gg = 0; gg < kAoMaxKv; ++gg)
+        if (gg < nkv) ok = ok && static_cast<uint32_t>(v[gg] >> 32) == tag_t;
+      if (ok) break;
+      if (spins >= kSpinLimit) {
+        if (fault != nullptr) __hip_atomic_store(fault, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        break;
+      }
+      __builtin_amdgcn_s_sleep(1);
+    }
+    float sum = 0.f;
+#pragma unroll
+    for (int gg = 0; gg < kAoMaxKv; ++gg)
+      if (gg < nkv) sum += __uint_as_float(static_cast<uint32_t>(v[gg]));
+    bf16_t* hp = h + c * R + ct;
+    *hp = f32_to_bf16(bf16_to_f32(*hp) + sum);
+    ao_stamp(stp, 7, ct == 0);
+  }
+  if (ct == 0) {
+    __hip_atomic_store(tctr, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // re-arm the tile ticket
+    if (__hip_atomic_fetch_add(xctr, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == nc - 1) {
+      __hip_atomic_store(xctr, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(xctr + 1, static_cast<int>(tag_t), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+  }
+}
+
+}  // namespace llmc
+
+using namespace llmc;
+
+// > 64 KB of dynamic LDS (the per-wave V images): raise the kernel's limit once per instantiation
+template <int G, int D, int RW>
+static void ao_set_lds() {
+  static bool done = false;  // one flag per instantiation
+  const auto kern = attn_oproj_kernel<G, D, RW, false>;
+  const auto kern_late = attn_oproj_kernel<G, D, RW, true>;
+  if (!done) {
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize,
+                              160 * 1024);
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(kern_late), hipFuncAttributeMaxDynamicSharedMemorySize,
+                              160 * 1024);
+    done = true;
+  }
+}
+
+// Supported shape: G query heads per kv head and head dim D with G * D == 512, R = H / nc rows
+// per block = 4 * RW (RW in {8, 16, 32}), chunk in {32, 64, ..., 256} keys per block, page size
+// a multiple of 32. Returns 0 when (H, nh, nkv, D, nc) is supported.
+extern "C" int llmc_attn_oproj_check(int H, int nh, int nkv, int D, int nc, int K_o) {
+  if (nkv < 1 || nh % nkv != 0 || nc < 1 || H % nc != 0) return -1;
+  const int G = nh / nkv;
+  if (G * D != 512 || K_o != nh * D) return -2;
+  const int rw = H / nc / 4;
+  if (rw * 4 * nc != H || (rw != 8 && rw != 16 && rw != 32)) return -3;
+  if (!((G == 4 && D == 128) || (G == 8 && D == 64))) return -4;
+  return 0;
+}
+
+// mode bit 0: issue the o_proj weights after the attention sub-tile instead of right behind its K/V.
+// stamps (nullable, diagnostics): uint64 [nkv][nc][8] s_memrealtime per block: 0 start, 1 o wave 0's
+// attention done, 2 control wave 4's attention done, 3 head ticket taken, 4 head output in LDS,
+// 5 o wave 0's tile partial published, 6 tile ticket taken, 7 tile reduced (reducer only).
+// Workspace (zeroed once): part f32 [nkv][nc][G][D/4 + 1][4]; handoff u32 [nkv][G D / 4][4];
+// tile_part u64 [nc][nkv][H / nc]; ctr int32 [(nkv + nc + 1) * 16].
+extern "C" int llmc_attn_oproj(const void* q, const void* k_cache, const void* v_cache, const void* block_table,
+                               int bt_len, const void* seq_len, const void* w_o, void* h, void* attn_out, void* part,
+                               void* handoff, void* tile_part, void* ctr, void* fault, int H, int nh, int nkv, int D,
+                               int bs, int nblocks, int chunk, int nc, float scale, int mode, void* stamps,
+                               hipStream_t s) {
+  const int K_o = nh * D;
+  if (llmc_attn_oproj_check(H, nh, nkv, D, nc, K_o) != 0 || nkv > kAoMaxKv) return -1;
+  const bool late = (mode & 1) != 0;  // o_proj weights issued after the attention sub-tile
+  if (chunk < 32 || chunk > kAoWaves * 32 || chunk % 32 != 0 || bs % 32 != 0 || bt_len < 1 || nblocks < 1) return -1;
+  const int G = nh / nkv, rw = H / nc / 4;
+  const size_t lds = kAoWaves * 32 * kVRowBytes + static_cast<size_t>(kAoWaves) * G * (D + 2) * sizeof(float) +
+                     64 * 16 + 16;
+  dim3 grid(nc, nkv);
+  const float sl2 = scale * 1.4426950408889634f;
+#define LLMC_AO(GG, DD, RR)                                                                                      \
+  do {                                                                                                            \
+    ao_set_lds<GG, DD, RR>();                                                                    \
+    (late ? attn_oproj_kernel<GG, DD, RR, true> : attn_oproj_kernel<GG, DD, RR, false>)<<<grid, kAoThreads, lds, s>>>( \
+      (const bf16_t*)q, (const bf16_t*)k_cache, (const bf16_t*)v_cache, (const int32_t*)block_table, bt_len,       \
+      (const int32_t*)seq_len, (const bf16_t*)w_o, K_o, (bf16_t*)h, (bf16_t*)attn_out, (float*)part,               \
+      (uint32_t*)handoff, (uint64_t*)tile_part, (int*)ctr, (int*)fault, nkv, bs, nblocks, chunk, sl2, (uint64_t*)stamps); \
+  } while (0)
+  if (G == 4 && D == 128) {
+    if (rw == 8) LLMC_AO(4, 128, 8);
+    else if (rw == 16) LLMC_AO(4, 128, 16);
+    else LLMC_AO(4, 128, 32);
+  } else {
+    if (rw == 8) LLMC_AO(8, 64, 8);
+    else if (rw == 16) LLMC_AO(8, 64, 16);
+    else LLMC_AO(8, 64, 32);
+  }
+#undef LLMC_AO
+  return static_cast<int>(hipGetLastError());
+}

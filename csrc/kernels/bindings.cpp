@@ -32,6 +32,10 @@ int llmc_decode_layer(const void*, const void*, const void*, const void*, const 
                       void*, void*, void*, void*, void*, void*, void*, int, int, int, int, int, int, int, int, int, int,
                       float, float, hipStream_t);
 int llmc_attn_decode_groups(int);
+int llmc_attn_oproj_check(int, int, int, int, int, int);
+int llmc_attn_oproj(const void*, const void*, const void*, const void*, int, const void*, const void*, void*, void*,
+                    void*, void*, void*, void*, void*, int, int, int, int, int, int, int, int, float, int, void*,
+                    hipStream_t);
 int llmc_attn_decode(const void*, int, const void*, const void*, const void*, int, const void*, void*, void*, void*,
                      int, int, int, int, int, int, int, int, int, int, float, int, void*, hipStream_t);
 int llmc_gemv_qkv_rope(int, const void*, int, const void*, float, const void*, int, int, void*, int, void*, void*,
@@ -122,6 +126,17 @@ PYBIND11_MODULE(_llmc_hip, m) {
           "decode_layer");
   });
   m.def("attn_decode_groups", [](int max_chunks) { return llmc_attn_decode_groups(max_chunks); });
+  m.def("attn_oproj_check", [](int H, int nh, int nkv, int D, int nc, int K_o) {
+    return llmc_attn_oproj_check(H, nh, nkv, D, nc, K_o);
+  });
+  m.def("attn_oproj", [](ptr q, ptr kc, ptr vc, ptr bt, int bt_len, ptr sl, ptr w_o, ptr h, ptr attn_out, ptr part,
+                         ptr handoff, ptr tile_part, ptr ctr, ptr fault, int H, int nh, int nkv, int D, int bs,
+                         int nblocks, int chunk, int nc, float scale, int mode, ptr stamps, ptr s) {
+    check(llmc_attn_oproj(P(q), P(kc), P(vc), P(bt), bt_len, P(sl), P(w_o), P(h), P(attn_out), P(part), P(handoff),
+                          P(tile_part), P(ctr), P(fault), H, nh, nkv, D, bs, nblocks, chunk, nc, scale, mode, P(stamps),
+                          S(s)),
+          "attn_oproj");
+  });
   m.def("attn_decode", [](ptr q, int qs, ptr kc, ptr vc, ptr bt, int bts, ptr sl, ptr part, ptr ctr, ptr out, int os,
                           int B, int nh, int nkv, int D, int bs, int nblocks, int chunk, int grid_chunks,
                           int max_chunks, float scale, int fused, ptr fault, ptr s) {

@@ -21,6 +21,7 @@ from __future__ import annotations
 
 import dataclasses
 import math
+import os
 import time
 from typing import Callable, Dict, List, Optional, Sequence as Seq
 
@@ -60,6 +61,10 @@ class EngineConfig:
     # (csrc/kernels/decode_layer.hip) instead of five kernels. Off by default: measured slower
     # than the five tuned kernels so far (docs/ARCHITECTURE.md, "Fused decode layer")
     fused_layer: bool = False
+    # one-row engines without TP: decode attention + o_proj + residual as ONE launch per layer
+    # (csrc/kernels/attn_oproj.hip) for every context bucket it covers (<= 256 keys per block).
+    # Off unless LLMC_ATTN_OPROJ=1 until it beats the two launches (docs/ARCHITECTURE.md §8)
+    attn_oproj: bool = dataclasses.field(default_factory=lambda: os.environ.get("LLMC_ATTN_OPROJ", "0") == "1")
 
 
 FUSED_CHUNK_SMALL, FUSED_CHUNK_LARGE = 128, 256
@@ -256,6 +261,16 @@ class Engine:
             max_chunks = max(max_chunks, max(self.layer_gc))
             self.dl_sync = torch.zeros(ops.DECODE_LAYER_SYNC_WORDS, dtype=torch.int32, device=dev)
         self.attn_part, self.attn_counters = ops.decode_attn_workspace(B, self.nh, self.nkv, self.D, max_chunks, dev)
+        # fused attention + o_proj launch: per bucket its keys per block (0 = the bucket keeps the
+        # two launches)
+        self.ao_chunks: List[int] = [0] * len(self.attn_buckets)
+        self.ao_nc = 0
+        if (self.on_gpu and self.ecfg.attn_oproj and B == 1 and self.tp.size == 1 and not self.fused_layer
+                and self.bs % 32 == 0):
+            self.ao_nc = ops.attn_oproj_grid(c.hidden, self.nh, self.nkv, self.D)
+            if self.ao_nc:
+                self.ao_chunks = [ops.attn_oproj_chunk(cap, self.ao_nc) for cap, _, _, _ in self.attn_buckets]
+                self.ao_ws = ops.attn_oproj_workspace(c.hidden, self.nh, self.nkv, self.D, self.ao_nc, dev)
         # set by a decode-attention merger that gave up on a partial (checked after every decode)
         self.attn_fault = torch.zeros(1, dtype=torch.int32, device=dev) if self.on_gpu else None
         if self.on_gpu:
@@ -567,14 +582,20 @@ class Engine:
                                  self.bs, gc, c.rms_eps, self.scale)
             self._lm_head_sample(B)
             return
+        ao_chunk = self.ao_chunks[-1 if bucket is None else bucket] if B == 1 else 0
         for li, Lw in enumerate(self.w.layers):
             ops.qkv_rope(h, Lw.w_qkv, Lw.ln1, c.rms_eps, q, self.k_cache[li], self.v_cache[li], self.positions[:B],
                          self.slots[:B], self.cos_t, self.sin_t, self.nh, self.nkv, self.D, self.bs,
                          mfma=self.mfma_decode)
-            ops.attn_decode(q, self.k_cache[li], self.v_cache[li], self.block_tables[:B], self.seq_lens[:B], attn,
-                            part[:B], self.attn_counters[:B], self.nh, self.nkv, self.D, self.bs, chunk, self.scale,
-                            grid_chunks, fused=fused, fault=self.attn_fault)
-            self._row_parallel(attn, Lw.w_o, h)
+            if ao_chunk:
+                ops.attn_oproj(q, self.k_cache[li], self.v_cache[li], self.block_tables[:1], self.seq_lens[:1], Lw.w_o,
+                               h, attn, self.ao_ws, self.nh, self.nkv, self.D, self.bs, ao_chunk, self.ao_nc,
+                               self.scale, fault=self.attn_fault)
+            else:
+                ops.attn_decode(q, self.k_cache[li], self.v_cache[li], self.block_tables[:B], self.seq_lens[:B], attn,
+                                part[:B], self.attn_counters[:B], self.nh, self.nkv, self.D, self.bs, chunk,
+                                self.scale, grid_chunks, fused=fused, fault=self.attn_fault)
+                self._row_parallel(attn, Lw.w_o, h)
             if c.is_moe:
                 self._moe_decode(h, Lw, B)
             else:

@@ -8,6 +8,7 @@ stream, so every op is capturable in a HIP graph.
 
 from __future__ import annotations
 
+import os
 from typing import Optional
 
 import torch
@@ -219,6 +220,69 @@ def attn_decode(q, k_cache, v_cache, block_tables, seq_lens, out, part, counters
                           _p(seq_lens), _p(part), _p(counters), _p(out), out.stride(0), B, nh, nkv, D, bs,
                           k_cache.shape[0], chunk, gc, max_chunks, float(scale), 1 if fused else 0, _p(fault), _s(q))
     return out
+
+
+ATTN_OPROJ_MAX_CHUNK = 256  # attn_oproj: keys per block at most (8 waves x one 32-key sub-tile)
+ATTN_OPROJ_MODE = int(os.environ.get("LLMC_ATTN_OPROJ_MODE", "0"))  # kernel mode bits (A/B runs)
+
+
+def attn_oproj_grid(H: int, nh: int, nkv: int, D: int) -> int:
+    """Blocks per kv head of the fused attention + o_proj launch (``attn_oproj``) for this shape,
+    or 0 when the kernel library does not cover it: ~one block per CU over the kv heads (256 /
+    nkv; Llama-3-8B: 32), each owning H / nc o_proj rows (4 o waves x 8-32 rows)."""
+    top = max(1, 256 // max(1, nkv))
+    # ~one block per CU; else the largest grid whose tile gives each o wave 8-32 rows
+    for nc in sorted({top} | {n for n in (H // 128, H // 64, H // 32) if 0 < n <= top}, reverse=True):
+        if kernels().attn_oproj_check(H, nh, nkv, D, nc, nh * D) == 0:
+            return nc
+    return 0
+
+
+def attn_oproj_chunk(ctx_cap: int, nc: int) -> int:
+    """Keys per block for a context bucket of ``ctx_cap`` keys over ``nc`` blocks per kv head (a
+    multiple of 32), or 0 when the bucket needs more than ATTN_OPROJ_MAX_CHUNK keys per block."""
+    per = -(-ctx_cap // nc)
+    ch = max(32, (per + 31) // 32 * 32)
+    return ch if ch <= ATTN_OPROJ_MAX_CHUNK else 0
+
+
+def attn_oproj_workspace(H: int, nh: int, nkv: int, D: int, nc: int, device):
+    """(part, handoff, tile_part, counters) of ``attn_oproj``, zeroed once and never reset (the
+    kernel re-arms its tickets and advances its epochs): attention partial granules f32 [nkv, nc,
+    G, D/4 + 1, 4]; the merged per-head output as {bf16x2, tag} granules int32 [nkv, G D / 4, 4];
+    the o_proj tile partials as {f32, tag} int64 [nc, nkv, H / nc]; counters int32 [(nkv + nc + 1)
+    * 16] (head {ticket, epoch}, tile tickets, {exit, tile epoch}, one 64-B line each)."""
+    G = nh // nkv
+    dev = torch.device(device)
+    part = torch.zeros(nkv, nc, G, D // 4 + 1, 4, dtype=torch.float32, device=dev)
+    handoff = torch.zeros(nkv, G * D // 4, 4, dtype=torch.int32, device=dev)
+    tile_part = torch.zeros(nc, nkv, H // nc, dtype=torch.int64, device=dev)
+    counters = torch.zeros((nkv + nc + 1) * 16, dtype=torch.int32, device=dev)
+    return part, handoff, tile_part, counters
+
+
+def attn_oproj(q, k_cache, v_cache, block_table, seq_len, w_o, h, attn_out, ws, nh, nkv, D, bs, chunk, nc, scale,
+               fault: Optional[torch.Tensor] = None, stamps: Optional[torch.Tensor] = None, mode: int = -1) -> None:
+    """Decode attention of ONE row followed by its o_proj and residual add, in one launch
+    (csrc/kernels/attn_oproj.hip): ``h[0] += w_o @ attention(q[0])``; ``attn_out[0]`` also gets the
+    attention output. ``ws`` = ``attn_oproj_workspace(...)``; ``chunk`` = ``attn_oproj_chunk(cap,
+    nc)`` for a bucket whose capacity covers the sequence; ``fault`` as in ``attn_decode``;
+    ``stamps`` (diagnostics): int64 [nkv, nc, 8] per-block phase times (see the kernel's host
+    function); ``mode`` bit 0: o_proj weights requested after the attention sub-tile (-1 =
+    ATTN_OPROJ_MODE)."""
+    H = h.shape[-1]
+    if not q.is_cuda:
+        a = oracle.attn_decode(q[:1], k_cache, v_cache, block_table[:1], seq_len[:1], nh, nkv, D, bs, scale)
+        attn_out[:1].copy_(a)
+        oracle.linear(attn_out[:1], w_o, EPI_RESADD, h[:1])
+        return
+    if chunk <= 0 or chunk * nc < 1 or nc != ws[0].shape[1]:
+        raise ValueError("attn_oproj: chunk / workspace do not match (attn_oproj_chunk, attn_oproj_workspace)")
+    part, handoff, tile_part, counters = ws
+    kernels().attn_oproj(_p(q), _p(k_cache), _p(v_cache), _p(block_table), block_table.shape[-1], _p(seq_len), _p(w_o),
+                         _p(h), _p(attn_out), _p(part), _p(handoff), _p(tile_part), _p(counters), _p(fault), H, nh, nkv,
+                         D, bs, k_cache.shape[0], chunk, nc, float(scale), ATTN_OPROJ_MODE if mode < 0 else mode,
+                         _p(stamps), _s(h))
 
 
 DECODE_LAYER_MIN_CHUNK = 256  # fused decode layer: keys per attention block at least (8 waves x 32)

@@ -85,6 +85,61 @@ def bench_attn(shapes=((32, 8, 128), (32, 32, 96), (16, 2, 128), (8, 1, 128), (4
                   + f"  | best {gb / best * 1e6 / 1e3:5.2f} TB/s", flush=True)
 
 
+def bench_attn_oproj(shapes=((32, 8, 128, 4096),), lens=(128, 1024, 2048, 2300, 4096, 6000, 8000)):
+    """Decode attention + o_proj + residual of ONE row per layer: the fused launch (attn_oproj.hip)
+    against the engine's two launches (attn_decode in the bucket's form + o GEMV with the residual
+    epilogue). Graph-timed over COPIES cycled per call (>= 512 MB of weights and K/V, beyond the
+    256 MB Infinity Cache), so every call reads cold weights as a decode step does."""
+    from llm_consensus_amd.engine.engine import attn_buckets, split_blocks_per_head
+    from llm_consensus_amd.ops import EPI_RESADD
+
+    for nh, nkv, D, H in shapes:
+        nc = ops.attn_oproj_grid(H, nh, nkv, D)
+        sc = 1 / math.sqrt(D)
+        for L in lens:
+            cap = 1024
+            while cap < L:
+                cap *= 2
+            chunk = ops.attn_oproj_chunk(cap, nc)
+            bk = attn_buckets(cap, split_blocks_per_head(nh, nkv), ops.FUSED_ATTN_MAX_KEYS, nh // nkv, nkv)[-1]
+            _, ch2, gc2, fused2 = bk
+            w_bytes = H * nh * D * 2
+            kv_bytes = L * nkv * D * 4
+            copies = max(4, (512 << 20) // (w_bytes + kv_bytes) + 1)
+            cases = [_attn_case(L, nh, nkv, D) for _ in range(copies)]
+            wos = [(torch.randn(H, nh * D, device="cuda") / math.sqrt(nh * D)).to(BF) for _ in range(copies)]
+            h = torch.zeros(1, H, dtype=BF, device="cuda")
+            attn = torch.zeros(1, nh * D, dtype=BF, device="cuda")
+            ws = ops.attn_oproj_workspace(H, nh, nkv, D, nc, "cuda")
+            part, ctr = ops.decode_attn_workspace(1, nh, nkv, D, max(gc2, 32), "cuda")
+            fault = torch.zeros(1, dtype=torch.int32, device="cuda")
+            it = [0]
+
+            def two():
+                kc, vc, bt, sl, q, out = cases[it[0] % copies]
+                ops.attn_decode(q, kc, vc, bt, sl, out, part, ctr, nh, nkv, D, 64, ch2, sc, grid_chunks=gc2,
+                                fused=fused2, fault=fault)
+                ops.linear(out, wos[it[0] % copies], EPI_RESADD, out=h)
+                it[0] += 1
+
+            def one(mode=0):
+                kc, vc, bt, sl, q, out = cases[it[0] % copies]
+                ops.attn_oproj(q, kc, vc, bt, sl, wos[it[0] % copies], h, attn, ws, nh, nkv, D, 64, chunk, nc, sc,
+                               fault=fault, mode=mode)
+                it[0] += 1
+
+            n = copies * max(1, 48 // copies)
+            t2 = timeit(two, iters=n)
+            t1 = timeit(one, iters=n) if chunk else float("nan")
+            t1l = timeit(lambda: one(1), iters=n) if chunk else float("nan")
+            torch.cuda.synchronize()
+            print(f"attn+o nh={nh} nkv={nkv} D={D} H={H} L={L:5d} cap={cap}: two launches "
+                  f"({'fused' if fused2 else 'split'} c{ch2} g{gc2} + o GEMV) {t2:6.2f} us | one launch "
+                  f"(nc {nc}, {chunk} keys/block) {t1:6.2f} us, late weights {t1l:6.2f} us | fault {int(fault.item())}",
+                  flush=True)
+            del cases, wos
+
+
 def bench_attn_batched(shapes=((32, 8, 128),), rows=(1, 4, 16), lens=(2048, 2560, 8192)):
     """Decode attention for B rows per launch (continuous batching): the fused form over the
     engine's bucket (capacity = next power of two >= L, 128/256-key chunks) vs the balanced split
@@ -372,6 +427,8 @@ if __name__ == "__main__":
         bench_gemv_sweep([(768, 4096), (1536, 4096), (3584, 4096), (4096, 512), (4096, 1792)])
     if what in ("sweep-70b-tp4",):  # one TP=4 rank of Llama-3-70B: qkv, gate_up, o, down
         bench_gemv_sweep([(2560, 8192), (14336, 8192), (8192, 2048), (8192, 7168)])
+    if what in ("attn-oproj",):  # fused decode attention + o_proj (one row) vs the two launches
+        bench_attn_oproj()
     if what in ("attn-batched",):  # decode attention with many rows per launch
         bench_attn_batched()
     if what in ("gemvm-forms",):  # the MFMA decode form's variants

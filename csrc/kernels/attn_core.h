@@ -251,12 +251,12 @@ __device__ __forceinline__ void publish_partial(const float* red, __amdgpu_buffe
   }
 }
 
-// Merge the partial rows [r0, r0 + n) of a granule slab: thread = (output quad, row group), up to 8
-// rows' {O quad, lambda} loads in flight per thread, re-polled until every tag matches (a
+// Merge the partial rows [r0, r0 + n) of a granule slab: thread = (output quad, row group), up to
+// BATCH rows' {O quad, lambda} loads in flight per thread, re-polled until every tag matches (a
 // straggler is a store already issued by a block that has arrived: no wait on any block that is
 // not running), folded with an online log-sum-exp; row groups meet in LDS. On return threads
 // tid < G * D / 4 hold their quad's (M, S) in ms[0..1] and the unnormalised sums in acc.
-template <int G, int D, int NT>
+template <int G, int D, int NT, int BATCH = 8>
 __device__ __forceinline__ void merge_rows(__amdgpu_buffer_rsrc_t rsrc, const char* base, int r0, int n, uint32_t tag,
                                            f32x4* scratch, int tid, f32x4& ms, f32x4& acc, int* fault) {
   constexpr int HQ = D / 4, RU = HQ + 1, Q = G * HQ;
@@ -266,20 +266,20 @@ __device__ __forceinline__ void merge_rows(__amdgpu_buffer_rsrc_t rsrc, const ch
   float M = kNegInfM, S = 0.f, a[4] = {0.f, 0.f, 0.f, 0.f};
   if (gr < ngr) {
     const int g = (tid % Q) / HQ, u = (tid % Q) % HQ;
-    for (int c0 = gr; c0 < n; c0 += 8 * ngr) {
-      u32x4 ov[8];
-      u32x2 lv[8];
+    for (int c0 = gr; c0 < n; c0 += BATCH * ngr) {
+      u32x4 ov[BATCH];
+      u32x2 lv[BATCH];
       for (unsigned spins = 0;; ++spins) {
         bool ok = true;
 #pragma unroll
-        for (int j = 0; j < 8; ++j) {
+        for (int j = 0; j < BATCH; ++j) {
           const int cc = r0 + min(c0 + j * ngr, n - 1);  // clamped: every load in flight, masked below
           const int row = (cc * G + g) * RU;
           ov[j] = ld16_sc1(rsrc, (row + u) * 16);
           lv[j] = ld8_atomic(base, (row + HQ) * 16);
         }
 #pragma unroll
-        for (int j = 0; j < 8; ++j)
+        for (int j = 0; j < BATCH; ++j)
           if (c0 + j * ngr < n) ok = ok && ov[j][1] == tag && ov[j][3] == tag && lv[j][1] == tag;
         if (__all(ok)) break;
         if (spins >= kSpinLimit) {
@@ -291,7 +291,7 @@ __device__ __forceinline__ void merge_rows(__amdgpu_buffer_rsrc_t rsrc, const ch
         __builtin_amdgcn_s_sleep(2);
       }
 #pragma unroll
-      for (int j = 0; j < 8; ++j) {
+      for (int j = 0; j < BATCH; ++j) {
         if (c0 + j * ngr < n) {
           const float lam = __uint_as_float(lv[j][0]);
           const float mn = fmaxf(M, lam);

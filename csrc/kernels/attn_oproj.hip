@@ -36,6 +36,24 @@ constexpr int kAoThreads = 512, kAoWaves = kAoThreads / kWave;
 constexpr int kAoLine = 16;  // int32 words per counter line (64 B)
 constexpr int kAoMaxKv = 8;  // kv heads (= head groups summed per o_proj row) at most
 
+// Reduce-scatter of N per-lane row sums over the 64 lanes, one stage per lane bit M = 32, 16, ...:
+// lanes with bit M keep the upper half of the live rows, the others the lower half, and add the
+// partner's copy. Recursion keeps every index a constant (a loop over the stages left hipcc with
+// runtime-indexed register arrays: thousands of selects, ~10 us per call).
+template <int N, int M, int RWt>
+__device__ __forceinline__ void ao_reduce_scatter(float (&s)[RWt], int lane) {
+  if constexpr (N > 1) {
+    const bool up = (lane & M) != 0;
+#pragma unroll
+    for (int i = 0; i < N / 2; ++i) {
+      const float send = up ? s[i] : s[i + N / 2];
+      const float keep = up ? s[i + N / 2] : s[i];
+      s[i] = keep + __shfl_xor(send, M, 64);
+    }
+    ao_reduce_scatter<N / 2, M / 2, RWt>(s, lane);
+  }
+}
+
 // Diagnostics (stamps != nullptr): 8 s_memrealtime stamps (100 MHz) per block, see llmc_attn_oproj.
 __device__ __forceinline__ void ao_stamp(uint64_t* st, int k, bool who) {
   if (st != nullptr && who) st[k] = __builtin_amdgcn_s_memrealtime();
@@ -123,10 +141,6 @@ __global__ __launch_bounds__(kAoThreads) void attn_oproj_kernel(
     // Unconditional: a wave without keys masks every score (its state stays empty); under a branch
     // hipcc would sink the last K/V load into it, behind the weights.
     st.compute(wk0, wend_c, lane, vbuf, scale_log2, kf, vs);
-    if constexpr (LATE) {  // weights behind the attention: the K/V loads do not queue behind them
-#pragma unroll
-      for (int j = 0; j < RW; ++j) wt[j] = load16<true>(wrow + static_cast<int64_t>(j) * K_o);
-    }
     ao_stamp(stp, 1, tid == 0);
   } else {
     st.issue(wk0, wend_ld, lane, row, k_cache, v_cache, kf, vs);
@@ -144,14 +158,24 @@ __global__ __launch_bounds__(kAoThreads) void attn_oproj_kernel(
   if (ct == kTicketThread) *flag = __hip_atomic_fetch_add(hctr, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == nc - 1;
   __syncthreads();
   ao_stamp(stp, 3, tid == 0);
+  if constexpr (LATE) {
+    // weights behind the whole attention step: the K/V loads never queue behind them, and a wave
+    // stalled issuing 32 KB of loads holds no barrier the control waves need before the next one
+    if (o_wave) {
+#pragma unroll
+      for (int j = 0; j < RW; ++j) wt[j] = load16<true>(wrow + static_cast<int64_t>(j) * K_o);
+    }
+  }
 
   // ---- 3. the last arriver of head g merges (control waves) and publishes head g's output ----
   uint32_t* hoff = handoff + static_cast<int64_t>(g) * Q * 4;  // Q 16-B units {bf16x2, tag, bf16x2, tag}
   const __amdgpu_buffer_rsrc_t hr = __builtin_amdgcn_make_buffer_rsrc(hoff, 0, Q * 16, 0x00020000);
   if (*flag) {
     f32x4 ms, acc;
-    merge_rows<G, D, 256>(rsrc, reinterpret_cast<const char*>(slab), 0, nsplit, tag_h, reinterpret_cast<f32x4*>(smem),
-                          o_wave ? 256 + tid : ct, ms, acc, fault);
+    // (16 rows in flight per thread would merge 32 partials in one pass, but spills the 32-row
+    // o waves' registers: measured slower)
+    merge_rows<G, D, 256>(rsrc, reinterpret_cast<const char*>(slab), 0, nsplit, tag_h,
+                              reinterpret_cast<f32x4*>(smem), o_wave ? 256 + tid : ct, ms, acc, fault);
     if (!o_wave && ct < Q) {
       const float inv = 1.f / ms[1];
       const uint32_t lo = pack_bf16x2(acc[0] * inv, acc[1] * inv), hi = pack_bf16x2(acc[2] * inv, acc[3] * inv);
@@ -185,7 +209,7 @@ __global__ __launch_bounds__(kAoThreads) void attn_oproj_kernel(
       b1 = ld8_atomic(hb, 24);
       if (__all(a0[1] == tag_h && a1[1] == tag_h && b0[1] == tag_h && b1[1] == tag_h)) break;
       if (spins >= kSpinLimit) {
-        if (lane == 0 && fault != nullptr) __hip_atomic_store(fault, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (lane == 0 && fault != nullptr) __hip_atomic_store(fault, 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         break;
       }
       __builtin_amdgcn_s_sleep(1);
@@ -202,17 +226,7 @@ __global__ __launch_bounds__(kAoThreads) void attn_oproj_kernel(
     const u32x4 x = xs[lane];
 #pragma unroll
     for (int j = 0; j < RW; ++j) s[j] = dot8_bf16(wt[j], x, 0.f);
-    // stage m: lanes with bit m keep the upper half of the live rows, the others the lower half
-#pragma unroll
-    for (int m = 32, n = RW; n > 1; m >>= 1, n >>= 1) {
-      const bool up = (lane & m) != 0;
-#pragma unroll
-      for (int i = 0; i < n / 2; ++i) {
-        const float send = up ? s[i] : s[i + n / 2];
-        const float keep = up ? s[i + n / 2] : s[i];
-        s[i] = keep + __shfl_xor(send, m, 64);
-      }
-    }
+    ao_reduce_scatter<RW, 32>(s, lane);
     constexpr int LPR = 64 / RW;  // lanes sharing one row after the stages (the low log2(LPR) bits)
 #pragma unroll
     for (int m = LPR / 2; m >= 1; m >>= 1) s[0] += __shfl_xor(s[0], m, 64);
@@ -244,7 +258,7 @@ __global__ __launch_bounds__(kAoThreads) void attn_oproj_kernel(
         if (gg < nkv) ok = ok && static_cast<uint32_t>(v[gg] >> 32) == tag_t;
       if (ok) break;
       if (spins >= kSpinLimit) {
-        if (fault != nullptr) __hip_atomic_store(fault, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (fault != nullptr) __hip_atomic_store(fault, 3, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         break;
       }
       __builtin_amdgcn_s_sleep(1);
@@ -298,7 +312,8 @@ extern "C" int llmc_attn_oproj_check(int H, int nh, int nkv, int D, int nc, int 
   return 0;
 }
 
-// mode bit 0: issue the o_proj weights after the attention sub-tile instead of right behind its K/V.
+// mode bit 0: issue the o_proj weights after the head ticket instead of right behind the K/V loads.
+// fault codes: 1 a partial never arrived (merge), 2 the head output never arrived, 3 a tile partial.
 // stamps (nullable, diagnostics): uint64 [nkv][nc][8] s_memrealtime per block: 0 start, 1 o wave 0's
 // attention done, 2 control wave 4's attention done, 3 head ticket taken, 4 head output in LDS,
 // 5 o wave 0's tile partial published, 6 tile ticket taken, 7 tile reduced (reducer only).

@@ -62,9 +62,9 @@ class EngineConfig:
     # than the five tuned kernels so far (docs/ARCHITECTURE.md, "Fused decode layer")
     fused_layer: bool = False
     # one-row engines without TP: decode attention + o_proj + residual as ONE launch per layer
-    # (csrc/kernels/attn_oproj.hip) for every context bucket it covers (<= 256 keys per block).
-    # Off unless LLMC_ATTN_OPROJ=1 until it beats the two launches (docs/ARCHITECTURE.md §8)
-    attn_oproj: bool = dataclasses.field(default_factory=lambda: os.environ.get("LLMC_ATTN_OPROJ", "0") == "1")
+    # (csrc/kernels/attn_oproj.hip) in the context buckets where it measured faster than the two
+    # launches (ops.ATTN_OPROJ_MIN_CHUNK); LLMC_ATTN_OPROJ=0 / =all: never / every bucket it covers
+    attn_oproj: bool = dataclasses.field(default_factory=lambda: os.environ.get("LLMC_ATTN_OPROJ", "1") != "0")
 
 
 FUSED_CHUNK_SMALL, FUSED_CHUNK_LARGE = 128, 256
@@ -269,7 +269,9 @@ class Engine:
                 and self.bs % 32 == 0):
             self.ao_nc = ops.attn_oproj_grid(c.hidden, self.nh, self.nkv, self.D)
             if self.ao_nc:
-                self.ao_chunks = [ops.attn_oproj_chunk(cap, self.ao_nc) for cap, _, _, _ in self.attn_buckets]
+                lo = 32 if os.environ.get("LLMC_ATTN_OPROJ") == "all" else ops.ATTN_OPROJ_MIN_CHUNK
+                self.ao_chunks = [ch if ch >= lo else 0
+                                  for ch in (ops.attn_oproj_chunk(cap, self.ao_nc) for cap, _, _, _ in self.attn_buckets)]
                 self.ao_ws = ops.attn_oproj_workspace(c.hidden, self.nh, self.nkv, self.D, self.ao_nc, dev)
         # set by a decode-attention merger that gave up on a partial (checked after every decode)
         self.attn_fault = torch.zeros(1, dtype=torch.int32, device=dev) if self.on_gpu else None

@@ -223,7 +223,11 @@ def attn_decode(q, k_cache, v_cache, block_tables, seq_lens, out, part, counters
 
 
 ATTN_OPROJ_MAX_CHUNK = 256  # attn_oproj: keys per block at most (8 waves x one 32-key sub-tile)
-ATTN_OPROJ_MODE = int(os.environ.get("LLMC_ATTN_OPROJ_MODE", "0"))  # kernel mode bits (A/B runs)
+ATTN_OPROJ_MODE = int(os.environ.get("LLMC_ATTN_OPROJ_MODE", "1"))  # kernel mode bits (A/B runs)
+# engines take the fused launch only for buckets of >= this many keys per block: below, the two
+# launches measured faster (profiles/r3_attn_oproj.md: 8B at 2k keys 18.5 vs 16.3 us, at 6k-8k
+# keys 18.8-21.5 vs 20.9-23.4)
+ATTN_OPROJ_MIN_CHUNK = 256
 
 
 def attn_oproj_grid(H: int, nh: int, nkv: int, D: int) -> int:

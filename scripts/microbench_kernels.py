@@ -113,6 +113,7 @@ def bench_attn_oproj(shapes=((32, 8, 128, 4096),), lens=(128, 1024, 2048, 2300, 
             ws = ops.attn_oproj_workspace(H, nh, nkv, D, nc, "cuda")
             part, ctr = ops.decode_attn_workspace(1, nh, nkv, D, max(gc2, 32), "cuda")
             fault = torch.zeros(1, dtype=torch.int32, device="cuda")
+            fault1 = torch.zeros(1, dtype=torch.int32, device="cuda")
             it = [0]
 
             def two():
@@ -125,7 +126,7 @@ def bench_attn_oproj(shapes=((32, 8, 128, 4096),), lens=(128, 1024, 2048, 2300, 
             def one(mode=0):
                 kc, vc, bt, sl, q, out = cases[it[0] % copies]
                 ops.attn_oproj(q, kc, vc, bt, sl, wos[it[0] % copies], h, attn, ws, nh, nkv, D, 64, chunk, nc, sc,
-                               fault=fault, mode=mode)
+                               fault=fault1, mode=mode)
                 it[0] += 1
 
             n = copies * max(1, 48 // copies)
@@ -135,7 +136,7 @@ def bench_attn_oproj(shapes=((32, 8, 128, 4096),), lens=(128, 1024, 2048, 2300, 
             torch.cuda.synchronize()
             print(f"attn+o nh={nh} nkv={nkv} D={D} H={H} L={L:5d} cap={cap}: two launches "
                   f"({'fused' if fused2 else 'split'} c{ch2} g{gc2} + o GEMV) {t2:6.2f} us | one launch "
-                  f"(nc {nc}, {chunk} keys/block) {t1:6.2f} us, late weights {t1l:6.2f} us | fault {int(fault.item())}",
+                  f"(nc {nc}, {chunk} keys/block) {t1:6.2f} us, late weights {t1l:6.2f} us | fault {int(fault.item())} / {int(fault1.item())}",
                   flush=True)
             del cases, wos
 

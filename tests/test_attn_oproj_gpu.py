@@ -119,9 +119,11 @@ def test_attn_oproj_graph_replay_and_length_changes(cuda):
 
 
 @pytest.mark.parametrize("name,plen", [("llama-small", 90), ("llama-small", 1500), ("llama-small", 5000)])
-def test_engine_attn_oproj_matches_two_launch_step(cuda, name, plen):
+def test_engine_attn_oproj_matches_two_launch_step(cuda, name, plen, monkeypatch):
     """Teacher-forced decode logits of a one-row engine with the fused attention + o_proj launch
-    against the same weights on the two-launch step; graph replay == eager for the fused path."""
+    (in every bucket it covers: LLMC_ATTN_OPROJ=all) against the same weights on the two-launch
+    step; graph replay == eager for the fused path."""
+    monkeypatch.setenv("LLMC_ATTN_OPROJ", "all")
     cfg = FAMILIES[name]
     w = TransformerWeights(cfg, TPGroup.single(), torch.device("cuda:0"), seed=21)
     ctx = plen + 64

@@ -18,6 +18,9 @@ def timeit(fn, iters=50, warm=5):
     """Device time per call: `iters` calls captured in one HIP graph, replayed 10x (no host
     launch overhead; includes the inter-kernel boundary as in the real decode graph)."""
     s = torch.cuda.Stream()
+    # the side stream must see every buffer the default stream initialised (a workspace still being
+    # zeroed when the first launches ran left stale counters: a merger then gave up on a partial)
+    s.wait_stream(torch.cuda.current_stream())
     with torch.cuda.stream(s):
         for _ in range(warm):
             fn()

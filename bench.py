@@ -22,6 +22,9 @@ and decodes ``--max-tokens`` tokens.
   of config 3). ``--judge-tp 1`` puts the judge on the least-loaded GPU instead:
   ``--gpus 4 --n-models 3 --judge-tp 1`` is config 2 and ``--gpus 8 --judge-tp 1`` config 3 as
   BASELINE.json words them.
+* ``--shared-weights`` (fanout, secondary preset, never the default): the replicas placed whole on
+  one GPU share ONE weight copy and decode as rows of one batching engine (each with its own
+  sampling seed) — BASELINE config 2's "replicas" taken literally; ``config.name`` says so.
 * ``4``: 2 x Llama-3-70B responders, each TP=N/2 over its half of the node (RCCL + custom xGMI
   all-reduce), + Llama-3-8B judge. Needs an even N >= 2.
 * ``5``: mixed fleet — Mixtral-8x7B (MoE grouped GEMM) + Llama-3-8B + Phi-3-mini responders, one
@@ -247,6 +250,9 @@ def main() -> None:
     ap.add_argument("--prompt-tokens", type=int, default=128)
     ap.add_argument("--temperature", type=float, default=1.0)
     ap.add_argument("--judge-tp", type=int, default=0, help="0 = auto (config 5: 4)")
+    ap.add_argument("--shared-weights", action="store_true",
+                    help="fanout secondary preset: the replicas placed whole on one GPU share ONE weight copy and "
+                         "decode as rows of one engine (config.name says so; never the default)")
     ap.add_argument("--steps-per-graph", type=int, default=8)
     ap.add_argument("--no-graphs", action="store_true")
     ap.add_argument("--time-budget", type=float, default=560.0,
@@ -340,8 +346,20 @@ def main() -> None:
         return tp
 
     t0 = time.time()
-    responders = []  # (index, engine, prompt ids, tokenizer)
+    # responder engines: (plan indices, engine, prompt ids, tokenizer); one index per engine, or
+    # with --shared-weights every replica placed whole on the same GPU as a row of one engine
+    groups: List[List[int]] = []
     for i, e in enumerate(resp_plan):
+        key = (e["family"], tuple(e["ranks"]))
+        g = next((g for g in groups if args.shared_weights and len(e["ranks"]) == 1
+                  and (resp_plan[g[0]]["family"], tuple(resp_plan[g[0]]["ranks"])) == key), None)
+        if g is None:
+            groups.append([i])
+        else:
+            g.append(i)
+    responders = []
+    for idx in groups:
+        e = resp_plan[idx[0]]
         tp = tp_group(e["ranks"])
         if tp is None:
             continue
@@ -351,9 +369,10 @@ def main() -> None:
         ctx = len(ids) + args.max_tokens + 64
         graphs = not args.no_graphs and (tp.size == 1 or tp.custom is not None
                                          or (not on_cpu and tp.graph_capture_ok(dev)))
+        name = e["name"] if len(idx) == 1 else "+".join(resp_plan[i]["name"] for i in idx)
         eng = Engine(cfg, EngineConfig(device=dev, max_context=ctx, seed=e["seed"], steps_per_graph=args.steps_per_graph,
-                                       use_graphs=graphs), tp=tp, name=e["name"])
-        responders.append((i, eng, ids, tok))
+                                       use_graphs=graphs, max_batch=len(idx)), tp=tp, name=name)
+        responders.append((idx, eng, ids, tok))
     jtp_grp = tp_group(judge_plan["ranks"])
     judge = None
     judge_ctx = 0
@@ -405,18 +424,29 @@ def main() -> None:
 
         def run_one(j):
             try:
-                i, e, ids, _ = responders[j]
-                prog = Progress(f"round {step}: responder {i}") if (rank == 0 and j == 0) else None
+                idx, e, ids, _ = responders[j]
+                prog = Progress(f"round {step}: responder {idx[0]}") if (rank == 0 and j == 0) else None
 
-                def on_tokens(new, i=i, prog=prog):
+                def on_tokens(r, new, prog=prog):
+                    i = idx[r]
                     if times[i, 0] == 0:
                         times[i, 0] = time.perf_counter() - t_start
-                    if prog is not None:
+                    if prog is not None and r == 0:
                         prog(new)
 
-                outs[i] = e.generate_ids(ids, max_tokens, temperature=args.temperature,
-                                         seed=1000 * step + i + 1, stop_on_eos=False, on_tokens=on_tokens)
-                times[i, 1] = time.perf_counter() - t_start
+                if len(idx) == 1:
+                    outs[idx[0]] = e.generate_ids(ids, max_tokens, temperature=args.temperature,
+                                                  seed=1000 * step + idx[0] + 1, stop_on_eos=False,
+                                                  on_tokens=lambda new: on_tokens(0, new))
+                else:  # replicas of one weight copy: rows of one batch, each with its own sampling seed
+                    res = e.generate_batch([list(ids) for _ in idx],
+                                           [SamplingParams(max_tokens, args.temperature, 1.0, 0, 1000 * step + i + 1,
+                                                           False) for i in idx], on_tokens=on_tokens)
+                    for i, r in zip(idx, res):
+                        outs[i] = r
+                done = time.perf_counter() - t_start
+                for i in idx:
+                    times[i, 1] = done
             except BaseException as ex:  # noqa: BLE001
                 errs.append(ex)
 
@@ -433,12 +463,13 @@ def main() -> None:
         # gather every response to every rank: the leader of each responder writes its row
         # (token + 1; 0 = empty) and one SUM all-reduce assembles the table
         table = torch.zeros((n_resp, max_tokens), dtype=torch.int32)
-        for i, e, _, _ in responders:
-            if e.tp.is_leader:
-                r = torch.tensor(outs[i], dtype=torch.int32) + 1
-                table[i, : r.numel()] = r
-            else:
-                times[i] = 0.0  # the leader's clock reports this responder
+        for idx, e, _, _ in responders:
+            for i in idx:
+                if e.tp.is_leader:
+                    r = torch.tensor(outs[i], dtype=torch.int32) + 1
+                    table[i, : r.numel()] = r
+                else:
+                    times[i] = 0.0  # the leader's clock reports this responder
         if world > 1:
             tt = table.to(cdev)
             dist.all_reduce(tt)
@@ -557,7 +588,8 @@ def main() -> None:
         resp_tok_s = n_resp * round_tokens * args.steps / sum(p["responders_s"] for p in per_step)
         jtp = len(judge_plan["ranks"])
         rtp = sorted({len(e["ranks"]) for e in resp_plan if len(e["ranks"]) > 1})
-        par = {"fanout": f"fanout{n_resp}" + "".join(f"-resp_tp{t}" for t in rtp),
+        par = {"fanout": f"fanout{n_resp}" + "".join(f"-resp_tp{t}" for t in rtp)
+               + ("-shared_weights" if any(len(g) > 1 for g, _, _, _ in responders) else ""),
                "4": f"fanout2-tp{len(resp_plan[0]['ranks'])}", "5": "fanout3-mixed"}[args.config]
         out = {
             "metric": METRIC,
@@ -574,7 +606,9 @@ def main() -> None:
             "dtype": "bf16",
             "data": "synthetic prompt (synthetic tokenizer), random-init weights",
             "config": {
-                "name": config_name(args, n_gpus, resp_plan, judge_plan),
+                "name": config_name(args, n_gpus, resp_plan, judge_plan)
+                + (" [secondary preset: replicas on one GPU share one weight copy, batched as rows of one engine]"
+                   if args.shared_weights else ""),
                 "model": describe(resp_plan, judge_plan),
                 "global_batch": n_resp,
                 "seq_len": args.prompt_tokens + round_tokens,

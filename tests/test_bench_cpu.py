@@ -40,6 +40,18 @@ def test_fanout_one_rank_runs_judge():
     _tokens_ok(d, 12)
 
 
+def test_shared_weights_preset_batches_replicas_as_rows():
+    """--shared-weights: the three replicas on the one GPU are rows of ONE engine (one weight copy),
+    every responder still returns its own tokens and per-model timings; the config name and the
+    parallelism label say it is the secondary preset."""
+    d = _run(1, ["--shapes", "tiny", "--steps", "1", "--warmup", "1", "--max-tokens", "12", "--shared-weights"], 0)
+    assert d["config"]["global_batch"] == 3
+    assert "secondary preset" in d["config"]["name"] and d["config"]["parallelism"].endswith("-shared_weights")
+    _tokens_ok(d, 12)
+    lat = d["extra"]["per_model_latency_ms"]
+    assert len(set(lat.values())) == 1  # one batch: every replica finishes with it
+
+
 def test_config4_two_tp_groups():
     d = _run(4, ["--config", "4", "--shapes", "tiny", "--steps", "1", "--warmup", "0", "--max-tokens", "12"], 29691)
     assert d["config"]["name"] == "BASELINE config 4" and d["scaling"] == "strong"

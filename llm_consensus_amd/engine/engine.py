@@ -885,7 +885,8 @@ class Engine:
             attn_bad = self.tp.any_rank(attn_bad)
         if attn_bad:
             raise EngineError("decode attention: a partial merge timed out (a block never published its "
-                              "partial, or a fused layer step's wait gave up): this request's tokens are invalid")
+                              "partial, or a fused layer / attention + o_proj hand-off wait gave up): this "
+                              "request's tokens are invalid")
 
     def _bind_rows(self, seqs: List[Sequence], params: List[SamplingParams]) -> None:
         """Bind sequences to decode rows 0..B-1: block tables, prefill logits and sampling state."""

@@ -185,3 +185,47 @@ def test_engine_rejects_more_rows_than_the_decode_forms_take():
     with pytest.raises(EngineError):
         Engine(FAMILIES["llama-tiny"], EngineConfig(device="cpu", max_context=64, max_batch=33))
     Engine(FAMILIES["llama-tiny"], EngineConfig(device="cpu", max_context=64, max_batch=32))
+
+
+def test_attn_oproj_bucket_chunks():
+    """Keys per block of the fused attention + o_proj launch: the bucket capacity over the grid,
+    in 32-key sub-tiles, 0 above 256 keys per block (the kernel's one sub-tile per wave)."""
+    from llm_consensus_amd import ops
+
+    nc = 32
+    assert [ops.attn_oproj_chunk(c, nc) for c in (100, 1024, 2048, 4096, 8192, 8193, 16384)] == \
+        [32, 32, 64, 128, 256, 0, 0]
+    for cap in range(1, 8193, 97):
+        ch = ops.attn_oproj_chunk(cap, nc)
+        assert ch % 32 == 0 and ch * nc >= cap and (ch == 32 or (ch - 32) * nc < cap)
+    assert ops.ATTN_OPROJ_MIN_CHUNK <= ops.ATTN_OPROJ_MAX_CHUNK
+
+
+def test_attn_oproj_cpu_path_is_attention_then_residual_o_proj():
+    """The op's CPU path (the oracle) is exactly attention -> o_proj -> += residual on row 0."""
+    import math
+
+    from llm_consensus_amd import ops
+    from llm_consensus_amd.ops import EPI_RESADD, oracle
+
+    torch.manual_seed(0)
+    nh, nkv, D, H, bs, L = 4, 2, 16, 32, 16, 37
+    nb = 5
+    kc = torch.randn(nb, nkv, bs, D).to(torch.bfloat16)
+    vc = torch.randn(nb, nkv, bs, D).to(torch.bfloat16)
+    bt = torch.tensor([[3, 0, 4, 1]], dtype=torch.int32)
+    sl = torch.tensor([L], dtype=torch.int32)
+    q = torch.randn(1, nh * D).to(torch.bfloat16)
+    w_o = torch.randn(H, nh * D).to(torch.bfloat16)
+    h = torch.randn(1, H).to(torch.bfloat16)
+    h1, attn = h.clone(), torch.zeros(1, nh * D, dtype=torch.bfloat16)
+    ops.attn_oproj(q, kc, vc, bt, sl, w_o, h1, attn, None, nh, nkv, D, bs, 32, 2, 1 / math.sqrt(D))
+    a = oracle.attn_decode(q, kc, vc, bt, sl, nh, nkv, D, bs, 1 / math.sqrt(D))
+    h2 = h.clone()
+    oracle.linear(a, w_o, EPI_RESADD, h2)
+    assert torch.equal(attn, a) and torch.equal(h1, h2)
+
+
+def test_cpu_engines_never_take_the_fused_attention_oproj():
+    eng = Engine(FAMILIES["llama-tiny"], EngineConfig(device="cpu", max_context=256, attn_oproj=True))
+    assert eng.ao_nc == 0 and not any(eng.ao_chunks)

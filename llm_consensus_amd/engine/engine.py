@@ -265,8 +265,8 @@ class Engine:
         # two launches)
         self.ao_chunks: List[int] = [0] * len(self.attn_buckets)
         self.ao_nc = 0
-        if (self.on_gpu and self.ecfg.attn_oproj and B == 1 and self.tp.size == 1 and not self.fused_layer
-                and self.bs % 32 == 0):
+        if (self.on_gpu and self.ecfg.attn_oproj and B == 1 and not self.fused_layer and self.bs % 32 == 0
+                and (self.tp.size == 1 or ops.ATTN_OPROJ_TP)):
             self.ao_nc = ops.attn_oproj_grid(c.hidden, self.nh, self.nkv, self.D)
             if self.ao_nc:
                 lo = 32 if os.environ.get("LLMC_ATTN_OPROJ") == "all" else ops.ATTN_OPROJ_MIN_CHUNK
@@ -590,9 +590,11 @@ class Engine:
                          self.slots[:B], self.cos_t, self.sin_t, self.nh, self.nkv, self.D, self.bs,
                          mfma=self.mfma_decode)
             if ao_chunk:
+                # row-parallel under TP: rank 0's partial carries the residual, then the all-reduce
                 ops.attn_oproj(q, self.k_cache[li], self.v_cache[li], self.block_tables[:1], self.seq_lens[:1], Lw.w_o,
                                h, attn, self.ao_ws, self.nh, self.nkv, self.D, self.bs, ao_chunk, self.ao_nc,
-                               self.scale, fault=self.attn_fault)
+                               self.scale, fault=self.attn_fault, residual=self.tp.rank == 0)
+                self.tp.all_reduce_(h)
             else:
                 ops.attn_decode(q, self.k_cache[li], self.v_cache[li], self.block_tables[:B], self.seq_lens[:B], attn,
                                 part[:B], self.attn_counters[:B], self.nh, self.nkv, self.D, self.bs, chunk,

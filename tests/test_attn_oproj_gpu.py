@@ -84,6 +84,23 @@ def test_attn_oproj_vs_oracle_and_two_launches(cuda, nh, nkv, D, H, L, cap):
     assert torch.equal(c[:nkv, 1], torch.full((nkv,), 3, dtype=torch.int32)) and int(c[nkv + nc, 1]) == 3
 
 
+def test_attn_oproj_partial_without_residual(cuda):
+    """residual=False (a TP rank other than 0): h = o_proj(attention), the old h ignored."""
+    nh, nkv, D, H, bs, L = 32, 8, 128, 4096, 64, 1500
+    nc = ops.attn_oproj_grid(H, nh, nkv, D)
+    chunk = ops.attn_oproj_chunk(2048, nc)
+    kc, vc, bt, sl, q, w_o, h0 = _case(L, nh, nkv, D, H, bs, seed=9)
+    scale = 1 / math.sqrt(D)
+    _, h_ref = _reference(kc, vc, bt, sl, q, w_o, torch.zeros_like(h0), nh, nkv, D, bs, scale)
+    ws = ops.attn_oproj_workspace(H, nh, nkv, D, nc, "cuda")
+    h = h0.clone()
+    attn = torch.zeros(1, nh * D, dtype=BF, device="cuda")
+    ops.attn_oproj(q, kc, vc, bt.cuda(), sl.cuda(), w_o, h, attn, ws, nh, nkv, D, bs, chunk, nc, scale,
+                   residual=False)
+    err = (h.float().cpu() - h_ref).abs().max().item()
+    assert err < 2e-2 * max(1.0, h_ref.abs().max().item()), err
+
+
 def test_attn_oproj_graph_replay_and_length_changes(cuda):
     """Captured once, replayed while the length grows across chunk boundaries (blocks without keys
     still take their tickets and do their o_proj rows)."""

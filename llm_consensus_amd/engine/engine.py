@@ -62,9 +62,14 @@ class EngineConfig:
     # than the five tuned kernels so far (docs/ARCHITECTURE.md, "Fused decode layer")
     fused_layer: bool = False
     # one-row engines without TP: decode attention + o_proj + residual as ONE launch per layer
-    # (csrc/kernels/attn_oproj.hip) in the context buckets where it measured faster than the two
-    # launches (ops.ATTN_OPROJ_MIN_CHUNK); LLMC_ATTN_OPROJ=0 / =all: never / every bucket it covers
+    # (csrc/kernels/attn_oproj.hip) in the context buckets with at least ``attn_oproj_min_chunk``
+    # keys per block (ops.ATTN_OPROJ_MIN_CHUNK: where it measured faster than the two launches).
+    # Environment defaults (A/B runs): LLMC_ATTN_OPROJ=0 never, =all every bucket it covers;
+    # LLMC_ATTN_OPROJ_TP=1 also on tensor-parallel ranks (measured slower there: off)
     attn_oproj: bool = dataclasses.field(default_factory=lambda: os.environ.get("LLMC_ATTN_OPROJ", "1") != "0")
+    attn_oproj_min_chunk: int = dataclasses.field(
+        default_factory=lambda: 32 if os.environ.get("LLMC_ATTN_OPROJ") == "all" else ops.ATTN_OPROJ_MIN_CHUNK)
+    attn_oproj_tp: bool = dataclasses.field(default_factory=lambda: os.environ.get("LLMC_ATTN_OPROJ_TP", "0") == "1")
 
 
 FUSED_CHUNK_SMALL, FUSED_CHUNK_LARGE = 128, 256
@@ -266,10 +271,10 @@ class Engine:
         self.ao_chunks: List[int] = [0] * len(self.attn_buckets)
         self.ao_nc = 0
         if (self.on_gpu and self.ecfg.attn_oproj and B == 1 and not self.fused_layer and self.bs % 32 == 0
-                and (self.tp.size == 1 or ops.ATTN_OPROJ_TP)):
+                and (self.tp.size == 1 or self.ecfg.attn_oproj_tp)):
             self.ao_nc = ops.attn_oproj_grid(c.hidden, self.nh, self.nkv, self.D)
             if self.ao_nc:
-                lo = 32 if os.environ.get("LLMC_ATTN_OPROJ") == "all" else ops.ATTN_OPROJ_MIN_CHUNK
+                lo = self.ecfg.attn_oproj_min_chunk
                 self.ao_chunks = [ch if ch >= lo else 0
                                   for ch in (ops.attn_oproj_chunk(cap, self.ao_nc) for cap, _, _, _ in self.attn_buckets)]
                 self.ao_ws = ops.attn_oproj_workspace(c.hidden, self.nh, self.nkv, self.D, self.ao_nc, dev)

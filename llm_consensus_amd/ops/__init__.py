@@ -228,9 +228,6 @@ ATTN_OPROJ_MODE = int(os.environ.get("LLMC_ATTN_OPROJ_MODE", "1"))  # kernel mod
 # launches measured faster (profiles/r3_attn_oproj.md: 8B at 2k keys 18.5 vs 16.3 us, at 6k-8k
 # keys 18.8-21.5 vs 20.9-23.4)
 ATTN_OPROJ_MIN_CHUNK = 256
-# tensor-parallel one-row engines (the bench judge at N >= 2) may take it too (a rank's partial, then
-# the all-reduce); LLMC_ATTN_OPROJ_TP=1 (A/B until measured on the rank shards)
-ATTN_OPROJ_TP = os.environ.get("LLMC_ATTN_OPROJ_TP", "0") == "1"
 
 
 def attn_oproj_grid(H: int, nh: int, nkv: int, D: int) -> int:

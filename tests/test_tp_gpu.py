@@ -37,10 +37,8 @@ def _worker(rank, world, port, name, q, ekw=None):
         e = Engine(FAMILIES[name], EngineConfig(device="cuda:0", max_context=512, seed=5, **(ekw or {})), tp=tp)
         import os
 
-        from llm_consensus_amd import ops
-
         if os.environ.get("LLMC_ATTN_OPROJ_TP") == "1":  # the fused-path test: it must be taken
-            assert ops.ATTN_OPROJ_TP and e.ao_nc > 0 and any(e.ao_chunks), (e.ao_nc, e.ao_chunks)
+            assert e.ecfg.attn_oproj_tp and e.ao_nc > 0 and any(e.ao_chunks), (e.ao_nc, e.ao_chunks)
         e.warmup_graphs()
         s = e.new_sequence()
         e.prefill([s], [PROMPT])

@@ -3,9 +3,11 @@
 //
 // Why (profiles/r2_dec2k_kernel_stats.md, 8B at 2k keys): as two launches the attention is a
 // latency chain (10.6 us for ~10 MB of K/V) and o_proj pays its own boundary + ramp (7.2 us for
-// 34 MB, 4.7 TB/s). Here the o_proj weights are requested right behind the K/V loads, so they
-// stream while the attention computes and merges; when the merged attention output arrives the
-// projection is arithmetic on registers.
+// 34 MB, 4.7 TB/s). Here the o_proj weights stream while the attention merges and hands off; when
+// the merged head output arrives the projection is arithmetic on registers. Measured
+// (profiles/r3_attn_oproj.md): faster than the two launches only where the attention is long
+// (6k-8k keys: 18.9-21.5 vs 20.9-23.3 us), slower at <= 4k and on TP ranks; the engine takes it
+// for 256-key blocks (ops.ATTN_OPROJ_MIN_CHUNK).
 //
 // Grid: (nc, nkv) blocks of 8 waves; block (c, g) = kv head g x the fixed key range
 // [c * chunk, (c + 1) * chunk) (<= 256 keys: one 32-key MFMA sub-tile per wave, attn_core.h) AND
@@ -14,7 +16,8 @@
 // each lane one 16-B column chunk per row (G D = 512).
 //
 //   1. one round trip for Q, L, the wave's page id and the two epochs; K/V of the wave's
-//      sub-tile; the block's o_proj weight tile (nt loads, in flight from here on)
+//      sub-tile; the block's o_proj weight tile (nt loads) right behind the K/V (mode 0) or after
+//      the head ticket of step 2 (mode 1, the default: the K/V never queue behind the weights)
 //   2. attention sub-tile -> block state -> partial granules (attn_core.h publish) and a ticket
 //      on head g's counter (EVERY block of head g takes one, keys or not)
 //   3. the last arriver of head g merges the partials and publishes head g's output (bf16) as

@@ -10,7 +10,8 @@
 // for 256-key blocks (ops.ATTN_OPROJ_MIN_CHUNK).
 //
 // Grid: (nc, nkv) blocks of 8 waves; block (c, g) = kv head g x the fixed key range
-// [c * chunk, (c + 1) * chunk) (<= 256 keys: one 32-key MFMA sub-tile per wave, attn_core.h) AND
+// [c * chunk, (c + 1) * chunk) (<= 256 keys: one 32-key MFMA sub-tile per wave, attn_core.h; <= 512:
+// two, with the weights requested late so the second sub-tile's registers are free) AND
 // the o_proj tile rows [c R, (c + 1) R) x input columns of head group g (its G query heads):
 // R = H / nc rows, R / 4 per o wave (waves 0-3; waves 4-7 run the latency chain, see "Roles"),
 // each lane one 16-B column chunk per row (G D = 512).
@@ -62,7 +63,7 @@ __device__ __forceinline__ void ao_stamp(uint64_t* st, int k, bool who) {
   if (st != nullptr && who) st[k] = __builtin_amdgcn_s_memrealtime();
 }
 
-template <int G, int D, int RW, bool LATE>
+template <int G, int D, int RW, bool LATE, int SUBS>
 __global__ __launch_bounds__(kAoThreads) void attn_oproj_kernel(
     const bf16_t* __restrict__ q, const bf16_t* __restrict__ k_cache, const bf16_t* __restrict__ v_cache,
     const int32_t* __restrict__ block_table, int bt_len, const int32_t* __restrict__ seq_len,
@@ -72,6 +73,7 @@ __global__ __launch_bounds__(kAoThreads) void attn_oproj_kernel(
     uint64_t* __restrict__ stamps) {
   static_assert(G * D == 512, "one 16-B column chunk per lane per row");
   static_assert(RW >= 1 && RW <= 32 && (RW & (RW - 1)) == 0, "rows per wave: power of two <= 32");
+  static_assert(SUBS == 1 || (SUBS == 2 && LATE), "two sub-tiles per wave only with late weights (registers)");
   using ST = SubTile<G, D>;
   constexpr int HQ = D / 4, RU = HQ + 1, Q = G * HQ;  // 16-B units: per head, per partial row, per group
   constexpr int R = 4 * RW;                              // o_proj rows per block (4 o waves)
@@ -88,7 +90,7 @@ __global__ __launch_bounds__(kAoThreads) void attn_oproj_kernel(
   const uint32_t tag_t = static_cast<uint32_t>(__hip_atomic_load(xctr + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) + 1u;
   const int L = ld_scalar(seq_len);
   const int key_lo = c * chunk;
-  const int wk0 = key_lo + wave * 32;  // this wave's 32-key sub-tile (one page: bs % 32 == 0)
+  const int wk0 = key_lo + wave * 32 * SUBS;  // this wave's SUBS 32-key sub-tiles (one page: bs % (32 SUBS) == 0)
   const int pidx = __builtin_amdgcn_readfirstlane(min(wk0 / bs, bt_len - 1));
   const int page = min(max(ld_scalar(block_table + pidx), 0), nblocks - 1);  // clamped into the cache
   ST st;
@@ -104,18 +106,22 @@ __global__ __launch_bounds__(kAoThreads) void attn_oproj_kernel(
   u32x4* xs = reinterpret_cast<u32x4*>(red + kAoWaves * G * (D + 2));      // head g's output, 64 chunks
   int* flag = reinterpret_cast<int*>(xs + 64);
 
-  bf16x8 kf[2][ST::KS];
-  u32x4 vs[ST::NV];
-  const int wend = min(key_hi, wk0 + 32);
+  bf16x8 kf[2][ST::KS], kf2[2][ST::KS];
+  u32x4 vs[ST::NV], vs2[ST::NV];
   const int64_t kvbase = (static_cast<int64_t>(page) * nkv + g) * bs * D;
-  // a wave without keys issues its loads anyway, all at one row of its page (L2 hits): loads under
-  // a branch would end in a register merge at the join that waits for them before the weights issue
-  auto row = [&](const bf16_t* cache, int key) {
-    return cache + kvbase + (wave_keys ? static_cast<int64_t>(key % bs) * D : 0);
+  // sub-tile t: keys [k0_t, k0_t + 32) of the wave. A sub-tile without keys issues its loads anyway,
+  // all at one row of the page (L2 hits): loads under a branch would end in a register merge at
+  // the join that waits for them before the weights issue; its scores are all masked (end = k0_t)
+  const int k0_0 = wk0, k0_1 = wk0 + 32;
+  const bool has0 = wave_keys, has1 = SUBS == 2 && k0_1 < key_hi;
+  const int end_ld0 = has0 ? min(key_hi, k0_0 + 32) : k0_0 + 1, end_c0 = has0 ? min(key_hi, k0_0 + 32) : k0_0;
+  const int end_ld1 = has1 ? min(key_hi, k0_1 + 32) : k0_1 + 1, end_c1 = has1 ? min(key_hi, k0_1 + 32) : k0_1;
+  auto row0 = [&](const bf16_t* cache, int key) {
+    return cache + kvbase + (has0 ? static_cast<int64_t>(key % bs) * D : 0);
   };
-  // keys [wk0, wend_ld) are loaded; a wave without keys loads one (masked below: end = wk0 masks all)
-  const int wend_ld = wave_keys ? wend : wk0 + 1;
-  const int wend_c = wave_keys ? wend : wk0;
+  auto row1 = [&](const bf16_t* cache, int key) {
+    return cache + kvbase + (has1 ? static_cast<int64_t>(key % bs) * D : 0);
+  };
 
   // Roles. The vector memory counter retires in order, so a wave with o_proj weights in flight
   // cannot use any later load's result (a ticket's return value, a merge or poll load) before its
@@ -134,7 +140,8 @@ __global__ __launch_bounds__(kAoThreads) void attn_oproj_kernel(
   u32x4 wt[RW];
   const bf16_t* wrow = w_o + static_cast<int64_t>(c * R + wave * RW) * K_o + g * G * D + 8 * lane;
   if (o_wave) {
-    st.issue(wk0, wend_ld, lane, row, k_cache, v_cache, kf, vs);
+    st.issue(k0_0, end_ld0, lane, row0, k_cache, v_cache, kf, vs);
+    if constexpr (SUBS == 2) st.issue(k0_1, end_ld1, lane, row1, k_cache, v_cache, kf2, vs2);
     __builtin_amdgcn_sched_barrier(0);  // every K/V load issues before the first weight load
     if constexpr (!LATE) {
 #pragma unroll
@@ -144,11 +151,14 @@ __global__ __launch_bounds__(kAoThreads) void attn_oproj_kernel(
     // ---- 2. attention sub-tile (K/V were issued before the weights: the wait leaves them in flight).
     // Unconditional: a wave without keys masks every score (its state stays empty); under a branch
     // hipcc would sink the last K/V load into it, behind the weights.
-    st.compute(wk0, wend_c, lane, vbuf, scale_log2, kf, vs);
+    st.compute(k0_0, end_c0, lane, vbuf, scale_log2, kf, vs);
+    if constexpr (SUBS == 2) st.compute(k0_1, end_c1, lane, vbuf, scale_log2, kf2, vs2);
     ao_stamp(stp, 1, tid == 0);
   } else {
-    st.issue(wk0, wend_ld, lane, row, k_cache, v_cache, kf, vs);
-    st.compute(wk0, wend_c, lane, vbuf, scale_log2, kf, vs);
+    st.issue(k0_0, end_ld0, lane, row0, k_cache, v_cache, kf, vs);
+    if constexpr (SUBS == 2) st.issue(k0_1, end_ld1, lane, row1, k_cache, v_cache, kf2, vs2);
+    st.compute(k0_0, end_c0, lane, vbuf, scale_log2, kf, vs);
+    if constexpr (SUBS == 2) st.compute(k0_1, end_c1, lane, vbuf, scale_log2, kf2, vs2);
     ao_stamp(stp, 2, ct == 0);
   }
   // ---- ... -> block state -> partial -> head ticket ----
@@ -292,12 +302,15 @@ using namespace llmc;
 template <int G, int D, int RW>
 static void ao_set_lds() {
   static bool done = false;  // one flag per instantiation
-  const auto kern = attn_oproj_kernel<G, D, RW, false>;
-  const auto kern_late = attn_oproj_kernel<G, D, RW, true>;
+  const auto kern = attn_oproj_kernel<G, D, RW, false, 1>;
+  const auto kern_late = attn_oproj_kernel<G, D, RW, true, 1>;
+  const auto kern_two = attn_oproj_kernel<G, D, RW, true, 2>;
   if (!done) {
     (void)hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize,
                               160 * 1024);
     (void)hipFuncSetAttribute(reinterpret_cast<const void*>(kern_late), hipFuncAttributeMaxDynamicSharedMemorySize,
+                              160 * 1024);
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(kern_two), hipFuncAttributeMaxDynamicSharedMemorySize,
                               160 * 1024);
     done = true;
   }
@@ -332,9 +345,13 @@ extern "C" int llmc_attn_oproj(const void* q, const void* k_cache, const void* v
                                hipStream_t s) {
   const int K_o = nh * D;
   if (llmc_attn_oproj_check(H, nh, nkv, D, nc, K_o) != 0 || nkv > kAoMaxKv) return -1;
-  const bool late = (mode & 1) != 0;  // o_proj weights issued after the head ticket
+  // up to 256 keys per block: one 32-key sub-tile per wave; up to 512: two (late weights only)
+  const bool two = chunk > kAoWaves * 32;
+  if (chunk < 32 || chunk > kAoWaves * 64 || chunk % (two ? 64 : 32) != 0 || bs % (two ? 64 : 32) != 0 ||
+      bt_len < 1 || nblocks < 1)
+    return -1;
+  const bool late = (mode & 1) != 0 || two;  // o_proj weights issued after the head ticket
   const int resid = (mode & 2) ? 0 : 1;  // bit 1: h = the o_proj partial (TP rank != 0), no residual
-  if (chunk < 32 || chunk > kAoWaves * 32 || chunk % 32 != 0 || bs % 32 != 0 || bt_len < 1 || nblocks < 1) return -1;
   const int G = nh / nkv, rw = H / nc / 4;
   const size_t lds = kAoWaves * 32 * kVRowBytes + static_cast<size_t>(kAoWaves) * G * (D + 2) * sizeof(float) +
                      64 * 16 + 16;
@@ -343,7 +360,9 @@ extern "C" int llmc_attn_oproj(const void* q, const void* k_cache, const void* v
 #define LLMC_AO(GG, DD, RR)                                                                                      \
   do {                                                                                                            \
     ao_set_lds<GG, DD, RR>();                                                                    \
-    (late ? attn_oproj_kernel<GG, DD, RR, true> : attn_oproj_kernel<GG, DD, RR, false>)<<<grid, kAoThreads, lds, s>>>( \
+    (two ? attn_oproj_kernel<GG, DD, RR, true, 2>                                                                 \
+         : late ? attn_oproj_kernel<GG, DD, RR, true, 1> : attn_oproj_kernel<GG, DD, RR, false, 1>)               \
+        <<<grid, kAoThreads, lds, s>>>(                                                                           \
       (const bf16_t*)q, (const bf16_t*)k_cache, (const bf16_t*)v_cache, (const int32_t*)block_table, bt_len,       \
       (const int32_t*)seq_len, (const bf16_t*)w_o, K_o, (bf16_t*)h, (bf16_t*)attn_out, (float*)part,               \
       (uint32_t*)handoff, (uint64_t*)tile_part, (int*)ctr, (int*)fault, nkv, bs, nblocks, chunk, sl2, resid, (uint64_t*)stamps); \

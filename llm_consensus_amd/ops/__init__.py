@@ -222,7 +222,7 @@ def attn_decode(q, k_cache, v_cache, block_tables, seq_lens, out, part, counters
     return out
 
 
-ATTN_OPROJ_MAX_CHUNK = 256  # attn_oproj: keys per block at most (8 waves x one 32-key sub-tile)
+ATTN_OPROJ_MAX_CHUNK = 512  # attn_oproj: keys per block at most (8 waves x two 32-key sub-tiles)
 ATTN_OPROJ_MODE = int(os.environ.get("LLMC_ATTN_OPROJ_MODE", "1"))  # kernel mode bits (A/B runs)
 # engines take the fused launch only for buckets of >= this many keys per block: below, the two
 # launches measured faster (profiles/r3_attn_oproj.md: 8B at 2k keys 18.5 vs 16.3 us, at 6k-8k
@@ -244,9 +244,12 @@ def attn_oproj_grid(H: int, nh: int, nkv: int, D: int) -> int:
 
 def attn_oproj_chunk(ctx_cap: int, nc: int) -> int:
     """Keys per block for a context bucket of ``ctx_cap`` keys over ``nc`` blocks per kv head (a
-    multiple of 32), or 0 when the bucket needs more than ATTN_OPROJ_MAX_CHUNK keys per block."""
+    multiple of 32; of 64 above 256, where each wave takes two 32-key sub-tiles), or 0 when the
+    bucket needs more than ATTN_OPROJ_MAX_CHUNK keys per block."""
     per = -(-ctx_cap // nc)
     ch = max(32, (per + 31) // 32 * 32)
+    if ch > 256:  # two sub-tiles per wave: 64-key units, so a wave's keys stay inside one page
+        ch = (per + 63) // 64 * 64
     return ch if ch <= ATTN_OPROJ_MAX_CHUNK else 0
 
 

@@ -88,7 +88,8 @@ def bench_attn(shapes=((32, 8, 128), (32, 32, 96), (16, 2, 128), (8, 1, 128), (4
                   + f"  | best {gb / best * 1e6 / 1e3:5.2f} TB/s", flush=True)
 
 
-def bench_attn_oproj(shapes=((32, 8, 128, 4096),), lens=(128, 1024, 2048, 2300, 4096, 6000, 8000)):
+def bench_attn_oproj(shapes=((32, 8, 128, 4096),), lens=(128, 1024, 2048, 2300, 4096, 6000, 8000, 9000, 12000,
+                                                          16000)):
     """Decode attention + o_proj + residual of ONE row per layer: the fused launch (attn_oproj.hip)
     against the engine's two launches (attn_decode in the bucket's form + o GEMV with the residual
     epilogue). Graph-timed over COPIES cycled per call (>= 512 MB of weights and K/V, beyond the

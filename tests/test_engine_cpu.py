@@ -189,15 +189,16 @@ def test_engine_rejects_more_rows_than_the_decode_forms_take():
 
 def test_attn_oproj_bucket_chunks():
     """Keys per block of the fused attention + o_proj launch: the bucket capacity over the grid,
-    in 32-key sub-tiles, 0 above 256 keys per block (the kernel's one sub-tile per wave)."""
+    in 32-key sub-tiles, 0 above 512 keys per block (the kernel's two sub-tiles per wave)."""
     from llm_consensus_amd import ops
 
     nc = 32
-    assert [ops.attn_oproj_chunk(c, nc) for c in (100, 1024, 2048, 4096, 8192, 8193, 16384)] == \
-        [32, 32, 64, 128, 256, 0, 0]
-    for cap in range(1, 8193, 97):
+    assert [ops.attn_oproj_chunk(c, nc) for c in (100, 1024, 2048, 4096, 8192, 8193, 16384, 16385)] == \
+        [32, 32, 64, 128, 256, 320, 512, 0]
+    for cap in range(1, 16385, 97):
         ch = ops.attn_oproj_chunk(cap, nc)
-        assert ch % 32 == 0 and ch * nc >= cap and (ch == 32 or (ch - 32) * nc < cap)
+        unit = 64 if ch > 256 else 32  # two sub-tiles per wave above 256 keys: page-aligned 64-key units
+        assert ch % unit == 0 and ch * nc >= cap and (ch == 32 or (ch - unit) * nc < cap)
     assert ops.ATTN_OPROJ_MIN_CHUNK <= ops.ATTN_OPROJ_MAX_CHUNK
 
 

@@ -232,9 +232,101 @@ def describe(resp, judge) -> str:
     return f"{rs} responders + {j} judge on {where} (own streams)"
 
 
+def topology(world: int, rank: int, dev: str, on_cpu: bool, tp_members, cdev) -> dict:
+    """Collective (every rank): the node as this run saw it, for the JSON record.
+
+    * ``dist_world_size``: the process group's size (``n_gpus`` only echoes WORLD_SIZE);
+    * ``rank_devices``: per rank, its current device index and PCI bus id (CPU ranks: -1 / None);
+    * ``peer_access``: rank 0's ``hipDeviceCanAccessPeer`` matrix over the visible devices (the
+      gate the custom xGMI all-reduce's IPC mapping depends on);
+    * ``allreduce_16k``: per TP engine group, the mean latency of a 16 KiB bf16 all-reduce over
+      ``n`` back-to-back calls (custom one-shot kernel replayed from a HIP graph, else the group's
+      torch.distributed backend eagerly), max over the group's ranks, measured before the warmups."""
+    import socket
+
+    import torch
+    import torch.distributed as dist
+
+    if on_cpu:
+        mine = {"rank": rank, "device": -1, "pci_bus_id": None, "host": socket.gethostname()}
+    else:
+        idx = torch.cuda.current_device()
+        props = torch.cuda.get_device_properties(idx)
+        bus = None
+        if hasattr(props, "pci_bus_id"):
+            bus = f"{getattr(props, 'pci_domain_id', 0):04x}:{props.pci_bus_id:02x}:{getattr(props, 'pci_device_id', 0):02x}"
+        mine = {"rank": rank, "device": idx, "pci_bus_id": bus, "host": socket.gethostname()}
+    if world > 1:
+        ranks_info = [None] * world
+        dist.all_gather_object(ranks_info, mine)
+    else:
+        ranks_info = [mine]
+    peer = []
+    if not on_cpu and rank == 0:
+        from llm_consensus_amd.utils.native import kernels
+
+        n = torch.cuda.device_count()
+        peer = [[int(kernels().can_access_peer(i, j)) for j in range(n)] for i in range(n)]
+    lat = torch.zeros(max(1, len(tp_members)), dtype=torch.float64, device=cdev)
+    impl = {}
+    for gi, (name, ranks, tp) in enumerate(tp_members):
+        if tp is None:
+            continue
+        n_calls = 1000 if not on_cpu else 50
+        x = torch.ones(8192, dtype=torch.bfloat16, device=dev)
+        if tp.custom is not None:
+            impl[name] = "custom_oneshot"
+            s = torch.cuda.Stream(torch.device(dev))
+            s.wait_stream(torch.cuda.current_stream())
+            with torch.cuda.stream(s):
+                tp.custom.all_reduce_(x)  # eager once: kernel attributes, a live epoch
+                g = torch.cuda.CUDAGraph()
+                with torch.cuda.graph(g, stream=s):
+                    for _ in range(50):
+                        tp.custom.all_reduce_(x)
+                torch.cuda.synchronize()
+                tp.barrier()
+                a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                a.record(s)
+                for _ in range(n_calls // 50):
+                    g.replay()
+                b.record(s)
+                torch.cuda.synchronize()
+            us = 1000.0 * a.elapsed_time(b) / n_calls
+            del g
+        else:
+            impl[name] = dist.get_backend(tp.group) if tp.group is not None else "none"
+            tp.all_reduce_(x)
+            if not on_cpu:
+                torch.cuda.synchronize()
+            tp.barrier()
+            t = time.perf_counter()
+            for _ in range(n_calls):
+                tp.all_reduce_(x)
+            if not on_cpu:
+                torch.cuda.synchronize()
+            us = 1e6 * (time.perf_counter() - t) / n_calls
+        lat[gi] = us
+    if world > 1:
+        dist.all_reduce(lat, op=dist.ReduceOp.MAX)
+        impls = [None] * world
+        dist.all_gather_object(impls, impl)
+        for d in impls:
+            impl.update(d)
+    return {
+        "dist_world_size": dist.get_world_size() if world > 1 else 1,
+        "rank_devices": ranks_info,
+        "peer_access": peer,
+        "allreduce_16k": {name: {"impl": impl.get(name), "ranks": ranks, "us": round(float(lat[gi]), 2)}
+                          for gi, (name, ranks, _) in enumerate(tp_members)},
+    }
+
+
 def main() -> None:
     ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--gpus", type=int, default=0,
+                    help="GPUs = ranks (default: WORLD_SIZE under a launcher, else 1); without a launcher, N > 1 "
+                         "starts the N rank processes itself")
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--config", default="fanout", choices=["fanout", "4", "5"])
@@ -263,6 +355,8 @@ def main() -> None:
                     help="rank 0 also writes the full record (per-step stats, p50/p90) here ('' = off)")
     args = ap.parse_args()
 
+    if not args.gpus:
+        args.gpus = int(os.environ.get("WORLD_SIZE", "1"))
     if "WORLD_SIZE" not in os.environ and args.gpus > 1:
         # no launcher: start the N ranks here, before this process touches the GPU (it never
         # imports torch), and exit with their status
@@ -330,6 +424,8 @@ def main() -> None:
     pids = torch.randint(lo, min(lo + 60000, ptok.vocab_size - 2), (args.prompt_tokens,), generator=g).tolist()
     prompt_text = ptok.decode(pids).strip()
 
+    tp_members = []  # (engine name, ranks, this rank's TPGroup or None) of every TP engine, plan order
+
     def tp_group(ranks: List[int]):
         """Collective over the world (dist.new_group): every rank calls it for every TP engine in
         plan order; returns this rank's TPGroup or None when it is not a member."""
@@ -362,6 +458,9 @@ def main() -> None:
         e = resp_plan[idx[0]]
         tp = tp_group(e["ranks"])
         if tp is None:
+            if len(e["ranks"]) > 1:
+                tp_members.append((e["name"] if len(idx) == 1 else "+".join(resp_plan[i]["name"] for i in idx),
+                                   e["ranks"], None))
             continue
         cfg = FAMILIES[e["family"]]
         tok = get_tokenizer(cfg.vocab)
@@ -370,10 +469,14 @@ def main() -> None:
         graphs = not args.no_graphs and (tp.size == 1 or tp.custom is not None
                                          or (not on_cpu and tp.graph_capture_ok(dev)))
         name = e["name"] if len(idx) == 1 else "+".join(resp_plan[i]["name"] for i in idx)
+        if tp.size > 1:
+            tp_members.append((name, e["ranks"], tp))
         eng = Engine(cfg, EngineConfig(device=dev, max_context=ctx, seed=e["seed"], steps_per_graph=args.steps_per_graph,
                                        use_graphs=graphs, max_batch=len(idx)), tp=tp, name=name)
         responders.append((idx, eng, ids, tok))
     jtp_grp = tp_group(judge_plan["ranks"])
+    if len(judge_plan["ranks"]) > 1:
+        tp_members.append((judge_plan["name"], judge_plan["ranks"], jtp_grp))
     judge = None
     judge_ctx = 0
     if jtp_grp is not None:
@@ -403,6 +506,11 @@ def main() -> None:
         dist.barrier()
     log(f"engines ready in {time.time() - t0:.1f}s: {[e.name for _, e, _, _ in responders]}"
         + (f" + {judge.name} (TP={judge.tp.size}, ctx {judge_ctx})" if judge else ""))
+    # what the run actually saw of the node (before any timed work): the RCCL world, each rank's
+    # device, the peer-access matrix and every TP group's 16 KiB all-reduce latency
+    topo = topology(world, rank, dev, on_cpu, tp_members, cdev)
+    if rank == 0:
+        log(f"topology: {topo}")
 
     def one_round(step: int, max_tokens: int = 0):
         max_tokens = max_tokens or args.max_tokens
@@ -546,9 +654,11 @@ def main() -> None:
         c1 = max((s2 - s1) / (t2 - t1), 1e-6)
         c0 = max(s1 - c1 * t1, 0.0)
         left = args.time_budget - (time.time() - T_START) - 10.0  # teardown margin
-        need = args.steps * (c0 + c1 * args.max_tokens)
+        # x 1.15: the probe rounds are short, and a full round's attention and judge prompt grow
+        # with its length (the two-point line under-estimates it)
+        need = 1.15 * args.steps * (c0 + c1 * args.max_tokens)
         if need > left:
-            fit = int(((left / args.steps) - c0) / c1) // 64 * 64
+            fit = int(((left / (1.15 * args.steps)) - c0) / c1) // 64 * 64
             round_tokens = max(64, min(args.max_tokens, fit))
             log(f"time budget: {args.steps} rounds of {args.max_tokens} tokens need ~{need:.0f}s, {left:.0f}s left: "
                 f"timed rounds decode {round_tokens} tokens")
@@ -582,6 +692,18 @@ def main() -> None:
         dist.all_reduce(jt, op=dist.ReduceOp.MAX)
         judge_stats = dict(judge_stats, judge_prompt_tokens=int(jt[0].item()), judge_prefill_s=float(jt[1].item()),
                            judge_decode_s=float(jt[2].item()), judge_ttft_s=float(jt[3].item()))
+    # every TP engine's custom-collective state at the end, from every rank that holds a shard
+    ar_state = {e.name: {"custom": e.tp.custom is not None, "timed_out": bool(e.tp.custom_timed_out())}
+                for e in [e for _, e, _, _ in responders] + ([judge] if judge is not None else []) if e.tp.size > 1}
+    if world > 1:
+        allst = [None] * world
+        dist.all_gather_object(allst, ar_state)
+        ar_state = {}
+        for d in allst:
+            for k, v in d.items():
+                cur = ar_state.setdefault(k, {"custom": True, "timed_out": False})
+                cur["custom"] = cur["custom"] and v["custom"]
+                cur["timed_out"] = cur["timed_out"] or v["timed_out"]
     if rank == 0:
         names = [e["name"] for e in resp_plan]
         value = tot_tokens / elapsed
@@ -591,6 +713,7 @@ def main() -> None:
         par = {"fanout": f"fanout{n_resp}" + "".join(f"-resp_tp{t}" for t in rtp)
                + ("-shared_weights" if any(len(g) > 1 for g, _, _, _ in responders) else ""),
                "4": f"fanout2-tp{len(resp_plan[0]['ranks'])}", "5": "fanout3-mixed"}[args.config]
+        shortened = round_tokens < args.max_tokens
         out = {
             "metric": METRIC,
             "value": round(value, 2),
@@ -608,7 +731,8 @@ def main() -> None:
             "config": {
                 "name": config_name(args, n_gpus, resp_plan, judge_plan)
                 + (" [secondary preset: replicas on one GPU share one weight copy, batched as rows of one engine]"
-                   if args.shared_weights else ""),
+                   if args.shared_weights else "")
+                + (f" [budget-shortened: {round_tokens}-token rounds instead of {args.max_tokens}]" if shortened else ""),
                 "model": describe(resp_plan, judge_plan),
                 "global_batch": n_resp,
                 "seq_len": args.prompt_tokens + round_tokens,
@@ -638,9 +762,11 @@ def main() -> None:
                 "warmup_rounds_tokens": [min(args.max_tokens, wt * (2 if (w == args.warmup - 1 and args.warmup >= 2)
                                                                       else 1)) for w in range(args.warmup)],
                 "max_tokens_requested": args.max_tokens,
+                "budget_shortened": shortened,
                 "time_budget_s": args.time_budget,
-                "custom_allreduce": {e.name: e.tp.custom is not None for _, e, _, _ in responders if e.tp.size > 1}
-                | ({judge.name: judge.tp.custom is not None} if judge is not None and judge.tp.size > 1 else {}),
+                "custom_allreduce": {k: v["custom"] for k, v in ar_state.items()},
+                "custom_allreduce_timed_out": {k: v["timed_out"] for k, v in ar_state.items()},
+                **topo,
             },
         }
         print(json.dumps(out), flush=True)

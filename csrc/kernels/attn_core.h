@@ -1,6 +1,6 @@
 // Decode-attention building blocks shared by attn_decode.hip (K5, its own launch) and
-// decode_layer.hip (the same attention as one phase of the fused decode-layer launch): the
-// MFMA sub-tile step, the wave/block merges and the in-launch partial publish + last-arriver merge.
+// attn_oproj.hip (the same attention feeding the o_proj tile in one launch): the MFMA sub-tile
+// step, the wave/block merges and the in-launch partial publish + last-arriver merge.
 // Design notes: attn_decode.hip's header.
 #pragma once
 #include "common.h"
@@ -32,8 +32,8 @@ struct SubTile {
   f32x4 acc[DT];
   float m_run, l_run;
 
-  // ld(p) loads the 16 B at p (plain by default; decode_layer.hip passes write-through-coherent
-  // sc1 buffer loads for data produced inside its launch)
+  // ld(p) loads the 16 B at p (plain by default; a caller whose operands are produced inside its
+  // own launch passes write-through-coherent sc1 loads)
   template <typename Ld = PlainLd16>
   __device__ __forceinline__ void init(const bf16_t* qrow_kvh, int lane, Ld ld = Ld{}) {
     // columns h >= G of the 16-head MFMA tile carry a copy of head 0 (finite; every column's

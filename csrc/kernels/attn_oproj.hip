@@ -69,7 +69,7 @@ __global__ __launch_bounds__(kAoThreads) void attn_oproj_kernel(
     const int32_t* __restrict__ block_table, int bt_len, const int32_t* __restrict__ seq_len,
     const bf16_t* __restrict__ w_o, int K_o, bf16_t* __restrict__ h, bf16_t* __restrict__ attn_out,
     float* __restrict__ part, uint32_t* __restrict__ handoff, uint64_t* __restrict__ tile_part, int* __restrict__ ctr,
-    int* __restrict__ fault, int nkv, int bs, int nblocks, int chunk, float scale_log2, int resid,
+    int* __restrict__ fault, int nkv, int bs, int nblocks, int chunk, float scale_log2,
     uint64_t* __restrict__ stamps) {
   static_assert(G * D == 512, "one 16-B column chunk per lane per row");
   static_assert(RW >= 1 && RW <= 32 && (RW & (RW - 1)) == 0, "rows per wave: power of two <= 32");
@@ -282,7 +282,7 @@ __global__ __launch_bounds__(kAoThreads) void attn_oproj_kernel(
     for (int gg = 0; gg < kAoMaxKv; ++gg)
       if (gg < nkv) sum += __uint_as_float(static_cast<uint32_t>(v[gg]));
     bf16_t* hp = h + c * R + ct;
-    *hp = f32_to_bf16(resid ? bf16_to_f32(*hp) + sum : sum);  // resid 0: a TP rank's partial (no residual)
+    *hp = f32_to_bf16(bf16_to_f32(*hp) + sum);
     ao_stamp(stp, 7, ct == 0);
   }
   if (ct == 0) {
@@ -320,7 +320,7 @@ static void ao_set_lds() {
 // per block = 4 * RW (RW in {8, 16, 32}), chunk in {32, 64, ..., 256} keys per block, page size
 // a multiple of 32. Returns 0 when (H, nh, nkv, D, nc) is supported.
 extern "C" int llmc_attn_oproj_check(int H, int nh, int nkv, int D, int nc, int K_o) {
-  if (nkv < 1 || nh % nkv != 0 || nc < 1 || H % nc != 0) return -1;
+  if (nkv < 1 || nkv > kAoMaxKv || nh % nkv != 0 || nc < 1 || H % nc != 0) return -1;
   const int G = nh / nkv;
   if (G * D != 512 || K_o != nh * D) return -2;
   const int rw = H / nc / 4;
@@ -329,9 +329,8 @@ extern "C" int llmc_attn_oproj_check(int H, int nh, int nkv, int D, int nc, int 
   return 0;
 }
 
-// mode bit 0: issue the o_proj weights after the head ticket instead of right behind the K/V loads;
-// bit 1: write h = o_proj(attention) (a tensor-parallel rank other than 0: the residual is folded
-// into rank 0's partial and the all-reduce follows), else h += o_proj(attention).
+// h += o_proj(attention). mode bit 0: issue the o_proj weights after the head ticket instead of
+// right behind the K/V loads.
 // fault codes: 1 a partial never arrived (merge), 2 the head output never arrived, 3 a tile partial.
 // stamps (nullable, diagnostics): uint64 [nkv][nc][8] s_memrealtime per block: 0 start, 1 o wave 0's
 // attention done, 2 control wave 4's attention done, 3 head ticket taken, 4 head output in LDS,
@@ -344,14 +343,13 @@ extern "C" int llmc_attn_oproj(const void* q, const void* k_cache, const void* v
                                int bs, int nblocks, int chunk, int nc, float scale, int mode, void* stamps,
                                hipStream_t s) {
   const int K_o = nh * D;
-  if (llmc_attn_oproj_check(H, nh, nkv, D, nc, K_o) != 0 || nkv > kAoMaxKv) return -1;
+  if (llmc_attn_oproj_check(H, nh, nkv, D, nc, K_o) != 0) return -1;
   // up to 256 keys per block: one 32-key sub-tile per wave; up to 512: two (late weights only)
   const bool two = chunk > kAoWaves * 32;
   if (chunk < 32 || chunk > kAoWaves * 64 || chunk % (two ? 64 : 32) != 0 || bs % (two ? 64 : 32) != 0 ||
       bt_len < 1 || nblocks < 1)
     return -1;
   const bool late = (mode & 1) != 0 || two;  // o_proj weights issued after the head ticket
-  const int resid = (mode & 2) ? 0 : 1;  // bit 1: h = the o_proj partial (TP rank != 0), no residual
   const int G = nh / nkv, rw = H / nc / 4;
   const size_t lds = kAoWaves * 32 * kVRowBytes + static_cast<size_t>(kAoWaves) * G * (D + 2) * sizeof(float) +
                      64 * 16 + 16;
@@ -365,7 +363,7 @@ extern "C" int llmc_attn_oproj(const void* q, const void* k_cache, const void* v
         <<<grid, kAoThreads, lds, s>>>(                                                                           \
       (const bf16_t*)q, (const bf16_t*)k_cache, (const bf16_t*)v_cache, (const int32_t*)block_table, bt_len,       \
       (const int32_t*)seq_len, (const bf16_t*)w_o, K_o, (bf16_t*)h, (bf16_t*)attn_out, (float*)part,               \
-      (uint32_t*)handoff, (uint64_t*)tile_part, (int*)ctr, (int*)fault, nkv, bs, nblocks, chunk, sl2, resid, (uint64_t*)stamps); \
+      (uint32_t*)handoff, (uint64_t*)tile_part, (int*)ctr, (int*)fault, nkv, bs, nblocks, chunk, sl2, (uint64_t*)stamps); \
   } while (0)
   if (G == 4 && D == 128) {
     if (rw == 8) LLMC_AO(4, 128, 8);

@@ -27,10 +27,6 @@ int llmc_moe_gemvm(int, const void*, int, const void*, float, const void*, const
 int llmc_gemm(const void*, int, const void*, int, void*, int, int, int, int, int, hipStream_t);
 int llmc_rope_kv_write(const void*, int, void*, int, const void*, const void*, const void*, void*, void*, const void*,
                        int, int, int, int, int, hipStream_t);
-int llmc_decode_layer(const void*, const void*, const void*, const void*, const void*, const void*, void*, void*,
-                      const void*, const void*, const void*, const void*, int, const void*, const void*, void*, void*,
-                      void*, void*, void*, void*, void*, void*, void*, int, int, int, int, int, int, int, int, int, int,
-                      float, float, hipStream_t);
 int llmc_attn_decode_groups(int);
 int llmc_attn_oproj_check(int, int, int, int, int, int);
 int llmc_attn_oproj(const void*, const void*, const void*, const void*, int, const void*, const void*, void*, void*,
@@ -114,16 +110,6 @@ PYBIND11_MODULE(_llmc_hip, m) {
     check(llmc_rope_kv_write(P(qkv), qs, P(qo), qos, P(pos), P(cos_t), P(sin_t), P(kc), P(vc), P(slots), T, nh, nkv, D,
                              bs, S(s)),
           "rope_kv_write");
-  });
-  m.def("decode_layer", [](ptr ln1, ptr w_qkv, ptr w_o, ptr ln2, ptr w_gu, ptr w_down, ptr kc, ptr vc, ptr pos,
-                           ptr slots, ptr sl, ptr bt, int bts, ptr cos_t, ptr sin_t, ptr h, ptr q, ptr attn, ptr act,
-                           ptr part, ptr actr, ptr sync, ptr fault, ptr stamps, int H, int nh, int nkv, int D, int I, int bs,
-                           int nblocks, int min_chunk, int gc, int max_chunks, float eps, float scale, ptr s) {
-    check(llmc_decode_layer(P(ln1), P(w_qkv), P(w_o), P(ln2), P(w_gu), P(w_down), P(kc), P(vc), P(pos), P(slots), P(sl),
-                            P(bt), bts, P(cos_t), P(sin_t), P(h), P(q), P(attn), P(act), P(part), P(actr), P(sync),
-                            P(fault), P(stamps), H, nh, nkv, D, I, bs, nblocks, min_chunk, gc, max_chunks, eps, scale,
-                            S(s)),
-          "decode_layer");
   });
   m.def("attn_decode_groups", [](int max_chunks) { return llmc_attn_decode_groups(max_chunks); });
   m.def("attn_oproj_check", [](int H, int nh, int nkv, int D, int nc, int K_o) {

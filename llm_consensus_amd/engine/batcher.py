@@ -176,11 +176,10 @@ class ContinuousBatcher:
             if self._pending is not None:
                 self._pending.synchronize()
                 if int(self._host_fault[0]):
-                    # a decode-attention merge gave up during the replays behind this snapshot:
-                    # the rows it covered carry invalid tokens — fail them instead of streaming
-                    from .engine import EngineError
-
-                    e.attn_fault.zero_()
+                    # a decode-attention merge gave up in the replay behind this snapshot (the
+                    # device word is re-armed right after each snapshot's copy, so it covers
+                    # exactly that replay, whose rows are all in ``_snap``): fail them instead of
+                    # streaming their tokens
                     self._host_fault.zero_()
                     for row in self._snap:
                         if not row.done:
@@ -192,6 +191,9 @@ class ContinuousBatcher:
             e.host_count.copy_(e.out_count, non_blocking=True)
             e.host_tokens.copy_(e.out_tokens, non_blocking=True)
             self._host_fault.copy_(e.attn_fault, non_blocking=True)
+            # re-arm before the next replay is queued: a fault that replay raises lands in the next
+            # snapshot instead of being wiped by a clear queued behind it
+            e.attn_fault.zero_()
             ev = torch.cuda.Event()
             ev.record(e.stream)
             self._pending, self._snap = ev, list(self.rows)

@@ -57,19 +57,15 @@ class EngineConfig:
     sp_min_tokens: int = 256
     # MoE under TP: each rank holds n_experts / tp whole experts instead of 1/tp of every expert
     expert_parallel: bool = False
-    # one-row engines (no TP, dense MLP): each decode layer as ONE fused launch
-    # (csrc/kernels/decode_layer.hip) instead of five kernels. Off by default: measured slower
-    # than the five tuned kernels so far (docs/ARCHITECTURE.md, "Fused decode layer")
-    fused_layer: bool = False
     # one-row engines without TP: decode attention + o_proj + residual as ONE launch per layer
     # (csrc/kernels/attn_oproj.hip) in the context buckets with at least ``attn_oproj_min_chunk``
     # keys per block (ops.ATTN_OPROJ_MIN_CHUNK: where it measured faster than the two launches).
-    # Environment defaults (A/B runs): LLMC_ATTN_OPROJ=0 never, =all every bucket it covers;
-    # LLMC_ATTN_OPROJ_TP=1 also on tensor-parallel ranks (measured slower there: off)
+    # Environment defaults (A/B runs): LLMC_ATTN_OPROJ=0 never, =all every bucket it covers.
+    # Tensor-parallel ranks never take it (their 1-2 kv heads make the merge the long pole and the
+    # o_proj it would hide is small: profiles/r3_attn_oproj.md)
     attn_oproj: bool = dataclasses.field(default_factory=lambda: os.environ.get("LLMC_ATTN_OPROJ", "1") != "0")
     attn_oproj_min_chunk: int = dataclasses.field(
         default_factory=lambda: 32 if os.environ.get("LLMC_ATTN_OPROJ") == "all" else ops.ATTN_OPROJ_MIN_CHUNK)
-    attn_oproj_tp: bool = dataclasses.field(default_factory=lambda: os.environ.get("LLMC_ATTN_OPROJ_TP", "0") == "1")
 
 
 FUSED_CHUNK_SMALL, FUSED_CHUNK_LARGE = 128, 256
@@ -256,26 +252,18 @@ class Engine:
                                          ops.FUSED_ATTN_MAX_KEYS if self.bs % 32 == 0 else 0, self.nh // self.nkv,
                                          self.nkv, rows=self.ecfg.max_batch)
         max_chunks = max(gc for _, _, gc, _ in self.attn_buckets)
-        # fused decode layer (one launch per layer) for one-row dense engines without TP
-        G = self.nh // max(1, self.nkv)
-        self.fused_layer = (self.on_gpu and self.ecfg.fused_layer and B == 1 and not c.is_moe and self.tp.size == 1
-                            and self.D in (64, 96, 128) and G in (1, 2, 4, 8) and c.hidden % 16 == 0
-                            and self.w.inter % 16 == 0 and self.D % 16 == 0)
-        if self.fused_layer:
-            self.layer_gc = [ops.decode_layer_grid(cap) for cap, _, _, _ in self.attn_buckets]
-            max_chunks = max(max_chunks, max(self.layer_gc))
-            self.dl_sync = torch.zeros(ops.DECODE_LAYER_SYNC_WORDS, dtype=torch.int32, device=dev)
         self.attn_part, self.attn_counters = ops.decode_attn_workspace(B, self.nh, self.nkv, self.D, max_chunks, dev)
         # fused attention + o_proj launch: per bucket its keys per block (0 = the bucket keeps the
         # two launches)
         self.ao_chunks: List[int] = [0] * len(self.attn_buckets)
         self.ao_nc = 0
-        if (self.on_gpu and self.ecfg.attn_oproj and B == 1 and not self.fused_layer and self.bs % 32 == 0
-                and (self.tp.size == 1 or self.ecfg.attn_oproj_tp)):
+        if self.on_gpu and self.ecfg.attn_oproj and B == 1 and self.bs % 32 == 0 and self.tp.size == 1:
             self.ao_nc = ops.attn_oproj_grid(c.hidden, self.nh, self.nkv, self.D)
             if self.ao_nc:
                 lo = self.ecfg.attn_oproj_min_chunk
-                self.ao_chunks = [ch if ch >= lo else 0
+                # a block of > 256 keys gives each wave two 32-key sub-tiles of one 64-key unit:
+                # pages must hold whole units there (the kernel rejects bs % 64 != 0)
+                self.ao_chunks = [ch if ch >= lo and (ch <= 256 or self.bs % 64 == 0) else 0
                                   for ch in (ops.attn_oproj_chunk(cap, self.ao_nc) for cap, _, _, _ in self.attn_buckets)]
                 self.ao_ws = ops.attn_oproj_workspace(c.hidden, self.nh, self.nkv, self.D, self.ao_nc, dev)
         # set by a decode-attention merger that gave up on a partial (checked after every decode)
@@ -580,26 +568,15 @@ class Engine:
         part = self.attn_part
         h, q, attn, act = self.h[:B], self.q[:B], self.attn[:B], self.act[:B]
         ops.embedding(self.tokens_in[:B], self.w.embed, out=h)
-        if self.fused_layer and B == 1:
-            gc = self.layer_gc[-1 if bucket is None else bucket]
-            for li, Lw in enumerate(self.w.layers):
-                ops.decode_layer(Lw, h, q, attn, act, self.k_cache[li], self.v_cache[li], self.positions[:1],
-                                 self.slots[:1], self.seq_lens[:1], self.block_tables[:1], self.cos_t, self.sin_t,
-                                 part, self.attn_counters, self.dl_sync, self.attn_fault, self.nh, self.nkv, self.D,
-                                 self.bs, gc, c.rms_eps, self.scale)
-            self._lm_head_sample(B)
-            return
         ao_chunk = self.ao_chunks[-1 if bucket is None else bucket] if B == 1 else 0
         for li, Lw in enumerate(self.w.layers):
             ops.qkv_rope(h, Lw.w_qkv, Lw.ln1, c.rms_eps, q, self.k_cache[li], self.v_cache[li], self.positions[:B],
                          self.slots[:B], self.cos_t, self.sin_t, self.nh, self.nkv, self.D, self.bs,
                          mfma=self.mfma_decode)
-            if ao_chunk:
-                # row-parallel under TP: rank 0's partial carries the residual, then the all-reduce
+            if ao_chunk:  # one-row engines without TP: attention + o_proj + residual in one launch
                 ops.attn_oproj(q, self.k_cache[li], self.v_cache[li], self.block_tables[:1], self.seq_lens[:1], Lw.w_o,
                                h, attn, self.ao_ws, self.nh, self.nkv, self.D, self.bs, ao_chunk, self.ao_nc,
-                               self.scale, fault=self.attn_fault, residual=self.tp.rank == 0)
-                self.tp.all_reduce_(h)
+                               self.scale, fault=self.attn_fault)
             else:
                 ops.attn_decode(q, self.k_cache[li], self.v_cache[li], self.block_tables[:B], self.seq_lens[:B], attn,
                                 part[:B], self.attn_counters[:B], self.nh, self.nkv, self.D, self.bs, chunk,
@@ -884,15 +861,13 @@ class Engine:
             attn_bad = bool(self.attn_fault.item())
             if attn_bad:
                 self.attn_fault.zero_()
-                if self.fused_layer:  # a fused layer that gave up left its step counters mid-count
-                    self.dl_sync.zero_()
         if self.tp.size > 1 and self.tp.ctrl is not None:
             if not self.tp.check_collectives():
                 raise EngineError("custom all-reduce timed out (a TP peer stalled): this request's tokens are invalid")
             attn_bad = self.tp.any_rank(attn_bad)
         if attn_bad:
             raise EngineError("decode attention: a partial merge timed out (a block never published its "
-                              "partial, or a fused layer / attention + o_proj hand-off wait gave up): this "
+                              "partial, or an attention + o_proj hand-off wait gave up): this "
                               "request's tokens are invalid")
 
     def _bind_rows(self, seqs: List[Sequence], params: List[SamplingParams]) -> None:

@@ -269,21 +269,19 @@ def attn_oproj_workspace(H: int, nh: int, nkv: int, D: int, nc: int, device):
 
 
 def attn_oproj(q, k_cache, v_cache, block_table, seq_len, w_o, h, attn_out, ws, nh, nkv, D, bs, chunk, nc, scale,
-               fault: Optional[torch.Tensor] = None, stamps: Optional[torch.Tensor] = None, mode: int = -1,
-               residual: bool = True) -> None:
+               fault: Optional[torch.Tensor] = None, stamps: Optional[torch.Tensor] = None, mode: int = -1) -> None:
     """Decode attention of ONE row followed by its o_proj and residual add, in one launch
     (csrc/kernels/attn_oproj.hip): ``h[0] += w_o @ attention(q[0])``; ``attn_out[0]`` also gets the
     attention output. ``ws`` = ``attn_oproj_workspace(...)``; ``chunk`` = ``attn_oproj_chunk(cap,
     nc)`` for a bucket whose capacity covers the sequence; ``fault`` as in ``attn_decode``;
     ``stamps`` (diagnostics): int64 [nkv, nc, 8] per-block phase times (see the kernel's host
     function); ``mode`` bit 0: o_proj weights requested after the head ticket (-1 =
-    ATTN_OPROJ_MODE); ``residual`` False: ``h[0] = w_o @ attention`` (a TP rank's row-parallel
-    partial, the residual folded into rank 0's; the caller all-reduces)."""
+    ATTN_OPROJ_MODE)."""
     H = h.shape[-1]
     if not q.is_cuda:
         a = oracle.attn_decode(q[:1], k_cache, v_cache, block_table[:1], seq_len[:1], nh, nkv, D, bs, scale)
         attn_out[:1].copy_(a)
-        oracle.linear(attn_out[:1], w_o, EPI_RESADD if residual else EPI_BF16, h[:1])
+        oracle.linear(attn_out[:1], w_o, EPI_RESADD, h[:1])
         return
     if chunk <= 0 or chunk * nc < 1 or nc != ws[0].shape[1]:
         raise ValueError("attn_oproj: chunk / workspace do not match (attn_oproj_chunk, attn_oproj_workspace)")
@@ -291,38 +289,7 @@ def attn_oproj(q, k_cache, v_cache, block_table, seq_len, w_o, h, attn_out, ws, 
     kernels().attn_oproj(_p(q), _p(k_cache), _p(v_cache), _p(block_table), block_table.shape[-1], _p(seq_len), _p(w_o),
                          _p(h), _p(attn_out), _p(part), _p(handoff), _p(tile_part), _p(counters), _p(fault), H, nh, nkv,
                          D, bs, k_cache.shape[0], chunk, nc, float(scale),
-                         (ATTN_OPROJ_MODE if mode < 0 else mode) | (0 if residual else 2), _p(stamps), _s(h))
-
-
-DECODE_LAYER_MIN_CHUNK = 256  # fused decode layer: keys per attention block at least (8 waves x 32)
-DECODE_LAYER_SYNC_WORDS = 1024  # its step counters, one 256-B line each
-
-
-def decode_layer_grid(ctx_cap: int) -> int:
-    """Attention blocks per kv head of the fused decode layer for a context bucket of ``ctx_cap``
-    keys: one per 256 keys, at most 32 (one-level merge)."""
-    return max(1, min(32, -(-ctx_cap // DECODE_LAYER_MIN_CHUNK)))
-
-
-def decode_layer(Lw, h, q, attn, act, k_cache, v_cache, positions, slots, seq_lens, block_table, cos_t, sin_t,
-                 part, counters, sync, fault, nh, nkv, D, bs, gc, eps, scale, stamps=None) -> None:
-    """One decode layer for ONE row in one launch (csrc/kernels/decode_layer.hip): qkv GEMV with
-    the RMSNorm prologue and RoPE / paged-KV epilogue -> split-KV attention over ``gc`` blocks per
-    kv head -> o GEMV + residual -> gate_up GEMV with the RMSNorm prologue and SiLU-mul -> down
-    GEMV + residual, as a dataflow of dispatch-ordered tasks. ``h`` [1, H] is updated in place;
-    ``q`` / ``attn`` / ``act`` are scratch; ``part`` / ``counters``: the attn_decode workspace;
-    ``sync``: int32 [DECODE_LAYER_SYNC_WORDS] zeroed once; ``fault``: the engine's fault word; ``stamps`` (diagnostics):
-    int64 [tasks, 8] per-task timeline (s_memrealtime at start / task taken / wait over / before and
-    after the done signal, dispatch time, blockIdx, XCC id)."""
-    groups = counters.shape[-1] - 2
-    max_chunks = part.shape[2] - groups
-    H, I = h.shape[-1], act.shape[-1]
-    kernels().decode_layer(_p(Lw.ln1), _p(Lw.w_qkv), _p(Lw.w_o), _p(Lw.ln2), _p(Lw.w_gu), _p(Lw.w_down), _p(k_cache),
-                           _p(v_cache), _p(positions), _p(slots), _p(seq_lens), _p(block_table), block_table.stride(0),
-                           _p(cos_t), _p(sin_t), _p(h), _p(q), _p(attn), _p(act), _p(part), _p(counters), _p(sync),
-                           _p(fault), _p(stamps), H, nh, nkv, D, I, bs, k_cache.shape[0], DECODE_LAYER_MIN_CHUNK, gc,
-                           max_chunks,
-                           float(eps), float(scale), _s(h))
+                         ATTN_OPROJ_MODE if mode < 0 else mode, _p(stamps), _s(h))
 
 
 def attn_prefill(q, k_cache, v_cache, block_tables, q_start, q_lens, ctx_lens, out, max_qlen, nh, nkv, D, bs, scale):

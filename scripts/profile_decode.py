@@ -14,11 +14,10 @@ ap.add_argument("--no-graphs", action="store_true")
 ap.add_argument("--ctx", type=int, default=8192)
 ap.add_argument("--batch", type=int, default=1, help="decode rows per step (continuous-batching engine)")
 ap.add_argument("--engine-rows", type=int, default=0, help="engine max_batch (0 = --batch): e.g. one row on a serving engine")
-ap.add_argument("--fused-layer", type=int, default=0, help="one-row engines: 1 = one fused launch per layer, 0 = five kernels")
 a = ap.parse_args()
 cfg = FAMILIES[a.model]
 e = Engine(cfg, EngineConfig(device="cuda:0", max_context=a.ctx, seed=1, use_graphs=not a.no_graphs,
-                             max_batch=max(a.batch, a.engine_rows), fused_layer=bool(a.fused_layer)))
+                             max_batch=max(a.batch, a.engine_rows)))
 prompt = [(i * 7919) % 30000 + 256 for i in range(a.prompt)]
 if a.batch > 1:
     from llm_consensus_amd.engine import SamplingParams

@@ -162,3 +162,41 @@ def test_attention_fault_fails_batched_rows(cuda):
     assert gone == [row] and row.error is not None and "merge timed out" in str(row.error)
     torch.cuda.synchronize()  # the re-arm is queued on the engine's stream
     assert int(eng.attn_fault.item()) == 0
+
+
+@pytest.mark.gpu
+def test_attention_fault_in_flight_replay_is_not_lost(cuda):
+    """A fault raised by the replay that is still in flight when the previous snapshot's fault is
+    handled must not be wiped: a row admitted after that snapshot (so not in it) but decoded by
+    the faulting replay fails too (the re-arm used to be queued behind that replay)."""
+    eng = _engine("cuda:0")
+    bat = ContinuousBatcher(eng)
+    inject = {"on": True}
+    real_graph = eng._graph
+
+    class Faulting:
+        def __init__(self, g):
+            self.g = g
+
+        def replay(self):
+            self.g.replay()
+            if inject["on"]:
+                eng.attn_fault.fill_(1)  # on the engine stream, after the replay's kernels
+
+    eng._graph = lambda B, bk: Faulting(real_graph(B, bk))
+    sa, sb = eng.new_sequence(), eng.new_sequence()
+    eng.prefill([sa], [[100 + i for i in range(20)]])
+    eng.prefill([sb], [[200 + i for i in range(20)]])
+    a = bat.admit(sa, SamplingParams(max_tokens=128, temperature=0.0, stop_on_eos=False))
+    bat.step()                      # replay 1 faults; snapshot 1 carries it
+    b = bat.admit(sb, SamplingParams(max_tokens=128, temperature=0.0, stop_on_eos=False))
+    gone = bat.step()               # replay 2 (rows a, b) faults too; snapshot 1 fails a
+    assert a in gone and a.error is not None
+    inject["on"] = False
+    for _ in range(3):
+        gone += bat.step()
+        if b in gone:
+            break
+    assert b in gone and b.error is not None and "merge timed out" in str(b.error)
+    torch.cuda.synchronize()
+    assert int(eng.attn_fault.item()) == 0

@@ -108,6 +108,7 @@ def test_time_budget_shortens_rounds_never_steps():
                  "--time-budget", "1"], 0)
     assert d["steps"] == 2 and d["extra"]["max_tokens_requested"] == 4096
     assert 64 <= d["config"]["max_tokens"] < 4096
+    assert d["extra"]["budget_shortened"] is True and "budget-shortened" in d["config"]["name"]
     _tokens_ok(d, d["config"]["max_tokens"])
 
 
@@ -126,11 +127,38 @@ def _self_launched(n, extra=()):
 
 
 def test_self_launch_n_ranks_without_a_launcher():
+    """Self-launched N ranks, and the record proves what the job saw: the process-group size, one
+    device entry per rank, every TP group's measured 16 KiB all-reduce latency and its
+    custom-collective state (CPU ranks: device -1, gloo, no custom kernels)."""
     for n in (2, 4, 8):
         d = _self_launched(n)
         assert d["n_gpus"] == n and d["steps"] == 1 and d["warmup"] == 1
         assert d["config"]["global_batch"] == max(3, n)
         _tokens_ok(d, 8)
+        x = d["extra"]
+        assert x["dist_world_size"] == n and x["budget_shortened"] is False
+        assert [r["rank"] for r in x["rank_devices"]] == list(range(n))
+        assert all(r["device"] == -1 for r in x["rank_devices"]) and x["peer_access"] == []
+        judge = [k for k in x["allreduce_16k"] if k.endswith("@judge")]
+        assert judge and x["allreduce_16k"][judge[0]]["impl"] == "gloo"
+        assert x["allreduce_16k"][judge[0]]["us"] > 0 and len(x["allreduce_16k"][judge[0]]["ranks"]) == x["judge_tp"]
+        assert set(x["custom_allreduce"]) == set(x["custom_allreduce_timed_out"]) == set(x["allreduce_16k"])
+        assert not any(x["custom_allreduce"].values()) and not any(x["custom_allreduce_timed_out"].values())
+
+
+def test_gpus_defaults_to_world_size_under_a_launcher():
+    """torchrun without --gpus: the rank count comes from WORLD_SIZE (an explicit mismatch fails)."""
+    env = dict(os.environ, LLMC_BENCH_DEVICE="cpu", OMP_NUM_THREADS="1")
+    base = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2", "--master-addr",
+            "127.0.0.1", "--master-port", "29695", "bench.py", "--shapes", "tiny", "--steps", "1", "--warmup", "0",
+            "--max-tokens", "8", "--results-dir", ""]
+    r = subprocess.run(base, cwd=ROOT, capture_output=True, timeout=600, env=env)
+    assert r.returncode == 0, r.stderr.decode()[-3000:]
+    d = json.loads([ln for ln in r.stdout.decode().splitlines() if ln.startswith("{")][0])
+    assert d["n_gpus"] == 2 and d["extra"]["dist_world_size"] == 2
+    base[base.index("29695")] = "29696"
+    r = subprocess.run(base + ["--gpus", "4"], cwd=ROOT, capture_output=True, timeout=600, env=env)
+    assert r.returncode != 0 and b"WORLD_SIZE" in r.stderr
 
 
 def test_self_launch_failing_rank_fails_the_job():

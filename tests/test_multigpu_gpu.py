@@ -1,0 +1,233 @@
+"""Cross-device multi-GPU paths, one rank process per GPU (rank i on cuda:i, RCCL bootstrap), gated
+on ``torch.cuda.device_count() >= N`` (skipped, not deselected, on a one-GPU box).
+
+These are the paths a one-GPU box cannot execute and the driver's 8-GPU scaling run depends on
+(reference fan-out ``internal/runner/runner.go:60-63``, judge ``internal/consensus/judge.go:96-99``):
+
+* the custom xGMI collectives between distinct devices: ``hipDeviceCanAccessPeer``, cross-device
+  ``hipIpcOpenMemHandle`` of the uncached buffers, one-shot all-reduce / all-gather and the two-shot
+  reduce-scatter / all-gather / all-reduce, eagerly and replayed from a HIP graph;
+* a TP = N engine's decode (custom collectives in its captured graphs) against TP = 1;
+* ``bench.py --gpus N`` self-launched: the record must show N ranks on N distinct devices, the
+  judge's custom all-reduce enabled and no spin timeout.
+"""
+
+import json
+import os
+import socket
+import subprocess
+import sys
+
+import pytest
+import torch
+import torch.multiprocessing as mp
+
+pytestmark = pytest.mark.gpu
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+WORLDS = [2, 4, 8]
+
+
+def _need(n):
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    have = torch.cuda.device_count()
+    if have < n:
+        pytest.skip(f"needs {n} GPUs, this box has {have}")
+
+
+def _port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _inp(rank, n, salt):
+    g = torch.Generator().manual_seed(1000 * rank + n + salt)
+    return torch.randn(n, generator=g).to(torch.bfloat16)
+
+
+def _init(rank, world, port):
+    import torch.distributed as dist
+
+    torch.cuda.set_device(rank)
+    dist.init_process_group("nccl", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world,
+                            device_id=torch.device("cuda", rank))
+    return dist
+
+
+def _run(target, world, *args, timeout=300):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _port()
+    procs = [ctx.Process(target=target, args=(r, world, port, q) + args) for r in range(world)]
+    for p in procs:
+        p.start()
+    try:
+        res = [q.get(timeout=timeout) for _ in range(world)]
+    finally:
+        for p in procs:
+            p.join(timeout=60)
+            if p.is_alive():
+                p.kill()
+    return res
+
+
+# ---- custom collectives across devices --------------------------------------------------------
+def _collectives_worker(rank, world, port, q):
+    try:
+        dist = _init(rank, world, port)
+        from llm_consensus_amd.parallel.comm import TPGroup
+        from llm_consensus_amd.utils.native import kernels
+
+        dev = f"cuda:{rank}"
+        peers_ok = all(kernels().can_access_peer(rank, r) for r in range(world))
+        tp = TPGroup(dist.group.WORLD, rank, world)
+        enabled = tp.enable_custom(dev, cap=1 << 20, cap2=16 << 20)
+        errs = []
+        if enabled:
+            for rep in range(2):
+                for n in (8, 4096, 4104, 3 * 4096 + 8, 128 * 1024, 4 * (1 << 20) // 2 + 8 * 37):
+                    x = _inp(rank, n, rep).to(dev)
+                    tp.all_reduce_(x)  # one-shot up to 1 MiB, two-shot above
+                    torch.cuda.synchronize()
+                    ref = sum(_inp(r, n, rep).float() for r in range(world))
+                    errs.append(float((x.float().cpu() - ref).abs().max() / (ref.abs().max() + 1e-6)))
+            loc = torch.full((2, 20), float(rank), dtype=torch.float32, device=dev)
+            out = torch.empty(world, 2, 20, dtype=torch.float32, device=dev)
+            tp.all_gather_rows(loc, out)
+            Ts, H = 700, 4096
+            full = _inp(rank, world * Ts * H, 7).view(world * Ts, H)
+            rs = torch.empty(Ts, H, dtype=torch.bfloat16, device=dev)
+            tp.reduce_scatter_rows(full.to(dev), rs)
+            torch.cuda.synchronize()
+            gather_ok = all(bool((out[r] == r).all()) for r in range(world))
+            ref = sum(_inp(r, world * Ts * H, 7).view(world * Ts, H).float() for r in range(world))[rank * Ts:(rank + 1) * Ts]
+            errs.append(float((rs.float().cpu() - ref).abs().max() / ref.abs().max()))
+            # graph replay with refreshed inputs (the decode graphs' pattern)
+            n = 8192
+            x = torch.zeros(n, dtype=torch.bfloat16, device=dev)
+            s = torch.cuda.Stream()
+            with torch.cuda.stream(s):
+                tp.all_reduce_(x)
+            torch.cuda.synchronize()
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g, stream=s):
+                for _ in range(3):
+                    tp.all_reduce_(x)
+            for rep in range(4):
+                x.copy_(_inp(rank, n, 50 + rep))
+                torch.cuda.synchronize()
+                dist.barrier()
+                g.replay()
+                torch.cuda.synchronize()
+                one = sum(_inp(r, n, 50 + rep).float() for r in range(world))
+                ref = one * world * world  # three in-place all-reduces
+                errs.append(float((x.float().cpu() - ref).abs().max() / ref.abs().max()))
+        else:
+            gather_ok = False
+        q.put((rank, peers_ok, enabled, max(errs) if errs else 1.0, gather_ok, tp.custom_timed_out() if enabled else None))
+        dist.barrier()
+        dist.destroy_process_group()
+    except Exception as e:  # noqa: BLE001
+        import traceback
+
+        q.put((rank, False, False, repr(e) + traceback.format_exc(), False, True))
+
+
+@pytest.mark.parametrize("world", WORLDS)
+def test_custom_collectives_across_devices(world):
+    _need(world)
+    for rank, peers_ok, enabled, err, gather_ok, tmo in _run(_collectives_worker, world):
+        assert not isinstance(err, str), err
+        assert peers_ok, f"rank {rank}: hipDeviceCanAccessPeer is false for a peer"
+        assert enabled, f"rank {rank}: custom collectives fell back to RCCL"
+        assert not tmo, f"rank {rank}: a custom-collective spin timed out"
+        # bf16 rounding of sums over up to 8 ranks, and a triple in-place sum in the graph case
+        assert err < 3e-2, (rank, err)
+        assert gather_ok, rank
+
+
+# ---- TP decode across devices ----------------------------------------------------------------
+def _tp_cfg():
+    from llm_consensus_amd.models.config import ModelConfig
+
+    # every sharded dimension divisible by 8: 16 heads, 8 kv heads, FFN 2048, vocab 32000
+    return ModelConfig("llama-tp8-test", "llama", 2, 1024, 16, 8, 64, 2048, 32000, 500000.0, max_position=4096)
+
+
+PROMPT = [(i * 13) % 700 + 256 for i in range(60)]
+
+
+def _tp_worker(rank, world, port, q):
+    try:
+        dist = _init(rank, world, port)
+        from llm_consensus_amd.engine import Engine, EngineConfig
+        from llm_consensus_amd.parallel.comm import TPGroup
+
+        ctrl = dist.new_group(list(range(world)), backend="gloo")
+        tp = TPGroup(dist.group.WORLD, rank, world, ctrl=ctrl)
+        enabled = tp.enable_custom(f"cuda:{rank}")
+        e = Engine(_tp_cfg(), EngineConfig(device=f"cuda:{rank}", max_context=1024, seed=5), tp=tp)
+        e.warmup_graphs()
+        s = e.new_sequence()
+        e.prefill([s], [PROMPT])
+        logits = e.full_logits(s).float().cpu()
+        e.free_sequence(s)
+        gen = e.generate_ids(PROMPT, 32, temperature=0.0, stop_on_eos=False)
+        torch.cuda.synchronize()
+        q.put((rank, enabled, logits.tolist() if rank == 0 else None, gen, tp.custom_timed_out()))
+        dist.barrier()
+        dist.destroy_process_group()
+    except Exception as ex:  # noqa: BLE001
+        import traceback
+
+        q.put((rank, False, repr(ex) + traceback.format_exc(), None, True))
+
+
+@pytest.mark.parametrize("world", WORLDS)
+def test_tp_decode_across_devices_matches_tp1(world):
+    _need(world)
+    from llm_consensus_amd.engine import Engine, EngineConfig
+
+    ref = Engine(_tp_cfg(), EngineConfig(device="cuda:0", max_context=1024, seed=5))
+    s = ref.new_sequence()
+    ref.prefill([s], [PROMPT])
+    ref_logits = ref.full_logits(s).float().cpu()
+    ref.free_sequence(s)
+    ref_gen = ref.generate_ids(PROMPT, 32, temperature=0.0, stop_on_eos=False)
+    del ref
+    torch.cuda.empty_cache()
+    res = _run(_tp_worker, world)
+    gens = {}
+    for rank, enabled, logits, gen, tmo in res:
+        assert not isinstance(logits, str), logits
+        assert enabled, f"rank {rank}: custom collectives fell back to RCCL"
+        assert not tmo, f"rank {rank}: a custom-collective spin timed out"
+        gens[rank] = gen
+        if rank == 0:
+            lg = torch.tensor(logits)
+            assert (lg - ref_logits).abs().max().item() < 0.05 * ref_logits.abs().max().item()
+    assert all(g == gens[0] for g in gens.values()), "TP ranks sampled different tokens"
+    agree = next((i for i, (a, b) in enumerate(zip(gens[0], ref_gen)) if a != b), len(ref_gen))
+    assert agree >= 8, (agree, gens[0], ref_gen)  # bf16 sums in a different order: near-ties only late
+
+
+# ---- the bench's own multi-GPU flow ---------------------------------------------------------
+@pytest.mark.parametrize("world", WORLDS)
+def test_bench_self_launch_across_devices(world):
+    _need(world)
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_PORT")}
+    r = subprocess.run([sys.executable, "bench.py", "--gpus", str(world), "--shapes", "tiny", "--steps", "1",
+                        "--warmup", "0", "--max-tokens", "32", "--results-dir", ""],
+                       cwd=ROOT, capture_output=True, timeout=600, env=env)
+    assert r.returncode == 0, r.stderr.decode()[-3000:]
+    d = json.loads([ln for ln in r.stdout.decode().splitlines() if ln.startswith("{")][0])
+    x = d["extra"]
+    assert d["n_gpus"] == world and x["dist_world_size"] == world
+    assert [rd["device"] for rd in x["rank_devices"]] == list(range(world))
+    assert len({rd["pci_bus_id"] for rd in x["rank_devices"]}) == world
+    assert len(x["peer_access"]) >= world and all(x["peer_access"][i][j] for i in range(world) for j in range(world))
+    judge = [k for k in x["custom_allreduce"] if k.endswith("@judge")]
+    assert judge and x["custom_allreduce"][judge[0]] and not any(x["custom_allreduce_timed_out"].values())
+    assert x["allreduce_16k"][judge[0]]["impl"] == "custom_oneshot" and x["allreduce_16k"][judge[0]]["us"] > 0

@@ -35,10 +35,6 @@ def _worker(rank, world, port, name, q, ekw=None):
         tp = TPGroup(dist.group.WORLD, rank, world)
         tp.enable_custom("cuda:0")
         e = Engine(FAMILIES[name], EngineConfig(device="cuda:0", max_context=512, seed=5, **(ekw or {})), tp=tp)
-        import os
-
-        if os.environ.get("LLMC_ATTN_OPROJ_TP") == "1":  # the fused-path test: it must be taken
-            assert e.ecfg.attn_oproj_tp and e.ao_nc > 0 and any(e.ao_chunks), (e.ao_nc, e.ao_chunks)
         e.warmup_graphs()
         s = e.new_sequence()
         e.prefill([s], [PROMPT])
@@ -64,14 +60,6 @@ def _worker(rank, world, port, name, q, ekw=None):
 ])
 def test_tp2_gpu_matches_tp1(cuda, name, ekw):
     _tp2_vs_tp1(name, ekw)
-
-
-def test_tp2_gpu_fused_attention_oproj_matches_tp1(cuda, monkeypatch):
-    """The fused attention + o_proj launch on TP ranks (every bucket: LLMC_ATTN_OPROJ=all, TP on):
-    rank 0's partial carries the residual, the other rank's does not, the all-reduce follows."""
-    monkeypatch.setenv("LLMC_ATTN_OPROJ", "all")
-    monkeypatch.setenv("LLMC_ATTN_OPROJ_TP", "1")
-    _tp2_vs_tp1("llama-small", {})
 
 
 def _tp2_vs_tp1(name, ekw):

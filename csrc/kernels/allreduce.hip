@@ -1,63 +1,36 @@
 // K13: custom one-shot all-reduce / all-gather over IPC-mapped peer buffers (xGMI).
 //
-// Decode-sized TP collectives (a [B, H] bf16 hidden state: 8-64 KiB, 2 per layer) are pure
-// latency for RCCL (ring steps over one link each); MI355X has a direct xGMI link to every peer
-// (7 x ~153 GB/s), so a ONE-SHOT exchange — every rank reads every peer's copy directly and
-// reduces locally — is one link round trip. SURVEY.md §5.8 (2).
+// Decode-sized TP collectives (a [B, H] bf16 hidden state: 8-64 KiB, 2 per layer; the vocab-shard
+// logits gather) are pure latency for RCCL (ring steps over one link each); MI355X has a direct
+// xGMI link to every peer (7 x ~153 GB/s), so a ONE-SHOT exchange — every rank pushes its copy
+// into every peer's buffer and each reduces locally — is one one-way trip. SURVEY.md §5.8 (2).
+// Buffer layout and protocol (push, data-tagged granules, per-block epochs): car_proto.h.
 //
-// Buffers: each rank owns ONE uncached (fine-grained) allocation, exported with hipIpc and
-// mapped by every peer:   [ signals 64 KiB | data parity 0 (cap) | data parity 1 (cap) ]
-//   signals: ctr[kBlocks] (per-block launch epoch, persists across graph replays),
-//            flag[kMaxBlocks][kMaxRanks] (epoch of the last arrival of rank r for block b),
-//            timeout word (set when a bounded spin gives up).
-// Block b always owns the same 4 KiB chunks (c % kBlocks == b) whatever the message size, so
-// block b's epochs and data slices line up across ranks and across calls of different sizes. A
-// launch runs only the blocks that own data (min(kBlocks, chunks)): every rank issues the same
-// sequence of sizes, so an idle block's epoch simply stays put on every rank, and a decode-sized
-// [1, 4096] bf16 message costs 2 blocks' flag exchanges over xGMI instead of 32. Protocol per
-// launch, per block b:
-//   1. epoch = ctr[b] + 1; stage my slice into my data[epoch & 1] (uncached stores);
-//   2. every wave drains its stores (s_waitcnt vmcnt(0)), barrier, then ONE lane per peer
-//      stores `epoch` into peer.flag[b][me] (system-scope release);
-//   3. one lane per peer polls my flag[b][peer] >= epoch (relaxed, s_sleep, BOUNDED), then one
-//      system-scope acquire;
-//   4. read every rank's slice from data[epoch & 1] (fixed rank order -> bitwise-identical
-//      results on every rank), sum in f32, write the local output;
-//   5. ctr[b] = epoch.
-// Double-buffered data (by epoch parity) + monotone ">= epoch" flags make a second barrier
-// unnecessary: a peer can be at most one launch ahead (it cannot pass launch k+1's step 3 before
-// I signal k+1), so it writes the other parity while I still read this one.
-// The whole launch is graph-capturable: peers and sizes are fixed, epochs live in device memory.
+// Data mapping, shared by both one-shot kernels (so a granule position is only ever written by
+// ONE block, whose epochs are monotone): thread t of block b holds the 16-B vector v = b * 256 + t
+// of the message; its payload word j (4 B) travels as granule b * 1024 + j * 256 + t, so each
+// store / load instruction of a wave moves 64 consecutive granules (512 B).
+#include <hip/hip_ext.h>
+
 #include <cstring>
 
-#include "common.h"
+#include "car_proto.h"
 
 namespace llmc {
 
-constexpr int kMaxRanks = 8;
-constexpr int kMaxBlocks = 256;  // signal slots (two-shot launches use all of them)
-constexpr int kBlocks = 32;      // one-shot: blocks per launch (at most; see car_grid)
+constexpr int kBlocks = 64;      // one-shot: blocks per launch at most (256 KiB of payload)
 // two-shot: fixed grid (every launch, every rank). Kept to a quarter of the chip: the blocks spin
 // on their peers, and a full-chip grid of spinning blocks can starve a peer's queued kernel of CUs
 // when ranks share a GPU (a 512-thread, 160-KiB GEMM block needs a whole CU) -> spin timeout.
 constexpr int kTsBlocks = 64;
-constexpr int kChunk = 256;      // 16-B vectors per chunk (one per thread)
-constexpr size_t kSigBytes = 64 * 1024;
-constexpr int kFlagOff = 1024;                              // bytes: after ctr[kMaxBlocks]
-constexpr int kFlag2Off = kFlagOff + kMaxBlocks * kMaxRanks * 4;  // two-shot's second barrier
-constexpr int kTimeoutOff = kFlag2Off + kMaxBlocks * kMaxRanks * 4;
-static_assert(kTimeoutOff + 4 <= static_cast<int>(kSigBytes), "signal layout");
+static_assert(kTsBlocks <= kTsFlagBlocks, "two-shot flags");
+constexpr int kChunk = 256;      // 16-B vectors per block (one per thread)
 
-struct CarPeers {
-  char* base[kMaxRanks];  // each rank's buffer (own one included), mapped in this process
-};
-
-__device__ __forceinline__ uint32_t* sig_ctr(char* b) { return reinterpret_cast<uint32_t*>(b); }
 __device__ __forceinline__ uint32_t* sig_flag(char* b, int blk, int r, int off = kFlagOff) {
   return reinterpret_cast<uint32_t*>(b + off) + blk * kMaxRanks + r;
 }
 
-// steps 1-3: returns the epoch (LDS-broadcast). ``off``: which flag array (two-shot: 2 barriers)
+// two-shot barrier: returns the epoch (LDS-broadcast). ``off``: which flag array (2 barriers)
 __device__ __forceinline__ uint32_t car_arrive_and_wait(const CarPeers& P, int rank, int world, uint32_t* lds_epoch,
                                                         int off = kFlagOff) {
   const int b = blockIdx.x, tid = threadIdx.x;
@@ -72,9 +45,8 @@ __device__ __forceinline__ uint32_t car_arrive_and_wait(const CarPeers& P, int r
     unsigned spins = 0;
     while (__hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) < epoch) {
       __builtin_amdgcn_s_sleep(2);
-      if (++spins > (1u << 24)) {  // ~seconds: give up instead of hanging the GPU
-        __hip_atomic_store(reinterpret_cast<uint32_t*>(P.base[rank] + kTimeoutOff), 1u, __ATOMIC_RELAXED,
-                           __HIP_MEMORY_SCOPE_SYSTEM);
+      if (++spins > kCarSpinLimit) {  // ~seconds: give up instead of hanging the GPU
+        car_set_timeout(P, rank);
         break;
       }
     }
@@ -86,7 +58,7 @@ __device__ __forceinline__ uint32_t car_arrive_and_wait(const CarPeers& P, int r
 
 __device__ __forceinline__ uint32_t car_begin(const CarPeers& P, int rank, uint32_t* lds_epoch) {
   if (threadIdx.x == 0) {
-    *lds_epoch = __hip_atomic_load(sig_ctr(P.base[rank]) + blockIdx.x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) + 1;
+    *lds_epoch = __hip_atomic_load(car_ctr(P.base[rank]) + blockIdx.x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) + 1;
   }
   __syncthreads();
   return *lds_epoch;
@@ -94,38 +66,46 @@ __device__ __forceinline__ uint32_t car_begin(const CarPeers& P, int rank, uint3
 
 __device__ __forceinline__ void car_end(const CarPeers& P, int rank, uint32_t epoch) {
   if (threadIdx.x == 0)
-    __hip_atomic_store(sig_ctr(P.base[rank]) + blockIdx.x, epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    __hip_atomic_store(car_ctr(P.base[rank]) + blockIdx.x, epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
-// In-place sum over ranks of x [n16 x 16 B] (bf16).
+// Push my vector to every peer, then collect every peer's copy of the same vector (rank order).
+__device__ __forceinline__ void car_exchange(const CarPeers& P, int rank, int world, size_t cap, uint32_t epoch,
+                                             const u32x4& mine, uint32_t (&in)[kMaxRanks][4]) {
+  const long g0 = static_cast<long>(blockIdx.x) * 1024 + threadIdx.x;
+  const long g[4] = {g0, g0 + 256, g0 + 512, g0 + 768};
+#pragma unroll
+  for (int p = 0; p < kMaxRanks; ++p) {
+    if (p < world && p != rank) {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) car_put(P.base[p] + car_granule_off(epoch, cap, rank, g[j]), mine[j], epoch);
+    }
+  }
+  car_collect<4>(P, rank, world, cap, epoch, g, in);
+#pragma unroll
+  for (int j = 0; j < 4; ++j) in[rank][j] = mine[j];
+}
+
+// In-place sum over ranks of x [n16 x 16 B] (bf16), f32 in rank order (same bits on every rank).
 __global__ __launch_bounds__(256) void car_allreduce_kernel(CarPeers P, bf16_t* __restrict__ x, int n16, int rank,
                                                             int world, size_t cap) {
   __shared__ uint32_t lds_epoch;
-  const int v0 = blockIdx.x * kChunk + threadIdx.x, vstep = kBlocks * kChunk;
-  const u32x4* xv = reinterpret_cast<const u32x4*>(x);
-  // this thread's first vector is loaded before the epoch: the two memory round trips overlap
-  // (a decode-sized message is one vector per thread)
-  u32x4 first{};
-  if (v0 < n16) first = xv[v0];
+  const int v = blockIdx.x * kChunk + threadIdx.x;
+  u32x4 mine{};
+  if (v < n16) mine = reinterpret_cast<const u32x4*>(x)[v];  // overlaps the epoch round trip
   const uint32_t epoch = car_begin(P, rank, &lds_epoch);
-  const size_t doff = kSigBytes + (epoch & 1) * cap;
-  u32x4* mine = reinterpret_cast<u32x4*>(P.base[rank] + doff);
-  if (v0 < n16) mine[v0] = first;
-  for (int v = v0 + vstep; v < n16; v += vstep) mine[v] = xv[v];
-  car_arrive_and_wait(P, rank, world, &lds_epoch);
-  for (int v = v0; v < n16; v += vstep) {
+  if (v < n16) {
+    uint32_t in[kMaxRanks][4];
+    car_exchange(P, rank, world, cap, epoch, mine, in);
     float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-    u32x4 in[kMaxRanks];
-#pragma unroll
-    for (int r = 0; r < kMaxRanks; ++r)  // all peer loads in flight before the sums
-      if (r < world) in[r] = reinterpret_cast<const u32x4*>(P.base[r] + doff)[v];
 #pragma unroll
     for (int r = 0; r < kMaxRanks; ++r) {
       if (r < world) {
-        float f[8];
-        unpack8(in[r], f);
 #pragma unroll
-        for (int j = 0; j < 8; ++j) acc[j] += f[j];
+        for (int j = 0; j < 4; ++j) {
+          acc[2 * j] += bf16_lo(in[r][j]);
+          acc[2 * j + 1] += bf16_hi(in[r][j]);
+        }
       }
     }
     reinterpret_cast<u32x4*>(x)[v] = pack8(acc);
@@ -137,25 +117,17 @@ __global__ __launch_bounds__(256) void car_allreduce_kernel(CarPeers P, bf16_t* 
 __global__ __launch_bounds__(256) void car_allgather_kernel(CarPeers P, const char* __restrict__ x, char* __restrict__ out,
                                                             int n16, int rank, int world, size_t cap) {
   __shared__ uint32_t lds_epoch;
-  const int v0 = blockIdx.x * kChunk + threadIdx.x, vstep = kBlocks * kChunk;
-  const u32x4* xv = reinterpret_cast<const u32x4*>(x);
-  u32x4 first{};
-  if (v0 < n16) first = xv[v0];  // overlaps the epoch load (see car_allreduce_kernel)
+  const int v = blockIdx.x * kChunk + threadIdx.x;
+  u32x4 mine{};
+  if (v < n16) mine = reinterpret_cast<const u32x4*>(x)[v];
   const uint32_t epoch = car_begin(P, rank, &lds_epoch);
-  const size_t doff = kSigBytes + (epoch & 1) * cap;
-  u32x4* mine = reinterpret_cast<u32x4*>(P.base[rank] + doff);
-  if (v0 < n16) mine[v0] = first;
-  for (int v = v0 + vstep; v < n16; v += vstep) mine[v] = xv[v];
-  car_arrive_and_wait(P, rank, world, &lds_epoch);
-  u32x4* ov = reinterpret_cast<u32x4*>(out);
-  for (int v = v0; v < n16; v += vstep) {
-    u32x4 in[kMaxRanks];
+  if (v < n16) {
+    uint32_t in[kMaxRanks][4];
+    car_exchange(P, rank, world, cap, epoch, mine, in);
+    u32x4* ov = reinterpret_cast<u32x4*>(out);
 #pragma unroll
     for (int r = 0; r < kMaxRanks; ++r)
-      if (r < world) in[r] = reinterpret_cast<const u32x4*>(P.base[r] + doff)[v];
-#pragma unroll
-    for (int r = 0; r < kMaxRanks; ++r)
-      if (r < world) ov[static_cast<int64_t>(r) * n16 + v] = in[r];
+      if (r < world) ov[static_cast<int64_t>(r) * n16 + v] = u32x4{in[r][0], in[r][1], in[r][2], in[r][3]};
   }
   car_end(P, rank, epoch);
 }
@@ -264,7 +236,14 @@ using namespace llmc;
 
 static int car_grid(int n16) {
   const int chunks = (n16 + kChunk - 1) / kChunk;
-  return chunks < 1 ? 1 : (chunks < kBlocks ? chunks : kBlocks);
+  return chunks < 1 ? 1 : chunks;
+}
+
+// One-shot payload bytes per rank that a buffer of `cap` bytes per parity carries: kMaxRanks
+// slots of cap / kMaxRanks bytes, 8-B granules with 4 B of payload, 1024 granules per block.
+static size_t car_oneshot_max(size_t cap) {
+  const size_t blocks = cap / kMaxRanks / 8 / 1024;
+  return (blocks < static_cast<size_t>(kBlocks) ? blocks : kBlocks) * kChunk * 16;
 }
 
 extern "C" {
@@ -302,12 +281,25 @@ int llmc_ipc_close(void* p) { return static_cast<int>(hipIpcCloseMemHandle(p)); 
 size_t llmc_car_timeout_off() { return kTimeoutOff; }
 
 // Re-synchronise after a timeout: the caller's group has drained every stream (no launch in
-// flight on any rank) and meets in a host barrier before and after: epochs, flags and the
-// timeout word go back to zero on every rank.
-int llmc_car_reset(void* own) {
-  hipError_t e = hipMemset(own, 0, kSigBytes);
+// flight on any rank) and meets in a host barrier before and after: epochs, flags, granules and
+// the timeout word go back to zero on every rank.
+int llmc_car_reset(void* own, size_t cap) {
+  // the data too: granule tags restart with the epochs
+  hipError_t e = hipMemset(own, 0, kSigBytes + 2 * cap);
   if (e != hipSuccess) return static_cast<int>(e);
   return static_cast<int>(hipDeviceSynchronize());
+}
+
+// A new stream on `device` whose kernels run only on the CUs set in `mask` (bit i of word w = CU
+// 32 w + i): one-GPU rehearsals of multi-rank flows give each rank its own CUs, so ranks that
+// spin on each other (the custom collectives) run side by side as on separate GPUs.
+int llmc_stream_cu_mask(int device, const uint32_t* mask, int words, void** out) {
+  hipError_t e = hipSetDevice(device);
+  if (e != hipSuccess) return static_cast<int>(e);
+  hipStream_t st = nullptr;
+  e = hipExtStreamCreateWithCUMask(&st, static_cast<uint32_t>(words), mask);
+  *out = st;
+  return static_cast<int>(e);
 }
 
 // 1 if device `dev` can map memory of device `peer` (xGMI P2P), else 0; same device -> 1.
@@ -330,9 +322,12 @@ int llmc_car_timed_out(void* own, int* out) {
   return static_cast<int>(e);
 }
 
+size_t llmc_car_oneshot_max(size_t cap) { return car_oneshot_max(cap); }
+
 int llmc_car_allreduce(const void* const* bases, int rank, int world, size_t cap, void* x, size_t nbytes,
                        hipStream_t s) {
-  if (world < 1 || world > kMaxRanks || rank < 0 || rank >= world || nbytes % 16 || nbytes > cap) return -1;
+  if (world < 1 || world > kMaxRanks || rank < 0 || rank >= world || nbytes % 16 || nbytes > car_oneshot_max(cap))
+    return -1;
   CarPeers P;
   for (int r = 0; r < kMaxRanks; ++r) P.base[r] = r < world ? static_cast<char*>(const_cast<void*>(bases[r])) : nullptr;
   const int n16 = static_cast<int>(nbytes / 16);
@@ -342,7 +337,8 @@ int llmc_car_allreduce(const void* const* bases, int rank, int world, size_t cap
 
 int llmc_car_allgather(const void* const* bases, int rank, int world, size_t cap, const void* x, void* out,
                        size_t nbytes, hipStream_t s) {
-  if (world < 1 || world > kMaxRanks || rank < 0 || rank >= world || nbytes % 16 || nbytes > cap) return -1;
+  if (world < 1 || world > kMaxRanks || rank < 0 || rank >= world || nbytes % 16 || nbytes > car_oneshot_max(cap))
+    return -1;
   CarPeers P;
   for (int r = 0; r < kMaxRanks; ++r) P.base[r] = r < world ? static_cast<char*>(const_cast<void*>(bases[r])) : nullptr;
   const int n16 = static_cast<int>(nbytes / 16);

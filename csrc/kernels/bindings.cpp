@@ -62,7 +62,11 @@ int llmc_ipc_open(const void*, void**);
 int llmc_ipc_close(void*);
 int llmc_car_timed_out(void*, int*);
 size_t llmc_car_timeout_off();
-int llmc_car_reset(void*);
+int llmc_car_reset(void*, size_t);
+size_t llmc_car_oneshot_max(size_t);
+int llmc_gemv_ar(int, const void*, int, const void*, void*, int, int, int, const void* const*, int, int, size_t,
+                 hipStream_t);
+int llmc_stream_cu_mask(int, const uint32_t*, int, void**);
 int llmc_can_access_peer(int, int, int*);
 int llmc_car_twoshot(const void* const*, int, int, size_t, int, const void*, void*, long, int, int, hipStream_t);
 int llmc_car_allreduce(const void* const*, int, int, size_t, void*, size_t, hipStream_t);
@@ -210,7 +214,20 @@ PYBIND11_MODULE(_llmc_hip, m) {
     return v;
   });
   m.def("car_timeout_off", []() { return llmc_car_timeout_off(); });
-  m.def("car_reset", [](ptr own) { check(llmc_car_reset(P(own)), "car_reset"); });
+  m.def("car_reset", [](ptr own, size_t cap) { check(llmc_car_reset(P(own), cap), "car_reset"); });
+  m.def("car_oneshot_max", [](size_t cap) { return llmc_car_oneshot_max(cap); });
+  m.def("gemv_ar", [](int M, ptr x, int xs, ptr W, ptr h, int hs, int N, int K, const std::vector<ptr>& bases, int rank,
+                      int world, size_t cap, ptr s) {
+    std::vector<const void*> b(bases.size());
+    for (size_t i = 0; i < bases.size(); ++i) b[i] = P(bases[i]);
+    check(llmc_gemv_ar(M, P(x), xs, P(W), P(h), hs, N, K, b.data(), rank, world, cap, S(s)), "gemv_ar");
+  });
+  // a stream restricted to a set of CUs (rehearsals: ranks sharing one GPU on disjoint CUs)
+  m.def("stream_cu_mask", [](int device, const std::vector<uint32_t>& mask) {
+    void* st = nullptr;
+    check(llmc_stream_cu_mask(device, mask.data(), static_cast<int>(mask.size()), &st), "stream_cu_mask");
+    return reinterpret_cast<ptr>(st);
+  });
   m.def("can_access_peer", [](int dev, int peer) {
     int v = 0;
     check(llmc_can_access_peer(dev, peer, &v), "can_access_peer");

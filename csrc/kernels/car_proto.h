@@ -1,0 +1,100 @@
+// K13 custom-collective protocol shared by the standalone one-shot kernels (allreduce.hip) and the
+// row-parallel GEMV's fused all-reduce epilogue (gemv_core.h, EPI_AR).
+//
+// Each rank owns ONE uncached (fine-grained) allocation, exported with hipIpc and mapped by every
+// peer:   [ signals kSigBytes | data parity 0 (cap) | data parity 1 (cap) ]
+//   signals: ctr[kMaxBlocks]   per-block launch epoch (persists across graph replays),
+//            two-shot flags    (allreduce.hip, car_twoshot_kernel),
+//            timeout word      (set when a bounded spin gives up).
+//   data parity p: kMaxRanks slots of cap / kMaxRanks bytes; slot r receives rank r's pushes.
+//
+// One-shot protocol (push, data-tagged granules; MI355X_MICROARCH.md "handoff-1to1": the price of
+// a hand-off is in the consumer's queue, and a granule that carries its own tag needs no flag):
+//   1. epoch = ctr[b] + 1 (block b owns the same data on every rank and every launch);
+//   2. every rank STORES its contribution straight into every peer's slot [parity][rank] as 8-byte
+//      granules {4-B payload, 4-B tag = epoch}, one 64-bit atomic store each (single-copy atomic
+//      by the memory model, also across xGMI), fire and forget: no fence, no flag, no drain;
+//   3. it polls its OWN buffer (local memory) until every peer's granules carry this epoch
+//      (bounded spin), and combines them in rank order (bitwise-identical results on all ranks);
+//   4. ctr[b] = epoch.
+// A peer can be at most one participation of block b ahead (it cannot finish its launch k+1
+// before my launch-(k+1) pushes, which follow my launch k), so it writes the other parity while I
+// still read this one; tags never repeat (epochs only grow; a resync zeroes the whole buffer).
+// Against the pull protocol it replaces (stage locally, release-flag each peer, poll, acquire,
+// read the peers' copies over xGMI) this is one one-way trip instead of a flag trip plus a remote
+// read round trip, and no system-scope fences.
+#pragma once
+#include "common.h"
+
+namespace llmc {
+
+constexpr int kMaxRanks = 8;
+constexpr int kMaxBlocks = 1024;     // epoch counters: blocks of any one-shot / EPI_AR launch
+constexpr int kTsFlagBlocks = 256;   // two-shot flag slots (its grid is kTsBlocks <= this)
+constexpr size_t kSigBytes = 128 * 1024;
+constexpr int kFlagOff = 4 * kMaxBlocks;                              // bytes: after ctr[kMaxBlocks]
+constexpr int kFlag2Off = kFlagOff + kTsFlagBlocks * kMaxRanks * 4;   // two-shot's second barrier
+constexpr int kTimeoutOff = kFlag2Off + kTsFlagBlocks * kMaxRanks * 4;
+static_assert(kTimeoutOff + 4 <= static_cast<int>(kSigBytes), "signal layout");
+constexpr unsigned kCarSpinLimit = 1u << 24;  // polls (s_sleep 2 each, ~seconds) before giving up
+
+struct CarPeers {
+  char* base[kMaxRanks];  // each rank's buffer (own one included), mapped in this process
+};
+
+// What a fused epilogue needs besides the buffers: who I am and the data parity size.
+struct CarArgs {
+  CarPeers P;
+  int rank, world;
+  long cap;  // bytes per data parity
+};
+
+__device__ __forceinline__ uint32_t* car_ctr(char* b) { return reinterpret_cast<uint32_t*>(b); }
+
+// Byte offset of granule g of slot r in parity (epoch & 1).
+__device__ __forceinline__ size_t car_granule_off(uint32_t epoch, size_t cap, int r, long g) {
+  return kSigBytes + (epoch & 1) * cap + static_cast<size_t>(r) * (cap / kMaxRanks) + static_cast<size_t>(g) * 8;
+}
+
+__device__ __forceinline__ void car_put(char* p, uint32_t payload, uint32_t tag) {
+  __hip_atomic_store(reinterpret_cast<uint64_t*>(p), (static_cast<uint64_t>(tag) << 32) | payload, __ATOMIC_RELAXED,
+                     __HIP_MEMORY_SCOPE_SYSTEM);
+}
+__device__ __forceinline__ uint64_t car_get(const char* p) {
+  return __hip_atomic_load(reinterpret_cast<const uint64_t*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+__device__ __forceinline__ void car_set_timeout(const CarPeers& P, int rank) {
+  __hip_atomic_store(reinterpret_cast<uint32_t*>(P.base[rank] + kTimeoutOff), 1u, __ATOMIC_RELAXED,
+                     __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+// Wait until granules g[0..NG) of every peer's slot (not mine) carry `epoch`; payloads out in
+// v[r][i] (v[rank][*] untouched). Every load in flight at once, re-polled together; bounded.
+template <int NG>
+__device__ __forceinline__ void car_collect(const CarPeers& P, int rank, int world, size_t cap, uint32_t epoch,
+                                            const long (&g)[NG], uint32_t (&v)[kMaxRanks][NG]) {
+  const char* own = P.base[rank];
+  for (unsigned spins = 0;; ++spins) {
+    bool ok = true;
+#pragma unroll
+    for (int r = 0; r < kMaxRanks; ++r) {
+      if (r < world && r != rank) {
+#pragma unroll
+        for (int i = 0; i < NG; ++i) {
+          const uint64_t x = car_get(own + car_granule_off(epoch, cap, r, g[i]));
+          v[r][i] = static_cast<uint32_t>(x);
+          ok = ok && static_cast<uint32_t>(x >> 32) == epoch;
+        }
+      }
+    }
+    if (ok) return;
+    if (spins >= kCarSpinLimit) {
+      car_set_timeout(P, rank);
+      return;
+    }
+    __builtin_amdgcn_s_sleep(2);
+  }
+}
+
+}  // namespace llmc

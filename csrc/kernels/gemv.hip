@@ -29,7 +29,7 @@ static int launch_gemv_g(const void* x, int x_stride, const void* nw, float eps,
   const int rows_per_block = WAVES * RPW;
   const int grid = (N + rows_per_block - 1) / rows_per_block;
   kern<<<grid, NT, lds, s>>>((const bf16_t*)x, x_stride, (const bf16_t*)nw, eps, (const bf16_t*)W, out, out_stride, N,
-                             K, nullptr, 1, rope);
+                             K, nullptr, 1, rope, CarArgs{});
   return static_cast<int>(hipGetLastError());
 }
 
@@ -137,6 +137,63 @@ extern "C" int llmc_gemv_qkv_rope(int M, const void* x, int x_stride, const void
   return gemv_dispatch(M, x, x_stride, norm_w, eps, W, nullptr, 0, N, K, EPI_ROPE, rope, mfma != 0, s);
 }
 
+// Row-parallel decode projection with the all-reduce fused into the epilogue (EPI_AR, gemv_core.h):
+// h = sum over ranks of W_r . x_r (+ h on rank 0), for M <= 2 tokens. `bases`: every rank's fused-AR
+// buffer (car_proto.h layout), `cap` its bytes per data parity.
+namespace llmc {
+template <int M, int NT, int UNROLL>
+static int launch_gemv_ar(const void* x, int x_stride, const void* W, void* h, int h_stride, int N, int K,
+                          const CarArgs& ar, hipStream_t s) {
+  constexpr int WAVES = NT / kWave;
+  auto kern = gemv_kernel<M, NT, 1, UNROLL, PRO_NONE, EPI_AR, false>;
+  const size_t lds = static_cast<size_t>(M) * K * sizeof(bf16_t) + 2 * M * WAVES * sizeof(float);
+  if (lds > 160 * 1024) return -2;
+  static bool attr_set = false;
+  if (lds > 64 * 1024 && !attr_set) {
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize,
+                              160 * 1024);
+    attr_set = true;
+  }
+  const int grid = (N + WAVES - 1) / WAVES;
+  if (grid > kMaxBlocks || static_cast<size_t>(grid) * kArGranulesPerBlock * 8 > static_cast<size_t>(ar.cap) / kMaxRanks)
+    return -6;
+  kern<<<grid, NT, lds, s>>>((const bf16_t*)x, x_stride, nullptr, 0.f, (const bf16_t*)W, h, h_stride, N, K, nullptr, 1,
+                             RopeEpi{}, ar);
+  return static_cast<int>(hipGetLastError());
+}
+
+template <int M>
+static int gemv_ar_geom(const void* x, int x_stride, const void* W, void* h, int h_stride, int N, int K,
+                        const CarArgs& ar, hipStream_t s) {
+  // the dense GEMV's geometry rule (pick_waves): same blocks, same accumulation order, same bits
+  const int w = pick_waves(N, false);
+  if (w == 16 && K >= 8192 && N <= 4096) return launch_gemv_ar<M, 1024, 8>(x, x_stride, W, h, h_stride, N, K, ar, s);
+  switch (w) {
+    case 16: return launch_gemv_ar<M, 1024, 4>(x, x_stride, W, h, h_stride, N, K, ar, s);
+    case 12: return launch_gemv_ar<M, 768, 4>(x, x_stride, W, h, h_stride, N, K, ar, s);
+    case 8: return launch_gemv_ar<M, 512, 4>(x, x_stride, W, h, h_stride, N, K, ar, s);
+    case 4: return launch_gemv_ar<M, 256, 8>(x, x_stride, W, h, h_stride, N, K, ar, s);
+    default: return -7;
+  }
+}
+}  // namespace llmc
+
+extern "C" int llmc_gemv_ar(int M, const void* x, int x_stride, const void* W, void* h, int h_stride, int N, int K,
+                            const void* const* bases, int rank, int world, size_t cap, hipStream_t s) {
+  if (K % 8 != 0 || N % 2 != 0 || world < 1 || world > kMaxRanks || rank < 0 || rank >= world) return -1;
+  CarArgs ar{};
+  for (int r = 0; r < kMaxRanks; ++r)
+    ar.P.base[r] = r < world ? static_cast<char*>(const_cast<void*>(bases[r])) : nullptr;
+  ar.rank = rank;
+  ar.world = world;
+  ar.cap = static_cast<long>(cap);
+  switch (M) {
+    case 1: return gemv_ar_geom<1>(x, x_stride, W, h, h_stride, N, K, ar, s);
+    case 2: return gemv_ar_geom<2>(x, x_stride, W, h, h_stride, N, K, ar, s);
+    default: return -3;
+  }
+}
+
 // MoE decode (K11 at batch 1): one GEMV per (token, top-k slot) pair against the selected
 // expert's weights; expert ids are read on device, so the launch is graph-replayable.
 namespace llmc {
@@ -149,7 +206,7 @@ static int launch_moe_gemv(int npairs, const void* x, int x_stride, const void* 
   dim3 grid((N + WAVES * RPW - 1) / (WAVES * RPW), npairs);
   gemv_kernel<1, NT, RPW, 4, PRO, EPI, true><<<grid, NT, lds, s>>>(
       (const bf16_t*)x, x_stride, (const bf16_t*)nw, eps, (const bf16_t*)W, out, out_stride, N, K,
-      (const int32_t*)ids, x_div, RopeEpi{});
+      (const int32_t*)ids, x_div, RopeEpi{}, CarArgs{});
   return static_cast<int>(hipGetLastError());
 }
 
@@ -188,7 +245,7 @@ extern "C" int llmc_moe_down_combine(int T, const void* act, int act_stride, con
   wts.cos_t = static_cast<const float*>(w);
   dim3 grid((N + WAVES - 1) / WAVES, T);
   kern<<<grid, NT, lds, s>>>((const bf16_t*)act, act_stride, nullptr, 0.f, (const bf16_t*)W, h, h_stride, N, K,
-                             (const int32_t*)ids, 1, wts);
+                             (const int32_t*)ids, 1, wts, CarArgs{});
   return static_cast<int>(hipGetLastError());
 }
 
@@ -218,7 +275,7 @@ static int launch_sweep(const void* x, const void* nw, const void* W, void* out,
   const size_t lds = static_cast<size_t>(K) * sizeof(bf16_t) + WAVES * sizeof(float);
   const int grid = (N + WAVES * RPW - 1) / (WAVES * RPW);
   gemv_kernel<1, NT, RPW, UNROLL, PRO_NORM, EPI_BF16, false><<<grid, NT, lds, s>>>(
-      (const bf16_t*)x, K, (const bf16_t*)nw, 1e-5f, (const bf16_t*)W, out, N, N, K, nullptr, 1, RopeEpi{});
+      (const bf16_t*)x, K, (const bf16_t*)nw, 1e-5f, (const bf16_t*)W, out, N, N, K, nullptr, 1, RopeEpi{}, CarArgs{});
   return static_cast<int>(hipGetLastError());
 }
 }  // namespace llmc

@@ -20,12 +20,25 @@
 #pragma once
 #include <type_traits>
 
+#include "car_proto.h"
 #include "common.h"
 
 namespace llmc {
 
 enum { PRO_NONE = 0, PRO_NORM = 1 };
-enum { EPI_BF16 = 0, EPI_F32 = 1, EPI_RESADD = 2, EPI_SILU = 3, EPI_ROPE = 4, EPI_COMBINE = 5 };
+enum { EPI_BF16 = 0, EPI_F32 = 1, EPI_RESADD = 2, EPI_SILU = 3, EPI_ROPE = 4, EPI_COMBINE = 5, EPI_AR = 6 };
+
+// EPI_AR: a tensor-parallel rank's row-parallel projection (decode o_proj / down_proj) with the
+// all-reduce in its own epilogue: h = sum over ranks of (W_r . x_r), rank 0's term carrying the
+// residual h. Block b of every rank owns the same rows, so block b only exchanges with block b
+// of its peers, over car_proto.h's push protocol (its own buffer, granules [16 b, 16 b + NG) of
+// every slot): the block's bf16 partials go straight into every peer's buffer as data-tagged
+// granules, and it sums its peers' granules in rank order as they land — the numerics of a
+// separate EPI_RESADD / EPI_BF16 GEMV followed by the one-shot all-reduce, bit for bit, without
+// that kernel's launch, its boundary and its re-read of h. Every block of a launch is dispatched
+// in index order on every rank, so the lowest unfinished block is resident everywhere: no
+// deadlock whatever else shares the GPUs (the spin is bounded anyway).
+constexpr int kArGranulesPerBlock = 16;
 
 struct RopeEpi {
   bf16_t* q_out;            // [M, q_stride], canonical head-major layout
@@ -51,7 +64,7 @@ __global__ __launch_bounds__(NT) void gemv_kernel(const bf16_t* __restrict__ x, 
                                                   const bf16_t* __restrict__ norm_w, float eps,
                                                   const bf16_t* __restrict__ W, void* __restrict__ out,
                                                   int out_stride, int N, int K, const int32_t* __restrict__ expert_ids,
-                                                  int x_div, RopeEpi rope) {
+                                                  int x_div, RopeEpi rope, CarArgs ar) {
   constexpr int WAVES = NT / kWave;
   constexpr bool PAIR_LDS = (EPI == EPI_SILU || EPI == EPI_ROPE) && RPW == 1;  // host: N % (2 * WAVES) == 0
   // EXPERT (MoE decode): blockIdx.y = (token, slot) pair; weights of expert expert_ids[pair],
@@ -132,6 +145,22 @@ __global__ __launch_bounds__(NT) void gemv_kernel(const bf16_t* __restrict__ x, 
   issue(cur, lane);
   __builtin_amdgcn_sched_barrier(0);
 
+
+  // EPI_AR: this block's epoch and (rank 0) the residual of this wave's row, both issued behind the
+  // first weight batch (in-order retirement: waiting for them later waits for nothing else)
+  uint32_t ar_epoch = 0;
+  float ar_resid[M];
+  if constexpr (EPI == EPI_AR) {
+    static_assert(RPW == 1 && M <= 2 && M * WAVES / 2 <= kArGranulesPerBlock, "EPI_AR geometry");
+    if (tid == 0)
+      ar_epoch = __hip_atomic_load(car_ctr(ar.P.base[ar.rank]) + blockIdx.x, __ATOMIC_RELAXED,
+                                   __HIP_MEMORY_SCOPE_SYSTEM) + 1;
+#pragma unroll
+    for (int m = 0; m < M; ++m)
+      ar_resid[m] = ar.rank == 0 && row0 < N
+                        ? bf16_to_f32(reinterpret_cast<const bf16_t*>(out)[static_cast<int64_t>(m) * out_stride + row0])
+                        : 0.f;
+  }
 
   // RoPE epilogue operands (PAIR_LDS: one row per even wave) are wave-uniform, so they come
   // through the SCALAR cache (s_load, counted by lgkmcnt): as vector loads they queued behind the
@@ -255,7 +284,7 @@ __global__ __launch_bounds__(NT) void gemv_kernel(const bf16_t* __restrict__ x, 
     }
   }
   __syncthreads();
-  if (!PAIR_LDS && row0 >= N) return;  // PAIR_LDS: every wave reaches the pair barrier
+  if (!PAIR_LDS && EPI != EPI_AR && row0 >= N) return;  // PAIR_LDS / EPI_AR: every wave reaches the barriers
   if constexpr (PAIR_LDS && EPI == EPI_ROPE) {
     const int w_u = __builtin_amdgcn_readfirstlane(wave);
     const int r_u = (blockIdx.x * WAVES + w_u) * RPW;
@@ -387,6 +416,49 @@ __global__ __launch_bounds__(NT) void gemv_kernel(const bf16_t* __restrict__ x, 
           }
         }
     }
+    return;
+  }
+  if constexpr (EPI == EPI_AR) {
+    constexpr int HP = WAVES / 2, NG = M * HP;  // row pairs per block; granules per rank
+    // the block's values (rank 0: + residual), [M][WAVES] f32 after the norm-partials area
+    float* rowv = reinterpret_cast<float*>(smem + static_cast<size_t>(M) * K * sizeof(bf16_t)) + M * WAVES;
+#pragma unroll
+    for (int m = 0; m < M; ++m)
+      if (lane == m) rowv[m * WAVES + wave] = acc[0][m] + ar_resid[m];
+    __syncthreads();
+    if (wave != 0) return;
+    const uint32_t epoch = __shfl(ar_epoch, 0, 64);
+    const int rb = blockIdx.x * WAVES;
+    const int pairs = max(0, min(WAVES, N - rb)) / 2;  // N even: a pair is whole or absent
+    const long gbase = static_cast<long>(blockIdx.x) * kArGranulesPerBlock;
+    auto payload = [&](int gi) {  // my bf16 pair of granule gi (rows 2j, 2j + 1 of token m)
+      const int m = gi / HP, j = gi % HP;
+      return pack_bf16x2(rowv[m * WAVES + 2 * j], rowv[m * WAVES + 2 * j + 1]);
+    };
+    for (int idx = lane; idx < ar.world * NG; idx += kWave) {  // push: (peer, granule)
+      const int p = idx / NG, gi = idx % NG;
+      if (p != ar.rank && gi % HP < pairs)
+        car_put(ar.P.base[p] + car_granule_off(epoch, ar.cap, ar.rank, gbase + gi), payload(gi), epoch);
+    }
+    if (lane < NG && lane % HP < pairs) {  // collect my granule of every peer, sum in rank order
+      const long g[1] = {gbase + lane};
+      uint32_t in[kMaxRanks][1];
+      car_collect<1>(ar.P, ar.rank, ar.world, ar.cap, epoch, g, in);
+      in[ar.rank][0] = payload(lane);
+      float lo = 0.f, hi = 0.f;
+#pragma unroll
+      for (int r = 0; r < kMaxRanks; ++r) {
+        if (r < ar.world) {
+          lo += bf16_lo(in[r][0]);
+          hi += bf16_hi(in[r][0]);
+        }
+      }
+      const int m = lane / HP, j = lane % HP;
+      *reinterpret_cast<uint32_t*>(reinterpret_cast<bf16_t*>(out) + static_cast<int64_t>(m) * out_stride + rb + 2 * j) =
+          pack_bf16x2(lo, hi);
+    }
+    if (lane == 0)
+      __hip_atomic_store(car_ctr(ar.P.base[ar.rank]) + blockIdx.x, epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     return;
   }
   if constexpr (COMBINE) {

@@ -51,6 +51,9 @@ class EngineConfig:
     prefill_chunk: int = 8192
     init_scale: float = 1.0
     stream_priority: int = 0
+    # rehearsals only: run this engine's stream on CUs [lo, hi] ("lo-hi"; default LLMC_CU_MASK), so
+    # TP ranks sharing one GPU each get CUs of their own, as they would have GPUs of their own
+    cu_mask: str = dataclasses.field(default_factory=lambda: os.environ.get("LLMC_CU_MASK", ""))
     # TP prefill: shard the residual stream by token rows between layers (reduce-scatter +
     # all-gather instead of all-reduce) for chunks of >= sp_min_tokens tokens
     sequence_parallel: bool = True
@@ -185,7 +188,17 @@ class Engine:
         self.mfma_decode = self.on_gpu and self.ecfg.max_batch >= 3
         if self.on_gpu:
             torch.cuda.set_device(self.device)
-            self.stream = torch.cuda.Stream(self.device, priority=self.ecfg.stream_priority)
+            if self.ecfg.cu_mask:
+                lo, hi = (int(v) for v in self.ecfg.cu_mask.split("-"))
+                words = [0] * max(8, hi // 32 + 1)
+                for cu in range(lo, hi + 1):
+                    words[cu // 32] |= 1 << (cu % 32)
+                from ..utils.native import kernels
+
+                ptr = kernels().stream_cu_mask(self.device.index or 0, words)
+                self.stream = torch.cuda.ExternalStream(ptr, device=self.device)
+            else:
+                self.stream = torch.cuda.Stream(self.device, priority=self.ecfg.stream_priority)
         else:
             self.stream = None
         e = self.ecfg
@@ -463,7 +476,13 @@ class Engine:
         self.tp.reduce_scatter_rows(pbuf, hs)
 
     def _row_parallel(self, x: torch.Tensor, W: torch.Tensor, h: torch.Tensor) -> None:
-        """h += x @ W^T across the TP group (residual folded into rank 0's partial)."""
+        """h += x @ W^T across the TP group (residual folded into rank 0's partial). Decode rows
+        (<= 2, VALU GEMV form) of a group with mapped peers: ONE launch, the all-reduce in the
+        GEMV's epilogue (EPI_AR); otherwise the GEMV/GEMM, then the group's all-reduce."""
+        car = self.tp.custom_fused
+        if car is not None and h.is_cuda and x.shape[0] <= 2 and not self.mfma_decode and h.is_contiguous():
+            car.gemv_allreduce(x, W, h)
+            return
         ops.linear(x, W, EPI_RESADD if self.tp.rank == 0 else EPI_BF16, out=h, mfma=self.mfma_decode)
         self.tp.all_reduce_(h)
 
@@ -569,7 +588,10 @@ class Engine:
         h, q, attn, act = self.h[:B], self.q[:B], self.attn[:B], self.act[:B]
         ops.embedding(self.tokens_in[:B], self.w.embed, out=h)
         ao_chunk = self.ao_chunks[-1 if bucket is None else bucket] if B == 1 else 0
+        dbg = self._debug_layer_io  # eager debug steps only: each layer's input, then the last output
         for li, Lw in enumerate(self.w.layers):
+            if dbg is not None:
+                dbg.append(h.clone())
             ops.qkv_rope(h, Lw.w_qkv, Lw.ln1, c.rms_eps, q, self.k_cache[li], self.v_cache[li], self.positions[:B],
                          self.slots[:B], self.cos_t, self.sin_t, self.nh, self.nkv, self.D, self.bs,
                          mfma=self.mfma_decode)
@@ -587,7 +609,40 @@ class Engine:
             else:
                 ops.linear(h, Lw.w_gu, EPI_SILU, out=act, norm_w=Lw.ln2, eps=c.rms_eps, mfma=self.mfma_decode)
                 self._row_parallel(act, Lw.w_down, h)
+        if dbg is not None:
+            dbg.append(h.clone())
         self._lm_head_sample(B)
+
+    _debug_layer_io: Optional[list] = None
+
+    @torch.no_grad()
+    def debug_decode_layers(self, prompt: Seq[int]):
+        """Per-layer hidden states of ONE eager decode step after prefilling ``prompt`` (TP=1, one
+        row): (hs [n_layers + 1, H] bf16 — the input of every layer, then the last layer's output —,
+        the position of the decoded token). The hook of the per-layer numerics test, which runs an
+        fp32 oracle of each layer on the engine's own input and KV cache."""
+        if self.tp.size != 1:
+            raise EngineError("debug_decode_layers: TP=1 only")
+        seq = self.new_sequence()
+        try:
+            with self._on_stream():
+                self.prefill([seq], [list(prompt)])
+                self._reserve(seq, seq.length + 4)
+                self._use_topkp = False
+                self._bind_rows([seq], [SamplingParams(2, 0.0, 1.0, 0, 0, False)])
+                self._sample(1, self._gather_logits(1))  # the prefill's token -> this step's input
+                pos = int(self.positions[0].item())
+                self._debug_layer_io = []
+                try:
+                    self._decode_step(1, self._bucket(seq.length + 4))
+                    hs = torch.cat(self._debug_layer_io)
+                finally:
+                    self._debug_layer_io = None
+            if self.on_gpu:
+                self.stream.synchronize()
+            return hs, pos
+        finally:
+            self.free_sequence(seq)
 
     def _lm_head_sample(self, B: int) -> None:
         lg = self.logits_local[:B]

@@ -319,3 +319,43 @@ def reference_logits(w, cfg, ids, out_pos, cos_t: torch.Tensor, sin_t: torch.Ten
     sel = torch.as_tensor(out_pos, dtype=torch.long, device=dev)
     hn = rmsnorm(h[sel], w.final_norm, cfg.rms_eps)
     return hn.float() @ w.lm_head.float().t()
+
+
+@torch.no_grad()
+def reference_decode_layer(L, cfg, h_in: torch.Tensor, k_cache: torch.Tensor, v_cache: torch.Tensor,
+                           bt_row: torch.Tensor, pos: int, cos_t: torch.Tensor, sin_t: torch.Tensor, nh: int, nkv: int,
+                           bs: int, p_bf16: bool = False) -> torch.Tensor:
+    """fp32 reference of ONE dense decode layer for one token at position ``pos``, fed the engine's
+    own layer input ``h_in`` [1, H] and the engine's own paged K/V of positions [0, pos) (the
+    token's own k/v are computed here): the layer output h [1, H] bf16, rounded where the engine
+    rounds (normed rows, q/k/v, attention output, residual stream, SiLU product). Isolates one
+    layer's error from the depth amplification of a whole-model comparison."""
+    dev = h_in.device
+    bf = torch.bfloat16
+    D = cfg.head_dim
+    G, half = nh // nkv, D // 2
+    xn = rmsnorm(h_in, L.ln1, cfg.rms_eps)
+    qkv = (xn.float() @ L.w_qkv.float().t()).to(bf)[0]
+    qk = qkv[: (nh + nkv) * D].view(nh + nkv, half, 2).float()
+    c, sn = cos_t.to(dev)[pos].float(), sin_t.to(dev)[pos].float()
+    x1, x2 = qk[..., 0], qk[..., 1]
+    rot = torch.cat([x1 * c - x2 * sn, x2 * c + x1 * sn], dim=-1).to(bf)  # [nh + nkv, D]
+    q = rot[:nh].float().view(nkv, G, D)
+    k_new = rot[nh:].float()
+    v_new = qkv[(nh + nkv) * D:(nh + 2 * nkv) * D].view(nkv, D).float()
+    k_old = _gather_kv(k_cache, bt_row, pos, bs).float()  # [pos, nkv, D]
+    v_old = _gather_kv(v_cache, bt_row, pos, bs).float()
+    k = torch.cat([k_old, k_new.unsqueeze(0)])
+    v = torch.cat([v_old, v_new.unsqueeze(0)])
+    s = torch.einsum("kgd,tkd->kgt", q, k) / math.sqrt(D)
+    if p_bf16:
+        e = torch.exp(s - s.amax(-1, keepdim=True))
+        o = torch.einsum("kgt,tkd->kgd", e.to(bf).float(), v) / e.sum(-1, keepdim=True)
+    else:
+        o = torch.einsum("kgt,tkd->kgd", torch.softmax(s, dim=-1), v)
+    attn = o.reshape(1, nh * D).to(bf)
+    h = (h_in.float() + attn.float() @ L.w_o.float().t()).to(bf)
+    xn = rmsnorm(h, L.ln2, cfg.rms_eps)
+    gu = xn.float() @ L.w_gu.float().t()
+    act = (torch.nn.functional.silu(gu[:, 0::2]) * gu[:, 1::2]).to(bf)
+    return (h.float() + act.float() @ L.w_down.float().t()).to(bf)

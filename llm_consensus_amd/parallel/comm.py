@@ -56,24 +56,34 @@ class TPGroup:
         self.ctrl = ctrl      # host control group (gloo) over the same ranks, or None
         self.custom = None    # one-shot CustomAllReduce once enable_custom() ran
         self.custom2 = None   # its two-shot twin for prefill-sized messages
+        self.custom_fused = None  # the row-parallel decode GEMVs' fused all-reduce buffer (EPI_AR)
 
     def enable_custom(self, device, cap: Optional[int] = None, cap2: Optional[int] = None) -> bool:
         """Map the group's IPC buffers for the custom collectives (GPU groups of 2..8 ranks).
         Collective; returns False on every rank (RCCL stays in charge) when any rank failed."""
         if self.size == 1 or self.custom is not None:
             return self.custom is not None
-        from .custom_ar import DEFAULT_CAP, TWOSHOT_CAP, CustomAllReduce, CustomAllReduceUnavailable
+        import os
+
+        from .custom_ar import DEFAULT_CAP, FUSED_CAP, TWOSHOT_CAP, CustomAllReduce, CustomAllReduceUnavailable
 
         try:
             self.custom = CustomAllReduce(self.group, self.rank, self.size, device, cap or DEFAULT_CAP)
             self.custom2 = CustomAllReduce(self.group, self.rank, self.size, device, cap2 or TWOSHOT_CAP)
+            # the same decision on every rank (environment of the whole job; A/B: LLMC_FUSED_AR=0)
+            if os.environ.get("LLMC_FUSED_AR", "1") != "0":
+                self.custom_fused = CustomAllReduce(self.group, self.rank, self.size, device, FUSED_CAP)
         except CustomAllReduceUnavailable as e:
             warnings.warn(f"custom all-reduce disabled, using RCCL: {e}")
-            if self.custom is not None:
-                self.custom.close()
-            self.custom = self.custom2 = None
+            for c in (self.custom, self.custom2, self.custom_fused):
+                if c is not None:
+                    c.close()
+            self.custom = self.custom2 = self.custom_fused = None
             return False
         return True
+
+    def collectives(self):
+        return [c for c in (self.custom, self.custom2, self.custom_fused) if c is not None]
 
     def graph_capture_ok(self, device) -> bool:
         """Can this group's RCCL collectives run inside the engine's decode HIP graphs? The
@@ -131,7 +141,7 @@ class TPGroup:
     def custom_timed_out(self) -> bool:
         """Local: did a custom-collective spin give up since the last resync (reads device memory,
         after the caller synchronised its stream)?"""
-        return any(c is not None and c.timed_out() for c in (self.custom, self.custom2))
+        return any(c.timed_out() for c in self.collectives())
 
     def check_collectives(self) -> bool:
         """Collective over ``ctrl`` (every rank calls it at the same point): True when every rank's
@@ -142,9 +152,8 @@ class TPGroup:
             return True
         if not self.any_rank(self.custom_timed_out()):
             return True
-        for c in (self.custom, self.custom2):
-            if c is not None:
-                c.resync()
+        for c in self.collectives():
+            c.resync()
         return False
 
     @staticmethod

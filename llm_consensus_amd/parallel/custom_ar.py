@@ -7,8 +7,10 @@ theirs (bounded spin) and reads the peers' copies directly. No host involvement 
 is capturable in the decode HIP graph.
 
 Two buffer classes per TP group (``TPGroup.enable_custom``):
-  * one-shot (decode: <= 1 MiB, e.g. a [B, H] hidden state or a vocab-shard logits gather): every
-    rank reads every peer's whole message — one link round trip;
+  * one-shot (decode: <= 256 KiB, e.g. a [B, H] hidden state or a vocab-shard logits gather): every
+    rank pushes its whole message into every peer's buffer as data-tagged granules and reduces what
+    its peers pushed — one one-way trip over the link, no flag or fence; the same exchange also
+    runs inside the row-parallel decode GEMVs' epilogue (``gemv_allreduce``, its own buffer);
   * two-shot (prefill: > 1 MiB, sequence-parallel reduce-scatter / all-gather): reduce-scatter +
     all-gather phases inside one launch, each rank pulling only 1/world of every peer's message per
     phase over all of its xGMI links at once; messages larger than the buffer run as pieces.
@@ -25,7 +27,10 @@ import torch
 
 from ..utils.native import kernels
 
-DEFAULT_CAP = 1 << 20  # bytes per parity: [4, 8192] bf16 hidden = 64 KiB; logits gather [4, 32064] f32 = 512 KiB
+# bytes per data parity. One-shot: 8 slots of 8-B granules carrying 4 B each -> cap / 16 of payload
+# per rank (256 KiB: a [4, 8192] bf16 hidden row is 64 KiB, the TP=2 logits gather [1, 64128] f32 256 KiB)
+DEFAULT_CAP = 4 << 20
+FUSED_CAP = 1 << 20     # the row-parallel GEMVs' fused all-reduce (EPI_AR): 16 granules x 1024 blocks per slot
 TWOSHOT_CAP = 64 << 20  # bytes per parity of the two-shot buffer (larger messages run in pieces)
 MODE_AR, MODE_RS, MODE_AG = 0, 1, 2
 
@@ -118,7 +123,8 @@ class CustomAllReduce:
         """One real collective through the mapped peers before anything depends on it: a wrong
         sum or a spin that gave up (peer writes not visible over the link) disables the path."""
         try:
-            n = max(8, min(8192, self.cap // 2) // 8 * 8)  # <= 16 KiB: the decode hidden state of an 8B model
+            one = kernels().car_oneshot_max(self.cap) // 2 if self.cap <= DEFAULT_CAP else self.cap // 2
+            n = max(8, min(8192, one) // 8 * 8)  # <= 16 KiB: the decode hidden state of an 8B model
             x = torch.full((n,), float(self.rank + 1), dtype=torch.bfloat16, device=self.device)
             if self.cap > DEFAULT_CAP:
                 self.all_reduce_large_(x)
@@ -132,7 +138,19 @@ class CustomAllReduce:
             return False
 
     def fits(self, nbytes: int) -> bool:
-        return nbytes % 16 == 0 and nbytes <= self.cap
+        """Does a one-shot all-reduce / all-gather of ``nbytes`` per rank fit this buffer?"""
+        return nbytes % 16 == 0 and nbytes <= kernels().car_oneshot_max(self.cap)
+
+    # -- fused into the row-parallel GEMV (decode o_proj / down_proj) -----------------------------
+    def gemv_allreduce(self, x: torch.Tensor, W: torch.Tensor, h: torch.Tensor) -> torch.Tensor:
+        """h = sum over ranks of W_r . x_r, rank 0's term + h (the residual): one GEMV launch with
+        the one-shot exchange in its epilogue (gemv_core.h EPI_AR). x [M <= 2, K], W [N, K], h [M, N]
+        bf16; same bits as ``linear(EPI_RESADD / EPI_BF16)`` + ``all_reduce_``."""
+        M, K = x.shape
+        N = W.shape[0]
+        kernels().gemv_ar(M, x.data_ptr(), x.stride(0), W.data_ptr(), h.data_ptr(), h.stride(0), N, K, self.bases,
+                          self.rank, self.world, self.cap, self._stream(h))
+        return h
 
     @staticmethod
     def _stream(t: torch.Tensor) -> int:
@@ -212,7 +230,7 @@ class CustomAllReduce:
             torch.cuda.synchronize(self.device)
         dist.barrier(group=self.group)
         with _on(self.device):
-            kernels().car_reset(self.own)
+            kernels().car_reset(self.own, self.cap)
         dist.barrier(group=self.group)
 
     def close(self) -> None:

@@ -236,3 +236,100 @@ def test_tp_cancel_mid_decode_keeps_protocol_in_step(cuda):
         assert err == "context canceled", (rank, err)
         assert same, f"rank {rank}: the request after the cancel differs from the clean run"
         assert not tmo, f"rank {rank}: a spin timed out"
+
+
+def _fused_worker(rank, world, port, q):
+    """Row-parallel GEMV with the all-reduce in its epilogue (EPI_AR) against the two-launch path
+    (EPI_RESADD on rank 0 / EPI_BF16 elsewhere, then the one-shot all-reduce): bit-identical, for
+    one and two tokens, short (4-wave) and long (16-wave, 512-block) outputs, eagerly and replayed
+    from a HIP graph with fresh inputs (epochs and data parities advance across launches)."""
+    try:
+        import torch.distributed as dist
+
+        from llm_consensus_amd import ops
+        from llm_consensus_amd.ops import EPI_BF16, EPI_RESADD
+        from llm_consensus_amd.parallel.comm import TPGroup
+
+        torch.cuda.set_device(0)
+        dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world)
+        tp = TPGroup(dist.group.WORLD, rank, world)
+        assert tp.enable_custom("cuda:0") and tp.custom_fused is not None
+        car = tp.custom_fused
+        bad = []
+
+        def case(M, N, K, salt):
+            g = torch.Generator().manual_seed(77 * rank + salt)
+            x = torch.randn(M, K, generator=g).to(torch.bfloat16).cuda()
+            W = (torch.randn(N, K, generator=g) / K ** 0.5).to(torch.bfloat16).cuda()
+            h0 = torch.randn(M, N, generator=torch.Generator().manual_seed(salt)).to(torch.bfloat16).cuda()
+            return x, W, h0
+
+        for M, N, K in ((1, 4096, 512), (1, 4096, 1792), (2, 4096, 512), (1, 1024, 256), (2, 1536, 384),
+                        (1, 8192, 2048)):
+            for rep in range(3):
+                x, W, h0 = case(M, N, K, 1000 * rep + N + K + M)
+                hf = h0.clone()
+                car.gemv_allreduce(x, W, hf)
+                hr = h0.clone()
+                ops.linear(x, W, EPI_RESADD if rank == 0 else EPI_BF16, out=hr)
+                tp.all_reduce_(hr)
+                torch.cuda.synchronize()
+                if not torch.equal(hf, hr):
+                    bad.append((M, N, K, rep, float((hf.float() - hr.float()).abs().max())))
+        # graph: o-like then down-like fused launches per replay, inputs refreshed in place
+        x1, W1, h = case(1, 4096, 512, 5)
+        x2, W2, _ = case(1, 4096, 1792, 6)
+        s = torch.cuda.Stream()
+        with torch.cuda.stream(s):
+            car.gemv_allreduce(x1, W1, h)
+        torch.cuda.synchronize()
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g, stream=s):
+            car.gemv_allreduce(x1, W1, h)
+            car.gemv_allreduce(x2, W2, h)
+        for rep in range(4):
+            xa, _, h0 = case(1, 4096, 512, 50 + rep)
+            xb, _, _ = case(1, 4096, 1792, 90 + rep)
+            x1.copy_(xa)
+            x2.copy_(xb)
+            h.copy_(h0)
+            torch.cuda.synchronize()
+            dist.barrier()
+            g.replay()
+            torch.cuda.synchronize()
+            hr = h0.clone()
+            ops.linear(x1, W1, EPI_RESADD if rank == 0 else EPI_BF16, out=hr)
+            tp.all_reduce_(hr)
+            ops.linear(x2, W2, EPI_RESADD if rank == 0 else EPI_BF16, out=hr)
+            tp.all_reduce_(hr)
+            torch.cuda.synchronize()
+            if not torch.equal(h, hr):
+                bad.append(("graph", rep, float((h.float() - hr.float()).abs().max())))
+        q.put((rank, bad, tp.custom_timed_out()))
+        dist.barrier()
+        dist.destroy_process_group()
+    except Exception as e:  # noqa: BLE001
+        import traceback
+
+        q.put((rank, repr(e) + traceback.format_exc(), True))
+
+
+@pytest.mark.parametrize("world", [2, 4])
+def test_fused_rowparallel_gemv_allreduce(cuda, world):
+    import socket
+
+    with socket.socket() as sk:
+        sk.bind(("127.0.0.1", 0))
+        port = sk.getsockname()[1]
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_fused_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=300) for _ in range(world)]
+    for p in procs:
+        p.join(timeout=60)
+    for rank, bad, tmo in res:
+        assert not isinstance(bad, str), bad
+        assert not tmo, f"rank {rank}: a spin timed out"
+        assert bad == [], (rank, bad)

@@ -230,3 +230,21 @@ def test_attn_oproj_cpu_path_is_attention_then_residual_o_proj():
 def test_cpu_engines_never_take_the_fused_attention_oproj():
     eng = Engine(FAMILIES["llama-tiny"], EngineConfig(device="cpu", max_context=256, attn_oproj=True))
     assert eng.ao_nc == 0 and not any(eng.ao_chunks)
+
+
+def test_debug_decode_layers_matches_per_layer_oracle_cpu():
+    """The per-layer decode hook (the full-depth GPU test's instrument) on the CPU path: every
+    layer's output equals the one-layer fp32 oracle fed the engine's own input and KV cache to
+    within bf16 rounding of the residual stream."""
+    from llm_consensus_amd.ops import oracle
+
+    cfg = FAMILIES["llama-tiny"]
+    eng = Engine(cfg, EngineConfig(device="cpu", max_context=256, seed=5))
+    prompt = [(i * 7919) % (cfg.vocab - 300) + 256 for i in range(100)]
+    hs, pos = eng.debug_decode_layers(prompt)
+    assert pos == len(prompt) and hs.shape == (cfg.n_layers + 1, cfg.hidden)
+    for li, L in enumerate(eng.w.layers):
+        ref = oracle.reference_decode_layer(L, cfg, hs[li:li + 1], eng.k_cache[li], eng.v_cache[li], eng.block_tables[0],
+                                            pos, eng.cos_t, eng.sin_t, eng.nh, eng.nkv, eng.bs).float()
+        err = (hs[li + 1].float() - ref).abs().max().item()
+        assert err <= 0.01 * ref.abs().max().item(), (li, err)

@@ -155,6 +155,9 @@ class _FakeCarKernels:
     def car_timed_out(self, own):
         return 1 if self.rank == self.timeout_rank else 0
 
+    def car_oneshot_max(self, cap):  # as allreduce.hip's car_oneshot_max
+        return min(cap // 8 // 8 // 1024, 64) * 256 * 16
+
     def car_allreduce(self, bases, rank, world, cap, ptr, nbytes, stream):
         import ctypes
 

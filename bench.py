@@ -322,6 +322,131 @@ def topology(world: int, rank: int, dev: str, on_cpu: bool, tp_members, cdev) ->
     }
 
 
+def cli_path_bench(args) -> None:
+    """The same consensus round through the shipping path (reference ``cmd/llm-consensus/main.go``
+    132-170 + ``runner.go`` + ``judge.go``): ``ConsensusService`` places the engines once (worker
+    processes, weights, graph capture: reported as ``startup_s``, outside the timed rounds), then
+    every round is Runner fan-out -> LocalProvider -> worker pipe -> streamed detokenisation, the
+    incrementally prefilled judge session, and the result persisted as ``data/<run-id>/``
+    (result.json, prompt.txt, consensus.md) — with per-phase times."""
+    import tempfile
+
+    if "WORLD_SIZE" in os.environ and int(os.environ["WORLD_SIZE"]) > 1:
+        raise SystemExit("--path cli starts its own worker processes: run it without a launcher")
+    if args.config != "fanout":
+        raise SystemExit("--path cli: fanout preset only")
+    from llm_consensus_amd.context import Context
+    from llm_consensus_amd.output import encode_result
+    from llm_consensus_amd.server import ConsensusService
+    from llm_consensus_amd.utils.tokenizer import get_tokenizer
+    from llm_consensus_amd.models.config import FAMILIES
+
+    n = args.gpus
+    fam = TINY.get(args.model, args.model) if args.shapes == "tiny" else args.model
+    jfam = TINY.get(args.judge, args.judge) if args.shapes == "tiny" else args.judge
+    n_resp = args.n_models or max(3, n)
+    models = [f"{fam}@{i}" for i in range(n_resp)]
+    judge = f"{jfam}@judge"
+    jtp = judge_tp_degree(FAMILIES[jfam], n, args.judge_tp) if n > 1 else 0
+    ptok = get_tokenizer(FAMILIES[fam].vocab)
+    import random
+
+    rng = random.Random(1234)
+    prompt = ptok.decode([rng.randrange(256, min(256 + 60000, ptok.vocab_size - 2))
+                          for _ in range(args.prompt_tokens)]).strip()
+    t0 = time.perf_counter()
+    svc = ConsensusService(models, judge, gpus=",".join(str(g) for g in range(n)), judge_tp=jtp if jtp > 1 else 0,
+                           concurrency=1, timeout=3600.0, max_tokens=args.max_tokens, temperature=args.temperature)
+    startup = time.perf_counter() - t0
+    log(f"product path ready in {startup:.1f}s: {models} + {judge}")
+    tmp = tempfile.mkdtemp(prefix="llmc-bench-cli-")
+
+    def one_round(step: int, max_tokens: int):
+        ev = []
+        req = svc.parse({"prompt": prompt, "models": models, "judge": judge, "max_tokens": max_tokens,
+                         "temperature": args.temperature, "seed": 1000 * step + 1})
+        req["stop_on_eos"] = False  # full-length responses, as the engine-path bench decodes
+        ts = time.perf_counter()
+        res = svc.run(Context.background(), req, lambda name, data: ev.append((time.perf_counter() - ts, name, data)))
+        t_run = time.perf_counter() - ts
+        # persistence exactly as the CLI's auto-save (main.go:186-236)
+        run_dir = os.path.join(tmp, f"run{step}")
+        os.makedirs(run_dir, exist_ok=True)
+        with open(os.path.join(run_dir, "prompt.txt"), "w") as f:
+            f.write(prompt)
+        with open(os.path.join(run_dir, "consensus.md"), "w") as f:
+            f.write(res.consensus)
+        with open(os.path.join(run_dir, "result.json"), "w") as f:
+            f.write(encode_result(res))
+        t_end = time.perf_counter() - ts
+        done = [t for t, name, _ in ev if name == "model_done"]
+        jstart = next((t for t, name, _ in ev if name == "judge_start"), t_run)
+        jfirst = next((t for t, name, _ in ev if name == "judge_chunk"), t_run)
+        jdone = next((d for _, name, d in ev if name == "judge_done"), {})
+        resp_tokens = sum(r.output_tokens for r in res.responses)
+        return {
+            "e2e_s": t_end,
+            "responders_s": max(done) if done else 0.0,
+            "judge_start_s": jstart,
+            "judge_ttft_s": jfirst - jstart,
+            "judge_decode_s": t_run - jfirst,
+            "persist_s": t_end - t_run,
+            "tokens": resp_tokens + int(jdone.get("output_tokens", 0)),
+            "response_tokens": [r.output_tokens for r in res.responses],
+            "judge_tokens": int(jdone.get("output_tokens", 0)),
+            "judge_prompt_tokens": int(jdone.get("prompt_tokens", 0)),
+            "per_model_latency_ms": {r.model: r.latency_ms for r in res.responses},
+            "per_model_ttft_ms": {r.model: round(r.ttft_ns / 1e6, 1) for r in res.responses},
+        }
+
+    try:
+        for w in range(args.warmup):
+            st = one_round(w, min(args.max_tokens, args.warmup_tokens or args.max_tokens))
+            log(f"warmup {w}: {st}")
+        per_step = []
+        t0 = time.perf_counter()
+        for s_ in range(args.steps):
+            st = one_round(100 + s_, args.max_tokens)
+            per_step.append(st)
+            log(f"step {s_}: {st}")
+        elapsed = time.perf_counter() - t0
+    finally:
+        svc.close()
+    lat = [p["e2e_s"] for p in per_step]
+    tot = sum(p["tokens"] for p in per_step)
+    med = lambda k: round(statistics.median(p[k] for p in per_step), 3)  # noqa: E731
+    out = {
+        "metric": METRIC, "value": round(tot / elapsed, 2), "unit": "tokens/s", "n_gpus": n, "steps": args.steps,
+        "warmup": args.warmup, "ms_per_step": round(1000 * elapsed / args.steps, 2), "higher_is_better": True,
+        "scaling": "weak", "vs_baseline": None, "dtype": "bf16",
+        "data": "synthetic prompt (synthetic tokenizer), random-init weights",
+        "config": {"name": "product path (Runner -> LocalProvider -> worker -> pipe -> detokenizer -> result.json): "
+                           + f"{n_resp} x {fam} + {jfam} judge on {n} GPU(s)",
+                   "model": f"{n_resp}x {fam} responders + {jfam} judge" + (f" TP={jtp}" if jtp > 1 else ""),
+                   "global_batch": n_resp, "seq_len": args.prompt_tokens + args.max_tokens,
+                   "max_tokens": args.max_tokens, "prompt_tokens": args.prompt_tokens, "path": "cli",
+                   "parallelism": f"fanout{n_resp}" + (f"-judge_tp{jtp}" if jtp > 1 else "")},
+        "extra": {
+            "startup_s": round(startup, 1),
+            "p50_e2e_latency_s": round(statistics.median(lat), 3),
+            "responders_s": med("responders_s"), "judge_start_s": med("judge_start_s"),
+            "judge_ttft_s": med("judge_ttft_s"), "judge_decode_s": med("judge_decode_s"),
+            "persist_s": med("persist_s"),
+            "judge_prompt_tokens": per_step[-1]["judge_prompt_tokens"] if per_step else 0,
+            "tokens_per_round": [p["tokens"] for p in per_step],
+        },
+    }
+    print(json.dumps(out), flush=True)
+    if args.results_dir:
+        try:
+            os.makedirs(args.results_dir, exist_ok=True)
+            fn = os.path.join(args.results_dir, f"bench_cli_{time.strftime('%Y%m%dT%H%M%SZ', time.gmtime())}_n{n}.json")
+            with open(fn, "w") as f:
+                json.dump(dict(out, per_step=per_step, argv=sys.argv[1:]), f, indent=2)
+        except OSError as e:
+            log(f"could not write results record: {e}")
+
+
 def main() -> None:
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=0,
@@ -351,12 +476,19 @@ def main() -> None:
                     help="seconds the whole command may take (0 = off): the last two warmup rounds (W >= 2) are "
                          "timed at two lengths, and if K full rounds would overrun, the timed rounds decode fewer "
                          "tokens (recorded as config.max_tokens, with max_tokens_requested)")
+    ap.add_argument("--path", default="engine", choices=["engine", "cli"],
+                    help="engine: the engines driven directly on threads (the headline); cli: the product path "
+                         "(Runner -> LocalProvider -> worker process -> pipe -> detokenizer -> result.json) through "
+                         "ConsensusService with the same round, per-phase times in extra (fanout preset only)")
     ap.add_argument("--results-dir", default=os.path.join(ROOT, "bench", "results"),
                     help="rank 0 also writes the full record (per-step stats, p50/p90) here ('' = off)")
     args = ap.parse_args()
 
     if not args.gpus:
         args.gpus = int(os.environ.get("WORLD_SIZE", "1"))
+    if args.path == "cli":
+        # the driver process of the product path never touches a GPU: its worker processes do
+        return cli_path_bench(args)
     if "WORLD_SIZE" not in os.environ and args.gpus > 1:
         # no launcher: start the N ranks here, before this process touches the GPU (it never
         # imports torch), and exit with their status

@@ -31,6 +31,7 @@ class Request:
     top_p: Optional[float] = None
     top_k: Optional[int] = None
     seed: Optional[int] = None
+    stop_on_eos: Optional[bool] = None  # None = stop at the model's EOS (benchmarks pin full lengths)
 
 
 @dataclasses.dataclass

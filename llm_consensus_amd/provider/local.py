@@ -327,7 +327,7 @@ class LocalProvider:
         seed = req.seed if req.seed is not None else (zlib.crc32(self.model.encode()) & 0x7FFFFFFF)
         return {"max_tokens": int(mt), "temperature": 1.0 if req.temperature is None else float(req.temperature),
                 "top_p": 1.0 if req.top_p is None else float(req.top_p), "top_k": int(req.top_k or 0),
-                "seed": int(seed), "stop_on_eos": True}
+                "seed": int(seed), "stop_on_eos": True if req.stop_on_eos is None else bool(req.stop_on_eos)}
 
     def _stream(self, ctx: Context, rid: int, q: "queue.Queue", callback: Optional[StreamCallback], t0: int,
                 prompt_tokens: int) -> Response:

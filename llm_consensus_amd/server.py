@@ -56,20 +56,27 @@ class ServiceError(Exception):
 
 class _SessionJudge:
     """Provider facade binding one request's judge session (``consensus.Judge`` looks for
-    ``close_session`` / ``query_stream_session`` on its provider)."""
+    ``close_session`` / ``query_stream_session`` on its provider); keeps the judge's Response
+    (token counts, latency) for the caller."""
 
     def __init__(self, provider, session):
         self.provider = provider
         self.session = session
+        self.response: Optional[Response] = None
 
     def close_session(self) -> None:
-        self.session.close()
+        if self.session is not None:
+            self.session.close()
 
     def query_stream_session(self, ctx, req, callback):
-        return self.session.finish(ctx, req, callback)
+        if self.session is None:
+            return self.query_stream(ctx, req, callback)
+        self.response = self.session.finish(ctx, req, callback)
+        return self.response
 
     def query_stream(self, ctx, req, callback):
-        return self.provider.query_stream(ctx, req, callback)
+        self.response = self.provider.query_stream(ctx, req, callback)
+        return self.response
 
 
 class ConsensusService:
@@ -164,7 +171,8 @@ class ConsensusService:
     def _run(self, ctx: Context, req: dict, ev: EventFn) -> Result:
         prompt, models, judge_name = req["prompt"], req["models"], req["judge"]
         tmpl = Request(model="", prompt="", max_tokens=req["max_tokens"] or None, temperature=req["temperature"],
-                       top_p=req["top_p"], top_k=req["top_k"] or None, seed=req["seed"] or None)
+                       top_p=req["top_p"], top_k=req["top_k"] or None, seed=req["seed"] or None,
+                       stop_on_eos=req.get("stop_on_eos"))
         jp = self.registry.get(judge_name)
         session = None
         if hasattr(jp, "new_session") and len(models) > 1 and judge_name == self.judge:
@@ -190,12 +198,16 @@ class ConsensusService:
                 session.close()
             raise ServiceError(f"running queries: {e}") from None
         ev("judge_start", {"judge": judge_name, "responses": len(result.responses)})
-        judge = Judge(_SessionJudge(jp, session) if session is not None else jp, judge_name, tmpl)
+        jw = _SessionJudge(jp, session) if session is not None or hasattr(jp, "new_session") else None
+        judge = Judge(jw if jw is not None else jp, judge_name, tmpl)
         try:
             consensus = judge.synthesize_stream(ctx.with_timeout(req["timeout"]), prompt, result.responses,
                                                 lambda c: ev("judge_chunk", {"text": c}))
         except Exception as e:  # noqa: BLE001
             raise ServiceError(f"consensus synthesis: {e}") from None
+        if jw is not None and jw.response is not None:
+            ev("judge_done", {"output_tokens": jw.response.output_tokens, "prompt_tokens": jw.response.prompt_tokens,
+                              "latency_ms": jw.response.latency_ms})
         return Result(prompt=prompt, responses=result.responses, consensus=consensus, judge=judge_name,
                       warnings=result.warnings, failed_models=result.failed_models)
 

@@ -194,3 +194,19 @@ def test_config_names_are_honest():
     assert name.startswith("variant of BASELINE config 2") and "4 responders" in name
     name, _, j = plan(1)
     assert name.startswith("BASELINE config 2 on one GPU") and j["ranks"] == [0]
+
+
+def test_product_path_round_reports_phases():
+    """--path cli: the same round through ConsensusService (Runner -> LocalProvider -> worker
+    process -> pipe -> detokenizer -> persisted result), full-length responses, per-phase times."""
+    env = dict(os.environ, LLMC_DEVICE="cpu", OMP_NUM_THREADS="1")
+    r = subprocess.run([sys.executable, "bench.py", "--path", "cli", "--shapes", "tiny", "--steps", "1", "--warmup", "1",
+                        "--max-tokens", "12", "--warmup-tokens", "4", "--results-dir", ""],
+                       cwd=ROOT, capture_output=True, timeout=600, env=env)
+    assert r.returncode == 0, r.stderr.decode()[-3000:]
+    d = json.loads([ln for ln in r.stdout.decode().splitlines() if ln.startswith("{")][0])
+    assert d["config"]["path"] == "cli" and d["config"]["global_batch"] == 3
+    x = d["extra"]
+    assert x["tokens_per_round"] == [4 * 12]  # 3 full responses + the judge, EOS ignored as in the engine bench
+    assert 0 < x["responders_s"] <= x["judge_start_s"] < d["ms_per_step"] / 1000
+    assert x["judge_prompt_tokens"] > 0 and x["judge_decode_s"] > 0 and x["persist_s"] >= 0

@@ -72,7 +72,11 @@ class TPGroup:
             self.custom2 = CustomAllReduce(self.group, self.rank, self.size, device, cap2 or TWOSHOT_CAP)
             # the same decision on every rank (environment of the whole job; A/B: LLMC_FUSED_AR=0)
             if os.environ.get("LLMC_FUSED_AR", "1") != "0":
-                self.custom_fused = CustomAllReduce(self.group, self.rank, self.size, device, FUSED_CAP)
+                # no one-shot self-test on this buffer: its granule layout is the fused GEMV's
+                # (16 per block), and a one-shot kernel's granules (1024 per block) left in it would
+                # carry tags that block's epochs reach again; the peers were just verified above
+                self.custom_fused = CustomAllReduce(self.group, self.rank, self.size, device, FUSED_CAP,
+                                                    selftest=False)
         except CustomAllReduceUnavailable as e:
             warnings.warn(f"custom all-reduce disabled, using RCCL: {e}")
             for c in (self.custom, self.custom2, self.custom_fused):

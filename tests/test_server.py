@@ -226,9 +226,10 @@ def test_server_tp_judge_concurrent_cpu(monkeypatch):
 def test_server_local_engines_concurrent_gpu(cuda):
     """The same on the MI355X: continuous-batched responder rows (retiring at different replays)
     and judge sessions through the HIP kernels and decode graphs. Token-exactness against a lone
-    request is not asserted here: a batched prefill of >= 64 tokens takes the hipBLASLt GEMM path
-    instead of the MFMA kernel, and with random weights greedy decoding flips on near-ties; the
-    batcher's exactness is tests/test_batcher.py (rows prefilled alone)."""
+    request is not asserted here: requests prefilled together share one chunk, whose 256 x 256
+    MFMA GEMM tiles sum in a different order than a lone prompt's (and with random weights greedy
+    decoding flips on near-ties); the batcher's exactness is tests/test_batcher.py (rows prefilled
+    alone)."""
     svc = ConsensusService(["llama-small@1", "llama-small@2"], "llama-small@j", concurrency=3, max_tokens=40,
                            temperature=0.0)
     try:

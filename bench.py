@@ -825,7 +825,8 @@ def main() -> None:
         judge_stats = dict(judge_stats, judge_prompt_tokens=int(jt[0].item()), judge_prefill_s=float(jt[1].item()),
                            judge_decode_s=float(jt[2].item()), judge_ttft_s=float(jt[3].item()))
     # every TP engine's custom-collective state at the end, from every rank that holds a shard
-    ar_state = {e.name: {"custom": e.tp.custom is not None, "timed_out": bool(e.tp.custom_timed_out())}
+    ar_state = {e.name: {"custom": e.tp.custom is not None, "fused": e.tp.custom_fused is not None,
+                         "timed_out": bool(e.tp.custom_timed_out())}
                 for e in [e for _, e, _, _ in responders] + ([judge] if judge is not None else []) if e.tp.size > 1}
     if world > 1:
         allst = [None] * world
@@ -833,8 +834,9 @@ def main() -> None:
         ar_state = {}
         for d in allst:
             for k, v in d.items():
-                cur = ar_state.setdefault(k, {"custom": True, "timed_out": False})
+                cur = ar_state.setdefault(k, {"custom": True, "fused": True, "timed_out": False})
                 cur["custom"] = cur["custom"] and v["custom"]
+                cur["fused"] = cur["fused"] and v["fused"]
                 cur["timed_out"] = cur["timed_out"] or v["timed_out"]
     if rank == 0:
         names = [e["name"] for e in resp_plan]
@@ -898,6 +900,8 @@ def main() -> None:
                 "time_budget_s": args.time_budget,
                 "custom_allreduce": {k: v["custom"] for k, v in ar_state.items()},
                 "custom_allreduce_timed_out": {k: v["timed_out"] for k, v in ar_state.items()},
+                # the row-parallel decode GEMVs' all-reduce fused into their epilogue (EPI_AR)
+                "fused_rowparallel_allreduce": {k: v["fused"] for k, v in ar_state.items()},
                 **topo,
             },
         }

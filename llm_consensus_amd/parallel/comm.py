@@ -77,6 +77,10 @@ class TPGroup:
                 # carry tags that block's epochs reach again; the peers were just verified above
                 self.custom_fused = CustomAllReduce(self.group, self.rank, self.size, device, FUSED_CAP,
                                                     selftest=False)
+                if not self.custom.agree(self._fused_selftest(device)):
+                    warnings.warn("fused row-parallel all-reduce failed its self-test: separate all-reduce launches")
+                    self.custom_fused.close()
+                    self.custom_fused = None
         except CustomAllReduceUnavailable as e:
             warnings.warn(f"custom all-reduce disabled, using RCCL: {e}")
             for c in (self.custom, self.custom2, self.custom_fused):
@@ -85,6 +89,32 @@ class TPGroup:
             self.custom = self.custom2 = self.custom_fused = None
             return False
         return True
+
+    def _fused_selftest(self, device) -> bool:
+        """The fused row-parallel GEMV all-reduce (EPI_AR) against the same GEMV + the one-shot
+        all-reduce just verified, bit for bit, over three launches (epochs and both data parities);
+        any error or spin timeout is a failure. Collective (every rank runs it)."""
+        try:
+            from .. import ops
+
+            dev = torch.device(device)
+            g = torch.Generator().manual_seed(4242 + self.rank)
+            ok = True
+            for rep in range(3):
+                x = torch.randn(1, 512, generator=g).to(torch.bfloat16).to(dev)
+                W = (torch.randn(1024, 512, generator=g) / 16).to(torch.bfloat16).to(dev)
+                h0 = torch.randn(1, 1024, generator=torch.Generator().manual_seed(rep)).to(torch.bfloat16).to(dev)
+                hf = h0.clone()
+                self.custom_fused.gemv_allreduce(x, W, hf)
+                hr = h0.clone()
+                ops.linear(x, W, ops.EPI_RESADD if self.rank == 0 else ops.EPI_BF16, out=hr)
+                self.custom.all_reduce_(hr)
+                if dev.type == "cuda":
+                    torch.cuda.synchronize(dev)
+                ok = ok and bool(torch.equal(hf, hr))
+            return ok and not self.custom_fused.timed_out() and not self.custom.timed_out()
+        except Exception:  # noqa: BLE001
+            return False
 
     def collectives(self):
         return [c for c in (self.custom, self.custom2, self.custom_fused) if c is not None]

@@ -110,6 +110,10 @@ class CustomAllReduce:
             raise CustomAllReduceUnavailable(f"rank {rank}: {err!r}" if err else f"rank {rank}: a peer failed")
         dist.barrier(group=group)
 
+    def agree(self, ok: bool) -> bool:
+        """MIN over the group of a local success flag (collective)."""
+        return self._agree(ok)
+
     def _agree(self, ok: bool) -> bool:
         """MIN over the group of a local success flag (nccl wants a device tensor, gloo a host one)."""
         import torch.distributed as dist

@@ -1,0 +1,12 @@
+# Round 4: per-layer numerics at the judge context, the product path vs the engine path at the bench
+# configuration (2 timed rounds each), and a rocprofv3 table of the TP=8-shaped decode rehearsed over
+# 2 CU-partitioned ranks (the fused all-reduce epilogue: no standalone all-reduce launches).
+# usage: gpurun --timeout 1100 -- bash scripts/gpu/r4_paths.sh <tag>
+set -o pipefail
+cd $GRAFT_REPO_ROOT
+tag=${1:-r4p}
+mkdir -p gpurun_out
+timeout -k 10 300 python -u -m pytest tests/test_numerics_full_gpu.py -k per_layer -x -q -s --timeout 280 --timeout-method thread > gpurun_out/${tag}_perlayer.log 2>&1 && \
+timeout -k 10 300 python -u bench.py --path cli --steps 2 --warmup 1 > gpurun_out/${tag}_cli.log 2>&1 && \
+timeout -k 10 240 python -u bench.py --steps 2 --warmup 1 > gpurun_out/${tag}_engine.log 2>&1 && \
+bash scripts/prof_tp_rehearsal.sh ${tag}_reh_prof --shape-tp 8 --world 2 --tokens 128 --reps 1

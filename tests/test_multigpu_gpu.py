@@ -176,7 +176,8 @@ def _tp_worker(rank, world, port, q):
         e.free_sequence(s)
         gen = e.generate_ids(PROMPT, 32, temperature=0.0, stop_on_eos=False)
         torch.cuda.synchronize()
-        q.put((rank, enabled, logits.tolist() if rank == 0 else None, gen, tp.custom_timed_out()))
+        q.put((rank, enabled and tp.custom_fused is not None, logits.tolist() if rank == 0 else None, gen,
+               tp.custom_timed_out()))
         dist.barrier()
         dist.destroy_process_group()
     except Exception as ex:  # noqa: BLE001
@@ -202,7 +203,7 @@ def test_tp_decode_across_devices_matches_tp1(world):
     gens = {}
     for rank, enabled, logits, gen, tmo in res:
         assert not isinstance(logits, str), logits
-        assert enabled, f"rank {rank}: custom collectives fell back to RCCL"
+        assert enabled, f"rank {rank}: custom collectives (or the fused row-parallel all-reduce) fell back"
         assert not tmo, f"rank {rank}: a custom-collective spin timed out"
         gens[rank] = gen
         if rank == 0:
@@ -230,4 +231,5 @@ def test_bench_self_launch_across_devices(world):
     assert len(x["peer_access"]) >= world and all(x["peer_access"][i][j] for i in range(world) for j in range(world))
     judge = [k for k in x["custom_allreduce"] if k.endswith("@judge")]
     assert judge and x["custom_allreduce"][judge[0]] and not any(x["custom_allreduce_timed_out"].values())
+    assert x["fused_rowparallel_allreduce"][judge[0]]
     assert x["allreduce_16k"][judge[0]]["impl"] == "custom_oneshot" and x["allreduce_16k"][judge[0]]["us"] > 0

@@ -501,6 +501,24 @@ extern "C" int llmc_gemm(const void* A, int lda, const void* W, int ldw, void* C
   return static_cast<int>(hipGetLastError());
 }
 
+// The 128 x 128 two-buffer kernel on a dense problem (microbenchmarks and the narrow-N dispatch
+// of llmc_gemm): same operands / epilogues as llmc_gemm.
+extern "C" int llmc_gemm_t128(const void* A, int lda, const void* W, int ldw, void* C, int ldc, int M, int N, int K,
+                              int epi, hipStream_t s) {
+  if (K % kBK != 0 || M <= 0 || N <= 0 || (epi == 3 && N % 2 != 0) || lda % 8 != 0 || ldw % 8 != 0) return -1;
+  const int nwg = ((M + kBM - 1) / kBM) * ((N + kBN - 1) / kBN);
+  const bf16_t* a = (const bf16_t*)A;
+  const bf16_t* w = (const bf16_t*)W;
+  switch (epi) {
+    case 0: gemm_kernel<0, false><<<nwg, 256, 0, s>>>(a, lda, w, ldw, C, ldc, M, N, K); break;
+    case 1: gemm_kernel<1, false><<<nwg, 256, 0, s>>>(a, lda, w, ldw, C, ldc, M, N, K); break;
+    case 2: gemm_kernel<2, false><<<nwg, 256, 0, s>>>(a, lda, w, ldw, C, ldc, M, N, K); break;
+    case 3: gemm_kernel<3, false><<<nwg, 256, 0, s>>>(a, lda, w, ldw, C, ldc, M, N, K); break;
+    default: return -2;
+  }
+  return static_cast<int>(hipGetLastError());
+}
+
 // Grouped expert GEMM over moe_align's padded row list (max_tiles * tile rows of capacity; tile =
 // 256: the 256 x 256 LDS-DMA pipeline, 128: the two-buffer 128 x 128 kernel for small groups).
 // A: a_rows rows (gathered by sorted_rows / a_row_div); epi 0 bf16, 1 f32, 3 SiLU-mul of

@@ -118,6 +118,19 @@ def gemm(x: torch.Tensor, W: torch.Tensor, epi: int = EPI_BF16, out: Optional[to
     return out
 
 
+def gemm128(x: torch.Tensor, W: torch.Tensor, epi: int = EPI_BF16, out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """Always the 128 x 128 two-buffer MFMA kernel (tests / microbenchmarks of the narrow-N choice)."""
+    if not x.is_cuda:
+        return oracle.linear(x, W, epi, out)
+    M, K = x.shape
+    N = W.shape[0]
+    if out is None:
+        n_out = N // 2 if epi == EPI_SILU else N
+        out = torch.empty(M, n_out, dtype=torch.float32 if epi == EPI_F32 else torch.bfloat16, device=x.device)
+    kernels().gemm_t128(_p(x), x.stride(0), _p(W), W.stride(0), _p(out), out.stride(0), M, N, K, epi, _s(x))
+    return out
+
+
 def gemv(x: torch.Tensor, W: torch.Tensor, epi: int = EPI_BF16, out: Optional[torch.Tensor] = None,
          norm_w: Optional[torch.Tensor] = None, eps: float = 1e-5, mfma: bool = False) -> torch.Tensor:
     """Always the weight-streaming path (M <= 32; the kernel library picks VALU / MFMA form)."""

@@ -11,4 +11,5 @@ timeout -k 10 120 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_ou
 timeout -k 10 150 python -u scripts/car_latency.py --world 2,4 > gpurun_out/${tag}_carlat.log 2>&1 && \
 timeout -k 10 200 python -u scripts/tp_rehearsal.py --shape-tp 8 --world 2 --fused-ar 0 > gpurun_out/${tag}_reh.log 2>&1 && \
 timeout -k 10 200 python -u scripts/tp_rehearsal.py --shape-tp 8 --world 2 --fused-ar 1 >> gpurun_out/${tag}_reh.log 2>&1 && \
-timeout -k 10 200 python -u scripts/tp_shard_decode.py --tp 8 --ctx 2048 --tokens 256 > gpurun_out/${tag}_shard.log 2>&1
+timeout -k 10 200 python -u scripts/tp_shard_decode.py --tp 8 --ctx 2048 --tokens 256 > gpurun_out/${tag}_shard.log 2>&1 && \
+timeout -k 10 240 python -u scripts/microbench_kernels.py prefill > gpurun_out/${tag}_prefill_gemm.log 2>&1

@@ -70,8 +70,14 @@ class TPGroup:
         try:
             self.custom = CustomAllReduce(self.group, self.rank, self.size, device, cap or DEFAULT_CAP)
             self.custom2 = CustomAllReduce(self.group, self.rank, self.size, device, cap2 or TWOSHOT_CAP)
-            # the same decision on every rank (environment of the whole job; A/B: LLMC_FUSED_AR=0)
-            if os.environ.get("LLMC_FUSED_AR", "1") != "0":
+            # the same decision on every rank (environment of the whole job; A/B: LLMC_FUSED_AR=0).
+            # Ranks sharing one GPU keep separate launches unless forced (LLMC_FUSED_AR=force: the
+            # CU-partitioned rehearsals): a fused GEMV block spins on its peers' blocks of the SAME
+            # launch, and two ranks' full-chip grids on one device can leave a peer's blocks
+            # waiting for CUs the spinning blocks hold (on separate GPUs the lowest unfinished
+            # block is always resident)
+            fused = os.environ.get("LLMC_FUSED_AR", "1")
+            if fused == "force" or (fused != "0" and self.custom.distinct_devices):
                 # no one-shot self-test on this buffer: its granule layout is the fused GEMV's
                 # (16 per block), and a one-shot kernel's granules (1024 per block) left in it would
                 # carry tags that block's epochs reach again; the peers were just verified above

@@ -100,6 +100,9 @@ class CustomAllReduce:
                         self._opened.append(p)
             except Exception as e:  # noqa: BLE001
                 err = e
+        # every rank on a device of its own (the fused row-parallel all-reduce needs it, comm.py)
+        devs = [p[1] for p in peers if p is not None]
+        self.distinct_devices = len(devs) == world and len(set(devs)) == world and all(d >= 0 for d in devs)
         ok = self._agree(err is None)
         if ok and selftest:
             ok = self._agree(self._selftest())

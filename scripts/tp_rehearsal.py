@@ -22,7 +22,8 @@ def _worker(rank, a, port, q):
     total = 256
     per = total // a.world
     os.environ["LLMC_CU_MASK"] = f"{rank * per}-{(rank + 1) * per - 1}" if a.cu_mask else ""
-    os.environ["LLMC_FUSED_AR"] = str(a.fused_ar)
+    # ranks share the GPU: the fused all-reduce only runs when forced (each rank has its own CUs here)
+    os.environ["LLMC_FUSED_AR"] = "force" if a.fused_ar else "0"
     import torch
     import torch.distributed as dist
 

@@ -250,10 +250,14 @@ def _fused_worker(rank, world, port, q):
         from llm_consensus_amd.ops import EPI_BF16, EPI_RESADD
         from llm_consensus_amd.parallel.comm import TPGroup
 
+        import os
+
+        os.environ["LLMC_FUSED_AR"] = "force"  # ranks share the GPU (see comm.py): grids below fit together
         torch.cuda.set_device(0)
         dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world)
         tp = TPGroup(dist.group.WORLD, rank, world)
         assert tp.enable_custom("cuda:0") and tp.custom_fused is not None
+        assert not tp.custom.distinct_devices
         car = tp.custom_fused
         bad = []
 
@@ -264,8 +268,12 @@ def _fused_worker(rank, world, port, q):
             h0 = torch.randn(M, N, generator=torch.Generator().manual_seed(salt)).to(torch.bfloat16).cuda()
             return x, W, h0
 
-        for M, N, K in ((1, 4096, 512), (1, 4096, 1792), (2, 4096, 512), (1, 1024, 256), (2, 1536, 384),
-                        (1, 8192, 2048)):
+        # every rank's grid resident at once on the shared GPU (2 x 1024-thread blocks or 8 x 256 per
+        # CU): 16-wave grids of N / 16 blocks, 4-wave grids of N / 4 below N = 2048
+        shapes = [(1, 2048, 512), (1, 2048, 1792), (2, 2048, 512), (1, 1024, 256), (2, 1536, 384)]
+        if world == 2:
+            shapes += [(1, 4096, 512), (2, 4096, 1792)]
+        for M, N, K in shapes:
             for rep in range(3):
                 x, W, h0 = case(M, N, K, 1000 * rep + N + K + M)
                 hf = h0.clone()
@@ -277,8 +285,8 @@ def _fused_worker(rank, world, port, q):
                 if not torch.equal(hf, hr):
                     bad.append((M, N, K, rep, float((hf.float() - hr.float()).abs().max())))
         # graph: o-like then down-like fused launches per replay, inputs refreshed in place
-        x1, W1, h = case(1, 4096, 512, 5)
-        x2, W2, _ = case(1, 4096, 1792, 6)
+        x1, W1, h = case(1, 2048, 512, 5)
+        x2, W2, _ = case(1, 2048, 1792, 6)
         s = torch.cuda.Stream()
         with torch.cuda.stream(s):
             car.gemv_allreduce(x1, W1, h)
@@ -288,8 +296,8 @@ def _fused_worker(rank, world, port, q):
             car.gemv_allreduce(x1, W1, h)
             car.gemv_allreduce(x2, W2, h)
         for rep in range(4):
-            xa, _, h0 = case(1, 4096, 512, 50 + rep)
-            xb, _, _ = case(1, 4096, 1792, 90 + rep)
+            xa, _, h0 = case(1, 2048, 512, 50 + rep)
+            xb, _, _ = case(1, 2048, 1792, 90 + rep)
             x1.copy_(xa)
             x2.copy_(xb)
             h.copy_(h0)

@@ -34,7 +34,10 @@ def _worker(rank, world, port, name, q, ekw=None):
 
         tp = TPGroup(dist.group.WORLD, rank, world)
         tp.enable_custom("cuda:0")
-        e = Engine(FAMILIES[name], EngineConfig(device="cuda:0", max_context=512, seed=5, **(ekw or {})), tp=tp)
+        ekw = dict(ekw or {})
+        if ekw.pop("_expect_fused", False):
+            assert tp.custom_fused is not None
+        e = Engine(FAMILIES[name], EngineConfig(device="cuda:0", max_context=512, seed=5, **ekw), tp=tp)
         e.warmup_graphs()
         s = e.new_sequence()
         e.prefill([s], [PROMPT])
@@ -60,6 +63,13 @@ def _worker(rank, world, port, name, q, ekw=None):
 ])
 def test_tp2_gpu_matches_tp1(cuda, name, ekw):
     _tp2_vs_tp1(name, ekw)
+
+
+def test_tp2_gpu_fused_rowparallel_allreduce_matches_tp1(cuda, monkeypatch):
+    """The TP engine's decode with the all-reduce fused into the row-parallel GEMVs (EPI_AR, forced
+    on although the two ranks share the GPU: llama-small's grids all fit on the chip at once)."""
+    monkeypatch.setenv("LLMC_FUSED_AR", "force")
+    _tp2_vs_tp1("llama-small", {"_expect_fused": True})
 
 
 def _tp2_vs_tp1(name, ekw):

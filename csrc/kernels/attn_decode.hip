@@ -35,6 +35,7 @@
 // a per-(row, kv head) epoch in device memory the merger advances (tag = epoch + 1: never 0,
 // never reused), so a granule left by any earlier launch can never match. Spins are bounded.
 #include "attn_core.h"
+#include "car_proto.h"
 
 namespace llmc {
 
@@ -274,13 +275,18 @@ static int launch_g(bool fused, int D, dim3 grid, hipStream_t s, const void* q, 
 // (in index order), and the merge only waits on blocks that have taken their tickets. The o_proj
 // blocks count their exits; the last re-arms the counter and advances their epoch (the tag they
 // expect = that epoch + 1 = the launch count, as the heads' epochs). Bounded spins (fault word 2).
-template <int G, int D, int NR, int KC>
+// AR (a tensor-parallel rank): the o_proj rows are this rank's row-parallel partial; the block's
+// 32 rows (rank 0's carrying the residual) go through car_proto.h's push exchange with o_proj block
+// ob of every peer (the fused-all-reduce buffer: granules [16 ob, 16 ob + 16), epoch ctr[ob], as
+// gemv_core.h's EPI_AR blocks) and the summed rows are written to h — attention, o_proj and its
+// all-reduce in one launch.
+template <int G, int D, int NR, int KC, bool AR>
 __global__ __launch_bounds__(512) void attn_split_oproj_kernel(
     const bf16_t* __restrict__ q, const bf16_t* __restrict__ k_cache, const bf16_t* __restrict__ v_cache,
     const int32_t* __restrict__ block_tables, int bt_stride, const int32_t* __restrict__ seq_lens, float* __restrict__ part,
     int* __restrict__ counters, bf16_t* __restrict__ attn_out, int nkv, int bs, int nblocks, int min_chunk,
     int max_chunks, int gsize, int max_groups, float scale_log2, int* __restrict__ fault, const bf16_t* __restrict__ w_o,
-    bf16_t* __restrict__ h, uint32_t* __restrict__ handoff, int* __restrict__ octr, int nca) {
+    bf16_t* __restrict__ h, uint32_t* __restrict__ handoff, int* __restrict__ octr, int nca, CarArgs ar) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int A = nca * nkv;
   if (static_cast<int>(blockIdx.x) < A) {
@@ -291,15 +297,22 @@ __global__ __launch_bounds__(512) void attn_split_oproj_kernel(
   }
   constexpr int K_o = KC * 512;  // input columns (all heads): 8 bf16 per chunk, 64 lanes
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
-  const int row0 = (blockIdx.x - A) * (8 * NR) + wave * NR;
+  const int ob = blockIdx.x - A;
+  const int row0 = ob * (8 * NR) + wave * NR;
   const uint32_t tag = static_cast<uint32_t>(__hip_atomic_load(octr + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) + 1u;
   u32x4 wt[NR][KC];
 #pragma unroll
   for (int r = 0; r < NR; ++r)
 #pragma unroll
     for (int i = 0; i < KC; ++i) wt[r][i] = load16<true>(w_o + static_cast<int64_t>(row0 + r) * K_o + 8 * (lane + 64 * i));
-  float resid = 0.f;
-  if (lane < NR) resid = bf16_to_f32(h[row0 + lane]);
+  uint32_t ar_epoch = 0;
+  if constexpr (AR) {
+    static_assert(8 * NR / 2 <= kArGranulesPerBlock, "one block's row pairs per granule slot range");
+    if (tid == 0)
+      ar_epoch = __hip_atomic_load(car_ctr(ar.P.base[ar.rank]) + ob, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) + 1;
+  }
+  float resid = 0.f;  // the residual rides on rank 0's partial only
+  if (lane < NR && (!AR || ar.rank == 0)) resid = bf16_to_f32(h[row0 + lane]);
   // hand-off: units U = 0 .. K_o / 4 (dims 4U .. 4U + 3), head-major as attention's output
   u32x2* xh = reinterpret_cast<u32x2*>(smem);
   if (wave == 0) {
@@ -341,10 +354,48 @@ __global__ __launch_bounds__(512) void attn_split_oproj_kernel(
 #pragma unroll
     for (int r = 0; r < NR; ++r) acc[r] = dot8_bf16(wt[r][i], x, acc[r]);
   }
+  if constexpr (!AR) {
 #pragma unroll
-  for (int r = 0; r < NR; ++r) {
-    const float v = wave_sum(acc[r]);
-    if (lane == r) h[row0 + r] = f32_to_bf16(resid + v);
+    for (int r = 0; r < NR; ++r) {
+      const float v = wave_sum(acc[r]);
+      if (lane == r) h[row0 + r] = f32_to_bf16(resid + v);
+    }
+  } else {
+    float* rowv = reinterpret_cast<float*>(smem + K_o * 2);  // the block's 8 NR row values (after xs)
+#pragma unroll
+    for (int r = 0; r < NR; ++r) {
+      const float v = wave_sum(acc[r]);
+      if (lane == r) rowv[wave * NR + r] = resid + v;
+    }
+    __syncthreads();
+    if (wave == 0) {
+      constexpr int NG = 8 * NR / 2;  // row pairs = granules per peer
+      const uint32_t epoch = __shfl(ar_epoch, 0, 64);
+      const long gbase = static_cast<long>(ob) * kArGranulesPerBlock;
+      for (int idx = lane; idx < ar.world * NG; idx += 64) {
+        const int p = idx / NG, gi = idx % NG;
+        if (p != ar.rank)
+          car_put(ar.P.base[p] + car_granule_off(epoch, ar.cap, ar.rank, gbase + gi),
+                  pack_bf16x2(rowv[2 * gi], rowv[2 * gi + 1]), epoch);
+      }
+      if (lane < NG) {
+        const long g[1] = {gbase + lane};
+        uint32_t in[kMaxRanks][1];
+        car_collect<1>(ar.P, ar.rank, ar.world, ar.cap, epoch, g, in);
+        in[ar.rank][0] = pack_bf16x2(rowv[2 * lane], rowv[2 * lane + 1]);
+        float lo = 0.f, hi = 0.f;
+#pragma unroll
+        for (int r = 0; r < kMaxRanks; ++r) {
+          if (r < ar.world) {
+            lo += bf16_lo(in[r][0]);
+            hi += bf16_hi(in[r][0]);
+          }
+        }
+        *reinterpret_cast<uint32_t*>(h + ob * 8 * NR + 2 * lane) = pack_bf16x2(lo, hi);
+      }
+      if (lane == 0)
+        __hip_atomic_store(car_ctr(ar.P.base[ar.rank]) + ob, epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
   }
   if (tid == 0) {
     const int O = gridDim.x - A;
@@ -407,8 +458,9 @@ extern "C" int llmc_attn_split_oproj_check(int H, int nh, int nkv, int D, int nc
   if (nkv < 1 || nh % nkv || nca < 1) return -1;
   const int G = nh / nkv, K_o = nh * D;
   if (!((G == 4 && D == 128) || (G == 8 && D == 128) || (G == 4 && D == 64) || (G == 1 && D == 128))) return -2;
-  if (K_o != 2048 && K_o != 4096) return -3;  // 4 x K_o / 512 register chunks of weights per lane
-  if (H % 32 != 0) return -4;
+  // 4 x K_o / 512 register chunks of weights per lane (K_o 512-1024: a TP rank's head shard)
+  if (K_o != 512 && K_o != 1024 && K_o != 2048 && K_o != 4096) return -3;
+  if (H % 32 != 0 || H / 32 > kMaxBlocks) return -4;
   return 0;
 }
 
@@ -416,10 +468,20 @@ extern "C" int llmc_attn_split_oproj(const void* q, const void* k_cache, const v
                                      int bt_stride, const void* seq_len, void* part, void* counters, void* attn_out,
                                      const void* w_o, void* h, void* handoff, void* octr, int H, int nh, int nkv, int D,
                                      int bs, int nblocks, int min_chunk, int nca, int max_chunks, float scale, void* fault,
-                                     hipStream_t s) {
+                                     const void* const* bases, int rank, int world, size_t cap, hipStream_t s) {
   if (llmc_attn_split_oproj_check(H, nh, nkv, D, nca) != 0 || nca > max_chunks || min_chunk % 128 != 0 || bt_stride < 1 ||
-      nblocks < 1)
+      nblocks < 1 || world < 1 || world > kMaxRanks || rank < 0 || rank >= world)
     return -1;
+  const bool ar_on = world > 1;
+  CarArgs ar{};
+  if (ar_on) {
+    if (bases == nullptr || static_cast<size_t>(H / 32) * kArGranulesPerBlock * 8 > cap / kMaxRanks) return -1;
+    for (int r = 0; r < kMaxRanks; ++r)
+      ar.P.base[r] = r < world ? static_cast<char*>(const_cast<void*>(bases[r])) : nullptr;
+    ar.rank = rank;
+    ar.world = world;
+    ar.cap = static_cast<long>(cap);
+  }
   const int G = nh / nkv, K_o = nh * D;
   const int max_groups = llmc_attn_decode_groups(max_chunks);
   const int gsize = nca > kAttnOneLevel ? kAttnGroup : nca;
@@ -429,7 +491,7 @@ extern "C" int llmc_attn_split_oproj(const void* q, const void* k_cache, const v
   const int max_chunk = bal > 2 * min_chunk ? bal : 2 * min_chunk;
   size_t lds = 8 * 32 * kVRowBytes + static_cast<size_t>(8) * G * (D + 2) * sizeof(float) +
                static_cast<size_t>((max_chunk + bs - 1) / bs + 2) * sizeof(int);
-  if (lds < static_cast<size_t>(K_o) * 2) lds = static_cast<size_t>(K_o) * 2;
+  if (lds < static_cast<size_t>(K_o) * 2 + 32 * sizeof(float)) lds = static_cast<size_t>(K_o) * 2 + 32 * sizeof(float);
   if (lds > 160 * 1024) return -4;
   constexpr int NR = 4;
   const int O = H / (8 * NR);
@@ -437,7 +499,7 @@ extern "C" int llmc_attn_split_oproj(const void* q, const void* k_cache, const v
   const float sl2 = scale * 1.4426950408889634f;
 #define LLMC_SO(GG, DD, KC)                                                                                        \
   do {                                                                                                               \
-    auto kern = attn_split_oproj_kernel<GG, DD, NR, KC>;                                                             \
+    auto kern = ar_on ? attn_split_oproj_kernel<GG, DD, NR, KC, true> : attn_split_oproj_kernel<GG, DD, NR, KC, false>; \
     static bool attr = false;                                                                                        \
     if (!attr) {                                                                                                     \
       (void)hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize,    \
@@ -448,18 +510,21 @@ extern "C" int llmc_attn_split_oproj(const void* q, const void* k_cache, const v
                                 (const int32_t*)block_table, bt_stride, (const int32_t*)seq_len, (float*)part,        \
                                 (int*)counters, (bf16_t*)attn_out, nkv, bs, nblocks, min_chunk, max_chunks, gsize,     \
                                 max_groups, sl2, (int*)fault, (const bf16_t*)w_o, (bf16_t*)h, (uint32_t*)handoff,      \
-                                (int*)octr, nca);                                                                    \
+                                (int*)octr, nca, ar);                                                                \
   } while (0)
   const int kc = K_o / 512;
-  if (G == 4 && D == 128) {
-    if (kc == 8) LLMC_SO(4, 128, 8); else LLMC_SO(4, 128, 4);
-  } else if (G == 8 && D == 128) {
-    if (kc == 8) LLMC_SO(8, 128, 8); else LLMC_SO(8, 128, 4);
-  } else if (G == 4 && D == 64) {
-    if (kc == 8) LLMC_SO(4, 64, 8); else LLMC_SO(4, 64, 4);
-  } else {
-    if (kc == 8) LLMC_SO(1, 128, 8); else LLMC_SO(1, 128, 4);
-  }
+#define LLMC_SO_KC(GG, DD)                                                                                         \
+  do {                                                                                                               \
+    if (kc == 8) LLMC_SO(GG, DD, 8);                                                                                 \
+    else if (kc == 4) LLMC_SO(GG, DD, 4);                                                                            \
+    else if (kc == 2) LLMC_SO(GG, DD, 2);                                                                            \
+    else LLMC_SO(GG, DD, 1);                                                                                         \
+  } while (0)
+  if (G == 4 && D == 128) LLMC_SO_KC(4, 128);
+  else if (G == 8 && D == 128) LLMC_SO_KC(8, 128);
+  else if (G == 4 && D == 64) LLMC_SO_KC(4, 64);
+  else LLMC_SO_KC(1, 128);
+#undef LLMC_SO_KC
 #undef LLMC_SO
   return static_cast<int>(hipGetLastError());
 }

@@ -32,7 +32,7 @@ int llmc_attn_decode_groups(int);
 int llmc_attn_split_oproj_check(int, int, int, int, int);
 int llmc_attn_split_oproj(const void*, const void*, const void*, const void*, int, const void*, void*, void*, void*,
                           const void*, void*, void*, void*, int, int, int, int, int, int, int, int, int, float, void*,
-                          hipStream_t);
+                          const void* const*, int, int, size_t, hipStream_t);
 int llmc_attn_oproj_check(int, int, int, int, int, int);
 int llmc_attn_oproj(const void*, const void*, const void*, const void*, int, const void*, const void*, void*, void*,
                     void*, void*, void*, void*, void*, int, int, int, int, int, int, int, int, float, int, void*,
@@ -129,10 +129,13 @@ PYBIND11_MODULE(_llmc_hip, m) {
   });
   m.def("attn_split_oproj", [](ptr q, ptr kc, ptr vc, ptr bt, int bts, ptr sl, ptr part, ptr ctr, ptr attn_out,
                                ptr w_o, ptr h, ptr handoff, ptr octr, int H, int nh, int nkv, int D, int bs,
-                               int nblocks, int min_chunk, int nca, int max_chunks, float scale, ptr fault, ptr s) {
+                               int nblocks, int min_chunk, int nca, int max_chunks, float scale, ptr fault,
+                               const std::vector<ptr>& bases, int rank, int world, size_t cap, ptr s) {
+    std::vector<const void*> b(bases.size());
+    for (size_t i = 0; i < bases.size(); ++i) b[i] = P(bases[i]);
     check(llmc_attn_split_oproj(P(q), P(kc), P(vc), P(bt), bts, P(sl), P(part), P(ctr), P(attn_out), P(w_o), P(h),
                                 P(handoff), P(octr), H, nh, nkv, D, bs, nblocks, min_chunk, nca, max_chunks, scale,
-                                P(fault), S(s)),
+                                P(fault), b.empty() ? nullptr : b.data(), rank, world, cap, S(s)),
           "attn_split_oproj");
   });
   m.def("attn_oproj_check", [](int H, int nh, int nkv, int D, int nc, int K_o) {

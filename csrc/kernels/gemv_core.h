@@ -37,8 +37,8 @@ enum { EPI_BF16 = 0, EPI_F32 = 1, EPI_RESADD = 2, EPI_SILU = 3, EPI_ROPE = 4, EP
 // separate EPI_RESADD / EPI_BF16 GEMV followed by the one-shot all-reduce, bit for bit, without
 // that kernel's launch, its boundary and its re-read of h. Every block of a launch is dispatched
 // in index order on every rank, so the lowest unfinished block is resident everywhere: no
-// deadlock whatever else shares the GPUs (the spin is bounded anyway).
-constexpr int kArGranulesPerBlock = 16;
+// deadlock whatever else shares the GPUs (the spin is bounded anyway). Granules per block:
+// car_proto.h kArGranulesPerBlock.
 
 struct RopeEpi {
   bf16_t* q_out;            // [M, q_stride], canonical head-major layout

@@ -289,7 +289,9 @@ class Engine:
         self.so_buckets: List[bool] = [False] * len(self.attn_buckets)
         self.so_nca = 0
         so = self.ecfg.split_oproj
-        if self.on_gpu and so not in ("", "0") and B == 1 and self.tp.size == 1 and not c.is_moe:
+        # TP ranks: the o_proj blocks all-reduce their rows themselves (the fused-all-reduce buffer)
+        tp_ok = self.tp.size == 1 or self.tp.custom_fused is not None
+        if self.on_gpu and so not in ("", "0") and B == 1 and tp_ok:
             self.so_nca = ops.split_oproj_nca(c.hidden, self.nh, self.nkv, self.D)
             if self.so_nca:
                 self.so_buckets = [so == "all" or not fused for _, _, _, fused in self.attn_buckets]
@@ -613,10 +615,11 @@ class Engine:
             ops.qkv_rope(h, Lw.w_qkv, Lw.ln1, c.rms_eps, q, self.k_cache[li], self.v_cache[li], self.positions[:B],
                          self.slots[:B], self.cos_t, self.sin_t, self.nh, self.nkv, self.D, self.bs,
                          mfma=self.mfma_decode)
-            if so:  # split roles: attention blocks + o_proj blocks of one grid, residual added
+            if so:  # split roles: attention blocks + o_proj blocks of one grid (+ the TP all-reduce)
                 ops.attn_split_oproj(q, self.k_cache[li], self.v_cache[li], self.block_tables[:1], self.seq_lens[:1],
                                      Lw.w_o, h, attn, self.so_part, self.so_ctr, self.so_ws, self.nh, self.nkv, self.D,
-                                     self.bs, self.so_nca, self.scale, fault=self.attn_fault)
+                                     self.bs, self.so_nca, self.scale, fault=self.attn_fault,
+                                     car=self.tp.custom_fused if self.tp.size > 1 else None)
             elif ao_chunk:  # one-row engines without TP: attention + o_proj + residual in one launch
                 ops.attn_oproj(q, self.k_cache[li], self.v_cache[li], self.block_tables[:1], self.seq_lens[:1], Lw.w_o,
                                h, attn, self.ao_ws, self.nh, self.nkv, self.D, self.bs, ao_chunk, self.ao_nc,

@@ -324,11 +324,14 @@ def split_oproj_workspace(nh: int, D: int, device):
 
 
 def attn_split_oproj(q, k_cache, v_cache, block_table, seq_len, w_o, h, attn_out, part, counters, ws, nh, nkv, D, bs,
-                     nca, scale, fault: Optional[torch.Tensor] = None, min_chunk: int = 128) -> None:
+                     nca, scale, fault: Optional[torch.Tensor] = None, min_chunk: int = 128, car=None) -> None:
     """Decode attention of ONE row + o_proj + residual in one launch with split roles
     (csrc/kernels/attn_decode.hip ``attn_split_oproj_kernel``): ``h[0] += w_o @ attention(q[0])``;
     ``attn_out[0]`` gets the attention output. ``part`` / ``counters`` = ``decode_attn_workspace``
-    (max_chunks >= nca), ``ws`` = ``split_oproj_workspace``, ``nca`` = ``split_oproj_nca``."""
+    (max_chunks >= nca), ``ws`` = ``split_oproj_workspace``, ``nca`` = ``split_oproj_nca``.
+    ``car`` (a TP rank): the group's fused-all-reduce buffer (``TPGroup.custom_fused``): the o_proj
+    rows are this rank's row-parallel partial, summed over the group inside the launch
+    (``h[0] = h[0] + sum over ranks of w_o_r @ attention_r``)."""
     H = h.shape[-1]
     if not q.is_cuda:
         a = oracle.attn_decode(q[:1], k_cache, v_cache, block_table[:1], seq_len[:1], nh, nkv, D, bs, scale)
@@ -338,9 +341,11 @@ def attn_split_oproj(q, k_cache, v_cache, block_table, seq_len, w_o, h, attn_out
     groups = counters.shape[-1] - 2
     max_chunks = part.shape[2] - groups
     handoff, octr = ws
+    bases, rank, world, cap = (car.bases, car.rank, car.world, car.cap) if car is not None else ([], 0, 1, 0)
     kernels().attn_split_oproj(_p(q), _p(k_cache), _p(v_cache), _p(block_table), block_table.shape[-1], _p(seq_len),
                                _p(part), _p(counters), _p(attn_out), _p(w_o), _p(h), _p(handoff), _p(octr), H, nh, nkv,
-                               D, bs, k_cache.shape[0], min_chunk, nca, max_chunks, float(scale), _p(fault), _s(h))
+                               D, bs, k_cache.shape[0], min_chunk, nca, max_chunks, float(scale), _p(fault), bases, rank,
+                               world, cap, _s(h))
 
 
 def attn_prefill(q, k_cache, v_cache, block_tables, q_start, q_lens, ctx_lens, out, max_qlen, nh, nkv, D, bs, scale):

@@ -32,12 +32,19 @@ def _worker(rank, world, port, name, q, ekw=None):
         from llm_consensus_amd.models.config import FAMILIES
         from llm_consensus_amd.parallel.comm import TPGroup
 
+        ekw = dict(ekw or {})
+        if ekw.pop("_cu_split", False):  # each rank on its own half of the chip (as on GPUs of their own)
+            import os
+
+            os.environ["LLMC_CU_MASK"] = f"{rank * 128}-{rank * 128 + 127}"
         tp = TPGroup(dist.group.WORLD, rank, world)
         tp.enable_custom("cuda:0")
-        ekw = dict(ekw or {})
         if ekw.pop("_expect_fused", False):
             assert tp.custom_fused is not None
+        expect_so = ekw.pop("_expect_so", False)
         e = Engine(FAMILIES[name], EngineConfig(device="cuda:0", max_context=512, seed=5, **ekw), tp=tp)
+        if expect_so:
+            assert e.so_nca > 0 and all(e.so_buckets), (e.so_nca, e.so_buckets)
         e.warmup_graphs()
         s = e.new_sequence()
         e.prefill([s], [PROMPT])
@@ -72,11 +79,19 @@ def test_tp2_gpu_fused_rowparallel_allreduce_matches_tp1(cuda, monkeypatch):
     _tp2_vs_tp1("llama-small", {"_expect_fused": True})
 
 
+def test_tp2_gpu_split_oproj_fused_allreduce_matches_tp1(cuda, monkeypatch):
+    """The split-role attention + o_proj launch on TP ranks, its o_proj blocks all-reducing their
+    rows in the same launch (every bucket), the two ranks on separate halves of the chip."""
+    monkeypatch.setenv("LLMC_FUSED_AR", "force")
+    monkeypatch.setenv("LLMC_SPLIT_OPROJ", "all")
+    _tp2_vs_tp1("llama-small", {"_expect_fused": True, "_cu_split": True, "_expect_so": True})
+
+
 def _tp2_vs_tp1(name, ekw):
     from llm_consensus_amd.engine import Engine, EngineConfig
     from llm_consensus_amd.models.config import FAMILIES
 
-    ref = Engine(FAMILIES[name], EngineConfig(device="cuda:0", max_context=512, seed=5))
+    ref = Engine(FAMILIES[name], EngineConfig(device="cuda:0", max_context=512, seed=5, split_oproj="0"))
     s = ref.new_sequence()
     ref.prefill([s], [PROMPT])
     ref_logits = ref.full_logits(s).float().cpu()
@@ -107,7 +122,7 @@ def _tp2_vs_tp1(name, ekw):
             break
         agree += 1
     if agree < 8:
-        ref = Engine(FAMILIES[name], EngineConfig(device="cuda:0", max_context=512, seed=5))
+        ref = Engine(FAMILIES[name], EngineConfig(device="cuda:0", max_context=512, seed=5, split_oproj="0"))
         s = ref.new_sequence()
         ref.prefill([s], [PROMPT + gen[:agree]])
         lt = ref.full_logits(s).float().cpu()

@@ -12,6 +12,7 @@ step smoke 120 python -c "import __graft_entry__ as g; g.smoke()"
 step carlat 150 python -u scripts/car_latency.py --world 2,4
 step reh0 200 python -u scripts/tp_rehearsal.py --shape-tp 8 --world 2 --fused-ar 0
 step reh1 200 python -u scripts/tp_rehearsal.py --shape-tp 8 --world 2 --fused-ar 1
+step reh2 200 python -u scripts/tp_rehearsal.py --shape-tp 8 --world 2 --fused-ar 1 --split-oproj all
 step shard 200 python -u scripts/tp_shard_decode.py --tp 8 --ctx 2048 --tokens 256
 step attn_oproj 240 python -u scripts/microbench_kernels.py attn-oproj
 step prefill_gemm 240 python -u scripts/microbench_kernels.py prefill

@@ -333,14 +333,11 @@ __device__ __forceinline__ void merge_rows(__amdgpu_buffer_rsrc_t rsrc, const ch
 // one block). The last merger re-arms the tickets it took and advances the epoch (every block of
 // this launch read the epoch before it arrived). ctr = {top ticket, epoch, group tickets...};
 // `flag` is one LDS word. Every block but the last returns inside.
-// ``handoff`` (nullable): the final merger also publishes the head's output as 16-B units {bf16x2
-// dims 4u..4u+1, tag, bf16x2 dims 4u+2..4u+3, tag} (write-through), for a consumer in the same
-// launch that polls the tags (attn_split_oproj.hip).
 template <int G, int D, int NW, bool SC1OUT = false>
 __device__ __forceinline__ bool publish_and_merge(const float* red, float* part, int* ctr, int b, int nkv, int kvh,
                                                   int c, int nchunks, int gsize, int max_chunks, int max_groups,
                                                   uint32_t tag, bf16_t* out_row, char* smem, int* flag, int tid,
-                                                  int* fault, uint32_t* handoff = nullptr) {
+                                                  int* fault) {
   constexpr int HQ = D / 4, RU = HQ + 1, Q = G * HQ;
   const int rows = max_chunks + max_groups;
   float* slab = part + (static_cast<int64_t>(b) * nkv + kvh) * rows * G * RU * 4;
@@ -389,11 +386,6 @@ __device__ __forceinline__ bool publish_and_merge(const float* red, float* part,
                          __HIP_MEMORY_SCOPE_AGENT);
     } else {
       *reinterpret_cast<u32x2*>(out_row + g * D + 4 * u) = o2;
-    }
-    if (handoff != nullptr) {
-      const __amdgpu_buffer_rsrc_t hr =
-          __builtin_amdgcn_make_buffer_rsrc(handoff + static_cast<int64_t>(kvh) * Q * 4, 0, Q * 16, 0x00020000);
-      st16_sc1(hr, tid * 16, u32x4{o2[0], tag, o2[1], tag});
     }
   }
   if (tid == 0) {

@@ -35,21 +35,18 @@
 // a per-(row, kv head) epoch in device memory the merger advances (tag = epoch + 1: never 0,
 // never reused), so a granule left by any earlier launch can never match. Spins are bounded.
 #include "attn_core.h"
-#include "car_proto.h"
 
 namespace llmc {
 
 // ---------------------------------------------------------------------------------------------
 // One block of the split form: chunk c (of a grid of `gridc` per head) of kv head kvh, row b.
-// Also the attention role of attn_split_oproj.hip (`handoff` non-null: the merged head output is
-// published for the o_proj blocks of the same launch).
 template <int G, int D, int NW>
 __device__ __forceinline__ void attn_split_block(
     int c, int kvh, int b, int gridc, const bf16_t* __restrict__ q, int q_stride, const bf16_t* __restrict__ k_cache,
     const bf16_t* __restrict__ v_cache, const int32_t* __restrict__ block_tables, int bt_stride,
     const int32_t* __restrict__ seq_lens, float* __restrict__ part, int* __restrict__ counters, bf16_t* __restrict__ out,
     int out_stride, int nkv, int bs, int nblocks, int min_chunk, int max_chunks, int gsize, int max_groups,
-    float scale_log2, int* __restrict__ fault, char* smem, uint32_t* handoff = nullptr) {
+    float scale_log2, int* __restrict__ fault, char* smem) {
   static_assert(G <= 16 && D % 32 == 0 && D <= 128, "shape");
   using ST = SubTile<G, D>;
   constexpr int NT = NW * 64;
@@ -100,14 +97,12 @@ __device__ __forceinline__ void attn_split_block(
   st.to_lds(red, wave, lane);
   __syncthreads();
   bf16_t* out_row = out + static_cast<int64_t>(b) * out_stride + kvh * G * D;
-  if (nchunks == 1 && handoff == nullptr) {
+  if (nchunks == 1) {
     store_direct<G, D, NW>(red, out_row, tid);
     return;
   }
-  // (with a hand-off even a lone chunk goes through the merge: it publishes the granules and
-  // advances the epoch, like every other launch)
   publish_and_merge<G, D, NW>(red, part, ctr, b, nkv, kvh, c, nchunks, gsize, max_chunks, max_groups, tag, out_row, smem,
-                              reinterpret_cast<int*>(pages), tid, fault, handoff);
+                              reinterpret_cast<int*>(pages), tid, fault);
 }
 
 template <int G, int D, int NW>
@@ -254,158 +249,6 @@ static int launch_g(bool fused, int D, dim3 grid, hipStream_t s, const void* q, 
 #undef LLMC_ATTN_D
 }
 
-// ---------------------------------------------------------------------------------------------
-// Split-role attention + o_proj + residual of ONE decode row in one launch (docs/ARCHITECTURE.md
-// §8 "next step for the batch-1 chain"): h[n] += sum_k Wo[n, k] * attention(q)[k].
-//
-// attn_oproj.hip puts an attention range AND an o_proj tile on every block, and a CU's memory
-// requests share one queue: the block's weight stream lands in front of its own latency-critical
-// K/V and hand-off loads. Here the two jobs get different blocks of one grid, each alone on its CU:
-//  * blocks [0, A) (A = nca x nkv, dispatched first) are the split attention (attn_split_block,
-//    8 waves, balanced key ranges over nca blocks per kv head); each head's last arriver merges
-//    and publishes the head output as tagged granules (publish_and_merge's hand-off);
-//  * blocks [A, A + O) are o_proj blocks: 8 waves x NR rows, the block's whole weight tile
-//    (NR x K_o bf16 per wave: KC 16-B chunks per lane per row) issued into registers at once — it
-//    streams while the attention runs — then ONE wave polls the hand-off (one granule per head
-//    first, then every unit, re-read until all tags match) into LDS, and the projection is
-//    arithmetic on registers; lane r < NR adds row r to the residual h.
-// Both roles' registers (the weight tile is 4 x KC x 4 VGPRs) keep one 512-thread block per CU, so a
-// grid of A + O = 256 blocks puts every block on a CU of its own on an idle chip. Deadlock-free
-// whatever the residency: attention blocks never wait on o_proj blocks and are dispatched first
-// (in index order), and the merge only waits on blocks that have taken their tickets. The o_proj
-// blocks count their exits; the last re-arms the counter and advances their epoch (the tag they
-// expect = that epoch + 1 = the launch count, as the heads' epochs). Bounded spins (fault word 2).
-// AR (a tensor-parallel rank): the o_proj rows are this rank's row-parallel partial; the block's
-// 32 rows (rank 0's carrying the residual) go through car_proto.h's push exchange with o_proj block
-// ob of every peer (the fused-all-reduce buffer: granules [16 ob, 16 ob + 16), epoch ctr[ob], as
-// gemv_core.h's EPI_AR blocks) and the summed rows are written to h — attention, o_proj and its
-// all-reduce in one launch.
-template <int G, int D, int NR, int KC, bool AR>
-__global__ __launch_bounds__(512) void attn_split_oproj_kernel(
-    const bf16_t* __restrict__ q, const bf16_t* __restrict__ k_cache, const bf16_t* __restrict__ v_cache,
-    const int32_t* __restrict__ block_tables, int bt_stride, const int32_t* __restrict__ seq_lens, float* __restrict__ part,
-    int* __restrict__ counters, bf16_t* __restrict__ attn_out, int nkv, int bs, int nblocks, int min_chunk,
-    int max_chunks, int gsize, int max_groups, float scale_log2, int* __restrict__ fault, const bf16_t* __restrict__ w_o,
-    bf16_t* __restrict__ h, uint32_t* __restrict__ handoff, int* __restrict__ octr, int nca, CarArgs ar) {
-  extern __shared__ __attribute__((aligned(16))) char smem[];
-  const int A = nca * nkv;
-  if (static_cast<int>(blockIdx.x) < A) {
-    attn_split_block<G, D, 8>(blockIdx.x % nca, blockIdx.x / nca, 0, nca, q, G * D * nkv, k_cache, v_cache, block_tables,
-                              bt_stride, seq_lens, part, counters, attn_out, G * D * nkv, nkv, bs, nblocks, min_chunk,
-                              max_chunks, gsize, max_groups, scale_log2, fault, smem, handoff);
-    return;
-  }
-  constexpr int K_o = KC * 512;  // input columns (all heads): 8 bf16 per chunk, 64 lanes
-  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
-  const int ob = blockIdx.x - A;
-  const int row0 = ob * (8 * NR) + wave * NR;
-  const uint32_t tag = static_cast<uint32_t>(__hip_atomic_load(octr + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) + 1u;
-  u32x4 wt[NR][KC];
-#pragma unroll
-  for (int r = 0; r < NR; ++r)
-#pragma unroll
-    for (int i = 0; i < KC; ++i) wt[r][i] = load16<true>(w_o + static_cast<int64_t>(row0 + r) * K_o + 8 * (lane + 64 * i));
-  uint32_t ar_epoch = 0;
-  if constexpr (AR) {
-    static_assert(8 * NR / 2 <= kArGranulesPerBlock, "one block's row pairs per granule slot range");
-    if (tid == 0)
-      ar_epoch = __hip_atomic_load(car_ctr(ar.P.base[ar.rank]) + ob, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) + 1;
-  }
-  float resid = 0.f;  // the residual rides on rank 0's partial only
-  if (lane < NR && (!AR || ar.rank == 0)) resid = bf16_to_f32(h[row0 + lane]);
-  // hand-off: units U = 0 .. K_o / 4 (dims 4U .. 4U + 3), head-major as attention's output
-  u32x2* xh = reinterpret_cast<u32x2*>(smem);
-  if (wave == 0) {
-    constexpr int UPL = K_o / 4 / 64;  // units per lane
-    const char* hb = reinterpret_cast<const char*>(handoff);
-    constexpr int Q = G * D / 4;  // units per kv head
-    if (lane < nkv) {  // one granule per head first: the wave's full sweep only once they have landed
-      for (unsigned spins = 0; ld8_atomic(hb, lane * Q * 16)[1] != tag && spins < kSpinLimit; ++spins)
-        __builtin_amdgcn_s_sleep(2);
-    }
-    u32x2 a[UPL], b[UPL];
-    for (unsigned spins = 0;; ++spins) {
-      bool ok = true;
-#pragma unroll
-      for (int j = 0; j < UPL; ++j) {
-        const int U = lane + 64 * j;
-        a[j] = ld8_atomic(hb, U * 16);
-        b[j] = ld8_atomic(hb, U * 16 + 8);
-        ok = ok && a[j][1] == tag && b[j][1] == tag;
-      }
-      if (__all(ok)) break;
-      if (spins >= kSpinLimit) {
-        if (lane == 0 && fault != nullptr) __hip_atomic_store(fault, 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        break;
-      }
-      __builtin_amdgcn_s_sleep(1);
-    }
-#pragma unroll
-    for (int j = 0; j < UPL; ++j) xh[lane + 64 * j] = u32x2{a[j][0], b[j][0]};
-  }
-  __syncthreads();
-  const u32x4* xs = reinterpret_cast<const u32x4*>(smem);
-  float acc[NR];
-#pragma unroll
-  for (int r = 0; r < NR; ++r) acc[r] = 0.f;
-#pragma unroll
-  for (int i = 0; i < KC; ++i) {
-    const u32x4 x = xs[lane + 64 * i];
-#pragma unroll
-    for (int r = 0; r < NR; ++r) acc[r] = dot8_bf16(wt[r][i], x, acc[r]);
-  }
-  if constexpr (!AR) {
-#pragma unroll
-    for (int r = 0; r < NR; ++r) {
-      const float v = wave_sum(acc[r]);
-      if (lane == r) h[row0 + r] = f32_to_bf16(resid + v);
-    }
-  } else {
-    float* rowv = reinterpret_cast<float*>(smem + K_o * 2);  // the block's 8 NR row values (after xs)
-#pragma unroll
-    for (int r = 0; r < NR; ++r) {
-      const float v = wave_sum(acc[r]);
-      if (lane == r) rowv[wave * NR + r] = resid + v;
-    }
-    __syncthreads();
-    if (wave == 0) {
-      constexpr int NG = 8 * NR / 2;  // row pairs = granules per peer
-      const uint32_t epoch = __shfl(ar_epoch, 0, 64);
-      const long gbase = static_cast<long>(ob) * kArGranulesPerBlock;
-      for (int idx = lane; idx < ar.world * NG; idx += 64) {
-        const int p = idx / NG, gi = idx % NG;
-        if (p != ar.rank)
-          car_put(ar.P.base[p] + car_granule_off(epoch, ar.cap, ar.rank, gbase + gi),
-                  pack_bf16x2(rowv[2 * gi], rowv[2 * gi + 1]), epoch);
-      }
-      if (lane < NG) {
-        const long g[1] = {gbase + lane};
-        uint32_t in[kMaxRanks][1];
-        car_collect<1>(ar.P, ar.rank, ar.world, ar.cap, epoch, g, in);
-        in[ar.rank][0] = pack_bf16x2(rowv[2 * lane], rowv[2 * lane + 1]);
-        float lo = 0.f, hi = 0.f;
-#pragma unroll
-        for (int r = 0; r < kMaxRanks; ++r) {
-          if (r < ar.world) {
-            lo += bf16_lo(in[r][0]);
-            hi += bf16_hi(in[r][0]);
-          }
-        }
-        *reinterpret_cast<uint32_t*>(h + ob * 8 * NR + 2 * lane) = pack_bf16x2(lo, hi);
-      }
-      if (lane == 0)
-        __hip_atomic_store(car_ctr(ar.P.base[ar.rank]) + ob, epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-    }
-  }
-  if (tid == 0) {
-    const int O = gridDim.x - A;
-    if (__hip_atomic_fetch_add(octr, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == O - 1) {
-      __hip_atomic_store(octr, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      __hip_atomic_store(octr + 1, static_cast<int>(tag), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
-  }
-}
-
 }  // namespace llmc
 
 using namespace llmc;
@@ -447,84 +290,4 @@ extern "C" int llmc_attn_decode(const void* q, int q_stride, const void* k_cache
     case 8: return launch_g<8>(f, D, grid, s, q, q_stride, k_cache, v_cache, block_tables, bt_stride, seq_lens, part, counters, out, out_stride, nkv, bs, nblocks, chunk, max_chunks, gsize, max_groups, scale, static_cast<int*>(fault));
     default: return -3;
   }
-}
-
-// Split-role attention + o_proj + residual of one decode row (attn_split_oproj_kernel). nca
-// attention blocks per kv head over >= min_chunk keys each (a multiple of 128), then H / (8 NR)
-// o_proj blocks. Shapes: G * D * nkv = K_o in {2048, 4096}; H % (8 * NR) == 0.
-// Workspace: part / counters of decode_attn_workspace (max_chunks >= nca), handoff u32 [K_o],
-// octr int32 [16] (zeroed once). Returns 0 when the shape is supported and launched.
-extern "C" int llmc_attn_split_oproj_check(int H, int nh, int nkv, int D, int nca) {
-  if (nkv < 1 || nh % nkv || nca < 1) return -1;
-  const int G = nh / nkv, K_o = nh * D;
-  if (!((G == 4 && D == 128) || (G == 8 && D == 128) || (G == 4 && D == 64) || (G == 1 && D == 128))) return -2;
-  // 4 x K_o / 512 register chunks of weights per lane (K_o 512-1024: a TP rank's head shard)
-  if (K_o != 512 && K_o != 1024 && K_o != 2048 && K_o != 4096) return -3;
-  if (H % 32 != 0 || H / 32 > kMaxBlocks) return -4;
-  return 0;
-}
-
-extern "C" int llmc_attn_split_oproj(const void* q, const void* k_cache, const void* v_cache, const void* block_table,
-                                     int bt_stride, const void* seq_len, void* part, void* counters, void* attn_out,
-                                     const void* w_o, void* h, void* handoff, void* octr, int H, int nh, int nkv, int D,
-                                     int bs, int nblocks, int min_chunk, int nca, int max_chunks, float scale, void* fault,
-                                     const void* const* bases, int rank, int world, size_t cap, hipStream_t s) {
-  if (llmc_attn_split_oproj_check(H, nh, nkv, D, nca) != 0 || nca > max_chunks || min_chunk % 128 != 0 || bt_stride < 1 ||
-      nblocks < 1 || world < 1 || world > kMaxRanks || rank < 0 || rank >= world)
-    return -1;
-  const bool ar_on = world > 1;
-  CarArgs ar{};
-  if (ar_on) {
-    if (bases == nullptr || static_cast<size_t>(H / 32) * kArGranulesPerBlock * 8 > cap / kMaxRanks) return -1;
-    for (int r = 0; r < kMaxRanks; ++r)
-      ar.P.base[r] = r < world ? static_cast<char*>(const_cast<void*>(bases[r])) : nullptr;
-    ar.rank = rank;
-    ar.world = world;
-    ar.cap = static_cast<long>(cap);
-  }
-  const int G = nh / nkv, K_o = nh * D;
-  const int max_groups = llmc_attn_decode_groups(max_chunks);
-  const int gsize = nca > kAttnOneLevel ? kAttnGroup : nca;
-  // attention role LDS, as launch_split_nw<G, D, 8> sizes it for this table
-  const int units = (bt_stride * bs + 31) / 32;
-  const int bal = 32 * ((units + nca - 1) / nca) + 32;
-  const int max_chunk = bal > 2 * min_chunk ? bal : 2 * min_chunk;
-  size_t lds = 8 * 32 * kVRowBytes + static_cast<size_t>(8) * G * (D + 2) * sizeof(float) +
-               static_cast<size_t>((max_chunk + bs - 1) / bs + 2) * sizeof(int);
-  if (lds < static_cast<size_t>(K_o) * 2 + 32 * sizeof(float)) lds = static_cast<size_t>(K_o) * 2 + 32 * sizeof(float);
-  if (lds > 160 * 1024) return -4;
-  constexpr int NR = 4;
-  const int O = H / (8 * NR);
-  const dim3 grid(nca * nkv + O);
-  const float sl2 = scale * 1.4426950408889634f;
-#define LLMC_SO(GG, DD, KC)                                                                                        \
-  do {                                                                                                               \
-    auto kern = ar_on ? attn_split_oproj_kernel<GG, DD, NR, KC, true> : attn_split_oproj_kernel<GG, DD, NR, KC, false>; \
-    static bool attr = false;                                                                                        \
-    if (!attr) {                                                                                                     \
-      (void)hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize,    \
-                                160 * 1024);                                                                         \
-      attr = true;                                                                                                   \
-    }                                                                                                                \
-    kern<<<grid, 512, lds, s>>>((const bf16_t*)q, (const bf16_t*)k_cache, (const bf16_t*)v_cache,                    \
-                                (const int32_t*)block_table, bt_stride, (const int32_t*)seq_len, (float*)part,        \
-                                (int*)counters, (bf16_t*)attn_out, nkv, bs, nblocks, min_chunk, max_chunks, gsize,     \
-                                max_groups, sl2, (int*)fault, (const bf16_t*)w_o, (bf16_t*)h, (uint32_t*)handoff,      \
-                                (int*)octr, nca, ar);                                                                \
-  } while (0)
-  const int kc = K_o / 512;
-#define LLMC_SO_KC(GG, DD)                                                                                         \
-  do {                                                                                                               \
-    if (kc == 8) LLMC_SO(GG, DD, 8);                                                                                 \
-    else if (kc == 4) LLMC_SO(GG, DD, 4);                                                                            \
-    else if (kc == 2) LLMC_SO(GG, DD, 2);                                                                            \
-    else LLMC_SO(GG, DD, 1);                                                                                         \
-  } while (0)
-  if (G == 4 && D == 128) LLMC_SO_KC(4, 128);
-  else if (G == 8 && D == 128) LLMC_SO_KC(8, 128);
-  else if (G == 4 && D == 64) LLMC_SO_KC(4, 64);
-  else LLMC_SO_KC(1, 128);
-#undef LLMC_SO_KC
-#undef LLMC_SO
-  return static_cast<int>(hipGetLastError());
 }

@@ -29,10 +29,6 @@ int llmc_gemm_t128(const void*, int, const void*, int, void*, int, int, int, int
 int llmc_rope_kv_write(const void*, int, void*, int, const void*, const void*, const void*, void*, void*, const void*,
                        int, int, int, int, int, hipStream_t);
 int llmc_attn_decode_groups(int);
-int llmc_attn_split_oproj_check(int, int, int, int, int);
-int llmc_attn_split_oproj(const void*, const void*, const void*, const void*, int, const void*, void*, void*, void*,
-                          const void*, void*, void*, void*, int, int, int, int, int, int, int, int, int, float, void*,
-                          const void* const*, int, int, size_t, hipStream_t);
 int llmc_attn_oproj_check(int, int, int, int, int, int);
 int llmc_attn_oproj(const void*, const void*, const void*, const void*, int, const void*, const void*, void*, void*,
                     void*, void*, void*, void*, void*, int, int, int, int, int, int, int, int, float, int, void*,
@@ -124,20 +120,6 @@ PYBIND11_MODULE(_llmc_hip, m) {
           "rope_kv_write");
   });
   m.def("attn_decode_groups", [](int max_chunks) { return llmc_attn_decode_groups(max_chunks); });
-  m.def("attn_split_oproj_check", [](int H, int nh, int nkv, int D, int nca) {
-    return llmc_attn_split_oproj_check(H, nh, nkv, D, nca);
-  });
-  m.def("attn_split_oproj", [](ptr q, ptr kc, ptr vc, ptr bt, int bts, ptr sl, ptr part, ptr ctr, ptr attn_out,
-                               ptr w_o, ptr h, ptr handoff, ptr octr, int H, int nh, int nkv, int D, int bs,
-                               int nblocks, int min_chunk, int nca, int max_chunks, float scale, ptr fault,
-                               const std::vector<ptr>& bases, int rank, int world, size_t cap, ptr s) {
-    std::vector<const void*> b(bases.size());
-    for (size_t i = 0; i < bases.size(); ++i) b[i] = P(bases[i]);
-    check(llmc_attn_split_oproj(P(q), P(kc), P(vc), P(bt), bts, P(sl), P(part), P(ctr), P(attn_out), P(w_o), P(h),
-                                P(handoff), P(octr), H, nh, nkv, D, bs, nblocks, min_chunk, nca, max_chunks, scale,
-                                P(fault), b.empty() ? nullptr : b.data(), rank, world, cap, S(s)),
-          "attn_split_oproj");
-  });
   m.def("attn_oproj_check", [](int H, int nh, int nkv, int D, int nc, int K_o) {
     return llmc_attn_oproj_check(H, nh, nkv, D, nc, K_o);
   });

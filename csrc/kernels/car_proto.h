@@ -1,6 +1,5 @@
-// K13 custom-collective protocol shared by the standalone one-shot kernels (allreduce.hip), the
-// row-parallel GEMV's fused all-reduce epilogue (gemv_core.h, EPI_AR) and the o_proj blocks of the
-// split-role attention launch on TP ranks (attn_decode.hip).
+// K13 custom-collective protocol shared by the standalone one-shot kernels (allreduce.hip) and the
+// row-parallel GEMV's fused all-reduce epilogue (gemv_core.h, EPI_AR).
 //
 // Each rank owns ONE uncached (fine-grained) allocation, exported with hipIpc and mapped by every
 // peer:   [ signals kSigBytes | data parity 0 (cap) | data parity 1 (cap) ]
@@ -38,8 +37,8 @@ constexpr int kFlag2Off = kFlagOff + kTsFlagBlocks * kMaxRanks * 4;   // two-sho
 constexpr int kTimeoutOff = kFlag2Off + kTsFlagBlocks * kMaxRanks * 4;
 static_assert(kTimeoutOff + 4 <= static_cast<int>(kSigBytes), "signal layout");
 constexpr unsigned kCarSpinLimit = 1u << 24;  // polls (s_sleep 2 each, ~seconds) before giving up
-// fused-all-reduce buffer (gemv_core.h EPI_AR, attn_split_oproj's AR o_proj blocks): block b of a
-// launch owns granules [16 b, 16 b + 16) of every slot and epoch ctr[b], whatever the kernel
+// fused-all-reduce buffer (gemv_core.h EPI_AR): block b of a launch owns granules [16 b, 16 b + 16)
+// of every slot and epoch ctr[b]
 constexpr int kArGranulesPerBlock = 16;
 
 struct CarPeers {

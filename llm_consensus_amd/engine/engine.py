@@ -69,11 +69,6 @@ class EngineConfig:
     attn_oproj: bool = dataclasses.field(default_factory=lambda: os.environ.get("LLMC_ATTN_OPROJ", "1") != "0")
     attn_oproj_min_chunk: int = dataclasses.field(
         default_factory=lambda: 32 if os.environ.get("LLMC_ATTN_OPROJ") == "all" else ops.ATTN_OPROJ_MIN_CHUNK)
-    # one-row engines without TP: the split-role attention + o_proj launch (attention blocks and
-    # o_proj blocks on different CUs of one grid, attn_decode.hip attn_split_oproj_kernel), taking
-    # precedence over attn_oproj. "long": the buckets of the balanced-split (long-context) attention
-    # form; "all": every bucket; "0": never (LLMC_SPLIT_OPROJ)
-    split_oproj: str = dataclasses.field(default_factory=lambda: os.environ.get("LLMC_SPLIT_OPROJ", "0"))
 
 
 FUSED_CHUNK_SMALL, FUSED_CHUNK_LARGE = 128, 256
@@ -284,19 +279,6 @@ class Engine:
                 self.ao_chunks = [ch if ch >= lo and (ch <= 256 or self.bs % 64 == 0) else 0
                                   for ch in (ops.attn_oproj_chunk(cap, self.ao_nc) for cap, _, _, _ in self.attn_buckets)]
                 self.ao_ws = ops.attn_oproj_workspace(c.hidden, self.nh, self.nkv, self.D, self.ao_nc, dev)
-        # split-role attention + o_proj: per bucket whether it runs (own attention workspace: its
-        # heads' epochs must count exactly its launches, as its o_proj blocks' epoch does)
-        self.so_buckets: List[bool] = [False] * len(self.attn_buckets)
-        self.so_nca = 0
-        so = self.ecfg.split_oproj
-        # TP ranks: the o_proj blocks all-reduce their rows themselves (the fused-all-reduce buffer)
-        tp_ok = self.tp.size == 1 or self.tp.custom_fused is not None
-        if self.on_gpu and so not in ("", "0") and B == 1 and tp_ok:
-            self.so_nca = ops.split_oproj_nca(c.hidden, self.nh, self.nkv, self.D)
-            if self.so_nca:
-                self.so_buckets = [so == "all" or not fused for _, _, _, fused in self.attn_buckets]
-                self.so_part, self.so_ctr = ops.decode_attn_workspace(1, self.nh, self.nkv, self.D, self.so_nca, dev)
-                self.so_ws = ops.split_oproj_workspace(self.nh, self.D, dev)
         # set by a decode-attention merger that gave up on a partial (checked after every decode)
         self.attn_fault = torch.zeros(1, dtype=torch.int32, device=dev) if self.on_gpu else None
         if self.on_gpu:
@@ -606,8 +588,7 @@ class Engine:
         h, q, attn, act = self.h[:B], self.q[:B], self.attn[:B], self.act[:B]
         ops.embedding(self.tokens_in[:B], self.w.embed, out=h)
         bi = -1 if bucket is None else bucket
-        so = B == 1 and self.so_buckets[bi]
-        ao_chunk = self.ao_chunks[bi] if B == 1 and not so else 0
+        ao_chunk = self.ao_chunks[bi] if B == 1 else 0
         dbg = self._debug_layer_io  # eager debug steps only: each layer's input, then the last output
         for li, Lw in enumerate(self.w.layers):
             if dbg is not None:
@@ -615,12 +596,7 @@ class Engine:
             ops.qkv_rope(h, Lw.w_qkv, Lw.ln1, c.rms_eps, q, self.k_cache[li], self.v_cache[li], self.positions[:B],
                          self.slots[:B], self.cos_t, self.sin_t, self.nh, self.nkv, self.D, self.bs,
                          mfma=self.mfma_decode)
-            if so:  # split roles: attention blocks + o_proj blocks of one grid (+ the TP all-reduce)
-                ops.attn_split_oproj(q, self.k_cache[li], self.v_cache[li], self.block_tables[:1], self.seq_lens[:1],
-                                     Lw.w_o, h, attn, self.so_part, self.so_ctr, self.so_ws, self.nh, self.nkv, self.D,
-                                     self.bs, self.so_nca, self.scale, fault=self.attn_fault,
-                                     car=self.tp.custom_fused if self.tp.size > 1 else None)
-            elif ao_chunk:  # one-row engines without TP: attention + o_proj + residual in one launch
+            if ao_chunk:  # one-row engines without TP: attention + o_proj + residual in one launch
                 ops.attn_oproj(q, self.k_cache[li], self.v_cache[li], self.block_tables[:1], self.seq_lens[:1], Lw.w_o,
                                h, attn, self.ao_ws, self.nh, self.nkv, self.D, self.bs, ao_chunk, self.ao_nc,
                                self.scale, fault=self.attn_fault)

@@ -305,49 +305,6 @@ def attn_oproj(q, k_cache, v_cache, block_table, seq_len, w_o, h, attn_out, ws, 
                          ATTN_OPROJ_MODE if mode < 0 else mode, _p(stamps), _s(h))
 
 
-SPLIT_OPROJ_ATTN_BLOCKS = 128  # split-role launch: attention blocks (over the kv heads); the rest of 256 are o_proj
-
-
-def split_oproj_nca(H: int, nh: int, nkv: int, D: int) -> int:
-    """Attention blocks per kv head of the split-role attention + o_proj launch for this shape
-    (``attn_split_oproj``), or 0 when the kernel library does not cover it."""
-    nca = max(1, SPLIT_OPROJ_ATTN_BLOCKS // max(1, nkv))
-    return nca if kernels().attn_split_oproj_check(H, nh, nkv, D, nca) == 0 else 0
-
-
-def split_oproj_workspace(nh: int, D: int, device):
-    """(handoff, octr) of ``attn_split_oproj``: the merged heads' output granules u32 [nh D] and
-    the o_proj blocks' {exit count, epoch} int32 [16], zeroed once (the attention part / counters
-    come from ``decode_attn_workspace``)."""
-    dev = torch.device(device)
-    return (torch.zeros(nh * D, dtype=torch.int32, device=dev), torch.zeros(16, dtype=torch.int32, device=dev))
-
-
-def attn_split_oproj(q, k_cache, v_cache, block_table, seq_len, w_o, h, attn_out, part, counters, ws, nh, nkv, D, bs,
-                     nca, scale, fault: Optional[torch.Tensor] = None, min_chunk: int = 128, car=None) -> None:
-    """Decode attention of ONE row + o_proj + residual in one launch with split roles
-    (csrc/kernels/attn_decode.hip ``attn_split_oproj_kernel``): ``h[0] += w_o @ attention(q[0])``;
-    ``attn_out[0]`` gets the attention output. ``part`` / ``counters`` = ``decode_attn_workspace``
-    (max_chunks >= nca), ``ws`` = ``split_oproj_workspace``, ``nca`` = ``split_oproj_nca``.
-    ``car`` (a TP rank): the group's fused-all-reduce buffer (``TPGroup.custom_fused``): the o_proj
-    rows are this rank's row-parallel partial, summed over the group inside the launch
-    (``h[0] = h[0] + sum over ranks of w_o_r @ attention_r``)."""
-    H = h.shape[-1]
-    if not q.is_cuda:
-        a = oracle.attn_decode(q[:1], k_cache, v_cache, block_table[:1], seq_len[:1], nh, nkv, D, bs, scale)
-        attn_out[:1].copy_(a)
-        oracle.linear(attn_out[:1], w_o, EPI_RESADD, h[:1])
-        return
-    groups = counters.shape[-1] - 2
-    max_chunks = part.shape[2] - groups
-    handoff, octr = ws
-    bases, rank, world, cap = (car.bases, car.rank, car.world, car.cap) if car is not None else ([], 0, 1, 0)
-    kernels().attn_split_oproj(_p(q), _p(k_cache), _p(v_cache), _p(block_table), block_table.shape[-1], _p(seq_len),
-                               _p(part), _p(counters), _p(attn_out), _p(w_o), _p(h), _p(handoff), _p(octr), H, nh, nkv,
-                               D, bs, k_cache.shape[0], min_chunk, nca, max_chunks, float(scale), _p(fault), bases, rank,
-                               world, cap, _s(h))
-
-
 def attn_prefill(q, k_cache, v_cache, block_tables, q_start, q_lens, ctx_lens, out, max_qlen, nh, nkv, D, bs, scale):
     if not q.is_cuda:
         return oracle.attn_prefill(q, k_cache, v_cache, block_tables, q_start, q_lens, ctx_lens, nh, nkv, D, bs,

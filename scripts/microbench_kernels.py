@@ -133,29 +133,15 @@ def bench_attn_oproj(shapes=((32, 8, 128, 4096),), lens=(128, 1024, 2048, 2300, 
                                fault=fault1, mode=mode)
                 it[0] += 1
 
-            nca = ops.split_oproj_nca(H, nh, nkv, D)
-            if nca:
-                spart, sctr = ops.decode_attn_workspace(1, nh, nkv, D, nca, "cuda")
-                sws = ops.split_oproj_workspace(nh, D, "cuda")
-            fault2 = torch.zeros(1, dtype=torch.int32, device="cuda")
-
-            def split_roles():
-                kc, vc, bt, sl, q, out = cases[it[0] % copies]
-                ops.attn_split_oproj(q, kc, vc, bt, sl, wos[it[0] % copies], h, attn, spart, sctr, sws, nh, nkv, D, 64,
-                                     nca, sc, fault=fault2)
-                it[0] += 1
-
             n = copies * max(1, 48 // copies)
             t2 = timeit(two, iters=n)
             t1 = timeit(one, iters=n) if chunk else float("nan")
             t1l = timeit(lambda: one(1), iters=n) if chunk else float("nan")
-            ts = timeit(split_roles, iters=n) if nca else float("nan")
             torch.cuda.synchronize()
             print(f"attn+o nh={nh} nkv={nkv} D={D} H={H} L={L:5d} cap={cap}: two launches "
                   f"({'fused' if fused2 else 'split'} c{ch2} g{gc2} + o GEMV) {t2:6.2f} us | one launch "
-                  f"(nc {nc}, {chunk} keys/block) {t1:6.2f} us, late weights {t1l:6.2f} us | split roles "
-                  f"({nca} x {nkv} attention + {H // 32} o_proj blocks) {ts:6.2f} us | fault {int(fault.item())} / "
-                  f"{int(fault1.item())} / {int(fault2.item())}", flush=True)
+                  f"(nc {nc}, {chunk} keys/block) {t1:6.2f} us, late weights {t1l:6.2f} us | fault "
+                  f"{int(fault.item())} / {int(fault1.item())}", flush=True)
             del cases, wos
 
 

@@ -24,7 +24,6 @@ def _worker(rank, a, port, q):
     os.environ["LLMC_CU_MASK"] = f"{rank * per}-{(rank + 1) * per - 1}" if a.cu_mask else ""
     # ranks share the GPU: the fused all-reduce only runs when forced (each rank has its own CUs here)
     os.environ["LLMC_FUSED_AR"] = "force" if a.fused_ar else "0"
-    os.environ["LLMC_SPLIT_OPROJ"] = a.split_oproj
     import torch
     import torch.distributed as dist
 
@@ -82,7 +81,6 @@ def main():
     ap.add_argument("--reps", type=int, default=2)
     ap.add_argument("--fused-ar", type=int, default=1)
     ap.add_argument("--cu-mask", type=int, default=1, help="0: ranks time-share every CU")
-    ap.add_argument("--split-oproj", default="0", help="LLMC_SPLIT_OPROJ for the engines: 0 | long | all")
     a = ap.parse_args()
     with socket.socket() as s:
         s.bind(("127.0.0.1", 0))
@@ -101,7 +99,7 @@ def main():
             sys.exit(1)
     worst = max(r[3] for r in res)
     print(f"{a.model} shape TP={a.shape_tp} over {a.world} ranks (cu_mask={a.cu_mask}, custom={res[0][1]}, "
-          f"fused_ar={res[0][2]}, split_oproj={a.split_oproj}) ctx={a.ctx}: decode {worst:.3f} ms/token (ranks {[round(r[3], 3) for r in res]}), "
+          f"fused_ar={res[0][2]}) ctx={a.ctx}: decode {worst:.3f} ms/token (ranks {[round(r[3], 3) for r in res]}), "
           f"timed_out={any(r[4] for r in res)}", flush=True)
 
 

@@ -161,78 +161,3 @@ def test_engine_attn_oproj_matches_two_launch_step(cuda, name, plen, monkeypatch
     b = ee.generate_ids(prompt, 24, temperature=0.8, seed=7, stop_on_eos=False)
     assert a == b
     assert int(ea.attn_fault.item()) == 0
-
-
-@pytest.mark.parametrize("nh,nkv,D,H", [(32, 8, 128, 4096), (16, 2, 128, 2048), (32, 8, 64, 2048)])
-@pytest.mark.parametrize("L", [1, 100, 2048, 5000, 9400, 16384])
-def test_attn_split_oproj_vs_oracle(cuda, nh, nkv, D, H, L):
-    """Split-role attention + o_proj + residual (attention blocks and o_proj blocks in one grid,
-    hand-off by tagged granules) against the fp32 oracle, over three launches on one workspace
-    (head and o_proj epochs advance together) and then in a HIP graph while the length changes."""
-    bs = 64
-    nca = ops.split_oproj_nca(H, nh, nkv, D)
-    assert nca > 0
-    kc, vc, bt, sl, q, w_o, h0 = _case(max(L, 1), nh, nkv, D, H, bs, seed=L + nkv)
-    scale = 1 / math.sqrt(D)
-    part, ctr = ops.decode_attn_workspace(1, nh, nkv, D, nca, "cuda")
-    ws = ops.split_oproj_workspace(nh, D, "cuda")
-    fault = torch.zeros(1, dtype=torch.int32, device="cuda")
-    btd, sld = bt.cuda(), sl.cuda()
-    a_ref, h_ref = _reference(kc, vc, bt, sl, q, w_o, h0, nh, nkv, D, bs, scale)
-    for _ in range(3):
-        h = h0.clone()
-        attn = torch.zeros(1, nh * D, dtype=BF, device="cuda")
-        ops.attn_split_oproj(q, kc, vc, btd, sld, w_o, h, attn, part, ctr, ws, nh, nkv, D, bs, nca, scale, fault=fault)
-        torch.cuda.synchronize()
-        assert int(fault.item()) == 0
-        err = (h.float().cpu() - h_ref).abs().max().item()
-        assert err < 2e-2 * max(1.0, h_ref.abs().max().item()), err
-        aerr = (attn.float().cpu() - a_ref.float()).abs().max().item()
-        assert aerr < 2e-2 * max(1.0, a_ref.float().abs().max().item()), aerr
-    # captured once, replayed at other lengths of the same table
-    h = h0.clone()
-    attn = torch.zeros(1, nh * D, dtype=BF, device="cuda")
-    s = torch.cuda.Stream()
-    s.wait_stream(torch.cuda.current_stream())
-    g = torch.cuda.CUDAGraph()
-    with torch.cuda.graph(g, stream=s):
-        ops.attn_split_oproj(q, kc, vc, btd, sld, w_o, h, attn, part, ctr, ws, nh, nkv, D, bs, nca, scale, fault=fault)
-    for L2 in sorted({1, max(1, L // 3), L}):
-        sld.fill_(L2)
-        h.copy_(h0)
-        g.replay()
-        torch.cuda.synchronize()
-        _, hr = _reference(kc, vc, bt, torch.tensor([L2], dtype=torch.int32), q, w_o, h0, nh, nkv, D, bs, scale)
-        err = (h.float().cpu() - hr).abs().max().item()
-        assert err < 2e-2 * max(1.0, hr.abs().max().item()), (L2, err)
-    assert int(fault.item()) == 0
-
-
-@pytest.mark.parametrize("plen", [90, 1500, 5000])
-def test_engine_split_oproj_matches_two_launch_step(cuda, plen, monkeypatch):
-    """Engine level: teacher-forced decode logits with the split-role launch in every bucket
-    (LLMC_SPLIT_OPROJ=all) against the two-launch step on the same weights; graph == eager."""
-    from llm_consensus_amd.models.config import ModelConfig
-
-    # o_proj input of 2048 columns (16 heads x 128; the kernel takes 2048 or 4096), 4 kv heads
-    cfg = ModelConfig("llama-so-test", "llama", 2, 2048, 16, 4, 128, 2816, 32000, 500000.0, max_position=8192)
-    w = TransformerWeights(cfg, TPGroup.single(), torch.device("cuda:0"), seed=23)
-    ctx = plen + 64
-    es = Engine(cfg, EngineConfig(device="cuda:0", max_context=ctx, attn_oproj=False, split_oproj="all"), weights=w)
-    e2 = Engine(cfg, EngineConfig(device="cuda:0", max_context=ctx, attn_oproj=False, split_oproj="0"), weights=w)
-    assert es.so_nca > 0 and all(es.so_buckets) and not any(e2.so_buckets)
-    prompt = [(i * 7919) % (cfg.vocab - 300) + 256 for i in range(plen)]
-    n = 10
-    ts, ls = es.debug_decode_logits(prompt, n)
-    t2, l2 = e2.debug_decode_logits(prompt, n)
-    for i in range(n):
-        if ts[:i] != t2[:i]:
-            break
-        err = (ls[i] - l2[i]).abs().max().item()
-        assert err < 0.02 * max(1.0, l2[i].abs().max().item()), (i, err)
-    a = es.generate_ids(prompt, 24, temperature=0.8, seed=7, stop_on_eos=False)
-    ee = Engine(cfg, EngineConfig(device="cuda:0", max_context=ctx, attn_oproj=False, split_oproj="all",
-                                  use_graphs=False), weights=w)
-    b = ee.generate_ids(prompt, 24, temperature=0.8, seed=7, stop_on_eos=False)
-    assert a == b
-    assert int(es.attn_fault.item()) == 0

@@ -41,10 +41,7 @@ def _worker(rank, world, port, name, q, ekw=None):
         tp.enable_custom("cuda:0")
         if ekw.pop("_expect_fused", False):
             assert tp.custom_fused is not None
-        expect_so = ekw.pop("_expect_so", False)
         e = Engine(FAMILIES[name], EngineConfig(device="cuda:0", max_context=512, seed=5, **ekw), tp=tp)
-        if expect_so:
-            assert e.so_nca > 0 and all(e.so_buckets), (e.so_nca, e.so_buckets)
         e.warmup_graphs()
         s = e.new_sequence()
         e.prefill([s], [PROMPT])
@@ -79,19 +76,18 @@ def test_tp2_gpu_fused_rowparallel_allreduce_matches_tp1(cuda, monkeypatch):
     _tp2_vs_tp1("llama-small", {"_expect_fused": True})
 
 
-def test_tp2_gpu_split_oproj_fused_allreduce_matches_tp1(cuda, monkeypatch):
-    """The split-role attention + o_proj launch on TP ranks, its o_proj blocks all-reducing their
-    rows in the same launch (every bucket), the two ranks on separate halves of the chip."""
+def test_tp2_gpu_fused_allreduce_cu_partitioned_matches_tp1(cuda, monkeypatch):
+    """The fused row-parallel all-reduce with each rank's engine streams on its own half of the
+    chip (EngineConfig.cu_mask via LLMC_CU_MASK, as scripts/tp_rehearsal.py runs a TP group)."""
     monkeypatch.setenv("LLMC_FUSED_AR", "force")
-    monkeypatch.setenv("LLMC_SPLIT_OPROJ", "all")
-    _tp2_vs_tp1("llama-small", {"_expect_fused": True, "_cu_split": True, "_expect_so": True})
+    _tp2_vs_tp1("llama-small", {"_expect_fused": True, "_cu_split": True})
 
 
 def _tp2_vs_tp1(name, ekw):
     from llm_consensus_amd.engine import Engine, EngineConfig
     from llm_consensus_amd.models.config import FAMILIES
 
-    ref = Engine(FAMILIES[name], EngineConfig(device="cuda:0", max_context=512, seed=5, split_oproj="0"))
+    ref = Engine(FAMILIES[name], EngineConfig(device="cuda:0", max_context=512, seed=5))
     s = ref.new_sequence()
     ref.prefill([s], [PROMPT])
     ref_logits = ref.full_logits(s).float().cpu()
@@ -122,7 +118,7 @@ def _tp2_vs_tp1(name, ekw):
             break
         agree += 1
     if agree < 8:
-        ref = Engine(FAMILIES[name], EngineConfig(device="cuda:0", max_context=512, seed=5, split_oproj="0"))
+        ref = Engine(FAMILIES[name], EngineConfig(device="cuda:0", max_context=512, seed=5))
         s = ref.new_sequence()
         ref.prefill([s], [PROMPT + gen[:agree]])
         lt = ref.full_logits(s).float().cpu()

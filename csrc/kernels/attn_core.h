@@ -13,6 +13,11 @@ typedef __attribute__((address_space(3))) s16x4m lds_s16x4m;
 constexpr float kNegInfM = -1e30f;
 constexpr int kVRowBytes = 256;              // LDS pitch of one V row (D <= 128)
 constexpr unsigned kSpinLimit = 1u << 22;    // polls before a merger gives up (never in practice)
+// Decode-attention counters: every word (top ticket, epoch, group tickets) of a (row, kv head) on
+// its own 128-B line. Returning atomics on one line serialise (MI355X_MICROARCH.md dequeue / fanin:
+// ~11-13 ns each), and with the words of all kv heads packed in one line every block of the grid
+// (256-512) queued its ticket behind the others'.
+constexpr int kCtrPitch = 32;  // int32 words per counter line
 
 __device__ __forceinline__ int vswz(int row, int chunk) { return row * kVRowBytes + ((chunk ^ ((row & 7) << 1)) << 4); }
 
@@ -331,7 +336,8 @@ __device__ __forceinline__ void merge_rows(__amdgpu_buffer_rsrc_t rsrc, const ch
 // result is published as one more granule row (slab row max_chunks + group) and the last group
 // merger merges those (two levels: a 256-block split merges 16 rows twice instead of 256 rows in
 // one block). The last merger re-arms the tickets it took and advances the epoch (every block of
-// this launch read the epoch before it arrived). ctr = {top ticket, epoch, group tickets...};
+// this launch read the epoch before it arrived). ctr = {top ticket, epoch, group tickets...}, one
+// kCtrPitch line each;
 // `flag` is one LDS word. Every block but the last returns inside.
 template <int G, int D, int NW, bool SC1OUT = false>
 __device__ __forceinline__ bool publish_and_merge(const float* red, float* part, int* ctr, int b, int nkv, int kvh,
@@ -347,7 +353,7 @@ __device__ __forceinline__ bool publish_and_merge(const float* red, float* part,
   publish_partial<G, D, NW>(red, rsrc, c, tag, tid);
   const int grp = c / gsize, ngroups = (nchunks + gsize - 1) / gsize;
   const int g0 = grp * gsize, gn = min(gsize, nchunks - g0);
-  int* gctr = ngroups == 1 ? ctr : ctr + 2 + grp;
+  int* gctr = ngroups == 1 ? ctr : ctr + (2 + grp) * kCtrPitch;
   __syncthreads();  // every wave's stores are issued (not drained: the merger checks tags)
   if (tid == 0) *flag = __hip_atomic_fetch_add(gctr, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == gn - 1;
   __syncthreads();
@@ -390,7 +396,7 @@ __device__ __forceinline__ bool publish_and_merge(const float* red, float* part,
   }
   if (tid == 0) {
     __hip_atomic_store(ctr, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);                          // re-arm
-    __hip_atomic_store(ctr + 1, static_cast<int>(tag), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // epoch
+    __hip_atomic_store(ctr + kCtrPitch, static_cast<int>(tag), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // epoch
   }
   return true;
 }

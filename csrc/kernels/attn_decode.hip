@@ -50,8 +50,8 @@ __device__ __forceinline__ void attn_split_block(
   static_assert(G <= 16 && D % 32 == 0 && D <= 128, "shape");
   using ST = SubTile<G, D>;
   constexpr int NT = NW * 64;
-  int* ctr = counters + (b * nkv + kvh) * (2 + max_groups);  // {ticket, epoch, group tickets}
-  const uint32_t tag = static_cast<uint32_t>(__hip_atomic_load(ctr + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) + 1u;
+  int* ctr = counters + (b * nkv + kvh) * (2 + max_groups) * kCtrPitch;  // {ticket, epoch, group tickets}
+  const uint32_t tag = static_cast<uint32_t>(__hip_atomic_load(ctr + kCtrPitch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) + 1u;
   const int L = seq_lens[b];
   const int nchunks = decode_nsplit(L, gridc, -min_chunk);
   if (c >= nchunks) return;
@@ -138,8 +138,8 @@ __global__ __launch_bounds__(256) void attn_decode_fused_kernel(
   const int pidx = __builtin_amdgcn_readfirstlane(min(key0 / bs, bt_stride - 1));
   const int page = min(max(ld_scalar(bt + pidx), 0), nblocks - 1);  // clamped into the cache
   const int L = ld_scalar(seq_lens + b);
-  int* ctr = counters + (b * nkv + kvh) * (2 + max_groups);  // {ticket, epoch, group tickets}
-  const uint32_t tag = static_cast<uint32_t>(__hip_atomic_load(ctr + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) + 1u;
+  int* ctr = counters + (b * nkv + kvh) * (2 + max_groups) * kCtrPitch;  // {ticket, epoch, group tickets}
+  const uint32_t tag = static_cast<uint32_t>(__hip_atomic_load(ctr + kCtrPitch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) + 1u;
   ST st;
   st.init(q + static_cast<int64_t>(b) * q_stride + kvh * G * D, lane);
   if (c * chunk >= L) return;  // block-uniform
@@ -255,7 +255,8 @@ using namespace llmc;
 
 // Attention of one decode step for rows 0..B-1, one launch.
 // part: f32 [B, nkv, max_chunks + max_groups, G, D + 4] partial granules (zeroed once); counters:
-// int32 [B, nkv, 2 + max_groups] {top ticket, epoch, group tickets} (zeroed once; the kernel re-arms
+// int32 [B, nkv, 2 + max_groups, kCtrPitch] {top ticket, epoch, group tickets}, one 128-B line per
+// word (zeroed once; the kernel re-arms
 // the tickets and advances the epoch); max_groups = attn_decode_groups(max_chunks).
 // fused = 1 (short contexts): grid_chunks fixed chunk-key blocks (chunk 128 or 256; bs % (chunk/4) == 0).
 // fused = 0 (long contexts): balanced split over <= grid_chunks blocks of >= chunk keys (multiple of 128).

@@ -196,18 +196,22 @@ FUSED_ATTN_MAX_KEYS = 4096  # decode attention: fused single-launch form up to t
 FUSED_CHUNK = 128           # keys per block of the fused form
 
 
+ATTN_CTR_PITCH = 32  # int32 words per decode-attention counter line (attn_core.h kCtrPitch)
+
+
 def decode_attn_workspace(B, nh, nkv, D, max_chunks, device, fused: bool = False):
     """(part, counters) for attn_decode, either form: partial granules f32 [B, nkv, max_chunks +
     groups, G, D + 4] (bf16 {value pair, tag} granules merged in-launch; the extra rows hold the
     group results of a two-level merge) and the per-(row, kv head) {top ticket, epoch, group
-    tickets} int32 [B, nkv, 2 + groups], both zeroed once and never reset (the kernel re-arms the
+    tickets} int32 [B, nkv, 2 + groups, ATTN_CTR_PITCH] (one 128-B line per word: returning atomics
+    on one line serialise), both zeroed once and never reset (the kernel re-arms the
     tickets and advances the epochs). ``groups`` comes from the kernel library
     (``llmc_attn_decode_groups``). ``fused`` is accepted for call-site symmetry."""
     G = nh // nkv
     dev = torch.device(device)
     groups = kernels().attn_decode_groups(max_chunks) if dev.type == "cuda" else 0  # CPU: oracle path
     part = torch.zeros(B, nkv, max_chunks + groups, G, D + 4, dtype=torch.float32, device=dev)
-    counters = torch.zeros(B, nkv, 2 + groups, dtype=torch.int32, device=dev)
+    counters = torch.zeros(B, nkv, 2 + groups, ATTN_CTR_PITCH, dtype=torch.int32, device=dev)
     return part, counters
 
 
@@ -223,10 +227,10 @@ def attn_decode(q, k_cache, v_cache, block_tables, seq_lens, out, part, counters
         out.copy_(oracle.attn_decode(q, k_cache, v_cache, block_tables, seq_lens, nh, nkv, D, bs, scale))
         return out
     B = q.shape[0]
-    groups = counters.shape[-1] - 2
+    groups = counters.shape[-2] - 2
     max_chunks = part.shape[2] - groups
     gc = max_chunks if grid_chunks is None else min(grid_chunks, max_chunks)
-    if (part.shape[-1] != D + 4 or counters.shape[0] < B or groups < 0
+    if (part.shape[-1] != D + 4 or counters.shape[0] < B or groups < 0 or counters.shape[-1] != ATTN_CTR_PITCH
             or kernels().attn_decode_groups(max_chunks) != groups):
         raise ValueError("attn_decode: workspace does not match (use decode_attn_workspace)")
     kernels().attn_decode(_p(q), q.stride(0), _p(k_cache), _p(v_cache), _p(block_tables), block_tables.stride(0),

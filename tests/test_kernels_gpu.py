@@ -320,7 +320,8 @@ def test_attn_decode_fused(cuda, nh, nkv, D, lens, chunk):
         close(out, ref, 2e-2)
     # tickets re-armed, epochs advanced once per launch where a merge ran
     epochs = torch.tensor([3 if n > chunk else 0 for n in lens], dtype=torch.int32).view(-1, 1).expand(B, nkv)
-    assert int(ctr[..., 0].abs().sum()) == 0 and torch.equal(ctr[..., 1].cpu(), epochs), ctr
+    assert int(ctr[..., 0, 0].abs().sum()) == 0 and torch.equal(ctr[..., 1, 0].cpu(), epochs), ctr
+    assert int(ctr[..., 1:].abs().sum()) == 0  # one word per 128-B counter line
 
 
 @pytest.mark.parametrize("nh,nkv,D", [(32, 8, 128), (32, 32, 96), (16, 2, 128)])
@@ -368,7 +369,7 @@ def test_attn_decode_fused_long_context(cuda, nh, nkv, chunk, cap):
         ops.attn_decode(q, kc, vc, bt.cuda(), sl.cuda(), out, part, ctr, nh, nkv, D, bs, chunk, scale,
                         grid_chunks=gc, fused=True)
         close(out, ref, 2e-2)
-    tickets = torch.cat([ctr[..., :1], ctr[..., 2:]], dim=-1)
+    tickets = torch.cat([ctr[..., :1, 0], ctr[..., 2:, 0]], dim=-1)
     assert int(tickets.abs().sum()) == 0, ctr
 
 
@@ -393,7 +394,7 @@ def test_attn_decode_wide_split(cuda, nh, nkv, gc):
         out.zero_()
         ops.attn_decode(q, kc, vc, bt.cuda(), sl.cuda(), out, part, ctr, nh, nkv, D, bs, 128, scale, grid_chunks=gc)
         close(out, ref, 2e-2)
-    tickets = torch.cat([ctr[..., :1], ctr[..., 2:]], dim=-1)
+    tickets = torch.cat([ctr[..., :1, 0], ctr[..., 2:, 0]], dim=-1)
     assert int(tickets.abs().sum()) == 0, ctr
 
 

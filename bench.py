@@ -156,15 +156,24 @@ def make_plan(args, world: int):
         # pile onto the first GPUs (N=2: GPU 0 decoding two models, GPU 1 one, the round waiting
         # on GPU 0), so each leftover responder is tensor-parallel over an equal share of the GPUs
         # instead: every GPU then streams the same bytes per step
-        whole = n - n % world if world > 1 else n
-        rest = n - whole
-        tp = world // rest if rest else 1
-        if rest and (world % rest or judge_tp_degree(FAMILIES[rf], tp, 0) != tp):
-            whole, rest = n, 0  # no even sharding: round-robin all of them
-        resp = [{"name": f"{args.model}@{i}", "family": rf, "ranks": [i % world], "seed": 1000 + i}
-                for i in range(whole)]
-        resp += [{"name": f"{args.model}@{whole + j}", "family": rf, "ranks": list(range(j * tp, (j + 1) * tp)),
-                  "seed": 1000 + whole + j} for j in range(rest)]
+        rt = args.resp_tp if world > 1 else 1
+        if rt > 1 and world % rt == 0 and (n * rt) % world == 0 and judge_tp_degree(FAMILIES[rf], rt, 0) == rt:
+            # --resp-tp t: every responder tensor-parallel over t consecutive GPUs, the groups
+            # cycling over the N / t GPU groups, so each GPU hosts n t / N shards at once (N=8, t=2:
+            # two half-models per GPU instead of one whole model)
+            ng = world // rt
+            resp = [{"name": f"{args.model}@{i}", "family": rf, "ranks": list(range((i % ng) * rt, (i % ng + 1) * rt)),
+                     "seed": 1000 + i} for i in range(n)]
+        else:
+            whole = n - n % world if world > 1 else n
+            rest = n - whole
+            tp = world // rest if rest else 1
+            if rest and (world % rest or judge_tp_degree(FAMILIES[rf], tp, 0) != tp):
+                whole, rest = n, 0  # no even sharding: round-robin all of them
+            resp = [{"name": f"{args.model}@{i}", "family": rf, "ranks": [i % world], "seed": 1000 + i}
+                    for i in range(whole)]
+            resp += [{"name": f"{args.model}@{whole + j}", "family": rf, "ranks": list(range(j * tp, (j + 1) * tp)),
+                      "seed": 1000 + whole + j} for j in range(rest)]
         jf = fam(args.judge)
         jtp = judge_tp_degree(FAMILIES[jf], world, args.judge_tp)
         if jtp == 1:
@@ -467,6 +476,9 @@ def main() -> None:
     ap.add_argument("--prompt-tokens", type=int, default=128)
     ap.add_argument("--temperature", type=float, default=1.0)
     ap.add_argument("--judge-tp", type=int, default=0, help="0 = auto (config 5: 4)")
+    ap.add_argument("--resp-tp", type=int, default=1,
+                    help="fanout, N > 1: every responder tensor-parallel over this many GPUs (1 = whole models "
+                         "round-robin); ignored when it does not shard evenly")
     ap.add_argument("--shared-weights", action="store_true",
                     help="fanout secondary preset: the replicas placed whole on one GPU share ONE weight copy and "
                          "decode as rows of one engine (config.name says so; never the default)")

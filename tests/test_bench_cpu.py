@@ -81,6 +81,14 @@ def test_fanout_eight_ranks_like_the_scale_run():
     _tokens_ok(d, 12)
 
 
+def test_fanout_responders_tensor_parallel_pairs():
+    """--resp-tp 2 on 4 gloo ranks: four TP=2 responders, two per rank pair, and the TP=4 judge."""
+    d = _run(4, ["--shapes", "tiny", "--steps", "1", "--warmup", "0", "--max-tokens", "12", "--resp-tp", "2"], 29695)
+    assert d["config"]["global_batch"] == 4
+    assert "4x llama-tiny TP=2 responders" in d["config"]["model"]
+    _tokens_ok(d, 12)
+
+
 def test_fanout_two_ranks_balances_the_third_responder():
     """N=2: two whole responders (one per rank) and the third tensor-parallel over both ranks, so
     both GPUs stream the same bytes per step; the judge is TP=2."""
@@ -180,7 +188,8 @@ def test_config_names_are_honest():
 
     def plan(n, **kw):
         a = argparse.Namespace(config="fanout", shapes="full", model="llama-3-8b", judge="llama-3-8b",
-                               n_models=kw.get("n_models", 0), judge_tp=kw.get("judge_tp", 0))
+                               n_models=kw.get("n_models", 0), judge_tp=kw.get("judge_tp", 0),
+                               resp_tp=kw.get("resp_tp", 1))
         r, j, _ = bench.make_plan(a, n)
         return bench.config_name(a, n, r, j), r, j
 

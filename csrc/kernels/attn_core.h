@@ -18,6 +18,9 @@ constexpr unsigned kSpinLimit = 1u << 22;    // polls before a merger gives up (
 // ~11-13 ns each), and with the words of all kv heads packed in one line every block of the grid
 // (256-512) queued its ticket behind the others'.
 constexpr int kCtrPitch = 32;  // int32 words per counter line
+// Chunk partials are merged in one level up to kAttnOneLevel chunks, else in groups of kAttnGroup
+// (one-level merges of 64 rows measured 1.3-1.5x slower)
+constexpr int kAttnOneLevel = 32, kAttnGroup = 16;
 
 __device__ __forceinline__ int vswz(int row, int chunk) { return row * kVRowBytes + ((chunk ^ ((row & 7) << 1)) << 4); }
 

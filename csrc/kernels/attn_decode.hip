@@ -263,7 +263,6 @@ using namespace llmc;
 // Chunk partials are merged in one level up to kAttnOneLevel chunks, else in groups of kAttnGroup.
 // fault (nullable int32): set to 1 when a merger gave up waiting for a partial (bounded spin): the
 // step's attention output is then invalid and the caller must fail the request.
-constexpr int kAttnOneLevel = 32, kAttnGroup = 16;  // one-level merges of 64 rows measured 1.3-1.5x slower
 
 extern "C" int llmc_attn_decode_groups(int max_chunks) {
   return max_chunks > kAttnOneLevel ? (max_chunks + kAttnGroup - 1) / kAttnGroup : 0;

@@ -29,6 +29,10 @@ int llmc_gemm_t128(const void*, int, const void*, int, void*, int, int, int, int
 int llmc_rope_kv_write(const void*, int, void*, int, const void*, const void*, const void*, void*, void*, const void*,
                        int, int, int, int, int, hipStream_t);
 int llmc_attn_decode_groups(int);
+int llmc_qkv_attn_check(int, int, int, int);
+int llmc_qkv_attn(const void*, const void*, float, const void*, int, void*, void*, void*, const void*, const void*,
+                  const void*, const void*, const void*, int, const void*, void*, void*, void*, int, int, int, int, int,
+                  int, int, int, float, void*, void*, void*, hipStream_t);
 int llmc_attn_oproj_check(int, int, int, int, int, int);
 int llmc_attn_oproj(const void*, const void*, const void*, const void*, int, const void*, const void*, void*, void*,
                     void*, void*, void*, void*, void*, int, int, int, int, int, int, int, int, float, int, void*,
@@ -120,6 +124,16 @@ PYBIND11_MODULE(_llmc_hip, m) {
           "rope_kv_write");
   });
   m.def("attn_decode_groups", [](int max_chunks) { return llmc_attn_decode_groups(max_chunks); });
+  m.def("qkv_attn_check", [](int nh, int nkv, int D, int K) { return llmc_qkv_attn_check(nh, nkv, D, K); });
+  m.def("qkv_attn", [](ptr x, ptr nw, float eps, ptr W, int K, ptr qo, ptr kc, ptr vc, ptr pos, ptr slots, ptr cos_t,
+                       ptr sin_t, ptr bt, int bt_len, ptr sl, ptr part, ptr ctr, ptr out, int nh, int nkv, int D, int bs,
+                       int nblocks, int chunk, int gc, int max_chunks, float scale, ptr fault, ptr gran, ptr hctr,
+                       ptr s) {
+    check(llmc_qkv_attn(P(x), P(nw), eps, P(W), K, P(qo), P(kc), P(vc), P(pos), P(slots), P(cos_t), P(sin_t), P(bt),
+                        bt_len, P(sl), P(part), P(ctr), P(out), nh, nkv, D, bs, nblocks, chunk, gc, max_chunks, scale,
+                        P(fault), P(gran), P(hctr), S(s)),
+          "qkv_attn");
+  });
   m.def("attn_oproj_check", [](int H, int nh, int nkv, int D, int nc, int K_o) {
     return llmc_attn_oproj_check(H, nh, nkv, D, nc, K_o);
   });

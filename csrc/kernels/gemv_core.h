@@ -50,6 +50,12 @@ struct RopeEpi {
   const float* cos_t;       // [max_pos][D/2]
   const float* sin_t;
   int nh, nkv, D, bs;
+  // optional (qkv_attn.hip): every rotated q / k pair and v pair also published as an 8-B
+  // {bf16x2, gtag} granule for the attention blocks of the same launch: q head h pair i at
+  // [h][i] = dims (i, i + D/2); k head j at [nh + j][i], same dims; v head j at [nh + nkv + j][d/2]
+  // = dims (d, d + 1); D/2 granules per head
+  uint64_t* granules;
+  uint32_t gtag;
 };
 
 // Batched decode (3 <= M <= 32 rows): the MFMA form in gemv_mfma.hip, same prologue/epilogues
@@ -59,41 +65,42 @@ constexpr int kGemvMaxM = 2, kGemvmMaxM = 32, kMoeGemvmMaxTokens = 16;
 int gemvm_dispatch(int M, const void* x, int x_stride, const void* norm_w, float eps, const void* W, void* out,
                    int out_stride, int N, int K, int epi, const RopeEpi& rope, hipStream_t st, int form = 0);
 
+// One block of the GEMV (block (bx, by) of its grid; smem = the block's dynamic LDS): the body of
+// gemv_kernel, also the projection role of fused launches (qkv_attn.hip).
 template <int M, int NT, int RPW, int UNROLL, int PRO, int EPI, bool EXPERT = false>
-__global__ __launch_bounds__(NT) void gemv_kernel(const bf16_t* __restrict__ x, int x_stride,
-                                                  const bf16_t* __restrict__ norm_w, float eps,
-                                                  const bf16_t* __restrict__ W, void* __restrict__ out,
-                                                  int out_stride, int N, int K, const int32_t* __restrict__ expert_ids,
-                                                  int x_div, RopeEpi rope, CarArgs ar) {
+__device__ __forceinline__ void gemv_block(const int bx, const int by, char* smem, const bf16_t* __restrict__ x,
+                                           int x_stride, const bf16_t* __restrict__ norm_w, float eps,
+                                           const bf16_t* __restrict__ W, void* __restrict__ out, int out_stride, int N,
+                                           int K, const int32_t* __restrict__ expert_ids, int x_div, const RopeEpi& rope,
+                                           const CarArgs& ar) {
   constexpr int WAVES = NT / kWave;
   constexpr bool PAIR_LDS = (EPI == EPI_SILU || EPI == EPI_ROPE) && RPW == 1;  // host: N % (2 * WAVES) == 0
-  // EXPERT (MoE decode): blockIdx.y = (token, slot) pair; weights of expert expert_ids[pair],
+  // EXPERT (MoE decode): by = (token, slot) pair; weights of expert expert_ids[pair],
   // input row pair / x_div, output row pair (M must be 1).
   // EPI_COMBINE (MoE decode down projection fused with the combine; EXPERT, M == RPW == top-k):
-  // blockIdx.y = token t; wave row n streams row n of each of the token's k experts ("rows" r =
+  // by = token t; wave row n streams row n of each of the token's k experts ("rows" r =
   // slots), x row r = the slot's activation; acc[r][r] is that expert's output and the epilogue
   // does h[t][n] += sum_r w[t][r] * acc[r][r] in a fixed order (replaces moe_combine's launch and
   // the y round trip). x_div carries nothing here; the router weights come in through `rope.cos_t`.
   constexpr bool COMBINE = EPI == EPI_COMBINE;
   static_assert(!COMBINE || (EXPERT && M == RPW), "combine: one x row per expert slot");
   if constexpr (EXPERT && !COMBINE) {
-    const int pair = blockIdx.y;
+    const int pair = by;
     if (expert_ids[pair] < 0) return;  // another rank's expert (expert parallel): whole block exits
     W += static_cast<int64_t>(expert_ids[pair]) * N * K;
     x += static_cast<int64_t>(pair / x_div) * x_stride;
     out = reinterpret_cast<char*>(out) + static_cast<int64_t>(pair) * out_stride * (EPI == EPI_F32 ? 4 : 2);
   }
   if constexpr (COMBINE) {
-    const int t = blockIdx.y;
+    const int t = by;
     x += static_cast<int64_t>(t) * RPW * x_stride;
     out = reinterpret_cast<char*>(out) + static_cast<int64_t>(t) * out_stride * 2;
   }
-  extern __shared__ __attribute__((aligned(16))) char smem[];
   bf16_t* xs = reinterpret_cast<bf16_t*>(smem);  // [M][K]
   const int tid = threadIdx.x;
   const int nchunk = K / 8;
   const int wave = tid / kWave, lane = tid % kWave;
-  const int row0 = COMBINE ? blockIdx.x * WAVES + wave : (blockIdx.x * WAVES + wave) * RPW;
+  const int row0 = COMBINE ? bx * WAVES + wave : (bx * WAVES + wave) * RPW;
 
   // Weight rows (clamped: waves past N still load a valid row and discard it, so no lane
   // diverges before the block barrier). The first UNROLL-batch of W is issued BEFORE the x
@@ -103,7 +110,7 @@ __global__ __launch_bounds__(NT) void gemv_kernel(const bf16_t* __restrict__ x, 
 #pragma unroll
   for (int r = 0; r < RPW; ++r) {
     if constexpr (COMBINE) {
-      const int e = expert_ids[blockIdx.y * RPW + r];
+      const int e = expert_ids[by * RPW + r];
       wrow[r] = reinterpret_cast<const u32x4*>(W + (static_cast<int64_t>(e) * N + min(row0, N - 1)) * K);
     } else {
       const int n = min(row0 + r, N - 1);
@@ -153,7 +160,7 @@ __global__ __launch_bounds__(NT) void gemv_kernel(const bf16_t* __restrict__ x, 
   if constexpr (EPI == EPI_AR) {
     static_assert(RPW == 1 && M <= 2 && M * WAVES / 2 <= kArGranulesPerBlock, "EPI_AR geometry");
     if (tid == 0)
-      ar_epoch = __hip_atomic_load(car_ctr(ar.P.base[ar.rank]) + blockIdx.x, __ATOMIC_RELAXED,
+      ar_epoch = __hip_atomic_load(car_ctr(ar.P.base[ar.rank]) + bx, __ATOMIC_RELAXED,
                                    __HIP_MEMORY_SCOPE_SYSTEM) + 1;
 #pragma unroll
     for (int m = 0; m < M; ++m)
@@ -287,7 +294,7 @@ __global__ __launch_bounds__(NT) void gemv_kernel(const bf16_t* __restrict__ x, 
   if (!PAIR_LDS && EPI != EPI_AR && row0 >= N) return;  // PAIR_LDS / EPI_AR: every wave reaches the barriers
   if constexpr (PAIR_LDS && EPI == EPI_ROPE) {
     const int w_u = __builtin_amdgcn_readfirstlane(wave);
-    const int r_u = (blockIdx.x * WAVES + w_u) * RPW;
+    const int r_u = (bx * WAVES + w_u) * RPW;
     const int D = rope.D, half = D / 2;
     const bool qk = r_u / D < rope.nh + rope.nkv;
     const int i = (r_u % D) / 2;
@@ -389,11 +396,21 @@ __global__ __launch_bounds__(NT) void gemv_kernel(const bf16_t* __restrict__ x, 
           ko[i] = f32_to_bf16(o1);
           ko[i + half] = f32_to_bf16(o2);
         }
-      } else if (slot >= 0) {  // V rows keep canonical order
+        if (rope.granules != nullptr)  // one row (M == 1): rows are heads x D
+          __hip_atomic_store(rope.granules + head * half + i,
+                             static_cast<uint64_t>(pack_bf16x2(o1, o2)) | (static_cast<uint64_t>(rope.gtag) << 32),
+                             __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      } else {  // V rows keep canonical order
         const int vh = head - rope.nh - rope.nkv, d = n % D;
-        bf16_t* vv = rope.v_cache + ((page * rope.nkv + vh) * rope.bs + off) * D;
-        vv[d] = f32_to_bf16(v);
-        vv[d + 1] = f32_to_bf16(x2);
+        if (slot >= 0) {
+          bf16_t* vv = rope.v_cache + ((page * rope.nkv + vh) * rope.bs + off) * D;
+          vv[d] = f32_to_bf16(v);
+          vv[d + 1] = f32_to_bf16(x2);
+        }
+        if (rope.granules != nullptr)
+          __hip_atomic_store(rope.granules + head * half + d / 2,
+                             static_cast<uint64_t>(pack_bf16x2(v, x2)) | (static_cast<uint64_t>(rope.gtag) << 32),
+                             __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       }
     }
   };
@@ -428,9 +445,9 @@ __global__ __launch_bounds__(NT) void gemv_kernel(const bf16_t* __restrict__ x, 
     __syncthreads();
     if (wave != 0) return;
     const uint32_t epoch = __shfl(ar_epoch, 0, 64);
-    const int rb = blockIdx.x * WAVES;
+    const int rb = bx * WAVES;
     const int pairs = max(0, min(WAVES, N - rb)) / 2;  // N even: a pair is whole or absent
-    const long gbase = static_cast<long>(blockIdx.x) * kArGranulesPerBlock;
+    const long gbase = static_cast<long>(bx) * kArGranulesPerBlock;
     auto payload = [&](int gi) {  // my bf16 pair of granule gi (rows 2j, 2j + 1 of token m)
       const int m = gi / HP, j = gi % HP;
       return pack_bf16x2(rowv[m * WAVES + 2 * j], rowv[m * WAVES + 2 * j + 1]);
@@ -458,12 +475,12 @@ __global__ __launch_bounds__(NT) void gemv_kernel(const bf16_t* __restrict__ x, 
           pack_bf16x2(lo, hi);
     }
     if (lane == 0)
-      __hip_atomic_store(car_ctr(ar.P.base[ar.rank]) + blockIdx.x, epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      __hip_atomic_store(car_ctr(ar.P.base[ar.rank]) + bx, epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     return;
   }
   if constexpr (COMBINE) {
     if (lane == 0 && row0 < N) {
-      const float* wt = rope.cos_t + blockIdx.y * RPW;  // router weights [T, k]
+      const float* wt = rope.cos_t + by * RPW;  // router weights [T, k]
       bf16_t* h = reinterpret_cast<bf16_t*>(out) + row0;
       float v = bf16_to_f32(*h);
 #pragma unroll
@@ -498,6 +515,17 @@ __global__ __launch_bounds__(NT) void gemv_kernel(const bf16_t* __restrict__ x, 
       }
     }
   }
+}
+
+template <int M, int NT, int RPW, int UNROLL, int PRO, int EPI, bool EXPERT = false>
+__global__ __launch_bounds__(NT) void gemv_kernel(const bf16_t* __restrict__ x, int x_stride,
+                                                  const bf16_t* __restrict__ norm_w, float eps,
+                                                  const bf16_t* __restrict__ W, void* __restrict__ out,
+                                                  int out_stride, int N, int K, const int32_t* __restrict__ expert_ids,
+                                                  int x_div, RopeEpi rope, CarArgs ar) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  gemv_block<M, NT, RPW, UNROLL, PRO, EPI, EXPERT>(blockIdx.x, blockIdx.y, smem, x, x_stride, norm_w, eps, W, out,
+                                                   out_stride, N, K, expert_ids, x_div, rope, ar);
 }
 
 }  // namespace llmc

@@ -1,0 +1,244 @@
+// qkv projection (+ RMSNorm prologue, RoPE / paged-KV-write epilogue) AND the decode attention of
+// the same token in ONE launch, for one-row engines whose qkv output is short (N < 2048: the
+// tensor-parallel ranks' shards, 1-2 kv heads). Host: llmc_qkv_attn.
+//
+// Why (profiles/r4_tp8_shard_kernel_stats.md, a Llama-3-8B TP=8 rank at 2k keys): the qkv GEMV
+// (4.8 us) and the attention (9.0 us for ~1 MB of K/V) are both latency chains; as two launches
+// the attention's own round trips (length and page id, then the K/V stream) start only after the
+// GEMV's boundary. Here they run under the GEMV: the K/V of the cached keys do not depend on this
+// token, so the attention blocks request them at once and only wait for the rotated q.
+//
+// Grid: blocks [0, Nq) are the GEMV (gemv_core.h gemv_block: 4 waves x 1 row, 8 x 16-B loads per
+// lane in flight, the engine's geometry for N < 2048, so the projection is the same arithmetic as
+// the qkv_rope launch); blocks [Nq, Nq + gc * nkv) are the fused-form attention chunks (attn_core.h
+// SubTile, 4 waves x 32 / 64 keys of one page). Attention blocks only wait on GEMV blocks, which
+// have lower indices and are dispatched first: no wait is on a block that has not started.
+//
+// Hand-off: the GEMV epilogue publishes every rotated q / k pair and v pair as an 8-B {bf16x2, tag}
+// granule (RopeEpi::granules: one single-copy-atomic write-through store, the data IS the flag,
+// MI355X_MICROARCH.md handoff-1to1). An attention block requests its K/V (keys < L - 1: already
+// in the cache), then gathers its kv head's q granules into LDS, polling tags; the block holding
+// key L - 1 (this token's, still being written to the cache) also gathers its k / v granules and
+// folds that key into wave 0's softmax state. Then the usual publish + last-arriver merge.
+// The hand-off tag = a per-launch epoch in hctr: every attention block counts its exit, the last
+// one advances the epoch (by then every GEMV block has published, so every block of the launch
+// has read it). Bounded spins: a lost granule sets fault = 4.
+#include "attn_core.h"
+#include "gemv_core.h"
+
+namespace llmc {
+
+constexpr int kQaThreads = 256, kQaWaves = 4;
+
+template <int G, int D>
+__device__ __forceinline__ void qa_attention(int c, int kvh, char* smem, const int32_t* __restrict__ block_table,
+                                             int bt_len, int L, const bf16_t* __restrict__ k_cache,
+                                             const bf16_t* __restrict__ v_cache, float* __restrict__ part,
+                                             int* __restrict__ counters, bf16_t* __restrict__ out, int nh, int nkv,
+                                             int bs, int nblocks, int chunk, int max_chunks, int gsize, int max_groups,
+                                             float scale_log2, int* __restrict__ fault,
+                                             const uint64_t* __restrict__ granules, uint32_t htag) {
+  static_assert(G <= 16 && D % 32 == 0 && D <= 128, "shape");
+  using ST = SubTile<G, D>;
+  constexpr int HALF = D / 2;
+  const int tid = threadIdx.x, wave = tid / kWave, lane = tid % kWave;
+  int* ctr = counters + kvh * (2 + max_groups) * kCtrPitch;  // row 0: {ticket, epoch, group tickets}
+  const uint32_t tag = static_cast<uint32_t>(__hip_atomic_load(ctr + kCtrPitch, __ATOMIC_RELAXED,
+                                                               __HIP_MEMORY_SCOPE_AGENT)) + 1u;
+  const int per_wave = chunk / kQaWaves;  // 32 or 64 keys, inside one page (host-checked)
+  const int key0 = c * chunk + wave * per_wave;
+  const int pidx = __builtin_amdgcn_readfirstlane(min(key0 / bs, bt_len - 1));
+  const int page = min(max(ld_scalar(block_table + pidx), 0), nblocks - 1);  // clamped into the cache
+  const int Lc = L - 1;  // keys already in the cache; key L - 1 is this launch's
+  const int nchunks = (L + chunk - 1) / chunk;
+  const bool last = c == (L - 1) / chunk;  // block-uniform: this block folds in the new key
+  const int end = min(Lc, key0 + per_wave);
+  const bool wk = key0 < end;  // wave-uniform
+
+  char* vbuf = smem + wave * 32 * kVRowBytes;
+  float* red = reinterpret_cast<float*>(smem + kQaWaves * 32 * kVRowBytes);
+  int* flag = reinterpret_cast<int*>(red + kQaWaves * G * (D + 2));
+  bf16_t* qn = reinterpret_cast<bf16_t*>(flag + 4);  // [G][D] this kv head's rotated q
+  bf16_t* kn = qn + G * D;                           // [D] the new key
+  bf16_t* vn = kn + D;                               // [D] its value
+
+  // 1. the cached keys' K / V first: in flight while the projection still runs
+  ST st;
+  bf16x8 kfA[2][ST::KS], kfB[2][ST::KS];
+  u32x4 vsA[ST::NV], vsB[ST::NV];
+  const int64_t base = (static_cast<int64_t>(page) * nkv + kvh) * bs * D;
+  auto row = [&](const bf16_t* cache, int key) { return cache + base + static_cast<int64_t>(key % bs) * D; };
+  if (wk) {
+    st.issue(key0, end, lane, row, k_cache, v_cache, kfA, vsA);
+    if (key0 + 32 < end) st.issue(key0 + 32, end, lane, row, k_cache, v_cache, kfB, vsB);
+  }
+  // 2. this kv head's q (and in the last block the new key's k / v) granules -> LDS
+  const int nq = G * HALF, total = nq + (last ? 2 * HALF : 0);
+  for (int t = tid; t < total; t += kQaThreads) {
+    const int gi = t < nq ? kvh * G * HALF + t
+                          : (t < nq + HALF ? (nh + kvh) * HALF + (t - nq) : (nh + nkv + kvh) * HALF + (t - nq - HALF));
+    uint64_t v = 0;
+    for (unsigned spins = 0;; ++spins) {
+      v = __hip_atomic_load(granules + gi, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (static_cast<uint32_t>(v >> 32) == htag) break;
+      if (spins >= kSpinLimit) {
+        if (fault != nullptr) __hip_atomic_store(fault, 4, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        break;
+      }
+      __builtin_amdgcn_s_sleep(1);
+    }
+    const bf16_t lo = static_cast<bf16_t>(v & 0xffffu), hi = static_cast<bf16_t>((v >> 16) & 0xffffu);
+    if (t < nq) {  // q head g pair i = dims (i, i + D/2)
+      const int g = t / HALF, i = t % HALF;
+      qn[g * D + i] = lo;
+      qn[g * D + i + HALF] = hi;
+    } else if (t < nq + HALF) {  // k pair i = dims (i, i + D/2)
+      const int i = t - nq;
+      kn[i] = lo;
+      kn[i + HALF] = hi;
+    } else {  // v pair j = dims (2j, 2j + 1)
+      const int j = t - nq - HALF;
+      vn[2 * j] = lo;
+      vn[2 * j + 1] = hi;
+    }
+  }
+  __syncthreads();
+  st.init(qn, lane);
+  if (wk) {
+    st.compute(key0, end, lane, vbuf, scale_log2, kfA, vsA);
+    if (key0 + 32 < end) st.compute(key0 + 32, end, lane, vbuf, scale_log2, kfB, vsB);
+  }
+  // 3. the new key into wave 0's online-softmax state (head h = lane & 15; columns >= G copy head 0)
+  if (last && wave == 0) {
+    const int h = lane & 15, g4 = lane >> 4;
+    const bf16_t* qh = qn + (h < G ? h : 0) * D;
+    float s = 0.f;
+#pragma unroll
+    for (int e = 0; e < D / 4; ++e) {
+      const int d = g4 * (D / 4) + e;
+      s += bf16_to_f32(qh[d]) * bf16_to_f32(kn[d]);
+    }
+    s += __shfl_xor(s, 16, 64);
+    s += __shfl_xor(s, 32, 64);
+    s *= scale_log2;
+    const float m_new = fmaxf(st.m_run, s);
+    const float alpha = exp2f(st.m_run - m_new), p = exp2f(s - m_new);
+    st.l_run = st.l_run * alpha + p;
+    st.m_run = m_new;
+#pragma unroll
+    for (int dt = 0; dt < ST::DT; ++dt)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) st.acc[dt][i] = st.acc[dt][i] * alpha + p * bf16_to_f32(vn[dt * 16 + 4 * g4 + i]);
+  }
+  st.to_lds(red, wave, lane);
+  __syncthreads();
+  bf16_t* out_row = out + kvh * G * D;
+  if (nchunks == 1) {
+    store_direct<G, D, kQaWaves>(red, out_row, tid);
+    return;
+  }
+  publish_and_merge<G, D, kQaWaves>(red, part, ctr, 0, nkv, kvh, c, nchunks, gsize, max_chunks, max_groups, tag,
+                                    out_row, smem, flag, tid, fault);
+}
+
+template <int G, int D>
+__global__ __launch_bounds__(kQaThreads) void qkv_attn_kernel(
+    const bf16_t* __restrict__ x, const bf16_t* __restrict__ norm_w, float eps, const bf16_t* __restrict__ W, int N,
+    int K, RopeEpi rope, int nq_blocks, const int32_t* __restrict__ block_table, int bt_len,
+    const int32_t* __restrict__ seq_len, float* __restrict__ part, int* __restrict__ counters, bf16_t* __restrict__ out,
+    int bs, int nblocks, int chunk, int gc, int max_chunks, int gsize, int max_groups, float scale_log2,
+    int* __restrict__ fault, uint64_t* __restrict__ granules, int* __restrict__ hctr) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int bid = blockIdx.x;
+  const uint32_t htag =
+      static_cast<uint32_t>(__hip_atomic_load(hctr + kCtrPitch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) + 1u;
+  if (bid < nq_blocks) {  // block-uniform
+    RopeEpi r = rope;
+    r.granules = granules;
+    r.gtag = htag;
+    gemv_block<1, kQaThreads, 1, 8, PRO_NORM, EPI_ROPE, false>(bid, 0, smem, x, K, norm_w, eps, W, nullptr, 0, N, K,
+                                                               nullptr, 1, r, CarArgs{});
+    return;
+  }
+  const int a = bid - nq_blocks;
+  const int c = a % gc, kvh = a / gc;
+  const int L = ld_scalar(seq_len);
+  if (c * chunk < L)
+    qa_attention<G, D>(c, kvh, smem, block_table, bt_len, L, rope.k_cache, rope.v_cache, part, counters, out, rope.nh,
+                       rope.nkv, bs, nblocks, chunk, max_chunks, gsize, max_groups, scale_log2, fault, granules, htag);
+  // every attention block counts its exit; the last advances the hand-off epoch (every GEMV block
+  // has published by now: each one's granules were waited for, so each one read the epoch)
+  if (threadIdx.x == 0) {
+    const int A = static_cast<int>(gridDim.x) - nq_blocks;
+    if (__hip_atomic_fetch_add(hctr, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == A - 1) {
+      __hip_atomic_store(hctr, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(hctr + kCtrPitch, static_cast<int>(htag), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+  }
+}
+
+}  // namespace llmc
+
+using namespace llmc;
+
+extern "C" int llmc_attn_decode_groups(int max_chunks);
+
+// 0 when (nh, nkv, D, K) is covered: qkv output N = (nh + 2 nkv) D < 2048 rows and a multiple of 8
+// (the 4-wave paired GEMV geometry), G = nh / nkv in {1, 2, 4, 8}, D in {64, 96, 128}.
+extern "C" int llmc_qkv_attn_check(int nh, int nkv, int D, int K) {
+  if (nkv < 1 || nh % nkv != 0 || K % 8 != 0 || K <= 0) return -1;
+  const int G = nh / nkv, N = (nh + 2 * nkv) * D;
+  if (N >= 2048 || N % 8 != 0) return -2;
+  if (!(G == 1 || G == 2 || G == 4 || G == 8) || !(D == 64 || D == 96 || D == 128)) return -3;
+  if (static_cast<size_t>(K) * 2 + 64 > 64 * 1024) return -4;
+  return 0;
+}
+
+// One decode row: q/k/v = rope(W . rmsnorm(x)) (k / v written to the paged cache at slots[0]) and
+// out = attention(q, cache keys < L - 1 and this token's key) in the fused form: grid_chunks
+// blocks of `chunk` (128 / 256) keys per kv head, bs % (chunk / 4) == 0. part / counters: the
+// decode-attention workspace (max_chunks >= grid_chunks, its row 0). granules: u64 [(nh + 2 nkv)
+// D / 2]; hctr: int32 [2 kCtrPitch]; both zeroed once.
+extern "C" int llmc_qkv_attn(const void* x, const void* norm_w, float eps, const void* W, int K, void* q_out,
+                             void* k_cache, void* v_cache, const void* positions, const void* slots, const void* cos_t,
+                             const void* sin_t, const void* block_table, int bt_len, const void* seq_len, void* part,
+                             void* counters, void* out, int nh, int nkv, int D, int bs, int nblocks, int chunk,
+                             int grid_chunks, int max_chunks, float scale, void* fault, void* granules, void* hctr,
+                             hipStream_t s) {
+  if (llmc_qkv_attn_check(nh, nkv, D, K) != 0) return -1;
+  if ((chunk != 128 && chunk != 256) || bs % (chunk / 4) != 0 || grid_chunks < 1 || grid_chunks > max_chunks ||
+      bt_len < 1 || nblocks < 1 || counters == nullptr || granules == nullptr || hctr == nullptr)
+    return -1;
+  const int G = nh / nkv, N = (nh + 2 * nkv) * D;
+  const int nq_blocks = N / kQaWaves;
+  const int max_groups = llmc_attn_decode_groups(max_chunks);
+  const int gsize = grid_chunks > kAttnOneLevel ? kAttnGroup : grid_chunks;
+  const size_t lds_gemv = static_cast<size_t>(K) * 2 + 2 * kQaWaves * sizeof(float);
+  const size_t lds_attn = kQaWaves * 32 * kVRowBytes + static_cast<size_t>(kQaWaves) * G * (D + 2) * sizeof(float) +
+                          16 + static_cast<size_t>(G * D + 2 * D) * sizeof(bf16_t);
+  const size_t lds = lds_gemv > lds_attn ? lds_gemv : lds_attn;
+  if (lds > 64 * 1024) return -4;
+  RopeEpi rope{(bf16_t*)q_out, nh * D, (bf16_t*)k_cache, (bf16_t*)v_cache, (const int32_t*)positions,
+               (const int32_t*)slots, (const float*)cos_t, (const float*)sin_t, nh, nkv, D, bs};
+  const dim3 grid(nq_blocks + grid_chunks * nkv);
+  const float sl2 = scale * 1.4426950408889634f;
+#define LLMC_QA(GG, DD)                                                                                         \
+  qkv_attn_kernel<GG, DD><<<grid, kQaThreads, lds, s>>>(                                                        \
+      (const bf16_t*)x, (const bf16_t*)norm_w, eps, (const bf16_t*)W, N, K, rope, nq_blocks,                     \
+      (const int32_t*)block_table, bt_len, (const int32_t*)seq_len, (float*)part, (int*)counters, (bf16_t*)out,   \
+      bs, nblocks, chunk, grid_chunks, max_chunks, gsize, max_groups, sl2, (int*)fault, (uint64_t*)granules,      \
+      (int*)hctr)
+#define LLMC_QA_D(GG)                     \
+  if (D == 64) LLMC_QA(GG, 64);           \
+  else if (D == 96) LLMC_QA(GG, 96);      \
+  else LLMC_QA(GG, 128)
+  switch (G) {
+    case 1: LLMC_QA_D(1); break;
+    case 2: LLMC_QA_D(2); break;
+    case 4: LLMC_QA_D(4); break;
+    default: LLMC_QA_D(8); break;
+  }
+#undef LLMC_QA_D
+#undef LLMC_QA
+  return static_cast<int>(hipGetLastError());
+}

@@ -69,6 +69,10 @@ class EngineConfig:
     attn_oproj: bool = dataclasses.field(default_factory=lambda: os.environ.get("LLMC_ATTN_OPROJ", "1") != "0")
     attn_oproj_min_chunk: int = dataclasses.field(
         default_factory=lambda: 32 if os.environ.get("LLMC_ATTN_OPROJ") == "all" else ops.ATTN_OPROJ_MIN_CHUNK)
+    # one-row engines whose qkv output is short (N < 2048: the TP ranks' shards): the qkv projection
+    # and the decode attention as ONE launch in the buckets of the fused attention form
+    # (csrc/kernels/qkv_attn.hip; LLMC_QKV_ATTN=0 keeps the two launches)
+    qkv_attn: bool = dataclasses.field(default_factory=lambda: os.environ.get("LLMC_QKV_ATTN", "1") != "0")
 
 
 FUSED_CHUNK_SMALL, FUSED_CHUNK_LARGE = 128, 256
@@ -279,6 +283,15 @@ class Engine:
                 self.ao_chunks = [ch if ch >= lo and (ch <= 256 or self.bs % 64 == 0) else 0
                                   for ch in (ops.attn_oproj_chunk(cap, self.ao_nc) for cap, _, _, _ in self.attn_buckets)]
                 self.ao_ws = ops.attn_oproj_workspace(c.hidden, self.nh, self.nkv, self.D, self.ao_nc, dev)
+        # one-launch qkv + attention: per bucket whether it runs (fused-form buckets of one-row
+        # engines the kernel covers, where attn_oproj does not run)
+        self.qa_buckets: List[bool] = [False] * len(self.attn_buckets)
+        if (self.on_gpu and self.ecfg.qkv_attn and B == 1 and not self.mfma_decode
+                and ops.qkv_attn_supported(self.nh, self.nkv, self.D, c.hidden)):
+            self.qa_buckets = [fused and ch in (128, 256) and self.bs % (ch // 4) == 0 and not self.ao_chunks[i]
+                               for i, (_, ch, _, fused) in enumerate(self.attn_buckets)]
+            if any(self.qa_buckets):
+                self.qa_ws = ops.qkv_attn_workspace(self.nh, self.nkv, self.D, dev)
         # set by a decode-attention merger that gave up on a partial (checked after every decode)
         self.attn_fault = torch.zeros(1, dtype=torch.int32, device=dev) if self.on_gpu else None
         if self.on_gpu:
@@ -589,22 +602,30 @@ class Engine:
         ops.embedding(self.tokens_in[:B], self.w.embed, out=h)
         bi = -1 if bucket is None else bucket
         ao_chunk = self.ao_chunks[bi] if B == 1 else 0
+        qa = B == 1 and self.qa_buckets[bi]
         dbg = self._debug_layer_io  # eager debug steps only: each layer's input, then the last output
         for li, Lw in enumerate(self.w.layers):
             if dbg is not None:
                 dbg.append(h.clone())
-            ops.qkv_rope(h, Lw.w_qkv, Lw.ln1, c.rms_eps, q, self.k_cache[li], self.v_cache[li], self.positions[:B],
-                         self.slots[:B], self.cos_t, self.sin_t, self.nh, self.nkv, self.D, self.bs,
-                         mfma=self.mfma_decode)
-            if ao_chunk:  # one-row engines without TP: attention + o_proj + residual in one launch
-                ops.attn_oproj(q, self.k_cache[li], self.v_cache[li], self.block_tables[:1], self.seq_lens[:1], Lw.w_o,
-                               h, attn, self.ao_ws, self.nh, self.nkv, self.D, self.bs, ao_chunk, self.ao_nc,
-                               self.scale, fault=self.attn_fault)
-            else:
-                ops.attn_decode(q, self.k_cache[li], self.v_cache[li], self.block_tables[:B], self.seq_lens[:B], attn,
-                                part[:B], self.attn_counters[:B], self.nh, self.nkv, self.D, self.bs, chunk,
-                                self.scale, grid_chunks, fused=fused, fault=self.attn_fault)
+            if qa:  # qkv projection + attention in one launch (one row), then o_proj
+                ops.qkv_attn(h, Lw.w_qkv, Lw.ln1, c.rms_eps, q, self.k_cache[li], self.v_cache[li], self.positions[:1],
+                             self.slots[:1], self.cos_t, self.sin_t, self.block_tables[:1], self.seq_lens[:1], attn,
+                             part, self.attn_counters, self.qa_ws, self.nh, self.nkv, self.D, self.bs, chunk,
+                             grid_chunks, self.scale, fault=self.attn_fault)
                 self._row_parallel(attn, Lw.w_o, h)
+            else:
+                ops.qkv_rope(h, Lw.w_qkv, Lw.ln1, c.rms_eps, q, self.k_cache[li], self.v_cache[li],
+                             self.positions[:B], self.slots[:B], self.cos_t, self.sin_t, self.nh, self.nkv, self.D,
+                             self.bs, mfma=self.mfma_decode)
+                if ao_chunk:  # one-row engines without TP: attention + o_proj + residual in one launch
+                    ops.attn_oproj(q, self.k_cache[li], self.v_cache[li], self.block_tables[:1], self.seq_lens[:1],
+                                   Lw.w_o, h, attn, self.ao_ws, self.nh, self.nkv, self.D, self.bs, ao_chunk, self.ao_nc,
+                                   self.scale, fault=self.attn_fault)
+                else:
+                    ops.attn_decode(q, self.k_cache[li], self.v_cache[li], self.block_tables[:B], self.seq_lens[:B],
+                                    attn, part[:B], self.attn_counters[:B], self.nh, self.nkv, self.D, self.bs, chunk,
+                                    self.scale, grid_chunks, fused=fused, fault=self.attn_fault)
+                    self._row_parallel(attn, Lw.w_o, h)
             if c.is_moe:
                 self._moe_decode(h, Lw, B)
             else:

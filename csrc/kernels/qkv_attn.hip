@@ -72,8 +72,20 @@ __device__ __forceinline__ void qa_attention(int c, int kvh, char* smem, const i
     st.issue(key0, end, lane, row, k_cache, v_cache, kfA, vsA);
     if (key0 + 32 < end) st.issue(key0 + 32, end, lane, row, k_cache, v_cache, kfB, vsB);
   }
-  // 2. this kv head's q (and in the last block the new key's k / v) granules -> LDS
+  // 2. this kv head's q (and in the last block the new key's k / v) granules -> LDS. One thread
+  // polls a sentinel (this head group's last q granule) until it lands, the block then reads them
+  // all (re-polling any that lags): every thread polling its own granule flooded the memory path
+  // the projection's weights stream through (MI355X_MICROARCH.md polling-cost)
   const int nq = G * HALF, total = nq + (last ? 2 * HALF : 0);
+  if (tid == 0) {
+    for (unsigned spins = 0; spins < kSpinLimit; ++spins) {
+      const uint64_t v = __hip_atomic_load(granules + (kvh * G + G - 1) * HALF + HALF - 1, __ATOMIC_RELAXED,
+                                           __HIP_MEMORY_SCOPE_AGENT);
+      if (static_cast<uint32_t>(v >> 32) == htag) break;
+      __builtin_amdgcn_s_sleep(2);
+    }
+  }
+  __syncthreads();
   for (int t = tid; t < total; t += kQaThreads) {
     const int gi = t < nq ? kvh * G * HALF + t
                           : (t < nq + HALF ? (nh + kvh) * HALF + (t - nq) : (nh + nkv + kvh) * HALF + (t - nq - HALF));

@@ -1,0 +1,54 @@
+"""The one-launch qkv + attention (csrc/kernels/qkv_attn.hip) on the host: which shapes the kernel
+library covers (the engine's per-bucket choice depends on it) and the op's CPU path (qkv_rope +
+the attention oracle, what an engine on the CPU would compute)."""
+
+import math
+
+import torch
+
+from llm_consensus_amd import ops
+from llm_consensus_amd.ops import oracle
+
+
+def test_shape_gate():
+    # the TP ranks' shards (qkv output < 2048 rows)
+    assert ops.qkv_attn_supported(4, 1, 128, 4096)    # Llama-3-8B TP=8
+    assert ops.qkv_attn_supported(8, 2, 128, 4096)    # Llama-3-8B TP=4
+    assert ops.qkv_attn_supported(8, 1, 128, 8192)    # Llama-3-70B TP=8
+    assert ops.qkv_attn_supported(4, 4, 96, 3072)     # Phi-3-mini TP=8
+    # whole models and wide shards keep the two launches
+    assert not ops.qkv_attn_supported(32, 8, 128, 4096)   # Llama-3-8B
+    assert not ops.qkv_attn_supported(16, 4, 128, 4096)   # Llama-3-8B TP=2 (3072 rows)
+    assert not ops.qkv_attn_supported(16, 2, 128, 8192)   # Llama-3-70B TP=4 (2560 rows)
+    assert not ops.qkv_attn_supported(4, 1, 80, 4096)     # head dim off the MFMA slabs
+    assert not ops.qkv_attn_supported(12, 1, 128, 4096)   # G = 12
+
+
+def test_cpu_path_is_qkv_rope_then_attention():
+    torch.manual_seed(0)
+    nh, nkv, D, K, bs, L = 4, 1, 64, 256, 16, 37
+    N = (nh + 2 * nkv) * D
+    x = torch.randn(1, K).to(torch.bfloat16)
+    nw = torch.ones(K, dtype=torch.bfloat16)
+    W = (torch.randn(N, K) / math.sqrt(K)).to(torch.bfloat16)
+    nb = 6
+    kc = torch.randn(nb, nkv, bs, D).to(torch.bfloat16)
+    vc = torch.randn(nb, nkv, bs, D).to(torch.bfloat16)
+    bt = torch.tensor([[3, 1, 5, 0, 2]], dtype=torch.int32)
+    sl = torch.tensor([L], dtype=torch.int32)
+    pos = torch.tensor([L - 1], dtype=torch.int32)
+    slots = torch.tensor([int(bt[0, (L - 1) // bs]) * bs + (L - 1) % bs], dtype=torch.int32)
+    ang = torch.arange(64, dtype=torch.float32)[:, None] * (1e-2 * torch.arange(D // 2, dtype=torch.float32))[None]
+    cos, sin = torch.cos(ang), torch.sin(ang)
+    scale = 1 / math.sqrt(D)
+    q = torch.zeros(1, nh * D, dtype=torch.bfloat16)
+    out = torch.zeros(1, nh * D, dtype=torch.bfloat16)
+    kc1, vc1 = kc.clone(), vc.clone()
+    ops.qkv_attn(x, W, nw, 1e-5, q, kc1, vc1, pos, slots, cos, sin, bt, sl, out, None, None, None, nh, nkv, D, bs,
+                 128, 1, scale)
+    q2 = torch.zeros(1, nh * D, dtype=torch.bfloat16)
+    kc2, vc2 = kc.clone(), vc.clone()
+    ops.qkv_rope(x, W, nw, 1e-5, q2, kc2, vc2, pos, slots, cos, sin, nh, nkv, D, bs)
+    ref = oracle.attn_decode(q2, kc2, vc2, bt, sl, nh, nkv, D, bs, scale)
+    assert torch.equal(q, q2) and torch.equal(kc1, kc2) and torch.equal(vc1, vc2)
+    assert torch.equal(out, ref.to(out.dtype))

@@ -286,8 +286,8 @@ class Engine:
         # one-launch qkv + attention: per bucket whether it runs (fused-form buckets of one-row
         # engines the kernel covers, where attn_oproj does not run)
         self.qa_buckets: List[bool] = [False] * len(self.attn_buckets)
-        if (self.on_gpu and self.ecfg.qkv_attn and B == 1 and not self.mfma_decode
-                and ops.qkv_attn_supported(self.nh, self.nkv, self.D, c.hidden)):
+        # (B = max_batch: one-row engines only, so a row's tokens never depend on what shared its steps)
+        if self.on_gpu and self.ecfg.qkv_attn and B == 1 and ops.qkv_attn_supported(self.nh, self.nkv, self.D, c.hidden):
             self.qa_buckets = [fused and ch in (128, 256) and self.bs % (ch // 4) == 0 and not self.ao_chunks[i]
                                for i, (_, ch, _, fused) in enumerate(self.attn_buckets)]
             if any(self.qa_buckets):

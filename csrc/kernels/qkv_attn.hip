@@ -1,6 +1,6 @@
 // qkv projection (+ RMSNorm prologue, RoPE / paged-KV-write epilogue) AND the decode attention of
-// the same token in ONE launch, for one-row engines whose qkv output is short (N < 2048: the
-// tensor-parallel ranks' shards, 1-2 kv heads). Host: llmc_qkv_attn.
+// the same token in ONE launch, for one-row engines (the tensor-parallel ranks' shards with 1-2 kv
+// heads, where it measured faster; the engine decides per shape). Host: llmc_qkv_attn.
 //
 // Why (profiles/r4_tp8_shard_kernel_stats.md, a Llama-3-8B TP=8 rank at 2k keys): the qkv GEMV
 // (4.8 us) and the attention (9.0 us for ~1 MB of K/V) are both latency chains; as two launches
@@ -8,11 +8,14 @@
 // GEMV's boundary. Here they run under the GEMV: the K/V of the cached keys do not depend on this
 // token, so the attention blocks request them at once and only wait for the rotated q.
 //
-// Grid: blocks [0, Nq) are the GEMV (gemv_core.h gemv_block: 4 waves x 1 row, 8 x 16-B loads per
-// lane in flight, the engine's geometry for N < 2048, so the projection is the same arithmetic as
-// the qkv_rope launch); blocks [Nq, Nq + gc * nkv) are the fused-form attention chunks (attn_core.h
-// SubTile, 4 waves x 32 / 64 keys of one page). Attention blocks only wait on GEMV blocks, which
-// have lower indices and are dispatched first: no wait is on a block that has not started.
+// Grid: one segment per kv head g: the GEMV blocks of its G q heads, of its k head and of its v head
+// (gemv_core.h gemv_block: 4 waves x 1 row, 8 x 16-B loads per lane in flight; every row's dot
+// product in the same order as the qkv_rope launch, whose geometry for outputs under 2048 rows this
+// is, so there q / k / v are the same bits; wider outputs group the RMS norm's sum of squares
+// differently, last bits), then its gc
+// fused-form attention chunks (attn_core.h SubTile, 4 waves x 32 / 64 keys of one page). An
+// attention block only waits on GEMV blocks of its own segment, which have lower indices and are
+// dispatched first: no wait is on a block that has not started.
 //
 // Hand-off: the GEMV epilogue publishes every rotated q / k pair and v pair as an 8-B {bf16x2, tag}
 // granule (RopeEpi::granules: one single-copy-atomic write-through store, the data IS the flag,
@@ -156,32 +159,39 @@ __device__ __forceinline__ void qa_attention(int c, int kvh, char* smem, const i
 template <int G, int D>
 __global__ __launch_bounds__(kQaThreads) void qkv_attn_kernel(
     const bf16_t* __restrict__ x, const bf16_t* __restrict__ norm_w, float eps, const bf16_t* __restrict__ W, int N,
-    int K, RopeEpi rope, int nq_blocks, const int32_t* __restrict__ block_table, int bt_len,
+    int K, RopeEpi rope, const int32_t* __restrict__ block_table, int bt_len,
     const int32_t* __restrict__ seq_len, float* __restrict__ part, int* __restrict__ counters, bf16_t* __restrict__ out,
     int bs, int nblocks, int chunk, int gc, int max_chunks, int gsize, int max_groups, float scale_log2,
     int* __restrict__ fault, uint64_t* __restrict__ granules, int* __restrict__ hctr) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  const int bid = blockIdx.x;
+  // Block order: one segment per kv head g = [its G q heads' GEMV blocks | its k head's | its v
+  // head's | its gc attention blocks], so head g's attention starts after 1 / nkv of the projection
+  // has been dispatched and still waits only on lower-index blocks
+  constexpr int QB = G * D / kQaWaves, KB = D / kQaWaves;  // GEMV blocks (4 rows each) per segment part
+  const int seg = QB + 2 * KB + gc;
+  const int g = blockIdx.x / seg, r = blockIdx.x % seg;
   const uint32_t htag =
       static_cast<uint32_t>(__hip_atomic_load(hctr + kCtrPitch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) + 1u;
-  if (bid < nq_blocks) {  // block-uniform
-    RopeEpi r = rope;
-    r.granules = granules;
-    r.gtag = htag;
-    gemv_block<1, kQaThreads, 1, 8, PRO_NORM, EPI_ROPE, false>(bid, 0, smem, x, K, norm_w, eps, W, nullptr, 0, N, K,
-                                                               nullptr, 1, r, CarArgs{});
+  if (r < QB + 2 * KB) {  // block-uniform: the projection of 4 rows
+    const int row0 = r < QB ? g * G * D + kQaWaves * r
+                            : (r < QB + KB ? (rope.nh + g) * D + kQaWaves * (r - QB)
+                                           : (rope.nh + rope.nkv + g) * D + kQaWaves * (r - QB - KB));
+    RopeEpi re = rope;
+    re.granules = granules;
+    re.gtag = htag;
+    gemv_block<1, kQaThreads, 1, 8, PRO_NORM, EPI_ROPE, false>(row0 / kQaWaves, 0, smem, x, K, norm_w, eps, W, nullptr,
+                                                               0, N, K, nullptr, 1, re, CarArgs{});
     return;
   }
-  const int a = bid - nq_blocks;
-  const int c = a % gc, kvh = a / gc;
+  const int c = r - QB - 2 * KB;
   const int L = ld_scalar(seq_len);
   if (c * chunk < L)
-    qa_attention<G, D>(c, kvh, smem, block_table, bt_len, L, rope.k_cache, rope.v_cache, part, counters, out, rope.nh,
+    qa_attention<G, D>(c, g, smem, block_table, bt_len, L, rope.k_cache, rope.v_cache, part, counters, out, rope.nh,
                        rope.nkv, bs, nblocks, chunk, max_chunks, gsize, max_groups, scale_log2, fault, granules, htag);
   // every attention block counts its exit; the last advances the hand-off epoch (every GEMV block
   // has published by now: each one's granules were waited for, so each one read the epoch)
   if (threadIdx.x == 0) {
-    const int A = static_cast<int>(gridDim.x) - nq_blocks;
+    const int A = gc * rope.nkv;
     if (__hip_atomic_fetch_add(hctr, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == A - 1) {
       __hip_atomic_store(hctr, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       __hip_atomic_store(hctr + kCtrPitch, static_cast<int>(htag), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -195,12 +205,11 @@ using namespace llmc;
 
 extern "C" int llmc_attn_decode_groups(int max_chunks);
 
-// 0 when (nh, nkv, D, K) is covered: qkv output N = (nh + 2 nkv) D < 2048 rows and a multiple of 8
-// (the 4-wave paired GEMV geometry), G = nh / nkv in {1, 2, 4, 8}, D in {64, 96, 128}.
+// 0 when (nh, nkv, D, K) is covered: G = nh / nkv in {1, 2, 4, 8}, D in {64, 96, 128} (whole
+// 4-row GEMV blocks per head, pairs inside a block), x of K <= 32 Ki bf16 in LDS.
 extern "C" int llmc_qkv_attn_check(int nh, int nkv, int D, int K) {
   if (nkv < 1 || nh % nkv != 0 || K % 8 != 0 || K <= 0) return -1;
-  const int G = nh / nkv, N = (nh + 2 * nkv) * D;
-  if (N >= 2048 || N % 8 != 0) return -2;
+  const int G = nh / nkv;
   if (!(G == 1 || G == 2 || G == 4 || G == 8) || !(D == 64 || D == 96 || D == 128)) return -3;
   if (static_cast<size_t>(K) * 2 + 64 > 64 * 1024) return -4;
   return 0;
@@ -222,7 +231,6 @@ extern "C" int llmc_qkv_attn(const void* x, const void* norm_w, float eps, const
       bt_len < 1 || nblocks < 1 || counters == nullptr || granules == nullptr || hctr == nullptr)
     return -1;
   const int G = nh / nkv, N = (nh + 2 * nkv) * D;
-  const int nq_blocks = N / kQaWaves;
   const int max_groups = llmc_attn_decode_groups(max_chunks);
   const int gsize = grid_chunks > kAttnOneLevel ? kAttnGroup : grid_chunks;
   const size_t lds_gemv = static_cast<size_t>(K) * 2 + 2 * kQaWaves * sizeof(float);
@@ -232,11 +240,11 @@ extern "C" int llmc_qkv_attn(const void* x, const void* norm_w, float eps, const
   if (lds > 64 * 1024) return -4;
   RopeEpi rope{(bf16_t*)q_out, nh * D, (bf16_t*)k_cache, (bf16_t*)v_cache, (const int32_t*)positions,
                (const int32_t*)slots, (const float*)cos_t, (const float*)sin_t, nh, nkv, D, bs};
-  const dim3 grid(nq_blocks + grid_chunks * nkv);
+  const dim3 grid(N / kQaWaves + grid_chunks * nkv);
   const float sl2 = scale * 1.4426950408889634f;
 #define LLMC_QA(GG, DD)                                                                                         \
   qkv_attn_kernel<GG, DD><<<grid, kQaThreads, lds, s>>>(                                                        \
-      (const bf16_t*)x, (const bf16_t*)norm_w, eps, (const bf16_t*)W, N, K, rope, nq_blocks,                     \
+      (const bf16_t*)x, (const bf16_t*)norm_w, eps, (const bf16_t*)W, N, K, rope,                                \
       (const int32_t*)block_table, bt_len, (const int32_t*)seq_len, (float*)part, (int*)counters, (bf16_t*)out,   \
       bs, nblocks, chunk, grid_chunks, max_chunks, gsize, max_groups, sl2, (int*)fault, (uint64_t*)granules,      \
       (int*)hctr)

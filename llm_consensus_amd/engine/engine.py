@@ -69,13 +69,16 @@ class EngineConfig:
     attn_oproj: bool = dataclasses.field(default_factory=lambda: os.environ.get("LLMC_ATTN_OPROJ", "1") != "0")
     attn_oproj_min_chunk: int = dataclasses.field(
         default_factory=lambda: 32 if os.environ.get("LLMC_ATTN_OPROJ") == "all" else ops.ATTN_OPROJ_MIN_CHUNK)
-    # one-row engines whose qkv output is short (N < 2048: the TP ranks' shards): the qkv projection
-    # and the decode attention as ONE launch in the buckets of the fused attention form
-    # (csrc/kernels/qkv_attn.hip; LLMC_QKV_ATTN=0 keeps the two launches)
-    qkv_attn: bool = dataclasses.field(default_factory=lambda: os.environ.get("LLMC_QKV_ATTN", "1") != "0")
+    # one-row engines: the qkv projection and the decode attention as ONE launch in the buckets of
+    # the fused attention form (csrc/kernels/qkv_attn.hip). "1": shards whose qkv output is under
+    # QKV_ATTN_MAX_ROWS rows (the TP ranks', where it measured faster: profiles/r4_qkv_attn.md);
+    # "all": every covered shape and fused bucket, ahead of attn_oproj; "0": never (LLMC_QKV_ATTN)
+    qkv_attn: str = dataclasses.field(default_factory=lambda: os.environ.get("LLMC_QKV_ATTN", "1"))
 
 
 FUSED_CHUNK_SMALL, FUSED_CHUNK_LARGE = 128, 256
+# one-launch qkv + attention by default only for qkv outputs under this many rows (TP shards)
+QKV_ATTN_MAX_ROWS = 2048
 # batching engines: minimum keys per split block (see attn_buckets) when rows x kv heads fill the
 # chip with >= 32 (row, head) units, and below that (3 duplicate 8B responders = 24 units, TP
 # ranks holding 1-2 kv heads) where a row needs more blocks of its own
@@ -287,9 +290,16 @@ class Engine:
         # engines the kernel covers, where attn_oproj does not run)
         self.qa_buckets: List[bool] = [False] * len(self.attn_buckets)
         # (B = max_batch: one-row engines only, so a row's tokens never depend on what shared its steps)
-        if self.on_gpu and self.ecfg.qkv_attn and B == 1 and ops.qkv_attn_supported(self.nh, self.nkv, self.D, c.hidden):
-            self.qa_buckets = [fused and ch in (128, 256) and self.bs % (ch // 4) == 0 and not self.ao_chunks[i]
+        qa = str(self.ecfg.qkv_attn)
+        qa_all = qa == "all"
+        rows = (self.nh + 2 * self.nkv) * self.D
+        if (self.on_gpu and qa not in ("0", "False", "") and B == 1 and (qa_all or rows < QKV_ATTN_MAX_ROWS)
+                and ops.qkv_attn_supported(self.nh, self.nkv, self.D, c.hidden)):
+            self.qa_buckets = [fused and ch in (128, 256) and self.bs % (ch // 4) == 0
+                               and (qa_all or not self.ao_chunks[i])
                                for i, (_, ch, _, fused) in enumerate(self.attn_buckets)]
+            if qa_all:  # the one launch replaces attn_oproj where both cover a bucket
+                self.ao_chunks = [0 if q else a for q, a in zip(self.qa_buckets, self.ao_chunks)]
             if any(self.qa_buckets):
                 self.qa_ws = ops.qkv_attn_workspace(self.nh, self.nkv, self.D, dev)
         # set by a decode-attention merger that gave up on a partial (checked after every decode)

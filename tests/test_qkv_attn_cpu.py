@@ -11,17 +11,20 @@ from llm_consensus_amd.ops import oracle
 
 
 def test_shape_gate():
-    # the TP ranks' shards (qkv output < 2048 rows)
-    assert ops.qkv_attn_supported(4, 1, 128, 4096)    # Llama-3-8B TP=8
-    assert ops.qkv_attn_supported(8, 2, 128, 4096)    # Llama-3-8B TP=4
-    assert ops.qkv_attn_supported(8, 1, 128, 8192)    # Llama-3-70B TP=8
-    assert ops.qkv_attn_supported(4, 4, 96, 3072)     # Phi-3-mini TP=8
-    # whole models and wide shards keep the two launches
-    assert not ops.qkv_attn_supported(32, 8, 128, 4096)   # Llama-3-8B
-    assert not ops.qkv_attn_supported(16, 4, 128, 4096)   # Llama-3-8B TP=2 (3072 rows)
-    assert not ops.qkv_attn_supported(16, 2, 128, 8192)   # Llama-3-70B TP=4 (2560 rows)
+    from llm_consensus_amd.engine.engine import QKV_ATTN_MAX_ROWS
+
+    # the kernel covers GQA groups 1-8 at D = 64 / 96 / 128 ...
+    for nh, nkv, D, K in [(4, 1, 128, 4096),    # Llama-3-8B TP=8
+                          (8, 2, 128, 4096),    # Llama-3-8B TP=4
+                          (8, 1, 128, 8192),    # Llama-3-70B TP=8
+                          (4, 4, 96, 3072),     # Phi-3-mini TP=8
+                          (32, 8, 128, 4096)]:  # Llama-3-8B
+        assert ops.qkv_attn_supported(nh, nkv, D, K), (nh, nkv, D, K)
     assert not ops.qkv_attn_supported(4, 1, 80, 4096)     # head dim off the MFMA slabs
     assert not ops.qkv_attn_supported(12, 1, 128, 4096)   # G = 12
+    # ... and engines take it by default only for the TP ranks' short qkv outputs
+    assert (4 + 2) * 128 < QKV_ATTN_MAX_ROWS and (8 + 4) * 128 < QKV_ATTN_MAX_ROWS
+    assert (32 + 16) * 128 >= QKV_ATTN_MAX_ROWS
 
 
 def test_cpu_path_is_qkv_rope_then_attention():

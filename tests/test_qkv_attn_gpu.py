@@ -73,11 +73,13 @@ SHAPES = [(4, 1, 128, 4096),   # Llama-3-8B TP=8 rank
           (8, 2, 128, 4096),   # Llama-3-8B TP=4 rank
           (8, 1, 128, 8192),   # Llama-3-70B TP=8 rank
           (4, 4, 96, 3072),    # Phi-3-mini TP=8 rank (no GQA, D = 96)
-          (4, 2, 64, 1024)]
+          (4, 2, 64, 1024),
+          (32, 8, 128, 4096),  # Llama-3-8B (LLMC_QKV_ATTN=all)
+          (16, 4, 128, 4096)]  # Llama-3-8B TP=2 rank
 
 
 @pytest.mark.parametrize("nh,nkv,D,K", SHAPES)
-@pytest.mark.parametrize("L", [1, 2, 64, 127, 128, 129, 700, 2048, 3001])
+@pytest.mark.parametrize("L", [1, 2, 64, 127, 128, 129, 700, 2048, 3001, 7000])
 def test_qkv_attn_vs_two_launches_and_oracle(cuda, nh, nkv, D, K, L):
     assert ops.qkv_attn_supported(nh, nkv, D, K)
     cs = _Case(nh, nkv, D, K, L, seed=L + nh)
@@ -98,7 +100,11 @@ def test_qkv_attn_vs_two_launches_and_oracle(cuda, nh, nkv, D, K, L):
                      ctr, ws, nh, nkv, D, cs.bs, chunk, gc, scale, fault=fault)
         torch.cuda.synchronize()
         assert int(fault.item()) == 0
-        assert torch.equal(q, q_ref) and torch.equal(kc, kc_ref) and torch.equal(vc, vc_ref)
+        if (nh + 2 * nkv) * D < 2048:  # the qkv launch's own 4-wave geometry: the same bits
+            assert torch.equal(q, q_ref) and torch.equal(kc, kc_ref) and torch.equal(vc, vc_ref)
+        else:  # wider outputs: the RMS norm's sum of squares is grouped differently (last bits)
+            for a, b in ((q, q_ref), (kc, kc_ref), (vc, vc_ref)):
+                assert (a.float() - b.float()).abs().max().item() < 2e-2 * max(1.0, b.float().abs().max().item())
         o = out.float().cpu()
         ref = out_ref.float().cpu()
         tol = 2e-2 * max(1.0, ref.abs().max().item())
@@ -152,8 +158,8 @@ def test_engine_qkv_attn_matches_two_launch_step(cuda):
 
     cfg = FAMILIES["llama-small"]
     w = TransformerWeights(cfg, TPGroup.single(), torch.device("cuda:0"), seed=31)
-    eq = Engine(cfg, EngineConfig(device="cuda:0", max_context=2400, qkv_attn=True), weights=w)
-    e2 = Engine(cfg, EngineConfig(device="cuda:0", max_context=2400, qkv_attn=False), weights=w)
+    eq = Engine(cfg, EngineConfig(device="cuda:0", max_context=2400, qkv_attn="1"), weights=w)
+    e2 = Engine(cfg, EngineConfig(device="cuda:0", max_context=2400, qkv_attn="0"), weights=w)
     assert any(eq.qa_buckets) and not any(e2.qa_buckets)
     for plen in (40, 1030, 2000):
         prompt = [(i * 7919) % (cfg.vocab - 300) + 256 for i in range(plen)]
@@ -166,7 +172,33 @@ def test_engine_qkv_attn_matches_two_launch_step(cuda):
             assert err < 0.02 * max(1.0, l2[i].abs().max().item()), (plen, i, err)
     prompt = [(i * 31) % 3000 + 256 for i in range(1500)]
     a = eq.generate_ids(prompt, 32, temperature=0.0, stop_on_eos=False)
-    ee = Engine(cfg, EngineConfig(device="cuda:0", max_context=2400, qkv_attn=True, use_graphs=False), weights=w)
+    ee = Engine(cfg, EngineConfig(device="cuda:0", max_context=2400, qkv_attn="1", use_graphs=False), weights=w)
     b = ee.generate_ids(prompt, 32, temperature=0.0, stop_on_eos=False)
     assert a == b
     assert int(eq.attn_fault.item()) == 0
+
+
+def test_engine_qkv_attn_all_replaces_attn_oproj(cuda):
+    """LLMC_QKV_ATTN=all on a whole Llama-3-8B-shaped model (2 layers): the one launch takes the
+    fused buckets, attn_oproj's too; logits match the default engine's."""
+    from llm_consensus_amd.engine import Engine, EngineConfig
+    from llm_consensus_amd.models.config import FAMILIES
+    from llm_consensus_amd.models.transformer import TransformerWeights
+    from llm_consensus_amd.parallel.comm import TPGroup
+
+    cfg = FAMILIES["llama-3-8b"].with_(name="llama-3-8b-2l", n_layers=2)
+    w = TransformerWeights(cfg, TPGroup.single(), torch.device("cuda:0"), seed=41)
+    ea = Engine(cfg, EngineConfig(device="cuda:0", max_context=8300, qkv_attn="all"), weights=w)
+    ed = Engine(cfg, EngineConfig(device="cuda:0", max_context=8300), weights=w)
+    assert any(ea.qa_buckets) and not any(ed.qa_buckets)
+    assert not any(q and a for q, a in zip(ea.qa_buckets, ea.ao_chunks))
+    for plen in (100, 3000, 7000):
+        prompt = [(i * 7919) % (cfg.vocab - 300) + 256 for i in range(plen)]
+        ta, la = ea.debug_decode_logits(prompt, 6)
+        t2, l2 = ed.debug_decode_logits(prompt, 6)
+        for i in range(6):
+            if ta[:i] != t2[:i]:
+                break
+            err = (la[i] - l2[i]).abs().max().item()
+            assert err < 0.02 * max(1.0, l2[i].abs().max().item()), (plen, i, err)
+    assert int(ea.attn_fault.item()) == 0

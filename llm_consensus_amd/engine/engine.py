@@ -271,8 +271,6 @@ class Engine:
         self.attn_buckets = attn_buckets(ctxmax, split_blocks_per_head(self.nh, self.nkv),
                                          ops.FUSED_ATTN_MAX_KEYS if self.bs % 32 == 0 else 0, self.nh // self.nkv,
                                          self.nkv, rows=self.ecfg.max_batch)
-        max_chunks = max(gc for _, _, gc, _ in self.attn_buckets)
-        self.attn_part, self.attn_counters = ops.decode_attn_workspace(B, self.nh, self.nkv, self.D, max_chunks, dev)
         # fused attention + o_proj launch: per bucket its keys per block (0 = the bucket keeps the
         # two launches)
         self.ao_chunks: List[int] = [0] * len(self.attn_buckets)
@@ -286,22 +284,28 @@ class Engine:
                 self.ao_chunks = [ch if ch >= lo and (ch <= 256 or self.bs % 64 == 0) else 0
                                   for ch in (ops.attn_oproj_chunk(cap, self.ao_nc) for cap, _, _, _ in self.attn_buckets)]
                 self.ao_ws = ops.attn_oproj_workspace(c.hidden, self.nh, self.nkv, self.D, self.ao_nc, dev)
-        # one-launch qkv + attention: per bucket whether it runs (fused-form buckets of one-row
-        # engines the kernel covers, where attn_oproj does not run)
-        self.qa_buckets: List[bool] = [False] * len(self.attn_buckets)
-        # (B = max_batch: one-row engines only, so a row's tokens never depend on what shared its steps)
+        # one-launch qkv + attention: per bucket its (chunk, grid) of the fused attention form, or
+        # None (B = max_batch: one-row engines only, so a row's tokens never depend on what shared
+        # their steps). Default: the fused-form buckets of short-qkv shards where attn_oproj does not
+        # run; "all": every bucket, ahead of attn_oproj, the long ones as 256-key chunks
+        self.qa_plan: List[Optional[tuple]] = [None] * len(self.attn_buckets)
         qa = str(self.ecfg.qkv_attn)
         qa_all = qa == "all"
         rows = (self.nh + 2 * self.nkv) * self.D
         if (self.on_gpu and qa not in ("0", "False", "") and B == 1 and (qa_all or rows < QKV_ATTN_MAX_ROWS)
                 and ops.qkv_attn_supported(self.nh, self.nkv, self.D, c.hidden)):
-            self.qa_buckets = [fused and ch in (128, 256) and self.bs % (ch // 4) == 0
-                               and (qa_all or not self.ao_chunks[i])
-                               for i, (_, ch, _, fused) in enumerate(self.attn_buckets)]
+            for i, (cap, ch, gc, fused) in enumerate(self.attn_buckets):
+                if fused and ch in (128, 256) and self.bs % (ch // 4) == 0 and (qa_all or not self.ao_chunks[i]):
+                    self.qa_plan[i] = (ch, gc)
+                elif qa_all and not fused and self.bs % 64 == 0:
+                    self.qa_plan[i] = (256, (cap + 255) // 256)
             if qa_all:  # the one launch replaces attn_oproj where both cover a bucket
-                self.ao_chunks = [0 if q else a for q, a in zip(self.qa_buckets, self.ao_chunks)]
-            if any(self.qa_buckets):
+                self.ao_chunks = [0 if q else a for q, a in zip(self.qa_plan, self.ao_chunks)]
+            if any(self.qa_plan):
                 self.qa_ws = ops.qkv_attn_workspace(self.nh, self.nkv, self.D, dev)
+        self.qa_buckets = [p is not None for p in self.qa_plan]
+        max_chunks = max([gc for _, _, gc, _ in self.attn_buckets] + [p[1] for p in self.qa_plan if p])
+        self.attn_part, self.attn_counters = ops.decode_attn_workspace(B, self.nh, self.nkv, self.D, max_chunks, dev)
         # set by a decode-attention merger that gave up on a partial (checked after every decode)
         self.attn_fault = torch.zeros(1, dtype=torch.int32, device=dev) if self.on_gpu else None
         if self.on_gpu:
@@ -612,7 +616,7 @@ class Engine:
         ops.embedding(self.tokens_in[:B], self.w.embed, out=h)
         bi = -1 if bucket is None else bucket
         ao_chunk = self.ao_chunks[bi] if B == 1 else 0
-        qa = B == 1 and self.qa_buckets[bi]
+        qa = self.qa_plan[bi] if B == 1 else None
         dbg = self._debug_layer_io  # eager debug steps only: each layer's input, then the last output
         for li, Lw in enumerate(self.w.layers):
             if dbg is not None:
@@ -620,8 +624,8 @@ class Engine:
             if qa:  # qkv projection + attention in one launch (one row), then o_proj
                 ops.qkv_attn(h, Lw.w_qkv, Lw.ln1, c.rms_eps, q, self.k_cache[li], self.v_cache[li], self.positions[:1],
                              self.slots[:1], self.cos_t, self.sin_t, self.block_tables[:1], self.seq_lens[:1], attn,
-                             part, self.attn_counters, self.qa_ws, self.nh, self.nkv, self.D, self.bs, chunk,
-                             grid_chunks, self.scale, fault=self.attn_fault)
+                             part, self.attn_counters, self.qa_ws, self.nh, self.nkv, self.D, self.bs, qa[0], qa[1],
+                             self.scale, fault=self.attn_fault)
                 self._row_parallel(attn, Lw.w_o, h)
             else:
                 ops.qkv_rope(h, Lw.w_qkv, Lw.ln1, c.rms_eps, q, self.k_cache[li], self.v_cache[li],

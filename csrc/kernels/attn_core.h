@@ -206,19 +206,6 @@ __device__ __forceinline__ void store_direct(const float* red, bf16_t* out_row, 
     out_row[hh * D + d] = f32_to_bf16(o / l);
   }
 }
-// ... as {bf16x2, tag} granules (dims (d, d + 1) of head hh at ogran[(hh D + d) / 2]), for consumers
-// in the same launch that poll the tags (qkv_attn.hip's o_proj blocks)
-template <int G, int D, int NW>
-__device__ __forceinline__ void store_direct_gran(const float* red, uint64_t* ogran, uint32_t tag, int tid) {
-  for (int idx = tid; idx < G * D / 2; idx += NW * 64) {
-    const int hh = (2 * idx) / D, d = (2 * idx) % D;
-    float o0, o1, m, l;
-    merge_waves<G, D, NW>(red, hh, d, o0, m, l);
-    merge_waves<G, D, NW>(red, hh, d + 1, o1, m, l);
-    __hip_atomic_store(ogran + idx, static_cast<uint64_t>(pack_bf16x2(o0 / l, o1 / l)) | (static_cast<uint64_t>(tag) << 32),
-                       __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  }
-}
 // ... written through as 4-B pairs, for a consumer in the same launch
 template <int G, int D, int NW>
 __device__ __forceinline__ void store_direct_sc1(const float* red, bf16_t* out_row, int tid) {
@@ -355,12 +342,11 @@ __device__ __forceinline__ void merge_rows(__amdgpu_buffer_rsrc_t rsrc, const ch
 // this launch read the epoch before it arrived). ctr = {top ticket, epoch, group tickets...}, one
 // kCtrPitch line each;
 // `flag` is one LDS word. Every block but the last returns inside.
-// OGRAN: the output is also published as {bf16x2, otag} granules at ogran (store_direct_gran's layout).
-template <int G, int D, int NW, bool SC1OUT = false, bool OGRAN = false>
+template <int G, int D, int NW, bool SC1OUT = false>
 __device__ __forceinline__ bool publish_and_merge(const float* red, float* part, int* ctr, int b, int nkv, int kvh,
                                                   int c, int nchunks, int gsize, int max_chunks, int max_groups,
                                                   uint32_t tag, bf16_t* out_row, char* smem, int* flag, int tid,
-                                                  int* fault, uint64_t* ogran = nullptr, uint32_t otag = 0) {
+                                                  int* fault) {
   constexpr int HQ = D / 4, RU = HQ + 1, Q = G * HQ;
   const int rows = max_chunks + max_groups;
   float* slab = part + (static_cast<int64_t>(b) * nkv + kvh) * rows * G * RU * 4;
@@ -409,13 +395,6 @@ __device__ __forceinline__ bool publish_and_merge(const float* red, float* part,
                          __HIP_MEMORY_SCOPE_AGENT);
     } else {
       *reinterpret_cast<u32x2*>(out_row + g * D + 4 * u) = o2;
-    }
-    if constexpr (OGRAN) {
-      const uint64_t t = static_cast<uint64_t>(otag) << 32;
-      __hip_atomic_store(ogran + (g * D + 4 * u) / 2, static_cast<uint64_t>(o2[0]) | t, __ATOMIC_RELAXED,
-                         __HIP_MEMORY_SCOPE_AGENT);
-      __hip_atomic_store(ogran + (g * D + 4 * u) / 2 + 1, static_cast<uint64_t>(o2[1]) | t, __ATOMIC_RELAXED,
-                         __HIP_MEMORY_SCOPE_AGENT);
     }
   }
   if (tid == 0) {

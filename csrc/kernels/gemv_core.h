@@ -25,10 +25,7 @@
 
 namespace llmc {
 
-enum { PRO_NONE = 0, PRO_NORM = 1, PRO_HANDOFF = 2 };
-// PRO_HANDOFF (qkv_attn.hip's o_proj blocks, M = 1): x is produced inside the same launch and
-// arrives as K / 2 {bf16x2, tag} granules at rope.granules (tag rope.gtag) from rope.nkv producers
-// (one region of K / 2 / nkv granules each); a lost granule sets *rope.hfault = 5.
+enum { PRO_NONE = 0, PRO_NORM = 1 };
 enum { EPI_BF16 = 0, EPI_F32 = 1, EPI_RESADD = 2, EPI_SILU = 3, EPI_ROPE = 4, EPI_COMBINE = 5, EPI_AR = 6 };
 
 // EPI_AR: a tensor-parallel rank's row-parallel projection (decode o_proj / down_proj) with the
@@ -59,7 +56,6 @@ struct RopeEpi {
   // = dims (d, d + 1); D/2 granules per head
   uint64_t* granules;
   uint32_t gtag;
-  int* hfault;  // PRO_HANDOFF: set to 5 when a hand-off granule never arrived (bounded spin)
 };
 
 // Batched decode (3 <= M <= 32 rows): the MFMA form in gemv_mfma.hip, same prologue/epilogues
@@ -190,40 +186,7 @@ __device__ __forceinline__ void gemv_block(const int bx, const int by, char* sme
   }
 
   // ---- prologue: x -> LDS (optionally RMS-normalised) ----
-  if constexpr (PRO == PRO_HANDOFF) {
-    static_assert(M == 1, "hand-off x: one row");
-    // one thread per producer polls its region's last granule (the weights' first batch is already
-    // in flight), then every thread gathers its chunks' granules, re-polling a straggler
-    const uint64_t* xg = rope.granules;
-    const int per = K / 2 / rope.nkv;
-    if (tid < rope.nkv) {
-      for (unsigned spins = 0; spins < kCarSpinLimit; ++spins) {
-        const uint64_t v = __hip_atomic_load(xg + (tid + 1) * per - 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        if (static_cast<uint32_t>(v >> 32) == rope.gtag) break;
-        __builtin_amdgcn_s_sleep(2);
-      }
-    }
-    __syncthreads();
-    for (int c = tid; c < nchunk; c += NT) {
-      uint64_t g[4];
-      for (unsigned spins = 0;; ++spins) {
-        bool ok = true;
-#pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          g[e] = __hip_atomic_load(xg + 4 * c + e, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-          ok = ok && static_cast<uint32_t>(g[e] >> 32) == rope.gtag;
-        }
-        if (ok) break;
-        if (spins >= kCarSpinLimit) {
-          if (rope.hfault != nullptr) __hip_atomic_store(rope.hfault, 5, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-          break;
-        }
-        __builtin_amdgcn_s_sleep(1);
-      }
-      reinterpret_cast<u32x4*>(xs)[c] = u32x4{static_cast<uint32_t>(g[0]), static_cast<uint32_t>(g[1]),
-                                              static_cast<uint32_t>(g[2]), static_cast<uint32_t>(g[3])};
-    }
-  } else if constexpr (PRO == PRO_NORM) {
+  if constexpr (PRO == PRO_NORM) {
     float(*red)[WAVES] = reinterpret_cast<float(*)[WAVES]>(smem + static_cast<size_t>(M) * K * sizeof(bf16_t));
     float ss[M];
 #pragma unroll

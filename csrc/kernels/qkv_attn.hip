@@ -33,15 +33,14 @@ namespace llmc {
 
 constexpr int kQaThreads = 256, kQaWaves = 4;
 
-template <int G, int D, bool OG>
+template <int G, int D>
 __device__ __forceinline__ void qa_attention(int c, int kvh, char* smem, const int32_t* __restrict__ block_table,
                                              int bt_len, int L, const bf16_t* __restrict__ k_cache,
                                              const bf16_t* __restrict__ v_cache, float* __restrict__ part,
                                              int* __restrict__ counters, bf16_t* __restrict__ out, int nh, int nkv,
                                              int bs, int nblocks, int chunk, int max_chunks, int gsize, int max_groups,
                                              float scale_log2, int* __restrict__ fault,
-                                             const uint64_t* __restrict__ granules, uint32_t htag,
-                                             uint64_t* __restrict__ ogran) {
+                                             const uint64_t* __restrict__ granules, uint32_t htag) {
   static_assert(G <= 16 && D % 32 == 0 && D <= 128, "shape");
   using ST = SubTile<G, D>;
   constexpr int HALF = D / 2;
@@ -149,62 +148,34 @@ __device__ __forceinline__ void qa_attention(int c, int kvh, char* smem, const i
   st.to_lds(red, wave, lane);
   __syncthreads();
   bf16_t* out_row = out + kvh * G * D;
-  // OG: the head group's output also goes to the o_proj blocks of this launch as granules
-  uint64_t* og = OG ? ogran + kvh * G * D / 2 : nullptr;
   if (nchunks == 1) {
     store_direct<G, D, kQaWaves>(red, out_row, tid);
-    if constexpr (OG) store_direct_gran<G, D, kQaWaves>(red, og, htag, tid);
     return;
   }
-  publish_and_merge<G, D, kQaWaves, false, OG>(red, part, ctr, 0, nkv, kvh, c, nchunks, gsize, max_chunks, max_groups,
-                                               tag, out_row, smem, flag, tid, fault, og, htag);
+  publish_and_merge<G, D, kQaWaves>(red, part, ctr, 0, nkv, kvh, c, nchunks, gsize, max_chunks, max_groups, tag,
+                                    out_row, smem, flag, tid, fault);
 }
 
-// OM (o_proj role): 0 none; 1 the one-row o_proj + residual (h += W_o . attention); 2 a TP rank's
-// row-parallel o_proj with the all-reduce in its epilogue (gemv_core.h EPI_AR, the engine's fused
-// buffer: h = sum over ranks, rank 0 adding the residual). The o_proj blocks come after every
-// segment: they issue their weight tile, then gather the attention output granules the mergers
-// published (PRO_HANDOFF). They read the hand-off epoch at start and say so (a release increment
-// of the started count); the last attention block to exit waits for all of them before it
-// advances the epoch.
-template <int G, int D, int OM>
+template <int G, int D>
 __global__ __launch_bounds__(kQaThreads) void qkv_attn_kernel(
     const bf16_t* __restrict__ x, const bf16_t* __restrict__ norm_w, float eps, const bf16_t* __restrict__ W, int N,
     int K, RopeEpi rope, const int32_t* __restrict__ block_table, int bt_len,
     const int32_t* __restrict__ seq_len, float* __restrict__ part, int* __restrict__ counters, bf16_t* __restrict__ out,
     int bs, int nblocks, int chunk, int gc, int max_chunks, int gsize, int max_groups, float scale_log2,
-    int* __restrict__ fault, uint64_t* __restrict__ granules, int* __restrict__ hctr, const bf16_t* __restrict__ W_o,
-    bf16_t* __restrict__ h, int H, uint64_t* __restrict__ ogran, CarArgs ar) {
+    int* __restrict__ fault, uint64_t* __restrict__ granules, int* __restrict__ hctr) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   // Block order: one segment per kv head g = [its G q heads' GEMV blocks | its k head's | its v
   // head's | its gc attention blocks], so head g's attention starts after 1 / nkv of the projection
-  // has been dispatched and still waits only on lower-index blocks; then the o_proj blocks
+  // has been dispatched and still waits only on lower-index blocks
   constexpr int QB = G * D / kQaWaves, KB = D / kQaWaves;  // GEMV blocks (4 rows each) per segment part
   const int seg = QB + 2 * KB + gc;
-  const int nkv = rope.nkv;
+  const int g = blockIdx.x / seg, r = blockIdx.x % seg;
   const uint32_t htag =
       static_cast<uint32_t>(__hip_atomic_load(hctr + kCtrPitch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) + 1u;
-  if constexpr (OM != 0) {
-    const int ob = static_cast<int>(blockIdx.x) - seg * nkv;
-    if (ob >= 0) {  // block-uniform: o_proj rows [4 ob, 4 ob + 4)
-      if (threadIdx.x == 0)  // started (after the epoch read above: release)
-        __hip_atomic_fetch_add(hctr + 2 * kCtrPitch, 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
-      RopeEpi ro{};
-      ro.granules = ogran;
-      ro.gtag = htag;
-      ro.nkv = nkv;
-      ro.hfault = fault;
-      const int Ko = rope.nh * D;
-      gemv_block<1, kQaThreads, 1, 8, PRO_HANDOFF, OM == 2 ? EPI_AR : EPI_RESADD, false>(
-          ob, 0, smem, nullptr, Ko, nullptr, 0.f, W_o, h, H, H, Ko, nullptr, 1, ro, ar);
-      return;
-    }
-  }
-  const int g = blockIdx.x / seg, r = blockIdx.x % seg;
   if (r < QB + 2 * KB) {  // block-uniform: the projection of 4 rows
     const int row0 = r < QB ? g * G * D + kQaWaves * r
                             : (r < QB + KB ? (rope.nh + g) * D + kQaWaves * (r - QB)
-                                           : (rope.nh + nkv + g) * D + kQaWaves * (r - QB - KB));
+                                           : (rope.nh + rope.nkv + g) * D + kQaWaves * (r - QB - KB));
     RopeEpi re = rope;
     re.granules = granules;
     re.gtag = htag;
@@ -215,22 +186,13 @@ __global__ __launch_bounds__(kQaThreads) void qkv_attn_kernel(
   const int c = r - QB - 2 * KB;
   const int L = ld_scalar(seq_len);
   if (c * chunk < L)
-    qa_attention<G, D, OM != 0>(c, g, smem, block_table, bt_len, L, rope.k_cache, rope.v_cache, part, counters, out,
-                                rope.nh, nkv, bs, nblocks, chunk, max_chunks, gsize, max_groups, scale_log2, fault,
-                                granules, htag, ogran);
+    qa_attention<G, D>(c, g, smem, block_table, bt_len, L, rope.k_cache, rope.v_cache, part, counters, out, rope.nh,
+                       rope.nkv, bs, nblocks, chunk, max_chunks, gsize, max_groups, scale_log2, fault, granules, htag);
   // every attention block counts its exit; the last advances the hand-off epoch (every GEMV block
-  // has published by now: each one's granules were waited for, so each one read the epoch; with
-  // o_proj blocks, once every one of them has read it too)
+  // has published by now: each one's granules were waited for, so each one read the epoch)
   if (threadIdx.x == 0) {
-    if (__hip_atomic_fetch_add(hctr, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == gc * nkv - 1) {
-      if constexpr (OM != 0) {
-        const int no = static_cast<int>(gridDim.x) - seg * nkv;
-        for (unsigned spins = 0; spins < kSpinLimit; ++spins) {
-          if (__hip_atomic_load(hctr + 2 * kCtrPitch, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) >= no) break;
-          __builtin_amdgcn_s_sleep(2);
-        }
-        __hip_atomic_store(hctr + 2 * kCtrPitch, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      }
+    const int A = gc * rope.nkv;
+    if (__hip_atomic_fetch_add(hctr, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == A - 1) {
       __hip_atomic_store(hctr, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       __hip_atomic_store(hctr + kCtrPitch, static_cast<int>(htag), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
@@ -257,66 +219,39 @@ extern "C" int llmc_qkv_attn_check(int nh, int nkv, int D, int K) {
 // out = attention(q, cache keys < L - 1 and this token's key) in the fused form: grid_chunks
 // blocks of `chunk` (128 / 256) keys per kv head, bs % (chunk / 4) == 0. part / counters: the
 // decode-attention workspace (max_chunks >= grid_chunks, its row 0). granules: u64 [(nh + 2 nkv)
-// D / 2 + nh D / 2] (the last nh D / 2: the attention output for the o_proj blocks); hctr: int32
-// [3 kCtrPitch]; both zeroed once. omode 1: also h[0] += W_o . out (W_o [H, nh D]); omode 2: a TP
-// rank's row-parallel o_proj with the all-reduce fused (bases / rank / world / cap: the engine's
-// fused-all-reduce buffer, car_proto.h).
+// D / 2]; hctr: int32 [2 kCtrPitch]; both zeroed once.
 extern "C" int llmc_qkv_attn(const void* x, const void* norm_w, float eps, const void* W, int K, void* q_out,
                              void* k_cache, void* v_cache, const void* positions, const void* slots, const void* cos_t,
                              const void* sin_t, const void* block_table, int bt_len, const void* seq_len, void* part,
                              void* counters, void* out, int nh, int nkv, int D, int bs, int nblocks, int chunk,
                              int grid_chunks, int max_chunks, float scale, void* fault, void* granules, void* hctr,
-                             int omode, const void* W_o, void* h, int H, const void* const* bases, int rank, int world,
-                             size_t cap, hipStream_t s) {
+                             hipStream_t s) {
   if (llmc_qkv_attn_check(nh, nkv, D, K) != 0) return -1;
   if ((chunk != 128 && chunk != 256) || bs % (chunk / 4) != 0 || grid_chunks < 1 || grid_chunks > max_chunks ||
       bt_len < 1 || nblocks < 1 || counters == nullptr || granules == nullptr || hctr == nullptr)
     return -1;
-  const int G = nh / nkv, N = (nh + 2 * nkv) * D, Ko = nh * D;
-  CarArgs ar{};
-  int no = 0;  // o_proj blocks
-  if (omode != 0) {
-    if (W_o == nullptr || h == nullptr || H < 4 || H % 4 != 0 || Ko % 8 != 0 ||
-        static_cast<size_t>(Ko) * 2 + 64 > 64 * 1024)
-      return -1;
-    no = H / kQaWaves;
-    if (omode == 2) {
-      if (bases == nullptr || world < 2 || world > kMaxRanks || rank < 0 || rank >= world || no > kMaxBlocks ||
-          static_cast<size_t>(no) * kArGranulesPerBlock * 8 > cap / kMaxRanks)
-        return -1;
-      for (int r = 0; r < kMaxRanks; ++r)
-        ar.P.base[r] = r < world ? static_cast<char*>(const_cast<void*>(bases[r])) : nullptr;
-      ar.rank = rank;
-      ar.world = world;
-      ar.cap = static_cast<long>(cap);
-    }
-  }
+  const int G = nh / nkv, N = (nh + 2 * nkv) * D;
   const int max_groups = llmc_attn_decode_groups(max_chunks);
   const int gsize = grid_chunks > kAttnOneLevel ? kAttnGroup : grid_chunks;
-  const size_t lds_gemv = static_cast<size_t>(K > Ko ? K : Ko) * 2 + 2 * kQaWaves * sizeof(float);
+  const size_t lds_gemv = static_cast<size_t>(K) * 2 + 2 * kQaWaves * sizeof(float);
   const size_t lds_attn = kQaWaves * 32 * kVRowBytes + static_cast<size_t>(kQaWaves) * G * (D + 2) * sizeof(float) +
                           16 + static_cast<size_t>(G * D + 2 * D) * sizeof(bf16_t);
   const size_t lds = lds_gemv > lds_attn ? lds_gemv : lds_attn;
   if (lds > 64 * 1024) return -4;
   RopeEpi rope{(bf16_t*)q_out, nh * D, (bf16_t*)k_cache, (bf16_t*)v_cache, (const int32_t*)positions,
                (const int32_t*)slots, (const float*)cos_t, (const float*)sin_t, nh, nkv, D, bs};
-  const dim3 grid(N / kQaWaves + grid_chunks * nkv + no);
+  const dim3 grid(N / kQaWaves + grid_chunks * nkv);
   const float sl2 = scale * 1.4426950408889634f;
-  uint64_t* ogran = static_cast<uint64_t*>(granules) + static_cast<size_t>(N) / 2;
-#define LLMC_QA(GG, DD, OM)                                                                                        \
-  qkv_attn_kernel<GG, DD, OM><<<grid, kQaThreads, lds, s>>>(                                                       \
-      (const bf16_t*)x, (const bf16_t*)norm_w, eps, (const bf16_t*)W, N, K, rope, (const int32_t*)block_table,     \
-      bt_len, (const int32_t*)seq_len, (float*)part, (int*)counters, (bf16_t*)out, bs, nblocks, chunk, grid_chunks, \
-      max_chunks, gsize, max_groups, sl2, (int*)fault, (uint64_t*)granules, (int*)hctr, (const bf16_t*)W_o,         \
-      (bf16_t*)h, H, ogran, ar)
-#define LLMC_QA_OM(GG, DD)                    \
-  if (omode == 0) LLMC_QA(GG, DD, 0);         \
-  else if (omode == 1) LLMC_QA(GG, DD, 1);    \
-  else LLMC_QA(GG, DD, 2)
-#define LLMC_QA_D(GG)                       \
-  if (D == 64) LLMC_QA_OM(GG, 64);          \
-  else if (D == 96) LLMC_QA_OM(GG, 96);     \
-  else LLMC_QA_OM(GG, 128)
+#define LLMC_QA(GG, DD)                                                                                         \
+  qkv_attn_kernel<GG, DD><<<grid, kQaThreads, lds, s>>>(                                                        \
+      (const bf16_t*)x, (const bf16_t*)norm_w, eps, (const bf16_t*)W, N, K, rope,                                \
+      (const int32_t*)block_table, bt_len, (const int32_t*)seq_len, (float*)part, (int*)counters, (bf16_t*)out,   \
+      bs, nblocks, chunk, grid_chunks, max_chunks, gsize, max_groups, sl2, (int*)fault, (uint64_t*)granules,      \
+      (int*)hctr)
+#define LLMC_QA_D(GG)                     \
+  if (D == 64) LLMC_QA(GG, 64);           \
+  else if (D == 96) LLMC_QA(GG, 96);      \
+  else LLMC_QA(GG, 128)
   switch (G) {
     case 1: LLMC_QA_D(1); break;
     case 2: LLMC_QA_D(2); break;
@@ -324,7 +259,6 @@ extern "C" int llmc_qkv_attn(const void* x, const void* norm_w, float eps, const
     default: LLMC_QA_D(8); break;
   }
 #undef LLMC_QA_D
-#undef LLMC_QA_OM
 #undef LLMC_QA
   return static_cast<int>(hipGetLastError());
 }

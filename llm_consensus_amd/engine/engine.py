@@ -74,9 +74,6 @@ class EngineConfig:
     # QKV_ATTN_MAX_ROWS rows (the TP ranks', where it measured faster: profiles/r4_qkv_attn.md);
     # "all": every covered shape and fused bucket, ahead of attn_oproj; "0": never (LLMC_QKV_ATTN)
     qkv_attn: str = dataclasses.field(default_factory=lambda: os.environ.get("LLMC_QKV_ATTN", "1"))
-    # ... and the o_proj (+ residual; on TP ranks with the fused all-reduce) in the same launch
-    # (LLMC_QKV_ATTN_O=0 keeps it a GEMV launch of its own)
-    qkv_attn_o: bool = dataclasses.field(default_factory=lambda: os.environ.get("LLMC_QKV_ATTN_O", "1") != "0")
 
 
 FUSED_CHUNK_SMALL, FUSED_CHUNK_LARGE = 128, 256
@@ -307,11 +304,6 @@ class Engine:
             if any(self.qa_plan):
                 self.qa_ws = ops.qkv_attn_workspace(self.nh, self.nkv, self.D, dev)
         self.qa_buckets = [p is not None for p in self.qa_plan]
-        # the o_proj in the same launch: one rank, or a TP rank whose row-parallel all-reduce can run
-        # in the GEMV epilogue (the fused buffer; the RCCL fallback keeps the o_proj launch)
-        # (one o_proj block per 4 rows: the fused buffer's per-block epochs cover 1024 of them)
-        self.qa_o = bool(self.ecfg.qkv_attn_o and any(self.qa_buckets) and c.hidden % 4 == 0
-                         and (self.tp.size == 1 or (self.tp.custom_fused is not None and c.hidden // 4 <= 1024)))
         max_chunks = max([gc for _, _, gc, _ in self.attn_buckets] + [p[1] for p in self.qa_plan if p])
         self.attn_part, self.attn_counters = ops.decode_attn_workspace(B, self.nh, self.nkv, self.D, max_chunks, dev)
         # set by a decode-attention merger that gave up on a partial (checked after every decode)
@@ -629,14 +621,12 @@ class Engine:
         for li, Lw in enumerate(self.w.layers):
             if dbg is not None:
                 dbg.append(h.clone())
-            if qa:  # qkv projection + attention (+ o_proj) in one launch (one row)
+            if qa:  # qkv projection + attention in one launch (one row), then o_proj
                 ops.qkv_attn(h, Lw.w_qkv, Lw.ln1, c.rms_eps, q, self.k_cache[li], self.v_cache[li], self.positions[:1],
                              self.slots[:1], self.cos_t, self.sin_t, self.block_tables[:1], self.seq_lens[:1], attn,
                              part, self.attn_counters, self.qa_ws, self.nh, self.nkv, self.D, self.bs, qa[0], qa[1],
-                             self.scale, fault=self.attn_fault, w_o=Lw.w_o if self.qa_o else None, h=h,
-                             car=self.tp.custom_fused if self.qa_o and self.tp.size > 1 else None)
-                if not self.qa_o:
-                    self._row_parallel(attn, Lw.w_o, h)
+                             self.scale, fault=self.attn_fault)
+                self._row_parallel(attn, Lw.w_o, h)
             else:
                 ops.qkv_rope(h, Lw.w_qkv, Lw.ln1, c.rms_eps, q, self.k_cache[li], self.v_cache[li],
                              self.positions[:B], self.slots[:B], self.cos_t, self.sin_t, self.nh, self.nkv, self.D,

@@ -202,35 +202,3 @@ def test_engine_qkv_attn_all_replaces_attn_oproj(cuda):
             err = (la[i] - l2[i]).abs().max().item()
             assert err < 0.02 * max(1.0, l2[i].abs().max().item()), (plen, i, err)
     assert int(ea.attn_fault.item()) == 0
-
-
-@pytest.mark.parametrize("nh,nkv,D,K", [SHAPES[0], SHAPES[1], SHAPES[2]])
-@pytest.mark.parametrize("L", [1, 129, 2048, 5000])
-def test_qkv_attn_with_oproj(cuda, nh, nkv, D, K, L):
-    """The o_proj in the same launch (its blocks gather the attention output granules): h += W_o .
-    out, bit for bit the o GEMV (EPI_RESADD) on the launch's own attention output; three launches
-    on one workspace (the started count re-armed, the epoch advanced)."""
-    H = K
-    cs = _Case(nh, nkv, D, K, L, seed=7 + L)
-    chunk, gc = _bucket(L)
-    scale = 1 / math.sqrt(D)
-    w_o = (torch.randn(H, nh * D, device="cuda") / math.sqrt(nh * D)).to(BF)
-    h0 = torch.randn(1, H, device="cuda").to(BF)
-    part, ctr = ops.decode_attn_workspace(1, nh, nkv, D, gc, "cuda", fused=True)
-    ws = ops.qkv_attn_workspace(nh, nkv, D, "cuda")
-    fault = torch.zeros(1, dtype=torch.int32, device="cuda")
-    for _ in range(3):
-        kc, vc = cs.kc.clone(), cs.vc.clone()
-        q = torch.zeros(1, nh * D, dtype=BF, device="cuda")
-        out = torch.zeros(1, nh * D, dtype=BF, device="cuda")
-        h = h0.clone()
-        ops.qkv_attn(cs.x, cs.W, cs.nw, 1e-5, q, kc, vc, cs.pos, cs.slots, cs.cos, cs.sin, cs.bt, cs.sl, out, part,
-                     ctr, ws, nh, nkv, D, cs.bs, chunk, gc, scale, fault=fault, w_o=w_o, h=h)
-        torch.cuda.synchronize()
-        assert int(fault.item()) == 0
-        h_ref = h0.clone()
-        ops.linear(out, w_o, ops.EPI_RESADD, out=h_ref)
-        torch.cuda.synchronize()
-        assert torch.equal(h, h_ref), (h.float() - h_ref.float()).abs().max().item()
-    assert int(ws[1][0].item()) == 0 and int(ws[1][2 * ops.ATTN_CTR_PITCH].item()) == 0
-    assert int(ws[1][ops.ATTN_CTR_PITCH].item()) == 3

@@ -10,4 +10,5 @@ source scripts/gpu/steps.sh
 step engine 260 python -u bench.py --steps 2 --warmup 1
 step cli 320 python -u bench.py --path cli --steps 2 --warmup 1
 step mt4096 300 python -u bench.py --steps 2 --warmup 1 --max-tokens 4096
-step reh_prof 240 bash scripts/prof_tp_rehearsal.sh ${tag}_rehprof --shape-tp 8 --world 2 --tokens 128 --reps 1
+step reh_k1 240 python -u scripts/tp_rehearsal.py --shape-tp 8 --world 2 --tokens 128 --reps 1 --trace-kernels 1
+step reh_k0 240 python -u scripts/tp_rehearsal.py --shape-tp 8 --world 2 --tokens 128 --reps 1 --trace-kernels 1 --fused-ar 0

@@ -60,13 +60,26 @@ def _worker(rank, a, port, q):
             tp_s = time.perf_counter() - t
             e.free_sequence(s)
             res.append(1000 * (dt - tp_s) / len(out))
-        q.put((rank, ok, tp.custom_fused is not None, min(res), tp.custom_timed_out()))
+        kcount = None
+        if a.trace_kernels:  # the decode's kernels by name (torch.profiler / roctracer), 32 tokens
+            from torch.profiler import ProfilerActivity, profile
+
+            torch.cuda.synchronize()
+            dist.barrier()
+            with profile(activities=[ProfilerActivity.CUDA]) as prof:
+                e.generate_ids(prompt[:64], 32, stop_on_eos=False)
+                torch.cuda.synchronize()
+            kcount = {}
+            for ev in prof.key_averages():
+                if ev.device_type.name == "CUDA" or "CUDA" in str(ev.device_type):
+                    kcount[ev.key] = kcount.get(ev.key, 0) + ev.count
+        q.put((rank, ok, tp.custom_fused is not None, min(res), tp.custom_timed_out(), kcount))
         dist.barrier()
         dist.destroy_process_group()
     except Exception as ex:  # noqa: BLE001
         import traceback
 
-        q.put((rank, False, False, repr(ex) + traceback.format_exc(), True))
+        q.put((rank, False, False, repr(ex) + traceback.format_exc(), True, None))
 
 
 def main():
@@ -81,6 +94,8 @@ def main():
     ap.add_argument("--reps", type=int, default=2)
     ap.add_argument("--fused-ar", type=int, default=1)
     ap.add_argument("--cu-mask", type=int, default=1, help="0: ranks time-share every CU")
+    ap.add_argument("--trace-kernels", type=int, default=0,
+                    help="1: rank 0 lists the kernels of 32 decode tokens (prefill of 64 included) by name")
     a = ap.parse_args()
     with socket.socket() as s:
         s.bind(("127.0.0.1", 0))
@@ -93,7 +108,7 @@ def main():
     res = sorted(q.get(timeout=900) for _ in range(a.world))
     for p in procs:
         p.join(timeout=60)
-    for rank, ok, fused, ms, tmo in res:
+    for rank, ok, fused, ms, tmo, _ in res:
         if isinstance(ms, str):
             print(f"rank {rank} failed: {ms}", flush=True)
             sys.exit(1)
@@ -101,6 +116,12 @@ def main():
     print(f"{a.model} shape TP={a.shape_tp} over {a.world} ranks (cu_mask={a.cu_mask}, custom={res[0][1]}, "
           f"fused_ar={res[0][2]}) ctx={a.ctx}: decode {worst:.3f} ms/token (ranks {[round(r[3], 3) for r in res]}), "
           f"timed_out={any(r[4] for r in res)}", flush=True)
+    if res[0][5]:
+        print("rank 0 kernels over 32 decode tokens (+ a 64-token prefill), launches by name:", flush=True)
+        for name, n in sorted(res[0][5].items(), key=lambda kv: -kv[1])[:25]:
+            print(f"  {n:6d}  {name[:110]}", flush=True)
+        car = sum(n for k, n in res[0][5].items() if "car_" in k)
+        print(f"standalone custom all-reduce / all-gather launches (car_*): {car}", flush=True)
 
 
 if __name__ == "__main__":

@@ -8,14 +8,13 @@
 // GEMV's boundary. Here they run under the GEMV: the K/V of the cached keys do not depend on this
 // token, so the attention blocks request them at once and only wait for the rotated q.
 //
-// Grid: one segment per kv head g: the GEMV blocks of its G q heads, of its k head and of its v head
-// (gemv_core.h gemv_block: 4 waves x 1 row, 8 x 16-B loads per lane in flight; every row's dot
-// product in the same order as the qkv_rope launch, whose geometry for outputs under 2048 rows this
-// is, so there q / k / v are the same bits; wider outputs group the RMS norm's sum of squares
-// differently, last bits), then its gc
-// fused-form attention chunks (attn_core.h SubTile, 4 waves x 32 / 64 keys of one page). An
-// attention block only waits on GEMV blocks of its own segment, which have lower indices and are
-// dispatched first: no wait is on a block that has not started.
+// Grid: the GEMV blocks (gemv_core.h gemv_block: 4 waves x 1 row, 8 x 16-B loads per lane in
+// flight; every row's dot product in the same order as the qkv_rope launch, whose geometry for
+// outputs under 2048 rows this is, so there q / k / v are the same bits; wider outputs group the
+// RMS norm's sum of squares differently, last bits), then gc fused-form attention chunks per kv
+// head (attn_core.h SubTile, 4 waves x 32 / 64 keys of one page). An attention block only waits on
+// GEMV blocks, which have lower indices and are dispatched first: no wait is on a block that has
+// not started.
 //
 // Hand-off: the GEMV epilogue publishes every rotated q / k pair and v pair as an 8-B {bf16x2, tag}
 // granule (RopeEpi::granules: one single-copy-atomic write-through store, the data IS the flag,
@@ -164,26 +163,22 @@ __global__ __launch_bounds__(kQaThreads) void qkv_attn_kernel(
     int bs, int nblocks, int chunk, int gc, int max_chunks, int gsize, int max_groups, float scale_log2,
     int* __restrict__ fault, uint64_t* __restrict__ granules, int* __restrict__ hctr) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  // Block order: one segment per kv head g = [its G q heads' GEMV blocks | its k head's | its v
-  // head's | its gc attention blocks], so head g's attention starts after 1 / nkv of the projection
-  // has been dispatched and still waits only on lower-index blocks
-  constexpr int QB = G * D / kQaWaves, KB = D / kQaWaves;  // GEMV blocks (4 rows each) per segment part
-  const int seg = QB + 2 * KB + gc;
-  const int g = blockIdx.x / seg, r = blockIdx.x % seg;
+  // Block order: every GEMV block (4 rows each, natural row order), then the gc attention blocks
+  // of each kv head; an attention block only waits on lower-index blocks. (Per-head segments —
+  // a head's GEMV blocks, then its attention blocks — measured the same on one kv head and 3 %
+  // slower at 17k keys on two: profiles/r4_qkv_attn.md.)
+  const int nq = N / kQaWaves;
   const uint32_t htag =
       static_cast<uint32_t>(__hip_atomic_load(hctr + kCtrPitch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) + 1u;
-  if (r < QB + 2 * KB) {  // block-uniform: the projection of 4 rows
-    const int row0 = r < QB ? g * G * D + kQaWaves * r
-                            : (r < QB + KB ? (rope.nh + g) * D + kQaWaves * (r - QB)
-                                           : (rope.nh + rope.nkv + g) * D + kQaWaves * (r - QB - KB));
+  if (static_cast<int>(blockIdx.x) < nq) {  // block-uniform: the projection of 4 rows
     RopeEpi re = rope;
     re.granules = granules;
     re.gtag = htag;
-    gemv_block<1, kQaThreads, 1, 8, PRO_NORM, EPI_ROPE, false>(row0 / kQaWaves, 0, smem, x, K, norm_w, eps, W, nullptr,
-                                                               0, N, K, nullptr, 1, re, CarArgs{});
+    gemv_block<1, kQaThreads, 1, 8, PRO_NORM, EPI_ROPE, false>(blockIdx.x, 0, smem, x, K, norm_w, eps, W, nullptr, 0, N,
+                                                               K, nullptr, 1, re, CarArgs{});
     return;
   }
-  const int c = r - QB - 2 * KB;
+  const int g = (blockIdx.x - nq) / gc, c = (blockIdx.x - nq) % gc;
   const int L = ld_scalar(seq_len);
   if (c * chunk < L)
     qa_attention<G, D>(c, g, smem, block_table, bt_len, L, rope.k_cache, rope.v_cache, part, counters, out, rope.nh,

@@ -143,6 +143,26 @@ def attn_buckets(ctxmax: int, blocks_per_head: int = 32, fused_max: int = 4096, 
         cap *= 2
 
 
+def qkv_attn_plan(buckets: List[tuple], ao_chunks: List[int], mode: str, qkv_rows: int, bs: int):
+    """Per decode-attention bucket the (keys per block, blocks per kv head) of the one-launch qkv +
+    attention (csrc/kernels/qkv_attn.hip) or None, and the attn_oproj chunks it leaves, for a one-row
+    engine whose shape the kernel covers. ``mode`` (EngineConfig.qkv_attn): "0" never; "1" the
+    fused-form buckets of shards with fewer than QKV_ATTN_MAX_ROWS qkv rows where attn_oproj does not
+    run (the TP ranks: profiles/r4_qkv_attn.md); "all" every bucket, ahead of attn_oproj, the split-form
+    ones as 256-key blocks (measured slower on wide outputs; A/B runs)."""
+    plan: List[Optional[tuple]] = [None] * len(buckets)
+    if mode in ("0", "False", "") or (mode != "all" and qkv_rows >= QKV_ATTN_MAX_ROWS):
+        return plan, list(ao_chunks)
+    qa_all = mode == "all"
+    for i, (cap, ch, gc, fused) in enumerate(buckets):
+        if fused and ch in (128, 256) and bs % (ch // 4) == 0 and (qa_all or not ao_chunks[i]):
+            plan[i] = (ch, gc)
+        elif qa_all and not fused and bs % 64 == 0:
+            plan[i] = (256, (cap + 255) // 256)
+    ao = [0 if q else a for q, a in zip(plan, ao_chunks)] if qa_all else list(ao_chunks)
+    return plan, ao
+
+
 def split_blocks_per_head(nh: int, nkv: int) -> int:
     """Grid of the split (long-context) attention form per kv head: ~one block per CU over the row's
     kv heads (256; 512 without GQA, where a block's range costs less). A TP=8 rank's single kv
@@ -289,18 +309,9 @@ class Engine:
         # their steps). Default: the fused-form buckets of short-qkv shards where attn_oproj does not
         # run; "all": every bucket, ahead of attn_oproj, the long ones as 256-key chunks
         self.qa_plan: List[Optional[tuple]] = [None] * len(self.attn_buckets)
-        qa = str(self.ecfg.qkv_attn)
-        qa_all = qa == "all"
-        rows = (self.nh + 2 * self.nkv) * self.D
-        if (self.on_gpu and qa not in ("0", "False", "") and B == 1 and (qa_all or rows < QKV_ATTN_MAX_ROWS)
-                and ops.qkv_attn_supported(self.nh, self.nkv, self.D, c.hidden)):
-            for i, (cap, ch, gc, fused) in enumerate(self.attn_buckets):
-                if fused and ch in (128, 256) and self.bs % (ch // 4) == 0 and (qa_all or not self.ao_chunks[i]):
-                    self.qa_plan[i] = (ch, gc)
-                elif qa_all and not fused and self.bs % 64 == 0:
-                    self.qa_plan[i] = (256, (cap + 255) // 256)
-            if qa_all:  # the one launch replaces attn_oproj where both cover a bucket
-                self.ao_chunks = [0 if q else a for q, a in zip(self.qa_plan, self.ao_chunks)]
+        if self.on_gpu and B == 1 and ops.qkv_attn_supported(self.nh, self.nkv, self.D, c.hidden):
+            self.qa_plan, self.ao_chunks = qkv_attn_plan(self.attn_buckets, self.ao_chunks, str(self.ecfg.qkv_attn),
+                                                         (self.nh + 2 * self.nkv) * self.D, self.bs)
             if any(self.qa_plan):
                 self.qa_ws = ops.qkv_attn_workspace(self.nh, self.nkv, self.D, dev)
         self.qa_buckets = [p is not None for p in self.qa_plan]

@@ -55,3 +55,30 @@ def test_cpu_path_is_qkv_rope_then_attention():
     ref = oracle.attn_decode(q2, kc2, vc2, bt, sl, nh, nkv, D, bs, scale)
     assert torch.equal(q, q2) and torch.equal(kc1, kc2) and torch.equal(vc1, vc2)
     assert torch.equal(out, ref.to(out.dtype))
+
+
+def test_engine_plan_policy():
+    """Which buckets an engine runs as one qkv + attention launch (engine.qkv_attn_plan)."""
+    from llm_consensus_amd.engine.engine import attn_buckets, qkv_attn_plan, split_blocks_per_head
+
+    def plan(nh, nkv, ctx, mode, ao=None):
+        b = attn_buckets(ctx, split_blocks_per_head(nh, nkv), 4096, nh // nkv, nkv)
+        return b, qkv_attn_plan(b, ao or [0] * len(b), mode, (nh + 2 * nkv) * 128, 64)
+
+    # a TP=8 rank of Llama-3-8B (768 qkv rows): every fused bucket, the bucket's own chunking
+    b, (p, _) = plan(4, 1, 20000, "1")
+    assert all(q == (ch, gc) for q, (_, ch, gc, fused) in zip(p, b) if fused) and any(p)
+    # the whole model (6144 rows) keeps two launches by default ...
+    b, (p, _) = plan(32, 8, 9400, "1")
+    assert not any(p)
+    # ... "all" takes every bucket (the split-form ones as 256-key blocks) and drops attn_oproj there
+    ao = [256 if cap >= 4096 else 0 for cap, _, _, _ in b]
+    _, (p, ao2) = plan(32, 8, 9400, "all", ao)
+    assert all(p) and not any(ao2)
+    assert p[-1][0] == 256 and p[-1][1] * 256 >= b[-1][0]
+    # default mode never takes a bucket attn_oproj runs
+    b, (p, ao2) = plan(4, 1, 9400, "1", [0, 0, 0, 256, 0])
+    assert p[3] is None and ao2[3] == 256
+    # "0": off
+    _, (p, _) = plan(4, 1, 9400, "0")
+    assert not any(p)

@@ -143,9 +143,12 @@ def _batch_worker(rank, world, port, q):
         h.engine = _FakeEngine(rank)
         h.q = queue.Queue()
         h._stash = W._EMPTY
-        # arrivals: the leader sees r2 inside its 5 ms window and r3 after it; the follower sees
-        # r2 only after 40 ms (it must still batch it) and r3 right behind it (it must not)
-        late = {0: (0.002, 0.060), 1: (0.040, 0.041)}[rank]
+        # a 200 ms batching window (instead of the default 5 ms) so thread wake-up jitter on a
+        # loaded host cannot move an arrival across it: the leader sees r2 inside its window and
+        # r3 after it; the follower sees r2 only after 400 ms (it must still batch it) and r3 right
+        # behind it (it must not)
+        W.BATCH_WINDOW_S = 0.2
+        late = {0: (0.020, 0.600), 1: (0.400, 0.410)}[rank]
 
         def feed():
             time.sleep(late[0])

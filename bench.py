@@ -207,6 +207,15 @@ def make_plan(args, world: int):
     raise SystemExit(f"unknown --config {args.config}")
 
 
+def colocated_tp(resp_plan, idx) -> bool:
+    """Whether the tensor-parallel responder engine of plan entries ``idx`` shares a GPU with other
+    responders that decode at the same time: it then keeps the separate (64-block) all-reduce
+    launch instead of the row-parallel GEMVs' fused epilogue, whose 256 blocks would spin on the
+    peer GPU while holding CUs the co-located engine needs (EngineConfig.fused_ar)."""
+    ranks = set(resp_plan[idx[0]]["ranks"])
+    return len(ranks) > 1 and any(ranks & set(o["ranks"]) for j, o in enumerate(resp_plan) if j not in idx)
+
+
 def config_name(args, world: int, resp, judge) -> str:
     """Which BASELINE.json config this run is, and how a variant differs from its wording."""
     if args.config != "fanout":
@@ -616,7 +625,8 @@ def main() -> None:
         if tp.size > 1:
             tp_members.append((name, e["ranks"], tp))
         eng = Engine(cfg, EngineConfig(device=dev, max_context=ctx, seed=e["seed"], steps_per_graph=args.steps_per_graph,
-                                       use_graphs=graphs, max_batch=len(idx)), tp=tp, name=name)
+                                       use_graphs=graphs, max_batch=len(idx),
+                                       fused_ar=not colocated_tp(resp_plan, idx)), tp=tp, name=name)
         responders.append((idx, eng, ids, tok))
     jtp_grp = tp_group(judge_plan["ranks"])
     if len(judge_plan["ranks"]) > 1:
@@ -837,7 +847,8 @@ def main() -> None:
         judge_stats = dict(judge_stats, judge_prompt_tokens=int(jt[0].item()), judge_prefill_s=float(jt[1].item()),
                            judge_decode_s=float(jt[2].item()), judge_ttft_s=float(jt[3].item()))
     # every TP engine's custom-collective state at the end, from every rank that holds a shard
-    ar_state = {e.name: {"custom": e.tp.custom is not None, "fused": e.tp.custom_fused is not None,
+    ar_state = {e.name: {"custom": e.tp.custom is not None,
+                         "fused": e.tp.custom_fused is not None and e.ecfg.fused_ar,
                          "timed_out": bool(e.tp.custom_timed_out())}
                 for e in [e for _, e, _, _ in responders] + ([judge] if judge is not None else []) if e.tp.size > 1}
     if world > 1:

@@ -74,6 +74,11 @@ class EngineConfig:
     # QKV_ATTN_MAX_ROWS rows (the TP ranks', where it measured faster: profiles/r4_qkv_attn.md);
     # "all": every covered shape and fused bucket, ahead of attn_oproj; "0": never (LLMC_QKV_ATTN)
     qkv_attn: str = dataclasses.field(default_factory=lambda: os.environ.get("LLMC_QKV_ATTN", "1"))
+    # TP engines: the decode all-reduce inside the row-parallel GEMVs' epilogue when the group has
+    # the fused buffer (TPGroup.custom_fused). Its 256 blocks spin per block on their peers, so an
+    # engine whose GPUs also run other engines' decode at the same time (bench.py's N=2 third
+    # responder) keeps the separate, 64-block all-reduce launch
+    fused_ar: bool = True
 
 
 FUSED_CHUNK_SMALL, FUSED_CHUNK_LARGE = 128, 256
@@ -517,7 +522,7 @@ class Engine:
         """h += x @ W^T across the TP group (residual folded into rank 0's partial). Decode rows
         (<= 2, VALU GEMV form) of a group with mapped peers: ONE launch, the all-reduce in the
         GEMV's epilogue (EPI_AR); otherwise the GEMV/GEMM, then the group's all-reduce."""
-        car = self.tp.custom_fused
+        car = self.tp.custom_fused if self.ecfg.fused_ar else None
         if car is not None and h.is_cuda and x.shape[0] <= 2 and not self.mfma_decode and h.is_contiguous():
             car.gemv_allreduce(x, W, h)
             return

@@ -203,6 +203,20 @@ def test_config_names_are_honest():
     assert name.startswith("variant of BASELINE config 2") and "4 responders" in name
     name, _, j = plan(1)
     assert name.startswith("BASELINE config 2 on one GPU") and j["ranks"] == [0]
+    # --resp-tp 2 at N=8: 8 responders TP=2, two per GPU pair (every GPU hosts two half-models)
+    name, r, _ = plan(8, resp_tp=2)
+    assert [e["ranks"] for e in r] == [[0, 1], [2, 3], [4, 5], [6, 7]] * 2 and "some tensor-parallel" in name
+    _, r, _ = plan(4, resp_tp=2)
+    assert [e["ranks"] for e in r] == [[0, 1], [2, 3]] * 2
+    _, r, _ = plan(1, resp_tp=2)  # one GPU: whole models whatever the flag
+    assert [e["ranks"] for e in r] == [[0]] * 3
+    # a TP responder sharing its GPUs with other responders keeps the separate all-reduce launch
+    _, r, _ = plan(2)  # N=2: the third responder is TP=2 over both GPUs, beside the two whole ones
+    assert [bench.colocated_tp(r, [i]) for i in range(3)] == [False, False, True]
+    _, r, _ = plan(8, resp_tp=2)
+    assert all(bench.colocated_tp(r, [i]) for i in range(8))
+    _, r, _ = plan(8)
+    assert not any(bench.colocated_tp(r, [i]) for i in range(8))
 
 
 def test_product_path_round_reports_phases():

@@ -18,7 +18,10 @@
 //
 //   1. one round trip for Q, L, the wave's page id and the two epochs; K/V of the wave's
 //      sub-tile; the block's o_proj weight tile (nt loads) right behind the K/V (mode 0) or after
-//      the head ticket of step 2 (mode 1, the default: the K/V never queue behind the weights)
+//      the head ticket of step 2 (mode 1: the K/V never queue behind the weights) — except in the
+//      head's merger with mode bit 1 (mode 3, the default), which requests its tile after step 3:
+//      a CU's loads retire through one queue, so the merge's loads would wait behind 128 KB of
+//      weights (1.1-1.4 us per launch, profiles/r4_attn_oproj_defer.md)
 //   2. attention sub-tile -> block state -> partial granules (attn_core.h publish) and a ticket
 //      on head g's counter (EVERY block of head g takes one, keys or not)
 //   3. the last arriver of head g merges the partials and publishes head g's output (bf16) as
@@ -70,7 +73,7 @@ __global__ __launch_bounds__(kAoThreads) void attn_oproj_kernel(
     const bf16_t* __restrict__ w_o, int K_o, bf16_t* __restrict__ h, bf16_t* __restrict__ attn_out,
     float* __restrict__ part, uint32_t* __restrict__ handoff, uint64_t* __restrict__ tile_part, int* __restrict__ ctr,
     int* __restrict__ fault, int nkv, int bs, int nblocks, int chunk, float scale_log2,
-    uint64_t* __restrict__ stamps) {
+    uint64_t* __restrict__ stamps, int defer) {
   static_assert(G * D == 512, "one 16-B column chunk per lane per row");
   static_assert(RW >= 1 && RW <= 32 && (RW & (RW - 1)) == 0, "rows per wave: power of two <= 32");
   static_assert(SUBS == 1 || (SUBS == 2 && LATE), "two sub-tiles per wave only with late weights (registers)");
@@ -172,10 +175,13 @@ __global__ __launch_bounds__(kAoThreads) void attn_oproj_kernel(
   if (ct == kTicketThread) *flag = __hip_atomic_fetch_add(hctr, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == nc - 1;
   __syncthreads();
   ao_stamp(stp, 3, tid == 0);
+  // defer (late weights only): the head's merger requests its weight tile after the merge instead,
+  // so the merge's loads do not queue behind 128 KB of weights in this CU's memory pipeline
+  const bool merger_defers = LATE && defer && *flag;  // block-uniform
   if constexpr (LATE) {
     // weights behind the whole attention step: the K/V loads never queue behind them, and a wave
     // stalled issuing 32 KB of loads holds no barrier the control waves need before the next one
-    if (o_wave) {
+    if (o_wave && !merger_defers) {
 #pragma unroll
       for (int j = 0; j < RW; ++j) wt[j] = load16<true>(wrow + static_cast<int64_t>(j) * K_o);
     }
@@ -196,6 +202,10 @@ __global__ __launch_bounds__(kAoThreads) void attn_oproj_kernel(
       __builtin_amdgcn_raw_buffer_store_b128(u32x4{lo, tag_h, hi, tag_h}, hr, ct * 16, 0, 16);
       const int gq = ct / HQ, u = ct % HQ;
       *reinterpret_cast<u32x2*>(attn_out + (g * G + gq) * D + 4 * u) = u32x2{lo, hi};
+      if (merger_defers) {  // its own copy straight into LDS (units ct = dims 4 ct .. 4 ct + 3)
+        reinterpret_cast<uint32_t*>(xs)[2 * ct] = lo;
+        reinterpret_cast<uint32_t*>(xs)[2 * ct + 1] = hi;
+      }
     }
     if (ct == 0) {
       __hip_atomic_store(hctr, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);                            // re-arm
@@ -203,8 +213,8 @@ __global__ __launch_bounds__(kAoThreads) void attn_oproj_kernel(
     }
   }
 
-  // every block of head g: wave 4 polls head g's output granules into LDS (2 units per lane)
-  if (wave == 4) {
+  // every other block of head g: wave 4 polls head g's output granules into LDS (2 units per lane)
+  if (wave == 4 && !merger_defers) {
     // 8-B relaxed atomic loads, one granule each: ordered loads are re-issued on every poll (plain
     // buffer loads in this loop would look loop-invariant to hipcc and be hoisted out of it)
     const char* hb = reinterpret_cast<const char*>(hoff) + 32 * lane;
@@ -232,6 +242,12 @@ __global__ __launch_bounds__(kAoThreads) void attn_oproj_kernel(
   }
   __syncthreads();
   ao_stamp(stp, 4, tid == 0);
+  if constexpr (LATE) {
+    if (o_wave && merger_defers) {
+#pragma unroll
+      for (int j = 0; j < RW; ++j) wt[j] = load16<true>(wrow + static_cast<int64_t>(j) * K_o);
+    }
+  }
 
   // ---- 4. o_proj partial over head g's columns (o waves); reduce-scatter the RW row sums ----
   uint64_t* tp = tile_part + (static_cast<int64_t>(c) * nkv) * R;
@@ -330,7 +346,8 @@ extern "C" int llmc_attn_oproj_check(int H, int nh, int nkv, int D, int nc, int 
 }
 
 // h += o_proj(attention). mode bit 0: issue the o_proj weights after the head ticket instead of
-// right behind the K/V loads.
+// right behind the K/V loads; bit 1 (with late weights): the head's merger issues its own after the
+// merge.
 // fault codes: 1 a partial never arrived (merge), 2 the head output never arrived, 3 a tile partial.
 // stamps (nullable, diagnostics): uint64 [nkv][nc][8] s_memrealtime per block: 0 start, 1 o wave 0's
 // attention done, 2 control wave 4's attention done, 3 head ticket taken, 4 head output in LDS,
@@ -363,7 +380,8 @@ extern "C" int llmc_attn_oproj(const void* q, const void* k_cache, const void* v
         <<<grid, kAoThreads, lds, s>>>(                                                                           \
       (const bf16_t*)q, (const bf16_t*)k_cache, (const bf16_t*)v_cache, (const int32_t*)block_table, bt_len,       \
       (const int32_t*)seq_len, (const bf16_t*)w_o, K_o, (bf16_t*)h, (bf16_t*)attn_out, (float*)part,               \
-      (uint32_t*)handoff, (uint64_t*)tile_part, (int*)ctr, (int*)fault, nkv, bs, nblocks, chunk, sl2, (uint64_t*)stamps); \
+      (uint32_t*)handoff, (uint64_t*)tile_part, (int*)ctr, (int*)fault, nkv, bs, nblocks, chunk, sl2, (uint64_t*)stamps, \
+      (mode >> 1) & 1); \
   } while (0)
   if (G == 4 && D == 128) {
     if (rw == 8) LLMC_AO(4, 128, 8);

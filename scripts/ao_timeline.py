@@ -61,5 +61,5 @@ def run(L, nh=32, nkv=8, D=128, H=4096, bs=64, mode=0):
 
 if __name__ == "__main__":
     for L in [int(x) for x in sys.argv[1:]] or [128, 2048]:
-        for mode in (0, 1):
+        for mode in [int(m) for m in os.environ.get("AO_MODES", "0,1").split(",")]:
             run(L, mode=mode)

@@ -78,11 +78,21 @@ def test_attn_oproj_vs_oracle_and_two_launches(cuda, nh, nkv, D, H, L, cap):
         assert err_h < 2e-2 * max(1.0, h_ref.abs().max().item()), (it, err_h)
         err_2 = (h.float() - h2.float()).abs().max().item()
         assert err_2 < 2e-2 * max(1.0, h_ref.abs().max().item()), (it, err_2)
+    # the late-weight variants (the merger's own weights after the merge, or not) are the same sums
+    outs = []
+    for mode in (1, 3, 1):
+        hm = h0.clone()
+        am = torch.zeros(1, nh * D, dtype=BF, device="cuda")
+        ops.attn_oproj(q, kc, vc, btd, sld, w_o, hm, am, ws, nh, nkv, D, bs, chunk, nc, scale, fault=fault, mode=mode)
+        outs.append((hm, am))
+    torch.cuda.synchronize()
+    assert int(fault.item()) == 0
+    assert all(torch.equal(outs[0][0], o[0]) and torch.equal(outs[0][1], o[1]) for o in outs[1:])
     _, _, tile_part, counters = ws
     c = counters.view(-1, 16).cpu()
-    # head tickets and tile tickets re-armed, the exit counter re-armed; both epochs advanced 3 times
+    # head tickets and tile tickets re-armed, the exit counter re-armed; both epochs advanced 6 times
     assert int(c[: nkv + nc, 0].abs().sum()) == 0 and int(c[nkv + nc, 0]) == 0, c[:, :2]
-    assert torch.equal(c[:nkv, 1], torch.full((nkv,), 3, dtype=torch.int32)) and int(c[nkv + nc, 1]) == 3
+    assert torch.equal(c[:nkv, 1], torch.full((nkv,), 6, dtype=torch.int32)) and int(c[nkv + nc, 1]) == 6
 
 
 def test_attn_oproj_shape_gates(cuda):

@@ -1,4 +1,4 @@
-# Round 4: GPU suite on the final tree (after the qkv_attn policy refactor).
+# Round 4: GPU suite on the final tree.
 cd $GRAFT_REPO_ROOT
 tag=${1:-r4fin3}
 mkdir -p gpurun_out

@@ -22,6 +22,8 @@
 //      head's merger with mode bit 1 (mode 3, the default), which requests its tile after step 3:
 //      a CU's loads retire through one queue, so the merge's loads would wait behind 128 KB of
 //      weights (1.1-1.4 us per launch, profiles/r4_attn_oproj_defer.md)
+//   (mode bit 2, the default where the shape allows it: steps 4-5 become whole o_proj rows per
+//   block over every head's output, see FR below — no tile partials and no reduce chain)
 //   2. attention sub-tile -> block state -> partial granules (attn_core.h publish) and a ticket
 //      on head g's counter (EVERY block of head g takes one, keys or not)
 //   3. the last arriver of head g merges the partials and publishes head g's output (bf16) as
@@ -66,7 +68,12 @@ __device__ __forceinline__ void ao_stamp(uint64_t* st, int k, bool who) {
   if (st != nullptr && who) st[k] = __builtin_amdgcn_s_memrealtime();
 }
 
-template <int G, int D, int RW, bool LATE, int SUBS>
+// FR = 0: block (c, g) owns o_proj rows [c R, (c + 1) R) x head group g's columns, its partial
+// summed over the nkv head groups by the tile's last arriver (step 4). FR = nkv (full rows, mode
+// bit 2): block (c, g) owns R / nkv WHOLE rows [(g nc + c) R / nkv, ...) x every head group's
+// columns, gathers every head's output and writes its rows itself — no tile partials, no tile
+// ticket, no reduce chain after the dot (same weight bytes per block)
+template <int G, int D, int RW, bool LATE, int SUBS, int FR = 0>
 __global__ __launch_bounds__(kAoThreads) void attn_oproj_kernel(
     const bf16_t* __restrict__ q, const bf16_t* __restrict__ k_cache, const bf16_t* __restrict__ v_cache,
     const int32_t* __restrict__ block_table, int bt_len, const int32_t* __restrict__ seq_len,
@@ -77,6 +84,7 @@ __global__ __launch_bounds__(kAoThreads) void attn_oproj_kernel(
   static_assert(G * D == 512, "one 16-B column chunk per lane per row");
   static_assert(RW >= 1 && RW <= 32 && (RW & (RW - 1)) == 0, "rows per wave: power of two <= 32");
   static_assert(SUBS == 1 || (SUBS == 2 && LATE), "two sub-tiles per wave only with late weights (registers)");
+  static_assert(FR == 0 || (LATE && RW % FR == 0 && FR <= kAoMaxKv), "full rows: late weights, RW / FR rows per o wave");
   using ST = SubTile<G, D>;
   constexpr int HQ = D / 4, RU = HQ + 1, Q = G * HQ;  // 16-B units: per head, per partial row, per group
   constexpr int R = 4 * RW;                              // o_proj rows per block (4 o waves)
@@ -107,7 +115,7 @@ __global__ __launch_bounds__(kAoThreads) void attn_oproj_kernel(
   char* vbuf = smem + wave * 32 * kVRowBytes;                              // per-wave V image
   float* red = reinterpret_cast<float*>(smem + kAoWaves * 32 * kVRowBytes);  // [8][G][D + 2]
   u32x4* xs = reinterpret_cast<u32x4*>(red + kAoWaves * G * (D + 2));      // head g's output, 64 chunks
-  int* flag = reinterpret_cast<int*>(xs + 64);
+  int* flag = reinterpret_cast<int*>(xs + (FR ? FR : 1) * 64);  // xs: head g's output (FR: every head's)
 
   bf16x8 kf[2][ST::KS], kf2[2][ST::KS];
   u32x4 vs[ST::NV], vs2[ST::NV];
@@ -141,14 +149,22 @@ __global__ __launch_bounds__(kAoThreads) void attn_oproj_kernel(
   // branches, hipcc's counter model at the join would make the o waves wait for their weights
   // before the MFMAs (it assumes the fewest loads in flight over both paths).
   u32x4 wt[RW];
-  const bf16_t* wrow = w_o + static_cast<int64_t>(c * R + wave * RW) * K_o + g * G * D + 8 * lane;
+  // FR: o wave rows (g nc + c) R / FR + wave RW / FR + j, element j FR + jj = head group jj's columns
+  constexpr int RWF = FR ? RW / FR : RW;  // rows per o wave
+  const bf16_t* wrow = FR ? w_o + static_cast<int64_t>((g * nc + c) * (R / (FR ? FR : 1)) + wave * RWF) * K_o + 8 * lane
+                          : w_o + static_cast<int64_t>(c * R + wave * RW) * K_o + g * G * D + 8 * lane;
+  auto load_tile = [&]() {
+#pragma unroll
+    for (int j = 0; j < RW; ++j)
+      wt[j] = load16<true>(FR ? wrow + static_cast<int64_t>(j / (FR ? FR : 1)) * K_o + (j % (FR ? FR : 1)) * G * D
+                              : wrow + static_cast<int64_t>(j) * K_o);  // nt: read once
+  };
   if (o_wave) {
     st.issue(k0_0, end_ld0, lane, row0, k_cache, v_cache, kf, vs);
     if constexpr (SUBS == 2) st.issue(k0_1, end_ld1, lane, row1, k_cache, v_cache, kf2, vs2);
     __builtin_amdgcn_sched_barrier(0);  // every K/V load issues before the first weight load
     if constexpr (!LATE) {
-#pragma unroll
-      for (int j = 0; j < RW; ++j) wt[j] = load16<true>(wrow + static_cast<int64_t>(j) * K_o);  // nt: read once
+      load_tile();
       __builtin_amdgcn_sched_barrier(0);
     }
     // ---- 2. attention sub-tile (K/V were issued before the weights: the wait leaves them in flight).
@@ -181,10 +197,7 @@ __global__ __launch_bounds__(kAoThreads) void attn_oproj_kernel(
   if constexpr (LATE) {
     // weights behind the whole attention step: the K/V loads never queue behind them, and a wave
     // stalled issuing 32 KB of loads holds no barrier the control waves need before the next one
-    if (o_wave && !merger_defers) {
-#pragma unroll
-      for (int j = 0; j < RW; ++j) wt[j] = load16<true>(wrow + static_cast<int64_t>(j) * K_o);
-    }
+    if (o_wave && !merger_defers) load_tile();
   }
 
   // ---- 3. the last arriver of head g merges (control waves) and publishes head g's output ----
@@ -203,8 +216,9 @@ __global__ __launch_bounds__(kAoThreads) void attn_oproj_kernel(
       const int gq = ct / HQ, u = ct % HQ;
       *reinterpret_cast<u32x2*>(attn_out + (g * G + gq) * D + 4 * u) = u32x2{lo, hi};
       if (merger_defers) {  // its own copy straight into LDS (units ct = dims 4 ct .. 4 ct + 3)
-        reinterpret_cast<uint32_t*>(xs)[2 * ct] = lo;
-        reinterpret_cast<uint32_t*>(xs)[2 * ct + 1] = hi;
+        uint32_t* xg = reinterpret_cast<uint32_t*>(xs + (FR ? g * 64 : 0));
+        xg[2 * ct] = lo;
+        xg[2 * ct + 1] = hi;
       }
     }
     if (ct == 0) {
@@ -213,40 +227,73 @@ __global__ __launch_bounds__(kAoThreads) void attn_oproj_kernel(
     }
   }
 
-  // every other block of head g: wave 4 polls head g's output granules into LDS (2 units per lane)
-  if (wave == 4 && !merger_defers) {
-    // 8-B relaxed atomic loads, one granule each: ordered loads are re-issued on every poll (plain
-    // buffer loads in this loop would look loop-invariant to hipcc and be hoisted out of it)
-    const char* hb = reinterpret_cast<const char*>(hoff) + 32 * lane;
-    u32x2 a0, a1, b0, b1;
-    // one lane polls one granule (256 blocks polling every granule flooded the memory path the
-    // weights stream through); once it has landed the wave reads them all (re-read if any lags)
-    if (lane == 0) {
-      for (unsigned spins = 0; ld8_atomic(reinterpret_cast<const char*>(hoff), 0)[1] != tag_h && spins < kSpinLimit;
-           ++spins)
-        __builtin_amdgcn_s_sleep(2);
+  // FR: the merger's merge is done (its head output is in LDS): its weights go now, while its
+  // control waves poll the other heads
+  if constexpr (FR != 0) {
+    if (merger_defers) {
+      __syncthreads();
+      if (o_wave) load_tile();
     }
-    for (unsigned spins = 0;; ++spins) {
-      a0 = ld8_atomic(hb, 0);
-      a1 = ld8_atomic(hb, 8);
-      b0 = ld8_atomic(hb, 16);
-      b1 = ld8_atomic(hb, 24);
-      if (__all(a0[1] == tag_h && a1[1] == tag_h && b0[1] == tag_h && b1[1] == tag_h)) break;
-      if (spins >= kSpinLimit) {
-        if (lane == 0 && fault != nullptr) __hip_atomic_store(fault, 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        break;
+  }
+  // head outputs into LDS: head g only (FR = 0: wave 4) or every head (FR: control wave 4 + k
+  // takes heads k, k + 4, ...), the merger's own head skipped (already there)
+  if (!o_wave && (FR != 0 || wave == 4)) {
+    for (int gg = FR ? wave - 4 : g; gg < (FR ? nkv : g + 1); gg += 4) {
+      if (merger_defers && gg == g) continue;
+      const uint32_t* ho = handoff + static_cast<int64_t>(gg) * Q * 4;
+      // 8-B relaxed atomic loads, one granule each: ordered loads are re-issued on every poll
+      // (plain buffer loads in this loop would look loop-invariant to hipcc and be hoisted out)
+      const char* hb = reinterpret_cast<const char*>(ho) + 32 * lane;
+      u32x2 a0, a1, b0, b1;
+      // one lane polls one granule (256 blocks polling every granule flooded the memory path the
+      // weights stream through); once it has landed the wave reads them all (re-read if any lags)
+      if (lane == 0) {
+        for (unsigned spins = 0; ld8_atomic(reinterpret_cast<const char*>(ho), 0)[1] != tag_h && spins < kSpinLimit;
+             ++spins)
+          __builtin_amdgcn_s_sleep(2);
       }
-      __builtin_amdgcn_s_sleep(1);
+      for (unsigned spins = 0;; ++spins) {
+        a0 = ld8_atomic(hb, 0);
+        a1 = ld8_atomic(hb, 8);
+        b0 = ld8_atomic(hb, 16);
+        b1 = ld8_atomic(hb, 24);
+        if (__all(a0[1] == tag_h && a1[1] == tag_h && b0[1] == tag_h && b1[1] == tag_h)) break;
+        if (spins >= kSpinLimit) {
+          if (lane == 0 && fault != nullptr) __hip_atomic_store(fault, 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          break;
+        }
+        __builtin_amdgcn_s_sleep(1);
+      }
+      xs[(FR ? gg * 64 : 0) + lane] = u32x4{a0[0], a1[0], b0[0], b1[0]};  // dims 8 lane .. + 7 of head group gg
     }
-    xs[lane] = u32x4{a0[0], a1[0], b0[0], b1[0]};  // dims 8 lane .. 8 lane + 7 of head group g
   }
   __syncthreads();
   ao_stamp(stp, 4, tid == 0);
-  if constexpr (LATE) {
-    if (o_wave && merger_defers) {
+  if constexpr (LATE && FR == 0) {
+    if (o_wave && merger_defers) load_tile();
+  }
+  if constexpr (FR != 0) {
+    // ---- 4'. whole rows: dot over every head group, reduce-scatter, residual add, done ----
+    if (o_wave) {
+      float s[RWF];
 #pragma unroll
-      for (int j = 0; j < RW; ++j) wt[j] = load16<true>(wrow + static_cast<int64_t>(j) * K_o);
+      for (int j = 0; j < RWF; ++j) {
+        float a = 0.f;
+#pragma unroll
+        for (int jj = 0; jj < FR; ++jj) a = dot8_bf16(wt[j * FR + jj], xs[jj * 64 + lane], a);
+        s[j] = a;
+      }
+      ao_reduce_scatter<RWF, 32>(s, lane);
+      constexpr int LPR = 64 / RWF;
+#pragma unroll
+      for (int m = LPR / 2; m >= 1; m >>= 1) s[0] += __shfl_xor(s[0], m, 64);
+      if ((lane % LPR) == 0) {
+        bf16_t* hp = h + (g * nc + c) * (R / FR) + wave * RWF + lane / LPR;
+        *hp = f32_to_bf16(bf16_to_f32(*hp) + s[0]);
+      }
+      ao_stamp(stp, 5, tid == 0);
     }
+    return;
   }
 
   // ---- 4. o_proj partial over head g's columns (o waves); reduce-scatter the RW row sums ----
@@ -315,18 +362,11 @@ __global__ __launch_bounds__(kAoThreads) void attn_oproj_kernel(
 using namespace llmc;
 
 // > 64 KB of dynamic LDS (the per-wave V images): raise the kernel's limit once per instantiation
-template <int G, int D, int RW>
-static void ao_set_lds() {
+template <typename K>
+static void ao_set_lds(K kern) {
   static bool done = false;  // one flag per instantiation
-  const auto kern = attn_oproj_kernel<G, D, RW, false, 1>;
-  const auto kern_late = attn_oproj_kernel<G, D, RW, true, 1>;
-  const auto kern_two = attn_oproj_kernel<G, D, RW, true, 2>;
   if (!done) {
     (void)hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize,
-                              160 * 1024);
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(kern_late), hipFuncAttributeMaxDynamicSharedMemorySize,
-                              160 * 1024);
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(kern_two), hipFuncAttributeMaxDynamicSharedMemorySize,
                               160 * 1024);
     done = true;
   }
@@ -347,7 +387,8 @@ extern "C" int llmc_attn_oproj_check(int H, int nh, int nkv, int D, int nc, int 
 
 // h += o_proj(attention). mode bit 0: issue the o_proj weights after the head ticket instead of
 // right behind the K/V loads; bit 1 (with late weights): the head's merger issues its own after the
-// merge.
+// merge; bit 2 (with late weights, 8 kv heads, G = 4, D = 128, 32-row tiles): whole o_proj rows per
+// block (FR, see the kernel).
 // fault codes: 1 a partial never arrived (merge), 2 the head output never arrived, 3 a tile partial.
 // stamps (nullable, diagnostics): uint64 [nkv][nc][8] s_memrealtime per block: 0 start, 1 o wave 0's
 // attention done, 2 control wave 4's attention done, 3 head ticket taken, 4 head output in LDS,
@@ -368,22 +409,30 @@ extern "C" int llmc_attn_oproj(const void* q, const void* k_cache, const void* v
     return -1;
   const bool late = (mode & 1) != 0 || two;  // o_proj weights issued after the head ticket
   const int G = nh / nkv, rw = H / nc / 4;
+  const bool fr = (mode & 4) != 0 && late && nkv == kAoMaxKv && G == 4 && D == 128 && rw == 32;  // full rows
   const size_t lds = kAoWaves * 32 * kVRowBytes + static_cast<size_t>(kAoWaves) * G * (D + 2) * sizeof(float) +
-                     64 * 16 + 16;
+                     (fr ? kAoMaxKv : 1) * 64 * 16 + 16;
   dim3 grid(nc, nkv);
   const float sl2 = scale * 1.4426950408889634f;
-#define LLMC_AO(GG, DD, RR)                                                                                      \
+#define LLMC_AO_K(KERN)                                                                                          \
   do {                                                                                                            \
-    ao_set_lds<GG, DD, RR>();                                                                    \
-    (two ? attn_oproj_kernel<GG, DD, RR, true, 2>                                                                 \
-         : late ? attn_oproj_kernel<GG, DD, RR, true, 1> : attn_oproj_kernel<GG, DD, RR, false, 1>)               \
-        <<<grid, kAoThreads, lds, s>>>(                                                                           \
+    ao_set_lds(KERN);                                                                                             \
+    KERN<<<grid, kAoThreads, lds, s>>>(                                                                           \
       (const bf16_t*)q, (const bf16_t*)k_cache, (const bf16_t*)v_cache, (const int32_t*)block_table, bt_len,       \
       (const int32_t*)seq_len, (const bf16_t*)w_o, K_o, (bf16_t*)h, (bf16_t*)attn_out, (float*)part,               \
       (uint32_t*)handoff, (uint64_t*)tile_part, (int*)ctr, (int*)fault, nkv, bs, nblocks, chunk, sl2, (uint64_t*)stamps, \
       (mode >> 1) & 1); \
   } while (0)
-  if (G == 4 && D == 128) {
+#define LLMC_AO(GG, DD, RR)                                                                                      \
+  do {                                                                                                            \
+    if (two) LLMC_AO_K((attn_oproj_kernel<GG, DD, RR, true, 2>));                                                 \
+    else if (late) LLMC_AO_K((attn_oproj_kernel<GG, DD, RR, true, 1>));                                           \
+    else LLMC_AO_K((attn_oproj_kernel<GG, DD, RR, false, 1>));                                                    \
+  } while (0)
+  if (fr) {
+    if (two) LLMC_AO_K((attn_oproj_kernel<4, 128, 32, true, 2, kAoMaxKv>));
+    else LLMC_AO_K((attn_oproj_kernel<4, 128, 32, true, 1, kAoMaxKv>));
+  } else if (G == 4 && D == 128) {
     if (rw == 8) LLMC_AO(4, 128, 8);
     else if (rw == 16) LLMC_AO(4, 128, 16);
     else LLMC_AO(4, 128, 32);
@@ -393,5 +442,6 @@ extern "C" int llmc_attn_oproj(const void* q, const void* k_cache, const void* v
     else LLMC_AO(8, 64, 32);
   }
 #undef LLMC_AO
+#undef LLMC_AO_K
   return static_cast<int>(hipGetLastError());
 }

@@ -280,9 +280,10 @@ def qkv_attn(x, W, norm_w, eps, q_out, k_cache, v_cache, positions, slots, cos_t
 
 
 ATTN_OPROJ_MAX_CHUNK = 512  # attn_oproj: keys per block at most (8 waves x two 32-key sub-tiles)
-# kernel mode bits (A/B runs): 1 late weights, 2 the head's merger requests its own after the merge
-# (1.1-1.4 us per layer faster at every length, profiles/r4_attn_oproj_defer.md)
-ATTN_OPROJ_MODE = int(os.environ.get("LLMC_ATTN_OPROJ_MODE", "3"))
+# kernel mode bits (A/B runs): 1 late weights; 2 the head's merger requests its own after the merge
+# (1.1-1.4 us per layer faster at every length); 4 whole o_proj rows per block, no tile reduce
+# (8 kv heads x 128: another 0.3-0.9 us; profiles/r4_attn_oproj_defer.md)
+ATTN_OPROJ_MODE = int(os.environ.get("LLMC_ATTN_OPROJ_MODE", "7"))
 # engines take the fused launch only for buckets of >= this many keys per block: below, the two
 # launches measured faster (profiles/r3_attn_oproj.md: 8B at 2k keys 18.5 vs 16.3 us, at 6k-8k
 # keys 18.8-21.5 vs 20.9-23.4)
@@ -335,7 +336,8 @@ def attn_oproj(q, k_cache, v_cache, block_table, seq_len, w_o, h, attn_out, ws, 
     nc)`` for a bucket whose capacity covers the sequence; ``fault`` as in ``attn_decode``;
     ``stamps`` (diagnostics): int64 [nkv, nc, 8] per-block phase times (see the kernel's host
     function); ``mode`` bit 0: o_proj weights requested after the head ticket, bit 1 (with bit 0):
-    the head's merger requests its own after the merge (-1 = ATTN_OPROJ_MODE)."""
+    the head's merger requests its own after the merge, bit 2 (with bit 0; 8 kv heads, G = 4, D =
+    128, 128-row tiles, else ignored): whole o_proj rows per block (-1 = ATTN_OPROJ_MODE)."""
     H = h.shape[-1]
     if not q.is_cuda:
         a = oracle.attn_decode(q[:1], k_cache, v_cache, block_table[:1], seq_len[:1], nh, nkv, D, bs, scale)

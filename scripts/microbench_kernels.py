@@ -138,10 +138,11 @@ def bench_attn_oproj(shapes=((32, 8, 128, 4096),), lens=(128, 1024, 2048, 2300, 
             t1 = timeit(one, iters=n) if chunk else float("nan")
             t1l = timeit(lambda: one(1), iters=n) if chunk else float("nan")
             t1d = timeit(lambda: one(3), iters=n) if chunk else float("nan")
+            t1f = timeit(lambda: one(7), iters=n) if chunk else float("nan")
             torch.cuda.synchronize()
             print(f"attn+o nh={nh} nkv={nkv} D={D} H={H} L={L:5d} cap={cap}: two launches "
                   f"({'fused' if fused2 else 'split'} c{ch2} g{gc2} + o GEMV) {t2:6.2f} us | one launch "
-                  f"(nc {nc}, {chunk} keys/block) {t1:6.2f} us, late weights {t1l:6.2f} us, merger defers {t1d:6.2f} us | fault "
+                  f"(nc {nc}, {chunk} keys/block) {t1:6.2f} us, late weights {t1l:6.2f} us, merger defers {t1d:6.2f} us, + whole rows {t1f:6.2f} us | fault "
                   f"{int(fault.item())} / {int(fault1.item())}", flush=True)
             del cases, wos
 

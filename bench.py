@@ -818,6 +818,11 @@ def main() -> None:
                 f"timed rounds decode {round_tokens} tokens")
 
     sync()
+    # the custom collectives' wait statistics count the timed rounds only (a collective resync of
+    # every TP engine this rank holds, in plan order)
+    for e in [e for _, e, _, _ in responders] + ([judge] if judge is not None else []):
+        if e.tp.size > 1:
+            e.tp.resync_collectives()
     if world > 1:
         dist.barrier()
     lat = []
@@ -849,7 +854,8 @@ def main() -> None:
     # every TP engine's custom-collective state at the end, from every rank that holds a shard
     ar_state = {e.name: {"custom": e.tp.custom is not None,
                          "fused": e.tp.custom_fused is not None and e.ecfg.fused_ar,
-                         "timed_out": bool(e.tp.custom_timed_out())}
+                         "timed_out": bool(e.tp.custom_timed_out()),
+                         "max_wait_us": e.tp.collective_max_wait_us()}
                 for e in [e for _, e, _, _ in responders] + ([judge] if judge is not None else []) if e.tp.size > 1}
     if world > 1:
         allst = [None] * world
@@ -857,10 +863,12 @@ def main() -> None:
         ar_state = {}
         for d in allst:
             for k, v in d.items():
-                cur = ar_state.setdefault(k, {"custom": True, "fused": True, "timed_out": False})
+                cur = ar_state.setdefault(k, {"custom": True, "fused": True, "timed_out": False, "max_wait_us": {}})
                 cur["custom"] = cur["custom"] and v["custom"]
                 cur["fused"] = cur["fused"] and v["fused"]
                 cur["timed_out"] = cur["timed_out"] or v["timed_out"]
+                for c, us in v["max_wait_us"].items():  # the longest wait of any rank
+                    cur["max_wait_us"][c] = max(cur["max_wait_us"].get(c, 0.0), us)
     if rank == 0:
         names = [e["name"] for e in resp_plan]
         value = tot_tokens / elapsed
@@ -925,6 +933,10 @@ def main() -> None:
                 "custom_allreduce_timed_out": {k: v["timed_out"] for k, v in ar_state.items()},
                 # the row-parallel decode GEMVs' all-reduce fused into their epilogue (EPI_AR)
                 "fused_rowparallel_allreduce": {k: v["fused"] for k, v in ar_state.items()},
+                # per TP engine and collective buffer (oneshot / twoshot / fused), the longest time a
+                # rank's spin waited on its peers during the timed rounds, us (device counter; the
+                # spins give up at 1 s)
+                "collective_max_wait_us": {k: v["max_wait_us"] for k, v in ar_state.items()},
                 **topo,
             },
         }

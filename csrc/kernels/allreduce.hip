@@ -40,15 +40,22 @@ __device__ __forceinline__ uint32_t car_arrive_and_wait(const CarPeers& P, int r
   if (tid < world) {  // signal peer `tid`
     __hip_atomic_store(sig_flag(P.base[tid], b, rank, off), epoch, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
   }
-  if (tid < world) {  // wait for peer `tid`
+  if (tid < world) {  // wait for peer `tid` (bounded, see car_spin; this rank's timeout word ends it)
     uint32_t* f = sig_flag(P.base[rank], b, tid, off);
-    unsigned spins = 0;
-    while (__hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) < epoch) {
-      __builtin_amdgcn_s_sleep(2);
-      if (++spins > kCarSpinLimit) {  // ~seconds: give up instead of hanging the GPU
-        car_set_timeout(P, rank);
+    unsigned polls = 0;
+    uint64_t t0 = 0;
+    for (;;) {
+      const uint32_t got = __hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      const uint32_t tmo = car_timeout_word(P, rank);
+      if (got >= epoch) {
+        car_record_wait(P, rank, polls, t0);
         break;
       }
+      if (tmo != 0) {
+        car_mark_host(P);
+        break;
+      }
+      if (!car_spin(P, rank, world, polls, t0)) break;
     }
     __atomic_thread_fence(__ATOMIC_ACQUIRE);
   }
@@ -322,25 +329,64 @@ int llmc_car_timed_out(void* own, int* out) {
   return static_cast<int>(e);
 }
 
+// Longest wait (100-MHz ticks) any spin of this rank's buffer recorded since the last reset (host
+// read after a sync).
+int llmc_car_max_wait(void* own, uint32_t* out) {
+  return static_cast<int>(hipMemcpy(out, static_cast<char*>(own) + kStatOff, 4, hipMemcpyDeviceToHost));
+}
+
+// The host status page of one rank buffer (car_proto.h kHost*): pinned, coherent (fine-grained:
+// device stores reach the host and host stores reach the device without cache maintenance),
+// mapped; zeroed. *host is the host address, *dev the device address the kernels take.
+int llmc_car_host_alloc(void** host, void** dev) {
+  void* p = nullptr;
+  hipError_t e = hipHostMalloc(&p, kHostWords * sizeof(uint32_t), hipHostMallocCoherent | hipHostMallocMapped);
+  if (e != hipSuccess) return static_cast<int>(e);
+  std::memset(p, 0, kHostWords * sizeof(uint32_t));
+  void* d = nullptr;
+  e = hipHostGetDevicePointer(&d, p, 0);
+  if (e != hipSuccess) {
+    (void)hipHostFree(p);
+    return static_cast<int>(e);
+  }
+  *host = p;
+  *dev = d;
+  return 0;
+}
+
+int llmc_car_host_free(void* host) { return static_cast<int>(hipHostFree(host)); }
+
+// Host side of the status page: plain volatile accesses (no GPU call, usable while the stream is
+// busy). word: kHostAbort / kHostTimedOut.
+int llmc_car_host_get(const void* host, int word) {
+  return static_cast<int>(static_cast<const volatile uint32_t*>(host)[word]);
+}
+void llmc_car_host_set(void* host, int word, int v) {
+  static_cast<volatile uint32_t*>(host)[word] = static_cast<uint32_t>(v);
+}
+int llmc_car_host_word(int which) { return which == 0 ? kHostAbort : kHostTimedOut; }
+
 size_t llmc_car_oneshot_max(size_t cap) { return car_oneshot_max(cap); }
 
-int llmc_car_allreduce(const void* const* bases, int rank, int world, size_t cap, void* x, size_t nbytes,
+int llmc_car_allreduce(const void* const* bases, void* host, int rank, int world, size_t cap, void* x, size_t nbytes,
                        hipStream_t s) {
   if (world < 1 || world > kMaxRanks || rank < 0 || rank >= world || nbytes % 16 || nbytes > car_oneshot_max(cap))
     return -1;
   CarPeers P;
   for (int r = 0; r < kMaxRanks; ++r) P.base[r] = r < world ? static_cast<char*>(const_cast<void*>(bases[r])) : nullptr;
+  P.host = static_cast<uint32_t*>(host);
   const int n16 = static_cast<int>(nbytes / 16);
   car_allreduce_kernel<<<car_grid(n16), 256, 0, s>>>(P, static_cast<bf16_t*>(x), n16, rank, world, cap);
   return static_cast<int>(hipGetLastError());
 }
 
-int llmc_car_allgather(const void* const* bases, int rank, int world, size_t cap, const void* x, void* out,
+int llmc_car_allgather(const void* const* bases, void* host, int rank, int world, size_t cap, const void* x, void* out,
                        size_t nbytes, hipStream_t s) {
   if (world < 1 || world > kMaxRanks || rank < 0 || rank >= world || nbytes % 16 || nbytes > car_oneshot_max(cap))
     return -1;
   CarPeers P;
   for (int r = 0; r < kMaxRanks; ++r) P.base[r] = r < world ? static_cast<char*>(const_cast<void*>(bases[r])) : nullptr;
+  P.host = static_cast<uint32_t*>(host);
   const int n16 = static_cast<int>(nbytes / 16);
   car_allgather_kernel<<<car_grid(n16), 256, 0, s>>>(P, static_cast<const char*>(x), static_cast<char*>(out), n16, rank,
                                                world, cap);
@@ -349,13 +395,14 @@ int llmc_car_allgather(const void* const* bases, int rank, int world, size_t cap
 
 // Two-shot collective over one piece (see car_twoshot_kernel): mode 0 all-reduce (in == out,
 // nv vectors), 1 reduce-scatter, 2 all-gather; world * seg16 * 16 <= cap.
-int llmc_car_twoshot(const void* const* bases, int rank, int world, size_t cap, int mode, const void* in, void* out,
-                     long seg_stride, int seg16, int nv, hipStream_t s) {
+int llmc_car_twoshot(const void* const* bases, void* host, int rank, int world, size_t cap, int mode, const void* in,
+                     void* out, long seg_stride, int seg16, int nv, hipStream_t s) {
   if (world < 2 || world > kMaxRanks || rank < 0 || rank >= world || seg16 <= 0 || nv <= 0 ||
       nv > world * seg16 || static_cast<size_t>(world) * seg16 * 16 > cap)
     return -1;
   CarPeers P;
   for (int r = 0; r < kMaxRanks; ++r) P.base[r] = r < world ? static_cast<char*>(const_cast<void*>(bases[r])) : nullptr;
+  P.host = static_cast<uint32_t*>(host);
   const char* i = static_cast<const char*>(in);
   char* o = static_cast<char*>(out);
   switch (mode) {

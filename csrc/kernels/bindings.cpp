@@ -66,16 +66,22 @@ int llmc_ipc_handle_size();
 int llmc_ipc_open(const void*, void**);
 int llmc_ipc_close(void*);
 int llmc_car_timed_out(void*, int*);
+int llmc_car_max_wait(void*, uint32_t*);
+int llmc_car_host_alloc(void**, void**);
+int llmc_car_host_free(void*);
+int llmc_car_host_get(const void*, int);
+void llmc_car_host_set(void*, int, int);
+int llmc_car_host_word(int);
 size_t llmc_car_timeout_off();
 int llmc_car_reset(void*, size_t);
 size_t llmc_car_oneshot_max(size_t);
-int llmc_gemv_ar(int, const void*, int, const void*, void*, int, int, int, const void* const*, int, int, size_t,
+int llmc_gemv_ar(int, const void*, int, const void*, void*, int, int, int, const void* const*, void*, int, int, size_t,
                  hipStream_t);
 int llmc_stream_cu_mask(int, const uint32_t*, int, void**);
 int llmc_can_access_peer(int, int, int*);
-int llmc_car_twoshot(const void* const*, int, int, size_t, int, const void*, void*, long, int, int, hipStream_t);
-int llmc_car_allreduce(const void* const*, int, int, size_t, void*, size_t, hipStream_t);
-int llmc_car_allgather(const void* const*, int, int, size_t, const void*, void*, size_t, hipStream_t);
+int llmc_car_twoshot(const void* const*, void*, int, int, size_t, int, const void*, void*, long, int, int, hipStream_t);
+int llmc_car_allreduce(const void* const*, void*, int, int, size_t, void*, size_t, hipStream_t);
+int llmc_car_allgather(const void* const*, void*, int, int, size_t, const void*, void*, size_t, hipStream_t);
 }
 
 static inline void check(int rc, const char* what) {
@@ -232,13 +238,29 @@ PYBIND11_MODULE(_llmc_hip, m) {
     return v;
   });
   m.def("car_timeout_off", []() { return llmc_car_timeout_off(); });
+  m.def("car_max_wait", [](ptr own) {
+    uint32_t v = 0;
+    check(llmc_car_max_wait(P(own), &v), "car_max_wait");
+    return v;
+  });
+  // host status page: (host address, device address)
+  m.def("car_host_alloc", []() {
+    void* h = nullptr;
+    void* d = nullptr;
+    check(llmc_car_host_alloc(&h, &d), "car_host_alloc");
+    return py::make_tuple(reinterpret_cast<ptr>(h), reinterpret_cast<ptr>(d));
+  });
+  m.def("car_host_free", [](ptr h) { check(llmc_car_host_free(P(h)), "car_host_free"); });
+  m.def("car_host_get", [](ptr h, int word) { return llmc_car_host_get(P(h), word); });
+  m.def("car_host_set", [](ptr h, int word, int v) { llmc_car_host_set(P(h), word, v); });
+  m.def("car_host_word", [](int which) { return llmc_car_host_word(which); });
   m.def("car_reset", [](ptr own, size_t cap) { check(llmc_car_reset(P(own), cap), "car_reset"); });
   m.def("car_oneshot_max", [](size_t cap) { return llmc_car_oneshot_max(cap); });
-  m.def("gemv_ar", [](int M, ptr x, int xs, ptr W, ptr h, int hs, int N, int K, const std::vector<ptr>& bases, int rank,
-                      int world, size_t cap, ptr s) {
+  m.def("gemv_ar", [](int M, ptr x, int xs, ptr W, ptr h, int hs, int N, int K, const std::vector<ptr>& bases,
+                      ptr host, int rank, int world, size_t cap, ptr s) {
     std::vector<const void*> b(bases.size());
     for (size_t i = 0; i < bases.size(); ++i) b[i] = P(bases[i]);
-    check(llmc_gemv_ar(M, P(x), xs, P(W), P(h), hs, N, K, b.data(), rank, world, cap, S(s)), "gemv_ar");
+    check(llmc_gemv_ar(M, P(x), xs, P(W), P(h), hs, N, K, b.data(), P(host), rank, world, cap, S(s)), "gemv_ar");
   });
   // a stream restricted to a set of CUs (rehearsals: ranks sharing one GPU on disjoint CUs)
   m.def("stream_cu_mask", [](int device, const std::vector<uint32_t>& mask) {
@@ -251,23 +273,24 @@ PYBIND11_MODULE(_llmc_hip, m) {
     check(llmc_can_access_peer(dev, peer, &v), "can_access_peer");
     return v;
   });
-  m.def("car_twoshot", [](const std::vector<ptr>& bases, int rank, int world, size_t cap, int mode, ptr in, ptr out,
-                          long seg_stride, int seg16, int nv, ptr s) {
+  m.def("car_twoshot", [](const std::vector<ptr>& bases, ptr host, int rank, int world, size_t cap, int mode, ptr in,
+                          ptr out, long seg_stride, int seg16, int nv, ptr s) {
     std::vector<const void*> b(bases.size());
     for (size_t i = 0; i < bases.size(); ++i) b[i] = P(bases[i]);
-    check(llmc_car_twoshot(b.data(), rank, world, cap, mode, P(in), P(out), seg_stride, seg16, nv, S(s)), "car_twoshot");
+    check(llmc_car_twoshot(b.data(), P(host), rank, world, cap, mode, P(in), P(out), seg_stride, seg16, nv, S(s)),
+          "car_twoshot");
   });
-  m.def("car_allreduce", [](const std::vector<ptr>& bases, int rank, int world, size_t cap, ptr x, size_t nbytes,
-                            ptr s) {
-    std::vector<const void*> b(bases.size());
-    for (size_t i = 0; i < bases.size(); ++i) b[i] = P(bases[i]);
-    check(llmc_car_allreduce(b.data(), rank, world, cap, P(x), nbytes, S(s)), "car_allreduce");
-  });
-  m.def("car_allgather", [](const std::vector<ptr>& bases, int rank, int world, size_t cap, ptr x, ptr out,
+  m.def("car_allreduce", [](const std::vector<ptr>& bases, ptr host, int rank, int world, size_t cap, ptr x,
                             size_t nbytes, ptr s) {
     std::vector<const void*> b(bases.size());
     for (size_t i = 0; i < bases.size(); ++i) b[i] = P(bases[i]);
-    check(llmc_car_allgather(b.data(), rank, world, cap, P(x), P(out), nbytes, S(s)), "car_allgather");
+    check(llmc_car_allreduce(b.data(), P(host), rank, world, cap, P(x), nbytes, S(s)), "car_allreduce");
+  });
+  m.def("car_allgather", [](const std::vector<ptr>& bases, ptr host, int rank, int world, size_t cap, ptr x, ptr out,
+                            size_t nbytes, ptr s) {
+    std::vector<const void*> b(bases.size());
+    for (size_t i = 0; i < bases.size(); ++i) b[i] = P(bases[i]);
+    check(llmc_car_allgather(b.data(), P(host), rank, world, cap, P(x), P(out), nbytes, S(s)), "car_allgather");
   });
   m.def("gemv_sweep", [](int v, ptr x, ptr nw, ptr W, ptr out, int N, int K, ptr s) {
     check(llmc_gemv_sweep(v, P(x), P(nw), P(W), P(out), N, K, S(s)), "gemv_sweep");

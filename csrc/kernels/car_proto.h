@@ -35,14 +35,27 @@ constexpr size_t kSigBytes = 128 * 1024;
 constexpr int kFlagOff = 4 * kMaxBlocks;                              // bytes: after ctr[kMaxBlocks]
 constexpr int kFlag2Off = kFlagOff + kTsFlagBlocks * kMaxRanks * 4;   // two-shot's second barrier
 constexpr int kTimeoutOff = kFlag2Off + kTsFlagBlocks * kMaxRanks * 4;
-static_assert(kTimeoutOff + 4 <= static_cast<int>(kSigBytes), "signal layout");
-constexpr unsigned kCarSpinLimit = 1u << 24;  // polls (s_sleep 2 each, ~seconds) before giving up
+constexpr int kStatOff = kTimeoutOff + 128;  // u32: longest wait seen by a spin of this rank (ticks)
+static_assert(kStatOff + 4 <= static_cast<int>(kSigBytes), "signal layout");
+// Bounded waits: a spin gives up after kCarSpinTicks of the 100-MHz constant clock (s_memrealtime),
+// i.e. 1 s whatever the poll latency (local uncached load, xGMI, contention). Every kCarCheckPolls
+// polls it also reads the host abort word. A peer that is merely slow never waits this long in a
+// decode (the ranks are in lockstep through their collectives; host skew is milliseconds).
+constexpr uint64_t kCarSpinTicks = 100ull * 1000 * 1000;
+constexpr unsigned kCarCheckPolls = 64;
+// Host status page (pinned, coherent, mapped into the device; one per rank buffer), u32 words:
+//   [kHostAbort]    the host sets it (a replay overran its deadline): every spin gives up at its
+//                   next check instead of polling to the limit;
+//   [kHostTimedOut] a spin of this rank gave up or returned without its data: the host reads it
+//                   with a plain load, no GPU call (the stream may still be busy).
+constexpr int kHostAbort = 0, kHostTimedOut = 16, kHostWords = 64;
 // fused-all-reduce buffer (gemv_core.h EPI_AR): block b of a launch owns granules [16 b, 16 b + 16)
 // of every slot and epoch ctr[b]
 constexpr int kArGranulesPerBlock = 16;
 
 struct CarPeers {
   char* base[kMaxRanks];  // each rank's buffer (own one included), mapped in this process
+  uint32_t* host;         // this rank's host status page (device pointer), or nullptr
 };
 
 // What a fused epilogue needs besides the buffers: who I am and the data parity size.
@@ -67,18 +80,70 @@ __device__ __forceinline__ uint64_t car_get(const char* p) {
   return __hip_atomic_load(reinterpret_cast<const uint64_t*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
-__device__ __forceinline__ void car_set_timeout(const CarPeers& P, int rank) {
-  __hip_atomic_store(reinterpret_cast<uint32_t*>(P.base[rank] + kTimeoutOff), 1u, __ATOMIC_RELAXED,
-                     __HIP_MEMORY_SCOPE_SYSTEM);
+__device__ __forceinline__ uint32_t car_timeout_word(const CarPeers& P, int rank) {
+  return __hip_atomic_load(reinterpret_cast<const uint32_t*>(P.base[rank] + kTimeoutOff), __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+// This rank's collective results since the last resync are invalid: tell the host (its page).
+__device__ __forceinline__ void car_mark_host(const CarPeers& P) {
+  if (P.host != nullptr)
+    __hip_atomic_store(P.host + kHostTimedOut, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+// A spin gave up: set the timeout word of EVERY rank's buffer (mine: every later spin of this rank
+// returns at once; the peers': their spins on this exchange and the later ones end too, so a stalled
+// exchange fails on every rank within one check instead of each rank polling to its own limit) and
+// mark the host page.
+__device__ __forceinline__ void car_give_up(const CarPeers& P, int rank, int world) {
+  for (int r = 0; r < world && r < kMaxRanks; ++r)
+    __hip_atomic_store(reinterpret_cast<uint32_t*>(P.base[r] + kTimeoutOff), 1u, __ATOMIC_RELAXED,
+                       __HIP_MEMORY_SCOPE_SYSTEM);
+  car_mark_host(P);
+  (void)rank;
+}
+
+// Slow-path bookkeeping after a failed poll (`polls` failed polls so far, `t0` the clock at the
+// first): sleeps and returns true to poll again, or gives up (deadline passed or the host set its
+// abort word) and returns false.
+__device__ __forceinline__ bool car_spin(const CarPeers& P, int rank, int world, unsigned& polls, uint64_t& t0) {
+  if (polls == 0) t0 = __builtin_amdgcn_s_memrealtime();
+  ++polls;
+  if (polls % kCarCheckPolls == 0) {
+    bool stop = __builtin_amdgcn_s_memrealtime() - t0 > kCarSpinTicks;
+    if (!stop && P.host != nullptr)
+      stop = __hip_atomic_load(P.host + kHostAbort, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != 0;
+    if (stop) {
+      car_give_up(P, rank, world);
+      return false;
+    }
+  }
+  __builtin_amdgcn_s_sleep(2);
+  return true;
+}
+
+// A wait that ended with its data after `polls` failed polls: lane 0 records its length (ticks) in
+// this rank's longest-wait word (bench.py reports it per collective buffer).
+__device__ __forceinline__ void car_record_wait(const CarPeers& P, int rank, unsigned polls, uint64_t t0) {
+  if (polls != 0 && (threadIdx.x % kWave) == 0) {
+    const uint64_t dt = __builtin_amdgcn_s_memrealtime() - t0;
+    __hip_atomic_fetch_max(reinterpret_cast<uint32_t*>(P.base[rank] + kStatOff),
+                           static_cast<uint32_t>(dt > 0xffffffffull ? 0xffffffffull : dt), __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
+  }
 }
 
 // Wait until granules g[0..NG) of every peer's slot (not mine) carry `epoch`; payloads out in
-// v[r][i] (v[rank][*] untouched). Every load in flight at once, re-polled together; bounded.
+// v[r][i] (v[rank][*] untouched). Every load in flight at once, re-polled together, with this
+// rank's timeout word in the same batch: once any spin of the group has given up, the wait returns
+// at once (the results are invalid and the host is told). Bounded: car_spin.
 template <int NG>
 __device__ __forceinline__ void car_collect(const CarPeers& P, int rank, int world, size_t cap, uint32_t epoch,
                                             const long (&g)[NG], uint32_t (&v)[kMaxRanks][NG]) {
   const char* own = P.base[rank];
-  for (unsigned spins = 0;; ++spins) {
+  unsigned polls = 0;
+  uint64_t t0 = 0;
+  for (;;) {
     bool ok = true;
 #pragma unroll
     for (int r = 0; r < kMaxRanks; ++r) {
@@ -91,12 +156,16 @@ __device__ __forceinline__ void car_collect(const CarPeers& P, int rank, int wor
         }
       }
     }
-    if (ok) return;
-    if (spins >= kCarSpinLimit) {
-      car_set_timeout(P, rank);
+    const uint32_t tmo = car_timeout_word(P, rank);
+    if (ok) {
+      car_record_wait(P, rank, polls, t0);
       return;
     }
-    __builtin_amdgcn_s_sleep(2);
+    if (tmo != 0) {
+      car_mark_host(P);
+      return;
+    }
+    if (!car_spin(P, rank, world, polls, t0)) return;
   }
 }
 

@@ -179,11 +179,12 @@ static int gemv_ar_geom(const void* x, int x_stride, const void* W, void* h, int
 }  // namespace llmc
 
 extern "C" int llmc_gemv_ar(int M, const void* x, int x_stride, const void* W, void* h, int h_stride, int N, int K,
-                            const void* const* bases, int rank, int world, size_t cap, hipStream_t s) {
+                            const void* const* bases, void* host, int rank, int world, size_t cap, hipStream_t s) {
   if (K % 8 != 0 || N % 2 != 0 || world < 1 || world > kMaxRanks || rank < 0 || rank >= world) return -1;
   CarArgs ar{};
   for (int r = 0; r < kMaxRanks; ++r)
     ar.P.base[r] = r < world ? static_cast<char*>(const_cast<void*>(bases[r])) : nullptr;
+  ar.P.host = static_cast<uint32_t*>(host);
   ar.rank = rank;
   ar.world = world;
   ar.cap = static_cast<long>(cap);

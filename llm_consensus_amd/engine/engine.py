@@ -202,6 +202,14 @@ class EngineError(Exception):
     pass
 
 
+class InjectedEngineFault(EngineError):
+    """Raised by the ``Engine.fault_at`` test hook."""
+
+
+class _TPBroken(EngineError):
+    """The TP group of this engine can no longer agree (see Engine._tp_broken)."""
+
+
 class Engine:
     def __init__(self, cfg: ModelConfig, ecfg: Optional[EngineConfig] = None, tp: Optional[TPGroup] = None,
                  name: str = "", weights: Optional[TransformerWeights] = None):
@@ -387,6 +395,7 @@ class Engine:
     @torch.no_grad()
     def prefill(self, seqs: List[Sequence], token_lists: List[List[int]], want_logits: bool = True) -> None:
         """Append ``token_lists[i]`` to ``seqs[i]`` (chunked); optionally compute last-token logits."""
+        self._check_usable()
         with self._on_stream(), trace.span("prefill", engine=self.name, tokens=sum(len(t) for t in token_lists)):
             pending = [(s, list(t)) for s, t in zip(seqs, token_lists) if t]
             chunk = self.ecfg.prefill_chunk
@@ -790,6 +799,10 @@ class Engine:
         if not (self.on_gpu and self.ecfg.use_graphs):
             return 0
         n = 0
+        # TP: every rank starts its warm-up steps (eager, with collectives) together — a rank still
+        # warming another engine would otherwise hold its peers' spins past their 1-s bound — and
+        # leaves it with the collectives' protocol state re-synchronised
+        self.tp.barrier()
         with self._on_stream():
             for B in batch_sizes or list(range(1, self.ecfg.max_batch + 1)):
                 for bk in self.buckets():
@@ -798,6 +811,9 @@ class Engine:
                     n += 1
         self._use_topkp = False
         self.capture_on_demand = False
+        if self.tp.size > 1:
+            self.stream.synchronize()
+            self.tp.resync_collectives()
         return n
 
     capture_on_demand = True
@@ -840,6 +856,7 @@ class Engine:
         B = len(seqs)
         if B > self.ecfg.max_batch:
             raise EngineError(f"{B} sequences > max_batch {self.ecfg.max_batch}")
+        self._check_usable()
         S = self.ecfg.steps_per_graph
         eos_set = set(self.cfg.eos)
         with self._on_stream(), trace.span("decode", engine=self.name, rows=B):
@@ -879,14 +896,45 @@ class Engine:
                     if stop or n >= params[i].max_tokens:
                         done[i] = True
 
+            tp_ctl = self.tp.size > 1 and self.tp.ctrl is not None
+            failure: Optional[BaseException] = None
+
+            def agree() -> bool:
+                """After each consumed snapshot: True = every row is finished. Raises on a
+                cancellation (the leader's) or a failure anywhere in the TP group — on every rank at
+                the same replay (TPGroup.step_agree), after draining and checking the collectives."""
+                if tp_ctl:
+                    try:
+                        stop, failed, fin = self.tp.step_agree(self._ctx_done(ctx), failure is not None, all(done))
+                    except Exception as e:  # noqa: BLE001 - the control group itself failed (peer died)
+                        self._tp_broken(f"{type(e).__name__}: {e}")
+                    if failed:
+                        self._fail_tp(failure)
+                else:
+                    fin, stop = all(done), False
+                    if not fin:
+                        stop = self._stop_requested(ctx)
+                if fin:
+                    return True
+                if stop:
+                    self._drain()
+                    self._check_collectives()
+                    raise ContextError(self._stop_reason(ctx))
+                return False
+
             if not self.on_gpu:
                 while True:
-                    consume(self.out_count, self.out_tokens)
-                    if all(done):
+                    try:
+                        self._inject("decode", issued)
+                        consume(self.out_count, self.out_tokens)
+                    except Exception as e:  # noqa: BLE001
+                        if not tp_ctl:
+                            raise
+                        failure = e
+                    if agree():
                         break
-                    if self._stop_requested(ctx):
-                        raise ContextError(self._stop_reason(ctx))
                     self._decode_step(B)
+                    issued += 1
                 self._check_collectives()
                 self._finish(seqs, results)
                 return results
@@ -908,40 +956,112 @@ class Engine:
                 return ev
 
             pending_ev = launch_copy(issued)
+            last = False
             while True:
                 need_more = issued < max_new
-                if need_more:
-                    # context reached by the end of this replay decides the attention bucket
-                    bucket = self._bucket(base_len + issued + S + 1)
-                    graph = self._graph(B, bucket) if self.ecfg.use_graphs else None
-                    if graph is not None:
-                        graph.replay()
-                    else:
-                        for _ in range(S):
-                            self._decode_step(B, bucket)
-                    issued += S
-                # wait for the previous snapshot (the GPU keeps the just-issued replay queued)
-                pending_ev.synchronize()
-                consume(self.host_count, self.host_tokens)
-                if all(done):
-                    break
-                # every TP rank takes this decision identically (the leader's), at the same
-                # replay: one rank running an extra replay would desynchronise the collectives
-                if self._stop_requested(ctx):
-                    self.stream.synchronize()
-                    self._check_collectives()
-                    raise ContextError(self._stop_reason(ctx))
-                pending_ev = launch_copy(issued)
-                if not need_more:
-                    pending_ev.synchronize()
+                try:
+                    if need_more and failure is None:
+                        self._inject("decode", issued)
+                        # context reached by the end of this replay decides the attention bucket
+                        bucket = self._bucket(base_len + issued + S + 1)
+                        graph = self._graph(B, bucket) if self.ecfg.use_graphs else None
+                        if graph is not None:
+                            graph.replay()
+                        else:
+                            for _ in range(S):
+                                self._decode_step(B, bucket)
+                        issued += S
+                    # wait for the previous snapshot (the GPU keeps the just-issued replay queued)
+                    self._wait_event(pending_ev)
                     consume(self.host_count, self.host_tokens)
+                except Exception as e:  # noqa: BLE001 - under TP: agreed below, on every rank
+                    if not tp_ctl or isinstance(e, _TPBroken):
+                        raise
+                    failure = e
+                # every TP rank takes this decision identically, at the same replay: one rank
+                # running an extra replay would desynchronise the collectives
+                if agree() or last:
                     break
-            self.stream.synchronize()
+                pending_ev = launch_copy(issued)
+                last = not need_more
+            self._drain()
             self._check_collectives()
             self._finish(seqs, results)
             return results
 
+    # -- TP failure handling ------------------------------------------------------------------------
+    # Seconds a TP engine waits for a replay's snapshot before it aborts its custom-collective spins
+    # (a peer stalled or died: the device spins give up on their own after 1 s, so this only fires
+    # when they cannot, e.g. an RCCL fallback collective), and again before it declares the device
+    # stalled. LLMC_TP_STALL_S.
+    stall_s = float(os.environ.get("LLMC_TP_STALL_S", "5"))
+
+    def _wait_event(self, ev) -> None:
+        """Wait for ``ev``: a plain synchronize without TP peers; a TP engine polls it against a
+        deadline instead, so a replay stuck on a peer cannot block the host indefinitely."""
+        if self.tp.size == 1 or not self.on_gpu:
+            ev.synchronize()
+            return
+        deadline, aborted = time.monotonic() + self.stall_s, False
+        while not ev.query():
+            if time.monotonic() > deadline:
+                if aborted:
+                    self._tp_broken(f"a decode replay did not finish {2 * self.stall_s:.0f} s after it was due "
+                                    "(its collectives were aborted)")
+                self.tp.abort_collectives()  # the spins give up at their next check
+                deadline, aborted = time.monotonic() + self.stall_s, True
+            time.sleep(0.0002)
+
+    def _drain(self) -> None:
+        """The stream's queued work finished (bounded under TP, see ``_wait_event``)."""
+        if self.on_gpu:
+            ev = torch.cuda.Event()
+            ev.record(self.stream)
+            self._wait_event(ev)
+
+    def _fail_tp(self, failure: Optional[BaseException]) -> None:
+        """A rank of the TP group failed mid-decode (agreed by every rank at the same replay): the
+        replays every rank launched pair up, so drain them, check / re-synchronise the collectives
+        (a rank whose replays stopped made its peers' spins give up), then raise — the failed rank
+        its own error, the others an EngineError (reference runner.go:100-107: that model fails,
+        the run goes on)."""
+        self._drain()
+        try:
+            self._check_collectives()
+        except EngineError:
+            pass
+        if failure is not None:
+            raise failure
+        raise EngineError("a TP peer failed mid-decode: this request is failed on every rank of the group")
+
+    def _tp_broken(self, why: str) -> None:
+        """The group can no longer agree (a peer process died, a control round or a device wait
+        timed out): abort this rank's spins, mark the group broken (every later request fails at
+        once) and fail the request."""
+        self.tp.broken = why
+        self.tp.abort_collectives()
+        raise _TPBroken(f"TP group broken: {why}")
+
+    def _inject(self, stage: str, issued: int) -> None:
+        """Test hook (SURVEY.md §5.3 fault injection): ``fault_at`` = (stage, k) raises an
+        InjectedEngineFault before the decode replay that would produce token k (its peers' replays
+        then wait on this rank's collectives until their spins give up)."""
+        f = self.fault_at
+        if f is not None and f[0] == stage and issued >= f[1]:
+            self.fault_at = None
+            raise InjectedEngineFault(f"injected fault: {self.name} stops before decode token {issued}")
+
+    fault_at: Optional[tuple] = None
+
+    def _check_usable(self) -> None:
+        if self.tp.broken:
+            raise EngineError(f"{self.name}: TP group broken ({self.tp.broken}); the engine serves no more requests")
+
     # -- TP control plane -------------------------------------------------------------------------
+    @staticmethod
+    def _ctx_done(ctx: Optional[Context]) -> bool:
+        return ctx is not None and ctx.done()
+
     def _stop_requested(self, ctx: Optional[Context]) -> bool:
         """Cancellation / deadline between replays. Under TP with a control group the TP leader's
         context decides for every rank (a follower's own cancel arrives at its own time)."""

@@ -16,8 +16,11 @@ too, after a collective self-check: ``graph_capture_ok``); CPU/gloo groups use t
 Control plane: TP ranks must take every control decision identically (which requests form a
 batch, when a decode stops on cancellation or deadline), or their collectives desynchronise. A
 TP group therefore carries a host-side ``ctrl`` group (gloo) over the same ranks: the leader's
-decision is broadcast (``leader_decides``), and fault checks are agreed by all ranks
-(``any_rank``).
+decisions (``leader_decides``) and the per-replay stop / failure / done vote of a decode
+(``step_agree``) are the same sequence-checked all-reduce, and fault checks are agreed by all ranks
+(``any_rank``). A failure anywhere in the group therefore ends the request on every rank at the same
+replay; a peer that dies or stalls ends it within the custom collectives' 1-s spin bound plus one
+control round (``ctrl_timeout`` for a stalled host).
 
 Prefill under TP can run Megatron-style SEQUENCE PARALLEL (engine ``EngineConfig.sequence_parallel``):
 the residual stream is sharded by token rows between the layers, so each row-parallel output is a
@@ -38,7 +41,7 @@ import torch
 import torch.distributed as dist
 
 
-CTRL_KINDS = {"value": 1, "batch": 2, "stop": 3}
+CTRL_KINDS = {"value": 1, "batch": 2, "stop": 3, "step": 4}
 
 
 class ControlDesync(RuntimeError):
@@ -54,6 +57,9 @@ class TPGroup:
         self.rank = rank
         self.size = size
         self.ctrl = ctrl      # host control group (gloo) over the same ranks, or None
+        # set when the group can no longer agree (a peer process died, a control round timed out,
+        # or a device wait overran twice): every later request on its engines fails at once
+        self.broken: Optional[str] = None
         self.custom = None    # one-shot CustomAllReduce once enable_custom() ran
         self.custom2 = None   # its two-shot twin for prefill-sized messages
         self.custom_fused = None  # the row-parallel decode GEMVs' fused all-reduce buffer (EPI_AR)
@@ -149,26 +155,46 @@ class TPGroup:
         return agree(rccl_graph_replay_check(cap, self.rank, self.size, device))
 
     # -- control plane ----------------------------------------------------------------------------
-    def leader_decides(self, value: int, kind: str = "value") -> int:
-        """The leader's ``value`` on every rank (host broadcast over ``ctrl``); identity without one.
-
-        Each decision travels as (kind, sequence number, value): every rank counts its calls, and
-        a follower whose call does not meet the leader's same-kind call of the same number (one
-        rank left a decode early and the ranks' call sequences shifted, e.g. a batch size read as
-        a stop flag) raises ``ControlDesync`` instead of acting on a value meant for another
-        decision."""
-        if self.size == 1 or self.ctrl is None:
-            return value
+    def _ctrl_exchange(self, kind: str, vals: List[int]) -> List[int]:
+        """One control round over ``ctrl``: every rank contributes (kind, sequence number, vals) and
+        gets the element-wise MAX of ``vals``. Every control decision is this same collective (an
+        all-reduce), so ranks whose call sequences shifted (one left a decode early) still meet in
+        a matching collective and both see the mismatch: the kinds or sequence numbers differ, and
+        ``ControlDesync`` is raised on every rank involved instead of one acting on a value meant
+        for another decision. A peer process that died makes gloo raise at once; a stalled one,
+        after the group's timeout (``ctrl_timeout``)."""
         code = CTRL_KINDS[kind]
         self._ctrl_seq = getattr(self, "_ctrl_seq", 0) + 1
-        t = torch.tensor([code, self._ctrl_seq, int(value)], dtype=torch.int64)
-        dist.broadcast(t, src=dist.get_global_rank(self.ctrl, 0), group=self.ctrl)
-        got_kind, got_seq = int(t[0]), int(t[1])
-        if got_kind != code or got_seq != self._ctrl_seq:
+        seq = self._ctrl_seq
+        t = torch.tensor([code, -code, seq, -seq, *vals], dtype=torch.int64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX, group=self.ctrl)
+        hi_k, lo_k, hi_s, lo_s = int(t[0]), -int(t[1]), int(t[2]), -int(t[3])
+        if hi_k != code or lo_k != code or hi_s != seq or lo_s != seq:
             names = {v: k for k, v in CTRL_KINDS.items()}
-            raise ControlDesync(f"TP control channel out of step on rank {self.rank}: expected {kind} "
-                                f"#{self._ctrl_seq}, leader sent {names.get(got_kind, got_kind)} #{got_seq}")
-        return int(t[2])
+            other = names.get(hi_k if hi_k != code else lo_k, hi_k)
+            oseq = hi_s if hi_s != seq else lo_s
+            raise ControlDesync(f"TP control channel out of step on rank {self.rank}: expected {kind} #{seq}, "
+                                f"a peer sent {other} #{oseq}")
+        return [int(v) for v in t[4:]]
+
+    def leader_decides(self, value: int, kind: str = "value") -> int:
+        """The leader's ``value`` (>= 0) on every rank; identity without a control group. A
+        ``_ctrl_exchange`` in which only the leader's value counts (the followers send -1)."""
+        if self.size == 1 or self.ctrl is None:
+            return value
+        return self._ctrl_exchange(kind, [int(value) if self.is_leader else -1])[0]
+
+    def step_agree(self, stop: bool, failed: bool, done: bool):
+        """Per-replay decision of a TP decode, one control round: (stop, failed, done) where stop =
+        the LEADER's cancellation / deadline (a follower's own cancel arrives at its own time),
+        failed = ANY rank's engine failed since the last round (its replays stopped, or its
+        streaming raised), done = EVERY rank has all its rows finished. Every rank then leaves the
+        decode at the same replay, so the collectives of the replays they did launch pair up."""
+        if self.size == 1 or self.ctrl is None:
+            return bool(stop), bool(failed), bool(done)
+        lead = int(bool(stop)) if self.is_leader else 0
+        st, fl, notdone = self._ctrl_exchange("step", [lead, int(bool(failed)), int(not done)])
+        return bool(st), bool(fl), not notdone
 
     def any_rank(self, flag: bool) -> bool:
         """True on every rank if ``flag`` is True on any rank (host all-reduce over ``ctrl``)."""
@@ -177,6 +203,28 @@ class TPGroup:
         t = torch.tensor([1 if flag else 0], dtype=torch.int32)
         dist.all_reduce(t, op=dist.ReduceOp.MAX, group=self.ctrl)
         return bool(t.item())
+
+    def abort_collectives(self) -> None:
+        """Local, no GPU call: every custom-collective spin of this rank gives up at its next check
+        (a replay overran the host's deadline: a peer stalled or died). Cleared by a resync."""
+        for c in self.collectives():
+            c.abort()
+
+    def resync_collectives(self) -> None:
+        """Collective over the group: zero every custom collective's protocol state (epochs, flags,
+        timeout words, wait statistics) between two barriers."""
+        for c in self.collectives():
+            c.resync()
+
+    def collective_max_wait_us(self) -> dict:
+        """Longest wait any spin recorded per collective buffer since the last resync, us (device
+        reads: after a sync): one-shot (decode all-reduce / logits gather), two-shot (prefill),
+        fused (the row-parallel GEMVs' epilogue)."""
+        out = {}
+        for name, c in (("oneshot", self.custom), ("twoshot", self.custom2), ("fused", self.custom_fused)):
+            if c is not None:
+                out[name] = round(c.max_wait_us(), 2)
+        return out
 
     def custom_timed_out(self) -> bool:
         """Local: did a custom-collective spin give up since the last resync (reads device memory,

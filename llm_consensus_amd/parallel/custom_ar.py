@@ -60,6 +60,7 @@ class CustomAllReduce:
         self.device = torch.device(device)
         self.group = group
         self.own = 0
+        self.host = self.host_dev = 0  # host status page (car_proto.h kHost*): host / device address
         self.bases: List[int] = []
         self._opened: List[int] = []
         err: Optional[BaseException] = None
@@ -72,6 +73,8 @@ class CustomAllReduce:
                 k = kernels()
                 with _on(self.device):
                     self.own = k.car_alloc(self.cap)
+                    if self.device.type == "cuda":
+                        self.host, self.host_dev = k.car_host_alloc()
                     if self.device.type == "cuda":
                         dev_index = self.device.index if self.device.index is not None else torch.cuda.current_device()
                     else:
@@ -156,7 +159,7 @@ class CustomAllReduce:
         M, K = x.shape
         N = W.shape[0]
         kernels().gemv_ar(M, x.data_ptr(), x.stride(0), W.data_ptr(), h.data_ptr(), h.stride(0), N, K, self.bases,
-                          self.rank, self.world, self.cap, self._stream(h))
+                          self.host_dev, self.rank, self.world, self.cap, self._stream(h))
         return h
 
     @staticmethod
@@ -169,7 +172,8 @@ class CustomAllReduce:
         same bits)."""
         if t.dtype != torch.bfloat16 or not t.is_contiguous():
             raise TypeError("custom all-reduce: contiguous bf16 only")
-        kernels().car_allreduce(self.bases, self.rank, self.world, self.cap, t.data_ptr(), t.numel() * 2, self._stream(t))
+        kernels().car_allreduce(self.bases, self.host_dev, self.rank, self.world, self.cap, t.data_ptr(), t.numel() * 2,
+                                self._stream(t))
         return t
 
     def all_gather(self, x: torch.Tensor, out: torch.Tensor) -> torch.Tensor:
@@ -177,8 +181,8 @@ class CustomAllReduce:
         nbytes = x.numel() * x.element_size()
         if out.numel() * out.element_size() != nbytes * self.world:
             raise ValueError("custom all-gather: out must hold world * x")
-        kernels().car_allgather(self.bases, self.rank, self.world, self.cap, x.data_ptr(), out.data_ptr(), nbytes,
-                                self._stream(x))
+        kernels().car_allgather(self.bases, self.host_dev, self.rank, self.world, self.cap, x.data_ptr(), out.data_ptr(),
+                                nbytes, self._stream(x))
         return out
 
     # -- two-shot (prefill) -----------------------------------------------------------------------
@@ -194,7 +198,8 @@ class CustomAllReduce:
             nv = nb // 16
             seg16 = (nv + self.world - 1) // self.world
             p = t.data_ptr() + o
-            k.car_twoshot(self.bases, self.rank, self.world, self.cap, MODE_AR, p, p, seg16 * 16, seg16, nv, st)
+            k.car_twoshot(self.bases, self.host_dev, self.rank, self.world, self.cap, MODE_AR, p, p, seg16 * 16, seg16, nv,
+                          st)
         return t
 
     def reduce_scatter(self, full: torch.Tensor, out: torch.Tensor) -> torch.Tensor:
@@ -207,8 +212,8 @@ class CustomAllReduce:
         piece = self.cap // (16 * self.world) * 16
         for o in range(0, seg, piece):
             nb = min(piece, seg - o)
-            k.car_twoshot(self.bases, self.rank, self.world, self.cap, MODE_RS, full.data_ptr() + o, out.data_ptr() + o,
-                          seg, nb // 16, self.world * (nb // 16), st)
+            k.car_twoshot(self.bases, self.host_dev, self.rank, self.world, self.cap, MODE_RS, full.data_ptr() + o,
+                          out.data_ptr() + o, seg, nb // 16, self.world * (nb // 16), st)
         return out
 
     def all_gather_large(self, x: torch.Tensor, out: torch.Tensor) -> torch.Tensor:
@@ -220,13 +225,36 @@ class CustomAllReduce:
         piece = self.cap // (16 * self.world) * 16
         for o in range(0, seg, piece):
             nb = min(piece, seg - o)
-            k.car_twoshot(self.bases, self.rank, self.world, self.cap, MODE_AG, x.data_ptr() + o, out.data_ptr() + o,
-                          seg, nb // 16, self.world * (nb // 16), st)
+            k.car_twoshot(self.bases, self.host_dev, self.rank, self.world, self.cap, MODE_AG, x.data_ptr() + o,
+                          out.data_ptr() + o, seg, nb // 16, self.world * (nb // 16), st)
         return out
 
     # -- fault handling ---------------------------------------------------------------------------
     def timed_out(self) -> bool:
-        return bool(kernels().car_timed_out(self.own))
+        """Did a spin of this rank give up (or return without its data) since the last resync?
+        The host status page answers without a GPU call; the device word after a sync."""
+        k = kernels()
+        if self.host and k.car_host_get(self.host, k.car_host_word(1)):
+            return True
+        return bool(k.car_timed_out(self.own))
+
+    def host_timed_out(self) -> bool:
+        """``timed_out`` from the host status page only: no GPU call, safe while the stream runs."""
+        k = kernels()
+        return bool(self.host and k.car_host_get(self.host, k.car_host_word(1)))
+
+    def abort(self) -> None:
+        """Make every spin of this rank give up at its next check (~100 us) instead of polling to
+        its 1-s limit: the host's way out of a replay that overran its deadline (a TP peer stalled
+        or died). Cleared by ``resync``."""
+        if self.host:
+            k = kernels()
+            k.car_host_set(self.host, k.car_host_word(0), 1)
+
+    def max_wait_us(self) -> float:
+        """Longest wait any spin of this buffer recorded since the last resync, in us (device
+        read: call after a sync)."""
+        return kernels().car_max_wait(self.own) / 100.0 if self.own and self.device.type == "cuda" else 0.0
 
     def resync(self) -> None:
         """Collective: after a spin timeout, every rank drains its device, then the protocol state
@@ -237,7 +265,11 @@ class CustomAllReduce:
             torch.cuda.synchronize(self.device)
         dist.barrier(group=self.group)
         with _on(self.device):
-            kernels().car_reset(self.own, self.cap)
+            k = kernels()
+            k.car_reset(self.own, self.cap)
+            if self.host:
+                k.car_host_set(self.host, k.car_host_word(0), 0)
+                k.car_host_set(self.host, k.car_host_word(1), 0)
         dist.barrier(group=self.group)
 
     def close(self) -> None:
@@ -253,3 +285,6 @@ class CustomAllReduce:
         if self.own:
             k.car_free(self.own)
             self.own = 0
+        if self.host:
+            k.car_host_free(self.host)
+            self.host = self.host_dev = 0

@@ -152,6 +152,9 @@ def test_self_launch_n_ranks_without_a_launcher():
         assert x["allreduce_16k"][judge[0]]["us"] > 0 and len(x["allreduce_16k"][judge[0]]["ranks"]) == x["judge_tp"]
         assert set(x["custom_allreduce"]) == set(x["custom_allreduce_timed_out"]) == set(x["allreduce_16k"])
         assert not any(x["custom_allreduce"].values()) and not any(x["custom_allreduce_timed_out"].values())
+        # the longest peer wait per TP engine and collective buffer (none without custom kernels)
+        assert set(x["collective_max_wait_us"]) == set(x["custom_allreduce"])
+        assert all(v == {} for v in x["collective_max_wait_us"].values())
 
 
 def test_gpus_defaults_to_world_size_under_a_launcher():

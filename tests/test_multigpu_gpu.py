@@ -233,3 +233,5 @@ def test_bench_self_launch_across_devices(world):
     assert judge and x["custom_allreduce"][judge[0]] and not any(x["custom_allreduce_timed_out"].values())
     assert x["fused_rowparallel_allreduce"][judge[0]]
     assert x["allreduce_16k"][judge[0]]["impl"] == "custom_oneshot" and x["allreduce_16k"][judge[0]]["us"] > 0
+    waits = x["collective_max_wait_us"][judge[0]]
+    assert set(waits) >= {"oneshot", "fused"} and all(0 <= v < 1e6 for v in waits.values()), waits

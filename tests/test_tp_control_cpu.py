@@ -123,6 +123,11 @@ class _FakeTP:
 
         return TPGroup.leader_decides(self, v, kind)
 
+    def _ctrl_exchange(self, kind, vals):
+        from llm_consensus_amd.parallel.comm import TPGroup
+
+        return TPGroup._ctrl_exchange(self, kind, vals)
+
 
 class _FakeEngine:
     def __init__(self, rank):
@@ -249,9 +254,10 @@ def _desync_worker(rank, world, port, q):
 
 
 def test_control_decisions_of_different_kinds_never_pair_up():
+    """Both sides of a mismatched control round see it (every decision is the same all-reduce)."""
     (_, k0, v0), (_, k1, v1) = _spawn(_desync_worker, 2)
-    assert k0 == "value" and v0 == 0  # the leader's own value
-    assert k1 == "desync" and "expected batch" in v1 and "leader sent stop" in v1, (k1, v1)
+    assert k0 == "desync" and "expected stop" in v0 and "a peer sent batch" in v0, (k0, v0)
+    assert k1 == "desync" and "expected batch" in v1 and "a peer sent stop" in v1, (k1, v1)
 
 
 def test_gather_failure_replies_to_the_request_it_was_gathering_for():
@@ -275,3 +281,76 @@ def test_gather_failure_replies_to_the_request_it_was_gathering_for():
     h.t.join(timeout=10)
     assert [m[:2] for m in sent] == [("error", "r7")] and "peer gone" in sent[0][2]
     assert finished == ["r7"]
+
+
+def _fault_worker(rank, world, port, mode, q):
+    """A TP=2 engine on CPU ranks whose rank 1 fails mid-decode: ``stop`` = its engine raises before
+    a replay (it stops launching; the peer's collectives would wait on it), ``die`` = its process
+    exits. The survivor's request must fail within seconds, on the agreed replay; after a ``stop``
+    the group is still in step and the next request matches a clean run."""
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    import datetime
+
+    dist.init_process_group("gloo", rank=rank, world_size=world, timeout=datetime.timedelta(seconds=60))
+    try:
+        torch.set_num_threads(1)
+        from llm_consensus_amd.engine import Engine, EngineConfig, EngineError
+        from llm_consensus_amd.models.config import FAMILIES
+        from llm_consensus_amd.parallel.comm import TPGroup
+
+        tp = TPGroup(dist.group.WORLD, rank, world, ctrl=dist.group.WORLD)
+        e = Engine(FAMILIES["llama-tiny"], EngineConfig(device="cpu", max_context=256, seed=5), tp=tp)
+        p = [(i * 13) % 700 + 256 for i in range(16)]
+        ref = e.generate_ids(p, 12, temperature=0.0, stop_on_eos=False)
+        if rank == 1 and mode == "stop":
+            e.fault_at = ("decode", 7)
+
+        def die(ids):
+            os._exit(9)  # abrupt: no cleanup, like a segfault or an OOM kill
+
+        t0 = time.monotonic()
+        err = None
+        try:
+            e.generate_ids(p, 40, temperature=0.0, stop_on_eos=False,
+                           on_tokens=(die if (rank == 1 and mode == "die") else None))
+        except EngineError as ex:
+            err = f"{type(ex).__name__}: {ex}"
+        dt = time.monotonic() - t0
+        again = None
+        try:
+            again = e.generate_ids(p, 12, temperature=0.0, stop_on_eos=False)
+        except EngineError as ex:
+            again = f"{type(ex).__name__}: {ex}"
+        q.put((rank, err, dt, again == ref if isinstance(again, list) else again))
+    except Exception as ex:  # noqa: BLE001
+        import traceback
+
+        q.put((rank, repr(ex) + traceback.format_exc(), -1, None))
+    finally:
+        if mode != "die":
+            dist.destroy_process_group()
+
+
+def test_tp_peer_raising_mid_decode_fails_every_rank_then_group_recovers():
+    res = _spawn(_fault_worker, 2, "stop")
+    (_, e0, dt0, again0), (_, e1, dt1, again1) = res
+    assert e1 and e1.startswith("InjectedEngineFault"), res
+    assert e0 and "TP peer failed mid-decode" in e0, res
+    assert dt0 < 10 and dt1 < 10, res
+    assert again0 is True and again1 is True, res
+
+
+def test_tp_peer_process_death_fails_the_survivor_fast():
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    ps = [ctx.Process(target=_fault_worker, args=(r, 2, port, "die", q)) for r in range(2)]
+    for p in ps:
+        p.start()
+    rank, err, dt, again = q.get(timeout=240)
+    for p in ps:
+        p.join(timeout=60)
+    assert rank == 0 and err and "TP group broken" in err, (rank, err, dt, again)
+    assert dt < 10, dt
+    assert isinstance(again, str) and "TP group broken" in again, again

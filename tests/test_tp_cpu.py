@@ -158,16 +158,16 @@ class _FakeCarKernels:
     def car_oneshot_max(self, cap):  # as allreduce.hip's car_oneshot_max
         return min(cap // 8 // 8 // 1024, 64) * 256 * 16
 
-    def car_allreduce(self, bases, rank, world, cap, ptr, nbytes, stream):
+    def car_allreduce(self, bases, host, rank, world, cap, ptr, nbytes, stream):
         import ctypes
 
         if rank in self.correct:
             want = torch.full((nbytes // 2,), float(world * (world + 1) // 2), dtype=torch.bfloat16)
             ctypes.memmove(ptr, want.data_ptr(), nbytes)
 
-    def car_twoshot(self, bases, rank, world, cap, mode, src, dst, seg_stride, seg16, nv, stream):
+    def car_twoshot(self, bases, host, rank, world, cap, mode, src, dst, seg_stride, seg16, nv, stream):
         assert mode == 0 and src == dst  # the self-test is an in-place all-reduce
-        self.car_allreduce(bases, rank, world, cap, dst, nv * 16, stream)
+        self.car_allreduce(bases, host, rank, world, cap, dst, nv * 16, stream)
 
 
 def _car_agree_worker(rank, world, port, case, q):

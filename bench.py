@@ -210,10 +210,12 @@ def make_plan(args, world: int):
 def colocated_tp(resp_plan, idx) -> bool:
     """Whether the tensor-parallel responder engine of plan entries ``idx`` shares a GPU with other
     responders that decode at the same time: it then keeps the separate (64-block) all-reduce
-    launch instead of the row-parallel GEMVs' fused epilogue, whose 256 blocks would spin on the
-    peer GPU while holding CUs the co-located engine needs (EngineConfig.fused_ar)."""
-    ranks = set(resp_plan[idx[0]]["ranks"])
-    return len(ranks) > 1 and any(ranks & set(o["ranks"]) for j, o in enumerate(resp_plan) if j not in idx)
+    launch instead of the row-parallel GEMVs' fused epilogue — the product path's rule
+    (placement.fused_ar_allowed, used by LocalBackend for every worker)."""
+    from llm_consensus_amd.parallel.placement import fused_ar_allowed
+
+    gpus = {str(j): list(e["ranks"]) for j, e in enumerate(resp_plan)}
+    return not fused_ar_allowed(gpus, str(idx[0]), [str(j) for j in range(len(resp_plan)) if j not in idx])
 
 
 def config_name(args, world: int, resp, judge) -> str:

@@ -35,10 +35,13 @@ enum { EPI_BF16 = 0, EPI_F32 = 1, EPI_RESADD = 2, EPI_SILU = 3, EPI_ROPE = 4, EP
 // every slot): the block's bf16 partials go straight into every peer's buffer as data-tagged
 // granules, and it sums its peers' granules in rank order as they land — the numerics of a
 // separate EPI_RESADD / EPI_BF16 GEMV followed by the one-shot all-reduce, bit for bit, without
-// that kernel's launch, its boundary and its re-read of h. Every block of a launch is dispatched
-// in index order on every rank, so the lowest unfinished block is resident everywhere: no
-// deadlock whatever else shares the GPUs (the spin is bounded anyway). Granules per block:
-// car_proto.h kArGranulesPerBlock.
+// that kernel's launch, its boundary and its re-read of h. What holds: every wait is bounded (1 s,
+// car_proto.h car_spin; a give-up fails the request on every rank). Forward progress within that
+// bound is guaranteed only when each rank owns its GPU and no other engine's blocks can take the
+// CUs a peer's blocks need: blocks are dispatched in index order, so on a GPU of its own the lowest
+// unfinished block of every rank is resident. Ranks sharing a GPU, or a TP engine beside engines
+// that decode at the same time, keep the separate all-reduce launch (comm.py enable_custom,
+// placement.fused_ar_allowed). Granules per block: car_proto.h kArGranulesPerBlock.
 
 struct RopeEpi {
   bf16_t* q_out;            // [M, q_stride], canonical head-major layout

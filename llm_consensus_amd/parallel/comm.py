@@ -91,8 +91,12 @@ class TPGroup:
                                                     selftest=False)
                 if not self.custom.agree(self._fused_selftest(device)):
                     warnings.warn("fused row-parallel all-reduce failed its self-test: separate all-reduce launches")
+                    # every rank's fused launches have drained (the self-test synchronised, also on
+                    # its error path) before the agreement above, so no peer still writes into the
+                    # buffer being closed; then the one-shot path restarts from a clean state
                     self.custom_fused.close()
                     self.custom_fused = None
+                    self.custom.resync()
         except CustomAllReduceUnavailable as e:
             warnings.warn(f"custom all-reduce disabled, using RCCL: {e}")
             for c in (self.custom, self.custom2, self.custom_fused):
@@ -126,6 +130,11 @@ class TPGroup:
                 ok = ok and bool(torch.equal(hf, hr))
             return ok and not self.custom_fused.timed_out() and not self.custom.timed_out()
         except Exception:  # noqa: BLE001
+            if torch.device(device).type == "cuda":
+                try:  # whatever was launched finishes before the group decides (and closes buffers)
+                    torch.cuda.synchronize(torch.device(device))
+                except Exception:  # noqa: BLE001
+                    pass
             return False
 
     def collectives(self):

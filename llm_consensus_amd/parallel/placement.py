@@ -45,6 +45,35 @@ class PlacementError(Exception):
     pass
 
 
+def fused_ar_allowed(gpus: Dict[str, List[int]], name: str, concurrent: Sequence[str]) -> bool:
+    """May tensor-parallel engine ``name`` run its row-parallel decode all-reduce inside the GEMV
+    epilogue (``EngineConfig.fused_ar``)? Not when an engine that decodes at the same time
+    (``concurrent``) shares one of its GPUs: the fused launch's ~256 blocks per GPU spin on the peer
+    GPUs while holding CUs, and a co-located engine's blocks queued behind them delay the very
+    peers they wait for. Single-GPU engines have no all-reduce (True)."""
+    mine = set(gpus[name])
+    if len(mine) <= 1:
+        return True
+    return not any(mine & set(gpus[o]) for o in concurrent if o != name and o in gpus)
+
+
+def fused_ar_plan(gpus: Dict[str, List[int]], judge: Optional[str], concurrency: int = 1) -> Dict[str, bool]:
+    """``fused_ar_allowed`` for every placed engine of a consensus run: the responders decode
+    together; the judge decodes after the last response (runner.go:118 then judge.go:96), so with
+    one request in flight it shares its GPUs with nothing that runs at the same time — with several
+    (the server) one request's judge overlaps the next one's responders."""
+    out = {}
+    for m in gpus:
+        if concurrency > 1:
+            conc = [o for o in gpus if o != m]
+        elif m == judge:
+            conc = []
+        else:
+            conc = [o for o in gpus if o not in (m, judge)]
+        out[m] = fused_ar_allowed(gpus, m, conc)
+    return out
+
+
 def parse_pins(spec: str) -> Dict[str, List[int]]:
     """``--placement`` syntax: ``model=g[+g...][,model=g...]`` (a '+'-joined list is a TP group)."""
     pins: Dict[str, List[int]] = {}

@@ -16,6 +16,7 @@ command to all ranks in the same order); only TP rank 0 streams tokens back.
 
 from __future__ import annotations
 
+import datetime
 import os
 import queue
 import threading
@@ -48,6 +49,9 @@ class InjectedFault(RuntimeError):
 
 
 _EMPTY = object()
+# a TP group's host control rounds (TPGroup._ctrl_exchange) never wait this long on a live peer: the
+# ranks meet them in lockstep; a peer stalled past it fails the request and breaks the group
+CTRL_TIMEOUT = datetime.timedelta(seconds=float(os.environ.get("LLMC_CTRL_TIMEOUT_S", "30")))
 BATCH_WINDOW_S = float(os.environ.get("LLMC_BATCH_WINDOW_MS", "5")) / 1000.0
 
 
@@ -419,7 +423,7 @@ def worker_main(gpu: int, conn, models: List[dict], dist_info: Optional[dict], t
             for gname, ranks in dist_info["groups"]:  # every worker creates every group, same order
                 g = dist.new_group(ranks)
                 # host control channel of the TP group (leader decisions, fault agreement)
-                ctrl = g if on_cpu else dist.new_group(ranks, backend="gloo")
+                ctrl = g if on_cpu else dist.new_group(ranks, backend="gloo", timeout=CTRL_TIMEOUT)
                 if dist_info["rank"] in ranks:
                     groups[gname] = (g, ranks.index(dist_info["rank"]), len(ranks), ctrl)
         hosts: Dict[str, _EngineHost] = {}
@@ -447,6 +451,9 @@ def worker_main(gpu: int, conn, models: List[dict], dist_info: Optional[dict], t
                                 max_batch=m.get("max_batch", 1), max_seqs=m.get("max_seqs", 0), seed=m["seed"],
                                 kv_blocks=m.get("kv_blocks", 0),
                                 use_graphs=graphs,
+                                # the placement's rule (placement.fused_ar_plan): no fused
+                                # all-reduce beside an engine that decodes at the same time
+                                fused_ar=bool(m.get("fused_ar", True)),
                                 # MoE under TP: whole experts per rank (LLMC_EXPERT_PARALLEL=1)
                                 expert_parallel=os.environ.get("LLMC_EXPERT_PARALLEL", "0") == "1")
             with trace.span("engine_init", cat="startup", engine=m["name"]):

@@ -169,3 +169,34 @@ def test_visible_gpu_count_from_kfd_topology(tmp_path, monkeypatch):
     monkeypatch.delenv("HIP_VISIBLE_DEVICES")
     monkeypatch.setattr(placement, "_KFD_NODES", str(tmp_path / "missing"))
     assert placement.visible_gpu_count() == -1
+
+
+def test_fused_allreduce_rule_follows_the_placement():
+    """the product workers take the fused row-parallel all-reduce from the placement, by
+    the same rule as bench.colocated_tp — a TP engine placed beside an engine that decodes at the
+    same time keeps separate all-reduce launches; a judge alone in its phase keeps the fused one."""
+    import importlib.util
+    import os
+
+    from llm_consensus_amd.parallel.placement import ModelDemand, fused_ar_allowed, fused_ar_plan, solve
+
+    G = 10**9
+    # a TP=2 responder and a single-GPU responder on 2 GPUs: the solver puts them together
+    p = solve([ModelDemand("big", 40 * G, G, tp=2), ModelDemand("small", 16 * G, G, tp=1),
+               ModelDemand("judge", 16 * G, G, tp=2, is_judge=True)], [0, 1])
+    assert set(p.gpus["small"]) & set(p.gpus["big"])
+    plan = fused_ar_plan(p.gpus, "judge", concurrency=1)
+    assert plan["big"] is False          # decodes beside "small"
+    assert plan["small"] is True         # single GPU: no all-reduce at all
+    assert plan["judge"] is True         # decodes after the responders, alone
+    assert fused_ar_plan(p.gpus, "judge", concurrency=2)["judge"] is False  # server: overlaps responders
+    # a TP group with its GPUs to itself keeps the fused form
+    q = {"a": [0, 1], "b": [2], "c": [3]}
+    assert fused_ar_plan(q, None)["a"] is True and fused_ar_allowed(q, "a", ["b", "c"]) is True
+    # bench.py uses the same rule for its responder plan (N=2: the third responder is TP=2)
+    spec = importlib.util.spec_from_file_location("bench_mod", os.path.join(os.path.dirname(__file__), "..", "bench.py"))
+    bench = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(bench)
+    plan2 = [{"ranks": [0]}, {"ranks": [1]}, {"ranks": [0, 1]}]
+    assert bench.colocated_tp(plan2, [2]) is True and bench.colocated_tp(plan2, [0]) is False
+    assert bench.colocated_tp([{"ranks": [0, 1]}, {"ranks": [2]}], [0]) is False

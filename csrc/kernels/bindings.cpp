@@ -66,10 +66,6 @@ int llmc_ipc_handle_size();
 int llmc_ipc_open(const void*, void**);
 int llmc_ipc_close(void*);
 int llmc_car_timed_out(void*, int*);
-int llmc_gemv_chain_ws_words();
-int llmc_gemv_chain(void*, const void*, const void*, void*, const void*, int, int, const void*, const void*, int, void*,
-                    void*, void*, const void*, const void*, const void*, const void*, int, int, int, int, float, void*,
-                    void*, int, int, hipStream_t);
 int llmc_car_max_wait(void*, uint32_t*);
 int llmc_car_host_alloc(void**, void**);
 int llmc_car_host_free(void*);
@@ -242,15 +238,6 @@ PYBIND11_MODULE(_llmc_hip, m) {
     return v;
   });
   m.def("car_timeout_off", []() { return llmc_car_timeout_off(); });
-  m.def("gemv_chain_ws_words", []() { return llmc_gemv_chain_ws_words(); });
-  m.def("gemv_chain", [](ptr h, ptr ln2, ptr W_gu, ptr act, ptr W_down, int H, int I, ptr ln1n, ptr W_qkv, int Nq, ptr q,
-                         ptr kc, ptr vc, ptr pos, ptr slots, ptr cos_t, ptr sin_t, int nh, int nkv, int D, int bs, float eps,
-                         ptr ws, ptr fault, int down_unroll, int flags, ptr s) {
-    check(llmc_gemv_chain(P(h), P(ln2), P(W_gu), P(act), P(W_down), H, I, P(ln1n), P(W_qkv), Nq, P(q), P(kc), P(vc),
-                          P(pos), P(slots), P(cos_t), P(sin_t), nh, nkv, D, bs, eps, P(ws), P(fault), down_unroll, flags,
-                          S(s)),
-          "gemv_chain");
-  });
   m.def("car_max_wait", [](ptr own) {
     uint32_t v = 0;
     check(llmc_car_max_wait(P(own), &v), "car_max_wait");

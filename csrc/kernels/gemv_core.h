@@ -64,103 +64,18 @@ struct RopeEpi {
 // Batched decode (3 <= M <= 32 rows): the MFMA form in gemv_mfma.hip, same prologue/epilogues
 // (one 16-token MFMA column group up to 16 rows, two above). This kernel serves M <= kGemvMaxM
 // (and M <= 4 when K is not a multiple of 128). MoE pairs stay within one token group.
-// Chained GEMV launches (gemv_chain.hip): consecutive decode GEMVs of a layer as PHASES of one
-// grid (block index order = phase order), so the next GEMV's blocks start streaming their weights
-// while the previous one's last blocks finish, instead of after a kernel boundary plus ramp (~3.8
-// us per batch-1 GEMV launch: 8B qkv 50 MB in 10.5 us vs gate_up 235 MB in 35.6 us, both ~7.4 TB/s
-// at steady state). Hand-off: a producer block writes its outputs write-through (sc1), waits for
-// the stores (vmcnt), then adds 1 to its shard counter (blockIdx % kChainShards, ~one per XCD, so
-// the fan-in does not serialise on one line); a consumer block issues its first weight batch,
-// then one thread polls the shard counters up to the producer blocks each holds, and the block
-// reads x with coherent (sc1) loads. Deadlock-free whatever else shares the GPU: blocks are
-// dispatched in index order on every XCD, so a waiting consumer implies that every producer block
-// of its XCD was dispatched before it; the wait is bounded (1 s) anyway and reports a fault. The
-// last consumer to pass the wait re-arms the counters for the next launch.
-constexpr int kChainShards = 8, kChainPitch = 32;  // shard counters, each on its own 128-B line
-enum { CH_WAIT = 1, CH_COHERENT = 2 };
-
-struct ChainWait {
-  int* ctr;                   // [kChainShards + 1][kChainPitch] int32: shard counters, exit counter
-  int expect[kChainShards];   // producer blocks per shard
-  int consumers;              // consumer blocks (passes of the wait before the re-arm)
-  int* fault;                 // set to 5 when a wait gave up (nullable)
-  int poll_sleep;             // s_sleep(2) rounds between polls
-  int probe_nowait;           // microbenchmark only: skip the wait (wrong results; the overlap bound)
-};
-
-__device__ __forceinline__ void chain_wait(const ChainWait& cw) {
-  if (threadIdx.x == 0 && !cw.probe_nowait) {
-    unsigned polls = 0;
-    uint64_t t0 = 0;
-    for (;;) {
-      bool ok = true;
-#pragma unroll
-      for (int s = 0; s < kChainShards; ++s)
-        ok = ok && __hip_atomic_load(cw.ctr + s * kChainPitch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= cw.expect[s];
-      if (ok) break;
-      if (polls == 0) t0 = __builtin_amdgcn_s_memrealtime();
-      if (++polls % 64 == 0 && __builtin_amdgcn_s_memrealtime() - t0 > 100000000ull) {
-        if (cw.fault != nullptr) __hip_atomic_store(cw.fault, 5, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        break;
-      }
-      for (int i = 0; i < cw.poll_sleep; ++i) __builtin_amdgcn_s_sleep(2);
-    }
-    int* ex = cw.ctr + kChainShards * kChainPitch;
-    if (__hip_atomic_fetch_add(ex, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == cw.consumers - 1) {
-#pragma unroll
-      for (int s = 0; s < kChainShards; ++s)
-        __hip_atomic_store(cw.ctr + s * kChainPitch, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      __hip_atomic_store(ex, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
-  }
-  __syncthreads();
-}
-
-// Producer side, after the block's (write-through) output stores: every wave waits for its own
-// stores, then one thread counts the block in.
-__device__ __forceinline__ void chain_signal(int* ctr) {
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-  if (threadIdx.x == 0)
-    __hip_atomic_fetch_add(ctr + (blockIdx.x % kChainShards) * kChainPitch, 1, __ATOMIC_RELAXED,
-                           __HIP_MEMORY_SCOPE_AGENT);
-}
-
-// 16 B of a buffer another block of this launch wrote write-through: two coherent (sc1) loads.
-__device__ __forceinline__ u32x4 ld16_coherent(const void* p) {
-  const uint64_t a = __hip_atomic_load(reinterpret_cast<const uint64_t*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  const uint64_t b =
-      __hip_atomic_load(reinterpret_cast<const uint64_t*>(p) + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  return u32x4{static_cast<uint32_t>(a), static_cast<uint32_t>(a >> 32), static_cast<uint32_t>(b),
-               static_cast<uint32_t>(b >> 32)};
-}
-
-template <bool COH>
-__device__ __forceinline__ void st_bf16(bf16_t* p, bf16_t v) {
-  if constexpr (COH) {
-    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // global_store_short sc1
-  } else {
-    *p = v;
-  }
-}
-
 constexpr int kGemvMaxM = 2, kGemvmMaxM = 32, kMoeGemvmMaxTokens = 16;
 int gemvm_dispatch(int M, const void* x, int x_stride, const void* norm_w, float eps, const void* W, void* out,
                    int out_stride, int N, int K, int epi, const RopeEpi& rope, hipStream_t st, int form = 0);
 
 // One block of the GEMV (block (bx, by) of its grid; smem = the block's dynamic LDS): the body of
 // gemv_kernel, also the projection role of fused launches (qkv_attn.hip).
-// CH (chained launches, see ChainWait): CH_WAIT = x is produced inside this launch (wait for it
-// after the first weight batch is in flight, then read it coherently); CH_COHERENT = the outputs
-// feed a later phase of this launch (write-through stores).
-template <int M, int NT, int RPW, int UNROLL, int PRO, int EPI, bool EXPERT = false, int CH = 0>
+template <int M, int NT, int RPW, int UNROLL, int PRO, int EPI, bool EXPERT = false>
 __device__ __forceinline__ void gemv_block(const int bx, const int by, char* smem, const bf16_t* __restrict__ x,
                                            int x_stride, const bf16_t* __restrict__ norm_w, float eps,
                                            const bf16_t* __restrict__ W, void* __restrict__ out, int out_stride, int N,
                                            int K, const int32_t* __restrict__ expert_ids, int x_div, const RopeEpi& rope,
-                                           const CarArgs& ar, const ChainWait* cw = nullptr) {
-  constexpr bool WAIT = (CH & CH_WAIT) != 0, COH = (CH & CH_COHERENT) != 0;
-  static_assert(!WAIT || (M == 1 && !EXPERT), "chained phases: one row, dense");
+                                           const CarArgs& ar) {
   constexpr int WAVES = NT / kWave;
   constexpr bool PAIR_LDS = (EPI == EPI_SILU || EPI == EPI_ROPE) && RPW == 1;  // host: N % (2 * WAVES) == 0
   // EXPERT (MoE decode): by = (token, slot) pair; weights of expert expert_ids[pair],
@@ -230,11 +145,8 @@ __device__ __forceinline__ void gemv_block(const int bx, const int by, char* sme
         const int c = tid + j * NT;
         if (c < nchunk) {
           if constexpr (PRO == PRO_NORM) gr[j] = reinterpret_cast<const u32x4*>(norm_w)[c];
-          if constexpr (!WAIT) {
 #pragma unroll
-            for (int m = 0; m < M; ++m)
-              xr[j][m] = reinterpret_cast<const u32x4*>(x + static_cast<int64_t>(m) * x_stride)[c];
-          }
+          for (int m = 0; m < M; ++m) xr[j][m] = reinterpret_cast<const u32x4*>(x + static_cast<int64_t>(m) * x_stride)[c];
         }
       }
     }
@@ -242,18 +154,6 @@ __device__ __forceinline__ void gemv_block(const int bx, const int by, char* sme
   __builtin_amdgcn_sched_barrier(0);
   issue(cur, lane);
   __builtin_amdgcn_sched_barrier(0);
-  if constexpr (WAIT) {
-    // x is an earlier phase's output: its first weight batch is in flight, now wait for the
-    // producers and read x coherently (the slow path below reads it from the same buffer)
-    chain_wait(*cw);
-    if (x_fast) {
-#pragma unroll
-      for (int j = 0; j < 2; ++j) {
-        const int c = tid + j * NT;
-        if (c < nchunk) xr[j][0] = ld16_coherent(reinterpret_cast<const u32x4*>(x) + c);
-      }
-    }
-  }
 
 
   // EPI_AR: this block's epoch and (rank 0) the residual of this wave's row, both issued behind the
@@ -481,7 +381,7 @@ __device__ __forceinline__ void gemv_block(const int bx, const int by, char* sme
   };
   auto pair_epi = [&](int n, int m, float v, float x2, float c, float sn, int slot) {
     if constexpr (EPI == EPI_SILU) {  // rows (2j, 2j+1) = (gate, up) -> output column n/2
-      st_bf16<COH>(reinterpret_cast<bf16_t*>(out) + static_cast<int64_t>(m) * out_stride + n / 2, f32_to_bf16(silu(v) * x2));
+      reinterpret_cast<bf16_t*>(out)[static_cast<int64_t>(m) * out_stride + n / 2] = f32_to_bf16(silu(v) * x2);
     } else if constexpr (EPI == EPI_ROPE) {  // rows (2j, 2j+1) of a Q/K head = dims (i, i + D/2)
       const int D = rope.D, half = D / 2;
       const int head = n / D;
@@ -605,7 +505,7 @@ __device__ __forceinline__ void gemv_block(const int bx, const int by, char* sme
         reinterpret_cast<float*>(out)[static_cast<int64_t>(m) * out_stride + n] = v;
       } else if constexpr (EPI == EPI_RESADD) {
         bf16_t* h = reinterpret_cast<bf16_t*>(out) + static_cast<int64_t>(m) * out_stride + n;
-        st_bf16<COH>(h, f32_to_bf16(bf16_to_f32(*h) + v));
+        *h = f32_to_bf16(bf16_to_f32(*h) + v);
       } else {
         if constexpr (RPW >= 2) {
           if ((r & 1) == 0) {

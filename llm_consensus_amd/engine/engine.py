@@ -79,10 +79,6 @@ class EngineConfig:
     # engine whose GPUs also run other engines' decode at the same time (bench.py's N=2 third
     # responder) keeps the separate, 64-block all-reduce launch
     fused_ar: bool = True
-    # one-row engines without TP: each layer's gate_up + down and the next layer's qkv projection as
-    # ONE launch of chained GEMV phases (csrc/kernels/gemv_chain.hip; LLMC_GEMV_CHAIN=1; off by default
-    # until it measures faster than the separate launches: profiles/r5_gemv_chain.md)
-    gemv_chain: bool = dataclasses.field(default_factory=lambda: os.environ.get("LLMC_GEMV_CHAIN", "0") == "1")
 
 
 FUSED_CHUNK_SMALL, FUSED_CHUNK_LARGE = 128, 256
@@ -332,12 +328,6 @@ class Engine:
             if any(self.qa_plan):
                 self.qa_ws = ops.qkv_attn_workspace(self.nh, self.nkv, self.D, dev)
         self.qa_buckets = [p is not None for p in self.qa_plan]
-        # chained MLP (+ next qkv) launches: one-row dense engines without TP (their down projection
-        # has no all-reduce) whose shapes the kernel tiles
-        self.chain = (self.on_gpu and B == 1 and self.ecfg.gemv_chain and self.tp.size == 1 and not c.is_moe
-                      and c.hidden % 16 == 0 and self.w.inter % 16 == 0 and c.hidden <= 16384
-                      and self.w.inter <= 16384 and ((self.nh + 2 * self.nkv) * self.D) % 32 == 0)
-        self.chain_ws = ops.gemv_chain_workspace(dev) if self.chain else None
         max_chunks = max([gc for _, _, gc, _ in self.attn_buckets] + [p[1] for p in self.qa_plan if p])
         self.attn_part, self.attn_counters = ops.decode_attn_workspace(B, self.nh, self.nkv, self.D, max_chunks, dev)
         # set by a decode-attention merger that gave up on a partial (checked after every decode)
@@ -653,9 +643,7 @@ class Engine:
         ao_chunk = self.ao_chunks[bi] if B == 1 else 0
         qa = self.qa_plan[bi] if B == 1 else None
         dbg = self._debug_layer_io  # eager debug steps only: each layer's input, then the last output
-        chain = self.chain and B == 1
-        layers = self.w.layers
-        for li, Lw in enumerate(layers):
+        for li, Lw in enumerate(self.w.layers):
             if dbg is not None:
                 dbg.append(h.clone())
             if qa:  # qkv projection + attention in one launch (one row), then o_proj
@@ -665,10 +653,9 @@ class Engine:
                              self.scale, fault=self.attn_fault)
                 self._row_parallel(attn, Lw.w_o, h)
             else:
-                if not chain or li == 0:  # chained: the previous layer's launch projected this qkv
-                    ops.qkv_rope(h, Lw.w_qkv, Lw.ln1, c.rms_eps, q, self.k_cache[li], self.v_cache[li],
-                                 self.positions[:B], self.slots[:B], self.cos_t, self.sin_t, self.nh, self.nkv, self.D,
-                                 self.bs, mfma=self.mfma_decode)
+                ops.qkv_rope(h, Lw.w_qkv, Lw.ln1, c.rms_eps, q, self.k_cache[li], self.v_cache[li],
+                             self.positions[:B], self.slots[:B], self.cos_t, self.sin_t, self.nh, self.nkv, self.D,
+                             self.bs, mfma=self.mfma_decode)
                 if ao_chunk:  # one-row engines without TP: attention + o_proj + residual in one launch
                     ops.attn_oproj(q, self.k_cache[li], self.v_cache[li], self.block_tables[:1], self.seq_lens[:1],
                                    Lw.w_o, h, attn, self.ao_ws, self.nh, self.nkv, self.D, self.bs, ao_chunk, self.ao_nc,
@@ -680,15 +667,6 @@ class Engine:
                     self._row_parallel(attn, Lw.w_o, h)
             if c.is_moe:
                 self._moe_decode(h, Lw, B)
-            elif chain:
-                # gate_up + down (+ the next layer's qkv unless it is the last layer or the next
-                # layer projects its qkv inside its attention launch) as one launch
-                nxt = None
-                if li + 1 < len(layers) and not qa:
-                    Ln = layers[li + 1]
-                    nxt = (Ln.ln1, Ln.w_qkv, q, self.k_cache[li + 1], self.v_cache[li + 1], self.positions[:1],
-                           self.slots[:1], self.cos_t, self.sin_t, self.nh, self.nkv, self.D, self.bs)
-                ops.gemv_chain(h, Lw.ln2, Lw.w_gu, act, Lw.w_down, c.rms_eps, self.chain_ws, self.attn_fault, nxt)
             else:
                 ops.linear(h, Lw.w_gu, EPI_SILU, out=act, norm_w=Lw.ln2, eps=c.rms_eps, mfma=self.mfma_decode)
                 self._row_parallel(act, Lw.w_down, h)

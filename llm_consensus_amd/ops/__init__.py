@@ -192,47 +192,6 @@ def qkv_rope(x, W, norm_w, eps, q_out, k_cache, v_cache, positions, slots, cos_t
                             nh, nkv, D, bs, int(mfma), _s(x))
 
 
-def gemv_chain_workspace(device) -> torch.Tensor:
-    """Hand-off counters of ``gemv_chain`` (int32, zeroed once; the kernel re-arms them)."""
-    dev = torch.device(device)
-    n = kernels().gemv_chain_ws_words() if dev.type == "cuda" else 1
-    return torch.zeros(n, dtype=torch.int32, device=dev)
-
-
-GEMV_CHAIN_DOWN_UNROLL = int(os.environ.get("LLMC_CHAIN_DOWN_UNROLL", "4"))
-GEMV_CHAIN_FLAGS = int(os.environ.get("LLMC_CHAIN_FLAGS", "0"))  # microbenchmarks (gemv_chain.hip)
-
-
-def gemv_chain(h, ln2, W_gu, act, W_down, eps, ws, fault=None, nxt=None) -> None:
-    """One decode row's MLP — ``act = silu(g) * u`` of ``W_gu . rmsnorm(h) * ln2``, then
-    ``h += W_down . act`` — and, with ``nxt`` = (ln1, W_qkv, q_out, k_cache, v_cache, positions,
-    slots, cos_t, sin_t, nh, nkv, D, bs), the next layer's ``qkv_rope`` on the new h: ONE launch of
-    chained GEMV phases (csrc/kernels/gemv_chain.hip). Same results as ``linear(EPI_SILU)`` +
-    ``linear(EPI_RESADD)`` (+ ``qkv_rope``: within a bf16 rounding of its normalised input)."""
-    if not h.is_cuda:
-        a = oracle.linear(h, W_gu, EPI_SILU, None, ln2, eps)
-        act.copy_(a)
-        oracle.linear(act, W_down, EPI_RESADD, h)
-        if nxt is not None:
-            ln1, Wq, q, kc, vc, pos, slots, cos_t, sin_t, nh, nkv, D, bs = nxt
-            qkv_rope(h, Wq, ln1, eps, q, kc, vc, pos, slots, cos_t, sin_t, nh, nkv, D, bs)
-        return
-    H, I = h.shape[-1], act.shape[-1]
-    if h.shape[0] != 1 or act.shape[0] != 1 or W_gu.shape != (2 * I, H) or W_down.shape != (H, I):
-        raise ValueError("gemv_chain: one row, W_gu [2I, H], W_down [H, I]")
-    k = kernels()
-    if nxt is None:
-        k.gemv_chain(_p(h), _p(ln2), _p(W_gu), _p(act), _p(W_down), H, I, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0,
-                     float(eps), _p(ws), _p(fault), GEMV_CHAIN_DOWN_UNROLL, GEMV_CHAIN_FLAGS, _s(h))
-        return
-    ln1, Wq, q, kc, vc, pos, slots, cos_t, sin_t, nh, nkv, D, bs = nxt
-    if q.stride(0) != nh * D or Wq.shape[1] != H:
-        raise ValueError("gemv_chain: q rows of nh * D, W_qkv [Nq, H]")
-    k.gemv_chain(_p(h), _p(ln2), _p(W_gu), _p(act), _p(W_down), H, I, _p(ln1), _p(Wq), Wq.shape[0], _p(q), _p(kc),
-                 _p(vc), _p(pos), _p(slots), _p(cos_t), _p(sin_t), nh, nkv, D, bs, float(eps), _p(ws), _p(fault),
-                 GEMV_CHAIN_DOWN_UNROLL, GEMV_CHAIN_FLAGS, _s(h))
-
-
 FUSED_ATTN_MAX_KEYS = 4096  # decode attention: fused single-launch form up to this bucket capacity
 FUSED_CHUNK = 128           # keys per block of the fused form
 

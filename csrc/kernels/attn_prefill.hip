@@ -21,6 +21,8 @@
 // write LDS after: T14 async-STAGE split) into a 2-deep LDS ring. Keys are looked up through
 // the block table per row, so any page size works (64 is the engine default).
 // Numerics: S in f32, exp2 with log2(e) folded into the scale, P rounded to bf16 for PV, O in f32.
+#include <stdlib.h>
+
 #include "common.h"
 
 namespace llmc {
@@ -31,11 +33,12 @@ typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
 constexpr int kKT = 64;        // keys per tile
 constexpr int kRowBytes = 256; // LDS row pitch (128 bf16), D <= 128
 constexpr int kTileBytes = kKT * kRowBytes;  // 16 KB
+constexpr int kPrefillLookahead = 2;          // K/V tiles requested ahead of the one computing
 
 __device__ __forceinline__ int k_swz(int row, int ch) { return row * kRowBytes + ((ch ^ (row & 15)) << 4); }
 __device__ __forceinline__ int v_swz(int row, int ch) { return row * kRowBytes + ((ch ^ ((row & 3) << 2)) << 4); }
 
-template <int D, int WPB>
+template <int D, int WPB, int LA>
 __global__ __launch_bounds__(WPB * 64) void attn_prefill_kernel(
     const bf16_t* __restrict__ q, int q_stride, const bf16_t* __restrict__ k_cache, const bf16_t* __restrict__ v_cache,
     const int32_t* __restrict__ block_tables, int bt_stride, const int32_t* __restrict__ q_start,
@@ -98,8 +101,11 @@ __global__ __launch_bounds__(WPB * 64) void attn_prefill_kernel(
   const int32_t* bt = block_tables + static_cast<int64_t>(b) * bt_stride;
   const int64_t head_stride = static_cast<int64_t>(bs) * D;
 
-  u32x4 stk[NL], stv[NL];
-  auto issue = [&](int t) {
+  // LA register staging sets: tile t + LA is requested while tile t computes, so a tile's global
+  // loads have LA - 1 whole compute steps (plus one) to land before its commit to LDS (one tile
+  // of lookahead left every tile waiting on HBM latency at 2k tokens: ~3 us per 64-key tile)
+  u32x4 stk[LA][NL], stv[LA][NL];
+  auto issue = [&](int t, int set) {
 #pragma unroll
     for (int u = 0; u < NL; ++u) {
       const int idx = tid + u * NT;
@@ -109,11 +115,11 @@ __global__ __launch_bounds__(WPB * 64) void attn_prefill_kernel(
       key = min(key, ctx - 1);
       const int64_t page = bt[key / bs];
       const int64_t off = (page * nkv + kvh) * head_stride + static_cast<int64_t>(key % bs) * D + ch * 8;
-      stk[u] = *reinterpret_cast<const u32x4*>(k_cache + off);
-      stv[u] = *reinterpret_cast<const u32x4*>(v_cache + off);
+      stk[set][u] = *reinterpret_cast<const u32x4*>(k_cache + off);
+      stv[set][u] = *reinterpret_cast<const u32x4*>(v_cache + off);
     }
   };
-  auto commit = [&](int buf) {
+  auto commit = [&](int buf, int set) {
     char* kb = smem + buf * 2 * kTileBytes;
     char* vb = kb + kTileBytes;
 #pragma unroll
@@ -121,18 +127,28 @@ __global__ __launch_bounds__(WPB * 64) void attn_prefill_kernel(
       const int idx = tid + u * NT;
       if (!NL_EXACT && idx >= kKT * CH) continue;
       const int row = idx / CH, ch = idx % CH;
-      *reinterpret_cast<u32x4*>(kb + k_swz(row, ch)) = stk[u];
-      *reinterpret_cast<u32x4*>(vb + v_swz(row, ch)) = stv[u];
+      *reinterpret_cast<u32x4*>(kb + k_swz(row, ch)) = stk[set][u];
+      *reinterpret_cast<u32x4*>(vb + v_swz(row, ch)) = stv[set][u];
     }
   };
 
-  issue(0);
-  commit(0);
+  issue(0, 0);
+#pragma unroll
+  for (int j = 1; j < LA; ++j)
+    if (j < ntiles) issue(j, j);
+  commit(0, 0);
   __syncthreads();
 
-  for (int t = 0; t < ntiles; ++t) {
+  // unrolled by LA so that every staging-set index is a compile-time constant (a runtime index into
+  // a register array would go through scratch)
+  for (int t0 = 0; t0 < ntiles; t0 += LA) {
+#pragma unroll
+  for (int j = 0; j < LA; ++j) {
+    const int t = t0 + j;
+    if (t >= ntiles) break;
     const int buf = t & 1;
-    if (t + 1 < ntiles) issue(t + 1);
+    // the set tile t was staged in (j) is free again (committed): tile t + LA goes into it
+    if (t + LA < ntiles) issue(t + LA, j);
     const int kt = t * kKT;
     if (wvalid && kt < wave_kend) {
       const char* kb = smem + buf * 2 * kTileBytes;
@@ -236,8 +252,9 @@ __global__ __launch_bounds__(WPB * 64) void attn_prefill_kernel(
         }
       }
     }
-    if (t + 1 < ntiles) commit(buf ^ 1);
+    if (t + 1 < ntiles) commit(buf ^ 1, (j + 1) % LA);
     __syncthreads();
+  }
   }
 
   if (!wvalid || row_i >= qlen) return;
@@ -269,17 +286,28 @@ extern "C" int llmc_attn_prefill(const void* q, int q_stride, const void* k_cach
   constexpr int WPB = 8;  // 8 waves = 2 row tiles x 4 heads share every staged K/V tile
   dim3 grid((G * npb + WPB - 1) / WPB, nkv, B);
   const float sl2 = scale * 1.4426950408889634f;
-#define LLMC_PF(DD)                                                                                            \
-  attn_prefill_kernel<DD, WPB><<<grid, WPB * 64, 0, s>>>((const bf16_t*)q, q_stride, (const bf16_t*)k_cache, \
-                                               (const bf16_t*)v_cache, (const int32_t*)block_tables, bt_stride, \
-                                               (const int32_t*)q_start, (const int32_t*)q_lens,                \
+  static const int la = [] {
+    const char* e = getenv("LLMC_PREFILL_LOOKAHEAD");  // A/B runs: K/V tiles requested ahead
+    return e ? atoi(e) : kPrefillLookahead;
+  }();
+#define LLMC_PF(DD, L)                                                                                           \
+  attn_prefill_kernel<DD, WPB, L><<<grid, WPB * 64, 0, s>>>((const bf16_t*)q, q_stride, (const bf16_t*)k_cache, \
+                                               (const bf16_t*)v_cache, (const int32_t*)block_tables, bt_stride,   \
+                                               (const int32_t*)q_start, (const int32_t*)q_lens,                  \
                                                (const int32_t*)ctx_lens, (bf16_t*)out, out_stride, nh, nkv, bs, sl2)
+#define LLMC_PF_D(DD)                \
+  do {                               \
+    if (la >= 3) LLMC_PF(DD, 3);     \
+    else if (la == 2) LLMC_PF(DD, 2); \
+    else LLMC_PF(DD, 1);             \
+  } while (0)
   switch (D) {
-    case 64: LLMC_PF(64); break;
-    case 96: LLMC_PF(96); break;
-    case 128: LLMC_PF(128); break;
+    case 64: LLMC_PF_D(64); break;
+    case 96: LLMC_PF_D(96); break;
+    case 128: LLMC_PF_D(128); break;
     default: return -2;
   }
+#undef LLMC_PF_D
 #undef LLMC_PF
   return static_cast<int>(hipGetLastError());
 }

@@ -345,8 +345,15 @@ def bench_prefill():
         line = (f"gemm M={M} N={N} K={K}: ours {t_ours:8.1f} us {fl / t_ours / 1e6:6.0f} TF/s | 128x128 {t_128:8.1f} us "
                 f"{fl / t_128 / 1e6:6.0f} TF/s | torch {t_ref:8.1f} us {fl / t_ref / 1e6:6.0f} TF/s")
         print(line, flush=True)
-    nh, nkv, D, bs = 32, 8, 128, 64
-    for (T, ctx) in [(2048, 2048), (8192, 8192), (8192, 32768)]:
+    bench_attn_prefill()
+
+
+def bench_attn_prefill(cases=((32, 8, 2048, 2048), (32, 8, 8192, 8192), (32, 8, 8192, 32768), (32, 8, 2304, 9000),
+                              (4, 1, 8192, 8192), (4, 1, 8192, 32768), (16, 2, 8192, 8192))):
+    """Causal flash prefill (attn_prefill.hip) on (heads, kv heads, T new tokens, ctx keys): Llama-3-8B
+    and its TP=8 rank (4 heads on 1 kv head), Llama-3-70B TP=4 rank (16 on 2)."""
+    D, bs = 128, 64
+    for (nh, nkv, T, ctx) in cases:
         nb = (ctx + bs - 1) // bs + 1
         kc = torch.randn(nb, nkv, bs, D, device="cuda").to(BF)
         vc = torch.randn_like(kc)
@@ -360,7 +367,7 @@ def bench_prefill():
                     iters=3)
         # causal FLOPs of the last T queries over ctx keys
         fl = 4 * nh * D * (T * ctx - T * (T - 1) / 2)
-        print(f"attn_prefill T={T} ctx={ctx}: {us:8.1f} us {fl / us / 1e6:6.0f} TF/s", flush=True)
+        print(f"attn_prefill nh={nh} nkv={nkv} T={T} ctx={ctx}: {us:8.1f} us {fl / us / 1e6:6.0f} TF/s", flush=True)
 
 
 def bench_moe(tokens=(2048, 8192, 16384)):
@@ -456,5 +463,7 @@ if __name__ == "__main__":
         bench_qkv_rope()
     if what in ("moe",):  # Mixtral grouped expert GEMMs
         bench_moe()
+    if what in ("attn-prefill",):
+        bench_attn_prefill()
     if what in ("prefill",):
         bench_prefill()

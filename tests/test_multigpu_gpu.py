@@ -47,6 +47,18 @@ def _inp(rank, n, salt):
     return torch.randn(n, generator=g).to(torch.bfloat16)
 
 
+def _ar_exact(xs, times=1):
+    """The custom collectives' result, bit for bit: f32 sum in rank order, rounded once to bf16, per
+    in-place all-reduce (car_proto.h: every rank combines the granules in rank order)."""
+    xs = [x.clone() for x in xs]
+    for _ in range(times):
+        acc = torch.zeros_like(xs[0], dtype=torch.float32)
+        for x in xs:
+            acc = acc + x.float()
+        xs = [acc.to(torch.bfloat16)] * len(xs)
+    return xs[0]
+
+
 def _init(rank, world, port):
     import torch.distributed as dist
 
@@ -91,8 +103,7 @@ def _collectives_worker(rank, world, port, q):
                     x = _inp(rank, n, rep).to(dev)
                     tp.all_reduce_(x)  # one-shot up to 1 MiB, two-shot above
                     torch.cuda.synchronize()
-                    ref = sum(_inp(r, n, rep).float() for r in range(world))
-                    errs.append(float((x.float().cpu() - ref).abs().max() / (ref.abs().max() + 1e-6)))
+                    errs.append(0.0 if torch.equal(x.cpu(), _ar_exact([_inp(r, n, rep) for r in range(world)])) else 1.0)
             loc = torch.full((2, 20), float(rank), dtype=torch.float32, device=dev)
             out = torch.empty(world, 2, 20, dtype=torch.float32, device=dev)
             tp.all_gather_rows(loc, out)
@@ -102,8 +113,8 @@ def _collectives_worker(rank, world, port, q):
             tp.reduce_scatter_rows(full.to(dev), rs)
             torch.cuda.synchronize()
             gather_ok = all(bool((out[r] == r).all()) for r in range(world))
-            ref = sum(_inp(r, world * Ts * H, 7).view(world * Ts, H).float() for r in range(world))[rank * Ts:(rank + 1) * Ts]
-            errs.append(float((rs.float().cpu() - ref).abs().max() / ref.abs().max()))
+            ref = _ar_exact([_inp(r, world * Ts * H, 7).view(world * Ts, H) for r in range(world)])[rank * Ts:(rank + 1) * Ts]
+            errs.append(0.0 if torch.equal(rs.cpu(), ref) else 1.0)
             # graph replay with refreshed inputs (the decode graphs' pattern)
             n = 8192
             x = torch.zeros(n, dtype=torch.bfloat16, device=dev)
@@ -121,9 +132,8 @@ def _collectives_worker(rank, world, port, q):
                 dist.barrier()
                 g.replay()
                 torch.cuda.synchronize()
-                one = sum(_inp(r, n, 50 + rep).float() for r in range(world))
-                ref = one * world * world  # three in-place all-reduces
-                errs.append(float((x.float().cpu() - ref).abs().max() / ref.abs().max()))
+                ref = _ar_exact([_inp(r, n, 50 + rep) for r in range(world)], times=3)  # three in-place
+                errs.append(0.0 if torch.equal(x.cpu(), ref) else 1.0)
         else:
             gather_ok = False
         q.put((rank, peers_ok, enabled, max(errs) if errs else 1.0, gather_ok, tp.custom_timed_out() if enabled else None))
@@ -143,8 +153,9 @@ def test_custom_collectives_across_devices(world):
         assert peers_ok, f"rank {rank}: hipDeviceCanAccessPeer is false for a peer"
         assert enabled, f"rank {rank}: custom collectives fell back to RCCL"
         assert not tmo, f"rank {rank}: a custom-collective spin timed out"
-        # bf16 rounding of sums over up to 8 ranks, and a triple in-place sum in the graph case
-        assert err < 3e-2, (rank, err)
+        # every sum is the f32 rank-order sum rounded to bf16, bit for bit (a torn or stale granule
+        # over xGMI would show here, where a tolerance would pass it)
+        assert err == 0.0, f"rank {rank}: a cross-device sum differs from the f32 rank-order sum rounded to bf16"
         assert gather_ok, rank
 
 
@@ -159,16 +170,30 @@ def _tp_cfg():
 PROMPT = [(i * 13) % 700 + 256 for i in range(60)]
 
 
-def _tp_worker(rank, world, port, q):
+def _tp_worker(rank, world, port, q, layout="devices"):
+    """A TP = world engine: ``devices`` = rank i on cuda:i over RCCL; ``one_gpu`` = every rank on
+    cuda:0, each on its own 256 / world CUs (EngineConfig.cu_mask) with the fused row-parallel
+    all-reduce forced on — the rehearsal the cross-device run must reproduce bit for bit."""
     try:
-        dist = _init(rank, world, port)
+        if layout == "one_gpu":
+            import torch.distributed as dist
+
+            n = 256 // world
+            os.environ["LLMC_CU_MASK"] = f"{rank * n}-{rank * n + n - 1}"
+            os.environ["LLMC_FUSED_AR"] = "force"
+            torch.cuda.set_device(0)
+            dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world)
+            dev = "cuda:0"
+        else:
+            dist = _init(rank, world, port)
+            dev = f"cuda:{rank}"
         from llm_consensus_amd.engine import Engine, EngineConfig
         from llm_consensus_amd.parallel.comm import TPGroup
 
         ctrl = dist.new_group(list(range(world)), backend="gloo")
         tp = TPGroup(dist.group.WORLD, rank, world, ctrl=ctrl)
-        enabled = tp.enable_custom(f"cuda:{rank}")
-        e = Engine(_tp_cfg(), EngineConfig(device=f"cuda:{rank}", max_context=1024, seed=5), tp=tp)
+        enabled = tp.enable_custom(dev)
+        e = Engine(_tp_cfg(), EngineConfig(device=dev, max_context=1024, seed=5), tp=tp)
         e.warmup_graphs()
         s = e.new_sequence()
         e.prefill([s], [PROMPT])
@@ -214,6 +239,23 @@ def test_tp_decode_across_devices_matches_tp1(world):
     assert agree >= 8, (agree, gens[0], ref_gen)  # bf16 sums in a different order: near-ties only late
 
 
+@pytest.mark.parametrize("world", WORLDS)
+def test_tp_decode_across_devices_bit_identical_to_one_gpu_rehearsal(world):
+    """The same TP = N computation on N distinct devices (xGMI, RCCL bootstrap) and rehearsed on ONE
+    GPU with CU-partitioned ranks: the push protocol sums in rank order (car_proto.h), so the
+    prefill logits and the 32 greedy tokens must be bit-identical — a torn 8-byte granule or a stale
+    epoch over the link would break this where a tolerance against TP = 1 would not."""
+    _need(world)
+    one = {r[0]: r for r in _run(_tp_worker, world, "one_gpu")}
+    dev = {r[0]: r for r in _run(_tp_worker, world, "devices")}
+    for res in (one, dev):
+        for rank, enabled, logits, gen, tmo in res.values():
+            assert not isinstance(logits, str), logits
+            assert enabled and not tmo, rank
+    assert torch.equal(torch.tensor(one[0][2]), torch.tensor(dev[0][2])), "prefill logits differ across layouts"
+    assert all(one[r][3] == dev[r][3] for r in range(world)), (one[0][3], dev[0][3])
+
+
 # ---- the bench's own multi-GPU flow ---------------------------------------------------------
 @pytest.mark.parametrize("world", WORLDS)
 def test_bench_self_launch_across_devices(world):
@@ -235,3 +277,18 @@ def test_bench_self_launch_across_devices(world):
     assert x["allreduce_16k"][judge[0]]["impl"] == "custom_oneshot" and x["allreduce_16k"][judge[0]]["us"] > 0
     waits = x["collective_max_wait_us"][judge[0]]
     assert set(waits) >= {"oneshot", "fused"} and all(0 <= v < 1e6 for v in waits.values()), waits
+
+
+@pytest.mark.parametrize("world", [2, 4])
+def test_tp_one_gpu_rehearsal_is_deterministic(cuda, world):
+    """The reference side of the bit-identity test above, on one GPU: the CU-partitioned TP = N
+    rehearsal (fused row-parallel all-reduce forced on) gives the same prefill logits and greedy
+    tokens on every run (runs on a one-GPU box)."""
+    a = {r[0]: r for r in _run(_tp_worker, world, "one_gpu")}
+    b = {r[0]: r for r in _run(_tp_worker, world, "one_gpu")}
+    for res in (a, b):
+        for rank, enabled, logits, gen, tmo in res.values():
+            assert not isinstance(logits, str), logits
+            assert enabled and not tmo, rank
+    assert torch.equal(torch.tensor(a[0][2]), torch.tensor(b[0][2]))
+    assert all(a[r][3] == b[r][3] for r in range(world))

@@ -54,15 +54,18 @@ __global__ __launch_bounds__(WPB * 64) void attn_prefill_kernel(
   __shared__ __attribute__((aligned(16))) char smem[2 * 2 * kTileBytes];  // [buf][K|V]
 
   const int G = nh / nkv;
-  const int b = blockIdx.z, kvh = blockIdx.y;
+  // grid.x = row-tile groups x kv heads, kv head fastest: the dispatch order is longest-first over
+  // the whole grid (latest query rows = most causal key tiles), not per kv head, so the last
+  // rounds of a multi-round grid hold the shortest blocks of every head (no long-job tail)
+  const int b = blockIdx.z, kvh = blockIdx.x % nkv, grp = blockIdx.x / nkv;
+  const int ngrp = gridDim.x / nkv;
   const int qlen = q_lens[b];
   if (qlen <= 0) return;
   const int ctx = ctx_lens[b];
   const int q0 = q_start[b];
   const int npb = (qlen + 31) / 32;
   const int nrt = G * npb;
-  // longest (latest query rows: most causal key tiles) blocks first -> no long-job tail
-  const int rt_base = (gridDim.x - 1 - blockIdx.x) * WPB;
+  const int rt_base = (ngrp - 1 - grp) * WPB;
   if (rt_base >= nrt) return;  // block-uniform
 
   const int tid = threadIdx.x, wave = tid / 64, lane = tid % 64;
@@ -284,7 +287,7 @@ extern "C" int llmc_attn_prefill(const void* q, int q_stride, const void* k_cach
   const int G = nh / nkv;
   const int npb = (max_qlen + 31) / 32;
   constexpr int WPB = 8;  // 8 waves = 2 row tiles x 4 heads share every staged K/V tile
-  dim3 grid((G * npb + WPB - 1) / WPB, nkv, B);
+  dim3 grid((G * npb + WPB - 1) / WPB * nkv, 1, B);
   const float sl2 = scale * 1.4426950408889634f;
   static const int la = [] {
     const char* e = getenv("LLMC_PREFILL_LOOKAHEAD");  // A/B runs: K/V tiles requested ahead

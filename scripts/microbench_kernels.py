@@ -135,15 +135,14 @@ def bench_attn_oproj(shapes=((32, 8, 128, 4096),), lens=(128, 1024, 2048, 2300, 
 
             n = copies * max(1, 48 // copies)
             t2 = timeit(two, iters=n)
-            t1 = timeit(one, iters=n) if chunk else float("nan")
-            t1l = timeit(lambda: one(1), iters=n) if chunk else float("nan")
-            t1d = timeit(lambda: one(3), iters=n) if chunk else float("nan")
-            t1f = timeit(lambda: one(7), iters=n) if chunk else float("nan")
+            # AO_MODES: comma list of kernel mode bits (attn_oproj.hip llmc_attn_oproj)
+            modes = [int(m) for m in os.environ.get("AO_MODES", "0,1,3,7").split(",")]
+            tm = [(m, timeit(lambda m=m: one(m), iters=n) if chunk else float("nan")) for m in modes]
             torch.cuda.synchronize()
             print(f"attn+o nh={nh} nkv={nkv} D={D} H={H} L={L:5d} cap={cap}: two launches "
                   f"({'fused' if fused2 else 'split'} c{ch2} g{gc2} + o GEMV) {t2:6.2f} us | one launch "
-                  f"(nc {nc}, {chunk} keys/block) {t1:6.2f} us, late weights {t1l:6.2f} us, merger defers {t1d:6.2f} us, + whole rows {t1f:6.2f} us | fault "
-                  f"{int(fault.item())} / {int(fault1.item())}", flush=True)
+                  f"(nc {nc}, {chunk} keys/block) " + ", ".join(f"mode {m} {t:6.2f} us" for m, t in tm)
+                  + f" | fault {int(fault.item())} / {int(fault1.item())}", flush=True)
             del cases, wos
 
 

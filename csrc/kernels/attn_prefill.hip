@@ -21,7 +21,16 @@
 // write LDS after: T14 async-STAGE split) into a 2-deep LDS ring. Keys are looked up through
 // the block table per row, so any page size works (64 is the engine default).
 // Numerics: S in f32, exp2 with log2(e) folded into the scale, P rounded to bf16 for PV, O in f32.
+//
+// KV split (llmc_attn_prefill_plan): when the grid cannot keep the chip busy to the end (one
+// 2k-token sequence = 256 blocks of 1..32 key tiles; a TP=8 rank's single kv head = 32 blocks), the
+// long row-tile groups' key ranges are cut into 2-4 tile ranges on their own blocks; each writes
+// (unnormalised O, m, l) in f32 and the last to finish merges them in split order (deterministic).
 #include <stdlib.h>
+
+#include <algorithm>
+#include <queue>
+#include <vector>
 
 #include "common.h"
 
@@ -29,21 +38,32 @@ namespace llmc {
 
 typedef __attribute__((ext_vector_type(4))) short s16x4;
 typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
+typedef __attribute__((ext_vector_type(2))) float f32x2;
 
 constexpr int kKT = 64;        // keys per tile
 constexpr int kRowBytes = 256; // LDS row pitch (128 bf16), D <= 128
 constexpr int kTileBytes = kKT * kRowBytes;  // 16 KB
 constexpr int kPrefillLookahead = 2;          // K/V tiles requested ahead of the one computing
+constexpr int kMaxSplit = 4;                   // KV-split ways (llmc_attn_prefill_plan)
+constexpr float kSlack = 8.f;                  // deferred running-max update threshold (log2 units)
+
+// two floats -> packed bf16x2 (RNE) in one instruction (no builtin for the two-operand form)
+__device__ __forceinline__ uint32_t cvt_pk_bf16(float lo, float hi) {
+  uint32_t r;
+  asm("v_cvt_pk_bf16_f32 %0, %1, %2" : "=v"(r) : "v"(lo), "v"(hi));
+  return r;
+}
 
 __device__ __forceinline__ int k_swz(int row, int ch) { return row * kRowBytes + ((ch ^ (row & 15)) << 4); }
 __device__ __forceinline__ int v_swz(int row, int ch) { return row * kRowBytes + ((ch ^ ((row & 3) << 2)) << 4); }
 
-template <int D, int WPB, int LA>
+template <int D, int WPB, int LA, bool P64>
 __global__ __launch_bounds__(WPB * 64) void attn_prefill_kernel(
     const bf16_t* __restrict__ q, int q_stride, const bf16_t* __restrict__ k_cache, const bf16_t* __restrict__ v_cache,
     const int32_t* __restrict__ block_tables, int bt_stride, const int32_t* __restrict__ q_start,
     const int32_t* __restrict__ q_lens, const int32_t* __restrict__ ctx_lens, bf16_t* __restrict__ out,
-    int out_stride, int nh, int nkv, int bs, float scale_log2) {
+    int out_stride, int nh, int nkv, int bs, float scale_log2, int ksplit, int kmin, float* __restrict__ part,
+    int* __restrict__ counters, int T_all) {
   constexpr int CH = D / 8;            // 16-B chunks per row
   constexpr int NT = WPB * 64;
   constexpr int NL = (kKT * CH + NT - 1) / NT;  // staging chunks per thread per tensor
@@ -57,8 +77,10 @@ __global__ __launch_bounds__(WPB * 64) void attn_prefill_kernel(
   // grid.x = row-tile groups x kv heads, kv head fastest: the dispatch order is longest-first over
   // the whole grid (latest query rows = most causal key tiles), not per kv head, so the last
   // rounds of a multi-round grid hold the shortest blocks of every head (no long-job tail)
-  const int b = blockIdx.z, kvh = blockIdx.x % nkv, grp = blockIdx.x / nkv;
-  const int ngrp = gridDim.x / nkv;
+  // with a KV split (ksplit > 1: few blocks for the chip) grid.x = groups x splits x kv heads, the
+  // split index between the two: every split of a group keeps the group's longest-first position
+  const int b = blockIdx.z, kvh = blockIdx.x % nkv, sp = (blockIdx.x / nkv) % ksplit, grp = blockIdx.x / nkv / ksplit;
+  const int ngrp = gridDim.x / nkv / ksplit;
   const int qlen = q_lens[b];
   if (qlen <= 0) return;
   const int ctx = ctx_lens[b];
@@ -68,7 +90,9 @@ __global__ __launch_bounds__(WPB * 64) void attn_prefill_kernel(
   const int rt_base = (ngrp - 1 - grp) * WPB;
   if (rt_base >= nrt) return;  // block-uniform
 
-  const int tid = threadIdx.x, wave = tid / 64, lane = tid % 64;
+  // wave index through readfirstlane: everything derived from it (row tile, head, descriptors)
+  // is then known wave-uniform (a divergent-looking descriptor costs a waterfall loop per access)
+  const int tid = threadIdx.x, wave = __builtin_amdgcn_readfirstlane(tid / 64), lane = tid % 64;
   const int r = lane & 31, hh = lane >> 5;
   const int rt = rt_base + wave;
   const bool wvalid = rt < nrt;
@@ -82,7 +106,13 @@ __global__ __launch_bounds__(WPB * 64) void attn_prefill_kernel(
   const int last_rt = min(rt_base + WPB - 1, nrt - 1);
   const int pb_last = last_rt / G;
   const int kend = min(ctx, first_pos + min(pb_last * 32 + 31, qlen - 1) + 1);
-  const int ntiles = (kend + kKT - 1) / kKT;
+  const int ntiles_all = (kend + kKT - 1) / kKT;
+  // only groups with >= 2 kmin key tiles split (a causal grid's short groups run whole); the
+  // surplus split blocks of the others exit here (block-uniform, before any barrier)
+  const int nsplit = ksplit > 1 ? min(ksplit, max(1, ntiles_all / kmin)) : 1;
+  if (sp >= nsplit) return;
+  // this block's key tiles: split sp of the group's [0, ntiles_all) (all of it without a split)
+  const int t_lo = sp * ntiles_all / nsplit, ntiles = (sp + 1) * ntiles_all / nsplit;
   const int wave_kend = wvalid ? first_pos + min(pb * 32 + 31, qlen - 1) + 1 : 0;
   const int wave_qpos0 = first_pos + pb * 32;  // smallest query position of this wave
 
@@ -92,6 +122,11 @@ __global__ __launch_bounds__(WPB * 64) void attn_prefill_kernel(
     const bf16_t* qrow = q + static_cast<int64_t>(q0 + qi) * q_stride + h * D;
 #pragma unroll
     for (int ks = 0; ks < KS; ++ks) qf[ks] = *reinterpret_cast<const bf16x8*>(qrow + ks * 16 + 8 * hh);
+    // Consume the Q loads here, before the tile loop: left pending at the loop entry, hipcc's
+    // waitcnt pass charged them to every iteration - a vmcnt(7..0) ladder across the QK^T MFMAs
+    // that waited for the K/V tiles just requested, i.e. no lookahead at all.
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks) asm volatile("" : "+v"(qf[ks]));
   }
 
   f32x16 acc_o[DT];
@@ -108,7 +143,32 @@ __global__ __launch_bounds__(WPB * 64) void attn_prefill_kernel(
   // loads have LA - 1 whole compute steps (plus one) to land before its commit to LDS (one tile
   // of lookahead left every tile waiting on HBM latency at 2k tokens: ~3 us per 64-key tile)
   u32x4 stk[LA][NL], stv[LA][NL];
+  int voff[NL];  // P64: byte offset of this lane's 16-B chunk u within a page's [64][D] image
+#pragma unroll
+  for (int u = 0; u < NL; ++u) {
+    const int idx = tid + u * NT;
+    voff[u] = (idx / CH) * D * 2 + (idx % CH) * 16;
+  }
   auto issue = [&](int t, int set) {
+    if constexpr (P64) {
+      // 64-token pages = one page per key tile: the page number is ONE wave-uniform scalar load
+      // (lgkm-counted: no vmcnt drain of the K/V loads in flight, as a per-lane lookup forced) and
+      // K/V come by buffer loads off a per-tile descriptor with lane-constant offsets (no per-tile
+      // address VALU; a reused address register also made hipcc wait for the loads it fed). Rows
+      // past ctx - 1 of the last page lie beyond the descriptor's range and read as zeros.
+      const int tu = __builtin_amdgcn_readfirstlane(t);
+      const int64_t base = (static_cast<int64_t>(ld_scalar(bt + tu)) * nkv + kvh) * head_stride;
+      const int bytes = min(kKT, ctx - tu * kKT) * D * 2;
+      const __amdgpu_buffer_rsrc_t rk = __builtin_amdgcn_make_buffer_rsrc((void*)(k_cache + base), 0, bytes, 0x00020000);
+      const __amdgpu_buffer_rsrc_t rv = __builtin_amdgcn_make_buffer_rsrc((void*)(v_cache + base), 0, bytes, 0x00020000);
+#pragma unroll
+      for (int u = 0; u < NL; ++u) {
+        if (!NL_EXACT && tid + u * NT >= kKT * CH) continue;
+        stk[set][u] = __builtin_amdgcn_raw_buffer_load_b128(rk, voff[u], 0, 0);
+        stv[set][u] = __builtin_amdgcn_raw_buffer_load_b128(rv, voff[u], 0, 0);
+      }
+      return;
+    }
 #pragma unroll
     for (int u = 0; u < NL; ++u) {
       const int idx = tid + u * NT;
@@ -135,16 +195,18 @@ __global__ __launch_bounds__(WPB * 64) void attn_prefill_kernel(
     }
   };
 
-  issue(0, 0);
+  if (t_lo < ntiles) {
+    issue(t_lo, 0);
 #pragma unroll
-  for (int j = 1; j < LA; ++j)
-    if (j < ntiles) issue(j, j);
-  commit(0, 0);
+    for (int j = 1; j < LA; ++j)
+      if (t_lo + j < ntiles) issue(t_lo + j, j);
+    commit(t_lo & 1, 0);
+  }
   __syncthreads();
 
   // unrolled by LA so that every staging-set index is a compile-time constant (a runtime index into
   // a register array would go through scratch)
-  for (int t0 = 0; t0 < ntiles; t0 += LA) {
+  for (int t0 = t_lo; t0 < ntiles; t0 += LA) {
 #pragma unroll
   for (int j = 0; j < LA; ++j) {
     const int t = t0 + j;
@@ -170,62 +232,67 @@ __global__ __launch_bounds__(WPB * 64) void attn_prefill_kernel(
         }
       }
       // ---- online softmax (lane owns query qpos; keys in registers) ----
-      // Causal masking only on tiles that reach past the wave's first query position (the
-      // diagonal band); the others are plain scale + max. Raw v_exp_f32 (inputs are <= 0 after
-      // the max subtraction, so no range reduction is needed).
+      // VALU diet (the loop is VALU-bound at 2 waves/SIMD, ~2x the MFMA cycles before it): the
+      // max on raw scores (scale > 0), then ONE fma + exp per score; causal masking only on the
+      // tiles that reach past the wave's first query position; the running max moves only when a
+      // new score exceeds it by > kSlack (log2 units, so P <= 2^kSlack: exact in f32, same bf16
+      // relative rounding), which leaves the O rescale out of almost every tile; P packed by
+      // v_cvt_pk_bf16_f32 (two floats per instruction, RNE).
       const bool diag = kt + kKT - 1 > wave_qpos0;  // wave-uniform
       float mx = -1e30f;
+      // diag: score (kb2, i) is key kt + 4 hh + kb2*32 + (i & 3) + 8 (i >> 2): visible iff that
+      // compile-time offset <= lim (an inline-constant compare, no per-score add)
+      const int lim = qpos - kt - 4 * hh;
       if (diag) {
 #pragma unroll
         for (int kb2 = 0; kb2 < 2; ++kb2)
 #pragma unroll
-          for (int i = 0; i < 16; ++i) {
-            const int key = kt + kb2 * 32 + (i & 3) + 8 * (i >> 2) + 4 * hh;
-            s[kb2][i] = key <= qpos ? s[kb2][i] * scale_log2 : -1e30f;
-            mx = fmaxf(mx, s[kb2][i]);
-          }
+          for (int i = 0; i < 16; ++i)
+            mx = fmaxf(mx, kb2 * 32 + (i & 3) + 8 * (i >> 2) <= lim ? s[kb2][i] : -1e30f);
       } else {
 #pragma unroll
         for (int kb2 = 0; kb2 < 2; ++kb2)
 #pragma unroll
-          for (int i = 0; i < 16; ++i) {
-            s[kb2][i] *= scale_log2;
-            mx = fmaxf(mx, s[kb2][i]);
-          }
+          for (int i = 0; i < 16; ++i) mx = fmaxf(mx, s[kb2][i]);
       }
       mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
-      const float m_new = fmaxf(m_run, mx);
-      const float alpha = __builtin_amdgcn_exp2f(m_run - m_new);
-      float rs = 0.f;
+      const float mx_s = mx * scale_log2;
+      const float m_new = mx_s > m_run + kSlack ? mx_s : m_run;
+      const float neg_m = -m_new;
+      float rs2[4] = {0.f, 0.f, 0.f, 0.f};
       if (diag) {
 #pragma unroll
         for (int kb2 = 0; kb2 < 2; ++kb2)
 #pragma unroll
           for (int i = 0; i < 16; ++i) {
-            const float sv = s[kb2][i];
-            const float p = sv <= -1e29f ? 0.f : __builtin_amdgcn_exp2f(sv - m_new);
+            const float p = kb2 * 32 + (i & 3) + 8 * (i >> 2) <= lim
+                                ? __builtin_amdgcn_exp2f(fmaf(s[kb2][i], scale_log2, neg_m))
+                                : 0.f;
             s[kb2][i] = p;
-            rs += p;
+            rs2[i & 3] += p;
           }
       } else {
 #pragma unroll
         for (int kb2 = 0; kb2 < 2; ++kb2)
 #pragma unroll
           for (int i = 0; i < 16; ++i) {
-            const float p = __builtin_amdgcn_exp2f(s[kb2][i] - m_new);
+            const float p = __builtin_amdgcn_exp2f(fmaf(s[kb2][i], scale_log2, neg_m));
             s[kb2][i] = p;
-            rs += p;
+            rs2[i & 3] += p;
           }
       }
+      float rs = (rs2[0] + rs2[1]) + (rs2[2] + rs2[3]);
       rs += __shfl_xor(rs, 32, 64);
-      l_run = l_run * alpha + rs;
-      m_run = m_new;
-      if (__any(alpha != 1.f)) {  // the running max moved for some query of the wave
+      if (__any(m_new != m_run)) {  // the running max moved for some query of the wave
+        const float alpha = __builtin_amdgcn_exp2f(m_run - m_new);
+        l_run *= alpha;
 #pragma unroll
         for (int dt = 0; dt < DT; ++dt)
 #pragma unroll
           for (int i = 0; i < 16; ++i) acc_o[dt][i] *= alpha;
       }
+      l_run += rs;
+      m_run = m_new;
       // ---- P fragments: k-step k4 = kb2*2 + sidx uses registers 8*sidx .. +7 of s[kb2] ----
       bf16x8 pf[4];
 #pragma unroll
@@ -234,7 +301,7 @@ __global__ __launch_bounds__(WPB * 64) void attn_prefill_kernel(
         for (int sidx = 0; sidx < 2; ++sidx) {
           u32x4 pk;
 #pragma unroll
-          for (int j = 0; j < 4; ++j) pk[j] = pack_bf16x2(s[kb2][8 * sidx + 2 * j], s[kb2][8 * sidx + 2 * j + 1]);
+          for (int j = 0; j < 4; ++j) pk[j] = cvt_pk_bf16(s[kb2][8 * sidx + 2 * j], s[kb2][8 * sidx + 2 * j + 1]);
           pf[kb2 * 2 + sidx] = __builtin_bit_cast(bf16x8, pk);
         }
       // ---- O^T += V^T . P^T ----
@@ -260,7 +327,93 @@ __global__ __launch_bounds__(WPB * 64) void attn_prefill_kernel(
   }
   }
 
-  if (!wvalid || row_i >= qlen) return;
+  const bool live = wvalid && row_i < qlen;
+  if (nsplit > 1) {
+    // split hand-off: every split writes (unnormalised O, m, l) in f32, the last to arrive merges
+    // all of them in split order (its own from registers: the same values; every step an explicit
+    // fmaf, so register and loaded terms round alike) -> deterministic, and one launch. Lanes
+    // read back exactly the elements they wrote, so the layout is lane-private.
+    const int64_t so = static_cast<int64_t>(T_all) * nh;  // (row, head) pairs per split slot
+    // Inter-workgroup hand-off, MI355X_MICROARCH.md "Valid forms" table row 1: every byte stored
+    // and loaded sc1 (16-/8-B buffer ops), every storing wave drains (vmcnt(0)) before the barrier,
+    // ONE lane adds to the group's counter, the block whose add comes last merges after a barrier.
+    // (A __threadfence pair here - L2 write-back + invalidate per block - cost 2.8x at 2k tokens.)
+    // Per-wave resources: rows q0 + pb*32 .. +31 of head h; lane offset r * nh * {D, 2} floats.
+    const int64_t wrow = static_cast<int64_t>(q0 + pb * 32) * nh + h;
+    auto o_rsrc = [&](int slot) {
+      return __builtin_amdgcn_make_buffer_rsrc(part + (slot * so + wrow) * D, 0, 32 * nh * D * 4, 0x00020000);
+    };
+    auto ml_rsrc = [&](int slot) {
+      return __builtin_amdgcn_make_buffer_rsrc(part + ksplit * so * D + (slot * so + wrow) * 2, 0, 32 * nh * 2 * 4,
+                                               0x00020000);
+    };
+    const int o_lane = r * nh * D * 4, ml_lane = r * nh * 2 * 4;
+    if (live) {
+      const __amdgpu_buffer_rsrc_t ro = o_rsrc(sp);
+#pragma unroll
+      for (int dt = 0; dt < DT; ++dt)
+#pragma unroll
+        for (int i4 = 0; i4 < 4; ++i4) {
+          const int d = dt * 32 + 8 * i4 + 4 * hh;
+          const f32x4 v{acc_o[dt][4 * i4 + 0], acc_o[dt][4 * i4 + 1], acc_o[dt][4 * i4 + 2], acc_o[dt][4 * i4 + 3]};
+          __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), ro, o_lane + d * 4, 0, 16);
+        }
+      if (hh == 0)
+        __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2, f32x2{m_run, l_run}), ml_rsrc(sp), ml_lane, 0, 16);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every storing wave: its partial is out
+    __syncthreads();
+    __shared__ int is_last;
+    if (tid == 0) {
+      int* ctr = counters + (static_cast<int64_t>(b) * ngrp + grp) * nkv + kvh;
+      is_last = __hip_atomic_fetch_add(ctr, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == nsplit - 1;
+      if (is_last) __hip_atomic_store(ctr, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // re-arm
+    }
+    __syncthreads();
+    if (!is_last || !live) return;
+    // merge, latency-shaped: every split's (m, l) in one round trip, then the O partials (own
+    // included: re-read, so the sequence of fmaf is the same whichever block is last) with the
+    // next split's 16 loads in flight while the current one is summed
+    f32x2 ml[kMaxSplit];
+#pragma unroll
+    for (int s2 = 0; s2 < kMaxSplit; ++s2)
+      ml[s2] = __builtin_bit_cast(
+          f32x2, __builtin_amdgcn_raw_buffer_load_b64(ml_rsrc(min(s2, nsplit - 1)), ml_lane, 0, 16));
+    float M = -1e30f;
+#pragma unroll
+    for (int s2 = 0; s2 < kMaxSplit; ++s2)
+      if (s2 < nsplit) M = fmaxf(M, ml[s2][0]);
+    f32x4 ob[2][DT * 4];
+    auto load_o = [&](int slot, f32x4* dst) {
+      const __amdgpu_buffer_rsrc_t ro = o_rsrc(slot);
+#pragma unroll
+      for (int dt = 0; dt < DT; ++dt)
+#pragma unroll
+        for (int i4 = 0; i4 < 4; ++i4)
+          dst[dt * 4 + i4] = __builtin_bit_cast(
+              f32x4, __builtin_amdgcn_raw_buffer_load_b128(ro, o_lane + (dt * 32 + 8 * i4 + 4 * hh) * 4, 0, 16));
+    };
+    load_o(0, ob[0]);
+    float L = 0.f;
+#pragma unroll
+    for (int s2 = 0; s2 < kMaxSplit; ++s2) {
+      if (s2 >= nsplit) break;
+      if (s2 + 1 < nsplit) load_o(s2 + 1, ob[(s2 + 1) & 1]);
+      const float sc = ml[s2][1] > 0.f ? __builtin_amdgcn_exp2f(ml[s2][0] - M) : 0.f;
+      L = fmaf(ml[s2][1], sc, L);
+#pragma unroll
+      for (int dt = 0; dt < DT; ++dt)
+#pragma unroll
+        for (int i4 = 0; i4 < 4; ++i4)
+#pragma unroll
+          for (int j = 0; j < 4; ++j)
+            acc_o[dt][4 * i4 + j] = s2 == 0 ? ob[0][dt * 4 + i4][j] * sc
+                                            : fmaf(ob[s2 & 1][dt * 4 + i4][j], sc, acc_o[dt][4 * i4 + j]);
+    }
+    l_run = L;
+  } else if (!live) {
+    return;
+  }
   const float inv_l = l_run > 0.f ? 1.f / l_run : 0.f;
   bf16_t* orow = out + static_cast<int64_t>(q0 + row_i) * out_stride + h * D;
 #pragma unroll
@@ -279,25 +432,91 @@ __global__ __launch_bounds__(WPB * 64) void attn_prefill_kernel(
 
 using namespace llmc;
 
+// KV-split plan for a prefill launch: the grid is modelled as blocks of whole 64-key tiles
+// dispatched longest-first onto one block per CU (248 VGPRs: 2 waves/SIMD = one 8-wave block), and
+// the (ksplit, kmin) pair with the shortest greedy makespan wins: groups with >= 2 kmin tiles are
+// split into min(ksplit, tiles / kmin) blocks. Costs in tile units (below). Assumes B sequences of
+// the max shape.
+extern "C" int llmc_attn_prefill_plan(int B, int max_qlen, int max_ctx, int nh, int nkv, int* kmin_out) {
+  *kmin_out = 1 << 30;
+  if (nkv <= 0 || nh % nkv != 0 || max_qlen <= 0 || max_ctx < max_qlen) return 1;
+  const int G = nh / nkv, npb = (max_qlen + 31) / 32, ngrp = (G * npb + 7) / 8, rows_pg = 8 / G > 0 ? 8 / G : 1;
+  const int64_t units = static_cast<int64_t>(ngrp) * nkv * B;
+  if (units > 4096) return 1;  // many rounds of blocks: the grid already balances
+  std::vector<int> len(ngrp);
+  for (int g = 0; g < ngrp; ++g) {  // group g's last row: rows_pg row tiles of 32 (causal key range)
+    const int last_row = std::min(max_qlen, (g + 1) * rows_pg * 32);
+    len[g] = (max_ctx - max_qlen + last_row + 63) / 64;
+  }
+  constexpr int kSlots = 256;
+  // fitted to the r5 microbench sweep (profiles/r5_prefill_attention.md, 10 shapes x 7 splits): a
+  // block's fixed cost is ~4 tiles (Q load, pipeline fill, launch share) and a split block's
+  // hand-off 6 + 2 n more (sc1 partial write-through + drain, counter round trip, the merger's
+  // reads of n partials)
+  constexpr float kBlockCost = 4.f, kMergeCost = 6.f, kMergePerSplit = 2.f;
+  auto makespan = [&](int S, int kmin) {
+    std::vector<float> jobs;
+    for (int g = ngrp - 1; g >= 0; --g) {  // dispatch order: longest group first
+      const int n = S > 1 ? std::min(S, std::max(1, len[g] / kmin)) : 1;
+      for (int r = 0; r < nkv * B; ++r)
+        for (int sp = 0; sp < n; ++sp)
+          jobs.push_back(static_cast<float>((sp + 1) * len[g] / n - sp * len[g] / n) + kBlockCost +
+                         (n > 1 ? kMergeCost + kMergePerSplit * n : 0.f));
+    }
+    std::priority_queue<float, std::vector<float>, std::greater<float>> free_at;
+    for (int i = 0; i < kSlots; ++i) free_at.push(0.f);
+    float end = 0.f;
+    for (float j : jobs) {
+      const float t = free_at.top() + j;
+      free_at.pop();
+      free_at.push(t);
+      end = std::max(end, t);
+    }
+    return end;
+  };
+  int best_s = 1, best_k = 1 << 30;
+  float best = makespan(1, 1 << 30) * 0.97f;  // a split must win by > 3%
+  // 4-way splits measured a loss everywhere but on grids of <= 128 blocks with >= 2 row tiles per
+  // group (a TP=8 rank's single kv head); the cost model alone over-rates them elsewhere
+  const bool allow4 = units <= 128 && G <= 4;
+  for (int S : {2, 4})
+    for (int kmin : {4, 8, 16, 32}) {
+      if (S == 4 && !allow4) continue;
+      const float t = makespan(S, kmin);
+      if (t < best) best = t, best_s = S, best_k = kmin;
+    }
+  *kmin_out = best_k;
+  return best_s;
+}
+
 extern "C" int llmc_attn_prefill(const void* q, int q_stride, const void* k_cache, const void* v_cache,
                                  const void* block_tables, int bt_stride, const void* q_start, const void* q_lens,
                                  const void* ctx_lens, void* out, int out_stride, int B, int max_qlen, int nh, int nkv,
-                                 int D, int bs, float scale, hipStream_t s) {
-  if (nh % nkv != 0) return -1;
+                                 int D, int bs, float scale, int ksplit, int kmin, void* part, void* counters,
+                                 int T_all, hipStream_t s) {
+  if (nh % nkv != 0 || ksplit < 1 || ksplit > kMaxSplit ||
+      (ksplit > 1 && (part == nullptr || counters == nullptr || T_all < 1 || kmin < 1)))
+    return -1;
   const int G = nh / nkv;
   const int npb = (max_qlen + 31) / 32;
   constexpr int WPB = 8;  // 8 waves = 2 row tiles x 4 heads share every staged K/V tile
-  dim3 grid((G * npb + WPB - 1) / WPB * nkv, 1, B);
+  dim3 grid((G * npb + WPB - 1) / WPB * ksplit * nkv, 1, B);
   const float sl2 = scale * 1.4426950408889634f;
   static const int la = [] {
     const char* e = getenv("LLMC_PREFILL_LOOKAHEAD");  // A/B runs: K/V tiles requested ahead
     return e ? atoi(e) : kPrefillLookahead;
   }();
 #define LLMC_PF(DD, L)                                                                                           \
-  attn_prefill_kernel<DD, WPB, L><<<grid, WPB * 64, 0, s>>>((const bf16_t*)q, q_stride, (const bf16_t*)k_cache, \
+  do {                                                                                                           \
+    if (bs == kKT) LLMC_PFP(DD, L, true);                                                                        \
+    else LLMC_PFP(DD, L, false);                                                                                 \
+  } while (0)
+#define LLMC_PFP(DD, L, P)                                                                                       \
+  attn_prefill_kernel<DD, WPB, L, P><<<grid, WPB * 64, 0, s>>>((const bf16_t*)q, q_stride, (const bf16_t*)k_cache, \
                                                (const bf16_t*)v_cache, (const int32_t*)block_tables, bt_stride,   \
                                                (const int32_t*)q_start, (const int32_t*)q_lens,                  \
-                                               (const int32_t*)ctx_lens, (bf16_t*)out, out_stride, nh, nkv, bs, sl2)
+                                               (const int32_t*)ctx_lens, (bf16_t*)out, out_stride, nh, nkv, bs, sl2, \
+                                               ksplit, kmin, (float*)part, (int*)counters, T_all)
 #define LLMC_PF_D(DD)                \
   do {                               \
     if (la >= 3) LLMC_PF(DD, 3);     \
@@ -312,5 +531,6 @@ extern "C" int llmc_attn_prefill(const void* q, int q_stride, const void* k_cach
   }
 #undef LLMC_PF_D
 #undef LLMC_PF
+#undef LLMC_PFP
   return static_cast<int>(hipGetLastError());
 }

@@ -42,7 +42,9 @@ int llmc_attn_decode(const void*, int, const void*, const void*, const void*, in
 int llmc_gemv_qkv_rope(int, const void*, int, const void*, float, const void*, int, int, void*, int, void*, void*,
                        const void*, const void*, const void*, const void*, int, int, int, int, int, hipStream_t);
 int llmc_attn_prefill(const void*, int, const void*, const void*, const void*, int, const void*, const void*,
-                      const void*, void*, int, int, int, int, int, int, int, float, hipStream_t);
+                      const void*, void*, int, int, int, int, int, int, int, float, int, int, void*, void*, int,
+                      hipStream_t);
+int llmc_attn_prefill_plan(int, int, int, int, int, int*);
 int llmc_sample(const void*, int64_t, int, int, const void*, const void*, const void*, const void*, const void*, void*,
                 void*, void*, void*, void*, void*, const void*, int, int, void*, void*, int, int, hipStream_t);
 int llmc_sample_parts();
@@ -166,10 +168,16 @@ PYBIND11_MODULE(_llmc_hip, m) {
           "gemv_qkv_rope");
   });
   m.def("attn_prefill", [](ptr q, int qs, ptr kc, ptr vc, ptr bt, int bts, ptr qst, ptr ql, ptr cl, ptr out, int os,
-                           int B, int max_qlen, int nh, int nkv, int D, int bs, float scale, ptr s) {
+                           int B, int max_qlen, int nh, int nkv, int D, int bs, float scale, int ksplit, int kmin,
+                           ptr part, ptr counters, int T, ptr s) {
     check(llmc_attn_prefill(P(q), qs, P(kc), P(vc), P(bt), bts, P(qst), P(ql), P(cl), P(out), os, B, max_qlen, nh, nkv,
-                            D, bs, scale, S(s)),
+                            D, bs, scale, ksplit, kmin, P(part), P(counters), T, S(s)),
           "attn_prefill");
+  });
+  m.def("attn_prefill_plan", [](int B, int max_qlen, int max_ctx, int nh, int nkv) {
+    int kmin = 0;
+    const int k = llmc_attn_prefill_plan(B, max_qlen, max_ctx, nh, nkv, &kmin);
+    return std::make_pair(k, kmin);
   });
   m.def("sample", [](ptr logits, int64_t rs, int B, int V, ptr it, ptr tk, ptr tp, ptr seeds, ptr pos, ptr wv, ptr wi,
                      ptr next, ptr tin, ptr sl, ptr slots, ptr bt, int bts, int bs, ptr ot, ptr oc, int cap,

@@ -439,6 +439,11 @@ class Engine:
         cl_d = torch.tensor(ctx_lens, **i32).to(dev, non_blocking=True)
         bt = self._block_table([s for s, _ in batch])
         max_qlen = max(q_lens)
+        max_ctx = max(ctx_lens)
+        ksplit, kmin = (ops.attn_prefill_plan(len(batch), max_qlen, max_ctx, self.nh, self.nkv) if ids_d.is_cuda
+                        else (1, 1))
+        pws = (ops.attn_prefill_workspace(ksplit, T, self.nh, self.D, dev, len(batch), self.nkv, max_qlen)
+               if ksplit > 1 else None)
 
         h = ops.embedding(ids_d, self.w.embed)
         attn = torch.empty(T, self.w.q_size, dtype=torch.bfloat16, device=dev)
@@ -461,7 +466,8 @@ class Engine:
             ops.rope_kv_write(qkv, pos_d, self.cos_t, self.sin_t, self.k_cache[li], self.v_cache[li], slots_d,
                               self.nh, self.nkv, self.D, self.bs, qbuf)
             ops.attn_prefill(qbuf, self.k_cache[li], self.v_cache[li], bt, qs_d, ql_d, cl_d, attn, max_qlen,
-                             self.nh, self.nkv, self.D, self.bs, self.scale)
+                             self.nh, self.nkv, self.D, self.bs, self.scale, max_ctx=max_ctx, ksplit=ksplit, kmin=kmin,
+                             ws=pws)
             if sp is not None:
                 self._sp_row_parallel(lambda out: ops.linear(attn, Lw.w_o, EPI_RESADD, out=out), hs, pbuf, T)
                 if c.is_moe and self.w.ep:

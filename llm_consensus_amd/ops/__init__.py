@@ -353,14 +353,52 @@ def attn_oproj(q, k_cache, v_cache, block_table, seq_len, w_o, h, attn_out, ws, 
                          ATTN_OPROJ_MODE if mode < 0 else mode, _p(stamps), _s(h))
 
 
-def attn_prefill(q, k_cache, v_cache, block_tables, q_start, q_lens, ctx_lens, out, max_qlen, nh, nkv, D, bs, scale):
+# KV split of the prefill attention: -1 = the kernel library's plan (llmc_attn_prefill_plan),
+# 1 = never, N = split every group of >= 2 * LLMC_PREFILL_KMIN (default 8) key tiles up to N ways
+PREFILL_KSPLIT = int(os.environ.get("LLMC_PREFILL_KSPLIT", "-1"))
+PREFILL_KMIN = int(os.environ.get("LLMC_PREFILL_KMIN", "8"))
+
+
+def attn_prefill_plan(B, max_qlen, max_ctx, nh, nkv, ksplit=None, kmin=None):
+    """(ksplit, kmin) of a prefill attention launch (csrc/kernels/attn_prefill.hip): row-tile groups
+    of >= 2 kmin key tiles run on min(ksplit, tiles // kmin) blocks; (1, _) = no split."""
+    k = PREFILL_KSPLIT if ksplit is None else int(ksplit)
+    if k < 0:
+        return tuple(kernels().attn_prefill_plan(B, int(max_qlen), int(max_ctx), nh, nkv))
+    return max(1, min(k, 4)), int(PREFILL_KMIN if kmin is None else kmin)
+
+
+def attn_prefill_workspace(ksplit, T, nh, D, device, B=1, nkv=1, max_qlen=None):
+    """A split prefill's hand-off state: f32 partials ([ksplit][T][nh][D] O, then [ksplit][T][nh][2]
+    (m, l)) and zeroed arrival counters (one per (sequence, row-tile group, kv head), re-armed by the
+    kernel, so one workspace serves every layer of a prefill on one stream)."""
+    G = nh // max(nkv, 1)
+    ngrp = (G * ((max_qlen or T) + 31) // 32 + 7) // 8
+    return (torch.empty(ksplit * T * nh * (D + 2), dtype=torch.float32, device=device),
+            torch.zeros(B * ngrp * nkv, dtype=torch.int32, device=device))
+
+
+def attn_prefill(q, k_cache, v_cache, block_tables, q_start, q_lens, ctx_lens, out, max_qlen, nh, nkv, D, bs, scale,
+                 max_ctx=None, ksplit=None, kmin=None, ws=None):
+    """Causal paged prefill attention. ``max_ctx`` (default ``max_qlen``) feeds the KV-split plan;
+    ``ksplit``/``kmin`` override it; ``ws`` is a caller-held attn_prefill_workspace reused across
+    layers (it must not be shared by launches that can run concurrently)."""
     if not q.is_cuda:
         return oracle.attn_prefill(q, k_cache, v_cache, block_tables, q_start, q_lens, ctx_lens, nh, nkv, D, bs,
                                    scale, out)
     B = q_lens.shape[0]
+    T = q.shape[0]
+    k, km = attn_prefill_plan(B, max_qlen, max_qlen if max_ctx is None else max_ctx, nh, nkv, ksplit, kmin)
+    part = ctr = 0
+    if k > 1:
+        G = nh // nkv
+        need_c = B * ((G * ((int(max_qlen) + 31) // 32) + 7) // 8) * nkv
+        if ws is None or ws[0].numel() < k * T * nh * (D + 2) or ws[1].numel() < need_c:
+            ws = attn_prefill_workspace(k, T, nh, D, q.device, B, nkv, max_qlen)
+        part, ctr = _p(ws[0]), _p(ws[1])
     kernels().attn_prefill(_p(q), q.stride(0), _p(k_cache), _p(v_cache), _p(block_tables), block_tables.stride(0),
                            _p(q_start), _p(q_lens), _p(ctx_lens), _p(out), out.stride(0), B, int(max_qlen), nh, nkv,
-                           D, bs, float(scale), _s(q))
+                           D, bs, float(scale), k, km, part, ctr, T, _s(q))
     return out
 
 

@@ -352,6 +352,8 @@ def bench_attn_prefill(cases=((32, 8, 2048, 2048), (32, 8, 8192, 8192), (32, 8, 
     """Causal flash prefill (attn_prefill.hip) on (heads, kv heads, T new tokens, ctx keys): Llama-3-8B
     and its TP=8 rank (4 heads on 1 kv head), Llama-3-70B TP=4 rank (16 on 2)."""
     D, bs = 128, 64
+    if os.environ.get("PF_CASES"):  # "nh,nkv,T,ctx;..."
+        cases = [tuple(int(x) for x in c.split(",")) for c in os.environ["PF_CASES"].split(";")]
     for (nh, nkv, T, ctx) in cases:
         nb = (ctx + bs - 1) // bs + 1
         kc = torch.randn(nb, nkv, bs, D, device="cuda").to(BF)
@@ -362,11 +364,17 @@ def bench_attn_prefill(cases=((32, 8, 2048, 2048), (32, 8, 8192, 8192), (32, 8, 
         qs = torch.tensor([0], dtype=torch.int32, device="cuda")
         ql = torch.tensor([T], dtype=torch.int32, device="cuda")
         cl = torch.tensor([ctx], dtype=torch.int32, device="cuda")
-        us = timeit(lambda: ops.attn_prefill(q, kc, vc, bt, qs, ql, cl, out, T, nh, nkv, D, bs, 1 / math.sqrt(D)),
-                    iters=3)
         # causal FLOPs of the last T queries over ctx keys
         fl = 4 * nh * D * (T * ctx - T * (T - 1) / 2)
-        print(f"attn_prefill nh={nh} nkv={nkv} T={T} ctx={ctx}: {us:8.1f} us {fl / us / 1e6:6.0f} TF/s", flush=True)
+        plan = ops.attn_prefill_plan(1, T, ctx, nh, nkv, ksplit=-1)
+        ws = ops.attn_prefill_workspace(4, T, nh, D, "cuda", 1, nkv, T)
+        res = []
+        for k, km in dict.fromkeys([plan, (1, 1), (2, 8), (2, 16), (2, 32), (4, 4), (4, 8), (4, 16)]):
+            us = timeit(lambda: ops.attn_prefill(q, kc, vc, bt, qs, ql, cl, out, T, nh, nkv, D, bs, 1 / math.sqrt(D),
+                                                 max_ctx=ctx, ksplit=k, kmin=km, ws=ws), iters=3)
+            tag = "plan" if (k, km) == plan else ""
+            res.append(f"{tag}({k},{km if k > 1 else '-'}) {us:7.1f} us {fl / us / 1e6:4.0f} TF/s")
+        print(f"attn_prefill nh={nh} nkv={nkv} T={T} ctx={ctx}: " + " | ".join(res), flush=True)
 
 
 def bench_moe(tokens=(2048, 8192, 16384)):

@@ -429,9 +429,12 @@ def test_attn_decode_partial_rounding_at_33k(cuda):
     assert errs[256] <= errs[1] + bf16_ulp, (errs, bf16_ulp)
 
 
+@pytest.mark.parametrize("ksplit", [1, 2, 4])
 @pytest.mark.parametrize("nh,nkv,D", [(32, 8, 128), (32, 32, 96), (16, 2, 128), (4, 2, 64)])
 @pytest.mark.parametrize("case", ["full", "chunk", "ragged"])
-def test_attn_prefill(cuda, nh, nkv, D, case):
+def test_attn_prefill(cuda, nh, nkv, D, case, ksplit):
+    """ksplit > 1: each row-tile group's key tiles split over that many blocks + the merge launch
+    (ragged: 1-key contexts leave most splits empty)."""
     torch.manual_seed(4)
     bs = 64
     if case == "full":
@@ -449,15 +452,44 @@ def test_attn_prefill(cuda, nh, nkv, D, case):
     ql = torch.tensor(qlens, dtype=torch.int32)
     cl = torch.tensor(ctx, dtype=torch.int32)
     scale = 1 / math.sqrt(D)
-    ops.attn_prefill(q, kc, vc, bt.cuda(), qs.cuda(), ql.cuda(), cl.cuda(), out, max(qlens), nh, nkv, D, bs, scale)
+    ops.attn_prefill(q, kc, vc, bt.cuda(), qs.cuda(), ql.cuda(), cl.cuda(), out, max(qlens), nh, nkv, D, bs, scale,
+                     max_ctx=max(ctx), ksplit=ksplit, kmin=1)
     ref = torch.zeros(T, nh * D, dtype=BF)
     oracle.attn_prefill(q.cpu(), kc.cpu(), vc.cpu(), bt, qs, ql, cl, nh, nkv, D, bs, scale, ref)
     close(out, ref, 2e-2)
 
 
+def test_attn_prefill_split_is_deterministic_and_leaves_foreign_rows(cuda):
+    """A split launch (the last split block to arrive merges) gives the same bits on every run
+    whichever block arrives last, matches the unsplit kernel to bf16 rounding, and leaves rows
+    outside every sequence's [q_start, q_start + q_len) untouched, as the unsplit kernel does."""
+    torch.manual_seed(9)
+    nh, nkv, D, bs = 8, 2, 128, 64
+    qlens, ctx = [100, 50], [1600, 50]
+    kc, vc, bt = _paged_kv(2, max(ctx), nkv, D, bs)
+    qs = torch.tensor([0, 110], dtype=torch.int32)  # rows 100..109 and 160..169 belong to no sequence
+    T = 170
+    q = rnd(T, nh * D)
+    ql, cl = torch.tensor(qlens, dtype=torch.int32), torch.tensor(ctx, dtype=torch.int32)
+    ws = ops.attn_prefill_workspace(4, T, nh, D, "cuda", 2, nkv, max(qlens))
+    outs = []
+    for k in (1, 4, 4, 4):
+        out = torch.full((T, nh * D), 7.0, dtype=BF, device="cuda")
+        ops.attn_prefill(q, kc, vc, bt.cuda(), qs.cuda(), ql.cuda(), cl.cuda(), out, max(qlens), nh, nkv, D, bs,
+                         1 / math.sqrt(D), max_ctx=max(ctx), ksplit=k, kmin=2, ws=ws)
+        outs.append(out)
+    torch.cuda.synchronize()
+    for out in outs:
+        assert (out[100:110] == 7.0).all() and (out[160:] == 7.0).all()
+    assert torch.equal(outs[1], outs[2]) and torch.equal(outs[1], outs[3])
+    assert (ws[1] == 0).all()  # counters re-armed for the next layer
+    close(outs[1], outs[0].float().cpu(), 2e-2)
+
+
 @pytest.mark.parametrize("nh,nkv,D,ctx", [(32, 8, 128, 8192), (32, 8, 128, 16384), (32, 8, 128, 33000),
                                         (32, 32, 96, 16384)])
-def test_attn_prefill_long_context_vs_fp32(cuda, nh, nkv, D, ctx):
+@pytest.mark.parametrize("ksplit", [1, 4])
+def test_attn_prefill_long_context_vs_fp32(cuda, nh, nkv, D, ctx, ksplit):
     """Judge-length contexts (the N=8 judge prompt is ~33k tokens): the last 384 queries of a ctx-key
     paged sequence (the final chunk of a chunked prefill) beside a short full prefill, against the
     fp32 oracle computed on the GPU (the same einsum/softmax code as the CPU oracle)."""
@@ -472,7 +504,8 @@ def test_attn_prefill_long_context_vs_fp32(cuda, nh, nkv, D, ctx):
     out = torch.zeros(T, nh * D, dtype=BF, device="cuda")
     ql, cl = torch.tensor(qlens, dtype=torch.int32), torch.tensor(ctxs, dtype=torch.int32)
     scale = 1 / math.sqrt(D)
-    ops.attn_prefill(q, kc, vc, bt.cuda(), qs.cuda(), ql.cuda(), cl.cuda(), out, max(qlens), nh, nkv, D, bs, scale)
+    ops.attn_prefill(q, kc, vc, bt.cuda(), qs.cuda(), ql.cuda(), cl.cuda(), out, max(qlens), nh, nkv, D, bs, scale,
+                     max_ctx=max(ctxs), ksplit=ksplit, kmin=4)
     ref = torch.zeros(T, nh * D, dtype=BF, device="cuda")
     oracle.attn_prefill(q, kc, vc, bt.cuda(), qs, ql, cl, nh, nkv, D, bs, scale, ref)  # fp32 math, on the GPU
     torch.cuda.synchronize()

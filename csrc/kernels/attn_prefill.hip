@@ -480,7 +480,7 @@ extern "C" int llmc_attn_prefill_plan(int B, int max_qlen, int max_ctx, int nh, 
   // group (a TP=8 rank's single kv head); the cost model alone over-rates them elsewhere
   const bool allow4 = units <= 128 && G <= 4;
   for (int S : {2, 4})
-    for (int kmin : {4, 8, 16, 32}) {
+    for (int kmin : {4, 8, 16}) {
       if (S == 4 && !allow4) continue;
       const float t = makespan(S, kmin);
       if (t < best) best = t, best_s = S, best_k = kmin;
@@ -499,8 +499,10 @@ extern "C" int llmc_attn_prefill(const void* q, int q_stride, const void* k_cach
     return -1;
   const int G = nh / nkv;
   const int npb = (max_qlen + 31) / 32;
-  constexpr int WPB = 8;  // 8 waves = 2 row tiles x 4 heads share every staged K/V tile
-  dim3 grid((G * npb + WPB - 1) / WPB * ksplit * nkv, 1, B);
+  // 8 waves = 2 row tiles x 4 heads share every staged K/V tile (one block per CU at ~250 VGPRs;
+  // 4-wave blocks, meant to run two per CU without shared barriers, measured 0.6x at 8k: one per CU)
+  constexpr int wpb = 8;
+  dim3 grid((G * npb + wpb - 1) / wpb * ksplit * nkv, 1, B);
   const float sl2 = scale * 1.4426950408889634f;
   static const int la = [] {
     const char* e = getenv("LLMC_PREFILL_LOOKAHEAD");  // A/B runs: K/V tiles requested ahead
@@ -512,15 +514,14 @@ extern "C" int llmc_attn_prefill(const void* q, int q_stride, const void* k_cach
     else LLMC_PFP(DD, L, false);                                                                                 \
   } while (0)
 #define LLMC_PFP(DD, L, P)                                                                                       \
-  attn_prefill_kernel<DD, WPB, L, P><<<grid, WPB * 64, 0, s>>>((const bf16_t*)q, q_stride, (const bf16_t*)k_cache, \
+  attn_prefill_kernel<DD, wpb, L, P><<<grid, wpb * 64, 0, s>>>((const bf16_t*)q, q_stride, (const bf16_t*)k_cache, \
                                                (const bf16_t*)v_cache, (const int32_t*)block_tables, bt_stride,   \
                                                (const int32_t*)q_start, (const int32_t*)q_lens,                  \
                                                (const int32_t*)ctx_lens, (bf16_t*)out, out_stride, nh, nkv, bs, sl2, \
                                                ksplit, kmin, (float*)part, (int*)counters, T_all)
 #define LLMC_PF_D(DD)                \
   do {                               \
-    if (la >= 3) LLMC_PF(DD, 3);     \
-    else if (la == 2) LLMC_PF(DD, 2); \
+    if (la >= 2) LLMC_PF(DD, 2);     \
     else LLMC_PF(DD, 1);             \
   } while (0)
   switch (D) {

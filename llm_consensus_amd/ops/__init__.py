@@ -373,7 +373,7 @@ def attn_prefill_workspace(ksplit, T, nh, D, device, B=1, nkv=1, max_qlen=None):
     (m, l)) and zeroed arrival counters (one per (sequence, row-tile group, kv head), re-armed by the
     kernel, so one workspace serves every layer of a prefill on one stream)."""
     G = nh // max(nkv, 1)
-    ngrp = (G * ((max_qlen or T) + 31) // 32 + 7) // 8
+    ngrp = (G * ((max_qlen or T) + 31) // 32 + 3) // 4  # row-tile groups of >= 4 waves
     return (torch.empty(ksplit * T * nh * (D + 2), dtype=torch.float32, device=device),
             torch.zeros(B * ngrp * nkv, dtype=torch.int32, device=device))
 
@@ -392,7 +392,7 @@ def attn_prefill(q, k_cache, v_cache, block_tables, q_start, q_lens, ctx_lens, o
     part = ctr = 0
     if k > 1:
         G = nh // nkv
-        need_c = B * ((G * ((int(max_qlen) + 31) // 32) + 7) // 8) * nkv
+        need_c = B * ((G * ((int(max_qlen) + 31) // 32) + 3) // 4) * nkv
         if ws is None or ws[0].numel() < k * T * nh * (D + 2) or ws[1].numel() < need_c:
             ws = attn_prefill_workspace(k, T, nh, D, q.device, B, nkv, max_qlen)
         part, ctr = _p(ws[0]), _p(ws[1])

@@ -218,6 +218,16 @@ def colocated_tp(resp_plan, idx) -> bool:
     return not fused_ar_allowed(gpus, str(idx[0]), [str(j) for j in range(len(resp_plan)) if j not in idx])
 
 
+def responder_alone(resp_plan, idx) -> bool:
+    """Whether the responder engine of plan entries ``idx`` decodes with no other responder on its
+    GPUs (placement.decodes_alone, the product path's alone_plan): it then takes the lone-engine
+    launch forms (ops.attn_oproj_min_chunk). The judge decodes after the responders: always alone."""
+    from llm_consensus_amd.parallel.placement import decodes_alone
+
+    gpus = {str(j): list(e["ranks"]) for j, e in enumerate(resp_plan)}
+    return decodes_alone(gpus, str(idx[0]), [str(j) for j in range(len(resp_plan)) if j not in idx])
+
+
 def config_name(args, world: int, resp, judge) -> str:
     """Which BASELINE.json config this run is, and how a variant differs from its wording."""
     if args.config != "fanout":
@@ -560,6 +570,7 @@ def main() -> None:
         else:
             dist.init_process_group(backend)
 
+    from llm_consensus_amd import ops
     from llm_consensus_amd.consensus import build_judge_prompt, prompt_header
     from llm_consensus_amd.engine import Engine, EngineConfig, SamplingParams
     from llm_consensus_amd.models.config import FAMILIES
@@ -628,7 +639,9 @@ def main() -> None:
             tp_members.append((name, e["ranks"], tp))
         eng = Engine(cfg, EngineConfig(device=dev, max_context=ctx, seed=e["seed"], steps_per_graph=args.steps_per_graph,
                                        use_graphs=graphs, max_batch=len(idx),
-                                       fused_ar=not colocated_tp(resp_plan, idx)), tp=tp, name=name)
+                                       fused_ar=not colocated_tp(resp_plan, idx),
+                                       attn_oproj_min_chunk=ops.attn_oproj_min_chunk(responder_alone(resp_plan, idx))),
+                     tp=tp, name=name)
         responders.append((idx, eng, ids, tok))
     jtp_grp = tp_group(judge_plan["ranks"])
     if len(judge_plan["ranks"]) > 1:
@@ -643,7 +656,8 @@ def main() -> None:
         graphs = not args.no_graphs and (jtp_grp.size == 1 or jtp_grp.custom is not None
                                          or (not on_cpu and jtp_grp.graph_capture_ok(dev)))
         judge = Engine(jcfg, EngineConfig(device=dev, max_context=judge_ctx, seed=judge_plan["seed"],
-                                          steps_per_graph=args.steps_per_graph, use_graphs=graphs),
+                                          steps_per_graph=args.steps_per_graph, use_graphs=graphs,
+                                          attn_oproj_min_chunk=ops.attn_oproj_min_chunk(True)),
                        tp=jtp_grp, name=judge_plan["name"])
     # capture every decode graph up front (a capture beside another engine's running stream is
     # invalid; the worker process does the same before serving)

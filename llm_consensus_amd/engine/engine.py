@@ -67,8 +67,7 @@ class EngineConfig:
     # Tensor-parallel ranks never take it (their 1-2 kv heads make the merge the long pole and the
     # o_proj it would hide is small: profiles/r3_attn_oproj.md)
     attn_oproj: bool = dataclasses.field(default_factory=lambda: os.environ.get("LLMC_ATTN_OPROJ", "1") != "0")
-    attn_oproj_min_chunk: int = dataclasses.field(
-        default_factory=lambda: 32 if os.environ.get("LLMC_ATTN_OPROJ") == "all" else ops.ATTN_OPROJ_MIN_CHUNK)
+    attn_oproj_min_chunk: int = dataclasses.field(default_factory=ops.attn_oproj_min_chunk)
     # one-row engines: the qkv projection and the decode attention as ONE launch in the buckets of
     # the fused attention form (csrc/kernels/qkv_attn.hip). "1": shards whose qkv output is under
     # QKV_ATTN_MAX_ROWS rows (the TP ranks', where it measured faster: profiles/r4_qkv_attn.md);

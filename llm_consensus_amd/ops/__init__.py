@@ -290,6 +290,17 @@ ATTN_OPROJ_MODE = int(os.environ.get("LLMC_ATTN_OPROJ_MODE", "7"))
 ATTN_OPROJ_MIN_CHUNK = 256
 
 
+def attn_oproj_min_chunk(alone: bool = False) -> int:
+    """Smallest keys-per-block bucket a one-row engine runs as the fused attention + o_proj launch:
+    every bucket (32) for an engine that decodes alone on its GPU (8B at 2k-5k keys: 2.84 -> 2.79,
+    2.92 -> 2.85 ms/token, profiles/r5_decode_experiments.md), ATTN_OPROJ_MIN_CHUNK beside
+    co-located engines (whose blocks then wait on the head merge while another engine's kernels
+    want the CUs). LLMC_ATTN_OPROJ=all forces every bucket."""
+    if os.environ.get("LLMC_ATTN_OPROJ") == "all" or alone:
+        return 32
+    return ATTN_OPROJ_MIN_CHUNK
+
+
 def attn_oproj_grid(H: int, nh: int, nkv: int, D: int) -> int:
     """Blocks per kv head of the fused attention + o_proj launch (``attn_oproj``) for this shape,
     or 0 when the kernel library does not cover it: ~one block per CU over the kv heads (256 /

@@ -45,33 +45,46 @@ class PlacementError(Exception):
     pass
 
 
+def decodes_alone(gpus: Dict[str, List[int]], name: str, concurrent: Sequence[str]) -> bool:
+    """Does engine ``name`` decode with none of its GPUs shared by an engine that decodes at the
+    same time (``concurrent``)? Such an engine's latency-bound kernels have the chip to
+    themselves (no other stream fills their ramps), which changes which launch forms pay."""
+    mine = set(gpus[name])
+    return not any(mine & set(gpus[o]) for o in concurrent if o != name and o in gpus)
+
+
 def fused_ar_allowed(gpus: Dict[str, List[int]], name: str, concurrent: Sequence[str]) -> bool:
     """May tensor-parallel engine ``name`` run its row-parallel decode all-reduce inside the GEMV
     epilogue (``EngineConfig.fused_ar``)? Not when an engine that decodes at the same time
     (``concurrent``) shares one of its GPUs: the fused launch's ~256 blocks per GPU spin on the peer
     GPUs while holding CUs, and a co-located engine's blocks queued behind them delay the very
     peers they wait for. Single-GPU engines have no all-reduce (True)."""
-    mine = set(gpus[name])
-    if len(mine) <= 1:
+    if len(gpus[name]) <= 1:
         return True
-    return not any(mine & set(gpus[o]) for o in concurrent if o != name and o in gpus)
+    return decodes_alone(gpus, name, concurrent)
+
+
+def _concurrent(gpus: Dict[str, List[int]], m: str, judge: Optional[str], concurrency: int) -> List[str]:
+    """The engines that decode while ``m`` does in a consensus run: the responders decode
+    together; the judge decodes after the last response (runner.go:118 then judge.go:96), so with
+    one request in flight it overlaps nothing — with several (the server) one request's judge
+    overlaps the next one's responders."""
+    if concurrency > 1:
+        return [o for o in gpus if o != m]
+    if m == judge:
+        return []
+    return [o for o in gpus if o not in (m, judge)]
 
 
 def fused_ar_plan(gpus: Dict[str, List[int]], judge: Optional[str], concurrency: int = 1) -> Dict[str, bool]:
-    """``fused_ar_allowed`` for every placed engine of a consensus run: the responders decode
-    together; the judge decodes after the last response (runner.go:118 then judge.go:96), so with
-    one request in flight it shares its GPUs with nothing that runs at the same time — with several
-    (the server) one request's judge overlaps the next one's responders."""
-    out = {}
-    for m in gpus:
-        if concurrency > 1:
-            conc = [o for o in gpus if o != m]
-        elif m == judge:
-            conc = []
-        else:
-            conc = [o for o in gpus if o not in (m, judge)]
-        out[m] = fused_ar_allowed(gpus, m, conc)
-    return out
+    """``fused_ar_allowed`` for every placed engine of a consensus run (``_concurrent``)."""
+    return {m: fused_ar_allowed(gpus, m, _concurrent(gpus, m, judge, concurrency)) for m in gpus}
+
+
+def alone_plan(gpus: Dict[str, List[int]], judge: Optional[str], concurrency: int = 1) -> Dict[str, bool]:
+    """``decodes_alone`` for every placed engine of a consensus run (``_concurrent``): the engines
+    that take the lone-engine launch forms (``EngineConfig.attn_oproj_min_chunk``)."""
+    return {m: decodes_alone(gpus, m, _concurrent(gpus, m, judge, concurrency)) for m in gpus}
 
 
 def parse_pins(spec: str) -> Dict[str, List[int]]:

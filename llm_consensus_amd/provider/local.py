@@ -28,8 +28,8 @@ from typing import Dict, List, Optional
 
 from ..catalog import PROVIDER_LOCAL, ModelSpec
 from ..context import Context, ContextError
-from ..parallel.placement import (HBM_BYTES, USABLE_FRACTION, ModelDemand, default_gpus, describe, fused_ar_plan,
-                                  solve)
+from ..parallel.placement import (HBM_BYTES, USABLE_FRACTION, ModelDemand, alone_plan, default_gpus, describe,
+                                  fused_ar_plan, solve)
 from ..utils import trace as tracing
 from ..utils.tokenizer import tokenizer_for
 from .base import Request, Response, StreamCallback
@@ -204,6 +204,7 @@ class LocalBackend:
         kv_blocks = kv_pool_blocks(self.placement, self.specs, self._ctx,
                                    {m: max(1, n) + sess for m, (n, sess) in seqs.items()})
         fused = fused_ar_plan(self.placement.gpus, judge, conc)
+        alone = alone_plan(self.placement.gpus, judge, conc)
         for g in used:
             models = []
             for m, gs in self.placement.gpus.items():
@@ -218,7 +219,10 @@ class LocalBackend:
                                    "max_seqs": max(1, n) + sess,
                                    # TP: the all-reduce in the row-parallel GEMVs' epilogue unless
                                    # an engine decoding at the same time shares its GPUs
-                                   "fused_ar": fused[m]})
+                                   "fused_ar": fused[m],
+                                   # no other engine decodes on its GPUs meanwhile: the lone-engine
+                                   # launch forms (ops.attn_oproj_min_chunk)
+                                   "alone": alone[m]})
             if groups:
                 dist_info = {"port": port, "rank": rank_of[g], "world": len(used),
                              "groups": [(m, [rank_of[x] for x in gs]) for m, gs in groups]}

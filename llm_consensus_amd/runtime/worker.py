@@ -404,6 +404,7 @@ def worker_main(gpu: int, conn, models: List[dict], dist_info: Optional[dict], t
             import torch
 
             from ..context import Context
+            from .. import ops
             from ..engine import Engine, EngineConfig
             from ..models.config import FAMILIES
             from ..parallel.comm import TPGroup
@@ -454,6 +455,8 @@ def worker_main(gpu: int, conn, models: List[dict], dist_info: Optional[dict], t
                                 # the placement's rule (placement.fused_ar_plan): no fused
                                 # all-reduce beside an engine that decodes at the same time
                                 fused_ar=bool(m.get("fused_ar", True)),
+                                # placement.alone_plan: the lone-engine fused attention + o_proj
+                                attn_oproj_min_chunk=ops.attn_oproj_min_chunk(bool(m.get("alone", False))),
                                 # MoE under TP: whole experts per rank (LLMC_EXPERT_PARALLEL=1)
                                 expert_parallel=os.environ.get("LLMC_EXPERT_PARALLEL", "0") == "1")
             with trace.span("engine_init", cat="startup", engine=m["name"]):

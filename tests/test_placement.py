@@ -200,3 +200,32 @@ def test_fused_allreduce_rule_follows_the_placement():
     plan2 = [{"ranks": [0]}, {"ranks": [1]}, {"ranks": [0, 1]}]
     assert bench.colocated_tp(plan2, [2]) is True and bench.colocated_tp(plan2, [0]) is False
     assert bench.colocated_tp([{"ranks": [0, 1]}, {"ranks": [2]}], [0]) is False
+
+
+def test_lone_engine_rule_follows_the_placement():
+    """Engines that decode with no other engine on their GPUs take the lone-engine launch forms
+    (the fused attention + o_proj in every context bucket, ops.attn_oproj_min_chunk); co-located
+    responders keep the default. bench.py's responder_alone applies the same rule."""
+    import importlib.util
+    import os
+
+    from llm_consensus_amd import ops
+    from llm_consensus_amd.parallel.placement import alone_plan, decodes_alone
+
+    one_gpu = {"r0": [0], "r1": [0], "r2": [0], "judge": [0]}  # BASELINE config 2 on one GPU
+    plan = alone_plan(one_gpu, "judge")
+    assert plan == {"r0": False, "r1": False, "r2": False, "judge": True}
+    assert alone_plan(one_gpu, "judge", concurrency=2)["judge"] is False  # server: overlaps
+    eight = {f"r{i}": [i] for i in range(8)}
+    eight["judge"] = list(range(8))  # config 3 at N=8: one responder per GPU, TP=8 judge
+    plan8 = alone_plan(eight, "judge")
+    assert all(plan8[f"r{i}"] for i in range(8)) and plan8["judge"]
+    assert decodes_alone({"a": [0, 1], "b": [1]}, "a", ["b"]) is False
+    assert ops.attn_oproj_min_chunk(True) == 32
+    if os.environ.get("LLMC_ATTN_OPROJ") != "all":
+        assert ops.attn_oproj_min_chunk(False) == ops.ATTN_OPROJ_MIN_CHUNK
+    spec = importlib.util.spec_from_file_location("bench_mod", os.path.join(os.path.dirname(__file__), "..", "bench.py"))
+    bench = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(bench)
+    assert bench.responder_alone([{"ranks": [0]}, {"ranks": [0]}, {"ranks": [0]}], [0]) is False
+    assert bench.responder_alone([{"ranks": [0]}, {"ranks": [1]}, {"ranks": [2]}], [1]) is True

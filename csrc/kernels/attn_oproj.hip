@@ -205,20 +205,30 @@ __global__ __launch_bounds__(kAoThreads) void attn_oproj_kernel(
   const __amdgpu_buffer_rsrc_t hr = __builtin_amdgcn_make_buffer_rsrc(hoff, 0, Q * 16, 0x00020000);
   if (*flag) {
     f32x4 ms, acc;
-    // (16 rows in flight per thread would merge 32 partials in one pass, but spills the 32-row
-    // o waves' registers: measured slower)
-    merge_rows<G, D, 256>(rsrc, reinterpret_cast<const char*>(slab), 0, nsplit, tag_h,
-                              reinterpret_cast<f32x4*>(smem), o_wave ? 256 + tid : ct, ms, acc, fault);
-    if (!o_wave && ct < Q) {
+    // A deferring merger's o waves hold no weights yet: all 8 waves merge, so 32 partials are one
+    // pass of 8 loads in flight per thread (one round trip on the critical path instead of two;
+    // 16 rows per thread would spill the o waves' weight registers of the other blocks). Merge
+    // thread mt < Q ends with output unit mt (dims 4 mt .. 4 mt + 3).
+    int mt;
+    if (merger_defers) {
+      mt = tid;
+      merge_rows<G, D, kAoThreads>(rsrc, reinterpret_cast<const char*>(slab), 0, nsplit, tag_h,
+                                   reinterpret_cast<f32x4*>(smem), tid, ms, acc, fault);
+    } else {
+      mt = o_wave ? 256 + tid : ct;
+      merge_rows<G, D, 256>(rsrc, reinterpret_cast<const char*>(slab), 0, nsplit, tag_h,
+                            reinterpret_cast<f32x4*>(smem), mt, ms, acc, fault);
+    }
+    if (mt < Q) {
       const float inv = 1.f / ms[1];
       const uint32_t lo = pack_bf16x2(acc[0] * inv, acc[1] * inv), hi = pack_bf16x2(acc[2] * inv, acc[3] * inv);
-      __builtin_amdgcn_raw_buffer_store_b128(u32x4{lo, tag_h, hi, tag_h}, hr, ct * 16, 0, 16);
-      const int gq = ct / HQ, u = ct % HQ;
+      __builtin_amdgcn_raw_buffer_store_b128(u32x4{lo, tag_h, hi, tag_h}, hr, mt * 16, 0, 16);
+      const int gq = mt / HQ, u = mt % HQ;
       *reinterpret_cast<u32x2*>(attn_out + (g * G + gq) * D + 4 * u) = u32x2{lo, hi};
-      if (merger_defers) {  // its own copy straight into LDS (units ct = dims 4 ct .. 4 ct + 3)
+      if (merger_defers) {  // its own copy straight into LDS (units mt = dims 4 mt .. 4 mt + 3)
         uint32_t* xg = reinterpret_cast<uint32_t*>(xs + (FR ? g * 64 : 0));
-        xg[2 * ct] = lo;
-        xg[2 * ct + 1] = hi;
+        xg[2 * mt] = lo;
+        xg[2 * mt + 1] = hi;
       }
     }
     if (ct == 0) {

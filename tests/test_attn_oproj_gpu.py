@@ -43,7 +43,8 @@ def _reference(kc, vc, bt, sl, q, w_o, h, nh, nkv, D, bs, scale):
 
 @pytest.mark.parametrize("nh,nkv,D,H", [(32, 8, 128, 4096), (8, 2, 128, 1024), (16, 2, 64, 4096)])
 @pytest.mark.parametrize("L,cap", [(1, 1024), (31, 1024), (33, 1024), (100, 2048), (1000, 1024), (2048, 2048),
-                                   (2100, 4096), (4096, 4096), (7999, 8192), (9000, 16384), (13000, 13300),
+                                   (2100, 4096), (4096, 4096), (5000, 6144), (7999, 8192), (9000, 12288),
+                                   (9000, 16384), (13000, 13300),
                                    (16384, 16384)])
 def test_attn_oproj_vs_oracle_and_two_launches(cuda, nh, nkv, D, H, L, cap):
     bs = 64
@@ -78,16 +79,27 @@ def test_attn_oproj_vs_oracle_and_two_launches(cuda, nh, nkv, D, H, L, cap):
         assert err_h < 2e-2 * max(1.0, h_ref.abs().max().item()), (it, err_h)
         err_2 = (h.float() - h2.float()).abs().max().item()
         assert err_2 < 2e-2 * max(1.0, h_ref.abs().max().item()), (it, err_2)
-    # the late-weight variants (the merger's own weights after the merge, or not) are the same sums
+    # the late-weight variants: each deterministic launch to launch; the merger that defers its
+    # weights (3) merges over all 8 waves (four row groups instead of two: another summation
+    # order), so 1 and 3 agree to bf16 rounding
     outs = []
-    for mode in (1, 3, 1):
+    for mode in (1, 3, 1, 3):
         hm = h0.clone()
         am = torch.zeros(1, nh * D, dtype=BF, device="cuda")
         ops.attn_oproj(q, kc, vc, btd, sld, w_o, hm, am, ws, nh, nkv, D, bs, chunk, nc, scale, fault=fault, mode=mode)
         outs.append((hm, am))
     torch.cuda.synchronize()
     assert int(fault.item()) == 0
-    assert all(torch.equal(outs[0][0], o[0]) and torch.equal(outs[0][1], o[1]) for o in outs[1:])
+
+    def same(a, b):
+        return torch.equal(a[0], b[0]) and torch.equal(a[1], b[1])
+
+    def close_runs(a, b):
+        tol = 2e-2 * max(1.0, h_ref.abs().max().item())
+        return (a[0].float() - b[0].float()).abs().max().item() < tol and \
+            (a[1].float() - b[1].float()).abs().max().item() < 2e-2
+
+    assert same(outs[0], outs[2]) and same(outs[1], outs[3]) and close_runs(outs[0], outs[1])
     outs_c = outs
     if nkv == 8 and nh // nkv == 4 and D == 128 and H // nc == 128:
         # whole o_proj rows per block (mode bit 2): no tile partials; with and without the merger
@@ -103,18 +115,19 @@ def test_attn_oproj_vs_oracle_and_two_launches(cuda, nh, nkv, D, H, L, cap):
             outs.append((hm, am))
         torch.cuda.synchronize()
         assert int(fault.item()) == 0
-        assert all(torch.equal(outs[0][0], o[0]) and torch.equal(outs[0][1], o[1]) for o in outs[1:])
+        assert same(outs[0], outs[2]) and same(outs[1], outs[3]) and close_runs(outs[0], outs[1])
         assert torch.equal(outs[0][1], outs_c[0][1])  # the attention itself is the same launch's
+        assert torch.equal(outs[1][1], outs_c[1][1])
         err_fr = (outs[0][0].float().cpu() - h_ref).abs().max().item()
         assert err_fr < 2e-2 * max(1.0, h_ref.abs().max().item()), err_fr
     _, _, tile_part, counters = ws
     c = counters.view(-1, 16).cpu()
     # head tickets and tile tickets re-armed, the exit counter re-armed; the head epoch advanced by
-    # all 6 launches, the tile epoch by those with tile partials (not the default's whole rows)
+    # all 7 launches, the tile epoch by those with tile partials (not the default's whole rows)
     whole_rows = bool(ops.ATTN_OPROJ_MODE & 4) and nkv == 8 and nh // nkv == 4 and D == 128 and H // nc == 128
     assert int(c[: nkv + nc, 0].abs().sum()) == 0 and int(c[nkv + nc, 0]) == 0, c[:, :2]
-    assert torch.equal(c[:nkv, 1], torch.full((nkv,), 6, dtype=torch.int32))
-    assert int(c[nkv + nc, 1]) == (3 if whole_rows else 6)
+    assert torch.equal(c[:nkv, 1], torch.full((nkv,), 7, dtype=torch.int32))
+    assert int(c[nkv + nc, 1]) == (4 if whole_rows else 7)
 
 
 def test_attn_oproj_shape_gates(cuda):

@@ -372,7 +372,8 @@ def bench_attn_prefill(cases=((32, 8, 2048, 2048), (32, 8, 8192, 8192), (32, 8, 
         # one throwaway timing first: the first measurement of a shape ran ~7 % slow (clock ramp)
         timeit(lambda: ops.attn_prefill(q, kc, vc, bt, qs, ql, cl, out, T, nh, nkv, D, bs, 1 / math.sqrt(D),
                                         max_ctx=ctx, ksplit=1, ws=ws), iters=3)
-        for k, km in dict.fromkeys([plan, (1, 1), (2, 8), (2, 16), (4, 4), (4, 8), (4, 16)]):
+        extra = [tuple(int(x) for x in c.split(",")) for c in os.environ.get("PF_SPLITS", "").split(";") if c]
+        for k, km in dict.fromkeys([plan, (1, 1), (2, 8), (2, 16), (4, 4), (4, 8), (4, 16)] + extra):
             us = timeit(lambda: ops.attn_prefill(q, kc, vc, bt, qs, ql, cl, out, T, nh, nkv, D, bs, 1 / math.sqrt(D),
                                                  max_ctx=ctx, ksplit=k, kmin=km, ws=ws), iters=3)
             tag = "plan" if (k, km) == plan else ""

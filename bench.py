@@ -224,6 +224,10 @@ def responder_alone(resp_plan, idx) -> bool:
     launch forms (ops.attn_oproj_min_chunk). The judge decodes after the responders: always alone."""
     from llm_consensus_amd.parallel.placement import decodes_alone
 
+    if os.environ.get("LLMC_BENCH_SAME_GPU") == "1":
+        # rehearsal: every rank's engine is on cuda:0, so no responder has its GPU to itself (the
+        # fused attention + o_proj launch's waiting blocks would hold CUs the others need)
+        return False
     gpus = {str(j): list(e["ranks"]) for j, e in enumerate(resp_plan)}
     return decodes_alone(gpus, str(idx[0]), [str(j) for j in range(len(resp_plan)) if j not in idx])
 

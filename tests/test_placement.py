@@ -229,3 +229,9 @@ def test_lone_engine_rule_follows_the_placement():
     spec.loader.exec_module(bench)
     assert bench.responder_alone([{"ranks": [0]}, {"ranks": [0]}, {"ranks": [0]}], [0]) is False
     assert bench.responder_alone([{"ranks": [0]}, {"ranks": [1]}, {"ranks": [2]}], [1]) is True
+    # the one-GPU rehearsal puts every rank on cuda:0: nobody is alone there
+    os.environ["LLMC_BENCH_SAME_GPU"] = "1"
+    try:
+        assert bench.responder_alone([{"ranks": [0]}, {"ranks": [1]}, {"ranks": [2]}], [1]) is False
+    finally:
+        del os.environ["LLMC_BENCH_SAME_GPU"]

@@ -364,7 +364,7 @@ int llmc_car_host_get(const void* host, int word) {
 void llmc_car_host_set(void* host, int word, int v) {
   static_cast<volatile uint32_t*>(host)[word] = static_cast<uint32_t>(v);
 }
-int llmc_car_host_word(int which) { return which == 0 ? kHostAbort : kHostTimedOut; }
+int llmc_car_host_word(int which) { return which == 0 ? kHostAbort : which == 1 ? kHostTimedOut : kHostSpinTicks; }
 
 size_t llmc_car_oneshot_max(size_t cap) { return car_oneshot_max(cap); }
 

@@ -48,7 +48,9 @@ constexpr unsigned kCarCheckPolls = 64;
 //                   next check instead of polling to the limit;
 //   [kHostTimedOut] a spin of this rank gave up or returned without its data: the host reads it
 //                   with a plain load, no GPU call (the stream may still be busy).
-constexpr int kHostAbort = 0, kHostTimedOut = 16, kHostWords = 64;
+//   [kHostSpinTicks] the spin bound in ticks when non-zero (LLMC_CAR_SPIN_S: ranks time-sharing one
+//                    GPU without CU partitions can be starved for longer than kCarSpinTicks)
+constexpr int kHostAbort = 0, kHostTimedOut = 16, kHostSpinTicks = 32, kHostWords = 64;
 // fused-all-reduce buffer (gemv_core.h EPI_AR): block b of a launch owns granules [16 b, 16 b + 16)
 // of every slot and epoch ctr[b]
 constexpr int kArGranulesPerBlock = 16;
@@ -110,9 +112,14 @@ __device__ __forceinline__ bool car_spin(const CarPeers& P, int rank, int world,
   if (polls == 0) t0 = __builtin_amdgcn_s_memrealtime();
   ++polls;
   if (polls % kCarCheckPolls == 0) {
-    bool stop = __builtin_amdgcn_s_memrealtime() - t0 > kCarSpinTicks;
-    if (!stop && P.host != nullptr)
+    uint64_t bound = kCarSpinTicks;
+    bool stop = false;
+    if (P.host != nullptr) {
+      const uint32_t b = __hip_atomic_load(P.host + kHostSpinTicks, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      if (b != 0) bound = b;
       stop = __hip_atomic_load(P.host + kHostAbort, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != 0;
+    }
+    stop = stop || __builtin_amdgcn_s_memrealtime() - t0 > bound;
     if (stop) {
       car_give_up(P, rank, world);
       return false;

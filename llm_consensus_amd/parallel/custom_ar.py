@@ -21,6 +21,7 @@ devices, IPC failure) or whose self-test sum is wrong makes EVERY rank fall back
 from __future__ import annotations
 
 import contextlib
+import os
 from typing import List, Optional
 
 import torch
@@ -75,6 +76,9 @@ class CustomAllReduce:
                     self.own = k.car_alloc(self.cap)
                     if self.device.type == "cuda":
                         self.host, self.host_dev = k.car_host_alloc()
+                        spin_s = float(os.environ.get("LLMC_CAR_SPIN_S", "0") or 0)
+                        if spin_s > 0:  # the spin bound (car_proto.h kHostSpinTicks; default 1 s)
+                            k.car_host_set(self.host, k.car_host_word(2), int(min(max(spin_s, 0.01), 42.0) * 1e8))
                     if self.device.type == "cuda":
                         dev_index = self.device.index if self.device.index is not None else torch.cuda.current_device()
                     else:

@@ -577,7 +577,7 @@ def main() -> None:
     if os.environ.get("LLMC_BENCH_SAME_GPU") == "1":
         # ranks time-sharing one GPU without CU partitions: a peer's collective can wait well past
         # the 1-s spin bound meant for ranks that own their GPUs (car_proto.h kHostSpinTicks)
-        os.environ.setdefault("LLMC_CAR_SPIN_S", "30")
+        os.environ.setdefault("LLMC_CAR_SPIN_S", "20")
     from llm_consensus_amd import ops
     from llm_consensus_amd.consensus import build_judge_prompt, prompt_header
     from llm_consensus_amd.engine import Engine, EngineConfig, SamplingParams

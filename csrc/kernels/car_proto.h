@@ -48,8 +48,8 @@ constexpr unsigned kCarCheckPolls = 64;
 //                   next check instead of polling to the limit;
 //   [kHostTimedOut] a spin of this rank gave up or returned without its data: the host reads it
 //                   with a plain load, no GPU call (the stream may still be busy).
-//   [kHostSpinTicks] the spin bound in ticks when non-zero (LLMC_CAR_SPIN_S: ranks time-sharing one
-//                    GPU without CU partitions can be starved for longer than kCarSpinTicks)
+//   [kHostSpinTicks] the spin bound in ticks when non-zero (LLMC_CAR_SPIN_S, <= 21 s: ranks
+//                    time-sharing one GPU without CU partitions can be starved past kCarSpinTicks)
 constexpr int kHostAbort = 0, kHostTimedOut = 16, kHostSpinTicks = 32, kHostWords = 64;
 // fused-all-reduce buffer (gemv_core.h EPI_AR): block b of a launch owns granules [16 b, 16 b + 16)
 // of every slot and epoch ctr[b]

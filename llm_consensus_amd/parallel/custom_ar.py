@@ -78,7 +78,8 @@ class CustomAllReduce:
                         self.host, self.host_dev = k.car_host_alloc()
                         spin_s = float(os.environ.get("LLMC_CAR_SPIN_S", "0") or 0)
                         if spin_s > 0:  # the spin bound (car_proto.h kHostSpinTicks; default 1 s)
-                            k.car_host_set(self.host, k.car_host_word(2), int(min(max(spin_s, 0.01), 42.0) * 1e8))
+                            # ticks of the 100-MHz clock in a 32-bit word the binding takes as int: <= 21 s
+                            k.car_host_set(self.host, k.car_host_word(2), int(min(max(spin_s, 0.01), 21.0) * 1e8))
                     if self.device.type == "cuda":
                         dev_index = self.device.index if self.device.index is not None else torch.cuda.current_device()
                     else:

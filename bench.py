@@ -578,6 +578,15 @@ def main() -> None:
         # ranks time-sharing one GPU without CU partitions: a peer's collective can wait well past
         # the 1-s spin bound meant for ranks that own their GPUs (car_proto.h kHostSpinTicks)
         os.environ.setdefault("LLMC_CAR_SPIN_S", "20")
+        # ... and a TP replay of 8 decode steps over eight time-shared ranks takes ~6 s (round 4:
+        # 11 ms per all-reduce): beyond the 5-s host deadline that fails a stalled replay
+        os.environ.setdefault("LLMC_TP_STALL_S", "300")
+        if os.environ.get("LLMC_BENCH_CU_SPLIT") == "1" and world > 1:
+            # every rank's engines on a CU slice of their own, as on their own GPU: with eight ranks
+            # time-sharing every CU, the spinning collectives of the ranks that have arrived hold the
+            # CUs the last rank's kernels need (the custom all-reduce then times out)
+            per = 256 // world
+            os.environ.setdefault("LLMC_CU_MASK", f"{local * per}-{(local + 1) * per - 1}")
     from llm_consensus_amd import ops
     from llm_consensus_amd.consensus import build_judge_prompt, prompt_header
     from llm_consensus_amd.engine import Engine, EngineConfig, SamplingParams

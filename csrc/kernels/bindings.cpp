@@ -26,6 +26,9 @@ int llmc_moe_gemvm(int, const void*, int, const void*, float, const void*, const
                    int, hipStream_t);
 int llmc_gemm(const void*, int, const void*, int, void*, int, int, int, int, int, hipStream_t);
 int llmc_gemm_t128(const void*, int, const void*, int, void*, int, int, int, int, int, hipStream_t);
+int llmc_gemm_narrow(const void*, int, const void*, int, void*, int, int, int, int, int, hipStream_t);
+int llmc_gemm_kind(const void*, int, const void*, int, void*, int, int, int, int, int, int, hipStream_t);
+int llmc_gemm_plan(int, int);
 int llmc_rope_kv_write(const void*, int, void*, int, const void*, const void*, const void*, void*, void*, const void*,
                        int, int, int, int, int, hipStream_t);
 int llmc_attn_decode_groups(int);
@@ -124,6 +127,13 @@ PYBIND11_MODULE(_llmc_hip, m) {
   });
   m.def("gemm_t128", [](ptr A, int lda, ptr W, int ldw, ptr C, int ldc, int M, int N, int K, int epi, ptr s) {
     check(llmc_gemm_t128(P(A), lda, P(W), ldw, P(C), ldc, M, N, K, epi, S(s)), "gemm_t128");
+  });
+  m.def("gemm_kind", [](ptr A, int lda, ptr W, int ldw, ptr C, int ldc, int M, int N, int K, int epi, int kind, ptr s) {
+    check(llmc_gemm_kind(P(A), lda, P(W), ldw, P(C), ldc, M, N, K, epi, kind, S(s)), "gemm_kind");
+  });
+  m.def("gemm_plan", [](int M, int N) { return llmc_gemm_plan(M, N); });
+  m.def("gemm_narrow", [](ptr A, int lda, ptr W, int ldw, ptr C, int ldc, int M, int N, int K, int epi, ptr s) {
+    check(llmc_gemm_narrow(P(A), lda, P(W), ldw, P(C), ldc, M, N, K, epi, S(s)), "gemm_narrow");
   });
   m.def("rope_kv_write", [](ptr qkv, int qs, ptr qo, int qos, ptr pos, ptr cos_t, ptr sin_t, ptr kc, ptr vc,
                             ptr slots, int T, int nh, int nkv, int D, int bs, ptr s) {

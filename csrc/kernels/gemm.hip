@@ -478,14 +478,180 @@ __global__ __launch_bounds__(512, 1) void gemm256_kernel(const bf16_t* __restric
   }
 }
 
+// ---------------------------------------------------------------------------------------------
+// Narrow-N prefill GEMM: 128 x (32 NI) tiles (NI = 6: 128 x 192) for the outputs whose 256 x 256
+// grid cannot fill the chip — a Llama-3-8B TP=8 rank's qkv (N = 768) has 96 such tiles for 256 CUs
+// (0.62 PF/s) but 256 tiles of 128 x 192 at M = 8192, one per CU.
+//  * 256 threads = 4 waves (2 M x 2 N), one per SIMD, one block per CU; a wave owns 64 x (16 NI) of
+//    the tile = 4 x NI tiles of mfma_f32_16x16x32_bf16 with the operands swapped (W fragment as A:
+//    D[n][m], so the epilogue stores 4 consecutive columns per lane, as gemm256_kernel's).
+//  * LDS = 4 slots of one K-step (64) each (160 KiB): A 128 rows + W 32 NI rows, 128-B rows with
+//    the chunk ^ ((row >> 1) & 7) swizzle on the LDS-DMA source offset and on the ds_read_b128
+//    address (conflict-free, as gemm256_kernel's). Stage t + 4 is fetched into the slot of step t
+//    right after the barrier that retires step t's reads: three K-steps to land (3 slots measured
+//    the same: 53.6 vs 53.5 us at M = 8192, N = 768, so the fetch latency is covered).
+//  * each K-step is two halves of 32 K; the second half's fragments are read while the first
+//    half's 4 NI MFMAs run, the next step's first half while the second half's run, so the one
+//    barrier per K-step sits between two MFMA clusters and no LDS read latency is exposed
+//    (one wave per SIMD: MI355X_MICROARCH.md §LDS, keep reads in flight across MFMAs).
+//  * LDS reads per K-step: 4 waves x (64 + 16 NI) rows x 128 B = 80 KiB (NI = 6) = 320 cycles at
+//    256 B/clk against 768 MFMA cycles per SIMD.
+template <int EPI, int NI>
+__global__ __launch_bounds__(256, 1) void gemm_narrow_kernel(const bf16_t* __restrict__ A, int lda,
+                                                             const bf16_t* __restrict__ W, int ldw,
+                                                             void* __restrict__ C, int ldc, int M, int N, int K) {
+  constexpr int TM = 128, TN = 32 * NI, WN = 16 * NI, NS = 4;
+  constexpr int kAB = TM * kTK * 2, kWB = TN * kTK * 2, kSlot = kAB + kWB;
+  constexpr int LA = kAB / 4096, LI = LA + kWB / 4096;  // LDS-DMA instructions per lane per K-step
+  static_assert(kWB % 4096 == 0 && NS * kSlot <= 160 * 1024 && LI <= 10, "narrow GEMM tile");
+  __shared__ __attribute__((aligned(16))) char smem[NS * kSlot];
+  const int num_m = (M + TM - 1) / TM, num_n = (N + TN - 1) / TN;
+  // XCD remap (T1) with N fastest: the N tiles of one A row panel are consecutive ids on one XCD
+  const int id = xcd_remap(blockIdx.x, num_m * num_n);
+  const int m0 = (id / num_n) * TM, n0 = (id % num_n) * TN;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wr = wave >> 1, wc = wave & 1;
+  const int l16 = lane & 15, lg = lane >> 4;
+  const int rowsA = min(TM, M - m0), rowsW = min(TN, N - n0);
+  const __amdgpu_buffer_rsrc_t rsA =
+      __builtin_amdgcn_make_buffer_rsrc((void*)(A + static_cast<int64_t>(m0) * lda), 0, rowsA * lda * 2, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rsW =
+      __builtin_amdgcn_make_buffer_rsrc((void*)(W + static_cast<int64_t>(n0) * ldw), 0, rowsW * ldw * 2, 0x00020000);
+  uint32_t voff[10];  // fixed size: a template-dependent operand type on the buffer builtin drops the host stub
+#pragma unroll
+  for (int i = 0; i < LI; ++i) {
+    const int s = (i < LA ? i : i - LA) * 256 + tid;
+    const int r = s >> 3, c = (s & 7) ^ ((r >> 1) & 7);
+    voff[i] = i < LA ? static_cast<uint32_t>((min(r, rowsA - 1) * lda + c * 8) * 2)
+                     : static_cast<uint32_t>((min(r, rowsW - 1) * ldw + c * 8) * 2);
+  }
+  // stage(n, slot): K-step n into the slot at byte offset `slot`
+  auto stage = [&](int n, int slot) {
+    char* q = smem + slot + wave * 1024;
+    const int kbytes = n * kTK * 2;
+#pragma unroll
+    for (int i = 0; i < LI; ++i)
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(i < LA ? rsA : rsW, (__attribute__((address_space(3))) void*)(q + i * 4096),
+                                               16, voff[i], kbytes, 0, 0);
+  };
+  // per-lane read offsets: rows 16 apart share the swizzle, so one base per half (kk) and operand
+  const int offA[2] = {(wr * 64 + l16) * 128 + (((0 + lg) ^ ((l16 >> 1) & 7)) << 4),
+                       (wr * 64 + l16) * 128 + (((4 + lg) ^ ((l16 >> 1) & 7)) << 4)};
+  const int offW[2] = {kAB + (wc * WN + l16) * 128 + (((0 + lg) ^ ((l16 >> 1) & 7)) << 4),
+                       kAB + (wc * WN + l16) * 128 + (((4 + lg) ^ ((l16 >> 1) & 7)) << 4)};
+  auto read_half = [&](int slot, int kk, bf16x8(&af)[4], bf16x8(&bw)[NI]) {
+    const char* qa = smem + slot + offA[kk];
+    const char* qw = smem + slot + offW[kk];
+#pragma unroll
+    for (int mi = 0; mi < 4; ++mi) af[mi] = *reinterpret_cast<const bf16x8*>(qa + mi * 2048);
+#pragma unroll
+    for (int ni = 0; ni < NI; ++ni) bw[ni] = *reinterpret_cast<const bf16x8*>(qw + ni * 2048);
+  };
+  f32x4 acc[4][NI];
+#pragma unroll
+  for (int a = 0; a < 4; ++a)
+#pragma unroll
+    for (int b = 0; b < NI; ++b) acc[a][b] = f32x4{0.f, 0.f, 0.f, 0.f};
+  auto mma = [&](const bf16x8(&af)[4], const bf16x8(&bw)[NI]) {
+#pragma unroll
+    for (int mi = 0; mi < 4; ++mi)
+#pragma unroll
+      for (int ni = 0; ni < NI; ++ni) acc[mi][ni] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bw[ni], af[mi], acc[mi][ni], 0, 0, 0);
+  };
+  // one MFMA, one ds_read, ... : the next half's 4 + NI fragment reads ride between this half's
+  // first MFMAs (the fragments they replace were consumed at issue of the cluster's first MFMAs)
+  auto interleave = [&]() {
+#pragma unroll
+    for (int i = 0; i < 4 + NI; ++i) {
+      __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+      __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+    }
+    __builtin_amdgcn_sched_group_barrier(0x008, 4 * NI - (4 + NI), 0);
+  };
+  static_assert(LI == 10, "the counted waits below are written for 10 LDS-DMA loads per K-step");
+  const int nk = K / kTK;
+  bf16x8 af0[4], bw0[NI], af1[4], bw1[NI];
+  for (int n = 0; n < NS && n < nk; ++n) stage(n, n * kSlot);
+  if (nk >= 4) {
+    asm volatile("s_waitcnt vmcnt(30)" ::: "memory");
+  } else if (nk == 3) {
+    asm volatile("s_waitcnt vmcnt(20)" ::: "memory");
+  } else if (nk == 2) {
+    asm volatile("s_waitcnt vmcnt(10)" ::: "memory");
+  } else {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  }
+  asm volatile("s_barrier" ::: "memory");
+  int slot = 0;  // byte offset of step t's slot
+  read_half(0, 0, af0, bw0);
+  for (int t = 0; t + 1 < nk; ++t) {
+    const int nslot = slot + kSlot == NS * kSlot ? 0 : slot + kSlot;
+    __builtin_amdgcn_sched_barrier(0);
+    read_half(slot, 1, af1, bw1);
+    mma(af0, bw0);
+    interleave();
+    __builtin_amdgcn_sched_barrier(0);
+    // step t + 1 landed (steps t + 2, t + 3 may still be in flight); this wave's reads of step t retired
+    if (t + 3 < nk) {
+      asm volatile("s_waitcnt vmcnt(20) lgkmcnt(0)" ::: "memory");
+    } else if (t + 2 < nk) {
+      asm volatile("s_waitcnt vmcnt(10) lgkmcnt(0)" ::: "memory");
+    } else {
+      asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+    }
+    asm volatile("s_barrier" ::: "memory");
+    __builtin_amdgcn_sched_barrier(0);
+    if (t + NS < nk) stage(t + NS, slot);  // the slot step t just retired
+    __builtin_amdgcn_sched_barrier(0);
+    read_half(nslot, 0, af0, bw0);
+    mma(af1, bw1);
+    interleave();
+    __builtin_amdgcn_sched_barrier(0);
+    slot = nslot;
+  }
+  read_half(slot, 1, af1, bw1);
+  mma(af0, bw0);
+  mma(af1, bw1);
+  const bool vec_ok = (N % 4 == 0) && (ldc % 4 == 0);
+#pragma unroll
+  for (int mi = 0; mi < 4; ++mi) {
+    const int m = m0 + wr * 64 + mi * 16 + l16;
+    if (m >= M) continue;
+#pragma unroll
+    for (int ni = 0; ni < NI; ++ni) store4<EPI>(C, ldc, N, m, n0 + wc * WN + ni * 16 + 4 * lg, acc[mi][ni], vec_ok);
+  }
+}
+
 }  // namespace llmc
 
 using namespace llmc;
 
+// Kernel choice for a dense C[M, N]: 0 = 256 x 256 (gemm256_kernel), 1 = 128 x 192 (gemm_narrow_kernel).
+// Makespan model: rounds of 256 blocks (one per CU for both kernels) x the tile's area over its
+// full-chip rate; the narrow kernel's rate per unit area is 0.69 of the 256 x 256 kernel's (MI355X,
+// M = 8192: 870 vs 1268 TF/s at N = 6144), its tile 0.375 of the area. It wins where the 256 x 256
+// grid leaves CUs idle: a TP=8 rank's qkv (N = 768) at M = 8192 runs 53.5 us against 81.5
+// (hipBLASLt 50.5), at M = 2048 45.8 against 75.9; at M = 33000 (2 rounds against 5) the 256 x 256
+// kernel stays (188 vs 259 us). profiles/r5_gemm_narrow.md.
+extern "C" int llmc_gemm_plan(int M, int N) {
+  const int64_t t256 = static_cast<int64_t>((M + kT - 1) / kT) * ((N + kT - 1) / kT);
+  const int64_t tn = static_cast<int64_t>((M + 127) / 128) * ((N + 191) / 192);
+  const double r256 = static_cast<double>((t256 + 255) / 256), rn = static_cast<double>((tn + 255) / 256);
+  return rn * (0.375 / 0.69) < r256 ? 1 : 0;
+}
+
+extern "C" int llmc_gemm_narrow(const void* A, int lda, const void* W, int ldw, void* C, int ldc, int M, int N, int K,
+                                int epi, hipStream_t s);
+
 // C[M, N] (+)= A[M, K] . W[N, K]^T. epi: 0 bf16, 1 f32, 2 C += (bf16), 3 SiLU-mul of interleaved
 // gate/up columns into C[M, N / 2] (bf16). K must be a multiple of 64, lda/ldw multiples of 8.
-extern "C" int llmc_gemm(const void* A, int lda, const void* W, int ldw, void* C, int ldc, int M, int N, int K,
-                         int epi, hipStream_t s) {
+// kind: -1 = llmc_gemm_plan's choice, 0 = 256 x 256, 1 = 128 x 192.
+extern "C" int llmc_gemm_kind(const void* A, int lda, const void* W, int ldw, void* C, int ldc, int M, int N, int K,
+                              int epi, int kind, hipStream_t s) {
+  if (kind < 0) kind = M > 0 && N > 0 ? llmc_gemm_plan(M, N) : 0;
+  if (kind == 1) return llmc_gemm_narrow(A, lda, W, ldw, C, ldc, M, N, K, epi, s);
+  if (kind != 0) return -1;
   if (K % kTK != 0 || M <= 0 || N <= 0 || K <= 0 || (epi == 3 && N % 2 != 0)) return -1;
   if (lda % 8 != 0 || ldw % 8 != 0) return -1;  // 16-B aligned rows for the LDS-DMA
   // buffer offsets inside one 256-row tile must stay below 2^31 bytes
@@ -496,6 +662,30 @@ extern "C" int llmc_gemm(const void* A, int lda, const void* W, int ldw, void* C
     case 1: gemm256_kernel<1><<<nwg, 512, 0, s>>>((const bf16_t*)A, lda, (const bf16_t*)W, ldw, C, ldc, M, N, K); break;
     case 2: gemm256_kernel<2><<<nwg, 512, 0, s>>>((const bf16_t*)A, lda, (const bf16_t*)W, ldw, C, ldc, M, N, K); break;
     case 3: gemm256_kernel<3><<<nwg, 512, 0, s>>>((const bf16_t*)A, lda, (const bf16_t*)W, ldw, C, ldc, M, N, K); break;
+    default: return -2;
+  }
+  return static_cast<int>(hipGetLastError());
+}
+
+extern "C" int llmc_gemm(const void* A, int lda, const void* W, int ldw, void* C, int ldc, int M, int N, int K,
+                         int epi, hipStream_t s) {
+  return llmc_gemm_kind(A, lda, W, ldw, C, ldc, M, N, K, epi, -1, s);
+}
+
+// The narrow-N kernel (128 x 192 tiles) on a dense problem: same operands / epilogues as llmc_gemm
+// (microbenchmarks, tests and llmc_gemm's narrow-N dispatch).
+extern "C" int llmc_gemm_narrow(const void* A, int lda, const void* W, int ldw, void* C, int ldc, int M, int N, int K,
+                                int epi, hipStream_t s) {
+  if (K % kTK != 0 || M <= 0 || N <= 0 || (epi == 3 && N % 2 != 0) || lda % 8 != 0 || ldw % 8 != 0) return -1;
+  if (static_cast<int64_t>(192) * ldw * 2 >= (1ll << 31) || static_cast<int64_t>(128) * lda * 2 >= (1ll << 31)) return -1;
+  const int nwg = ((M + 127) / 128) * ((N + 191) / 192);
+  const bf16_t* a = (const bf16_t*)A;
+  const bf16_t* w = (const bf16_t*)W;
+  switch (epi) {
+    case 0: gemm_narrow_kernel<0, 6><<<nwg, 256, 0, s>>>(a, lda, w, ldw, C, ldc, M, N, K); break;
+    case 1: gemm_narrow_kernel<1, 6><<<nwg, 256, 0, s>>>(a, lda, w, ldw, C, ldc, M, N, K); break;
+    case 2: gemm_narrow_kernel<2, 6><<<nwg, 256, 0, s>>>(a, lda, w, ldw, C, ldc, M, N, K); break;
+    case 3: gemm_narrow_kernel<3, 6><<<nwg, 256, 0, s>>>(a, lda, w, ldw, C, ldc, M, N, K); break;
     default: return -2;
   }
   return static_cast<int>(hipGetLastError());

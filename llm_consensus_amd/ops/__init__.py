@@ -106,7 +106,7 @@ def linear(x: torch.Tensor, W: torch.Tensor, epi: int = EPI_BF16, out: Optional[
 
 
 def gemm(x: torch.Tensor, W: torch.Tensor, epi: int = EPI_BF16, out: Optional[torch.Tensor] = None) -> torch.Tensor:
-    """Always the MFMA GEMM path (tests / microbenchmarks)."""
+    """Always the MFMA GEMM path, kernel chosen by ``gemm_plan`` (tests / microbenchmarks)."""
     if not x.is_cuda:
         return oracle.linear(x, W, epi, out)
     M, K = x.shape
@@ -129,6 +129,34 @@ def gemm128(x: torch.Tensor, W: torch.Tensor, epi: int = EPI_BF16, out: Optional
         out = torch.empty(M, n_out, dtype=torch.float32 if epi == EPI_F32 else torch.bfloat16, device=x.device)
     kernels().gemm_t128(_p(x), x.stride(0), _p(W), W.stride(0), _p(out), out.stride(0), M, N, K, epi, _s(x))
     return out
+
+
+def _gemm_kind(x, W, epi, out, kind):
+    if not x.is_cuda:
+        return oracle.linear(x, W, epi, out)
+    M, K = x.shape
+    N = W.shape[0]
+    if out is None:
+        n_out = N // 2 if epi == EPI_SILU else N
+        out = torch.empty(M, n_out, dtype=torch.float32 if epi == EPI_F32 else torch.bfloat16, device=x.device)
+    kernels().gemm_kind(_p(x), x.stride(0), _p(W), W.stride(0), _p(out), out.stride(0), M, N, K, epi, kind, _s(x))
+    return out
+
+
+def gemm256(x: torch.Tensor, W: torch.Tensor, epi: int = EPI_BF16, out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """Always the 256 x 256 LDS-DMA ring kernel (tests / microbenchmarks)."""
+    return _gemm_kind(x, W, epi, out, 0)
+
+
+def gemm_narrow(x: torch.Tensor, W: torch.Tensor, epi: int = EPI_BF16, out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """Always the 128 x 192 narrow-N MFMA kernel (tests / microbenchmarks of the narrow-N dispatch)."""
+    return _gemm_kind(x, W, epi, out, 1)
+
+
+def gemm_plan(M: int, N: int) -> str:
+    """The prefill GEMM kernel ``linear`` / ``gemm`` launch for a dense [M, N] output (host-side model,
+    csrc/kernels/gemm.hip ``llmc_gemm_plan``): "256x256" or "128x192"."""
+    return ("256x256", "128x192")[kernels().gemm_plan(int(M), int(N))]
 
 
 def gemv(x: torch.Tensor, W: torch.Tensor, epi: int = EPI_BF16, out: Optional[torch.Tensor] = None,

@@ -333,16 +333,22 @@ def bench_prefill():
                       # Llama-3-70B TP=4 rank (config 5 judge prefill): qkv, o, gate_up, down
                       (8192, 2560, 8192), (8192, 8192, 2048), (8192, 14336, 8192), (8192, 8192, 7168),
                       # Llama-3-8B TP=8 rank (the N=8 bench judge): qkv, gate_up, down
-                      (8192, 768, 4096), (8192, 3584, 4096), (8192, 4096, 1792)]:
+                      (8192, 768, 4096), (8192, 3584, 4096), (8192, 4096, 1792),
+                      # the TP=8 rank's qkv on the 33k-token judge prompt and a 2k prompt
+                      (33000, 768, 4096), (2048, 768, 4096)]:
+        if os.environ.get("GEMM_CASES") and f"{M},{N},{K}" not in os.environ["GEMM_CASES"].split(";"):
+            continue
         x = (torch.rand(M, K, device="cuda") * 2 - 1).to(BF)  # full-range random data (guide rule 25)
         W = ((torch.rand(N, K, device="cuda") * 2 - 1) * 0.05).to(BF)
         out = torch.empty(M, N, dtype=BF, device="cuda")
         t_ours = timeit(lambda: ops.gemm(x, W, 0, out=out), iters=10)
         t_128 = timeit(lambda: ops.gemm128(x, W, 0, out=out), iters=10)
+        t_nar = timeit(lambda: ops.gemm_narrow(x, W, 0, out=out), iters=10)
         t_ref = timeit(lambda: torch.matmul(x, W.t(), out=out), iters=10)  # hipBLASLt: reference only
         fl = 2 * M * N * K
         line = (f"gemm M={M} N={N} K={K}: ours {t_ours:8.1f} us {fl / t_ours / 1e6:6.0f} TF/s | 128x128 {t_128:8.1f} us "
-                f"{fl / t_128 / 1e6:6.0f} TF/s | torch {t_ref:8.1f} us {fl / t_ref / 1e6:6.0f} TF/s")
+                f"{fl / t_128 / 1e6:6.0f} TF/s | 128x192 {t_nar:8.1f} us {fl / t_nar / 1e6:6.0f} TF/s | "
+                f"torch {t_ref:8.1f} us {fl / t_ref / 1e6:6.0f} TF/s")
         print(line, flush=True)
     bench_attn_prefill()
 

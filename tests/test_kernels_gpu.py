@@ -196,9 +196,19 @@ def test_gemm(cuda, M, N, K, epi):
     W = rnd(N, K, scale=0.05)
     out = rnd(M, N) if epi == 2 else None
     ref_out = out.cpu().clone() if out is not None else None
-    y = ops.gemm(x, W, epi, out=out)
+    y = ops.gemm256(x, W, epi, out=out)
     ref = oracle.linear(x.cpu(), W.cpu(), epi, ref_out)
     close(y, ref, 2e-2)
+
+
+@pytest.mark.parametrize("M,N,K", [(8192, 768, 512), (4100, 1536, 256), (4096, 4096, 128)])
+def test_gemm_dispatch(cuda, M, N, K):
+    """ops.gemm through llmc_gemm's kernel choice on shapes either side of the narrow-N rule
+    (gemm_plan: 128 x 192 for 8192 x 768, 256 x 256 for 4096 x 4096) vs the fp32 oracle."""
+    torch.manual_seed(M + N + K)
+    x = rnd(M, K)
+    W = rnd(N, K, scale=0.05)
+    close(ops.gemm(x, W, 0), oracle.linear(x.cpu(), W.cpu(), 0, None), 2e-2)
 
 
 @pytest.mark.parametrize("M,N,K", [(300, 768, 4096), (1024, 2560, 1024), (257, 130, 320), (37, 200, 256)])
@@ -218,13 +228,40 @@ def test_gemm128_dense(cuda, M, N, K, epi):
     close(y, ref, 2e-2)
 
 
+@pytest.mark.parametrize("M,N,K", [(300, 768, 4096), (1024, 2560, 1024), (257, 130, 320), (37, 200, 256),
+                                   (128, 192, 64), (200, 384, 128), (129, 194, 192)])
+@pytest.mark.parametrize("epi", [0, 1, 2, 3])
+def test_gemm_narrow(cuda, M, N, K, epi):
+    """The 128 x 192 narrow-N kernel vs the fp32 oracle: every epilogue, ragged M / N tiles, K of one,
+    two and three K-steps (the prologue's vmcnt forms) up to 64 (the 3-slot ring wrapping)."""
+    if epi == 3 and N % 2:
+        pytest.skip("SiLU pairs need even N")
+    torch.manual_seed(M + N + K + epi + 11)
+    x = rnd(M, K)
+    W = rnd(N, K, scale=0.05)
+    out = rnd(M, N) if epi == 2 else None
+    ref_out = out.cpu().clone() if out is not None else None
+    y = ops.gemm_narrow(x, W, epi, out=out)
+    ref = oracle.linear(x.cpu(), W.cpu(), epi, ref_out)
+    close(y, ref, 2e-2)
+
+
+@pytest.mark.parametrize("K", [128, 512])
+def test_gemm_narrow_identity_asymmetric(cuda, K):
+    """A = I against an asymmetric W through the narrow kernel: a transposed or misplaced C write
+    shows as a wrong element (K = 512: 4 M tiles x 3 N tiles, the last one partial)."""
+    A = torch.eye(K, dtype=BF, device="cuda")
+    W = (torch.arange(K * K, device="cuda").view(K, K) % 97).to(BF)
+    assert torch.equal(ops.gemm_narrow(A, W, 0).cpu(), W.t().contiguous().cpu())
+
+
 @pytest.mark.parametrize("K", [128, 512])
 def test_gemm_identity_asymmetric(cuda, K):
     """A = I with an asymmetric B catches a transposed C write (guide §3); K = 512 spans two
     256-row tiles in M and N."""
     A = torch.eye(K, dtype=BF, device="cuda")
     W = (torch.arange(K * K, device="cuda").view(K, K) % 97).to(BF)  # asymmetric
-    y = ops.gemm(A, W, 0)
+    y = ops.gemm256(A, W, 0)
     assert torch.equal(y.cpu(), W.t().contiguous().cpu())
 
 

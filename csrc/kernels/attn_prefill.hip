@@ -58,7 +58,7 @@ __device__ __forceinline__ int k_swz(int row, int ch) { return row * kRowBytes +
 __device__ __forceinline__ int v_swz(int row, int ch) { return row * kRowBytes + ((ch ^ ((row & 3) << 2)) << 4); }
 
 template <int D, int WPB, int LA, bool P64>
-__global__ __launch_bounds__(WPB * 64) void attn_prefill_kernel(
+__global__ __launch_bounds__(WPB * 64, 8 / WPB) void attn_prefill_kernel(
     const bf16_t* __restrict__ q, int q_stride, const bf16_t* __restrict__ k_cache, const bf16_t* __restrict__ v_cache,
     const int32_t* __restrict__ block_tables, int bt_stride, const int32_t* __restrict__ q_start,
     const int32_t* __restrict__ q_lens, const int32_t* __restrict__ ctx_lens, bf16_t* __restrict__ out,
@@ -489,6 +489,15 @@ extern "C" int llmc_attn_prefill_plan(int B, int max_qlen, int max_ctx, int nh, 
   return best_s;
 }
 
+// Waves per block of an (unsplit) prefill launch: 4 when the 8-wave grid is one round of the chip
+// and G >= 4, else 8 (llmc_attn_prefill's comment has the measurements).
+extern "C" int llmc_attn_prefill_wpb(int B, int max_qlen, int nh, int nkv, int ksplit) {
+  if (nkv <= 0 || nh % nkv != 0 || ksplit > 1) return 8;
+  const int G = nh / nkv, npb = (max_qlen + 31) / 32;
+  const int64_t units8 = static_cast<int64_t>((G * npb + 7) / 8) * nkv * B;
+  return G >= 4 && units8 <= 256 ? 4 : 8;
+}
+
 extern "C" int llmc_attn_prefill(const void* q, int q_stride, const void* k_cache, const void* v_cache,
                                  const void* block_tables, int bt_stride, const void* q_start, const void* q_lens,
                                  const void* ctx_lens, void* out, int out_stride, int B, int max_qlen, int nh, int nkv,
@@ -499,9 +508,20 @@ extern "C" int llmc_attn_prefill(const void* q, int q_stride, const void* k_cach
     return -1;
   const int G = nh / nkv;
   const int npb = (max_qlen + 31) / 32;
-  // 8 waves = 2 row tiles x 4 heads share every staged K/V tile (one block per CU at ~250 VGPRs;
-  // 4-wave blocks, meant to run two per CU without shared barriers, measured 0.6x at 8k: one per CU)
-  constexpr int wpb = 8;
+  // Waves (32-row tiles) per block. 8: 2 row tiles x 4 heads share every staged K/V tile, one block
+  // per CU (247 VGPRs: 2 waves / SIMD). 4, two blocks per CU (launch bound: <= 256 VGPRs, so the
+  // one-tile lookahead; two tiles spill): when the 8-wave grid is ONE round of the chip (<= 256
+  // blocks) its longest block (every key tile, 2 waves / SIMD) is the critical path; as 4-wave
+  // blocks dispatched longest-first, a CU pairs a long block with a short one. Measured (MI355X,
+  // profiles/r5_prefill_attention.md): Llama-3-8B 2k tokens 76.2 -> 69.7 us, 1k 39.0 -> 32.1; on
+  // multi-round grids 8 stays (8k: 556 vs 592 us) and with G = 2 too (70B TP=4 rank at 8k, 128
+  // blocks: 279 vs 320 us, its 4-wave blocks run alone at 1 wave / SIMD). A split grid keeps 8.
+  static const int wpb_env = [] {
+    const char* e = getenv("LLMC_PREFILL_WPB");  // A/B runs: force 4 or 8 (unsplit grids)
+    return e ? atoi(e) : 0;
+  }();
+  int wpb = llmc_attn_prefill_wpb(B, max_qlen, nh, nkv, ksplit);
+  if ((wpb_env == 4 || wpb_env == 8) && ksplit == 1) wpb = wpb_env;
   dim3 grid((G * npb + wpb - 1) / wpb * ksplit * nkv, 1, B);
   const float sl2 = scale * 1.4426950408889634f;
   static const int la = [] {
@@ -513,16 +533,21 @@ extern "C" int llmc_attn_prefill(const void* q, int q_stride, const void* k_cach
     if (bs == kKT) LLMC_PFP(DD, L, true);                                                                        \
     else LLMC_PFP(DD, L, false);                                                                                 \
   } while (0)
-#define LLMC_PFP(DD, L, P)                                                                                       \
-  attn_prefill_kernel<DD, wpb, L, P><<<grid, wpb * 64, 0, s>>>((const bf16_t*)q, q_stride, (const bf16_t*)k_cache, \
+#define LLMC_PFW(DD, L, P, W)                                                                                    \
+  attn_prefill_kernel<DD, W, L, P><<<grid, W * 64, 0, s>>>((const bf16_t*)q, q_stride, (const bf16_t*)k_cache,     \
                                                (const bf16_t*)v_cache, (const int32_t*)block_tables, bt_stride,   \
                                                (const int32_t*)q_start, (const int32_t*)q_lens,                  \
                                                (const int32_t*)ctx_lens, (bf16_t*)out, out_stride, nh, nkv, bs, sl2, \
                                                ksplit, kmin, (float*)part, (int*)counters, T_all)
-#define LLMC_PF_D(DD)                \
-  do {                               \
-    if (la >= 2) LLMC_PF(DD, 2);     \
-    else LLMC_PF(DD, 1);             \
+#define LLMC_PFP(DD, L, P)                         \
+  do {                                             \
+    if (L == 1 && wpb == 4) LLMC_PFW(DD, 1, P, 4); \
+    else LLMC_PFW(DD, L, P, 8);                    \
+  } while (0)
+#define LLMC_PF_D(DD)                          \
+  do {                                         \
+    if (la >= 2 && wpb == 8) LLMC_PF(DD, 2);   \
+    else LLMC_PF(DD, 1);                       \
   } while (0)
   switch (D) {
     case 64: LLMC_PF_D(64); break;
@@ -533,5 +558,6 @@ extern "C" int llmc_attn_prefill(const void* q, int q_stride, const void* k_cach
 #undef LLMC_PF_D
 #undef LLMC_PF
 #undef LLMC_PFP
+#undef LLMC_PFW
   return static_cast<int>(hipGetLastError());
 }

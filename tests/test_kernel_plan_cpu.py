@@ -30,6 +30,19 @@ def test_prefill_split_overrides():
     assert ops.attn_prefill_plan(1, 2048, 2048, 32, 8, ksplit=99, kmin=3) == (4, 3)
 
 
+@pytest.mark.parametrize("B,T,nh,nkv,ksplit,wpb", [
+    (1, 2048, 32, 8, 1, 4),     # Llama-3-8B 2k: 256 8-wave blocks = one round -> 4-wave blocks (76.2 -> 69.7 us)
+    (1, 1024, 32, 8, 1, 4),     # 39.0 -> 32.1 us
+    (1, 8192, 32, 8, 1, 8),     # 1024 blocks: 8 (556 vs 592 us)
+    (2, 2048, 32, 8, 1, 8),     # two sequences: 512 blocks
+    (1, 8192, 16, 2, 1, 8),     # G = 2 (70B TP=4 rank): 8 (279 vs 320 us)
+    (1, 8192, 4, 1, 4, 8),      # a split grid keeps 8
+])
+def test_prefill_waves_per_block(B, T, nh, nkv, ksplit, wpb):
+    from llm_consensus_amd.ops import kernels
+    assert kernels().attn_prefill_wpb(B, T, nh, nkv, ksplit) == wpb
+
+
 @pytest.mark.parametrize("M,N,kind", [
     (8192, 768, "128x192"),    # a TP=8 rank's qkv: 96 tiles of 256 x 256 for 256 CUs (53.5 vs 81.5 us)
     (2048, 768, "128x192"),

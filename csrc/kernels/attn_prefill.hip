@@ -63,7 +63,7 @@ __global__ __launch_bounds__(WPB * 64, 8 / WPB) void attn_prefill_kernel(
     const int32_t* __restrict__ block_tables, int bt_stride, const int32_t* __restrict__ q_start,
     const int32_t* __restrict__ q_lens, const int32_t* __restrict__ ctx_lens, bf16_t* __restrict__ out,
     int out_stride, int nh, int nkv, int bs, float scale_log2, int ksplit, int kmin, float* __restrict__ part,
-    int* __restrict__ counters, int T_all) {
+    int* __restrict__ counters, int T_all, int pair) {
   constexpr int CH = D / 8;            // 16-B chunks per row
   constexpr int NT = WPB * 64;
   constexpr int NL = (kKT * CH + NT - 1) / NT;  // staging chunks per thread per tensor
@@ -88,14 +88,26 @@ __global__ __launch_bounds__(WPB * 64, 8 / WPB) void attn_prefill_kernel(
   const int npb = (qlen + 31) / 32;
   const int nrt = G * npb;
   const int rt_base = (ngrp - 1 - grp) * WPB;
-  if (rt_base >= nrt) return;  // block-uniform
+  if (!pair && rt_base >= nrt) return;  // block-uniform
 
   // wave index through readfirstlane: everything derived from it (row tile, head, descriptors)
   // is then known wave-uniform (a divergent-looking descriptor costs a waterfall loop per access)
   const int tid = threadIdx.x, wave = __builtin_amdgcn_readfirstlane(tid / 64), lane = tid % 64;
   const int r = lane & 31, hh = lane >> 5;
-  const int rt = rt_base + wave;
-  const bool wvalid = rt < nrt;
+  // pair (unsplit grids, WPB / G = R >= 2 even): block grp (0 = dispatched first) takes the R / 2
+  // LATEST 32-row tiles still free (npb - 1 - grp R/2 - j) for waves [0, WPB / 2) and the R / 2
+  // EARLIEST (grp R/2 + j) for the others. An early tile's causal key range is a prefix of the late
+  // one's, so the block stages the late tiles' keys once for both, and every SIMD holds one late
+  // and one early wave: ~npb + 1 tile steps per SIMD in every block instead of 2 x the block's
+  // latest tile, whose longest block set the critical path of one-round grids.
+  int rt = rt_base + wave;
+  bool wvalid = rt < nrt;
+  if (pair) {
+    const int R = WPB / G, half = R / 2, slot = wave / G, top = ngrp * half;
+    const int pbp = slot < half ? npb - 1 - (grp * half + slot) : grp * half + (slot - half);
+    wvalid = pbp >= 0 && (slot < half || pbp < npb - top);
+    rt = pbp * G + wave % G;
+  }
   const int g = wvalid ? rt % G : 0;
   const int pb = wvalid ? rt / G : 0;
   const int h = kvh * G + g;
@@ -104,7 +116,7 @@ __global__ __launch_bounds__(WPB * 64, 8 / WPB) void attn_prefill_kernel(
   const int qi = min(row_i, qlen - 1);
   const int qpos = first_pos + qi;                 // absolute position (causal limit)
   const int last_rt = min(rt_base + WPB - 1, nrt - 1);
-  const int pb_last = last_rt / G;
+  const int pb_last = pair ? max(npb - 1 - grp * (WPB / G / 2), 0) : last_rt / G;
   const int kend = min(ctx, first_pos + min(pb_last * 32 + 31, qlen - 1) + 1);
   const int ntiles_all = (kend + kKT - 1) / kKT;
   // only groups with >= 2 kmin key tiles split (a causal grid's short groups run whole); the
@@ -475,10 +487,13 @@ extern "C" int llmc_attn_prefill_plan(int B, int max_qlen, int max_ctx, int nh, 
     return end;
   };
   int best_s = 1, best_k = 1 << 30;
-  float best = makespan(1, 1 << 30) * 0.97f;  // a split must win by > 3%
+  // a split must win by > 3%; on a one-round grid by > 20%: the unsplit grid then runs the paired
+  // or 4-wave form (llmc_attn_prefill_form), ~0.83x of the 8-wave time this model prices
+  float best = makespan(1, 1 << 30) * (units <= 256 ? 0.80f : 0.97f);
   // 4-way splits measured a loss everywhere but on grids of <= 128 blocks with >= 2 row tiles per
-  // group (a TP=8 rank's single kv head); the cost model alone over-rates them elsewhere
-  const bool allow4 = units <= 128 && G <= 4;
+  // group (a TP=8 rank's single kv head) at >= 8k keys or on the smallest grids; the cost model
+  // alone over-rates them elsewhere (8 / 2 heads at 4k keys: 0.56x predicted, 0.94x measured)
+  const bool allow4 = G <= 4 && ((units <= 128 && max_ctx >= 8192) || units <= 32);
   for (int S : {2, 4})
     for (int kmin : {4, 8, 16}) {
       if (S == 4 && !allow4) continue;
@@ -489,13 +504,27 @@ extern "C" int llmc_attn_prefill_plan(int B, int max_qlen, int max_ctx, int nh, 
   return best_s;
 }
 
-// Waves per block of an (unsplit) prefill launch: 4 when the 8-wave grid is one round of the chip
-// and G >= 4, else 8 (llmc_attn_prefill's comment has the measurements).
-extern "C" int llmc_attn_prefill_wpb(int B, int max_qlen, int nh, int nkv, int ksplit) {
-  if (nkv <= 0 || nh % nkv != 0 || ksplit > 1) return 8;
+// Block form of a prefill launch: 0 = 8 waves (2 row tiles x 4 heads of one kv head share every
+// staged K/V tile; one block per CU at 247 VGPRs), 1 = 8 waves with paired row tiles (a late and an
+// early one per SIMD: `pair` in the kernel), 2 = 4 waves, two blocks per CU (launch bound: <= 256
+// VGPRs, so the one-tile lookahead; two tiles spill). A split grid is form 0. On a grid of more
+// than one round of the chip the longest-first order balances already and form 0 stays (8k: 552
+// vs 587 us as 4-wave blocks, 630 paired); when the 8-wave grid is ONE round (<= 256 blocks) its
+// longest block (every key tile at 2 waves / SIMD) is the critical path, which forms 1 and 2
+// shorten. Measured (MI355X, unsplit, us; profiles/r5_prefill_attention.md):
+//   heads/kv  T      8 waves  paired  4 waves
+//   32/8     2048     76.6     63.2     69.2     (256 blocks: paired)
+//   32/32    2048     69.9     58.1     63.3
+//   32/8     1024     39.5     33.0     32.4     (128 blocks: 4 waves)
+//   32/32    1024     39.4     34.2     32.4
+//   16/2     2048     72.1      —       59.6     (G = 8: no pairs; 4 waves)
+//   16/2     4096    129.3      —      115.7
+extern "C" int llmc_attn_prefill_form(int B, int max_qlen, int nh, int nkv, int ksplit) {
+  if (nkv <= 0 || nh % nkv != 0 || ksplit > 1) return 0;
   const int G = nh / nkv, npb = (max_qlen + 31) / 32;
   const int64_t units8 = static_cast<int64_t>((G * npb + 7) / 8) * nkv * B;
-  return G >= 4 && units8 <= 256 ? 4 : 8;
+  if (units8 > 256) return 0;
+  return G <= 4 && units8 > 128 ? 1 : 2;
 }
 
 extern "C" int llmc_attn_prefill(const void* q, int q_stride, const void* k_cache, const void* v_cache,
@@ -508,20 +537,15 @@ extern "C" int llmc_attn_prefill(const void* q, int q_stride, const void* k_cach
     return -1;
   const int G = nh / nkv;
   const int npb = (max_qlen + 31) / 32;
-  // Waves (32-row tiles) per block. 8: 2 row tiles x 4 heads share every staged K/V tile, one block
-  // per CU (247 VGPRs: 2 waves / SIMD). 4, two blocks per CU (launch bound: <= 256 VGPRs, so the
-  // one-tile lookahead; two tiles spill): when the 8-wave grid is ONE round of the chip (<= 256
-  // blocks) its longest block (every key tile, 2 waves / SIMD) is the critical path; as 4-wave
-  // blocks dispatched longest-first, a CU pairs a long block with a short one. Measured (MI355X,
-  // profiles/r5_prefill_attention.md): Llama-3-8B 2k tokens 76.2 -> 69.7 us, 1k 39.0 -> 32.1; on
-  // multi-round grids 8 stays (8k: 556 vs 592 us) and with G = 2 too (70B TP=4 rank at 8k, 128
-  // blocks: 279 vs 320 us, its 4-wave blocks run alone at 1 wave / SIMD). A split grid keeps 8.
-  static const int wpb_env = [] {
-    const char* e = getenv("LLMC_PREFILL_WPB");  // A/B runs: force 4 or 8 (unsplit grids)
-    return e ? atoi(e) : 0;
+  // block form: llmc_attn_prefill_form (its comment has the measurements)
+  static const int form_env = [] {
+    const char* e = getenv("LLMC_PREFILL_FORM");  // A/B runs: force form 0 / 1 / 2 (unsplit grids)
+    return e ? atoi(e) : -1;
   }();
-  int wpb = llmc_attn_prefill_wpb(B, max_qlen, nh, nkv, ksplit);
-  if ((wpb_env == 4 || wpb_env == 8) && ksplit == 1) wpb = wpb_env;
+  int form = llmc_attn_prefill_form(B, max_qlen, nh, nkv, ksplit);
+  if (form_env >= 0 && form_env <= 2 && ksplit == 1) form = form_env;
+  if (form == 1 && (G > 4 || 8 % G != 0)) form = 0;  // pairs need WPB / G >= 2 row tiles
+  const int wpb = form == 2 ? 4 : 8, pair = form == 1 ? 1 : 0;
   dim3 grid((G * npb + wpb - 1) / wpb * ksplit * nkv, 1, B);
   const float sl2 = scale * 1.4426950408889634f;
   static const int la = [] {
@@ -538,7 +562,7 @@ extern "C" int llmc_attn_prefill(const void* q, int q_stride, const void* k_cach
                                                (const bf16_t*)v_cache, (const int32_t*)block_tables, bt_stride,   \
                                                (const int32_t*)q_start, (const int32_t*)q_lens,                  \
                                                (const int32_t*)ctx_lens, (bf16_t*)out, out_stride, nh, nkv, bs, sl2, \
-                                               ksplit, kmin, (float*)part, (int*)counters, T_all)
+                                               ksplit, kmin, (float*)part, (int*)counters, T_all, pair)
 #define LLMC_PFP(DD, L, P)                         \
   do {                                             \
     if (L == 1 && wpb == 4) LLMC_PFW(DD, 1, P, 4); \

@@ -11,7 +11,8 @@ from llm_consensus_amd import ops
     (1, 8192, 8192, 4, 1, 4),         # a TP=8 rank: one kv head, 128 blocks -> 4 ways (1.7x measured)
     (1, 2048, 2048, 4, 1, 4),
     (1, 8192, 8192, 8, 1, 2),         # 256 blocks of up to 128 tiles: 2 ways (1.3x)
-    (1, 2048, 2048, 16, 2, 2),        # 64 blocks: 2 ways (1.15x)
+    (1, 2048, 2048, 16, 2, 1),        # 128 blocks: the unsplit 4-wave form (59.6 us) beats 2 ways (61.5)
+    (1, 4096, 4096, 8, 2, 2),         # 2 ways (87.8 us; 4 ways measured 119, unsplit paired 99)
     (1, 2048, 2048, 32, 8, 1),        # 256 blocks of 1..32 tiles: a split costs more than it saves
     (1, 8192, 8192, 32, 8, 1),        # 1024 blocks: the longest-first order balances already
     (4, 8192, 8192, 32, 8, 1),
@@ -30,17 +31,20 @@ def test_prefill_split_overrides():
     assert ops.attn_prefill_plan(1, 2048, 2048, 32, 8, ksplit=99, kmin=3) == (4, 3)
 
 
-@pytest.mark.parametrize("B,T,nh,nkv,ksplit,wpb", [
-    (1, 2048, 32, 8, 1, 4),     # Llama-3-8B 2k: 256 8-wave blocks = one round -> 4-wave blocks (76.2 -> 69.7 us)
-    (1, 1024, 32, 8, 1, 4),     # 39.0 -> 32.1 us
-    (1, 8192, 32, 8, 1, 8),     # 1024 blocks: 8 (556 vs 592 us)
-    (2, 2048, 32, 8, 1, 8),     # two sequences: 512 blocks
-    (1, 8192, 16, 2, 1, 8),     # G = 2 (70B TP=4 rank): 8 (279 vs 320 us)
-    (1, 8192, 4, 1, 4, 8),      # a split grid keeps 8
+@pytest.mark.parametrize("B,T,nh,nkv,ksplit,form", [
+    (1, 2048, 32, 8, 1, 1),     # Llama-3-8B 2k: 256 8-wave blocks = one round -> paired (76.6 -> 63.2 us)
+    (1, 2048, 32, 32, 1, 1),    # 69.9 -> 58.1
+    (1, 1024, 32, 8, 1, 2),     # 128 blocks: 4-wave blocks (39.5 -> 32.4)
+    (1, 2048, 16, 2, 1, 2),     # G = 8 (70B TP=4 rank): no pairs; 4 waves (72.1 -> 59.6)
+    (1, 4096, 16, 2, 1, 2),     # 129.3 -> 115.7
+    (1, 8192, 32, 8, 1, 0),     # 1024 blocks: the 8-wave longest-first grid (552 vs 587 / 630)
+    (2, 2048, 32, 8, 1, 0),     # two sequences: 512 blocks
+    (1, 8192, 16, 2, 1, 0),     # 512 blocks
+    (1, 8192, 4, 1, 4, 0),      # a split grid
 ])
-def test_prefill_waves_per_block(B, T, nh, nkv, ksplit, wpb):
+def test_prefill_block_form(B, T, nh, nkv, ksplit, form):
     from llm_consensus_amd.ops import kernels
-    assert kernels().attn_prefill_wpb(B, T, nh, nkv, ksplit) == wpb
+    assert kernels().attn_prefill_form(B, T, nh, nkv, ksplit) == form
 
 
 @pytest.mark.parametrize("M,N,kind", [

@@ -44,6 +44,7 @@ constexpr int kKT = 64;        // keys per tile
 constexpr int kRowBytes = 256; // LDS row pitch (128 bf16), D <= 128
 constexpr int kTileBytes = kKT * kRowBytes;  // 16 KB
 constexpr int kPrefillLookahead = 2;          // K/V tiles requested ahead of the one computing
+constexpr int kDmaSlots = 4;                   // LDS-DMA staging: tiles resident (3 in flight)
 constexpr int kMaxSplit = 4;                   // KV-split ways (llmc_attn_prefill_plan)
 constexpr float kSlack = 8.f;                  // deferred running-max update threshold (log2 units)
 
@@ -57,7 +58,7 @@ __device__ __forceinline__ uint32_t cvt_pk_bf16(float lo, float hi) {
 __device__ __forceinline__ int k_swz(int row, int ch) { return row * kRowBytes + ((ch ^ (row & 15)) << 4); }
 __device__ __forceinline__ int v_swz(int row, int ch) { return row * kRowBytes + ((ch ^ ((row & 3) << 2)) << 4); }
 
-template <int D, int WPB, int LA, bool P64>
+template <int D, int WPB, int LA, bool P64, bool DMA = false>
 __global__ __launch_bounds__(WPB * 64, 8 / WPB) void attn_prefill_kernel(
     const bf16_t* __restrict__ q, int q_stride, const bf16_t* __restrict__ k_cache, const bf16_t* __restrict__ v_cache,
     const int32_t* __restrict__ block_tables, int bt_stride, const int32_t* __restrict__ q_start,
@@ -71,7 +72,12 @@ __global__ __launch_bounds__(WPB * 64, 8 / WPB) void attn_prefill_kernel(
   constexpr int KS = D / 16;           // k-steps for Q.K
   constexpr int DT = D / 32;           // 32-wide d tiles of O
 
-  __shared__ __attribute__((aligned(16))) char smem[2 * 2 * kTileBytes];  // [buf][K|V]
+  static_assert(!DMA || (P64 && D == 128 && WPB == 8), "LDS-DMA staging: 64-key pages, D = 128, 8 waves");
+  // [slot][K|V], then the split hand-off's is_last word. ONE LDS object: with a second __shared__
+  // variable the LDS lowering tags every access with alias scopes, and hipcc's waitcnt pass then
+  // makes each tile's first LDS read wait for every LDS-DMA in flight (vmcnt(0): no lookahead)
+  constexpr int kSmemMain = (DMA ? kDmaSlots : 2) * 2 * kTileBytes;
+  __shared__ __attribute__((aligned(16))) char smem[kSmemMain + 16];
 
   const int G = nh / nkv;
   // grid.x = row-tile groups x kv heads, kv head fastest: the dispatch order is longest-first over
@@ -207,6 +213,193 @@ __global__ __launch_bounds__(WPB * 64, 8 / WPB) void attn_prefill_kernel(
     }
   };
 
+  // one 64-key tile of every wave (kb / vb: the tile's K and V images in LDS)
+  auto tile_compute = [&](int t, const char* kb, const char* vb) {
+      const int kt = t * kKT;
+      if (wvalid && kt < wave_kend) {
+        // ---- S^T = K . Q^T for two 32-key halves ----
+        f32x16 s[2];
+  #pragma unroll
+        for (int kb2 = 0; kb2 < 2; ++kb2) {
+  #pragma unroll
+          for (int i = 0; i < 16; ++i) s[kb2][i] = 0.f;
+          const int row = kb2 * 32 + r;
+  #pragma unroll
+          for (int ks = 0; ks < KS; ++ks) {
+            const bf16x8 a = *reinterpret_cast<const bf16x8*>(kb + k_swz(row, 2 * ks + hh));
+            s[kb2] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, qf[ks], s[kb2], 0, 0, 0);
+          }
+        }
+        // ---- online softmax (lane owns query qpos; keys in registers) ----
+        // VALU diet (the loop is VALU-bound at 2 waves/SIMD, ~2x the MFMA cycles before it): the
+        // max on raw scores (scale > 0), then ONE fma + exp per score; causal masking only on the
+        // tiles that reach past the wave's first query position; the running max moves only when a
+        // new score exceeds it by > kSlack (log2 units, so P <= 2^kSlack: exact in f32, same bf16
+        // relative rounding), which leaves the O rescale out of almost every tile; P packed by
+        // v_cvt_pk_bf16_f32 (two floats per instruction, RNE).
+        const bool diag = kt + kKT - 1 > wave_qpos0;  // wave-uniform
+        float mx = -1e30f;
+        // diag: score (kb2, i) is key kt + 4 hh + kb2*32 + (i & 3) + 8 (i >> 2): visible iff that
+        // compile-time offset <= lim (an inline-constant compare, no per-score add)
+        const int lim = qpos - kt - 4 * hh;
+        if (diag) {
+  #pragma unroll
+          for (int kb2 = 0; kb2 < 2; ++kb2)
+  #pragma unroll
+            for (int i = 0; i < 16; ++i)
+              mx = fmaxf(mx, kb2 * 32 + (i & 3) + 8 * (i >> 2) <= lim ? s[kb2][i] : -1e30f);
+        } else {
+  #pragma unroll
+          for (int kb2 = 0; kb2 < 2; ++kb2)
+  #pragma unroll
+            for (int i = 0; i < 16; ++i) mx = fmaxf(mx, s[kb2][i]);
+        }
+        mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+        const float mx_s = mx * scale_log2;
+        const float m_new = mx_s > m_run + kSlack ? mx_s : m_run;
+        const float neg_m = -m_new;
+        float rs2[4] = {0.f, 0.f, 0.f, 0.f};
+        if (diag) {
+  #pragma unroll
+          for (int kb2 = 0; kb2 < 2; ++kb2)
+  #pragma unroll
+            for (int i = 0; i < 16; ++i) {
+              const float p = kb2 * 32 + (i & 3) + 8 * (i >> 2) <= lim
+                                  ? __builtin_amdgcn_exp2f(fmaf(s[kb2][i], scale_log2, neg_m))
+                                  : 0.f;
+              s[kb2][i] = p;
+              rs2[i & 3] += p;
+            }
+        } else {
+  #pragma unroll
+          for (int kb2 = 0; kb2 < 2; ++kb2)
+  #pragma unroll
+            for (int i = 0; i < 16; ++i) {
+              const float p = __builtin_amdgcn_exp2f(fmaf(s[kb2][i], scale_log2, neg_m));
+              s[kb2][i] = p;
+              rs2[i & 3] += p;
+            }
+        }
+        float rs = (rs2[0] + rs2[1]) + (rs2[2] + rs2[3]);
+        rs += __shfl_xor(rs, 32, 64);
+        if (__any(m_new != m_run)) {  // the running max moved for some query of the wave
+          const float alpha = __builtin_amdgcn_exp2f(m_run - m_new);
+          l_run *= alpha;
+  #pragma unroll
+          for (int dt = 0; dt < DT; ++dt)
+  #pragma unroll
+            for (int i = 0; i < 16; ++i) acc_o[dt][i] *= alpha;
+        }
+        l_run += rs;
+        m_run = m_new;
+        // ---- P fragments: k-step k4 = kb2*2 + sidx uses registers 8*sidx .. +7 of s[kb2] ----
+        bf16x8 pf[4];
+  #pragma unroll
+        for (int kb2 = 0; kb2 < 2; ++kb2)
+  #pragma unroll
+          for (int sidx = 0; sidx < 2; ++sidx) {
+            u32x4 pk;
+  #pragma unroll
+            for (int j = 0; j < 4; ++j) pk[j] = cvt_pk_bf16(s[kb2][8 * sidx + 2 * j], s[kb2][8 * sidx + 2 * j + 1]);
+            pf[kb2 * 2 + sidx] = __builtin_bit_cast(bf16x8, pk);
+          }
+        // ---- O^T += V^T . P^T ----
+        const int g1 = (lane >> 4) & 1, qq = (lane & 15) >> 2, p4 = lane & 3;
+#pragma unroll
+        for (int dt = 0; dt < DT; ++dt) {
+          const int ch = 4 * dt + 2 * g1 + (p4 >> 1);
+          const int sub = (p4 & 1) * 8;
+          if constexpr (DMA) {
+            // the transposing reads as inline asm: the builtin's memory operand carries no type info, so
+            // hipcc's waitcnt pass would make it wait for every LDS-DMA tile in flight (vmcnt(0)); asm
+            // reads are invisible to that pass, hence the explicit wait, which takes the eight registers
+            // through it so that no MFMA is scheduled above it
+            s16x4 lo[4], hi[4];
+#pragma unroll
+            for (int k4 = 0; k4 < 4; ++k4) {
+              const int row0 = k4 * 16 + 4 * hh + qq;
+              const uint32_t alo = static_cast<uint32_t>(reinterpret_cast<uintptr_t>(vb + v_swz(row0, ch) + sub));
+              const uint32_t ahi = static_cast<uint32_t>(reinterpret_cast<uintptr_t>(vb + v_swz(row0 + 8, ch) + sub));
+              asm volatile("ds_read_b64_tr_b16 %0, %1" : "=v"(lo[k4]) : "v"(alo));
+              asm volatile("ds_read_b64_tr_b16 %0, %1" : "=v"(hi[k4]) : "v"(ahi));
+            }
+            asm volatile("s_waitcnt lgkmcnt(0)"
+                         : "+v"(lo[0]), "+v"(hi[0]), "+v"(lo[1]), "+v"(hi[1]), "+v"(lo[2]), "+v"(hi[2]), "+v"(lo[3]),
+                           "+v"(hi[3]));
+#pragma unroll
+            for (int k4 = 0; k4 < 4; ++k4) {
+              bf16x8 a;
+              a[0] = lo[k4][0]; a[1] = lo[k4][1]; a[2] = lo[k4][2]; a[3] = lo[k4][3];
+              a[4] = hi[k4][0]; a[5] = hi[k4][1]; a[6] = hi[k4][2]; a[7] = hi[k4][3];
+              acc_o[dt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, pf[k4], acc_o[dt], 0, 0, 0);
+            }
+          } else {
+#pragma unroll
+            for (int k4 = 0; k4 < 4; ++k4) {
+              const int row0 = k4 * 16 + 4 * hh + qq;
+              const s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(vb + v_swz(row0, ch) + sub));
+              const s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(vb + v_swz(row0 + 8, ch) + sub));
+              bf16x8 a;
+              a[0] = lo[0]; a[1] = lo[1]; a[2] = lo[2]; a[3] = lo[3];
+              a[4] = hi[0]; a[5] = hi[1]; a[6] = hi[2]; a[7] = hi[3];
+              acc_o[dt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, pf[k4], acc_o[dt], 0, 0, 0);
+            }
+          }
+        }
+      }
+  };
+
+  if constexpr (DMA) {
+    // LDS-DMA staging (buffer_load ... lds): the tile's K / V land in LDS without a VGPR round trip,
+    // so the lookahead is bounded by LDS (kDmaSlots tiles), not by staging registers. The LDS
+    // image is lane-linear (instruction u of wave w writes bytes (u NT + 64 w + lane) x 16), so each
+    // lane loads the source chunk that k_swz / v_swz put at its position: the XOR swizzle inverted
+    // on the source side (rows of 256 B = 16 chunks). One counted wait + one barrier per tile.
+    static_assert(NL == 2, "DMA staging: 2 instructions per lane per tensor");
+    uint32_t dk[2], dv[2];  // fixed size: a template-dependent operand type drops the host stub
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const int idx = u * NT + tid, row = idx >> 4, pc = idx & 15;
+      dk[u] = static_cast<uint32_t>(row * kRowBytes + ((pc ^ (row & 15)) << 4));
+      dv[u] = static_cast<uint32_t>(row * kRowBytes + ((pc ^ ((row & 3) << 2)) << 4));
+    }
+    auto issue_dma = [&](int t) {
+      const int tu = __builtin_amdgcn_readfirstlane(t);
+      const int64_t base = (static_cast<int64_t>(ld_scalar(bt + tu)) * nkv + kvh) * head_stride;
+      const int bytes = min(kKT, ctx - tu * kKT) * D * 2;  // rows past ctx - 1 land as zeros
+      const __amdgpu_buffer_rsrc_t rk = __builtin_amdgcn_make_buffer_rsrc((void*)(k_cache + base), 0, bytes, 0x00020000);
+      const __amdgpu_buffer_rsrc_t rv = __builtin_amdgcn_make_buffer_rsrc((void*)(v_cache + base), 0, bytes, 0x00020000);
+      char* sk = smem + (tu % kDmaSlots) * 2 * kTileBytes + wave * 1024;
+#pragma unroll
+      for (int u = 0; u < 2; ++u) {
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(rk, (__attribute__((address_space(3))) void*)(sk + u * 8192), 16, dk[u], 0, 0, 0);
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(rv, (__attribute__((address_space(3))) void*)(sk + kTileBytes + u * 8192), 16,
+                                                 dv[u], 0, 0, 0);
+      }
+    };
+#pragma unroll
+    for (int j = 0; j < kDmaSlots - 1; ++j)
+      if (t_lo + j < ntiles) issue_dma(t_lo + j);
+    for (int t = t_lo; t < ntiles; ++t) {
+      // tile t landed (this wave's 4 loads of it; the next tiles' may stay in flight), then the
+      // barrier: every wave's tile t landed and every wave finished reading slot (t - 1) % slots
+      const int ahead = min(ntiles - 1 - t, kDmaSlots - 2);
+      if (ahead >= 2) {
+        asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+      } else if (ahead == 1) {
+        asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+      } else {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      }
+      // a bare s_barrier: __syncthreads()'s fence would drain every tile in flight (vmcnt(0))
+      __builtin_amdgcn_sched_barrier(0);
+      asm volatile("s_barrier" ::: "memory");
+      __builtin_amdgcn_sched_barrier(0);
+      if (t + kDmaSlots - 1 < ntiles) issue_dma(t + kDmaSlots - 1);  // into the slot just retired
+      const char* kb = smem + (t % kDmaSlots) * 2 * kTileBytes;
+      tile_compute(t, kb, kb + kTileBytes);
+    }
+  } else {
   if (t_lo < ntiles) {
     issue(t_lo, 0);
 #pragma unroll
@@ -226,116 +419,10 @@ __global__ __launch_bounds__(WPB * 64, 8 / WPB) void attn_prefill_kernel(
     const int buf = t & 1;
     // the set tile t was staged in (j) is free again (committed): tile t + LA goes into it
     if (t + LA < ntiles) issue(t + LA, j);
-    const int kt = t * kKT;
-    if (wvalid && kt < wave_kend) {
-      const char* kb = smem + buf * 2 * kTileBytes;
-      const char* vb = kb + kTileBytes;
-      // ---- S^T = K . Q^T for two 32-key halves ----
-      f32x16 s[2];
-#pragma unroll
-      for (int kb2 = 0; kb2 < 2; ++kb2) {
-#pragma unroll
-        for (int i = 0; i < 16; ++i) s[kb2][i] = 0.f;
-        const int row = kb2 * 32 + r;
-#pragma unroll
-        for (int ks = 0; ks < KS; ++ks) {
-          const bf16x8 a = *reinterpret_cast<const bf16x8*>(kb + k_swz(row, 2 * ks + hh));
-          s[kb2] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, qf[ks], s[kb2], 0, 0, 0);
-        }
-      }
-      // ---- online softmax (lane owns query qpos; keys in registers) ----
-      // VALU diet (the loop is VALU-bound at 2 waves/SIMD, ~2x the MFMA cycles before it): the
-      // max on raw scores (scale > 0), then ONE fma + exp per score; causal masking only on the
-      // tiles that reach past the wave's first query position; the running max moves only when a
-      // new score exceeds it by > kSlack (log2 units, so P <= 2^kSlack: exact in f32, same bf16
-      // relative rounding), which leaves the O rescale out of almost every tile; P packed by
-      // v_cvt_pk_bf16_f32 (two floats per instruction, RNE).
-      const bool diag = kt + kKT - 1 > wave_qpos0;  // wave-uniform
-      float mx = -1e30f;
-      // diag: score (kb2, i) is key kt + 4 hh + kb2*32 + (i & 3) + 8 (i >> 2): visible iff that
-      // compile-time offset <= lim (an inline-constant compare, no per-score add)
-      const int lim = qpos - kt - 4 * hh;
-      if (diag) {
-#pragma unroll
-        for (int kb2 = 0; kb2 < 2; ++kb2)
-#pragma unroll
-          for (int i = 0; i < 16; ++i)
-            mx = fmaxf(mx, kb2 * 32 + (i & 3) + 8 * (i >> 2) <= lim ? s[kb2][i] : -1e30f);
-      } else {
-#pragma unroll
-        for (int kb2 = 0; kb2 < 2; ++kb2)
-#pragma unroll
-          for (int i = 0; i < 16; ++i) mx = fmaxf(mx, s[kb2][i]);
-      }
-      mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
-      const float mx_s = mx * scale_log2;
-      const float m_new = mx_s > m_run + kSlack ? mx_s : m_run;
-      const float neg_m = -m_new;
-      float rs2[4] = {0.f, 0.f, 0.f, 0.f};
-      if (diag) {
-#pragma unroll
-        for (int kb2 = 0; kb2 < 2; ++kb2)
-#pragma unroll
-          for (int i = 0; i < 16; ++i) {
-            const float p = kb2 * 32 + (i & 3) + 8 * (i >> 2) <= lim
-                                ? __builtin_amdgcn_exp2f(fmaf(s[kb2][i], scale_log2, neg_m))
-                                : 0.f;
-            s[kb2][i] = p;
-            rs2[i & 3] += p;
-          }
-      } else {
-#pragma unroll
-        for (int kb2 = 0; kb2 < 2; ++kb2)
-#pragma unroll
-          for (int i = 0; i < 16; ++i) {
-            const float p = __builtin_amdgcn_exp2f(fmaf(s[kb2][i], scale_log2, neg_m));
-            s[kb2][i] = p;
-            rs2[i & 3] += p;
-          }
-      }
-      float rs = (rs2[0] + rs2[1]) + (rs2[2] + rs2[3]);
-      rs += __shfl_xor(rs, 32, 64);
-      if (__any(m_new != m_run)) {  // the running max moved for some query of the wave
-        const float alpha = __builtin_amdgcn_exp2f(m_run - m_new);
-        l_run *= alpha;
-#pragma unroll
-        for (int dt = 0; dt < DT; ++dt)
-#pragma unroll
-          for (int i = 0; i < 16; ++i) acc_o[dt][i] *= alpha;
-      }
-      l_run += rs;
-      m_run = m_new;
-      // ---- P fragments: k-step k4 = kb2*2 + sidx uses registers 8*sidx .. +7 of s[kb2] ----
-      bf16x8 pf[4];
-#pragma unroll
-      for (int kb2 = 0; kb2 < 2; ++kb2)
-#pragma unroll
-        for (int sidx = 0; sidx < 2; ++sidx) {
-          u32x4 pk;
-#pragma unroll
-          for (int j = 0; j < 4; ++j) pk[j] = cvt_pk_bf16(s[kb2][8 * sidx + 2 * j], s[kb2][8 * sidx + 2 * j + 1]);
-          pf[kb2 * 2 + sidx] = __builtin_bit_cast(bf16x8, pk);
-        }
-      // ---- O^T += V^T . P^T ----
-      const int g1 = (lane >> 4) & 1, qq = (lane & 15) >> 2, p4 = lane & 3;
-#pragma unroll
-      for (int dt = 0; dt < DT; ++dt) {
-        const int ch = 4 * dt + 2 * g1 + (p4 >> 1);
-        const int sub = (p4 & 1) * 8;
-#pragma unroll
-        for (int k4 = 0; k4 < 4; ++k4) {
-          const int row0 = k4 * 16 + 4 * hh + qq;
-          const s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(vb + v_swz(row0, ch) + sub));
-          const s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(vb + v_swz(row0 + 8, ch) + sub));
-          bf16x8 a;
-          a[0] = lo[0]; a[1] = lo[1]; a[2] = lo[2]; a[3] = lo[3];
-          a[4] = hi[0]; a[5] = hi[1]; a[6] = hi[2]; a[7] = hi[3];
-          acc_o[dt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, pf[k4], acc_o[dt], 0, 0, 0);
-        }
-      }
-    }
+    tile_compute(t, smem + buf * 2 * kTileBytes, smem + buf * 2 * kTileBytes + kTileBytes);
     if (t + 1 < ntiles) commit(buf ^ 1, (j + 1) % LA);
     __syncthreads();
+  }
   }
   }
 
@@ -375,7 +462,7 @@ __global__ __launch_bounds__(WPB * 64, 8 / WPB) void attn_prefill_kernel(
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every storing wave: its partial is out
     __syncthreads();
-    __shared__ int is_last;
+    int& is_last = *reinterpret_cast<int*>(smem + kSmemMain);
     if (tid == 0) {
       int* ctr = counters + (static_cast<int64_t>(b) * ngrp + grp) * nkv + kvh;
       is_last = __hip_atomic_fetch_add(ctr, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == nsplit - 1;
@@ -546,6 +633,13 @@ extern "C" int llmc_attn_prefill(const void* q, int q_stride, const void* k_cach
   if (form_env >= 0 && form_env <= 2 && ksplit == 1) form = form_env;
   if (form == 1 && (G > 4 || 8 % G != 0)) form = 0;  // pairs need WPB / G >= 2 row tiles
   const int wpb = form == 2 ? 4 : 8, pair = form == 1 ? 1 : 0;
+  static const int dma_env = [] {
+    // LDS-DMA K/V staging (64-key pages, D = 128, 8-wave blocks): 2-5 % faster on every measured
+    // shape (2k 65.8 -> 62.5 us, 8k 601 -> 587, 32k keys 3893 -> 3831; profiles/r5_prefill_attention.md)
+    const char* e = getenv("LLMC_PREFILL_DMA");  // A/B runs: 0 = register staging
+    return e ? atoi(e) : 1;
+  }();
+  const bool dma = dma_env && wpb == 8 && D == 128 && bs == kKT;
   dim3 grid((G * npb + wpb - 1) / wpb * ksplit * nkv, 1, B);
   const float sl2 = scale * 1.4426950408889634f;
   static const int la = [] {
@@ -573,6 +667,13 @@ extern "C" int llmc_attn_prefill(const void* q, int q_stride, const void* k_cach
     if (la >= 2 && wpb == 8) LLMC_PF(DD, 2);   \
     else LLMC_PF(DD, 1);                       \
   } while (0)
+  if (dma) {
+    attn_prefill_kernel<128, 8, 1, true, true><<<grid, 512, 0, s>>>(
+        (const bf16_t*)q, q_stride, (const bf16_t*)k_cache, (const bf16_t*)v_cache, (const int32_t*)block_tables,
+        bt_stride, (const int32_t*)q_start, (const int32_t*)q_lens, (const int32_t*)ctx_lens, (bf16_t*)out, out_stride,
+        nh, nkv, bs, sl2, ksplit, kmin, (float*)part, (int*)counters, T_all, pair);
+    return static_cast<int>(hipGetLastError());
+  }
   switch (D) {
     case 64: LLMC_PF_D(64); break;
     case 96: LLMC_PF_D(96); break;

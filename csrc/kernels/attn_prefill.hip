@@ -618,7 +618,7 @@ extern "C" int llmc_attn_prefill(const void* q, int q_stride, const void* k_cach
                                  const void* block_tables, int bt_stride, const void* q_start, const void* q_lens,
                                  const void* ctx_lens, void* out, int out_stride, int B, int max_qlen, int nh, int nkv,
                                  int D, int bs, float scale, int ksplit, int kmin, void* part, void* counters,
-                                 int T_all, hipStream_t s) {
+                                 int T_all, int form_arg, hipStream_t s) {
   if (nh % nkv != 0 || ksplit < 1 || ksplit > kMaxSplit ||
       (ksplit > 1 && (part == nullptr || counters == nullptr || T_all < 1 || kmin < 1)))
     return -1;
@@ -629,8 +629,10 @@ extern "C" int llmc_attn_prefill(const void* q, int q_stride, const void* k_cach
     const char* e = getenv("LLMC_PREFILL_FORM");  // A/B runs: force form 0 / 1 / 2 (unsplit grids)
     return e ? atoi(e) : -1;
   }();
+  // form_arg: -1 = llmc_attn_prefill_form's choice, 0 / 1 / 2 forced (tests; unsplit grids only)
   int form = llmc_attn_prefill_form(B, max_qlen, nh, nkv, ksplit);
   if (form_env >= 0 && form_env <= 2 && ksplit == 1) form = form_env;
+  if (form_arg >= 0 && form_arg <= 2 && ksplit == 1) form = form_arg;
   if (form == 1 && (G > 4 || 8 % G != 0)) form = 0;  // pairs need WPB / G >= 2 row tiles
   const int wpb = form == 2 ? 4 : 8, pair = form == 1 ? 1 : 0;
   static const int dma_env = [] {

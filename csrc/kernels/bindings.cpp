@@ -46,7 +46,7 @@ int llmc_gemv_qkv_rope(int, const void*, int, const void*, float, const void*, i
                        const void*, const void*, const void*, const void*, int, int, int, int, int, hipStream_t);
 int llmc_attn_prefill(const void*, int, const void*, const void*, const void*, int, const void*, const void*,
                       const void*, void*, int, int, int, int, int, int, int, float, int, int, void*, void*, int,
-                      hipStream_t);
+                      int, hipStream_t);
 int llmc_attn_prefill_form(int, int, int, int, int);
 int llmc_attn_prefill_plan(int, int, int, int, int, int*);
 int llmc_sample(const void*, int64_t, int, int, const void*, const void*, const void*, const void*, const void*, void*,
@@ -180,9 +180,9 @@ PYBIND11_MODULE(_llmc_hip, m) {
   });
   m.def("attn_prefill", [](ptr q, int qs, ptr kc, ptr vc, ptr bt, int bts, ptr qst, ptr ql, ptr cl, ptr out, int os,
                            int B, int max_qlen, int nh, int nkv, int D, int bs, float scale, int ksplit, int kmin,
-                           ptr part, ptr counters, int T, ptr s) {
+                           ptr part, ptr counters, int T, int form, ptr s) {
     check(llmc_attn_prefill(P(q), qs, P(kc), P(vc), P(bt), bts, P(qst), P(ql), P(cl), P(out), os, B, max_qlen, nh, nkv,
-                            D, bs, scale, ksplit, kmin, P(part), P(counters), T, S(s)),
+                            D, bs, scale, ksplit, kmin, P(part), P(counters), T, form, S(s)),
           "attn_prefill");
   });
   m.def("attn_prefill_form", [](int B, int T, int nh, int nkv, int ksplit) { return llmc_attn_prefill_form(B, T, nh, nkv, ksplit); });

@@ -418,10 +418,12 @@ def attn_prefill_workspace(ksplit, T, nh, D, device, B=1, nkv=1, max_qlen=None):
 
 
 def attn_prefill(q, k_cache, v_cache, block_tables, q_start, q_lens, ctx_lens, out, max_qlen, nh, nkv, D, bs, scale,
-                 max_ctx=None, ksplit=None, kmin=None, ws=None):
+                 max_ctx=None, ksplit=None, kmin=None, ws=None, form=None):
     """Causal paged prefill attention. ``max_ctx`` (default ``max_qlen``) feeds the KV-split plan;
     ``ksplit``/``kmin`` override it; ``ws`` is a caller-held attn_prefill_workspace reused across
-    layers (it must not be shared by launches that can run concurrently)."""
+    layers (it must not be shared by launches that can run concurrently); ``form`` forces the block
+    form of an unsplit launch (0 = 8 waves, 1 = paired row tiles, 2 = 4 waves; default: the
+    kernel library's choice, ``kernels().attn_prefill_form``)."""
     if not q.is_cuda:
         return oracle.attn_prefill(q, k_cache, v_cache, block_tables, q_start, q_lens, ctx_lens, nh, nkv, D, bs,
                                    scale, out)
@@ -437,7 +439,7 @@ def attn_prefill(q, k_cache, v_cache, block_tables, q_start, q_lens, ctx_lens, o
         part, ctr = _p(ws[0]), _p(ws[1])
     kernels().attn_prefill(_p(q), q.stride(0), _p(k_cache), _p(v_cache), _p(block_tables), block_tables.stride(0),
                            _p(q_start), _p(q_lens), _p(ctx_lens), _p(out), out.stride(0), B, int(max_qlen), nh, nkv,
-                           D, bs, float(scale), k, km, part, ctr, T, _s(q))
+                           D, bs, float(scale), k, km, part, ctr, T, -1 if form is None else int(form), _s(q))
     return out
 
 

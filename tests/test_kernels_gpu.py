@@ -549,6 +549,32 @@ def test_attn_prefill_long_context_vs_fp32(cuda, nh, nkv, D, ctx, ksplit):
     close(out, ref.float().cpu(), 2e-2)
 
 
+@pytest.mark.parametrize("nh,nkv,D,qlens", [(32, 8, 128, [2048]), (32, 8, 128, [1000, 700]), (32, 32, 96, [1024]),
+                                          (16, 2, 128, [1500]), (8, 1, 128, [640, 130])])
+@pytest.mark.parametrize("form", [0, 1, 2])
+def test_attn_prefill_block_forms_vs_fp32(cuda, nh, nkv, D, qlens, form):
+    """Every block form of the unsplit prefill forced on the same problems against the fp32 oracle:
+    8-wave blocks (LDS-DMA staging for D = 128 on 64-key pages, register staging for D = 96), paired
+    late / early row tiles (G <= 4; G = 8 falls back to 8 waves) and 4-wave blocks; full and ragged
+    sequences, a short second sequence beside a long one."""
+    torch.manual_seed(sum(qlens) + D + form)
+    bs = 64
+    B = len(qlens)
+    kc, vc, bt = _paged_kv(B, max(qlens), nkv, D, bs)
+    qs = torch.tensor([sum(qlens[:i]) for i in range(B)], dtype=torch.int32)
+    T = sum(qlens)
+    q = rnd(T, nh * D)
+    out = torch.zeros(T, nh * D, dtype=BF, device="cuda")
+    ql = torch.tensor(qlens, dtype=torch.int32)
+    scale = 1 / math.sqrt(D)
+    ops.attn_prefill(q, kc, vc, bt.cuda(), qs.cuda(), ql.cuda(), ql.cuda(), out, max(qlens), nh, nkv, D, bs, scale,
+                     ksplit=1, form=form)
+    ref = torch.zeros(T, nh * D, dtype=BF, device="cuda")
+    oracle.attn_prefill(q, kc, vc, bt.cuda(), qs, ql, ql, nh, nkv, D, bs, scale, ref)
+    torch.cuda.synchronize()
+    close(out, ref.float().cpu(), 2e-2)
+
+
 def _sample_bufs(B, V):
     P = ops.sample_parts()
     return (torch.empty(B, P, device="cuda"), torch.empty(B, P, dtype=torch.int32, device="cuda"),

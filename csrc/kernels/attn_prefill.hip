@@ -64,7 +64,7 @@ __global__ __launch_bounds__(WPB * 64, 8 / WPB) void attn_prefill_kernel(
     const int32_t* __restrict__ block_tables, int bt_stride, const int32_t* __restrict__ q_start,
     const int32_t* __restrict__ q_lens, const int32_t* __restrict__ ctx_lens, bf16_t* __restrict__ out,
     int out_stride, int nh, int nkv, int bs, float scale_log2, int ksplit, int kmin, float* __restrict__ part,
-    int* __restrict__ counters, int T_all, int pair) {
+    int* __restrict__ counters, int T_all, int mode) {
   constexpr int CH = D / 8;            // 16-B chunks per row
   constexpr int NT = WPB * 64;
   constexpr int NL = (kKT * CH + NT - 1) / NT;  // staging chunks per thread per tensor
@@ -93,7 +93,11 @@ __global__ __launch_bounds__(WPB * 64, 8 / WPB) void attn_prefill_kernel(
   const int q0 = q_start[b];
   const int npb = (qlen + 31) / 32;
   const int nrt = G * npb;
-  const int rt_base = (ngrp - 1 - grp) * WPB;
+  // mode: 0 = WPB row tiles per block, 1 = paired late / early row tiles, 2 = key halves (DMA
+  // staging only): WPB / 2 row tiles, waves [0, WPB / 2) on the first half of their key tiles and
+  // waves [WPB / 2, WPB) on the second half, merged through LDS at the end
+  const bool pair = mode == 1, halves = DMA && mode == 2;
+  const int rt_base = (ngrp - 1 - grp) * (halves ? WPB / 2 : WPB);
   if (!pair && rt_base >= nrt) return;  // block-uniform
 
   // wave index through readfirstlane: everything derived from it (row tile, head, descriptors)
@@ -106,7 +110,8 @@ __global__ __launch_bounds__(WPB * 64, 8 / WPB) void attn_prefill_kernel(
   // one's, so the block stages the late tiles' keys once for both, and every SIMD holds one late
   // and one early wave: ~npb + 1 tile steps per SIMD in every block instead of 2 x the block's
   // latest tile, whose longest block set the critical path of one-round grids.
-  int rt = rt_base + wave;
+  const int khalf = halves ? wave / (WPB / 2) : 0;  // halves: which half of the key tiles
+  int rt = rt_base + (halves ? wave % (WPB / 2) : wave);
   bool wvalid = rt < nrt;
   if (pair) {
     const int R = WPB / G, half = R / 2, slot = wave / G, top = ngrp * half;
@@ -121,7 +126,7 @@ __global__ __launch_bounds__(WPB * 64, 8 / WPB) void attn_prefill_kernel(
   const int row_i = pb * 32 + r;                  // query row within the sequence chunk
   const int qi = min(row_i, qlen - 1);
   const int qpos = first_pos + qi;                 // absolute position (causal limit)
-  const int last_rt = min(rt_base + WPB - 1, nrt - 1);
+  const int last_rt = min(rt_base + (halves ? WPB / 2 : WPB) - 1, nrt - 1);
   const int pb_last = pair ? max(npb - 1 - grp * (WPB / G / 2), 0) : last_rt / G;
   const int kend = min(ctx, first_pos + min(pb_last * 32 + 31, qlen - 1) + 1);
   const int ntiles_all = (kend + kKT - 1) / kKT;
@@ -363,13 +368,13 @@ __global__ __launch_bounds__(WPB * 64, 8 / WPB) void attn_prefill_kernel(
       dk[u] = static_cast<uint32_t>(row * kRowBytes + ((pc ^ (row & 15)) << 4));
       dv[u] = static_cast<uint32_t>(row * kRowBytes + ((pc ^ ((row & 3) << 2)) << 4));
     }
-    auto issue_dma = [&](int t) {
+    auto issue_dma = [&](int t, int slot) {
       const int tu = __builtin_amdgcn_readfirstlane(t);
       const int64_t base = (static_cast<int64_t>(ld_scalar(bt + tu)) * nkv + kvh) * head_stride;
       const int bytes = min(kKT, ctx - tu * kKT) * D * 2;  // rows past ctx - 1 land as zeros
       const __amdgpu_buffer_rsrc_t rk = __builtin_amdgcn_make_buffer_rsrc((void*)(k_cache + base), 0, bytes, 0x00020000);
       const __amdgpu_buffer_rsrc_t rv = __builtin_amdgcn_make_buffer_rsrc((void*)(v_cache + base), 0, bytes, 0x00020000);
-      char* sk = smem + (tu % kDmaSlots) * 2 * kTileBytes + wave * 1024;
+      char* sk = smem + slot * 2 * kTileBytes + wave * 1024;
 #pragma unroll
       for (int u = 0; u < 2; ++u) {
         __builtin_amdgcn_raw_ptr_buffer_load_lds(rk, (__attribute__((address_space(3))) void*)(sk + u * 8192), 16, dk[u], 0, 0, 0);
@@ -377,9 +382,30 @@ __global__ __launch_bounds__(WPB * 64, 8 / WPB) void attn_prefill_kernel(
                                                  dv[u], 0, 0, 0);
       }
     };
+    if (halves) {
+      // key halves: step s stages tile s of the first half (slot 2 (s & 1)) and tile t_mid + s of
+      // the second (slot 2 (s & 1) + 1); step s + 1 is fetched into the slots of step s - 1 right
+      // after the barrier that retires them, so it lands while step s computes
+      const int t_mid = (ntiles + 1) / 2;  // unsplit: t_lo = 0
+      auto issue_step = [&](int st) {
+        issue_dma(st, 2 * (st & 1));
+        if (t_mid + st < ntiles) issue_dma(t_mid + st, 2 * (st & 1) + 1);
+      };
+      issue_step(0);
+      for (int st = 0; st < t_mid; ++st) {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // step st (the only one in flight)
+        __builtin_amdgcn_sched_barrier(0);
+        asm volatile("s_barrier" ::: "memory");
+        __builtin_amdgcn_sched_barrier(0);
+        if (st + 1 < t_mid) issue_step(st + 1);
+        const int t = khalf ? t_mid + st : st;
+        const char* kb = smem + (2 * (st & 1) + khalf) * 2 * kTileBytes;
+        if (t < (khalf ? ntiles : t_mid)) tile_compute(t, kb, kb + kTileBytes);
+      }
+    } else {
 #pragma unroll
     for (int j = 0; j < kDmaSlots - 1; ++j)
-      if (t_lo + j < ntiles) issue_dma(t_lo + j);
+      if (t_lo + j < ntiles) issue_dma(t_lo + j, (t_lo + j) % kDmaSlots);
     for (int t = t_lo; t < ntiles; ++t) {
       // tile t landed (this wave's 4 loads of it; the next tiles' may stay in flight), then the
       // barrier: every wave's tile t landed and every wave finished reading slot (t - 1) % slots
@@ -395,9 +421,10 @@ __global__ __launch_bounds__(WPB * 64, 8 / WPB) void attn_prefill_kernel(
       __builtin_amdgcn_sched_barrier(0);
       asm volatile("s_barrier" ::: "memory");
       __builtin_amdgcn_sched_barrier(0);
-      if (t + kDmaSlots - 1 < ntiles) issue_dma(t + kDmaSlots - 1);  // into the slot just retired
+      if (t + kDmaSlots - 1 < ntiles) issue_dma(t + kDmaSlots - 1, (t + kDmaSlots - 1) % kDmaSlots);  // the slot just retired
       const char* kb = smem + (t % kDmaSlots) * 2 * kTileBytes;
       tile_compute(t, kb, kb + kTileBytes);
+    }
     }
   } else {
   if (t_lo < ntiles) {
@@ -426,6 +453,34 @@ __global__ __launch_bounds__(WPB * 64, 8 / WPB) void attn_prefill_kernel(
   }
   }
 
+  if (halves) {
+    // the second half's waves hand (O, m, l) to the first half's (same rows and head: wave - WPB / 2)
+    // through LDS (the drained staging ring: [WPB / 2 waves][DT x 16 + 2][64 lanes] floats, lane
+    // innermost so that every access is one float per lane, conflict-free)
+    constexpr int NV = DT * 16 + 2;
+    static_assert(!DMA || (WPB / 2) * NV * 64 * 4 <= kSmemMain, "halves hand-off fits the ring");
+    float* xo = reinterpret_cast<float*>(smem) + (wave % (WPB / 2)) * NV * 64 + lane;
+    __syncthreads();  // every wave past its last tile read
+    if (khalf) {
+#pragma unroll
+      for (int dt = 0; dt < DT; ++dt)
+#pragma unroll
+        for (int i = 0; i < 16; ++i) xo[(dt * 16 + i) * 64] = acc_o[dt][i];
+      xo[(DT * 16) * 64] = m_run;
+      xo[(DT * 16 + 1) * 64] = l_run;
+    }
+    __syncthreads();
+    if (khalf) return;  // after the block's last barrier
+    const float m1 = xo[(DT * 16) * 64], l1 = xo[(DT * 16 + 1) * 64];
+    const float M = fmaxf(m_run, m1);
+    const float a0 = l_run > 0.f ? __builtin_amdgcn_exp2f(m_run - M) : 0.f;
+    const float a1 = l1 > 0.f ? __builtin_amdgcn_exp2f(m1 - M) : 0.f;
+#pragma unroll
+    for (int dt = 0; dt < DT; ++dt)
+#pragma unroll
+      for (int i = 0; i < 16; ++i) acc_o[dt][i] = fmaf(xo[(dt * 16 + i) * 64], a1, acc_o[dt][i] * a0);
+    l_run = fmaf(l1, a1, l_run * a0);
+  }
   const bool live = wvalid && row_i < qlen;
   if (nsplit > 1) {
     // split hand-off: every split writes (unnormalised O, m, l) in f32, the last to arrive merges
@@ -536,7 +591,7 @@ using namespace llmc;
 // the (ksplit, kmin) pair with the shortest greedy makespan wins: groups with >= 2 kmin tiles are
 // split into min(ksplit, tiles / kmin) blocks. Costs in tile units (below). Assumes B sequences of
 // the max shape.
-extern "C" int llmc_attn_prefill_plan(int B, int max_qlen, int max_ctx, int nh, int nkv, int* kmin_out) {
+extern "C" int llmc_attn_prefill_plan(int B, int max_qlen, int max_ctx, int nh, int nkv, int D, int bs, int* kmin_out) {
   *kmin_out = 1 << 30;
   if (nkv <= 0 || nh % nkv != 0 || max_qlen <= 0 || max_ctx < max_qlen) return 1;
   const int G = nh / nkv, npb = (max_qlen + 31) / 32, ngrp = (G * npb + 7) / 8, rows_pg = 8 / G > 0 ? 8 / G : 1;
@@ -574,9 +629,12 @@ extern "C" int llmc_attn_prefill_plan(int B, int max_qlen, int max_ctx, int nh, 
     return end;
   };
   int best_s = 1, best_k = 1 << 30;
-  // a split must win by > 3%; on a one-round grid by > 20%: the unsplit grid then runs the paired
-  // or 4-wave form (llmc_attn_prefill_form), ~0.83x of the 8-wave time this model prices
-  float best = makespan(1, 1 << 30) * (units <= 256 ? 0.80f : 0.97f);
+  // a split must win by > 3%; on a one-round grid by more: the unsplit grid then runs the key-halves
+  // form (~0.6-0.7x of the 8-wave time this model prices; D = 128 on 64-key pages) or the paired /
+  // 4-wave form (~0.83x) (llmc_attn_prefill_form). Measured: 4 / 1 heads at 8k keys still split
+  // (model 0.52: 134-142 us vs halves 157); at 2k (0.72), 4k (0.68), 8 / 1 at 8k (0.71) halves wins.
+  const bool halves_ok = D == 128 && bs == kKT;
+  float best = makespan(1, 1 << 30) * (units <= 256 ? (halves_ok ? 0.62f : 0.80f) : 0.97f);
   // 4-way splits measured a loss everywhere but on grids of <= 128 blocks with >= 2 row tiles per
   // group (a TP=8 rank's single kv head) at >= 8k keys or on the smallest grids; the cost model
   // alone over-rates them elsewhere (8 / 2 heads at 4k keys: 0.56x predicted, 0.94x measured)
@@ -592,26 +650,31 @@ extern "C" int llmc_attn_prefill_plan(int B, int max_qlen, int max_ctx, int nh, 
 }
 
 // Block form of a prefill launch: 0 = 8 waves (2 row tiles x 4 heads of one kv head share every
-// staged K/V tile; one block per CU at 247 VGPRs), 1 = 8 waves with paired row tiles (a late and an
-// early one per SIMD: `pair` in the kernel), 2 = 4 waves, two blocks per CU (launch bound: <= 256
-// VGPRs, so the one-tile lookahead; two tiles spill). A split grid is form 0. On a grid of more
-// than one round of the chip the longest-first order balances already and form 0 stays (8k: 552
-// vs 587 us as 4-wave blocks, 630 paired); when the 8-wave grid is ONE round (<= 256 blocks) its
-// longest block (every key tile at 2 waves / SIMD) is the critical path, which forms 1 and 2
-// shorten. Measured (MI355X, unsplit, us; profiles/r5_prefill_attention.md):
-//   heads/kv  T      8 waves  paired  4 waves
-//   32/8     2048     76.6     63.2     69.2     (256 blocks: paired)
-//   32/32    2048     69.9     58.1     63.3
-//   32/8     1024     39.5     33.0     32.4     (128 blocks: 4 waves)
-//   32/32    1024     39.4     34.2     32.4
-//   16/2     2048     72.1      —       59.6     (G = 8: no pairs; 4 waves)
-//   16/2     4096    129.3      —      115.7
-extern "C" int llmc_attn_prefill_form(int B, int max_qlen, int nh, int nkv, int ksplit) {
+// staged K/V tile; one block per CU at 246 VGPRs), 1 = 8 waves with paired row tiles (a late and an
+// early one per SIMD: mode 1 in the kernel), 2 = 4 waves, two blocks per CU (launch bound: <= 256
+// VGPRs, so the one-tile lookahead; two tiles spill), 3 = key halves (8 waves = 4 row tiles x two
+// halves of their key tiles, two tiles staged per step by LDS-DMA, the halves merged through LDS:
+// mode 2; D = 128 on 64-key pages only). A split grid is form 0. On a grid of more than one round
+// of the chip the longest-first order balances already and form 0 stays; when the 8-wave grid is
+// ONE round (<= 256 blocks) its longest block (every key tile at 2 waves / SIMD) is the critical
+// path, which the other forms shorten. Measured (MI355X, unsplit, us; two boxes ~5 % apart;
+// profiles/r5_prefill_attention.md):
+//   heads/kv  T      8 waves  paired  4 waves  halves
+//   32/8     2048     76.6     58.5     69.2     61.8    (256 blocks, G <= 4: paired)
+//   32/32    2048     69.9     57.0     63.3     57.3
+//   32/8     1024     39.5     33.0     32.4     27.8    (<= 128 blocks: halves)
+//   32/32    1024     39.4     35.3     32.4     26.9
+//   16/2     2048     72.1      —       59.6     42.8    (G = 8: no pairs)
+//   16/2     4096    129.3      —      115.7     92.1    (256 blocks, G = 8: halves)
+//   32/8     8192     552      630      587      628     (4 rounds: 8 waves)
+extern "C" int llmc_attn_prefill_form(int B, int max_qlen, int nh, int nkv, int ksplit, int D, int bs) {
   if (nkv <= 0 || nh % nkv != 0 || ksplit > 1) return 0;
   const int G = nh / nkv, npb = (max_qlen + 31) / 32;
   const int64_t units8 = static_cast<int64_t>((G * npb + 7) / 8) * nkv * B;
   if (units8 > 256) return 0;
-  return G <= 4 && units8 > 128 ? 1 : 2;
+  const bool halves_ok = D == 128 && bs == kKT, pairs_ok = G <= 4 && 8 % G == 0;
+  if (units8 > 128 && pairs_ok) return 1;
+  return halves_ok ? 3 : 2;
 }
 
 extern "C" int llmc_attn_prefill(const void* q, int q_stride, const void* k_cache, const void* v_cache,
@@ -630,19 +693,20 @@ extern "C" int llmc_attn_prefill(const void* q, int q_stride, const void* k_cach
     return e ? atoi(e) : -1;
   }();
   // form_arg: -1 = llmc_attn_prefill_form's choice, 0 / 1 / 2 forced (tests; unsplit grids only)
-  int form = llmc_attn_prefill_form(B, max_qlen, nh, nkv, ksplit);
-  if (form_env >= 0 && form_env <= 2 && ksplit == 1) form = form_env;
-  if (form_arg >= 0 && form_arg <= 2 && ksplit == 1) form = form_arg;
+  int form = llmc_attn_prefill_form(B, max_qlen, nh, nkv, ksplit, D, bs);
+  if (form_env >= 0 && form_env <= 3 && ksplit == 1) form = form_env;
+  if (form_arg >= 0 && form_arg <= 3 && ksplit == 1) form = form_arg;
   if (form == 1 && (G > 4 || 8 % G != 0)) form = 0;  // pairs need WPB / G >= 2 row tiles
-  const int wpb = form == 2 ? 4 : 8, pair = form == 1 ? 1 : 0;
+  if (form == 3 && !(D == 128 && bs == kKT)) form = 2;  // key halves: LDS-DMA staging only
+  const int wpb = form == 2 ? 4 : 8, mode = form == 1 ? 1 : form == 3 ? 2 : 0;
   static const int dma_env = [] {
     // LDS-DMA K/V staging (64-key pages, D = 128, 8-wave blocks): 2-5 % faster on every measured
     // shape (2k 65.8 -> 62.5 us, 8k 601 -> 587, 32k keys 3893 -> 3831; profiles/r5_prefill_attention.md)
     const char* e = getenv("LLMC_PREFILL_DMA");  // A/B runs: 0 = register staging
     return e ? atoi(e) : 1;
   }();
-  const bool dma = dma_env && wpb == 8 && D == 128 && bs == kKT;
-  dim3 grid((G * npb + wpb - 1) / wpb * ksplit * nkv, 1, B);
+  const bool dma = (dma_env || mode == 2) && wpb == 8 && D == 128 && bs == kKT;
+  dim3 grid((G * npb + (mode == 2 ? 4 : wpb) - 1) / (mode == 2 ? 4 : wpb) * ksplit * nkv, 1, B);
   const float sl2 = scale * 1.4426950408889634f;
   static const int la = [] {
     const char* e = getenv("LLMC_PREFILL_LOOKAHEAD");  // A/B runs: K/V tiles requested ahead
@@ -658,7 +722,7 @@ extern "C" int llmc_attn_prefill(const void* q, int q_stride, const void* k_cach
                                                (const bf16_t*)v_cache, (const int32_t*)block_tables, bt_stride,   \
                                                (const int32_t*)q_start, (const int32_t*)q_lens,                  \
                                                (const int32_t*)ctx_lens, (bf16_t*)out, out_stride, nh, nkv, bs, sl2, \
-                                               ksplit, kmin, (float*)part, (int*)counters, T_all, pair)
+                                               ksplit, kmin, (float*)part, (int*)counters, T_all, mode)
 #define LLMC_PFP(DD, L, P)                         \
   do {                                             \
     if (L == 1 && wpb == 4) LLMC_PFW(DD, 1, P, 4); \
@@ -673,7 +737,7 @@ extern "C" int llmc_attn_prefill(const void* q, int q_stride, const void* k_cach
     attn_prefill_kernel<128, 8, 1, true, true><<<grid, 512, 0, s>>>(
         (const bf16_t*)q, q_stride, (const bf16_t*)k_cache, (const bf16_t*)v_cache, (const int32_t*)block_tables,
         bt_stride, (const int32_t*)q_start, (const int32_t*)q_lens, (const int32_t*)ctx_lens, (bf16_t*)out, out_stride,
-        nh, nkv, bs, sl2, ksplit, kmin, (float*)part, (int*)counters, T_all, pair);
+        nh, nkv, bs, sl2, ksplit, kmin, (float*)part, (int*)counters, T_all, mode);
     return static_cast<int>(hipGetLastError());
   }
   switch (D) {

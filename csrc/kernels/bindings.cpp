@@ -47,8 +47,8 @@ int llmc_gemv_qkv_rope(int, const void*, int, const void*, float, const void*, i
 int llmc_attn_prefill(const void*, int, const void*, const void*, const void*, int, const void*, const void*,
                       const void*, void*, int, int, int, int, int, int, int, float, int, int, void*, void*, int,
                       int, hipStream_t);
-int llmc_attn_prefill_form(int, int, int, int, int);
-int llmc_attn_prefill_plan(int, int, int, int, int, int*);
+int llmc_attn_prefill_form(int, int, int, int, int, int, int);
+int llmc_attn_prefill_plan(int, int, int, int, int, int, int, int*);
 int llmc_sample(const void*, int64_t, int, int, const void*, const void*, const void*, const void*, const void*, void*,
                 void*, void*, void*, void*, void*, const void*, int, int, void*, void*, int, int, hipStream_t);
 int llmc_sample_parts();
@@ -185,10 +185,12 @@ PYBIND11_MODULE(_llmc_hip, m) {
                             D, bs, scale, ksplit, kmin, P(part), P(counters), T, form, S(s)),
           "attn_prefill");
   });
-  m.def("attn_prefill_form", [](int B, int T, int nh, int nkv, int ksplit) { return llmc_attn_prefill_form(B, T, nh, nkv, ksplit); });
-  m.def("attn_prefill_plan", [](int B, int max_qlen, int max_ctx, int nh, int nkv) {
+  m.def("attn_prefill_form", [](int B, int T, int nh, int nkv, int ksplit, int D, int bs) {
+    return llmc_attn_prefill_form(B, T, nh, nkv, ksplit, D, bs);
+  });
+  m.def("attn_prefill_plan", [](int B, int max_qlen, int max_ctx, int nh, int nkv, int D, int bs) {
     int kmin = 0;
-    const int k = llmc_attn_prefill_plan(B, max_qlen, max_ctx, nh, nkv, &kmin);
+    const int k = llmc_attn_prefill_plan(B, max_qlen, max_ctx, nh, nkv, D, bs, &kmin);
     return std::make_pair(k, kmin);
   });
   m.def("sample", [](ptr logits, int64_t rs, int B, int V, ptr it, ptr tk, ptr tp, ptr seeds, ptr pos, ptr wv, ptr wi,

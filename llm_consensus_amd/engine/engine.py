@@ -439,8 +439,8 @@ class Engine:
         bt = self._block_table([s for s, _ in batch])
         max_qlen = max(q_lens)
         max_ctx = max(ctx_lens)
-        ksplit, kmin = (ops.attn_prefill_plan(len(batch), max_qlen, max_ctx, self.nh, self.nkv) if ids_d.is_cuda
-                        else (1, 1))
+        ksplit, kmin = (ops.attn_prefill_plan(len(batch), max_qlen, max_ctx, self.nh, self.nkv, D=self.D, bs=self.bs)
+                        if ids_d.is_cuda else (1, 1))
         pws = (ops.attn_prefill_workspace(ksplit, T, self.nh, self.D, dev, len(batch), self.nkv, max_qlen)
                if ksplit > 1 else None)
 

@@ -398,12 +398,13 @@ PREFILL_KSPLIT = int(os.environ.get("LLMC_PREFILL_KSPLIT", "-1"))
 PREFILL_KMIN = int(os.environ.get("LLMC_PREFILL_KMIN", "8"))
 
 
-def attn_prefill_plan(B, max_qlen, max_ctx, nh, nkv, ksplit=None, kmin=None):
+def attn_prefill_plan(B, max_qlen, max_ctx, nh, nkv, ksplit=None, kmin=None, D=128, bs=64):
     """(ksplit, kmin) of a prefill attention launch (csrc/kernels/attn_prefill.hip): row-tile groups
-    of >= 2 kmin key tiles run on min(ksplit, tiles // kmin) blocks; (1, _) = no split."""
+    of >= 2 kmin key tiles run on min(ksplit, tiles // kmin) blocks; (1, _) = no split. ``D`` / ``bs``
+    (head dim, KV page size) tell the plan which unsplit block forms it competes against."""
     k = PREFILL_KSPLIT if ksplit is None else int(ksplit)
     if k < 0:
-        return tuple(kernels().attn_prefill_plan(B, int(max_qlen), int(max_ctx), nh, nkv))
+        return tuple(kernels().attn_prefill_plan(B, int(max_qlen), int(max_ctx), nh, nkv, int(D), int(bs)))
     return max(1, min(k, 4)), int(PREFILL_KMIN if kmin is None else kmin)
 
 
@@ -422,14 +423,14 @@ def attn_prefill(q, k_cache, v_cache, block_tables, q_start, q_lens, ctx_lens, o
     """Causal paged prefill attention. ``max_ctx`` (default ``max_qlen``) feeds the KV-split plan;
     ``ksplit``/``kmin`` override it; ``ws`` is a caller-held attn_prefill_workspace reused across
     layers (it must not be shared by launches that can run concurrently); ``form`` forces the block
-    form of an unsplit launch (0 = 8 waves, 1 = paired row tiles, 2 = 4 waves; default: the
-    kernel library's choice, ``kernels().attn_prefill_form``)."""
+    form of an unsplit launch (0 = 8 waves, 1 = paired row tiles, 2 = 4 waves, 3 = key halves;
+    default: the kernel library's choice, ``kernels().attn_prefill_form``)."""
     if not q.is_cuda:
         return oracle.attn_prefill(q, k_cache, v_cache, block_tables, q_start, q_lens, ctx_lens, nh, nkv, D, bs,
                                    scale, out)
     B = q_lens.shape[0]
     T = q.shape[0]
-    k, km = attn_prefill_plan(B, max_qlen, max_qlen if max_ctx is None else max_ctx, nh, nkv, ksplit, kmin)
+    k, km = attn_prefill_plan(B, max_qlen, max_qlen if max_ctx is None else max_ctx, nh, nkv, ksplit, kmin, D, bs)
     part = ctr = 0
     if k > 1:
         G = nh // nkv

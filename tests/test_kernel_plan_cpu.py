@@ -8,18 +8,21 @@ from llm_consensus_amd import ops
 
 
 @pytest.mark.parametrize("B,T,ctx,nh,nkv,split", [
-    (1, 8192, 8192, 4, 1, 4),         # a TP=8 rank: one kv head, 128 blocks -> 4 ways (1.7x measured)
-    (1, 2048, 2048, 4, 1, 4),
-    (1, 8192, 8192, 8, 1, 2),         # 256 blocks of up to 128 tiles: 2 ways (1.3x)
-    (1, 2048, 2048, 16, 2, 1),        # 128 blocks: the unsplit 4-wave form (59.6 us) beats 2 ways (61.5)
-    (1, 4096, 4096, 8, 2, 2),         # 2 ways (87.8 us; 4 ways measured 119, unsplit paired 99)
-    (1, 2048, 2048, 32, 8, 1),        # 256 blocks of 1..32 tiles: a split costs more than it saves
+    (1, 8192, 8192, 4, 1, 4),         # a TP=8 rank: one kv head, 128 blocks -> 4 ways (134-142 us vs key halves 157)
+    (1, 2048, 2048, 4, 1, 1),         # the unsplit key-halves form: 41.2 us vs 4 ways 50.7
+    (1, 4096, 4096, 4, 1, 1),         # 73.7 vs 2 ways 81.4
+    (1, 8192, 8192, 8, 1, 1),         # 175 vs 2 ways 191.6
+    (1, 4096, 4096, 8, 2, 1),         # 75.5 vs 2 ways 85.9
+    (1, 2048, 2048, 16, 2, 1),        # 42.8 vs 2 ways 61.5
+    (1, 2048, 2048, 32, 8, 1),        # 256 blocks of 1..32 tiles: the paired form
     (1, 8192, 8192, 32, 8, 1),        # 1024 blocks: the longest-first order balances already
     (4, 8192, 8192, 32, 8, 1),
     (1, 256, 256, 32, 8, 1),          # 4 key tiles: nothing worth sharing
 ])
 def test_prefill_split_plan(B, T, ctx, nh, nkv, split):
     k, kmin = ops.attn_prefill_plan(B, T, ctx, nh, nkv, ksplit=-1)
+    if split == 4:  # without the key-halves form (D = 96 / other page sizes) the 0.80 bar applies
+        assert ops.attn_prefill_plan(B, T, ctx, nh, nkv, ksplit=-1, D=96)[0] == 4
     assert k == split, (k, kmin)
     if k > 1:
         assert 1 <= kmin <= (ctx + 63) // 64 // 2  # some group is long enough to split
@@ -32,19 +35,21 @@ def test_prefill_split_overrides():
 
 
 @pytest.mark.parametrize("B,T,nh,nkv,ksplit,form", [
-    (1, 2048, 32, 8, 1, 1),     # Llama-3-8B 2k: 256 8-wave blocks = one round -> paired (76.6 -> 63.2 us)
-    (1, 2048, 32, 32, 1, 1),    # 69.9 -> 58.1
-    (1, 1024, 32, 8, 1, 2),     # 128 blocks: 4-wave blocks (39.5 -> 32.4)
-    (1, 2048, 16, 2, 1, 2),     # G = 8 (70B TP=4 rank): no pairs; 4 waves (72.1 -> 59.6)
-    (1, 4096, 16, 2, 1, 2),     # 129.3 -> 115.7
-    (1, 8192, 32, 8, 1, 0),     # 1024 blocks: the 8-wave longest-first grid (552 vs 587 / 630)
+    (1, 2048, 32, 8, 1, 1),     # Llama-3-8B 2k: 256 8-wave blocks = one round, G <= 4 -> paired (76.6 -> 58.5 us)
+    (1, 2048, 32, 32, 1, 1),    # 69.9 -> 57.0
+    (1, 1024, 32, 8, 1, 3),     # 128 blocks: key halves (39.5 -> 27.8)
+    (1, 2048, 16, 2, 1, 3),     # G = 8 (70B TP=4 rank): no pairs; key halves (72.1 -> 42.8)
+    (1, 4096, 16, 2, 1, 3),     # 256 blocks, G = 8: key halves (129.3 -> 92.1)
+    (1, 8192, 32, 8, 1, 0),     # 1024 blocks: the 8-wave longest-first grid
     (2, 2048, 32, 8, 1, 0),     # two sequences: 512 blocks
     (1, 8192, 16, 2, 1, 0),     # 512 blocks
     (1, 8192, 4, 1, 4, 0),      # a split grid
 ])
 def test_prefill_block_form(B, T, nh, nkv, ksplit, form):
     from llm_consensus_amd.ops import kernels
-    assert kernels().attn_prefill_form(B, T, nh, nkv, ksplit) == form
+    assert kernels().attn_prefill_form(B, T, nh, nkv, ksplit, 128, 64) == form
+    if form == 3:  # key halves need D = 128 on 64-key pages: otherwise 4-wave blocks
+        assert kernels().attn_prefill_form(B, T, nh, nkv, ksplit, 96, 64) == 2
 
 
 @pytest.mark.parametrize("M,N,kind", [

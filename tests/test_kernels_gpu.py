@@ -551,12 +551,13 @@ def test_attn_prefill_long_context_vs_fp32(cuda, nh, nkv, D, ctx, ksplit):
 
 @pytest.mark.parametrize("nh,nkv,D,qlens", [(32, 8, 128, [2048]), (32, 8, 128, [1000, 700]), (32, 32, 96, [1024]),
                                           (16, 2, 128, [1500]), (8, 1, 128, [640, 130])])
-@pytest.mark.parametrize("form", [0, 1, 2])
+@pytest.mark.parametrize("form", [0, 1, 2, 3])
 def test_attn_prefill_block_forms_vs_fp32(cuda, nh, nkv, D, qlens, form):
     """Every block form of the unsplit prefill forced on the same problems against the fp32 oracle:
     8-wave blocks (LDS-DMA staging for D = 128 on 64-key pages, register staging for D = 96), paired
-    late / early row tiles (G <= 4; G = 8 falls back to 8 waves) and 4-wave blocks; full and ragged
-    sequences, a short second sequence beside a long one."""
+    late / early row tiles (G <= 4; G = 8 falls back to 8 waves), 4-wave blocks and key halves (two
+    wave halves over the two halves of the key tiles, merged through LDS; D = 128 only, else 8
+    waves); full and ragged sequences, a short second sequence beside a long one."""
     torch.manual_seed(sum(qlens) + D + form)
     bs = 64
     B = len(qlens)

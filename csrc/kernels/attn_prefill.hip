@@ -1,31 +1,36 @@
 // K4: paged flash-attention PREFILL (chunked, causal, GQA) on MFMA 32x32x16 bf16.
 //
-// One workgroup = 4 waves = 4 "row tiles" of 32 query rows that share a kv head (with GQA
-// group G = 4 the 4 waves are the 4 query heads of one kv head at the same 32 positions, so
-// every K/V tile staged in LDS feeds 4 heads). Per 64-key tile (= one 64-token KV page):
+// A wave owns a "row tile" of 32 query rows of one head; the waves of a workgroup share a kv head,
+// so every K/V tile staged in LDS feeds all of them (with G = 4 query heads per kv head, an 8-wave
+// block = 2 row positions x 4 heads). Per 64-key tile (= one 64-token KV page):
 //
 //   S^T[key][q] = K . Q^T      A = K rows from LDS (ds_read_b128, XOR-swizzled chunks:
 //                              chunk ^ (row & 15) -> conflict-free, cdna_hip_programming T2)
 //                              B = Q^T fragments held in VGPRs for the whole kernel
 //   online softmax             the accumulator puts ONE query per lane (col = lane & 31) with 32
 //                              of the 64 keys in registers; the other 32 are in lane ^ 32
-//                              -> row max/sum = in-register reduce + one xor-32 exchange
-//   O^T[d][q] += V^T . P^T     B = P straight from the S^T accumulator (cvt to bf16, the
+//                              -> row max/sum = in-register reduce + one xor-32 exchange; one fma +
+//                              exp per score, the running max moved only past a slack (kSlack)
+//   O^T[d][q] += V^T . P^T     B = P straight from the S^T accumulator (v_cvt_pk_bf16_f32, the
 //                              permuted-k trick of guide §3 "accumulator tile as the next
 //                              MFMA's operand"); A = V^T via ds_read_b64_tr_b16 (T10) from a
 //                              row-major V tile swizzled chunk ^ ((row & 3) << 2): conflict-free.
 //                              O^T keeps query on the lane, so the online-softmax rescale uses
 //                              the lane's own alpha (no cross-lane broadcast).
 //
-// K/V tiles are register-staged one tile ahead (issue global loads for t+1 before computing t,
-// write LDS after: T14 async-STAGE split) into a 2-deep LDS ring. Keys are looked up through
-// the block table per row, so any page size works (64 is the engine default).
-// Numerics: S in f32, exp2 with log2(e) folded into the scale, P rounded to bf16 for PV, O in f32.
+// K/V staging: LDS-DMA (buffer_load ... lds, the swizzle inverted on the source side) into a 4-slot
+// ring for D = 128 on 64-key pages; otherwise register-staged one or two tiles ahead into a 2-deep
+// LDS ring. Numerics: S in f32, exp2 with log2(e) folded into the scale, P rounded to bf16 for PV,
+// O in f32.
 //
-// KV split (llmc_attn_prefill_plan): when the grid cannot keep the chip busy to the end (one
-// 2k-token sequence = 256 blocks of 1..32 key tiles; a TP=8 rank's single kv head = 32 blocks), the
-// long row-tile groups' key ranges are cut into 2-4 tile ranges on their own blocks; each writes
-// (unnormalised O, m, l) in f32 and the last to finish merges them in split order (deterministic).
+// Block forms (llmc_attn_prefill_form): 8 waves; 8 waves with paired late / early row tiles; 4 waves
+// (two blocks per CU); key halves (two wave halves over the two halves of the key tiles, merged
+// through LDS). The grid is ordered longest-first over all kv heads.
+//
+// KV split (llmc_attn_prefill_plan): when the grid cannot keep the chip busy to the end (a TP=8
+// rank's single kv head = 32-128 blocks), the long row-tile groups' key ranges are cut into 2-4
+// ranges on their own blocks; each writes (unnormalised O, m, l) in f32 and the last to finish merges
+// them in split order (deterministic).
 #include <stdlib.h>
 
 #include <algorithm>

@@ -85,3 +85,62 @@ def test_every_kernel_launch_has_its_host_stub():
     out = subprocess.run([nm, "-D", libs[0]], capture_output=True, text=True, check=True).stdout
     missing = [ln.split()[-1] for ln in out.splitlines() if ln.split()[:1] == ["U"] and "__device_stub__" in ln]
     assert not missing, missing
+
+
+def _kernel_scratch_bytes():
+    """{kernel symbol: private segment bytes per lane} of every gfx950 kernel in the built library:
+    the .hip_fatbin section holds one offload bundle per source file; each device code object's
+    metadata note pairs .private_segment_fixed_size with .symbol (keys sorted within a kernel)."""
+    import glob
+    import os
+    import subprocess
+    import tempfile
+
+    tools = "/opt/rocm/lib/llvm/bin"
+    if not all(os.path.exists(os.path.join(tools, t)) for t in ("llvm-objcopy", "clang-offload-bundler", "llvm-readelf")):
+        pytest.skip("ROCm LLVM tools not found")
+    libs = glob.glob(os.path.join(os.path.dirname(ops.__file__), "..", "_lib", "_llmc_hip*.so"))
+    assert libs, "kernel library not built"
+    res = {}
+    with tempfile.TemporaryDirectory() as d:
+        fb = os.path.join(d, "fatbin")
+        subprocess.run([f"{tools}/llvm-objcopy", f"--dump-section=.hip_fatbin={fb}", libs[0]], check=True)
+        data = open(fb, "rb").read()
+        magic = b"__CLANG_OFFLOAD_BUNDLE__"
+        offs, i = [], data.find(magic)
+        while i >= 0:
+            offs.append(i)
+            i = data.find(magic, i + 1)
+        for k, o in enumerate(offs):
+            bundle, co = os.path.join(d, f"b{k}"), os.path.join(d, f"c{k}.elf")
+            with open(bundle, "wb") as f:
+                f.write(data[o:offs[k + 1] if k + 1 < len(offs) else len(data)])
+            r = subprocess.run([f"{tools}/clang-offload-bundler", "--unbundle", "--type=o", f"--input={bundle}",
+                                "--targets=hipv4-amdgcn-amd-amdhsa--gfx950", f"--output={co}"], capture_output=True)
+            if r.returncode != 0:
+                continue
+            notes = subprocess.run([f"{tools}/llvm-readelf", "--notes", co], capture_output=True, text=True).stdout
+            pending = None
+            for ln in notes.splitlines():
+                ln = ln.strip()
+                if ln.startswith(".private_segment_fixed_size:"):
+                    pending = int(ln.split(":")[1])
+                elif ln.startswith(".symbol:") and pending is not None:
+                    res[ln.split(":", 1)[1].strip()] = pending
+                    pending = None
+    return res
+
+
+def test_no_kernel_uses_scratch():
+    """No gfx950 kernel of the library keeps per-lane state in scratch (a silent 10x slowdown: a
+    refactor of the prefill tile loop into lambdas called from three loops put their captures on the
+    stack, 640 B per lane, with vgpr_spill_count still 0). Known exception: the 3-4-row, 1024-thread,
+    8-loads-per-lane GEMV with the RMS-norm prologue (continuous-batching decode of K >= 8192
+    shards), 20-48 B."""
+    import re
+
+    res = _kernel_scratch_bytes()
+    assert len(res) > 100, len(res)
+    allowed = re.compile(r"gemv_kernelILi[34]ELi1024ELi1ELi8ELi1ELi\dELb0E")
+    bad = {k: v for k, v in res.items() if v and not allowed.search(k)}
+    assert not bad, bad

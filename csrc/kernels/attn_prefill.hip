@@ -694,10 +694,10 @@ extern "C" int llmc_attn_prefill(const void* q, int q_stride, const void* k_cach
   const int npb = (max_qlen + 31) / 32;
   // block form: llmc_attn_prefill_form (its comment has the measurements)
   static const int form_env = [] {
-    const char* e = getenv("LLMC_PREFILL_FORM");  // A/B runs: force form 0 / 1 / 2 (unsplit grids)
+    const char* e = getenv("LLMC_PREFILL_FORM");  // A/B runs: force form 0-3 (unsplit grids)
     return e ? atoi(e) : -1;
   }();
-  // form_arg: -1 = llmc_attn_prefill_form's choice, 0 / 1 / 2 forced (tests; unsplit grids only)
+  // form_arg: -1 = llmc_attn_prefill_form's choice, 0-3 forced (tests; unsplit grids only)
   int form = llmc_attn_prefill_form(B, max_qlen, nh, nkv, ksplit, D, bs);
   if (form_env >= 0 && form_env <= 3 && ksplit == 1) form = form_env;
   if (form_arg >= 0 && form_arg <= 3 && ksplit == 1) form = form_arg;

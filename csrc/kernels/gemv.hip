@@ -62,9 +62,13 @@ static int launch_gemv(const void* x, int x_stride, const void* nw, float eps, c
   constexpr bool paired = EPI == EPI_SILU || EPI == EPI_ROPE;
   const int w = pick_waves(N, paired);
   // long rows on few blocks (a 70B TP=4 rank's qkv: 2560 x 8192 = 160 fat blocks): 8 loads per
-  // lane in flight instead of 4 (9.67 vs 10.99 us, profiles/r1_attn_decode_tp_shapes.md)
-  if (w == 16 && K >= 8192 && N <= 4096)
-    return launch_gemv_g<M, 1024, 1, PRO, EPI, 8>(x, x_stride, nw, eps, W, out, out_stride, N, K, rope, s);
+  // lane in flight instead of 4 (9.67 vs 10.99 us, profiles/r1_attn_decode_tp_shapes.md). One or
+  // two rows only: with 3-4 rows (the VALU form runs them only when K is off the MFMA form's 128-k
+  // tiles) that geometry kept 20-48 B per lane in scratch (tests/test_kernel_plan_cpu.py)
+  if constexpr (M <= 2) {
+    if (w == 16 && K >= 8192 && N <= 4096)
+      return launch_gemv_g<M, 1024, 1, PRO, EPI, 8>(x, x_stride, nw, eps, W, out, out_stride, N, K, rope, s);
+  }
   switch (w) {
     case 16: return launch_gemv_g<M, 1024, 1, PRO, EPI>(x, x_stride, nw, eps, W, out, out_stride, N, K, rope, s);
     case 12: return launch_gemv_g<M, 768, 1, PRO, EPI>(x, x_stride, nw, eps, W, out, out_stride, N, K, rope, s);

@@ -23,17 +23,22 @@ BF = torch.bfloat16
 def main():
     nh, nkv, D, bs = 32, 8, 128, 64
     one = lambda v: torch.tensor([v], dtype=torch.int32, device="cuda")  # noqa: E731
-    # flash prefill: 4096 queries over 4096 keys
-    T = ctx = 4096
-    nb = ctx // bs + 1
-    kc = torch.randn(nb, nkv, bs, D, device="cuda").to(BF)
-    vc = torch.randn_like(kc)
-    bt = torch.arange(nb, dtype=torch.int32, device="cuda").view(1, -1)
-    q = torch.randn(T, nh * D, device="cuda").to(BF)
-    out = torch.empty_like(q)
-    for _ in range(2):
-        ops.attn_prefill(q, kc, vc, bt, one(0), one(T), one(ctx), out, T, nh, nkv, D, bs, 1 / math.sqrt(D))
-    del kc, vc, q, out
+    # flash prefill: full causal prompts of PMC_PREFILL tokens (default 4096; "2048,8192": the paired
+    # one-round form and the 8-wave multi-round form, both on LDS-DMA staging)
+    for T in [int(v) for v in os.environ.get("PMC_PREFILL", "4096").split(",")]:
+        ctx = T
+        nb = ctx // bs + 1
+        kc = torch.randn(nb, nkv, bs, D, device="cuda").to(BF)
+        vc = torch.randn_like(kc)
+        bt = torch.arange(nb, dtype=torch.int32, device="cuda").view(1, -1)
+        q = torch.randn(T, nh * D, device="cuda").to(BF)
+        out = torch.empty_like(q)
+        for _ in range(2):
+            ops.attn_prefill(q, kc, vc, bt, one(0), one(T), one(ctx), out, T, nh, nkv, D, bs, 1 / math.sqrt(D))
+        del kc, vc, q, out
+    if os.environ.get("PMC_PREFILL_ONLY") == "1":
+        torch.cuda.synchronize()
+        return
 
     # decode attention: fused form at 2048 keys (16 chunks of 128), split form at 16384 keys (32
     # 8-wave blocks per kv head); 8 MB and 64 MB of K/V

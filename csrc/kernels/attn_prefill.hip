@@ -682,6 +682,15 @@ extern "C" int llmc_attn_prefill_form(int B, int max_qlen, int nh, int nkv, int 
   return halves_ok ? 3 : 2;
 }
 
+// Arrival counters a split launch needs: one per (sequence, row-tile group, kv head), where a split
+// grid is the 8-wave form (ngrp = ceil(G * npb / 8), the kernel's gridDim.x / nkv / ksplit). The one
+// size both the workspace allocator and the launch check use.
+extern "C" int64_t llmc_attn_prefill_counters(int B, int max_qlen, int nh, int nkv) {
+  if (nkv <= 0 || nh % nkv != 0 || max_qlen <= 0 || B <= 0) return 0;
+  const int64_t npb = (max_qlen + 31) / 32, ngrp = ((nh / nkv) * npb + 7) / 8;
+  return static_cast<int64_t>(B) * ngrp * nkv;
+}
+
 extern "C" int llmc_attn_prefill(const void* q, int q_stride, const void* k_cache, const void* v_cache,
                                  const void* block_tables, int bt_stride, const void* q_start, const void* q_lens,
                                  const void* ctx_lens, void* out, int out_stride, int B, int max_qlen, int nh, int nkv,

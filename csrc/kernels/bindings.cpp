@@ -49,6 +49,7 @@ int llmc_attn_prefill(const void*, int, const void*, const void*, const void*, i
                       int, hipStream_t);
 int llmc_attn_prefill_form(int, int, int, int, int, int, int);
 int llmc_attn_prefill_plan(int, int, int, int, int, int, int, int*);
+int64_t llmc_attn_prefill_counters(int, int, int, int);
 int llmc_sample(const void*, int64_t, int, int, const void*, const void*, const void*, const void*, const void*, void*,
                 void*, void*, void*, void*, void*, const void*, int, int, void*, void*, int, int, hipStream_t);
 int llmc_sample_parts();
@@ -63,6 +64,8 @@ int llmc_moe_combine(const void*, const void*, const void*, void*, int, int, int
 int llmc_moe_gemv(int, const void*, int, const void*, float, const void*, const void*, int, void*, int, int, int, int,
                   hipStream_t);
 int llmc_moe_ep_localize(const void*, const void*, int, int, int, void*, void*, hipStream_t);
+int llmc_moe_ep_dispatch(const void*, int, int, int, int, void*, void*, void*, void*, hipStream_t);
+int llmc_gather_rows(const void*, int, const void*, int, int, int, void*, int, hipStream_t);
 int llmc_gemv_sweep(int, const void*, const void*, const void*, void*, int, int, hipStream_t);
 size_t llmc_car_sig_bytes();
 int llmc_car_alloc(size_t, void**);
@@ -185,6 +188,9 @@ PYBIND11_MODULE(_llmc_hip, m) {
                             D, bs, scale, ksplit, kmin, P(part), P(counters), T, form, S(s)),
           "attn_prefill");
   });
+  m.def("attn_prefill_counters", [](int B, int max_qlen, int nh, int nkv) {
+    return llmc_attn_prefill_counters(B, max_qlen, nh, nkv);
+  });
   m.def("attn_prefill_form", [](int B, int T, int nh, int nkv, int ksplit, int D, int bs) {
     return llmc_attn_prefill_form(B, T, nh, nkv, ksplit, D, bs);
   });
@@ -222,12 +228,18 @@ PYBIND11_MODULE(_llmc_hip, m) {
                         max_tiles, a_row_div, epi, tile, S(s)),
           "moe_gemm");
   });
-  m.def("moe_combine", [](ptr y, ptr w, ptr ids, ptr out, int T, int k, int H, ptr s) {
-    check(llmc_moe_combine(P(y), P(w), P(ids), P(out), T, k, H, S(s)), "moe_combine");
+  m.def("moe_combine", [](ptr y, ptr w, ptr rows, ptr out, int T, int k, int H, ptr s) {
+    check(llmc_moe_combine(P(y), P(w), P(rows), P(out), T, k, H, S(s)), "moe_combine");
   });
   m.def("moe_gemv", [](int k, ptr x, int xs, ptr nw, float eps, ptr W, ptr ids, int ids_stride, ptr out, int os,
                        int N, int K, int epi, ptr s) {
     check(llmc_moe_gemv(k, P(x), xs, P(nw), eps, P(W), P(ids), ids_stride, P(out), os, N, K, epi, S(s)), "moe_gemv");
+  });
+  m.def("moe_ep_dispatch", [](ptr ids, int npairs, int El, int n, int cap, ptr sp, ptr se, ptr slot, ptr cnt, ptr s) {
+    check(llmc_moe_ep_dispatch(P(ids), npairs, El, n, cap, P(sp), P(se), P(slot), P(cnt), S(s)), "moe_ep_dispatch");
+  });
+  m.def("gather_rows", [](ptr x, int xs, ptr rows, int M, int div, int H, ptr out, int os, ptr s) {
+    check(llmc_gather_rows(P(x), xs, P(rows), M, div, H, P(out), os, S(s)), "gather_rows");
   });
   m.def("moe_ep_localize", [](ptr ids, ptr w, int n, int e0, int nl, ptr lids, ptr lw, ptr s) {
     check(llmc_moe_ep_localize(P(ids), P(w), n, e0, nl, P(lids), P(lw), S(s)), "moe_ep_localize");

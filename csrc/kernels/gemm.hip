@@ -676,7 +676,7 @@ extern "C" int llmc_gemm(const void* A, int lda, const void* W, int ldw, void* C
 // (microbenchmarks, tests and llmc_gemm's narrow-N dispatch).
 extern "C" int llmc_gemm_narrow(const void* A, int lda, const void* W, int ldw, void* C, int ldc, int M, int N, int K,
                                 int epi, hipStream_t s) {
-  if (K % kTK != 0 || M <= 0 || N <= 0 || (epi == 3 && N % 2 != 0) || lda % 8 != 0 || ldw % 8 != 0) return -1;
+  if (K % kTK != 0 || M <= 0 || N <= 0 || K <= 0 || (epi == 3 && N % 2 != 0) || lda % 8 != 0 || ldw % 8 != 0) return -1;
   if (static_cast<int64_t>(192) * ldw * 2 >= (1ll << 31) || static_cast<int64_t>(128) * lda * 2 >= (1ll << 31)) return -1;
   const int nwg = ((M + 127) / 128) * ((N + 191) / 192);
   const bf16_t* a = (const bf16_t*)A;
@@ -695,7 +695,7 @@ extern "C" int llmc_gemm_narrow(const void* A, int lda, const void* W, int ldw, 
 // of llmc_gemm): same operands / epilogues as llmc_gemm.
 extern "C" int llmc_gemm_t128(const void* A, int lda, const void* W, int ldw, void* C, int ldc, int M, int N, int K,
                               int epi, hipStream_t s) {
-  if (K % kBK != 0 || M <= 0 || N <= 0 || (epi == 3 && N % 2 != 0) || lda % 8 != 0 || ldw % 8 != 0) return -1;
+  if (K % kBK != 0 || M <= 0 || N <= 0 || K <= 0 || (epi == 3 && N % 2 != 0) || lda % 8 != 0 || ldw % 8 != 0) return -1;
   const int nwg = ((M + kBM - 1) / kBM) * ((N + kBN - 1) / kBN);
   const bf16_t* a = (const bf16_t*)A;
   const bf16_t* w = (const bf16_t*)W;
@@ -716,7 +716,7 @@ extern "C" int llmc_gemm_t128(const void* A, int lda, const void* W, int ldw, vo
 extern "C" int llmc_moe_gemm(const void* A, int lda, int a_rows, const void* W, const void* sorted_rows,
                              const void* tile_expert, const void* tile_count, void* C, int ldc, int N, int K,
                              int max_tiles, int a_row_div, int epi, int tile, hipStream_t s) {
-  if (K % kTK != 0 || lda % 8 != 0 || K % 8 != 0 || a_rows < 1 || (epi == 3 && N % 2 != 0)) return -1;
+  if (K <= 0 || N <= 0 || K % kTK != 0 || lda % 8 != 0 || K % 8 != 0 || a_rows < 1 || (epi == 3 && N % 2 != 0)) return -1;
   if (epi != 0 && epi != 1 && epi != 3) return -2;
   const int32_t* sr = (const int32_t*)sorted_rows;
   const int32_t* te = (const int32_t*)tile_expert;

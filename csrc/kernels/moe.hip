@@ -135,6 +135,7 @@ __global__ __launch_bounds__(kRouterThreads) void moe_router_kernel(
 }
 
 constexpr int kAlignThreads = 1024;
+constexpr int kMaxEpRanks = 8;  // expert-parallel group size (one node)
 
 __global__ __launch_bounds__(kAlignThreads) void moe_align_kernel(const int32_t* __restrict__ ids, int npairs, int E,
                                                                   int cap, int max_tiles, int tile,
@@ -151,7 +152,10 @@ __global__ __launch_bounds__(kAlignThreads) void moe_align_kernel(const int32_t*
   }
   for (int i = threadIdx.x; i < cap; i += kAlignThreads) sorted_rows[i] = -1;
   __syncthreads();
-  for (int i = threadIdx.x; i < npairs; i += kAlignThreads) atomicAdd(&cnt[ids[i]], 1);
+  // ids < 0: a pair of another rank's expert (expert parallel) or an all-to-all padding slot —
+  // not placed in any tile, so the grouped GEMM never reads or writes its row
+  for (int i = threadIdx.x; i < npairs; i += kAlignThreads)
+    if (ids[i] >= 0) atomicAdd(&cnt[ids[i]], 1);
   __syncthreads();
   if (threadIdx.x == 0) {
     int o = 0;
@@ -169,14 +173,103 @@ __global__ __launch_bounds__(kAlignThreads) void moe_align_kernel(const int32_t*
   __syncthreads();
   for (int i = threadIdx.x; i < npairs; i += kAlignThreads) {
     const int e = ids[i];
+    if (e < 0) continue;
     const int pos = off[e] + atomicAdd(&cur[e], 1);
     sorted_rows[pos] = i;
   }
 }
 
-// h[t] (bf16, in place) += sum_j w[t, j] * y[t*k + j]
+// Expert-parallel dispatch plan of the sequence-parallel prefill (C4): pair i = t * k + j of this
+// rank's token shard goes to rank d = ids[i] / El. Its slot in the send buffer is d * cap + r, r =
+// its rank among the pairs bound for d in pair order (stable, so the plan is deterministic). All
+// outputs stay on the device (no host sync in the layer loop; the all-to-all moves cap rows per
+// peer): send_pair [n * cap] pair index or -1 (padding), send_e [n * cap] the expert id local to
+// rank d or -1, pair_slot [npairs] = the slot (the un-permute map of the rows coming back),
+// counts [n]. One block of 16 waves: each wave owns a contiguous run of pairs; pass 1 counts its
+// pairs per destination with ballots, a prefix over the waves gives every wave its first slot per
+// destination, pass 2 places each pair at that offset plus its rank within the 64-pair ballot.
+constexpr int kDispatchWaves = 16;
+
+__global__ __launch_bounds__(kDispatchWaves * kWave) void moe_ep_dispatch_kernel(
+    const int32_t* __restrict__ ids, int npairs, int El, int n, int cap, int32_t* __restrict__ send_pair,
+    int32_t* __restrict__ send_e, int32_t* __restrict__ pair_slot, int32_t* __restrict__ counts) {
+  __shared__ int wcnt[kDispatchWaves][kMaxEpRanks];
+  const int tid = threadIdx.x, wave = tid / kWave, lane = tid % kWave;
+  for (int i = tid; i < n * cap; i += kDispatchWaves * kWave) {
+    send_pair[i] = -1;
+    send_e[i] = -1;
+  }
+  const int seg = (npairs + kDispatchWaves * kWave - 1) / (kDispatchWaves * kWave) * kWave;
+  const int lo = wave * seg, hi = min(npairs, lo + seg);
+  int c[kMaxEpRanks];
+#pragma unroll
+  for (int d = 0; d < kMaxEpRanks; ++d) c[d] = 0;
+  for (int base = lo; base < hi; base += kWave) {
+    const int i = base + lane;
+    const int dst = i < hi ? ids[i] / El : -1;
+#pragma unroll
+    for (int d = 0; d < kMaxEpRanks; ++d)
+      if (d < n) c[d] += __popcll(__ballot(dst == d));
+  }
+  if (lane == 0) {
+#pragma unroll
+    for (int d = 0; d < kMaxEpRanks; ++d) wcnt[wave][d] = c[d];
+  }
+  __syncthreads();  // also orders the padding fill above before the placement below
+  int run[kMaxEpRanks];
+#pragma unroll
+  for (int d = 0; d < kMaxEpRanks; ++d) {
+    int o = 0;
+    for (int w = 0; w < wave; ++w) o += wcnt[w][d];
+    run[d] = o;
+  }
+  if (tid < n) {
+    int o = 0;
+    for (int w = 0; w < kDispatchWaves; ++w) o += wcnt[w][tid];
+    counts[tid] = o;
+  }
+  const uint64_t below = (1ull << lane) - 1ull;
+  for (int base = lo; base < hi; base += kWave) {
+    const int i = base + lane;
+    const int e = i < hi ? ids[i] : -1;
+    const int dst = e >= 0 ? e / El : -1;
+    int slot = -1;
+#pragma unroll
+    for (int d = 0; d < kMaxEpRanks; ++d) {
+      if (d >= n) break;
+      const uint64_t b = __ballot(dst == d);
+      if (dst == d) slot = d * cap + run[d] + __popcll(b & below);
+      run[d] += __popcll(b);
+    }
+    if (slot >= 0) {
+      send_pair[slot] = i;
+      send_e[slot] = e - dst * El;
+      pair_slot[i] = slot;
+    }
+  }
+}
+
+// out[j] = x[rows[j] / div] (bf16 rows of H), zeros where rows[j] < 0: the send buffer of the
+// expert-parallel all-to-all (row j = slot j of moe_ep_dispatch's plan, div = top-k).
+__global__ __launch_bounds__(256) void gather_rows_kernel(const bf16_t* __restrict__ x, int x_stride,
+                                                          const int32_t* __restrict__ rows, int div, int H,
+                                                          bf16_t* __restrict__ out, int out_stride) {
+  const int j = blockIdx.x;
+  const int r = rows[j];
+  u32x4* o = reinterpret_cast<u32x4*>(out + static_cast<int64_t>(j) * out_stride);
+  if (r < 0) {
+    for (int c = threadIdx.x; c < H / 8; c += 256) o[c] = u32x4{0u, 0u, 0u, 0u};
+    return;
+  }
+  const u32x4* src = reinterpret_cast<const u32x4*>(x + static_cast<int64_t>(r / div) * x_stride);
+  for (int c = threadIdx.x; c < H / 8; c += 256) o[c] = src[c];
+}
+
+// h[t] (bf16, in place) += sum_j w[t, j] * y[row(t*k + j)], row = rows[.] when given (the expert-
+// parallel all-to-all's returned slots, moe_ep_dispatch pair_slot), else the pair index itself
 __global__ __launch_bounds__(256) void moe_combine_kernel(const bf16_t* __restrict__ y, const float* __restrict__ w,
-                                                          bf16_t* __restrict__ h, int k, int H) {
+                                                          bf16_t* __restrict__ h, int k, int H,
+                                                          const int32_t* __restrict__ rows) {
   const int t = blockIdx.x;
   for (int c = threadIdx.x; c < H / 8; c += 256) {
     float acc[8];
@@ -186,7 +279,8 @@ __global__ __launch_bounds__(256) void moe_combine_kernel(const bf16_t* __restri
       const float wj = w[static_cast<int64_t>(t) * k + j];
       if (wj == 0.f) continue;  // another rank's expert (expert parallel): its y row is not written
       float f[8];
-      unpack8(reinterpret_cast<const u32x4*>(y + (static_cast<int64_t>(t) * k + j) * H)[c], f);
+      const int64_t yr = rows != nullptr ? rows[static_cast<int64_t>(t) * k + j] : static_cast<int64_t>(t) * k + j;
+      unpack8(reinterpret_cast<const u32x4*>(y + yr * H)[c], f);
 #pragma unroll
       for (int q = 0; q < 8; ++q) s[q] += wj * f[q];
     }
@@ -239,10 +333,29 @@ int llmc_moe_align(const void* ids, int T, int k, int E, int tile, void* sorted_
   return static_cast<int>(hipGetLastError());
 }
 
-int llmc_moe_combine(const void* y, const void* w, const void* ids, void* h, int T, int k, int H, hipStream_t s) {
-  (void)ids;
+// rows: nullptr = y row t*k + j for pair (t, j); else y row rows[t*k + j] (expert-parallel return slots)
+int llmc_moe_combine(const void* y, const void* w, const void* rows, void* h, int T, int k, int H, hipStream_t s) {
   if (H % 8 != 0) return -1;
-  moe_combine_kernel<<<T, 256, 0, s>>>((const bf16_t*)y, (const float*)w, (bf16_t*)h, k, H);
+  if (T <= 0) return 0;
+  moe_combine_kernel<<<T, 256, 0, s>>>((const bf16_t*)y, (const float*)w, (bf16_t*)h, k, H, (const int32_t*)rows);
+  return static_cast<int>(hipGetLastError());
+}
+
+int llmc_moe_ep_dispatch(const void* ids, int npairs, int El, int n, int cap, void* send_pair, void* send_e,
+                         void* pair_slot, void* counts, hipStream_t s) {
+  if (n < 1 || n > kMaxEpRanks || El < 1 || npairs < 0 || cap < npairs || cap < 1) return -1;
+  moe_ep_dispatch_kernel<<<1, kDispatchWaves * kWave, 0, s>>>((const int32_t*)ids, npairs, El, n, cap,
+                                                               (int32_t*)send_pair, (int32_t*)send_e,
+                                                               (int32_t*)pair_slot, (int32_t*)counts);
+  return static_cast<int>(hipGetLastError());
+}
+
+int llmc_gather_rows(const void* x, int x_stride, const void* rows, int M, int div, int H, void* out, int out_stride,
+                     hipStream_t s) {
+  if (H % 8 != 0 || x_stride % 8 != 0 || out_stride % 8 != 0 || div < 1) return -1;
+  if (M <= 0) return 0;
+  gather_rows_kernel<<<M, 256, 0, s>>>((const bf16_t*)x, x_stride, (const int32_t*)rows, div, H, (bf16_t*)out,
+                                       out_stride);
   return static_cast<int>(hipGetLastError());
 }
 

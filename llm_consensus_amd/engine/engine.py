@@ -558,6 +558,9 @@ class Engine:
         if not A.is_cuda:
             for p in range(n * k):
                 e = int(ids.view(-1)[p])
+                if e < 0:  # another rank's expert / an all-to-all padding slot: never read
+                    y[p].zero_()
+                    continue
                 gu = (A[p // k:p // k + 1].float() @ Lw.w_gu[e].float().t()).to(torch.bfloat16)
                 y[p] = (oracle.silu_mul_interleaved(gu).float() @ Lw.w_down[e].float().t()).to(torch.bfloat16)[0]
             return y
@@ -596,14 +599,13 @@ class Engine:
         T, k = xn.shape[0], c.top_k_experts
         w, ids = self._route(xn, Lw)
         if self.w.ep:
+            # other ranks' experts: local id -1 / weight 0 on the device; the expert GEMMs skip
+            # those pairs (moe_align places no -1 row, GEMV blocks of a -1 pair exit) and the
+            # combine skips zero-weight pairs — no host sync, no index kernels
             lids = torch.empty_like(ids)
             lw = torch.empty_like(w)
             ops.moe_ep_localize(ids, w, self.w.e0, self.w.n_local_experts, lids, lw)
-            sel = torch.nonzero(lids.view(-1) >= 0).view(-1)  # host sync: prefill only
-            y = torch.zeros(T * k, c.hidden, dtype=torch.bfloat16, device=xn.device)
-            if sel.numel():
-                y.index_copy_(0, sel, self._expert_ffn(xn.index_select(0, sel // k),
-                                                       lids.view(-1).index_select(0, sel).view(-1, 1), Lw))
+            y = self._expert_ffn(xn, lids, Lw)
             w, ids = lw, lids
         else:
             y = self._expert_ffn(xn, ids, Lw)
@@ -616,25 +618,26 @@ class Engine:
     def _moe_ep_a2a(self, xs: torch.Tensor, Lw, hs: torch.Tensor) -> None:
         """hs += MoE(xs) for this rank's token shard, experts sharded over the TP group: every
         (token, slot) pair is sent to the rank owning its expert (all-to-all, C4), computed there
-        by the grouped GEMM, and sent back for the deterministic combine."""
-        c = self.cfg
-        k, H = c.top_k_experts, c.hidden
-        El = self.w.n_local_experts
+        by the grouped GEMM, and sent back for the deterministic combine.
+
+        The plan stays on the device (``moe_ep_dispatch``: stable slots per destination rank, -1
+        padding; ``gather_rows`` builds the send buffer), so the layer loop has no host sync: the
+        all-to-all moves a fixed ``cap`` = T*k rows per peer (every pair of the shard may pick one
+        rank), the receiver's padding rows carry expert id -1 and are skipped by the expert GEMMs,
+        and the combine reads each pair's returned row through its slot. The price is padded
+        all-to-all traffic (n x the routed rows) for no host round trip per layer."""
+        k = self.cfg.top_k_experts
+        El, n = self.w.n_local_experts, self.tp.size
         w, ids = self._route(xs, Lw)
-        flat = ids.view(-1).long()
-        owner = flat // El
-        order = torch.argsort(owner, stable=True)
-        send = torch.bincount(owner, minlength=self.tp.size).tolist()
-        recv = self.tp.exchange_counts(send)
-        send_x = xs.index_select(0, order // k)
-        send_e = (flat - owner * El).index_select(0, order).to(torch.int32)
-        recv_x = self.tp.all_to_all_rows(send_x, send, recv)
-        recv_e = self.tp.all_to_all_rows(send_e, send, recv)
+        cap = ids.numel()
+        send_pair, send_e, slot, _ = ops.moe_ep_dispatch(ids, El, n, cap)
+        send_x = ops.gather_rows(xs, send_pair, k)
+        split = [cap] * n
+        recv_x = self.tp.all_to_all_rows(send_x, split, split)
+        recv_e = self.tp.all_to_all_rows(send_e, split, split)
         y_recv = self._expert_ffn(recv_x, recv_e.view(-1, 1), Lw)
-        y_back = self.tp.all_to_all_rows(y_recv, recv, send)
-        y = torch.empty(flat.numel(), H, dtype=torch.bfloat16, device=xs.device)
-        y.index_copy_(0, order, y_back)
-        ops.moe_combine(y, w, ids, hs)
+        y_back = self.tp.all_to_all_rows(y_recv, split, split)
+        ops.moe_combine(y_back, w, ids, hs, rows=slot)
 
     # -- decode -------------------------------------------------------------------------------------
     def _decode_step(self, B: int, bucket: Optional[int] = None) -> None:
@@ -960,6 +963,12 @@ class Engine:
                 ev.record(self.stream)
                 return ev
 
+            if self.tp.size > 1:
+                # the prefill and the first sample finish before the replay deadline clock starts
+                # (a long TP prefill is not a stalled replay: ADVICE r5); its collectives' spins are
+                # bounded, so this wait is too
+                self.stream.synchronize()
+            self._replay_aborted = False
             pending_ev = launch_copy(issued)
             last = False
             while True:
@@ -978,6 +987,9 @@ class Engine:
                         issued += S
                     # wait for the previous snapshot (the GPU keeps the just-issued replay queued)
                     self._wait_event(pending_ev)
+                    # a custom-collective spin that gave up (or a host abort) invalidates every later
+                    # collective result: fail before these tokens are streamed, not at the end
+                    self._raise_if_collectives_gave_up()
                     consume(self.host_count, self.host_tokens)
                 except Exception as e:  # noqa: BLE001 - under TP: agreed below, on every rank
                     if not tp_ctl or isinstance(e, _TPBroken):
@@ -1014,8 +1026,23 @@ class Engine:
                     self._tp_broken(f"a decode replay did not finish {2 * self.stall_s:.0f} s after it was due "
                                     "(its collectives were aborted)")
                 self.tp.abort_collectives()  # the spins give up at their next check
+                self._replay_aborted = True
                 deadline, aborted = time.monotonic() + self.stall_s, True
             time.sleep(0.0002)
+
+    _replay_aborted = False
+
+    def _raise_if_collectives_gave_up(self) -> None:
+        """Under TP: raise if a custom-collective spin of this rank gave up or returned without its
+        data since the last resync (the host status page: no GPU call, the stream keeps running), or
+        the host aborted a replay — from then on every collective of this rank returns at once with
+        stale data, so no later token may be streamed. The decode loop turns it into the
+        agreed failure of the group at this replay."""
+        if self.tp.size == 1:
+            return
+        if self._replay_aborted or any(c.host_timed_out() for c in self.tp.collectives()):
+            raise EngineError("custom all-reduce gave up on a stalled TP peer: this request's later tokens "
+                              "would be invalid")
 
     def _drain(self) -> None:
         """The stream's queued work finished (bounded under TP, see ``_wait_event``)."""
@@ -1050,10 +1077,14 @@ class Engine:
     def _inject(self, stage: str, issued: int) -> None:
         """Test hook (SURVEY.md §5.3 fault injection): ``fault_at`` = (stage, k) raises an
         InjectedEngineFault before the decode replay that would produce token k (its peers' replays
-        then wait on this rank's collectives until their spins give up)."""
+        then wait on this rank's collectives until their spins give up); (stage, k, seconds) stalls
+        the rank that long there instead, then lets it go on."""
         f = self.fault_at
         if f is not None and f[0] == stage and issued >= f[1]:
             self.fault_at = None
+            if len(f) > 2:  # (stage, k, seconds): a rank that stalls, then goes on
+                time.sleep(float(f[2]))
+                return
             raise InjectedEngineFault(f"injected fault: {self.name} stops before decode token {issued}")
 
     fault_at: Optional[tuple] = None

@@ -408,14 +408,19 @@ def attn_prefill_plan(B, max_qlen, max_ctx, nh, nkv, ksplit=None, kmin=None, D=1
     return max(1, min(k, 4)), int(PREFILL_KMIN if kmin is None else kmin)
 
 
+def attn_prefill_counters(B, max_qlen, nh, nkv) -> int:
+    """Arrival counters of a split prefill launch: one per (sequence, row-tile group of the 8-wave
+    split grid, kv head) — the kernel library's own count (``llmc_attn_prefill_counters``), used by
+    both the workspace allocator and ``attn_prefill``'s reuse check."""
+    return int(kernels().attn_prefill_counters(int(B), int(max_qlen), int(nh), int(nkv)))
+
+
 def attn_prefill_workspace(ksplit, T, nh, D, device, B=1, nkv=1, max_qlen=None):
     """A split prefill's hand-off state: f32 partials ([ksplit][T][nh][D] O, then [ksplit][T][nh][2]
     (m, l)) and zeroed arrival counters (one per (sequence, row-tile group, kv head), re-armed by the
     kernel, so one workspace serves every layer of a prefill on one stream)."""
-    G = nh // max(nkv, 1)
-    ngrp = (G * ((max_qlen or T) + 31) // 32 + 3) // 4  # row-tile groups of >= 4 waves
     return (torch.empty(ksplit * T * nh * (D + 2), dtype=torch.float32, device=device),
-            torch.zeros(B * ngrp * nkv, dtype=torch.int32, device=device))
+            torch.zeros(max(1, attn_prefill_counters(B, max_qlen or T, nh, nkv)), dtype=torch.int32, device=device))
 
 
 def attn_prefill(q, k_cache, v_cache, block_tables, q_start, q_lens, ctx_lens, out, max_qlen, nh, nkv, D, bs, scale,
@@ -433,14 +438,20 @@ def attn_prefill(q, k_cache, v_cache, block_tables, q_start, q_lens, ctx_lens, o
     k, km = attn_prefill_plan(B, max_qlen, max_qlen if max_ctx is None else max_ctx, nh, nkv, ksplit, kmin, D, bs)
     part = ctr = 0
     if k > 1:
-        G = nh // nkv
-        need_c = B * ((G * ((int(max_qlen) + 31) // 32) + 3) // 4) * nkv
+        need_c = attn_prefill_counters(B, max_qlen, nh, nkv)
         if ws is None or ws[0].numel() < k * T * nh * (D + 2) or ws[1].numel() < need_c:
             ws = attn_prefill_workspace(k, T, nh, D, q.device, B, nkv, max_qlen)
         part, ctr = _p(ws[0]), _p(ws[1])
-    kernels().attn_prefill(_p(q), q.stride(0), _p(k_cache), _p(v_cache), _p(block_tables), block_tables.stride(0),
-                           _p(q_start), _p(q_lens), _p(ctx_lens), _p(out), out.stride(0), B, int(max_qlen), nh, nkv,
-                           D, bs, float(scale), k, km, part, ctr, T, -1 if form is None else int(form), _s(q))
+    try:
+        kernels().attn_prefill(_p(q), q.stride(0), _p(k_cache), _p(v_cache), _p(block_tables), block_tables.stride(0),
+                               _p(q_start), _p(q_lens), _p(ctx_lens), _p(out), out.stride(0), B, int(max_qlen), nh,
+                               nkv, D, bs, float(scale), k, km, part, ctr, T, -1 if form is None else int(form), _s(q))
+    except Exception:
+        # a failed launch may leave arrival counters armed; the next launch on this workspace
+        # would merge before its partials arrived: re-zero them (stream-ordered)
+        if k > 1:
+            ws[1].zero_()
+        raise
     return out
 
 
@@ -530,12 +541,52 @@ def moe_gemm(A, W_experts, sorted_rows, tile_expert, tile_count, out, N, K, max_
     return out
 
 
-def moe_combine(y, w, ids, h):
+def moe_combine(y, w, ids, h, rows: Optional[torch.Tensor] = None):
+    """h[t] += sum_j w[t, j] * y[t*k + j] (K12; fixed order, f32, zero-weight pairs skipped);
+    ``rows`` [T*k] int32: pair (t, j)'s result is y row rows[t*k + j] instead (the slots of the
+    expert-parallel all-to-all, ``moe_ep_dispatch``)."""
     if not h.is_cuda:
+        if rows is not None:
+            y = y.index_select(0, rows.long().clamp(min=0))
         return oracle.moe_combine(y, w, h)
     T, k = w.shape
-    kernels().moe_combine(_p(y), _p(w), _p(ids), _p(h), T, k, h.shape[1], _s(h))
+    kernels().moe_combine(_p(y), _p(w), _p(rows), _p(h), T, k, h.shape[1], _s(h))
     return h
+
+
+def moe_ep_dispatch(ids: torch.Tensor, n_local: int, n_ranks: int, cap: int):
+    """Expert-parallel all-to-all plan of a token shard's (token, slot) pairs (C4), on the device:
+    pair i goes to rank d = ids[i] // n_local, slot d * cap + (its rank among d's pairs, in pair
+    order). -> (send_pair [n*cap] i32 pair index or -1, send_e [n*cap] i32 expert id local to d or
+    -1, pair_slot [T*k] i32, counts [n] i32). ``cap`` >= T*k (every pair may pick one rank)."""
+    P = ids.numel()
+    dev = ids.device
+    i32 = dict(dtype=torch.int32, device=dev)
+    send_pair = torch.empty(n_ranks * cap, **i32)
+    send_e = torch.empty(n_ranks * cap, **i32)
+    slot = torch.empty(P, **i32)
+    counts = torch.empty(n_ranks, **i32)
+    if not ids.is_cuda:
+        sp, se, sl, cn = oracle.moe_ep_dispatch(ids, n_local, n_ranks, cap)
+        return send_pair.copy_(sp), send_e.copy_(se), slot.copy_(sl), counts.copy_(cn)
+    kernels().moe_ep_dispatch(_p(ids), P, int(n_local), int(n_ranks), int(cap), _p(send_pair), _p(send_e), _p(slot),
+                              _p(counts), _s(ids))
+    return send_pair, send_e, slot, counts
+
+
+def gather_rows(x: torch.Tensor, rows: torch.Tensor, div: int, out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """out[j] = x[rows[j] // div], zero rows where rows[j] < 0 (the expert-parallel send buffer)."""
+    M = rows.numel()
+    if out is None:
+        out = torch.empty(M, x.shape[1], dtype=x.dtype, device=x.device)
+    if not x.is_cuda:
+        r = rows.long()
+        out.copy_(torch.where((r >= 0).unsqueeze(1), x.index_select(0, (r.clamp(min=0) // div)),
+                              torch.zeros((), dtype=x.dtype)))
+        return out
+    _bf16(x, "gather_rows.x")
+    kernels().gather_rows(_p(x), x.stride(0), _p(rows), M, int(div), x.shape[1], _p(out), out.stride(0), _s(x))
+    return out
 
 
 def moe_gemv(x, W_experts, ids, x_div, out, N, K, epi, norm_w=None, eps: float = 1e-5):

@@ -236,6 +236,22 @@ def moe_ep_localize(ids: torch.Tensor, w: torch.Tensor, e0: int, n_local: int):
     return lids.to(torch.int32), lw
 
 
+def moe_ep_dispatch(ids: torch.Tensor, n_local: int, n_ranks: int, cap: int):
+    """Reference of the expert-parallel dispatch plan (see ops.moe_ep_dispatch): stable slots per
+    destination rank in pair order, -1 padding."""
+    flat = ids.reshape(-1).long()
+    send_pair = torch.full((n_ranks * cap,), -1, dtype=torch.int32)
+    send_e = torch.full((n_ranks * cap,), -1, dtype=torch.int32)
+    slot = torch.empty(flat.numel(), dtype=torch.int32)
+    counts = torch.zeros(n_ranks, dtype=torch.int32)
+    for i, e in enumerate(flat.tolist()):
+        d = e // n_local
+        s = d * cap + int(counts[d])
+        counts[d] += 1
+        send_pair[s], send_e[s], slot[i] = i, e - d * n_local, s
+    return send_pair, send_e, slot, counts
+
+
 def softmax_scale(D: int) -> float:
     return 1.0 / math.sqrt(D)
 

@@ -236,9 +236,9 @@ class TPGroup:
         return out
 
     def custom_timed_out(self) -> bool:
-        """Local: did a custom-collective spin give up since the last resync (reads device memory,
-        after the caller synchronised its stream)?"""
-        return any(c.timed_out() for c in self.collectives())
+        """Local: did a custom-collective spin give up, or the host abort this rank's spins, since
+        the last resync (reads device memory, after the caller synchronised its stream)?"""
+        return any(c.timed_out() or c.aborted() for c in self.collectives())
 
     def check_collectives(self) -> bool:
         """Collective over ``ctrl`` (every rank calls it at the same point): True when every rank's

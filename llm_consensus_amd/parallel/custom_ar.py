@@ -248,6 +248,12 @@ class CustomAllReduce:
         k = kernels()
         return bool(self.host and k.car_host_get(self.host, k.car_host_word(1)))
 
+    def aborted(self) -> bool:
+        """Did the host set this rank's abort word since the last resync (every later spin then
+        gives up at once: the buffer needs a resync even if no spin was waiting at the time)?"""
+        k = kernels()
+        return bool(self.host and k.car_host_get(self.host, k.car_host_word(0)))
+
     def abort(self) -> None:
         """Make every spin of this rank give up at its next check (~100 us) instead of polling to
         its 1-s limit: the host's way out of a replay that overran its deadline (a TP peer stalled

@@ -64,27 +64,34 @@ def fused_ar_allowed(gpus: Dict[str, List[int]], name: str, concurrent: Sequence
     return decodes_alone(gpus, name, concurrent)
 
 
-def _concurrent(gpus: Dict[str, List[int]], m: str, judge: Optional[str], concurrency: int) -> List[str]:
+def _concurrent(gpus: Dict[str, List[int]], m: str, judge: Optional[str], concurrency: int,
+                responders: Optional[Sequence[str]] = None) -> List[str]:
     """The engines that decode while ``m`` does in a consensus run: the responders decode
     together; the judge decodes after the last response (runner.go:118 then judge.go:96), so with
     one request in flight it overlaps nothing — with several (the server) one request's judge
-    overlaps the next one's responders."""
+    overlaps the next one's responders. ``responders`` = the engines that answer the fan-out
+    (default: every engine but the judge). A judge that is also a responder (``--models`` names
+    it: LocalBackend gives it rows of its own) decodes during the fan-out too, so it is treated as
+    any other responder: its engine's launch forms are fixed for both phases."""
     if concurrency > 1:
         return [o for o in gpus if o != m]
-    if m == judge:
+    resp = set(responders) if responders is not None else {o for o in gpus if o != judge}
+    if m not in resp:
         return []
-    return [o for o in gpus if o not in (m, judge)]
+    return [o for o in gpus if o != m and o in resp]
 
 
-def fused_ar_plan(gpus: Dict[str, List[int]], judge: Optional[str], concurrency: int = 1) -> Dict[str, bool]:
+def fused_ar_plan(gpus: Dict[str, List[int]], judge: Optional[str], concurrency: int = 1,
+                  responders: Optional[Sequence[str]] = None) -> Dict[str, bool]:
     """``fused_ar_allowed`` for every placed engine of a consensus run (``_concurrent``)."""
-    return {m: fused_ar_allowed(gpus, m, _concurrent(gpus, m, judge, concurrency)) for m in gpus}
+    return {m: fused_ar_allowed(gpus, m, _concurrent(gpus, m, judge, concurrency, responders)) for m in gpus}
 
 
-def alone_plan(gpus: Dict[str, List[int]], judge: Optional[str], concurrency: int = 1) -> Dict[str, bool]:
+def alone_plan(gpus: Dict[str, List[int]], judge: Optional[str], concurrency: int = 1,
+               responders: Optional[Sequence[str]] = None) -> Dict[str, bool]:
     """``decodes_alone`` for every placed engine of a consensus run (``_concurrent``): the engines
     that take the lone-engine launch forms (``EngineConfig.attn_oproj_min_chunk``)."""
-    return {m: decodes_alone(gpus, m, _concurrent(gpus, m, judge, concurrency)) for m in gpus}
+    return {m: decodes_alone(gpus, m, _concurrent(gpus, m, judge, concurrency, responders)) for m in gpus}
 
 
 def parse_pins(spec: str) -> Dict[str, List[int]]:

@@ -203,8 +203,10 @@ class LocalBackend:
             seqs[m] = (n, sess)
         kv_blocks = kv_pool_blocks(self.placement, self.specs, self._ctx,
                                    {m: max(1, n) + sess for m, (n, sess) in seqs.items()})
-        fused = fused_ar_plan(self.placement.gpus, judge, conc)
-        alone = alone_plan(self.placement.gpus, judge, conc)
+        # the engines that decode during the fan-out (a judge named in --models is one of them)
+        responders = [m for m, (n, _) in seqs.items() if n > 0]
+        fused = fused_ar_plan(self.placement.gpus, judge, conc, responders)
+        alone = alone_plan(self.placement.gpus, judge, conc, responders)
         for g in used:
             models = []
             for m, gs in self.placement.gpus.items():

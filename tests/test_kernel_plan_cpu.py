@@ -28,6 +28,16 @@ def test_prefill_split_plan(B, T, ctx, nh, nkv, split):
         assert 1 <= kmin <= (ctx + 63) // 64 // 2  # some group is long enough to split
 
 
+@pytest.mark.parametrize("B,T,nh,nkv", [(1, 8192, 4, 1), (2, 300, 32, 8), (1, 33, 32, 32), (3, 2048, 16, 2)])
+def test_prefill_split_counters_match_the_kernel_grid(B, T, nh, nkv):
+    """one counter per (sequence, row-tile group of the 8-wave split grid, kv head) —
+    ngrp = ceil(G * ceil(T / 32) / 8), the kernel's gridDim.x / nkv / ksplit — from one helper that
+    both the workspace and the launch check use."""
+    G, npb = nh // nkv, (T + 31) // 32
+    assert ops.attn_prefill_counters(B, T, nh, nkv) == B * ((G * npb + 7) // 8) * nkv
+    assert ops.attn_prefill_workspace(2, T, nh, 128, "cpu", B, nkv, T)[1].numel() == B * ((G * npb + 7) // 8) * nkv
+
+
 def test_prefill_split_overrides():
     assert ops.attn_prefill_plan(1, 2048, 2048, 32, 8, ksplit=1)[0] == 1
     assert ops.attn_prefill_plan(1, 2048, 2048, 32, 8, ksplit=4, kmin=3) == (4, 3)

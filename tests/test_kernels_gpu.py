@@ -670,6 +670,65 @@ def test_moe(cuda, T):
     close(h, href, 3e-2)
 
 
+@pytest.mark.parametrize("n,Ts", [(2, 5), (2, 300), (4, 700), (8, 64)])
+def test_moe_expert_parallel_prefill_dispatch(cuda, n, Ts):
+    """The expert-parallel prefill dispatch on the device (engine ``_moe_ep_a2a``, C4) with n ranks
+    emulated on one GPU: per rank the router ids -> ``moe_ep_dispatch`` (stable slots per owner rank,
+    -1 padding, no host sync) -> ``gather_rows`` send buffer -> (the all-to-all as a block
+    transpose) -> every owner's grouped expert GEMMs over the received rows (``moe_align`` skips the
+    -1 padding) -> back -> ``moe_combine`` through the pair slots, against the fp32 oracle of the
+    whole MoE layer per token shard. The plan itself must equal the oracle plan exactly."""
+    torch.manual_seed(21 + n)
+    E, k, H, I = 8, 2, 256, 384
+    El = E // n
+    wgu = rnd(E, 2 * I, H, scale=0.05)
+    wd = rnd(E, H, I, scale=0.05)
+    cap = Ts * k
+    xs, ws, idss, plans, hs, hrefs = [], [], [], [], [], []
+    for r in range(n):
+        x = rnd(Ts, H)
+        bias = torch.zeros(E, device="cuda")
+        bias[r * El] = 3.0 if r == 0 else 0.0  # rank 0's tokens mostly pick its own first expert
+        logits = torch.randn(Ts, E, device="cuda") + bias
+        w = torch.empty(Ts, k, device="cuda")
+        ids = torch.empty(Ts, k, dtype=torch.int32, device="cuda")
+        ops.moe_route(logits, k, w, ids)
+        plan = ops.moe_ep_dispatch(ids, El, n, cap)
+        ref_plan = oracle.moe_ep_dispatch(ids.cpu(), El, n, cap)
+        for got, want in zip(plan, ref_plan):
+            assert torch.equal(got.cpu(), want), (r, got, want)
+        h = rnd(Ts, H)
+        href = h.cpu().clone()
+        oracle.moe_ffn(x.cpu(), wgu.cpu(), wd.cpu(), w.cpu(), ids.cpu(), href)
+        xs.append(x), ws.append(w), idss.append(ids), plans.append(plan), hs.append(h), hrefs.append(href)
+    send_x = [ops.gather_rows(xs[r], plans[r][0], k) for r in range(n)]
+    for r in range(n):  # padding rows are zeros, real rows the token's x
+        sp = plans[r][0].long()
+        real = sp >= 0
+        assert torch.equal(send_x[r][real], xs[r][sp[real] // k]) and not send_x[r][~real].any()
+    y_recv = []
+    for d in range(n):  # owner d: rows [d*cap, (d+1)*cap) of every rank's send buffer
+        rx = torch.cat([send_x[r][d * cap:(d + 1) * cap] for r in range(n)])
+        re = torch.cat([plans[r][1][d * cap:(d + 1) * cap] for r in range(n)]).view(-1, 1)
+        P = rx.shape[0]
+        tile = ops.moe_tile(P, El)
+        mt = ops.moe_max_tiles(P, El, tile)
+        sr = torch.empty(mt * tile, dtype=torch.int32, device="cuda")
+        te = torch.empty(mt, dtype=torch.int32, device="cuda")
+        tc = torch.empty(1, dtype=torch.int32, device="cuda")
+        ops.moe_align(re, El, sr, te, tc, tile=tile)
+        act = torch.empty(P, I, dtype=BF, device="cuda")
+        ops.moe_gemm(rx, wgu[d * El:(d + 1) * El].contiguous(), sr, te, tc, act, 2 * I, H, mt, 1, epi=ops.EPI_SILU,
+                     tile=tile)
+        y = torch.full((P, H), float("nan"), dtype=BF, device="cuda")
+        ops.moe_gemm(act, wd[d * El:(d + 1) * El].contiguous(), sr, te, tc, y, H, I, mt, 1, tile=tile)
+        y_recv.append(y)
+    for r in range(n):
+        y_back = torch.cat([y_recv[d][r * cap:(r + 1) * cap] for d in range(n)])
+        ops.moe_combine(y_back, ws[r], idss[r], hs[r], rows=plans[r][2])
+        close(hs[r], hrefs[r], 3e-2)
+
+
 @pytest.mark.parametrize("T,tile", [(700, 128), (1500, 256), (2600, 256)])
 def test_moe_grouped_gemm_ragged(cuda, T, tile):
     """The grouped expert GEMM on ragged groups: the router is skewed so two experts take most

@@ -235,3 +235,23 @@ def test_lone_engine_rule_follows_the_placement():
         assert bench.responder_alone([{"ranks": [0]}, {"ranks": [1]}, {"ranks": [2]}], [1]) is False
     finally:
         del os.environ["LLMC_BENCH_SAME_GPU"]
+
+
+def test_judge_that_also_responds_is_treated_as_a_responder():
+    """a judge named in --models decodes during the fan-out too. Pinned (--judge-tp)
+    onto the responders' GPUs it must neither take the fused row-parallel all-reduce nor the
+    lone-engine launch forms, and the responders beside it are not alone either."""
+    from llm_consensus_amd.parallel.placement import alone_plan, fused_ar_plan
+
+    gpus = {"judge": [0, 1], "r1": [1], "r2": [2]}
+    # judge-only: it decodes after the fan-out, alone on its GPUs
+    assert fused_ar_plan(gpus, "judge")["judge"] is True
+    assert alone_plan(gpus, "judge")["judge"] is True
+    assert alone_plan(gpus, "judge")["r1"] is True  # the judge does not decode during the fan-out
+    # the judge also answers: it shares GPU 1 with r1 while both decode
+    resp = ["judge", "r1", "r2"]
+    assert fused_ar_plan(gpus, "judge", responders=resp)["judge"] is False
+    a = alone_plan(gpus, "judge", responders=resp)
+    assert a["judge"] is False and a["r1"] is False and a["r2"] is True
+    # a judge that answers but shares no GPU stays alone
+    assert alone_plan({"judge": [0], "r1": [1]}, "judge", responders=["judge", "r1"])["judge"] is True

@@ -9,7 +9,12 @@ the collective resync a new request must reproduce a clean run's tokens bit for 
 
 Two layouts: both ranks on ONE GPU, each on its own half of the CUs (``LLMC_CU_MASK``, fused
 all-reduce forced: ``LLMC_FUSED_AR=force``), as the rehearsals run a TP group; and — gated on
-``torch.cuda.device_count() >= 2`` — rank i on ``cuda:i`` over RCCL."""
+``torch.cuda.device_count() >= 2`` — rank i on ``cuda:i`` over RCCL.
+
+Two more cases, on the one-GPU layout: a rank that STALLS for longer than the spin bound
+and then goes on (both requests fail at the replay where the survivor's spin gave up, and no token
+computed after the give-up is streamed on either rank), and a prefill that runs longer than the
+host's replay deadline (``Engine.stall_s``): the decode waits for it instead of aborting the group."""
 
 import os
 import socket
@@ -32,7 +37,7 @@ def _free_port():
     return p
 
 
-def _worker(rank, world, port, layout, q):
+def _worker(rank, world, port, layout, q, case="dead"):
     import datetime
 
     import torch.distributed as dist
@@ -61,6 +66,16 @@ def _worker(rank, world, port, layout, q):
         e = Engine(FAMILIES["llama-small"], EngineConfig(device=dev, max_context=1024, seed=5), tp=tp)
         e.warmup_graphs()
         ref = e.generate_ids(PROMPT, 24, temperature=0.0, stop_on_eos=False)
+        if case == "long_prefill":
+            q.put((rank,) + _long_prefill(e, ref))
+            dist.barrier()
+            dist.destroy_process_group()
+            return
+        if case == "stall":
+            q.put((rank,) + _stall(e, tp, rank))
+            dist.barrier()
+            dist.destroy_process_group()
+            return
         checks = []
         orig = tp.check_collectives
 
@@ -90,11 +105,66 @@ def _worker(rank, world, port, layout, q):
         q.put((rank, repr(ex) + traceback.format_exc(), -1.0, False, [], True))
 
 
-def _run(layout):
+def _stall(e, tp, rank):
+    """Rank 1 sleeps 3 s (> the 1-s spin bound) before the replay that would produce token 100,
+    then goes on. -> (error, seconds, streamed tokens, clean-run tokens, request after resync ok)."""
+    from llm_consensus_amd.engine import EngineError
+
+    long_ref = e.generate_ids(PROMPT, 200, temperature=0.0, stop_on_eos=False)
+    if rank == 1:
+        e.fault_at = ("decode", 100, 3.0)
+    streamed = []
+    t0 = time.monotonic()
+    err = None
+    try:
+        e.generate_ids(PROMPT, 600, temperature=0.0, stop_on_eos=False, on_tokens=streamed.extend)
+    except EngineError as ex:
+        err = f"{type(ex).__name__}: {ex}"
+    dt = time.monotonic() - t0
+    again = e.generate_ids(PROMPT, 200, temperature=0.0, stop_on_eos=False)
+    torch.cuda.synchronize()
+    return err, dt, streamed, long_ref, again == long_ref and not tp.custom_timed_out()
+
+
+def _long_prefill(e, ref):
+    """Work queued behind the prefill on the engine's stream takes ~4x the host's replay deadline:
+    the decode must wait for it (not abort the collectives / break the group) and match ``ref``.
+    -> (tokens match, group not broken, deadline s, queued work s)."""
+    from llm_consensus_amd import ops
+
+    x = torch.randn(4096, 4096, device=e.device).to(torch.bfloat16)
+    y = torch.empty_like(x)
+
+    def busy(n):
+        with e._on_stream():
+            for _ in range(n):
+                ops.linear(x, x, ops.EPI_BF16, out=y)
+
+    busy(2)
+    e.stream.synchronize()
+    t0 = time.monotonic()
+    busy(20)
+    e.stream.synchronize()
+    per = (time.monotonic() - t0) / 20
+    n = max(20, int(0.8 / per))  # ~0.8 s of queued work
+    e.stall_s = 0.2
+    orig = e.prefill
+
+    def prefill(*a, **k):
+        orig(*a, **k)
+        busy(n)
+
+    e.prefill = prefill
+    toks = e.generate_ids(PROMPT, 24, temperature=0.0, stop_on_eos=False)
+    torch.cuda.synchronize()
+    return toks == ref, e.tp.broken is None, e.stall_s, n * per
+
+
+def _run(layout, case="dead"):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, 2, port, layout, q)) for r in range(2)]
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, layout, q, case)) for r in range(2)]
     for p in procs:
         p.start()
     try:
@@ -127,3 +197,20 @@ def test_tp_rank_stopping_mid_decode_fails_fast_across_devices():
     if not torch.cuda.is_available() or torch.cuda.device_count() < 2:
         pytest.skip(f"needs 2 GPUs, this box has {torch.cuda.device_count()}")
     _check(_run("devices"))
+
+
+def test_tp_rank_stalling_past_the_spin_bound_fails_before_streaming_stale_tokens(cuda):
+    res = _run("cu_split", "stall")
+    for rank, err, dt, streamed, long_ref, again_ok in res:
+        assert err and err.startswith("EngineError"), res
+        assert dt < 15, (rank, dt)
+        # tokens up to the give-up are the clean run's; none computed after it reached the client
+        assert len(streamed) <= 105 and streamed == long_ref[:len(streamed)], (rank, len(streamed))
+        assert again_ok, rank
+
+
+def test_tp_prefill_longer_than_the_replay_deadline_is_not_a_stall(cuda):
+    res = _run("cu_split", "long_prefill")
+    for rank, same, not_broken, stall_s, work_s in res:
+        assert work_s > 2 * stall_s, (rank, stall_s, work_s)
+        assert same and not_broken, res

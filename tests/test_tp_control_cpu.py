@@ -199,6 +199,12 @@ def _timeout_worker(rank, world, port, q):
             def timed_out(self):
                 return self.tmo
 
+            def host_timed_out(self):
+                return self.tmo
+
+            def aborted(self):
+                return False
+
             def resync(self):
                 self.resyncs += 1
                 self.tmo = False

@@ -38,6 +38,7 @@
 //
 // Every spin is bounded: a give-up sets the fault word (checked by the engine like attn_decode's).
 #include "attn_core.h"
+#include "car_proto.h"
 
 namespace llmc {
 
@@ -80,7 +81,7 @@ __global__ __launch_bounds__(kAoThreads) void attn_oproj_kernel(
     const bf16_t* __restrict__ w_o, int K_o, bf16_t* __restrict__ h, bf16_t* __restrict__ attn_out,
     float* __restrict__ part, uint32_t* __restrict__ handoff, uint64_t* __restrict__ tile_part, int* __restrict__ ctr,
     int* __restrict__ fault, int nkv, int bs, int nblocks, int chunk, float scale_log2,
-    uint64_t* __restrict__ stamps, int defer) {
+    uint64_t* __restrict__ stamps, int defer, int add_resid, CarArgs ar) {
   static_assert(G * D == 512, "one 16-B column chunk per lane per row");
   static_assert(RW >= 1 && RW <= 32 && (RW & (RW - 1)) == 0, "rows per wave: power of two <= 32");
   static_assert(SUBS == 1 || (SUBS == 2 && LATE), "two sub-tiles per wave only with late weights (registers)");
@@ -299,7 +300,7 @@ __global__ __launch_bounds__(kAoThreads) void attn_oproj_kernel(
       for (int m = LPR / 2; m >= 1; m >>= 1) s[0] += __shfl_xor(s[0], m, 64);
       if ((lane % LPR) == 0) {
         bf16_t* hp = h + (g * nc + c) * (R / FR) + wave * RWF + lane / LPR;
-        *hp = f32_to_bf16(bf16_to_f32(*hp) + s[0]);
+        *hp = f32_to_bf16((add_resid ? bf16_to_f32(*hp) : 0.f) + s[0]);
       }
       ao_stamp(stp, 5, tid == 0);
     }
@@ -355,8 +356,59 @@ __global__ __launch_bounds__(kAoThreads) void attn_oproj_kernel(
     for (int gg = 0; gg < kAoMaxKv; ++gg)
       if (gg < nkv) sum += __uint_as_float(static_cast<uint32_t>(v[gg]));
     bf16_t* hp = h + c * R + ct;
-    *hp = f32_to_bf16(bf16_to_f32(*hp) + sum);
+    const float val = (add_resid ? bf16_to_f32(*hp) : 0.f) + sum;
+    if (ar.world > 1) {
+      red[ct] = val;  // the tile's row values (the attention state area is free by now)
+    } else {
+      *hp = f32_to_bf16(val);
+    }
     ao_stamp(stp, 7, ct == 0);
+  }
+  if (ar.world > 1) {
+    // ---- a tensor-parallel rank: the all-reduce of the tile's R rows in this epilogue (car_proto.h
+    // push protocol, gemv_core.h EPI_AR's exchange): every rank's reducer of tile c owns the same
+    // rows, pushes its bf16 row pairs (rank 0's carry the residual) into every peer's buffer as
+    // data-tagged granules and sums the peers' in rank order as they land — the bits of this
+    // launch's partial + the one-shot all-reduce, without that launch. The tile's R / 2 granules are
+    // R / 32 "virtual blocks" of kArGranulesPerBlock, vb = c R / 32 + i, each with its own epoch
+    // word (the row-parallel GEMVs' EPI_AR blocks use the same buffer and words: every use of vb
+    // advances its epoch by one on every rank, in the same stream order).
+    __syncthreads();
+    if (wave == 4) {
+      constexpr int NG = R / 2, NVB = NG / kArGranulesPerBlock;
+      static_assert(NG % kArGranulesPerBlock == 0 && NG <= kWave, "tile granules");
+      const int gi = lane < NG ? lane : 0;
+      const int vb = c * NVB + gi / kArGranulesPerBlock;
+      const long gidx = static_cast<long>(vb) * kArGranulesPerBlock + gi % kArGranulesPerBlock;
+      const uint32_t ep = __hip_atomic_load(car_ctr(ar.P.base[ar.rank]) + vb, __ATOMIC_RELAXED,
+                                            __HIP_MEMORY_SCOPE_SYSTEM) + 1u;
+      const uint32_t mine = pack_bf16x2(red[2 * gi], red[2 * gi + 1]);
+      for (int idx = lane; idx < ar.world * NG; idx += kWave) {  // push: (peer, granule)
+        const int p = idx / NG, g2 = idx % NG;
+        const uint32_t e2 = __shfl(ep, g2, 64);
+        const uint32_t pay = __shfl(mine, g2, 64);
+        const long gi2 = static_cast<long>(c * NVB + g2 / kArGranulesPerBlock) * kArGranulesPerBlock +
+                         g2 % kArGranulesPerBlock;
+        if (p != ar.rank) car_put(ar.P.base[p] + car_granule_off(e2, ar.cap, ar.rank, gi2), pay, e2);
+      }
+      if (lane < NG) {  // collect every peer's granule of my row pair, sum in rank order
+        const long g[1] = {gidx};
+        uint32_t in[kMaxRanks][1];
+        car_collect<1>(ar.P, ar.rank, ar.world, ar.cap, ep, g, in);
+        in[ar.rank][0] = mine;
+        float lo = 0.f, hi = 0.f;
+#pragma unroll
+        for (int r = 0; r < kMaxRanks; ++r) {
+          if (r < ar.world) {
+            lo += bf16_lo(in[r][0]);
+            hi += bf16_hi(in[r][0]);
+          }
+        }
+        *reinterpret_cast<uint32_t*>(h + c * R + 2 * lane) = pack_bf16x2(lo, hi);
+        if (lane % kArGranulesPerBlock == 0)
+          __hip_atomic_store(car_ctr(ar.P.base[ar.rank]) + vb, ep, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      }
+    }
   }
   if (ct == 0) {
     __hip_atomic_store(tctr, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // re-arm the tile ticket
@@ -405,13 +457,33 @@ extern "C" int llmc_attn_oproj_check(int H, int nh, int nkv, int D, int nc, int 
 // 5 o wave 0's tile partial published, 6 tile ticket taken, 7 tile reduced (reducer only).
 // Workspace (zeroed once): part f32 [nkv][nc][G][D/4 + 1][4]; handoff u32 [nkv][G D / 4][4];
 // tile_part u64 [nc][nkv][H / nc]; ctr int32 [(nkv + nc + 1) * 16].
+// Tensor-parallel ranks (h = this rank's row-parallel partial of the sum over ranks): add_resid = 0
+// writes h = W_o . attention instead of adding (a rank != 0 whose all-reduce follows as its own
+// launch); world > 1 runs the all-reduce in the tile reducers' epilogue (car_proto.h push protocol
+// over `bases` = every rank's fused-all-reduce buffer, `cap` bytes per data parity, host status
+// page `host`): h = sum over ranks, rank 0's term carrying the residual (add_resid = rank == 0).
+// The whole-row form (mode bit 2) has no tile reducer: never with world > 1.
 extern "C" int llmc_attn_oproj(const void* q, const void* k_cache, const void* v_cache, const void* block_table,
                                int bt_len, const void* seq_len, const void* w_o, void* h, void* attn_out, void* part,
                                void* handoff, void* tile_part, void* ctr, void* fault, int H, int nh, int nkv, int D,
                                int bs, int nblocks, int chunk, int nc, float scale, int mode, void* stamps,
+                               int add_resid, const void* const* bases, void* host, int rank, int world, size_t cap,
                                hipStream_t s) {
   const int K_o = nh * D;
   if (llmc_attn_oproj_check(H, nh, nkv, D, nc, K_o) != 0) return -1;
+  CarArgs ar{};
+  if (world > 1) {
+    if (world > kMaxRanks || rank < 0 || rank >= world || bases == nullptr) return -1;
+    const int vbs = nc * (H / nc / 2) / kArGranulesPerBlock;  // virtual blocks of the tiles' granules
+    if ((H / nc / 2) % kArGranulesPerBlock != 0 || vbs > kMaxBlocks ||
+        static_cast<size_t>(vbs) * kArGranulesPerBlock * 8 > cap / kMaxRanks)
+      return -6;
+    for (int r = 0; r < kMaxRanks; ++r) ar.P.base[r] = r < world ? static_cast<char*>(const_cast<void*>(bases[r])) : nullptr;
+    ar.P.host = static_cast<uint32_t*>(host);
+    ar.rank = rank;
+    ar.world = world;
+    ar.cap = static_cast<long>(cap);
+  }
   // up to 256 keys per block: one 32-key sub-tile per wave; up to 512: two (late weights only)
   const bool two = chunk > kAoWaves * 32;
   if (chunk < 32 || chunk > kAoWaves * 64 || chunk % (two ? 64 : 32) != 0 || bs % (two ? 64 : 32) != 0 ||
@@ -419,7 +491,8 @@ extern "C" int llmc_attn_oproj(const void* q, const void* k_cache, const void* v
     return -1;
   const bool late = (mode & 1) != 0 || two;  // o_proj weights issued after the head ticket
   const int G = nh / nkv, rw = H / nc / 4;
-  const bool fr = (mode & 4) != 0 && late && nkv == kAoMaxKv && G == 4 && D == 128 && rw == 32;  // full rows
+  const bool fr = (mode & 4) != 0 && late && nkv == kAoMaxKv && G == 4 && D == 128 && rw == 32 &&
+                  world <= 1;  // full rows (no tile reducer to run the all-reduce)
   const size_t lds = kAoWaves * 32 * kVRowBytes + static_cast<size_t>(kAoWaves) * G * (D + 2) * sizeof(float) +
                      (fr ? kAoMaxKv : 1) * 64 * 16 + 16;
   dim3 grid(nc, nkv);
@@ -431,7 +504,7 @@ extern "C" int llmc_attn_oproj(const void* q, const void* k_cache, const void* v
       (const bf16_t*)q, (const bf16_t*)k_cache, (const bf16_t*)v_cache, (const int32_t*)block_table, bt_len,       \
       (const int32_t*)seq_len, (const bf16_t*)w_o, K_o, (bf16_t*)h, (bf16_t*)attn_out, (float*)part,               \
       (uint32_t*)handoff, (uint64_t*)tile_part, (int*)ctr, (int*)fault, nkv, bs, nblocks, chunk, sl2, (uint64_t*)stamps, \
-      (mode >> 1) & 1); \
+      (mode >> 1) & 1, add_resid, ar); \
   } while (0)
 #define LLMC_AO(GG, DD, RR)                                                                                      \
   do {                                                                                                            \

@@ -39,7 +39,7 @@ int llmc_qkv_attn(const void*, const void*, float, const void*, int, void*, void
 int llmc_attn_oproj_check(int, int, int, int, int, int);
 int llmc_attn_oproj(const void*, const void*, const void*, const void*, int, const void*, const void*, void*, void*,
                     void*, void*, void*, void*, void*, int, int, int, int, int, int, int, int, float, int, void*,
-                    hipStream_t);
+                    int, const void* const*, void*, int, int, size_t, hipStream_t);
 int llmc_attn_decode(const void*, int, const void*, const void*, const void*, int, const void*, void*, void*, void*,
                      int, int, int, int, int, int, int, int, int, int, float, int, void*, hipStream_t);
 int llmc_gemv_qkv_rope(int, const void*, int, const void*, float, const void*, int, int, void*, int, void*, void*,
@@ -161,10 +161,13 @@ PYBIND11_MODULE(_llmc_hip, m) {
   });
   m.def("attn_oproj", [](ptr q, ptr kc, ptr vc, ptr bt, int bt_len, ptr sl, ptr w_o, ptr h, ptr attn_out, ptr part,
                          ptr handoff, ptr tile_part, ptr ctr, ptr fault, int H, int nh, int nkv, int D, int bs,
-                         int nblocks, int chunk, int nc, float scale, int mode, ptr stamps, ptr s) {
+                         int nblocks, int chunk, int nc, float scale, int mode, ptr stamps, int add_resid,
+                         const std::vector<ptr>& bases, ptr host, int rank, int world, size_t cap, ptr s) {
+    std::vector<const void*> b(bases.size());
+    for (size_t i = 0; i < bases.size(); ++i) b[i] = P(bases[i]);
     check(llmc_attn_oproj(P(q), P(kc), P(vc), P(bt), bt_len, P(sl), P(w_o), P(h), P(attn_out), P(part), P(handoff),
                           P(tile_part), P(ctr), P(fault), H, nh, nkv, D, bs, nblocks, chunk, nc, scale, mode, P(stamps),
-                          S(s)),
+                          add_resid, b.empty() ? nullptr : b.data(), P(host), rank, world, cap, S(s)),
           "attn_oproj");
   });
   m.def("attn_decode", [](ptr q, int qs, ptr kc, ptr vc, ptr bt, int bts, ptr sl, ptr part, ptr ctr, ptr out, int os,

@@ -64,6 +64,21 @@ __global__ __launch_bounds__(kRouterThreads) void moe_router_kernel(
   const int t = blockIdx.x, tid = threadIdx.x, wave = tid / kWave, lane = tid % kWave;
   const int nchunk = H / 8;
   const bf16_t* xr = x + static_cast<int64_t>(t) * x_stride;
+  // The router weights do not depend on x: with one expert per wave (E <= 8 waves) the wave's whole
+  // row is requested FIRST, so its HBM round trip overlaps the x load and the norm instead of
+  // following them (one memory round trip on the launch's chain instead of two; Mixtral: E = 8,
+  // H = 4096 -> 8 chunks per lane). x and the norm weights are issued right behind.
+  constexpr int kPre = 16;  // chunks per lane preloaded (H <= 8192)
+  const bool pre = E <= WAVES && nchunk <= kPre * kWave;  // block-uniform
+  u32x4 wpre[kPre];
+  if (pre && wave < E) {
+    const u32x4* wr = reinterpret_cast<const u32x4*>(Wr + static_cast<int64_t>(wave) * H);
+#pragma unroll
+    for (int i = 0; i < kPre; ++i) {
+      const int c = lane + i * kWave;
+      if (c < nchunk) wpre[i] = load16<true>(wr + c);
+    }
+  }
   u32x4 xv[2], gv[2];
   float ss = 0.f;
 #pragma unroll
@@ -99,12 +114,25 @@ __global__ __launch_bounds__(kRouterThreads) void moe_router_kernel(
   }
   __syncthreads();
   const u32x4* xsv = reinterpret_cast<const u32x4*>(xs);
-  for (int e = wave; e < E; e += WAVES) {
+  if (pre) {
+    if (wave < E) {
+      float acc = 0.f;  // same chunk order as the loop below: bit-identical logits
+#pragma unroll
+      for (int i = 0; i < kPre; ++i) {
+        const int c = lane + i * kWave;
+        if (c < nchunk) acc = dot8_bf16(wpre[i], xsv[c], acc);
+      }
+      acc = wave_sum(acc);
+      if (lane == 0) logit[wave] = acc;
+    }
+  } else {
+    for (int e = wave; e < E; e += WAVES) {
     const u32x4* wr = reinterpret_cast<const u32x4*>(Wr + static_cast<int64_t>(e) * H);
     float acc = 0.f;
     for (int c = lane; c < nchunk; c += kWave) acc = dot8_bf16(load16<true>(wr + c), xsv[c], acc);
     acc = wave_sum(acc);
     if (lane == 0) logit[e] = acc;
+    }
   }
   __syncthreads();
   if (tid == 0) {

@@ -64,9 +64,11 @@ class EngineConfig:
     # (csrc/kernels/attn_oproj.hip) in the context buckets with at least ``attn_oproj_min_chunk``
     # keys per block (ops.ATTN_OPROJ_MIN_CHUNK: where it measured faster than the two launches).
     # Environment defaults (A/B runs): LLMC_ATTN_OPROJ=0 never, =all every bucket it covers.
-    # Tensor-parallel ranks never take it (their 1-2 kv heads make the merge the long pole and the
-    # o_proj it would hide is small: profiles/r3_attn_oproj.md)
     attn_oproj: bool = dataclasses.field(default_factory=lambda: os.environ.get("LLMC_ATTN_OPROJ", "1") != "0")
+    # tensor-parallel ranks too: the rank's o_proj share as the launch's partial, its all-reduce in
+    # the kernel's tile-reducer epilogue when the group has the fused buffer (``fused_ar``), else the
+    # separate all-reduce launch after it (LLMC_TP_ATTN_OPROJ=0: the two launches, A/B runs)
+    tp_attn_oproj: bool = dataclasses.field(default_factory=lambda: os.environ.get("LLMC_TP_ATTN_OPROJ", "1") != "0")
     attn_oproj_min_chunk: int = dataclasses.field(default_factory=ops.attn_oproj_min_chunk)
     # one-row engines: the qkv projection and the decode attention as ONE launch in the buckets of
     # the fused attention form (csrc/kernels/qkv_attn.hip). "1": shards whose qkv output is under
@@ -307,7 +309,8 @@ class Engine:
         # two launches)
         self.ao_chunks: List[int] = [0] * len(self.attn_buckets)
         self.ao_nc = 0
-        if self.on_gpu and self.ecfg.attn_oproj and B == 1 and self.bs % 32 == 0 and self.tp.size == 1:
+        if (self.on_gpu and self.ecfg.attn_oproj and B == 1 and self.bs % 32 == 0
+                and (self.tp.size == 1 or self.ecfg.tp_attn_oproj)):
             self.ao_nc = ops.attn_oproj_grid(c.hidden, self.nh, self.nkv, self.D)
             if self.ao_nc:
                 lo = self.ecfg.attn_oproj_min_chunk
@@ -664,10 +667,8 @@ class Engine:
                 ops.qkv_rope(h, Lw.w_qkv, Lw.ln1, c.rms_eps, q, self.k_cache[li], self.v_cache[li],
                              self.positions[:B], self.slots[:B], self.cos_t, self.sin_t, self.nh, self.nkv, self.D,
                              self.bs, mfma=self.mfma_decode)
-                if ao_chunk:  # one-row engines without TP: attention + o_proj + residual in one launch
-                    ops.attn_oproj(q, self.k_cache[li], self.v_cache[li], self.block_tables[:1], self.seq_lens[:1],
-                                   Lw.w_o, h, attn, self.ao_ws, self.nh, self.nkv, self.D, self.bs, ao_chunk, self.ao_nc,
-                                   self.scale, fault=self.attn_fault)
+                if ao_chunk:  # one-row engines: attention + o_proj + residual (+ TP all-reduce) in one launch
+                    self._attn_oproj(q, li, Lw, h, attn, ao_chunk)
                 else:
                     ops.attn_decode(q, self.k_cache[li], self.v_cache[li], self.block_tables[:B], self.seq_lens[:B],
                                     attn, part[:B], self.attn_counters[:B], self.nh, self.nkv, self.D, self.bs, chunk,
@@ -683,6 +684,19 @@ class Engine:
         self._lm_head_sample(B)
 
     _debug_layer_io: Optional[list] = None
+
+    def _attn_oproj(self, q, li, Lw, h, attn, chunk) -> None:
+        """h += o_proj(attention(q)) for one row in one launch (csrc/kernels/attn_oproj.hip). A TP rank
+        computes its row-parallel share (rank 0's carries the residual) and all-reduces it inside the
+        kernel when the group has the fused buffer (``fused_ar``), else with the group's all-reduce
+        launch after it."""
+        tp = self.tp
+        car = tp.custom_fused if (tp.size > 1 and self.ecfg.fused_ar) else None
+        ops.attn_oproj(q, self.k_cache[li], self.v_cache[li], self.block_tables[:1], self.seq_lens[:1], Lw.w_o, h, attn,
+                       self.ao_ws, self.nh, self.nkv, self.D, self.bs, chunk, self.ao_nc, self.scale,
+                       fault=self.attn_fault, add_resid=tp.rank == 0, car=car)
+        if tp.size > 1 and car is None:
+            tp.all_reduce_(h)
 
     @torch.no_grad()
     def debug_decode_layers(self, prompt: Seq[int]):

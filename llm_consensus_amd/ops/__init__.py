@@ -368,7 +368,8 @@ def attn_oproj_workspace(H: int, nh: int, nkv: int, D: int, nc: int, device):
 
 
 def attn_oproj(q, k_cache, v_cache, block_table, seq_len, w_o, h, attn_out, ws, nh, nkv, D, bs, chunk, nc, scale,
-               fault: Optional[torch.Tensor] = None, stamps: Optional[torch.Tensor] = None, mode: int = -1) -> None:
+               fault: Optional[torch.Tensor] = None, stamps: Optional[torch.Tensor] = None, mode: int = -1,
+               add_resid: bool = True, car=None) -> None:
     """Decode attention of ONE row followed by its o_proj and residual add, in one launch
     (csrc/kernels/attn_oproj.hip): ``h[0] += w_o @ attention(q[0])``; ``attn_out[0]`` also gets the
     attention output. ``ws`` = ``attn_oproj_workspace(...)``; ``chunk`` = ``attn_oproj_chunk(cap,
@@ -376,20 +377,30 @@ def attn_oproj(q, k_cache, v_cache, block_table, seq_len, w_o, h, attn_out, ws, 
     ``stamps`` (diagnostics): int64 [nkv, nc, 8] per-block phase times (see the kernel's host
     function); ``mode`` bit 0: o_proj weights requested after the head ticket, bit 1 (with bit 0):
     the head's merger requests its own after the merge, bit 2 (with bit 0; 8 kv heads, G = 4, D =
-    128, 128-row tiles, else ignored): whole o_proj rows per block (-1 = ATTN_OPROJ_MODE)."""
+    128, 128-row tiles, else ignored): whole o_proj rows per block (-1 = ATTN_OPROJ_MODE).
+
+    Tensor-parallel ranks (``h`` gets this rank's row-parallel share): ``add_resid`` False writes
+    h = W_o . attention (a rank != 0 whose all-reduce follows as its own launch); ``car`` (the
+    group's fused-all-reduce ``CustomAllReduce``) runs the all-reduce in the kernel's tile-reducer
+    epilogue: h = the sum over ranks, rank 0's term carrying the residual (pass add_resid = rank 0)."""
     H = h.shape[-1]
     if not q.is_cuda:
+        if car is not None:
+            raise ValueError("attn_oproj: the fused all-reduce runs on GPU ranks only")
         a = oracle.attn_decode(q[:1], k_cache, v_cache, block_table[:1], seq_len[:1], nh, nkv, D, bs, scale)
         attn_out[:1].copy_(a)
-        oracle.linear(attn_out[:1], w_o, EPI_RESADD, h[:1])
+        oracle.linear(attn_out[:1], w_o, EPI_RESADD if add_resid else EPI_BF16, h[:1])
         return
     if chunk <= 0 or chunk * nc < 1 or nc != ws[0].shape[1]:
         raise ValueError("attn_oproj: chunk / workspace do not match (attn_oproj_chunk, attn_oproj_workspace)")
     part, handoff, tile_part, counters = ws
+    bases, host, rank, world, cap = (([], 0, 0, 1, 0) if car is None else
+                                     (car.bases, car.host_dev, car.rank, car.world, car.cap))
     kernels().attn_oproj(_p(q), _p(k_cache), _p(v_cache), _p(block_table), block_table.shape[-1], _p(seq_len), _p(w_o),
                          _p(h), _p(attn_out), _p(part), _p(handoff), _p(tile_part), _p(counters), _p(fault), H, nh, nkv,
                          D, bs, k_cache.shape[0], chunk, nc, float(scale),
-                         ATTN_OPROJ_MODE if mode < 0 else mode, _p(stamps), _s(h))
+                         ATTN_OPROJ_MODE if mode < 0 else mode, _p(stamps), int(bool(add_resid)), bases, host, rank,
+                         world, cap, _s(h))
 
 
 # KV split of the prefill attention: -1 = the kernel library's plan (llmc_attn_prefill_plan),

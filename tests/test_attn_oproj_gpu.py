@@ -206,3 +206,34 @@ def test_engine_attn_oproj_matches_two_launch_step(cuda, name, plen, monkeypatch
     b = ee.generate_ids(prompt, 24, temperature=0.8, seed=7, stop_on_eos=False)
     assert a == b
     assert int(ea.attn_fault.item()) == 0
+
+
+@pytest.mark.parametrize("nh,nkv,D,H", [(4, 1, 128, 4096), (8, 2, 128, 4096), (16, 4, 128, 4096)])
+@pytest.mark.parametrize("L,cap", [(7, 1024), (1000, 1024), (2048, 2048), (3000, 4096)])
+@pytest.mark.parametrize("add_resid", [True, False])
+def test_attn_oproj_tp_rank_shapes(cuda, nh, nkv, D, H, L, cap, add_resid):
+    """The Llama-3-8B TP=8 / 4 / 2 rank shapes (1-4 kv heads, the tile-reduce form) vs the fp32
+    oracle: rank 0 adds its share to the residual, the other ranks' launches write the share alone
+    (their all-reduce follows; the fused all-reduce epilogue is covered by tests/test_tp_gpu.py)."""
+    bs = 64
+    nc = ops.attn_oproj_grid(H, nh, nkv, D)
+    assert nc > 0
+    chunk = ops.attn_oproj_chunk(cap, nc)
+    assert chunk and chunk * nc >= L
+    kc, vc, bt, sl, q, w_o, h0 = _case(L, nh, nkv, D, H, bs)
+    scale = 1 / math.sqrt(D)
+    a_ref, h_ref = _reference(kc, vc, bt, sl, q, w_o, h0, nh, nkv, D, bs, scale)
+    if not add_resid:
+        h_ref = h_ref - h0.cpu().float()
+    ws = ops.attn_oproj_workspace(H, nh, nkv, D, nc, "cuda")
+    fault = torch.zeros(1, dtype=torch.int32, device="cuda")
+    for it in range(2):
+        h = h0.clone()
+        attn = torch.zeros(1, nh * D, dtype=BF, device="cuda")
+        ops.attn_oproj(q, kc, vc, bt.cuda(), sl.cuda(), w_o, h, attn, ws, nh, nkv, D, bs, chunk, nc, scale, fault=fault,
+                       add_resid=add_resid)
+        torch.cuda.synchronize()
+        assert int(fault.item()) == 0
+        assert (attn.float().cpu() - a_ref.float()).abs().max().item() < 2e-2
+        err_h = (h.float().cpu() - h_ref).abs().max().item()
+        assert err_h < 2e-2 * max(1.0, h_ref.abs().max().item()), (it, err_h)

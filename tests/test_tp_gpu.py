@@ -41,7 +41,10 @@ def _worker(rank, world, port, name, q, ekw=None):
         tp.enable_custom("cuda:0")
         if ekw.pop("_expect_fused", False):
             assert tp.custom_fused is not None
+        expect_ao = ekw.pop("_expect_ao", False)
         e = Engine(FAMILIES[name], EngineConfig(device="cuda:0", max_context=512, seed=5, **ekw), tp=tp)
+        if expect_ao:  # the fused attention + o_proj launch runs on this TP rank's decode buckets
+            assert all(e.ao_chunks), e.ao_chunks
         e.warmup_graphs()
         s = e.new_sequence()
         e.prefill([s], [PROMPT])
@@ -81,6 +84,22 @@ def test_tp2_gpu_fused_allreduce_cu_partitioned_matches_tp1(cuda, monkeypatch):
     chip (EngineConfig.cu_mask via LLMC_CU_MASK, as scripts/tp_rehearsal.py runs a TP group)."""
     monkeypatch.setenv("LLMC_FUSED_AR", "force")
     _tp2_vs_tp1("llama-small", {"_expect_fused": True, "_cu_split": True})
+
+
+def test_tp2_gpu_attn_oproj_fused_allreduce_matches_tp1(cuda, monkeypatch):
+    """TP ranks on the one-launch attention + o_proj (every bucket: LLMC_ATTN_OPROJ=all) with the
+    all-reduce in the kernel's tile-reducer epilogue (attn_oproj.hip, car_proto.h push protocol),
+    each rank on its own half of the chip."""
+    monkeypatch.setenv("LLMC_FUSED_AR", "force")
+    monkeypatch.setenv("LLMC_ATTN_OPROJ", "all")
+    _tp2_vs_tp1("llama-small", {"_expect_fused": True, "_cu_split": True, "_expect_ao": True})
+
+
+def test_tp2_gpu_attn_oproj_separate_allreduce_matches_tp1(cuda, monkeypatch):
+    """... and with the rank's partial (rank 0: + residual) followed by the group's all-reduce launch."""
+    monkeypatch.setenv("LLMC_FUSED_AR", "0")
+    monkeypatch.setenv("LLMC_ATTN_OPROJ", "all")
+    _tp2_vs_tp1("llama-small", {"_expect_ao": True})
 
 
 def _tp2_vs_tp1(name, ekw):

@@ -783,6 +783,14 @@ def main() -> None:
                 r = [t - 1 for t in table[i].tolist() if t > 0]
                 rtok = get_tokenizer(FAMILIES[e["family"]].vocab)
                 responses.append(Response(model=e["name"], content=rtok.decode(r), provider="rocm"))
+            # Why every response block is prefilled here, after the LAST response, while the product
+            # path (provider/local.py) extends the judge session as EACH response
+            # completes: (1) on N > 1 ranks the blocks must be identical and in the same order on
+            # every judge rank, and the responses only meet on every rank through the collective
+            # gather above; (2) the bench's responders all decode exactly max_tokens, so they
+            # complete within milliseconds of each other and the product path also has every block
+            # left to prefill once the last one lands. The product path itself is timed by
+            # `--path cli` (within +0.5 % of this engine path).
             full = build_judge_prompt(prompt_text, responses)
             head = prompt_header(prompt_text)
             rest_ids = jtok.encode(full[len(head):])

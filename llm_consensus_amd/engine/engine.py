@@ -68,7 +68,12 @@ class EngineConfig:
     # tensor-parallel ranks too: the rank's o_proj share as the launch's partial, its all-reduce in
     # the kernel's tile-reducer epilogue when the group has the fused buffer (``fused_ar``), else the
     # separate all-reduce launch after it (LLMC_TP_ATTN_OPROJ=0: the two launches, A/B runs)
-    tp_attn_oproj: bool = dataclasses.field(default_factory=lambda: os.environ.get("LLMC_TP_ATTN_OPROJ", "1") != "0")
+    # Measured slower on every 8B TP shape (MI355X, 2k keys, rank alone: TP=8 0.876 -> 1.047 ms/token,
+    # TP=4 1.143 -> 1.326; 2-rank TP=8-shaped rehearsal with collectives 1.356 -> 1.474): a rank's
+    # 1-4 kv heads make the head merge the long pole and the o_proj it hides is small, so the
+    # default keeps the one-launch qkv + attention and the o GEMV with its fused all-reduce
+    # (LLMC_TP_ATTN_OPROJ=1: A/B runs; profiles/r6_tp_decode.md)
+    tp_attn_oproj: bool = dataclasses.field(default_factory=lambda: os.environ.get("LLMC_TP_ATTN_OPROJ", "0") == "1")
     attn_oproj_min_chunk: int = dataclasses.field(default_factory=ops.attn_oproj_min_chunk)
     # one-row engines: the qkv projection and the decode attention as ONE launch in the buckets of
     # the fused attention form (csrc/kernels/qkv_attn.hip). "1": shards whose qkv output is under

@@ -1,5 +1,5 @@
-"""Expert-parallel prefill of a Mixtral-shaped MoE over 2 ranks sharing ONE GPU (gloo bootstrap,
-each rank on its own half of the CUs), for a kernel trace: the sequence-parallel expert dispatch
+"""Expert-parallel prefill of a Mixtral-shaped MoE over 2 ranks sharing ONE GPU (gloo collectives),
+for a kernel trace: the sequence-parallel expert dispatch
 (engine ``_moe_ep_a2a``: ``moe_ep_dispatch`` -> ``gather_rows`` -> all-to-all -> grouped expert
 GEMMs -> all-to-all -> ``moe_combine`` through the pair slots) and the replicated-token EP path must
 run on the llmc kernels only, with no torch sort / bincount / nonzero / index kernels and no host
@@ -16,7 +16,6 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
 
 def _worker(rank, world, port, tokens):
-    os.environ["LLMC_CU_MASK"] = f"{rank * 128}-{rank * 128 + 127}"
     import torch
     import torch.distributed as dist
 
@@ -28,8 +27,9 @@ def _worker(rank, world, port, tokens):
     dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world)
     # Mixtral's layer shape (8 experts, top-2, hidden 4096, FFN 14336) at 4 layers and a small vocab
     cfg = FAMILIES["mixtral-8x7b"].with_(name="mixtral-4l", n_layers=4, vocab=32000)
+    # gloo collectives (host bounce) only: no IPC-mapped buffers, so nothing of ours outlives the
+    # process's teardown under the profiler
     tp = TPGroup(dist.group.WORLD, rank, world)
-    tp.enable_custom("cuda:0")
     for sp in (True, False):
         e = Engine(cfg, EngineConfig(device="cuda:0", max_context=tokens + 64, seed=3, expert_parallel=True,
                                      sequence_parallel=sp, sp_min_tokens=64, use_graphs=False), tp=tp)

@@ -92,6 +92,7 @@ def test_tp2_gpu_attn_oproj_fused_allreduce_matches_tp1(cuda, monkeypatch):
     each rank on its own half of the chip."""
     monkeypatch.setenv("LLMC_FUSED_AR", "force")
     monkeypatch.setenv("LLMC_ATTN_OPROJ", "all")
+    monkeypatch.setenv("LLMC_TP_ATTN_OPROJ", "1")
     _tp2_vs_tp1("llama-small", {"_expect_fused": True, "_cu_split": True, "_expect_ao": True})
 
 
@@ -99,6 +100,7 @@ def test_tp2_gpu_attn_oproj_separate_allreduce_matches_tp1(cuda, monkeypatch):
     """... and with the rank's partial (rank 0: + residual) followed by the group's all-reduce launch."""
     monkeypatch.setenv("LLMC_FUSED_AR", "0")
     monkeypatch.setenv("LLMC_ATTN_OPROJ", "all")
+    monkeypatch.setenv("LLMC_TP_ATTN_OPROJ", "1")
     _tp2_vs_tp1("llama-small", {"_expect_ao": True})
 
 

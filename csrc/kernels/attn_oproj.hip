@@ -81,7 +81,7 @@ __global__ __launch_bounds__(kAoThreads) void attn_oproj_kernel(
     const bf16_t* __restrict__ w_o, int K_o, bf16_t* __restrict__ h, bf16_t* __restrict__ attn_out,
     float* __restrict__ part, uint32_t* __restrict__ handoff, uint64_t* __restrict__ tile_part, int* __restrict__ ctr,
     int* __restrict__ fault, int nkv, int bs, int nblocks, int chunk, float scale_log2,
-    uint64_t* __restrict__ stamps, int defer, int add_resid, CarArgs ar) {
+    uint64_t* __restrict__ stamps, int defer, int add_resid, CarArgs ar, int gate) {
   static_assert(G * D == 512, "one 16-B column chunk per lane per row");
   static_assert(RW >= 1 && RW <= 32 && (RW & (RW - 1)) == 0, "rows per wave: power of two <= 32");
   static_assert(SUBS == 1 || (SUBS == 2 && LATE), "two sub-tiles per wave only with late weights (registers)");
@@ -96,10 +96,12 @@ __global__ __launch_bounds__(kAoThreads) void attn_oproj_kernel(
   int* hctr = ctr + g * kAoLine;            // {head ticket, head epoch}
   int* tctr = ctr + (nkv + c) * kAoLine;    // {tile ticket}
   int* xctr = ctr + (nkv + nc) * kAoLine;   // {exit count, tile epoch}
+  int* gctr = ctr + (nkv + nc + 1) * kAoLine;  // {attention arrivals, weight-gate epoch} (mode bit 3)
 
   // ---- 1. one round trip: epochs, L, this wave's page id (scalar), Q (vector) ----
   const uint32_t tag_h = static_cast<uint32_t>(__hip_atomic_load(hctr + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) + 1u;
   const uint32_t tag_t = static_cast<uint32_t>(__hip_atomic_load(xctr + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) + 1u;
+  const int gate_e = gate ? __hip_atomic_load(gctr + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0;
   const int L = ld_scalar(seq_len);
   const int key_lo = c * chunk;
   const int wk0 = key_lo + wave * 32 * SUBS;  // this wave's SUBS 32-key sub-tiles (one page: bs % (32 SUBS) == 0)
@@ -189,16 +191,39 @@ __global__ __launch_bounds__(kAoThreads) void attn_oproj_kernel(
   const __amdgpu_buffer_rsrc_t rsrc = __builtin_amdgcn_make_buffer_rsrc(slab, 0, slab_rows * G * RU * 16, 0x00020000);
   if (block_keys) publish_partial<G, D, kAoWaves>(red, rsrc, c, tag_h, o_wave ? Q : ct);
   __syncthreads();  // every wave's stores are issued (the merger checks tags)
-  if (ct == kTicketThread) *flag = __hip_atomic_fetch_add(hctr, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == nc - 1;
+  if (ct == kTicketThread) {
+    *flag = __hip_atomic_fetch_add(hctr, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == nc - 1;
+    // weight gate (mode bit 3): the last block of the whole grid to finish its attention opens it
+    if (gate && __hip_atomic_fetch_add(gctr, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == nc * nkv - 1) {
+      __hip_atomic_store(gctr, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(gctr + 1, gate_e + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+  }
   __syncthreads();
   ao_stamp(stp, 3, tid == 0);
+  // Weight gate (mode bit 3, engines alone on their GPU): the o waves request their weight tile only
+  // once EVERY block of the grid has streamed its K/V, so no head's last K/V loads (the merge chain's
+  // start) queue behind other blocks' weight requests. Purely a scheduling device — no data depends
+  // on it — so the wait is short-bounded and then goes ahead regardless (never a deadlock, e.g.
+  // beside co-located engines whose blocks hold the CUs some of this grid's blocks need).
+  auto weight_gate = [&]() {
+    if (gate && lane == 0) {
+      for (unsigned spins = 0; spins < (1u << 14) &&
+                               __hip_atomic_load(gctr + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != gate_e + 1;
+           ++spins)
+        __builtin_amdgcn_s_sleep(2);
+    }
+  };
   // defer (late weights only): the head's merger requests its weight tile after the merge instead,
   // so the merge's loads do not queue behind 128 KB of weights in this CU's memory pipeline
   const bool merger_defers = LATE && defer && *flag;  // block-uniform
   if constexpr (LATE) {
     // weights behind the whole attention step: the K/V loads never queue behind them, and a wave
     // stalled issuing 32 KB of loads holds no barrier the control waves need before the next one
-    if (o_wave && !merger_defers) load_tile();
+    if (o_wave && !merger_defers) {
+      weight_gate();
+      load_tile();
+    }
   }
 
   // ---- 3. the last arriver of head g merges (control waves) and publishes head g's output ----
@@ -243,7 +268,10 @@ __global__ __launch_bounds__(kAoThreads) void attn_oproj_kernel(
   if constexpr (FR != 0) {
     if (merger_defers) {
       __syncthreads();
-      if (o_wave) load_tile();
+      if (o_wave) {
+        weight_gate();
+        load_tile();
+      }
     }
   }
   // head outputs into LDS: head g only (FR = 0: wave 4) or every head (FR: control wave 4 + k
@@ -281,7 +309,10 @@ __global__ __launch_bounds__(kAoThreads) void attn_oproj_kernel(
   __syncthreads();
   ao_stamp(stp, 4, tid == 0);
   if constexpr (LATE && FR == 0) {
-    if (o_wave && merger_defers) load_tile();
+    if (o_wave && merger_defers) {
+      weight_gate();
+      load_tile();
+    }
   }
   if constexpr (FR != 0) {
     // ---- 4'. whole rows: dot over every head group, reduce-scatter, residual add, done ----
@@ -450,13 +481,14 @@ extern "C" int llmc_attn_oproj_check(int H, int nh, int nkv, int D, int nc, int 
 // h += o_proj(attention). mode bit 0: issue the o_proj weights after the head ticket instead of
 // right behind the K/V loads; bit 1 (with late weights): the head's merger issues its own after the
 // merge; bit 2 (with late weights, 8 kv heads, G = 4, D = 128, 32-row tiles): whole o_proj rows per
-// block (FR, see the kernel).
+// block (FR, see the kernel); bit 3 (with late weights): the weight gate — no block requests its
+// weights before every block of the grid has streamed its K/V (lone engines).
 // fault codes: 1 a partial never arrived (merge), 2 the head output never arrived, 3 a tile partial.
 // stamps (nullable, diagnostics): uint64 [nkv][nc][8] s_memrealtime per block: 0 start, 1 o wave 0's
 // attention done, 2 control wave 4's attention done, 3 head ticket taken, 4 head output in LDS,
 // 5 o wave 0's tile partial published, 6 tile ticket taken, 7 tile reduced (reducer only).
 // Workspace (zeroed once): part f32 [nkv][nc][G][D/4 + 1][4]; handoff u32 [nkv][G D / 4][4];
-// tile_part u64 [nc][nkv][H / nc]; ctr int32 [(nkv + nc + 1) * 16].
+// tile_part u64 [nc][nkv][H / nc]; ctr int32 [(nkv + nc + 2) * 16].
 // Tensor-parallel ranks (h = this rank's row-parallel partial of the sum over ranks): add_resid = 0
 // writes h = W_o . attention instead of adding (a rank != 0 whose all-reduce follows as its own
 // launch); world > 1 runs the all-reduce in the tile reducers' epilogue (car_proto.h push protocol
@@ -504,7 +536,7 @@ extern "C" int llmc_attn_oproj(const void* q, const void* k_cache, const void* v
       (const bf16_t*)q, (const bf16_t*)k_cache, (const bf16_t*)v_cache, (const int32_t*)block_table, bt_len,       \
       (const int32_t*)seq_len, (const bf16_t*)w_o, K_o, (bf16_t*)h, (bf16_t*)attn_out, (float*)part,               \
       (uint32_t*)handoff, (uint64_t*)tile_part, (int*)ctr, (int*)fault, nkv, bs, nblocks, chunk, sl2, (uint64_t*)stamps, \
-      (mode >> 1) & 1, add_resid, ar); \
+      (mode >> 1) & 1, add_resid, ar, late ? (mode >> 3) & 1 : 0); \
   } while (0)
 #define LLMC_AO(GG, DD, RR)                                                                                      \
   do {                                                                                                            \

@@ -501,8 +501,8 @@ class Engine:
         sel = [i for i, (s, _) in enumerate(batch) if want_logits and s in finals]
         for i0 in range(0, len(sel), ops.GEMV_MAX_M):
             part = sel[i0:i0 + ops.GEMV_MAX_M]
-            last_d = torch.tensor([q_start[i] + q_lens[i] - 1 for i in part], dtype=torch.long).to(dev)
-            hl = h.index_select(0, last_d)
+            last_d = torch.tensor([q_start[i] + q_lens[i] - 1 for i in part], dtype=torch.int32).to(dev)
+            hl = ops.gather_rows(h, last_d, 1)  # K14 last-token gather
             lg = torch.empty(len(part), self.w.vocab_local, dtype=torch.float32, device=dev)
             ops.linear(hl, self.w.lm_head, EPI_F32, out=lg, norm_w=self.w.final_norm, eps=c.rms_eps,
                        mfma=self.mfma_decode)

@@ -237,3 +237,35 @@ def test_attn_oproj_tp_rank_shapes(cuda, nh, nkv, D, H, L, cap, add_resid):
         assert (attn.float().cpu() - a_ref.float()).abs().max().item() < 2e-2
         err_h = (h.float().cpu() - h_ref).abs().max().item()
         assert err_h < 2e-2 * max(1.0, h_ref.abs().max().item()), (it, err_h)
+
+
+@pytest.mark.parametrize("nh,nkv,D,H", [(32, 8, 128, 4096), (8, 2, 128, 1024)])
+@pytest.mark.parametrize("L,cap", [(100, 2048), (2048, 2048), (9000, 16384)])
+def test_attn_oproj_weight_gate_is_timing_only(cuda, nh, nkv, D, H, L, cap):
+    """Mode bit 3 (the grid-wide weight gate: no block requests its o_proj weights before every
+    block has streamed its K/V) changes when loads issue, never what is computed: the same bits as
+    the ungated mode, launch after launch on one workspace (the gate's epoch re-arms itself)."""
+    bs = 64
+    nc = ops.attn_oproj_grid(H, nh, nkv, D)
+    chunk = ops.attn_oproj_chunk(cap, nc)
+    if chunk == 0:
+        pytest.skip("bucket beyond the fused launch")
+    kc, vc, bt, sl, q, w_o, h0 = _case(L, nh, nkv, D, H, bs)
+    scale = 1 / math.sqrt(D)
+    fault = torch.zeros(1, dtype=torch.int32, device="cuda")
+    fr = nkv == 8 and nh // nkv == 4 and D == 128 and H // nc == 128
+    base = 7 if fr else 3
+    ws = ops.attn_oproj_workspace(H, nh, nkv, D, nc, "cuda")
+    outs = []
+    for mode in (base, base | 8, base | 8, base, base | 8):
+        hm = h0.clone()
+        am = torch.zeros(1, nh * D, dtype=BF, device="cuda")
+        ops.attn_oproj(q, kc, vc, bt.cuda(), sl.cuda(), w_o, hm, am, ws, nh, nkv, D, bs, chunk, nc, scale, fault=fault,
+                       mode=mode)
+        outs.append((hm, am))
+    torch.cuda.synchronize()
+    assert int(fault.item()) == 0
+    for o in outs[1:]:
+        assert torch.equal(o[0], outs[0][0]) and torch.equal(o[1], outs[0][1])
+    c = ws[3].view(-1, 16).cpu()
+    assert int(c[nkv + nc + 1, 0]) == 0 and int(c[nkv + nc + 1, 1]) == 3  # arrivals re-armed, 3 gated launches

@@ -12,6 +12,8 @@
 // MI355X_MICROARCH.md "Global float atomics" pitfall). Expert parallel: moe_ep_localize maps the
 // router's global ids to this rank's experts (-1, weight 0 elsewhere); expert GEMV blocks of a -1
 // pair exit and the combine skips zero-weight pairs.
+#include <algorithm>
+
 #include "common.h"
 
 namespace llmc {
@@ -64,6 +66,90 @@ __global__ void moe_route_kernel(const float* __restrict__ logits, int T, int E,
     if (j < k) {
       ids[static_cast<int64_t>(t) * k + j] = pick[j];
       w[static_cast<int64_t>(t) * k + j] = sel[j] / ssum;
+    }
+  }
+}
+
+// Prefill router, fused (replaces the router-logits GEMM + moe_route_kernel pair of the prefill
+// path: the GEMM ran as a narrow-N tile grid of M / 128 blocks for N = 8 outputs, ~125 us per
+// 2048-token layer, latency-bound): logits = x . Wr^T in f32, softmax, top-k, renormalise, ONE
+// launch. Each block stages the E x H router weights in LDS once (64 KB for Mixtral), then every
+// wave takes whole tokens: all of the token's 16-B x chunks in flight at once, E dot products per
+// lane against the LDS rows (lane-consecutive chunks: conflict-free), E wave sums, and lane 0 picks
+// the top-k (first max wins ties, as moe_route_kernel). x = the normalised rows the expert GEMMs
+// also read.
+constexpr int kRouteFusedMaxE = 16, kRouteFusedPre = 16;  // experts; x chunks per lane (H <= 8192)
+
+__global__ __launch_bounds__(256) void moe_route_fused_kernel(const bf16_t* __restrict__ x, int x_stride,
+                                                              const bf16_t* __restrict__ Wr, int T, int E, int H,
+                                                              int k, float* __restrict__ w_out,
+                                                              int32_t* __restrict__ ids_out) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  u32x4* wl = reinterpret_cast<u32x4*>(smem);  // [E][H / 8]
+  const int nch = H / 8;
+  for (int i = threadIdx.x; i < E * nch; i += 256) wl[i] = reinterpret_cast<const u32x4*>(Wr)[i];
+  __syncthreads();
+  const int wave = threadIdx.x / kWave, lane = threadIdx.x % kWave;
+  for (int t = blockIdx.x * 4 + wave; t < T; t += gridDim.x * 4) {  // wave-uniform
+    const u32x4* xr = reinterpret_cast<const u32x4*>(x + static_cast<int64_t>(t) * x_stride);
+    u32x4 xv[kRouteFusedPre];
+#pragma unroll
+    for (int i = 0; i < kRouteFusedPre; ++i) {
+      const int c = lane + i * kWave;
+      if (c < nch) xv[i] = xr[c];
+    }
+    float acc[kRouteFusedMaxE];
+#pragma unroll
+    for (int e = 0; e < kRouteFusedMaxE; ++e) {
+      acc[e] = 0.f;
+      if (e < E) {
+#pragma unroll
+        for (int i = 0; i < kRouteFusedPre; ++i) {
+          const int c = lane + i * kWave;
+          if (c < nch) acc[e] = dot8_bf16(wl[e * nch + c], xv[i], acc[e]);
+        }
+        acc[e] = wave_sum(acc[e]);
+      }
+    }
+    if (lane == 0) {
+      float mx = -INFINITY;
+#pragma unroll
+      for (int e = 0; e < kRouteFusedMaxE; ++e)
+        if (e < E) mx = fmaxf(mx, acc[e]);
+      float z = 0.f;
+#pragma unroll
+      for (int e = 0; e < kRouteFusedMaxE; ++e)
+        if (e < E) z += __expf(acc[e] - mx);
+      uint32_t taken = 0;
+      float sel[8];
+      int pick[8];
+      float ssum = 0.f;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        sel[j] = 0.f;
+        pick[j] = -1;
+        if (j < k) {
+          int best = -1;
+          float bv = -INFINITY;
+#pragma unroll
+          for (int e = 0; e < kRouteFusedMaxE; ++e) {
+            const bool ok = e < E && !((taken >> e) & 1u) && (best < 0 || acc[e] > bv);
+            bv = ok ? acc[e] : bv;
+            best = ok ? e : best;
+          }
+          taken |= 1u << best;
+          sel[j] = __expf(bv - mx) / z;
+          pick[j] = best;
+          ssum += sel[j];
+        }
+      }
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        if (j < k) {
+          ids_out[static_cast<int64_t>(t) * k + j] = pick[j];
+          w_out[static_cast<int64_t>(t) * k + j] = sel[j] / ssum;
+        }
+      }
     }
   }
 }
@@ -359,6 +445,28 @@ extern "C" {
 int llmc_moe_route(const void* logits, int T, int E, int k, void* w, void* ids, hipStream_t s) {
   if (E > 64 || k > 8 || k > E) return -1;
   moe_route_kernel<<<(T + 255) / 256, 256, 0, s>>>((const float*)logits, T, E, k, (float*)w, (int32_t*)ids);
+  return static_cast<int>(hipGetLastError());
+}
+
+// Prefill router in one launch (moe_route_fused_kernel): E <= 16, k <= min(8, E), H % 8 == 0,
+// H <= 8192 (x chunks per lane), E * H * 2 bytes of LDS.
+int llmc_moe_route_fused(const void* x, int x_stride, const void* Wr, int T, int E, int H, int k, void* w, void* ids,
+                         hipStream_t s) {
+  if (E < 1 || E > kRouteFusedMaxE || k < 1 || k > 8 || k > E || H % 8 != 0 || H > kRouteFusedPre * kWave * 8 ||
+      x_stride % 8 != 0)
+    return -1;
+  if (T <= 0) return 0;
+  const size_t lds = static_cast<size_t>(E) * H * 2;
+  if (lds > 160 * 1024) return -1;
+  static bool attr_set = false;
+  if (!attr_set) {
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(moe_route_fused_kernel),
+                              hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    attr_set = true;
+  }
+  const int grid = std::min(256, (T + 3) / 4);
+  moe_route_fused_kernel<<<grid, 256, lds, s>>>((const bf16_t*)x, x_stride, (const bf16_t*)Wr, T, E, H, k, (float*)w,
+                                                (int32_t*)ids);
   return static_cast<int>(hipGetLastError());
 }
 

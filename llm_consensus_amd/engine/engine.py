@@ -85,6 +85,12 @@ class EngineConfig:
     # engine whose GPUs also run other engines' decode at the same time (bench.py's N=2 third
     # responder) keeps the separate, 64-block all-reduce launch
     fused_ar: bool = True
+    # engines alone on their GPU (the fused attention + o_proj buckets): read the first
+    # ``prefetch_mb`` MB of each layer's gate_up weights on a side stream BESIDE the attention launch
+    # (a fork / join inside the decode graph), so they are in the Infinity Cache when the gate_up
+    # GEMV streams them (csrc/kernels/prefetch.hip). 0 = off. LLMC_PREFETCH_MB / _BLOCKS (A/B runs)
+    prefetch_mb: int = dataclasses.field(default_factory=lambda: int(os.environ.get("LLMC_PREFETCH_MB", "0")))
+    prefetch_blocks: int = dataclasses.field(default_factory=lambda: int(os.environ.get("LLMC_PREFETCH_BLOCKS", "64")))
 
 
 FUSED_CHUNK_SMALL, FUSED_CHUNK_LARGE = 128, 256
@@ -270,6 +276,8 @@ class Engine:
         self._alloc_decode_buffers()
         self._graphs: Dict[int, "torch.cuda.CUDAGraph"] = {}
         self._next_sid = 0
+        self._pf_stream = (torch.cuda.Stream(self.device) if self.on_gpu and self.ecfg.prefetch_mb > 0 and any(self.ao_chunks)
+                           else None)
 
     # ------------------------------------------------------------------------------------------
     def _on_stream(self):
@@ -590,11 +598,16 @@ class Engine:
         return y
 
     def _route(self, xn: torch.Tensor, Lw):
+        """Prefill router (K9): one fused launch (logits, softmax, top-k) where the kernel covers the
+        shape, else the router-logits GEMM + the top-k kernel."""
         c = self.cfg
         T, k = xn.shape[0], c.top_k_experts
-        rl = ops.linear(xn, Lw.w_router, EPI_F32)
         w = torch.empty(T, k, dtype=torch.float32, device=xn.device)
         ids = torch.empty(T, k, dtype=torch.int32, device=xn.device)
+        if xn.is_cuda and xn.is_contiguous() and ops.moe_route_fused_supported(c.n_experts, c.hidden):
+            ops.moe_route_fused(xn, Lw.w_router, k, w, ids)
+            return w, ids
+        rl = ops.linear(xn, Lw.w_router, EPI_F32)
         ops.moe_route(rl, k, w, ids)
         return w, ids
 
@@ -673,7 +686,15 @@ class Engine:
                              self.positions[:B], self.slots[:B], self.cos_t, self.sin_t, self.nh, self.nkv, self.D,
                              self.bs, mfma=self.mfma_decode)
                 if ao_chunk:  # one-row engines: attention + o_proj + residual (+ TP all-reduce) in one launch
+                    pf = self._pf_stream
+                    if pf is not None:  # fork: warm the gate_up weights beside the latency-bound launch
+                        cur = torch.cuda.current_stream(self.device)
+                        pf.wait_stream(cur)
+                        with torch.cuda.stream(pf):
+                            ops.prefetch(Lw.w_gu, self.ecfg.prefetch_mb << 20, self.ecfg.prefetch_blocks)
                     self._attn_oproj(q, li, Lw, h, attn, ao_chunk)
+                    if pf is not None:
+                        cur.wait_stream(pf)  # join
                 else:
                     ops.attn_decode(q, self.k_cache[li], self.v_cache[li], self.block_tables[:B], self.seq_lens[:B],
                                     attn, part[:B], self.attn_counters[:B], self.nh, self.nkv, self.D, self.bs, chunk,

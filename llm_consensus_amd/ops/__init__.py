@@ -533,6 +533,22 @@ def moe_route(logits: torch.Tensor, k: int, w_out: torch.Tensor, ids_out: torch.
     return w_out, ids_out
 
 
+def moe_route_fused(x: torch.Tensor, W_router: torch.Tensor, k: int, w_out: torch.Tensor, ids_out: torch.Tensor):
+    """Prefill router in one launch: logits = x . W_router^T (f32), softmax top-k, renormalised
+    (K9; csrc/kernels/moe.hip moe_route_fused_kernel). x [T, H] bf16 (normalised rows), W_router
+    [E <= 16, H]."""
+    if not x.is_cuda:
+        return moe_route(oracle.linear(x, W_router, EPI_F32), k, w_out, ids_out)
+    T, H = x.shape
+    kernels().moe_route_fused(_p(x), x.stride(0), _p(W_router), T, W_router.shape[0], H, k, _p(w_out), _p(ids_out),
+                              _s(x))
+    return w_out, ids_out
+
+
+def moe_route_fused_supported(E: int, H: int) -> bool:
+    return E <= 16 and H % 8 == 0 and H <= 8192 and E * H * 2 <= 160 * 1024
+
+
 def moe_max_tiles(npairs: int, E: int, tile: int = MOE_TILE) -> int:
     return (npairs + tile - 1) // tile + E
 
@@ -584,6 +600,17 @@ def moe_ep_dispatch(ids: torch.Tensor, n_local: int, n_ranks: int, cap: int):
     kernels().moe_ep_dispatch(_p(ids), P, int(n_local), int(n_ranks), int(cap), _p(send_pair), _p(send_e), _p(slot),
                               _p(counts), _s(ids))
     return send_pair, send_e, slot, counts
+
+
+def prefetch(t: torch.Tensor, nbytes: int, blocks: int = 64) -> None:
+    """Read the first ``nbytes`` of ``t`` (default cache policy) so they sit in the Infinity Cache for
+    the next kernel that streams them (csrc/kernels/prefetch.hip; the lone engine's decode runs it
+    on a side stream beside the attention launch). No-op on CPU tensors."""
+    if not t.is_cuda:
+        return
+    n = min(int(nbytes), t.numel() * t.element_size()) // 16 * 16
+    if n > 0:
+        kernels().prefetch(_p(t), n, int(blocks), 0, _s(t))
 
 
 def gather_rows(x: torch.Tensor, rows: torch.Tensor, div: int, out: Optional[torch.Tensor] = None) -> torch.Tensor:

@@ -451,6 +451,8 @@ if __name__ == "__main__":
         bench_launch()
     if what in ("attn", "all"):
         bench_attn()
+    if what in ("attn-phi3",):  # Phi-3-mini: 32 heads = 32 kv heads, D = 96
+        bench_attn(((32, 32, 96),))
     if what in ("attn-tp",):  # TP ranks' shapes only (G = 8 / 4 on one or two kv heads)
         bench_attn(((16, 2, 128), (8, 1, 128), (4, 1, 128)))
     if what in ("gemv", "all"):

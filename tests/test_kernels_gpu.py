@@ -806,3 +806,26 @@ def test_moe_router_fused(cuda, T, E, H):
         for j in range(k):
             href[t] += wc[t, j] * (wdc[idc[t, j]] @ a1c[t * k + j])
     close(h1, href, 2e-2)
+
+
+@pytest.mark.parametrize("T,E,H,k", [(1, 8, 4096, 2), (37, 8, 4096, 2), (2048, 8, 4096, 2), (300, 16, 1024, 4),
+                                     (129, 4, 192, 2)])
+def test_moe_route_fused(cuda, T, E, H, k):
+    """The one-launch prefill router (logits in f32 from the bf16 rows, softmax, top-k, renormalise)
+    vs the fp32 oracle: the same experts wherever the oracle's k-th and (k+1)-th logits are not a
+    near-tie, weights to f32 rounding."""
+    torch.manual_seed(31)
+    x = rnd(T, H)
+    wr = rnd(E, H, scale=0.05)
+    w = torch.empty(T, k, device="cuda")
+    ids = torch.empty(T, k, dtype=torch.int32, device="cuda")
+    ops.moe_route_fused(x, wr, k, w, ids)
+    logits = x.float().cpu() @ wr.float().cpu().t()
+    rw, rids = oracle.moe_route(logits, k)
+    srt = logits.sort(dim=-1, descending=True).values
+    clear = (srt[:, k - 1] - srt[:, k]) > 1e-3 * srt.abs().max()
+    if k > 1:
+        clear &= ((srt[:, :k - 1] - srt[:, 1:k]).abs() > 1e-3 * srt.abs().max()).all(-1)
+    assert clear.float().mean() > 0.9
+    assert torch.equal(ids.cpu()[clear], rids[clear])
+    close(w[clear.cuda()], rw[clear], 1e-4, 1e-3)

@@ -66,7 +66,6 @@ int llmc_moe_gemv(int, const void*, int, const void*, float, const void*, const 
 int llmc_moe_ep_localize(const void*, const void*, int, int, int, void*, void*, hipStream_t);
 int llmc_moe_ep_dispatch(const void*, int, int, int, int, void*, void*, void*, void*, hipStream_t);
 int llmc_gather_rows(const void*, int, const void*, int, int, int, void*, int, hipStream_t);
-int llmc_prefetch(const void*, int64_t, int, void*, hipStream_t);
 int llmc_moe_route_fused(const void*, int, const void*, int, int, int, int, void*, void*, hipStream_t);
 int llmc_gemv_sweep(int, const void*, const void*, const void*, void*, int, int, hipStream_t);
 size_t llmc_car_sig_bytes();
@@ -245,9 +244,6 @@ PYBIND11_MODULE(_llmc_hip, m) {
   });
   m.def("moe_route_fused", [](ptr x, int xs, ptr wr, int T, int E, int H, int k, ptr w, ptr ids, ptr s) {
     check(llmc_moe_route_fused(P(x), xs, P(wr), T, E, H, k, P(w), P(ids), S(s)), "moe_route_fused");
-  });
-  m.def("prefetch", [](ptr p, int64_t bytes, int blocks, ptr sink, ptr s) {
-    check(llmc_prefetch(P(p), bytes, blocks, P(sink), S(s)), "prefetch");
   });
   m.def("gather_rows", [](ptr x, int xs, ptr rows, int M, int div, int H, ptr out, int os, ptr s) {
     check(llmc_gather_rows(P(x), xs, P(rows), M, div, H, P(out), os, S(s)), "gather_rows");

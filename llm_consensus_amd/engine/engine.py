@@ -85,18 +85,6 @@ class EngineConfig:
     # engine whose GPUs also run other engines' decode at the same time (bench.py's N=2 third
     # responder) keeps the separate, 64-block all-reduce launch
     fused_ar: bool = True
-    # engines alone on their GPU (the fused attention + o_proj buckets): read the first
-    # ``prefetch_mb`` MB of each layer's gate_up weights on a side stream BESIDE the attention launch
-    # (a fork / join inside the decode graph), so they are in the Infinity Cache when the gate_up
-    # GEMV streams them (csrc/kernels/prefetch.hip). 0 = off. LLMC_PREFETCH_MB / _BLOCKS (A/B runs)
-    prefetch_mb: int = dataclasses.field(default_factory=lambda: int(os.environ.get("LLMC_PREFETCH_MB", "0")))
-    prefetch_blocks: int = dataclasses.field(default_factory=lambda: int(os.environ.get("LLMC_PREFETCH_BLOCKS", "64")))
-    # latency-bound shards (TP ranks: every kernel of their decode step runs far below the HBM rate):
-    # at the start of each layer a side stream reads the NEXT layer's projection weights (the lm_head
-    # shard after the last layer), up to ``prefetch_next_mb`` MB, so each kernel finds its weights in
-    # the Infinity Cache (~545-cycle hits vs ~900+ for HBM misses). Weights are read-only: the side
-    # stream only joins the step at its end. 0 = off. LLMC_PREFETCH_NEXT_MB (A/B runs)
-    prefetch_next_mb: int = dataclasses.field(default_factory=lambda: int(os.environ.get("LLMC_PREFETCH_NEXT_MB", "0")))
 
 
 FUSED_CHUNK_SMALL, FUSED_CHUNK_LARGE = 128, 256
@@ -282,9 +270,6 @@ class Engine:
         self._alloc_decode_buffers()
         self._graphs: Dict[int, "torch.cuda.CUDAGraph"] = {}
         self._next_sid = 0
-        self._pf_stream = (torch.cuda.Stream(self.device)
-                           if self.on_gpu and ((self.ecfg.prefetch_mb > 0 and any(self.ao_chunks))
-                                               or self.ecfg.prefetch_next_mb > 0) else None)
 
     # ------------------------------------------------------------------------------------------
     def _on_stream(self):
@@ -679,27 +664,10 @@ class Engine:
         ao_chunk = self.ao_chunks[bi] if B == 1 else 0
         qa = self.qa_plan[bi] if B == 1 else None
         dbg = self._debug_layer_io  # eager debug steps only: each layer's input, then the last output
-        pf_next = self._pf_stream if self.ecfg.prefetch_next_mb > 0 else None
-        cur_s = torch.cuda.current_stream(self.device) if pf_next is not None else None
         layers = self.w.layers
         for li, Lw in enumerate(layers):
             if dbg is not None:
                 dbg.append(h.clone())
-            if pf_next is not None:  # fork: warm the next layer's weights while this layer runs
-                pf_next.wait_stream(cur_s)
-                with torch.cuda.stream(pf_next):
-                    budget = self.ecfg.prefetch_next_mb << 20
-                    if li + 1 == len(layers):
-                        nxt = (self.w.lm_head,)
-                    else:  # MoE: the routed experts are not known yet, only the attention weights
-                        Ln = layers[li + 1]
-                        nxt = (Ln.w_qkv, Ln.w_o) if c.is_moe else (Ln.w_qkv, Ln.w_o, Ln.w_gu, Ln.w_down)
-                    for W in nxt:
-                        nb = min(budget, W.numel() * W.element_size())
-                        if nb <= 0:
-                            break
-                        ops.prefetch(W, nb, self.ecfg.prefetch_blocks)
-                        budget -= nb
             if qa:  # qkv projection + attention in one launch (one row), then o_proj
                 ops.qkv_attn(h, Lw.w_qkv, Lw.ln1, c.rms_eps, q, self.k_cache[li], self.v_cache[li], self.positions[:1],
                              self.slots[:1], self.cos_t, self.sin_t, self.block_tables[:1], self.seq_lens[:1], attn,
@@ -711,15 +679,7 @@ class Engine:
                              self.positions[:B], self.slots[:B], self.cos_t, self.sin_t, self.nh, self.nkv, self.D,
                              self.bs, mfma=self.mfma_decode)
                 if ao_chunk:  # one-row engines: attention + o_proj + residual (+ TP all-reduce) in one launch
-                    pf = self._pf_stream
-                    if pf is not None:  # fork: warm the gate_up weights beside the latency-bound launch
-                        cur = torch.cuda.current_stream(self.device)
-                        pf.wait_stream(cur)
-                        with torch.cuda.stream(pf):
-                            ops.prefetch(Lw.w_gu, self.ecfg.prefetch_mb << 20, self.ecfg.prefetch_blocks)
                     self._attn_oproj(q, li, Lw, h, attn, ao_chunk)
-                    if pf is not None:
-                        cur.wait_stream(pf)  # join
                 else:
                     ops.attn_decode(q, self.k_cache[li], self.v_cache[li], self.block_tables[:B], self.seq_lens[:B],
                                     attn, part[:B], self.attn_counters[:B], self.nh, self.nkv, self.D, self.bs, chunk,
@@ -733,8 +693,6 @@ class Engine:
         if dbg is not None:
             dbg.append(h.clone())
         self._lm_head_sample(B)
-        if pf_next is not None:
-            cur_s.wait_stream(pf_next)  # join: every forked prefetch rejoins the step (graph capture)
 
     _debug_layer_io: Optional[list] = None
 

@@ -602,17 +602,6 @@ def moe_ep_dispatch(ids: torch.Tensor, n_local: int, n_ranks: int, cap: int):
     return send_pair, send_e, slot, counts
 
 
-def prefetch(t: torch.Tensor, nbytes: int, blocks: int = 64) -> None:
-    """Read the first ``nbytes`` of ``t`` (default cache policy) so they sit in the Infinity Cache for
-    the next kernel that streams them (csrc/kernels/prefetch.hip; the lone engine's decode runs it
-    on a side stream beside the attention launch). No-op on CPU tensors."""
-    if not t.is_cuda:
-        return
-    n = min(int(nbytes), t.numel() * t.element_size()) // 16 * 16
-    if n > 0:
-        kernels().prefetch(_p(t), n, int(blocks), 0, _s(t))
-
-
 def gather_rows(x: torch.Tensor, rows: torch.Tensor, div: int, out: Optional[torch.Tensor] = None) -> torch.Tensor:
     """out[j] = x[rows[j] // div], zero rows where rows[j] < 0 (the expert-parallel send buffer)."""
     M = rows.numel()

@@ -1,5 +1,5 @@
-"""Microbenchmark of the MoE prefill router pieces (round 6): the router logits GEMM (M tokens x 8
-experts x K 4096, f32 out) and the top-k kernel, graph-timed on one GPU."""
+"""Microbenchmark of the MoE prefill router (round 6): the router-logits GEMM (M tokens x 8 experts
+x K 4096, f32 out) + the top-k kernel against the fused one-launch router, graph-timed on one GPU."""
 import os
 import sys
 
@@ -17,4 +17,6 @@ for T in (1024, 2048, 8192):
     ids = torch.empty(T, 2, dtype=torch.int32, device="cuda")
     g = timeit(lambda: ops.linear(x, wr, ops.EPI_F32, out=lg))
     r = timeit(lambda: ops.moe_route(lg, 2, w, ids))
-    print(f"T={T}: router GEMM [{T}x4096]x[8x4096]^T {g:8.2f} us ({ops.gemm_plan(T, 8)}), top-2 {r:8.2f} us", flush=True)
+    f = timeit(lambda: ops.moe_route_fused(x, wr, 2, w, ids))
+    print(f"T={T}: router GEMM [{T}x4096]x[8x4096]^T {g:8.2f} us ({ops.gemm_plan(T, 8)}), top-2 {r:8.2f} us; "
+          f"fused one-launch router {f:8.2f} us", flush=True)

@@ -414,13 +414,15 @@ __global__ __launch_bounds__(kAoThreads) void attn_oproj_kernel(
       const uint32_t ep = __hip_atomic_load(car_ctr(ar.P.base[ar.rank]) + vb, __ATOMIC_RELAXED,
                                             __HIP_MEMORY_SCOPE_SYSTEM) + 1u;
       const uint32_t mine = pack_bf16x2(red[2 * gi], red[2 * gi + 1]);
-      for (int idx = lane; idx < ar.world * NG; idx += kWave) {  // push: (peer, granule)
-        const int p = idx / NG, g2 = idx % NG;
-        const uint32_t e2 = __shfl(ep, g2, 64);
+      for (int base = 0; base < ar.world * NG; base += kWave) {  // push: (peer, granule); uniform trip count
+        const int idx = base + lane;
+        const bool live = idx < ar.world * NG;
+        const int p = idx / NG, g2 = live ? idx % NG : 0;
+        const uint32_t e2 = __shfl(ep, g2, 64);  // every lane takes part in both shuffles
         const uint32_t pay = __shfl(mine, g2, 64);
         const long gi2 = static_cast<long>(c * NVB + g2 / kArGranulesPerBlock) * kArGranulesPerBlock +
                          g2 % kArGranulesPerBlock;
-        if (p != ar.rank) car_put(ar.P.base[p] + car_granule_off(e2, ar.cap, ar.rank, gi2), pay, e2);
+        if (live && p != ar.rank) car_put(ar.P.base[p] + car_granule_off(e2, ar.cap, ar.rank, gi2), pay, e2);
       }
       if (lane < NG) {  // collect every peer's granule of my row pair, sum in rank order
         const long g[1] = {gidx};

@@ -81,7 +81,7 @@ __global__ __launch_bounds__(kAoThreads) void attn_oproj_kernel(
     const bf16_t* __restrict__ w_o, int K_o, bf16_t* __restrict__ h, bf16_t* __restrict__ attn_out,
     float* __restrict__ part, uint32_t* __restrict__ handoff, uint64_t* __restrict__ tile_part, int* __restrict__ ctr,
     int* __restrict__ fault, int nkv, int bs, int nblocks, int chunk, float scale_log2,
-    uint64_t* __restrict__ stamps, int defer, int add_resid, CarArgs ar, int gate) {
+    uint64_t* __restrict__ stamps, int defer, int add_resid, CarArgs ar, int gate, int prio) {
   static_assert(G * D == 512, "one 16-B column chunk per lane per row");
   static_assert(RW >= 1 && RW <= 32 && (RW & (RW - 1)) == 0, "rows per wave: power of two <= 32");
   static_assert(SUBS == 1 || (SUBS == 2 && LATE), "two sub-tiles per wave only with late weights (registers)");
@@ -144,6 +144,9 @@ __global__ __launch_bounds__(kAoThreads) void attn_oproj_kernel(
   // tickets, merge, poll the hand-off and reduce the tile. Every wave computes one attention
   // sub-tile. The o_proj tile: rows n = c R + ow RW + j (ow = o wave), columns g G D + 8 lane .. + 8.
   const bool o_wave = wave < 4;  // wave-uniform
+  // mode bit 4: the control waves (the latency chain: publish, tickets, merge, hand-off, tile
+  // reduce) issue ahead of the o waves on their SIMDs (s_setprio 3 vs 0)
+  if (prio && !o_wave) __builtin_amdgcn_s_setprio(3);
   const int ct = tid - 256;      // control-thread index (waves 4-7: 0..255)
   // tickets from wave 6: it has neither weights nor partial / hand-off stores in flight (stores
   // count in the same counter), so the returned value is usable at once
@@ -484,7 +487,8 @@ extern "C" int llmc_attn_oproj_check(int H, int nh, int nkv, int D, int nc, int 
 // right behind the K/V loads; bit 1 (with late weights): the head's merger issues its own after the
 // merge; bit 2 (with late weights, 8 kv heads, G = 4, D = 128, 32-row tiles): whole o_proj rows per
 // block (FR, see the kernel); bit 3 (with late weights): the weight gate — no block requests its
-// weights before every block of the grid has streamed its K/V (lone engines).
+// weights before every block of the grid has streamed its K/V (lone engines); bit 4: the control
+// waves run at a higher issue priority than the o waves (s_setprio).
 // fault codes: 1 a partial never arrived (merge), 2 the head output never arrived, 3 a tile partial.
 // stamps (nullable, diagnostics): uint64 [nkv][nc][8] s_memrealtime per block: 0 start, 1 o wave 0's
 // attention done, 2 control wave 4's attention done, 3 head ticket taken, 4 head output in LDS,
@@ -538,7 +542,7 @@ extern "C" int llmc_attn_oproj(const void* q, const void* k_cache, const void* v
       (const bf16_t*)q, (const bf16_t*)k_cache, (const bf16_t*)v_cache, (const int32_t*)block_table, bt_len,       \
       (const int32_t*)seq_len, (const bf16_t*)w_o, K_o, (bf16_t*)h, (bf16_t*)attn_out, (float*)part,               \
       (uint32_t*)handoff, (uint64_t*)tile_part, (int*)ctr, (int*)fault, nkv, bs, nblocks, chunk, sl2, (uint64_t*)stamps, \
-      (mode >> 1) & 1, add_resid, ar, late ? (mode >> 3) & 1 : 0); \
+      (mode >> 1) & 1, add_resid, ar, late ? (mode >> 3) & 1 : 0, (mode >> 4) & 1); \
   } while (0)
 #define LLMC_AO(GG, DD, RR)                                                                                      \
   do {                                                                                                            \

@@ -35,7 +35,8 @@ int llmc_attn_decode_groups(int);
 int llmc_qkv_attn_check(int, int, int, int);
 int llmc_qkv_attn(const void*, const void*, float, const void*, int, void*, void*, void*, const void*, const void*,
                   const void*, const void*, const void*, int, const void*, void*, void*, void*, int, int, int, int, int,
-                  int, int, int, float, void*, void*, void*, hipStream_t);
+                  int, int, int, float, void*, void*, void*, int, const void*, void*, int, const void* const*, void*,
+                  int, int, size_t, hipStream_t);
 int llmc_attn_oproj_check(int, int, int, int, int, int);
 int llmc_attn_oproj(const void*, const void*, const void*, const void*, int, const void*, const void*, void*, void*,
                     void*, void*, void*, void*, void*, int, int, int, int, int, int, int, int, float, int, void*,
@@ -151,10 +152,14 @@ PYBIND11_MODULE(_llmc_hip, m) {
   m.def("qkv_attn", [](ptr x, ptr nw, float eps, ptr W, int K, ptr qo, ptr kc, ptr vc, ptr pos, ptr slots, ptr cos_t,
                        ptr sin_t, ptr bt, int bt_len, ptr sl, ptr part, ptr ctr, ptr out, int nh, int nkv, int D, int bs,
                        int nblocks, int chunk, int gc, int max_chunks, float scale, ptr fault, ptr gran, ptr hctr,
-                       ptr s) {
+                       int o_mode, ptr w_o, ptr h, int o_n, const std::vector<ptr>& bases, ptr host, int rank, int world,
+                       size_t cap, ptr s) {
+    std::vector<const void*> b(bases.size());
+    for (size_t i = 0; i < bases.size(); ++i) b[i] = P(bases[i]);
     check(llmc_qkv_attn(P(x), P(nw), eps, P(W), K, P(qo), P(kc), P(vc), P(pos), P(slots), P(cos_t), P(sin_t), P(bt),
                         bt_len, P(sl), P(part), P(ctr), P(out), nh, nkv, D, bs, nblocks, chunk, gc, max_chunks, scale,
-                        P(fault), P(gran), P(hctr), S(s)),
+                        P(fault), P(gran), P(hctr), o_mode, P(w_o), P(h), o_n, b.empty() ? nullptr : b.data(), P(host),
+                        rank, world, cap, S(s)),
           "qkv_attn");
   });
   m.def("attn_oproj_check", [](int H, int nh, int nkv, int D, int nc, int K_o) {

@@ -80,6 +80,9 @@ class EngineConfig:
     # QKV_ATTN_MAX_ROWS rows (the TP ranks', where it measured faster: profiles/r4_qkv_attn.md);
     # "all": every covered shape and fused bucket, ahead of attn_oproj; "0": never (LLMC_QKV_ATTN)
     qkv_attn: str = dataclasses.field(default_factory=lambda: os.environ.get("LLMC_QKV_ATTN", "1"))
+    # ... and the token's o_proj (+ the TP all-reduce in its epilogue, ``fused_ar``) in the same
+    # launch (the o-role of csrc/kernels/qkv_attn.hip) instead of the o GEMV after it (LLMC_QKV_ATTN_O)
+    qkv_attn_o: bool = dataclasses.field(default_factory=lambda: os.environ.get("LLMC_QKV_ATTN_O", "0") == "1")
     # TP engines: the decode all-reduce inside the row-parallel GEMVs' epilogue when the group has
     # the fused buffer (TPGroup.custom_fused). Its 256 blocks spin per block on their peers, so an
     # engine whose GPUs also run other engines' decode at the same time (bench.py's N=2 third
@@ -335,6 +338,8 @@ class Engine:
             if any(self.qa_plan):
                 self.qa_ws = ops.qkv_attn_workspace(self.nh, self.nkv, self.D, dev)
         self.qa_buckets = [p is not None for p in self.qa_plan]
+        self.qa_o = (any(self.qa_plan) and self.ecfg.qkv_attn_o
+                     and ops.qkv_attn_o_supported(self.nh, self.D, c.hidden))
         max_chunks = max([gc for _, _, gc, _ in self.attn_buckets] + [p[1] for p in self.qa_plan if p])
         self.attn_part, self.attn_counters = ops.decode_attn_workspace(B, self.nh, self.nkv, self.D, max_chunks, dev)
         # set by a decode-attention merger that gave up on a partial (checked after every decode)
@@ -669,11 +674,18 @@ class Engine:
             if dbg is not None:
                 dbg.append(h.clone())
             if qa:  # qkv projection + attention in one launch (one row), then o_proj
+                o_in = self.qa_o and h.is_cuda  # ... o_proj (+ all-reduce) in the same launch
+                tp = self.tp
+                car = tp.custom_fused if (o_in and tp.size > 1 and self.ecfg.fused_ar) else None
                 ops.qkv_attn(h, Lw.w_qkv, Lw.ln1, c.rms_eps, q, self.k_cache[li], self.v_cache[li], self.positions[:1],
                              self.slots[:1], self.cos_t, self.sin_t, self.block_tables[:1], self.seq_lens[:1], attn,
                              part, self.attn_counters, self.qa_ws, self.nh, self.nkv, self.D, self.bs, qa[0], qa[1],
-                             self.scale, fault=self.attn_fault)
-                self._row_parallel(attn, Lw.w_o, h)
+                             self.scale, fault=self.attn_fault, w_o=Lw.w_o if o_in else None, h=h if o_in else None,
+                             add_resid=tp.rank == 0, car=car)
+                if not o_in:
+                    self._row_parallel(attn, Lw.w_o, h)
+                elif tp.size > 1 and car is None:
+                    tp.all_reduce_(h)
             else:
                 ops.qkv_rope(h, Lw.w_qkv, Lw.ln1, c.rms_eps, q, self.k_cache[li], self.v_cache[li],
                              self.positions[:B], self.slots[:B], self.cos_t, self.sin_t, self.nh, self.nkv, self.D,

@@ -275,36 +275,62 @@ def qkv_attn_supported(nh: int, nkv: int, D: int, K: int) -> bool:
 
 def qkv_attn_workspace(nh: int, nkv: int, D: int, device):
     """(granules, hctr) of ``qkv_attn``, zeroed once: the hand-off granules u64 [(nh + 2 nkv) D / 2]
-    and the {exit count, hand-off epoch} counter lines int32 [2 * ATTN_CTR_PITCH]."""
+    and the {exit count, hand-off epoch, o-role arrivals} counter lines int32 [3 * ATTN_CTR_PITCH]."""
     dev = torch.device(device)
     return (torch.zeros((nh + 2 * nkv) * D // 2, dtype=torch.int64, device=dev),
-            torch.zeros(2 * ATTN_CTR_PITCH, dtype=torch.int32, device=dev))
+            torch.zeros(3 * ATTN_CTR_PITCH, dtype=torch.int32, device=dev))
+
+
+QKV_ATTN_O_MAX_K = 2048  # the o-role's K (nh D) at most: 4 x 16-B chunks per lane per row
+
+
+def qkv_attn_o_supported(nh: int, D: int, H: int) -> bool:
+    """Whether ``qkv_attn`` can run the row's o_proj in the same launch (o-role): nh D a multiple of
+    512 up to QKV_ATTN_O_MAX_K, an even number of output rows."""
+    k_o = nh * D
+    return k_o % 512 == 0 and k_o <= QKV_ATTN_O_MAX_K and H % 2 == 0
 
 
 def qkv_attn(x, W, norm_w, eps, q_out, k_cache, v_cache, positions, slots, cos_t, sin_t, block_table, seq_len, out,
-             part, counters, ws, nh, nkv, D, bs, chunk, grid_chunks, scale, fault: Optional[torch.Tensor] = None):
+             part, counters, ws, nh, nkv, D, bs, chunk, grid_chunks, scale, fault: Optional[torch.Tensor] = None,
+             w_o: Optional[torch.Tensor] = None, h: Optional[torch.Tensor] = None, add_resid: bool = True, car=None):
     """ONE row's decode qkv projection (RMSNorm prologue, RoPE + paged-KV-write epilogue, as
     ``qkv_rope``) and its attention (the fused form: ``grid_chunks`` blocks of ``chunk`` keys per kv
     head, as ``attn_decode(fused=True)``) in one launch (csrc/kernels/qkv_attn.hip): the attention
     blocks stream the cached keys' K/V under the projection and take the rotated q / the new key
     from the projection blocks as tagged granules. ``part`` / ``counters`` = ``decode_attn_workspace``
     (row 0 used), ``ws`` = ``qkv_attn_workspace``; ``fault`` as in ``attn_decode`` (4 = a lost
-    hand-off granule)."""
+    hand-off granule).
+
+    ``w_o`` / ``h`` (o-role): the token's o_proj in the same launch — ``h[0] += w_o @ out[0]``
+    (``add_resid``; TP rank != 0 without ``car``: ``h[0] = w_o @ out[0]``, its all-reduce follows),
+    or with ``car`` (the group's fused-all-reduce buffer) the all-reduce in the o-role's epilogue,
+    rank 0 adding the residual (fault 5 = the attention output never arrived)."""
     if not x.is_cuda:
         qkv_rope(x[:1], W, norm_w, eps, q_out[:1], k_cache, v_cache, positions[:1], slots[:1], cos_t, sin_t, nh, nkv,
                  D, bs)
         out[:1].copy_(oracle.attn_decode(q_out[:1], k_cache, v_cache, block_table[:1], seq_len[:1], nh, nkv, D, bs,
                                          scale))
+        if w_o is not None:
+            if car is not None:
+                raise ValueError("qkv_attn: the fused all-reduce runs on GPU ranks only")
+            oracle.linear(out[:1], w_o, EPI_RESADD if add_resid else EPI_BF16, h[:1])
         return
     groups = counters.shape[-2] - 2
     max_chunks = part.shape[2] - groups
     if part.shape[-1] != D + 4 or counters.shape[-1] != ATTN_CTR_PITCH or grid_chunks > max_chunks:
         raise ValueError("qkv_attn: workspace does not match (decode_attn_workspace / qkv_attn_workspace)")
     gran, hctr = ws
+    o_mode = 0 if w_o is None else (3 if car is not None else (1 if add_resid else 2))
+    if o_mode and hctr.numel() < 3 * ATTN_CTR_PITCH:
+        raise ValueError("qkv_attn: the o-role needs the 3-line counter workspace (qkv_attn_workspace)")
+    bases, host, rank, world, cap = (([], 0, 0, 1, 0) if car is None else
+                                     (car.bases, car.host_dev, car.rank, car.world, car.cap))
     kernels().qkv_attn(_p(x), _p(norm_w), float(eps), _p(W), x.shape[-1], _p(q_out), _p(k_cache), _p(v_cache),
                        _p(positions), _p(slots), _p(cos_t), _p(sin_t), _p(block_table), block_table.shape[-1],
                        _p(seq_len), _p(part), _p(counters), _p(out), nh, nkv, D, bs, k_cache.shape[0], chunk,
-                       grid_chunks, max_chunks, float(scale), _p(fault), _p(gran), _p(hctr), _s(x))
+                       grid_chunks, max_chunks, float(scale), _p(fault), _p(gran), _p(hctr), o_mode, _p(w_o), _p(h),
+                       0 if h is None else h.shape[-1], bases, host, rank, world, cap, _s(x))
 
 
 ATTN_OPROJ_MAX_CHUNK = 512  # attn_oproj: keys per block at most (8 waves x two 32-key sub-tiles)

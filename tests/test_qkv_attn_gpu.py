@@ -202,3 +202,46 @@ def test_engine_qkv_attn_all_replaces_attn_oproj(cuda):
             err = (la[i] - l2[i]).abs().max().item()
             assert err < 0.02 * max(1.0, l2[i].abs().max().item()), (plen, i, err)
     assert int(ea.attn_fault.item()) == 0
+
+
+@pytest.mark.parametrize("nh,nkv,D,K,H", [(4, 1, 128, 4096, 4096),   # 8B TP=8 rank: o_proj K = 512
+                                          (8, 2, 128, 4096, 4096),   # 8B TP=4 rank: K = 1024
+                                          (16, 4, 128, 4096, 4096),  # 8B TP=2 rank: K = 2048
+                                          (8, 1, 64, 1024, 1000)])   # a partial last row block
+@pytest.mark.parametrize("add_resid", [True, False])
+def test_qkv_attn_o_role_matches_the_o_gemv(cuda, nh, nkv, D, K, H, add_resid):
+    """The o-role (the token's o_proj in the qkv + attention launch, after every attention block
+    has written its head output) against the same launch without it followed by the o GEMV
+    (EPI_RESADD / EPI_BF16): the same bits — one row per wave, its 16-B chunks in the same order,
+    the same wave sum — launch after launch on one workspace (the o-role's arrival counter and the
+    exit count re-arm), at lengths in the one-chunk and the merged forms."""
+    scale = 1 / math.sqrt(D)
+    torch.manual_seed(5)
+    w_o = (torch.randn(H, nh * D, device="cuda") / math.sqrt(nh * D)).to(BF)
+    h0 = torch.randn(1, H, device="cuda").to(BF)
+    for L in (40, 700, 2000):
+        cs = _Case(nh, nkv, D, K, L)
+        chunk, gc = _bucket(L)
+        part, ctr = ops.decode_attn_workspace(1, nh, nkv, D, gc, "cuda", fused=True)
+        ws = ops.qkv_attn_workspace(nh, nkv, D, "cuda")
+        fault = torch.zeros(1, dtype=torch.int32, device="cuda")
+        for it in range(3):
+            kc, vc = cs.kc.clone(), cs.vc.clone()
+            q = torch.zeros(1, nh * D, dtype=BF, device="cuda")
+            out = torch.zeros(1, nh * D, dtype=BF, device="cuda")
+            h = h0.clone()
+            ops.qkv_attn(cs.x, cs.W, cs.nw, 1e-5, q, kc, vc, cs.pos, cs.slots, cs.cos, cs.sin, cs.bt, cs.sl, out, part,
+                         ctr, ws, nh, nkv, D, cs.bs, chunk, gc, scale, fault=fault, w_o=w_o, h=h, add_resid=add_resid)
+            kc2, vc2 = cs.kc.clone(), cs.vc.clone()
+            q2 = torch.zeros(1, nh * D, dtype=BF, device="cuda")
+            out2 = torch.zeros(1, nh * D, dtype=BF, device="cuda")
+            ops.qkv_attn(cs.x, cs.W, cs.nw, 1e-5, q2, kc2, vc2, cs.pos, cs.slots, cs.cos, cs.sin, cs.bt, cs.sl, out2,
+                         part, ctr, ws, nh, nkv, D, cs.bs, chunk, gc, scale, fault=fault)
+            h2 = h0.clone()
+            ops.linear(out2, w_o, ops.EPI_RESADD if add_resid else ops.EPI_BF16, out=h2)
+            torch.cuda.synchronize()
+            assert int(fault.item()) == 0, (L, it)
+            assert torch.equal(out, out2), (L, it)
+            assert torch.equal(h, h2), (L, it, (h.float() - h2.float()).abs().max().item())
+        c = ws[1].view(-1, ops.ATTN_CTR_PITCH).cpu()
+        assert int(c[0, 0]) == 0 and int(c[2, 0]) == 0  # exit count and o-role arrivals re-armed

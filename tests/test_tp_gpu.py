@@ -42,7 +42,10 @@ def _worker(rank, world, port, name, q, ekw=None):
         if ekw.pop("_expect_fused", False):
             assert tp.custom_fused is not None
         expect_ao = ekw.pop("_expect_ao", False)
+        expect_qa_o = ekw.pop("_expect_qa_o", False)
         e = Engine(FAMILIES[name], EngineConfig(device="cuda:0", max_context=512, seed=5, **ekw), tp=tp)
+        if expect_qa_o:  # the one-launch qkv + attention + o_proj runs on this TP rank's buckets
+            assert e.qa_o and any(e.qa_plan), (e.qa_o, e.qa_plan)
         if expect_ao:  # the fused attention + o_proj launch runs on this TP rank's decode buckets
             assert all(e.ao_chunks), e.ao_chunks
         e.warmup_graphs()
@@ -102,6 +105,21 @@ def test_tp2_gpu_attn_oproj_separate_allreduce_matches_tp1(cuda, monkeypatch):
     monkeypatch.setenv("LLMC_ATTN_OPROJ", "all")
     monkeypatch.setenv("LLMC_TP_ATTN_OPROJ", "1")
     _tp2_vs_tp1("llama-small", {"_expect_ao": True})
+
+
+def test_tp2_gpu_qkv_attn_o_fused_allreduce_matches_tp1(cuda, monkeypatch):
+    """TP ranks on the one-launch qkv + attention + o_proj (the o-role of qkv_attn.hip) with the
+    all-reduce in the o-role's epilogue, each rank on its own half of the chip."""
+    monkeypatch.setenv("LLMC_FUSED_AR", "force")
+    monkeypatch.setenv("LLMC_QKV_ATTN_O", "1")
+    _tp2_vs_tp1("llama-small", {"_expect_fused": True, "_cu_split": True, "_expect_qa_o": True})
+
+
+def test_tp2_gpu_qkv_attn_o_separate_allreduce_matches_tp1(cuda, monkeypatch):
+    """... and with the rank's o_proj share (rank 0: + residual) followed by the all-reduce launch."""
+    monkeypatch.setenv("LLMC_FUSED_AR", "0")
+    monkeypatch.setenv("LLMC_QKV_ATTN_O", "1")
+    _tp2_vs_tp1("llama-small", {"_expect_qa_o": True})
 
 
 def _tp2_vs_tp1(name, ekw):

@@ -37,6 +37,14 @@
 //      read it before arriving)
 //
 // Every spin is bounded: a give-up sets the fault word (checked by the engine like attn_decode's).
+//
+// MoE router in the same launch (whole-row form, an engine alone on its GPU; AoRouter): a Mixtral
+// layer's decode router (RMSNorm -> E router logits -> top-k) was its own ~6.3-us launch between
+// this one and the expert GEMVs. The logits are linear in the block's rows: logit_e =
+// rsqrt(mean h^2 + eps) * sum_n Wr[e][n] norm_w[n] h[n], so each block publishes its 16 rows'
+// share (E partial dots and the partial sum of squares, from router / norm weights it requested at
+// its start) as data-tagged granules and block 0 sums them in block order and picks the top k
+// (ao_router_tail).
 #include "attn_core.h"
 #include "car_proto.h"
 
@@ -69,6 +77,123 @@ __device__ __forceinline__ void ao_stamp(uint64_t* st, int k, bool who) {
   if (st != nullptr && who) st[k] = __builtin_amdgcn_s_memrealtime();
 }
 
+// The MoE router folded into the whole-row launch (see the header). Wr == nullptr: off.
+struct AoRouter {
+  const bf16_t* norm_w;  // the layer's post-attention RMSNorm weights [H]
+  const bf16_t* Wr;      // router weights [E][H], E <= kAoRouterMaxE
+  float eps;
+  int E, k;              // top k of E
+  float* w_out;          // [k] renormalised top-k weights
+  int32_t* ids_out;      // [k] expert ids
+  uint64_t* part;        // [9][kAoRouterMaxBlocks] {f32, tag} granules: per block its logit partials [8], sum of squares
+  int* epoch;            // granule epoch (advanced by the merger)
+};
+constexpr int kAoRouterWave = 5;  // a control wave: no weight tile in its registers
+constexpr int kAoRouterMaxE = 8, kAoRouterMaxBlocks = 256;
+
+// Router partials, one wave (kAoRouterWave) of every block, after the block's 16 h rows are final:
+// rv = those rows (bf16 values as stored, in f32), rw / rg = lane (e = lane / 4, q = lane % 4)'s
+// router / norm weights of rows 4 q .. 4 q + 3 (requested at the block's start), tag = this
+// launch's granule tag. The block's 9 values go out as data-tagged granules (no drain, no ticket).
+// Block 0's router wave then merges: it re-polls the granule rows (by quantity, so a wave load
+// reads 64 consecutive blocks' values: a few lines) until every tag is this launch's, sums them in
+// block order and picks the top k. Block 0 waits on the grid's other blocks here: this form runs
+// only for an engine alone on its GPU, where the whole grid (one block per CU) is resident; the
+// wait is bounded (fault 4). (A ticketed last-arriver merge measured 5.1 us on the chain, the
+// top-k as its own launch 4.9: profiles/r6_decode_experiments.md.)
+__device__ __forceinline__ void ao_router_tail(const AoRouter& rt, const float* rv, u32x2 rw, u32x2 rg, uint32_t tag,
+                                               int blk, int nblk, int H, int lane, int* fault) {
+  float p = 0.f;
+  if (lane < 32) {
+    const int q4 = lane & 3;
+    const float w[4] = {bf16_lo(rw[0]), bf16_hi(rw[0]), bf16_lo(rw[1]), bf16_hi(rw[1])};
+    const float gm[4] = {bf16_lo(rg[0]), bf16_hi(rg[0]), bf16_lo(rg[1]), bf16_hi(rg[1])};
+#pragma unroll
+    for (int j = 0; j < 4; ++j) p += w[j] * (gm[j] * rv[4 * q4 + j]);
+  }
+  p += __shfl_xor(p, 1, 64);
+  p += __shfl_xor(p, 2, 64);
+  float sq = lane < 16 ? rv[lane] * rv[lane] : 0.f;
+#pragma unroll
+  for (int m = 1; m < 16; m <<= 1) sq += __shfl_xor(sq, m, 64);
+  const float pv = __shfl(p, (lane & 7) * 4, 64);  // every lane takes part in both shuffles
+  const float sv = __shfl(sq, 0, 64);
+  if (lane <= 8) {
+    const uint64_t gv = static_cast<uint64_t>(__float_as_uint(lane < 8 ? pv : sv)) | (static_cast<uint64_t>(tag) << 32);
+    __hip_atomic_store(rt.part + lane * kAoRouterMaxBlocks + blk, gv, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  if (blk != 0) return;
+  constexpr int NR = kAoRouterMaxBlocks / 64;
+  uint64_t v[NR][9];
+  for (unsigned spins = 0;; ++spins) {
+    bool ok = true;
+#pragma unroll
+    for (int r = 0; r < NR; ++r) {
+      const int b = min(r * 64 + lane, nblk - 1);  // clamped: loads in flight together, masked below
+#pragma unroll
+      for (int i = 0; i < 9; ++i)
+        v[r][i] = __hip_atomic_load(rt.part + i * kAoRouterMaxBlocks + b, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+#pragma unroll
+    for (int r = 0; r < NR; ++r)
+#pragma unroll
+      for (int i = 0; i < 9; ++i) ok = ok && static_cast<uint32_t>(v[r][i] >> 32) == tag;
+    if (__all(ok)) break;
+    if (spins >= kSpinLimit) {
+      if (lane == 0 && fault != nullptr) __hip_atomic_store(fault, 4, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      break;
+    }
+    __builtin_amdgcn_s_sleep(1);
+  }
+  float acc[9];
+#pragma unroll
+  for (int i = 0; i < 9; ++i) acc[i] = 0.f;
+#pragma unroll
+  for (int r = 0; r < NR; ++r)
+    if (r * 64 + lane < nblk)
+#pragma unroll
+      for (int i = 0; i < 9; ++i) acc[i] += __uint_as_float(static_cast<uint32_t>(v[r][i]));
+#pragma unroll
+  for (int m = 32; m >= 1; m >>= 1)
+#pragma unroll
+    for (int i = 0; i < 9; ++i) acc[i] += __shfl_xor(acc[i], m, 64);
+  if (lane == 0) {
+    // softmax over the E logits, top k (lowest index on ties), renormalised: moe_router_kernel's rule
+    const float inv = rsqrtf(acc[8] / H + rt.eps);
+    float lg[kAoRouterMaxE];
+    float mx = -INFINITY;
+#pragma unroll
+    for (int e = 0; e < kAoRouterMaxE; ++e) {
+      lg[e] = acc[e] * inv;
+      if (e < rt.E) mx = fmaxf(mx, lg[e]);
+    }
+    float z = 0.f;
+#pragma unroll
+    for (int e = 0; e < kAoRouterMaxE; ++e)
+      if (e < rt.E) z += __expf(lg[e] - mx);
+    uint32_t taken = 0;
+    float sel[kAoRouterMaxE];
+    float ssum = 0.f;
+    for (int j = 0; j < rt.k; ++j) {
+      int best = 0;
+      float bv = -INFINITY;
+      for (int e = 0; e < rt.E; ++e) {
+        if ((taken >> e) & 1u) continue;
+        if (lg[e] > bv) {
+          bv = lg[e];
+          best = e;
+        }
+      }
+      taken |= 1u << best;
+      sel[j] = __expf(bv - mx) / z;
+      ssum += sel[j];
+      rt.ids_out[j] = best;
+    }
+    for (int j = 0; j < rt.k; ++j) rt.w_out[j] = sel[j] / ssum;
+    __hip_atomic_store(rt.epoch, static_cast<int>(tag), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+}
+
 // FR = 0: block (c, g) owns o_proj rows [c R, (c + 1) R) x head group g's columns, its partial
 // summed over the nkv head groups by the tile's last arriver (step 4). FR = nkv (full rows, mode
 // bit 2): block (c, g) owns R / nkv WHOLE rows [(g nc + c) R / nkv, ...) x every head group's
@@ -81,7 +206,7 @@ __global__ __launch_bounds__(kAoThreads) void attn_oproj_kernel(
     const bf16_t* __restrict__ w_o, int K_o, bf16_t* __restrict__ h, bf16_t* __restrict__ attn_out,
     float* __restrict__ part, uint32_t* __restrict__ handoff, uint64_t* __restrict__ tile_part, int* __restrict__ ctr,
     int* __restrict__ fault, int nkv, int bs, int nblocks, int chunk, float scale_log2,
-    uint64_t* __restrict__ stamps, int defer, int add_resid, CarArgs ar, int gate, int prio) {
+    uint64_t* __restrict__ stamps, int defer, int add_resid, CarArgs ar, int gate, int prio, AoRouter rt) {
   static_assert(G * D == 512, "one 16-B column chunk per lane per row");
   static_assert(RW >= 1 && RW <= 32 && (RW & (RW - 1)) == 0, "rows per wave: power of two <= 32");
   static_assert(SUBS == 1 || (SUBS == 2 && LATE), "two sub-tiles per wave only with late weights (registers)");
@@ -109,6 +234,21 @@ __global__ __launch_bounds__(kAoThreads) void attn_oproj_kernel(
   const int page = min(max(ld_scalar(block_table + pidx), 0), nblocks - 1);  // clamped into the cache
   ST st;
   st.init(q + g * G * D, lane);
+  // fused router (FR): the router wave requests its rows' router / norm weights now (tiny, behind
+  // nothing), used only after the block's o_proj rows are final
+  u32x2 rt_w = {0u, 0u}, rt_g = {0u, 0u};
+  uint32_t rt_tag = 0;
+  if constexpr (FR != 0) {
+    if (rt.Wr != nullptr && wave == kAoRouterWave) {
+      rt_tag = static_cast<uint32_t>(__hip_atomic_load(rt.epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) + 1u;
+      if (lane < 32) {
+        const int e = lane >> 2;
+        const int rb = (g * nc + c) * (R / FR) + 4 * (lane & 3);
+        if (e < rt.E) rt_w = *reinterpret_cast<const u32x2*>(rt.Wr + static_cast<int64_t>(e) * nc * R + rb);
+        rt_g = *reinterpret_cast<const u32x2*>(rt.norm_w + rb);
+      }
+    }
+  }
   const int key_hi = min(L, key_lo + chunk);
   const bool wave_keys = wk0 < key_hi;  // wave-uniform
   const bool block_keys = key_lo < L;   // block-uniform
@@ -334,10 +474,17 @@ __global__ __launch_bounds__(kAoThreads) void attn_oproj_kernel(
       for (int m = LPR / 2; m >= 1; m >>= 1) s[0] += __shfl_xor(s[0], m, 64);
       if ((lane % LPR) == 0) {
         bf16_t* hp = h + (g * nc + c) * (R / FR) + wave * RWF + lane / LPR;
-        *hp = f32_to_bf16((add_resid ? bf16_to_f32(*hp) : 0.f) + s[0]);
+        const bf16_t hv = f32_to_bf16((add_resid ? bf16_to_f32(*hp) : 0.f) + s[0]);
+        *hp = hv;
+        if (rt.Wr != nullptr) reinterpret_cast<float*>(flag + 4)[wave * RWF + lane / LPR] = bf16_to_f32(hv);
       }
       ao_stamp(stp, 5, tid == 0);
     }
+    if (rt.Wr == nullptr) return;  // block-uniform
+    __syncthreads();               // the block's 16 rows are in LDS
+    if (wave == kAoRouterWave)
+      ao_router_tail(rt, reinterpret_cast<const float*>(flag + 4), rt_w, rt_g, rt_tag, g * nc + c, nc * gridDim.y, nc * R,
+                     lane, fault);
     return;
   }
 
@@ -489,7 +636,8 @@ extern "C" int llmc_attn_oproj_check(int H, int nh, int nkv, int D, int nc, int 
 // block (FR, see the kernel); bit 3 (with late weights): the weight gate — no block requests its
 // weights before every block of the grid has streamed its K/V (lone engines); bit 4: the control
 // waves run at a higher issue priority than the o waves (s_setprio).
-// fault codes: 1 a partial never arrived (merge), 2 the head output never arrived, 3 a tile partial.
+// fault codes: 1 a partial never arrived (merge), 2 the head output never arrived, 3 a tile partial,
+// 4 a router granule (rt_*).
 // stamps (nullable, diagnostics): uint64 [nkv][nc][8] s_memrealtime per block: 0 start, 1 o wave 0's
 // attention done, 2 control wave 4's attention done, 3 head ticket taken, 4 head output in LDS,
 // 5 o wave 0's tile partial published, 6 tile ticket taken, 7 tile reduced (reducer only).
@@ -501,14 +649,40 @@ extern "C" int llmc_attn_oproj_check(int H, int nh, int nkv, int D, int nc, int 
 // over `bases` = every rank's fused-all-reduce buffer, `cap` bytes per data parity, host status
 // page `host`): h = sum over ranks, rank 0's term carrying the residual (add_resid = rank == 0).
 // The whole-row form (mode bit 2) has no tile reducer: never with world > 1.
+// Which form a launch of this shape and mode takes: 2 = whole rows (FR), 1 = tile partials, 0 = not
+// covered. The fused MoE router (rt_wr != nullptr) needs the whole-row form.
+extern "C" int llmc_attn_oproj_form(int H, int nh, int nkv, int D, int nc, int chunk, int mode, int world) {
+  if (llmc_attn_oproj_check(H, nh, nkv, D, nc, nh * D) != 0) return 0;
+  const bool two = chunk > kAoWaves * 32;
+  const bool late = (mode & 1) != 0 || two;
+  const int G = nh / nkv, rw = H / nc / 4;
+  const bool fr = (mode & 4) != 0 && late && nkv == kAoMaxKv && G == 4 && D == 128 && rw == 32 && world <= 1;
+  return fr ? 2 : 1;
+}
+
+// rt_* (nullable rt_wr = off; whole-row form, world 1, an engine alone on its GPU, E <= 8 experts):
+// the layer's MoE decode router on the launch's output row — top rt_k ids (rt_ids int32 [k]) and
+// renormalised weights (rt_w f32 [k]) as moe_router writes them; rt_part u64 [9][256] granules and
+// rt_epoch int32 (one 64-B line), zeroed once. Fault code 4: the router merge gave up on a granule.
 extern "C" int llmc_attn_oproj(const void* q, const void* k_cache, const void* v_cache, const void* block_table,
                                int bt_len, const void* seq_len, const void* w_o, void* h, void* attn_out, void* part,
                                void* handoff, void* tile_part, void* ctr, void* fault, int H, int nh, int nkv, int D,
                                int bs, int nblocks, int chunk, int nc, float scale, int mode, void* stamps,
                                int add_resid, const void* const* bases, void* host, int rank, int world, size_t cap,
-                               hipStream_t s) {
+                               const void* rt_norm, const void* rt_wr, float rt_eps, int rt_E, int rt_k, void* rt_w,
+                               void* rt_ids, void* rt_part, void* rt_epoch, hipStream_t s) {
   const int K_o = nh * D;
   if (llmc_attn_oproj_check(H, nh, nkv, D, nc, K_o) != 0) return -1;
+  AoRouter rt{};
+  if (rt_wr != nullptr) {
+    if (llmc_attn_oproj_form(H, nh, nkv, D, nc, chunk, mode, world) != 2 || rt_E < 1 || rt_E > kAoRouterMaxE ||
+        rt_k < 1 || rt_k > rt_E || nc * nkv > kAoRouterMaxBlocks || rt_norm == nullptr || rt_w == nullptr ||
+        rt_ids == nullptr || rt_part == nullptr || rt_epoch == nullptr)
+      return -7;
+    rt = AoRouter{static_cast<const bf16_t*>(rt_norm), static_cast<const bf16_t*>(rt_wr), rt_eps, rt_E, rt_k,
+                  static_cast<float*>(rt_w), static_cast<int32_t*>(rt_ids), static_cast<uint64_t*>(rt_part),
+                  static_cast<int*>(rt_epoch)};
+  }
   CarArgs ar{};
   if (world > 1) {
     if (world > kMaxRanks || rank < 0 || rank >= world || bases == nullptr) return -1;
@@ -532,7 +706,7 @@ extern "C" int llmc_attn_oproj(const void* q, const void* k_cache, const void* v
   const bool fr = (mode & 4) != 0 && late && nkv == kAoMaxKv && G == 4 && D == 128 && rw == 32 &&
                   world <= 1;  // full rows (no tile reducer to run the all-reduce)
   const size_t lds = kAoWaves * 32 * kVRowBytes + static_cast<size_t>(kAoWaves) * G * (D + 2) * sizeof(float) +
-                     (fr ? kAoMaxKv : 1) * 64 * 16 + 16;
+                     (fr ? kAoMaxKv : 1) * 64 * 16 + 16 + 16 * sizeof(float);  // + flag, router rows
   dim3 grid(nc, nkv);
   const float sl2 = scale * 1.4426950408889634f;
 #define LLMC_AO_K(KERN)                                                                                          \
@@ -542,7 +716,7 @@ extern "C" int llmc_attn_oproj(const void* q, const void* k_cache, const void* v
       (const bf16_t*)q, (const bf16_t*)k_cache, (const bf16_t*)v_cache, (const int32_t*)block_table, bt_len,       \
       (const int32_t*)seq_len, (const bf16_t*)w_o, K_o, (bf16_t*)h, (bf16_t*)attn_out, (float*)part,               \
       (uint32_t*)handoff, (uint64_t*)tile_part, (int*)ctr, (int*)fault, nkv, bs, nblocks, chunk, sl2, (uint64_t*)stamps, \
-      (mode >> 1) & 1, add_resid, ar, late ? (mode >> 3) & 1 : 0, (mode >> 4) & 1); \
+      (mode >> 1) & 1, add_resid, ar, late ? (mode >> 3) & 1 : 0, (mode >> 4) & 1, rt); \
   } while (0)
 #define LLMC_AO(GG, DD, RR)                                                                                      \
   do {                                                                                                            \

@@ -38,9 +38,11 @@ int llmc_qkv_attn(const void*, const void*, float, const void*, int, void*, void
                   int, int, int, float, void*, void*, void*, int, const void*, void*, int, const void* const*, void*,
                   int, int, size_t, hipStream_t);
 int llmc_attn_oproj_check(int, int, int, int, int, int);
+int llmc_attn_oproj_form(int, int, int, int, int, int, int, int);
 int llmc_attn_oproj(const void*, const void*, const void*, const void*, int, const void*, const void*, void*, void*,
                     void*, void*, void*, void*, void*, int, int, int, int, int, int, int, int, float, int, void*,
-                    int, const void* const*, void*, int, int, size_t, hipStream_t);
+                    int, const void* const*, void*, int, int, size_t, const void*, const void*, float, int, int,
+                    void*, void*, void*, void*, hipStream_t);
 int llmc_attn_decode(const void*, int, const void*, const void*, const void*, int, const void*, void*, void*, void*,
                      int, int, int, int, int, int, int, int, int, int, float, int, void*, hipStream_t);
 int llmc_gemv_qkv_rope(int, const void*, int, const void*, float, const void*, int, int, void*, int, void*, void*,
@@ -165,15 +167,21 @@ PYBIND11_MODULE(_llmc_hip, m) {
   m.def("attn_oproj_check", [](int H, int nh, int nkv, int D, int nc, int K_o) {
     return llmc_attn_oproj_check(H, nh, nkv, D, nc, K_o);
   });
+  m.def("attn_oproj_form", [](int H, int nh, int nkv, int D, int nc, int chunk, int mode, int world) {
+    return llmc_attn_oproj_form(H, nh, nkv, D, nc, chunk, mode, world);
+  });
   m.def("attn_oproj", [](ptr q, ptr kc, ptr vc, ptr bt, int bt_len, ptr sl, ptr w_o, ptr h, ptr attn_out, ptr part,
                          ptr handoff, ptr tile_part, ptr ctr, ptr fault, int H, int nh, int nkv, int D, int bs,
                          int nblocks, int chunk, int nc, float scale, int mode, ptr stamps, int add_resid,
-                         const std::vector<ptr>& bases, ptr host, int rank, int world, size_t cap, ptr s) {
+                         const std::vector<ptr>& bases, ptr host, int rank, int world, size_t cap, ptr rt_norm,
+                         ptr rt_wr, float rt_eps, int rt_E, int rt_k, ptr rt_w, ptr rt_ids, ptr rt_part,
+                         ptr rt_epoch, ptr s) {
     std::vector<const void*> b(bases.size());
     for (size_t i = 0; i < bases.size(); ++i) b[i] = P(bases[i]);
     check(llmc_attn_oproj(P(q), P(kc), P(vc), P(bt), bt_len, P(sl), P(w_o), P(h), P(attn_out), P(part), P(handoff),
                           P(tile_part), P(ctr), P(fault), H, nh, nkv, D, bs, nblocks, chunk, nc, scale, mode, P(stamps),
-                          add_resid, b.empty() ? nullptr : b.data(), P(host), rank, world, cap, S(s)),
+                          add_resid, b.empty() ? nullptr : b.data(), P(host), rank, world, cap, P(rt_norm), P(rt_wr),
+                          rt_eps, rt_E, rt_k, P(rt_w), P(rt_ids), P(rt_part), P(rt_epoch), S(s)),
           "attn_oproj");
   });
   m.def("attn_decode", [](ptr q, int qs, ptr kc, ptr vc, ptr bt, int bts, ptr sl, ptr part, ptr ctr, ptr out, int os,
@@ -240,9 +248,9 @@ PYBIND11_MODULE(_llmc_hip, m) {
   m.def("moe_combine", [](ptr y, ptr w, ptr rows, ptr out, int T, int k, int H, ptr s) {
     check(llmc_moe_combine(P(y), P(w), P(rows), P(out), T, k, H, S(s)), "moe_combine");
   });
-  m.def("moe_gemv", [](int k, ptr x, int xs, ptr nw, float eps, ptr W, ptr ids, int ids_stride, ptr out, int os,
+  m.def("moe_gemv", [](int npairs, ptr x, int xs, ptr nw, float eps, ptr W, ptr ids, int x_div, ptr out, int os,
                        int N, int K, int epi, ptr s) {
-    check(llmc_moe_gemv(k, P(x), xs, P(nw), eps, P(W), P(ids), ids_stride, P(out), os, N, K, epi, S(s)), "moe_gemv");
+    check(llmc_moe_gemv(npairs, P(x), xs, P(nw), eps, P(W), P(ids), x_div, P(out), os, N, K, epi, S(s)), "moe_gemv");
   });
   m.def("moe_ep_dispatch", [](ptr ids, int npairs, int El, int n, int cap, ptr sp, ptr se, ptr slot, ptr cnt, ptr s) {
     check(llmc_moe_ep_dispatch(P(ids), npairs, El, n, cap, P(sp), P(se), P(slot), P(cnt), S(s)), "moe_ep_dispatch");

@@ -83,6 +83,10 @@ class EngineConfig:
     # ... and the token's o_proj (+ the TP all-reduce in its epilogue, ``fused_ar``) in the same
     # launch (the o-role of csrc/kernels/qkv_attn.hip) instead of the o GEMV after it (LLMC_QKV_ATTN_O)
     qkv_attn_o: bool = dataclasses.field(default_factory=lambda: os.environ.get("LLMC_QKV_ATTN_O", "0") == "1")
+    # MoE engines alone on one GPU: in the buckets that run the fused attention + o_proj's whole-row
+    # form, the decode router (RMSNorm -> logits -> top-k) inside that launch instead of its own
+    # launch after it (csrc/kernels/attn_oproj.hip AoRouter; LLMC_AO_ROUTER=0: the router launch)
+    ao_router: bool = dataclasses.field(default_factory=lambda: os.environ.get("LLMC_AO_ROUTER", "1") != "0")
     # TP engines: the decode all-reduce inside the row-parallel GEMVs' epilogue when the group has
     # the fused buffer (TPGroup.custom_fused). Its 256 blocks spin per block on their peers, so an
     # engine whose GPUs also run other engines' decode at the same time (bench.py's N=2 third
@@ -338,6 +342,14 @@ class Engine:
             if any(self.qa_plan):
                 self.qa_ws = ops.qkv_attn_workspace(self.nh, self.nkv, self.D, dev)
         self.qa_buckets = [p is not None for p in self.qa_plan]
+        # MoE router inside the fused attention + o_proj launch (whole-row form buckets)
+        self.ao_router = [False] * len(self.attn_buckets)
+        if (self.ao_nc and c.is_moe and self.tp.size == 1 and not self.w.ep and self.ecfg.ao_router
+                and c.n_experts <= 8 and not self.mfma_decode):
+            self.ao_router = [bool(ch) and ops.attn_oproj_form(c.hidden, self.nh, self.nkv, self.D, self.ao_nc, ch) == 2
+                              for ch in self.ao_chunks]
+            if any(self.ao_router):
+                self.ao_rws = ops.attn_oproj_router_workspace(self.nkv, self.ao_nc, dev)
         self.qa_o = (any(self.qa_plan) and self.ecfg.qkv_attn_o
                      and ops.qkv_attn_o_supported(self.nh, self.D, c.hidden))
         max_chunks = max([gc for _, _, gc, _ in self.attn_buckets] + [p[1] for p in self.qa_plan if p])
@@ -673,6 +685,7 @@ class Engine:
         for li, Lw in enumerate(layers):
             if dbg is not None:
                 dbg.append(h.clone())
+            routed = False
             if qa:  # qkv projection + attention in one launch (one row), then o_proj
                 o_in = self.qa_o and h.is_cuda  # ... o_proj (+ all-reduce) in the same launch
                 tp = self.tp
@@ -691,14 +704,15 @@ class Engine:
                              self.positions[:B], self.slots[:B], self.cos_t, self.sin_t, self.nh, self.nkv, self.D,
                              self.bs, mfma=self.mfma_decode)
                 if ao_chunk:  # one-row engines: attention + o_proj + residual (+ TP all-reduce) in one launch
-                    self._attn_oproj(q, li, Lw, h, attn, ao_chunk)
+                    routed = self.ao_router[bi] and h.is_cuda  # ... (+ the MoE router)
+                    self._attn_oproj(q, li, Lw, h, attn, ao_chunk, routed)
                 else:
                     ops.attn_decode(q, self.k_cache[li], self.v_cache[li], self.block_tables[:B], self.seq_lens[:B],
                                     attn, part[:B], self.attn_counters[:B], self.nh, self.nkv, self.D, self.bs, chunk,
                                     self.scale, grid_chunks, fused=fused, fault=self.attn_fault)
                     self._row_parallel(attn, Lw.w_o, h)
             if c.is_moe:
-                self._moe_decode(h, Lw, B)
+                self._moe_decode(h, Lw, B, routed)
             else:
                 ops.linear(h, Lw.w_gu, EPI_SILU, out=act, norm_w=Lw.ln2, eps=c.rms_eps, mfma=self.mfma_decode)
                 self._row_parallel(act, Lw.w_down, h)
@@ -708,16 +722,21 @@ class Engine:
 
     _debug_layer_io: Optional[list] = None
 
-    def _attn_oproj(self, q, li, Lw, h, attn, chunk) -> None:
+    def _attn_oproj(self, q, li, Lw, h, attn, chunk, routed: bool = False) -> None:
         """h += o_proj(attention(q)) for one row in one launch (csrc/kernels/attn_oproj.hip). A TP rank
         computes its row-parallel share (rank 0's carries the residual) and all-reduces it inside the
         kernel when the group has the fused buffer (``fused_ar``), else with the group's all-reduce
-        launch after it."""
+        launch after it. ``routed``: the MoE layer's router on the new h in the same launch (into
+        moe_w / moe_ids, as _moe_decode's router launch would write them)."""
         tp = self.tp
         car = tp.custom_fused if (tp.size > 1 and self.ecfg.fused_ar) else None
+        router = None
+        if routed:
+            router = (Lw.ln2, Lw.w_router, self.cfg.rms_eps, self.cfg.top_k_experts, self.moe_w[:1], self.moe_ids[:1],
+                      self.ao_rws)
         ops.attn_oproj(q, self.k_cache[li], self.v_cache[li], self.block_tables[:1], self.seq_lens[:1], Lw.w_o, h, attn,
                        self.ao_ws, self.nh, self.nkv, self.D, self.bs, chunk, self.ao_nc, self.scale,
-                       fault=self.attn_fault, add_resid=tp.rank == 0, car=car)
+                       fault=self.attn_fault, add_resid=tp.rank == 0, car=car, router=router)
         if tp.size > 1 and car is None:
             tp.all_reduce_(h)
 
@@ -757,7 +776,8 @@ class Engine:
         logits = self._gather_logits(B)
         self._sample(B, logits)
 
-    def _moe_decode(self, h, Lw, B) -> None:
+    def _moe_decode(self, h, Lw, B, routed: bool = False) -> None:
+        """``routed``: the fused attention + o_proj launch already wrote moe_w / moe_ids."""
         c = self.cfg
         if not h.is_cuda:
             xn = self.xn[:B]
@@ -768,7 +788,8 @@ class Engine:
         w, ids = self.moe_w[:B], self.moe_ids[:B]
         # one launch: rmsnorm -> router logits -> top-k; the expert gate_up GEMV normalises h
         # again in its own prologue, so the normed row never goes through memory
-        ops.moe_router(h, Lw.ln2, c.rms_eps, Lw.w_router, k, w, ids)
+        if not routed:
+            ops.moe_router(h, Lw.ln2, c.rms_eps, Lw.w_router, k, w, ids)
         if self.w.ep:  # pairs of other ranks' experts: id -1 (GEMV blocks exit), weight 0
             ops.moe_ep_localize(ids, w, self.w.e0, self.w.n_local_experts, self.moe_lids[:B], self.moe_lw[:B])
             w, ids = self.moe_lw[:B], self.moe_lids[:B]

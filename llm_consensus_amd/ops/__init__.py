@@ -394,9 +394,25 @@ def attn_oproj_workspace(H: int, nh: int, nkv: int, D: int, nc: int, device):
     return part, handoff, tile_part, counters
 
 
+def attn_oproj_form(H: int, nh: int, nkv: int, D: int, nc: int, chunk: int, mode: int = -1, world: int = 1) -> int:
+    """The form ``attn_oproj`` takes for this shape / bucket / mode: 2 = whole o_proj rows per block
+    (mode bit 2's form, the one that can run the MoE router too), 1 = tile partials, 0 = not covered."""
+    return int(kernels().attn_oproj_form(H, nh, nkv, D, nc, chunk, ATTN_OPROJ_MODE if mode < 0 else mode, world))
+
+
+def attn_oproj_router_workspace(nkv: int, nc: int, device):
+    """(granules int64 [9, 256]: per block its 8 logit partials and sum of squares as {f32, tag};
+    epoch int32 [16]) of the MoE router in ``attn_oproj(..., router=)``, zeroed once (the launch
+    advances the epoch)."""
+    if nkv * nc > 256:
+        raise ValueError("attn_oproj router: at most 256 blocks")
+    dev = torch.device(device)
+    return (torch.zeros(9, 256, dtype=torch.int64, device=dev), torch.zeros(16, dtype=torch.int32, device=dev))
+
+
 def attn_oproj(q, k_cache, v_cache, block_table, seq_len, w_o, h, attn_out, ws, nh, nkv, D, bs, chunk, nc, scale,
                fault: Optional[torch.Tensor] = None, stamps: Optional[torch.Tensor] = None, mode: int = -1,
-               add_resid: bool = True, car=None) -> None:
+               add_resid: bool = True, car=None, router=None) -> None:
     """Decode attention of ONE row followed by its o_proj and residual add, in one launch
     (csrc/kernels/attn_oproj.hip): ``h[0] += w_o @ attention(q[0])``; ``attn_out[0]`` also gets the
     attention output. ``ws`` = ``attn_oproj_workspace(...)``; ``chunk`` = ``attn_oproj_chunk(cap,
@@ -409,7 +425,13 @@ def attn_oproj(q, k_cache, v_cache, block_table, seq_len, w_o, h, attn_out, ws, 
     Tensor-parallel ranks (``h`` gets this rank's row-parallel share): ``add_resid`` False writes
     h = W_o . attention (a rank != 0 whose all-reduce follows as its own launch); ``car`` (the
     group's fused-all-reduce ``CustomAllReduce``) runs the all-reduce in the kernel's tile-reducer
-    epilogue: h = the sum over ranks, rank 0's term carrying the residual (pass add_resid = rank 0)."""
+    epilogue: h = the sum over ranks, rank 0's term carrying the residual (pass add_resid = rank 0).
+
+    ``router`` = (norm_w, W_router, eps, k, w_out, ids_out, rws): the MoE layer's decode router on
+    the launch's output row in the same launch — ``moe_router(h, norm_w, eps, W_router, k, w_out,
+    ids_out)``'s outputs up to the logits' summation order; ``rws`` =
+    ``attn_oproj_router_workspace``; needs ``attn_oproj_form(...) == 2``, no ``car`` and an engine
+    alone on its GPU (block 0 of the grid waits on the others' router partials; GPU only)."""
     H = h.shape[-1]
     if not q.is_cuda:
         if car is not None:
@@ -417,17 +439,28 @@ def attn_oproj(q, k_cache, v_cache, block_table, seq_len, w_o, h, attn_out, ws, 
         a = oracle.attn_decode(q[:1], k_cache, v_cache, block_table[:1], seq_len[:1], nh, nkv, D, bs, scale)
         attn_out[:1].copy_(a)
         oracle.linear(attn_out[:1], w_o, EPI_RESADD if add_resid else EPI_BF16, h[:1])
+        if router is not None:
+            raise ValueError("attn_oproj: the router partials are a GPU form")
         return
     if chunk <= 0 or chunk * nc < 1 or nc != ws[0].shape[1]:
         raise ValueError("attn_oproj: chunk / workspace do not match (attn_oproj_chunk, attn_oproj_workspace)")
     part, handoff, tile_part, counters = ws
     bases, host, rank, world, cap = (([], 0, 0, 1, 0) if car is None else
                                      (car.bases, car.host_dev, car.rank, car.world, car.cap))
+    rt = (None, None, 0.0, 0, 0, None, None, None, None)
+    if router is not None:
+        if car is not None:
+            raise ValueError("attn_oproj: the fused router runs on one-GPU engines only")
+        norm_w, W_r, eps, k, w_out, ids_out, (rpart, repoch) = router
+        if tuple(rpart.shape) != (9, 256) or W_r.shape[1] != H:
+            raise ValueError("attn_oproj: router workspace / weights do not match")
+        rt = (norm_w, W_r, float(eps), W_r.shape[0], int(k), w_out, ids_out, rpart, repoch)
     kernels().attn_oproj(_p(q), _p(k_cache), _p(v_cache), _p(block_table), block_table.shape[-1], _p(seq_len), _p(w_o),
                          _p(h), _p(attn_out), _p(part), _p(handoff), _p(tile_part), _p(counters), _p(fault), H, nh, nkv,
                          D, bs, k_cache.shape[0], chunk, nc, float(scale),
                          ATTN_OPROJ_MODE if mode < 0 else mode, _p(stamps), int(bool(add_resid)), bases, host, rank,
-                         world, cap, _s(h))
+                         world, cap, _p(rt[0]), _p(rt[1]), rt[2], rt[3], rt[4], _p(rt[5]), _p(rt[6]), _p(rt[7]),
+                         _p(rt[8]), _s(h))
 
 
 # KV split of the prefill attention: -1 = the kernel library's plan (llmc_attn_prefill_plan),

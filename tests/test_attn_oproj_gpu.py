@@ -269,3 +269,125 @@ def test_attn_oproj_weight_gate_is_timing_only(cuda, nh, nkv, D, H, L, cap):
         assert torch.equal(o[0], outs[0][0]) and torch.equal(o[1], outs[0][1])
     c = ws[3].view(-1, 16).cpu()
     assert int(c[nkv + nc + 1, 0]) == 0 and int(c[nkv + nc + 1, 1]) == 3  # arrivals re-armed, 3 gated launches
+
+
+@pytest.mark.parametrize("L,cap", [(100, 2048), (2048, 2048), (5000, 8192), (9000, 16384)])
+def test_attn_oproj_fused_moe_router(cuda, L, cap):
+    """Mixtral's attention shape (32 q / 8 kv heads x 128, H 4096; 8 experts, top 2): the decode
+    router inside the whole-row attention + o_proj launch. h and the attention output are the bits
+    of the launch without it; the ids are moe_router's on that h (and the fp32 oracle's top 2), the
+    weights agree to f32 rounding (another summation order), the expert gate_up GEMV on them is the
+    bits of the one on moe_router's ids; launch after launch (the epoch advances) and from a HIP
+    graph the same bits."""
+    nh, nkv, D, H, bs, E, k, eps, inter = 32, 8, 128, 4096, 64, 8, 2, 1e-5, 1024
+    nc = ops.attn_oproj_grid(H, nh, nkv, D)
+    chunk = ops.attn_oproj_chunk(cap, nc)
+    assert chunk and ops.attn_oproj_form(H, nh, nkv, D, nc, chunk) == 2
+    assert ops.attn_oproj_form(H, nh, nkv, D, nc, chunk, mode=3) == 1  # tile form: no partials there
+    kc, vc, bt, sl, q, w_o, h0 = _case(L, nh, nkv, D, H, bs, seed=3)
+    scale = 1 / math.sqrt(D)
+    g = torch.Generator(device="cuda").manual_seed(11)
+    norm_w = (1 + 0.1 * torch.randn(H, device="cuda", generator=g)).to(BF)
+    W_r = (torch.randn(E, H, device="cuda", generator=g) / math.sqrt(H)).to(BF)
+    W_gu = (torch.randn(E, 2 * inter, H, device="cuda", generator=g) / math.sqrt(H)).to(BF)
+    ws = ops.attn_oproj_workspace(H, nh, nkv, D, nc, "cuda")
+    rws = ops.attn_oproj_router_workspace(nkv, nc, "cuda")
+    fault = torch.zeros(1, dtype=torch.int32, device="cuda")
+    btd, sld = bt.cuda(), sl.cuda()
+    h_ref = h0.clone()
+    a_ref = torch.zeros(1, nh * D, dtype=BF, device="cuda")
+    ops.attn_oproj(q, kc, vc, btd, sld, w_o, h_ref, a_ref, ws, nh, nkv, D, bs, chunk, nc, scale, fault=fault)
+    w_ref = torch.zeros(1, k, dtype=torch.float32, device="cuda")
+    ids_ref = torch.zeros(1, k, dtype=torch.int32, device="cuda")
+    ops.moe_router(h_ref, norm_w, eps, W_r, k, w_ref, ids_ref)
+    act_ref = torch.zeros(k, inter, dtype=BF, device="cuda")
+    ops.moe_gemv(h_ref, W_gu, ids_ref, k, act_ref, 2 * inter, H, ops.EPI_SILU, norm_w=norm_w, eps=eps)
+    torch.cuda.synchronize()
+    # fp32 oracle of the logits on that h: its top 2 (skip the id checks on a near-tie)
+    hf = h_ref.float().cpu()
+    xn = hf * torch.rsqrt(hf.pow(2).mean(-1, keepdim=True) + eps) * norm_w.float().cpu()
+    lg = (xn @ W_r.float().cpu().t())[0]
+    top = torch.sort(lg, descending=True)
+    tie = float(top.values[k - 1] - top.values[k]) < 1e-3
+
+    h = h0.clone()
+    a = torch.zeros(1, nh * D, dtype=BF, device="cuda")
+    w = torch.zeros(1, k, dtype=torch.float32, device="cuda")
+    ids = torch.zeros(1, k, dtype=torch.int32, device="cuda")
+    act = torch.zeros(k, inter, dtype=BF, device="cuda")
+
+    def launch():
+        ops.attn_oproj(q, kc, vc, btd, sld, w_o, h, a, ws, nh, nkv, D, bs, chunk, nc, scale, fault=fault,
+                       router=(norm_w, W_r, eps, k, w, ids, rws))
+        ops.moe_gemv(h, W_gu, ids, k, act, 2 * inter, H, ops.EPI_SILU, norm_w=norm_w, eps=eps)
+
+    def check(tag):
+        assert int(fault.item()) == 0
+        assert torch.equal(h, h_ref) and torch.equal(a, a_ref), tag
+        if not tie:
+            assert torch.equal(ids, ids_ref), (tag, ids, ids_ref)
+            assert sorted(ids[0].tolist()) == sorted(top.indices[:k].tolist())
+            assert torch.equal(act, act_ref), tag
+        assert (w - w_ref).abs().max().item() < 1e-3, (tag, w, w_ref)
+        assert abs(float(w.sum()) - 1.0) < 1e-5
+
+    outs = []
+    for it in range(3):
+        h.copy_(h0)
+        w.fill_(-1.0)
+        ids.fill_(-1)
+        act.zero_()
+        launch()
+        torch.cuda.synchronize()
+        check(it)
+        assert int(rws[1][0].item()) == it + 1  # the epoch advanced once per launch
+        outs.append((ids.clone(), w.clone(), act.clone()))
+    for o in outs[1:]:
+        assert all(torch.equal(x, y) for x, y in zip(o, outs[0]))
+    s = torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(s):
+        launch()
+    torch.cuda.current_stream().wait_stream(s)
+    gr = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(gr):
+        launch()
+    for it in range(3):
+        h.copy_(h0)
+        w.zero_()
+        ids.zero_()
+        act.zero_()
+        gr.replay()
+        torch.cuda.synchronize()
+        check(("graph", it))
+        assert torch.equal(ids, outs[0][0]) and torch.equal(w, outs[0][1]) and torch.equal(act, outs[0][2])
+
+
+def test_engine_fused_moe_router_matches_router_launch(cuda):
+    """A two-layer Mixtral-8x7B-shaped engine (the whole-row attention + o_proj form needs its H =
+    4096): teacher-forced greedy logits with the router folded into the attention + o_proj launch
+    against the router's own launch, same weights; graph replay == eager with the fold."""
+    cfg = FAMILIES["mixtral-8x7b"].with_(name="mixtral-8x7b-2l", n_layers=2)
+    w = TransformerWeights(cfg, TPGroup.single(), torch.device("cuda:0"), seed=5)
+    plen = 300
+    ctx = plen + 64
+    ea = Engine(cfg, EngineConfig(device="cuda:0", max_context=ctx, attn_oproj=True, attn_oproj_min_chunk=32,
+                                  ao_router=True), weights=w)
+    eb = Engine(cfg, EngineConfig(device="cuda:0", max_context=ctx, attn_oproj=True, attn_oproj_min_chunk=32,
+                                  ao_router=False), weights=w)
+    assert any(ea.ao_router) and not any(eb.ao_router)
+    prompt = [(i * 7919) % (cfg.vocab - 300) + 256 for i in range(plen)]
+    n = 8
+    ta, la = ea.debug_decode_logits(prompt, n)
+    tb, lb = eb.debug_decode_logits(prompt, n)
+    for i in range(n):
+        if ta[:i] != tb[:i]:  # a near-tie sent the greedy streams apart
+            break
+        err = (la[i] - lb[i]).abs().max().item()
+        assert err < 0.02 * max(1.0, lb[i].abs().max().item()), (i, err)
+    a = ea.generate_ids(prompt, 16, temperature=0.8, seed=7, stop_on_eos=False)
+    ee = Engine(cfg, EngineConfig(device="cuda:0", max_context=ctx, attn_oproj=True, attn_oproj_min_chunk=32,
+                                  ao_router=True, use_graphs=False), weights=w)
+    b = ee.generate_ids(prompt, 16, temperature=0.8, seed=7, stop_on_eos=False)
+    assert a == b
+    assert int(ea.attn_fault.item()) == 0

@@ -167,7 +167,8 @@ __device__ __forceinline__ void qa_attention(int c, int kvh, char* smem, const i
 // all-reduce in this epilogue (car_proto.h push protocol, gemv_core.h EPI_AR's exchange: the block's
 // 16 rows as 8 granules of its virtual block bo, the same epoch words as the row-parallel GEMVs'
 // EPI_AR). Replaces the o GEMV launch after the one-launch qkv + attention on TP ranks.
-constexpr int kOrRpw = 4, kOrRows = kOrRpw * kQaWaves, kOrMaxCpl = 4;  // rows per wave / block; 16-B chunks per lane per row
+constexpr int kOrRpw = 4, kOrRows = kOrRpw * kQaWaves, kOrMaxCpl = 4;
+static_assert(kOrMaxCpl == 4, "the CPL dispatch below covers 1..4");  // rows per wave / block; 16-B chunks per lane per row
 
 struct OArgs {
   const bf16_t* w_o;  // [n_o, k_o]
@@ -301,9 +302,14 @@ __global__ __launch_bounds__(kQaThreads) void qkv_attn_kernel(
   const int no = o.mode != 0 ? (o.n_o + kOrRows - 1) / kOrRows : 0;
   if (static_cast<int>(blockIdx.x) >= nq + A) {  // block-uniform: the o-role
     const int bo = blockIdx.x - nq - A;
-    if (o.k_o <= kWave * 8) qa_oproj_block<1>(bo, smem, out, o, adone, A, fault);
-    else if (o.k_o <= 2 * kWave * 8) qa_oproj_block<2>(bo, smem, out, o, adone, A, fault);
-    else qa_oproj_block<kOrMaxCpl>(bo, smem, out, o, adone, A, fault);
+    // exactly k_o / 512 chunks per lane per row (host: k_o a multiple of 512, <= kOrMaxCpl x 512):
+    // a wider instantiation would read past the row (and past W_o at its last row)
+    switch (o.k_o / (kWave * 8)) {
+      case 1: qa_oproj_block<1>(bo, smem, out, o, adone, A, fault); break;
+      case 2: qa_oproj_block<2>(bo, smem, out, o, adone, A, fault); break;
+      case 3: qa_oproj_block<3>(bo, smem, out, o, adone, A, fault); break;
+      default: qa_oproj_block<kOrMaxCpl>(bo, smem, out, o, adone, A, fault); break;
+    }
   } else {
     const int g = (blockIdx.x - nq) / gc, c = (blockIdx.x - nq) % gc;
     const int L = ld_scalar(seq_len);

@@ -207,6 +207,7 @@ def test_engine_qkv_attn_all_replaces_attn_oproj(cuda):
 @pytest.mark.parametrize("nh,nkv,D,K,H", [(4, 1, 128, 4096, 4096),   # 8B TP=8 rank: o_proj K = 512
                                           (8, 2, 128, 4096, 4096),   # 8B TP=4 rank: K = 1024
                                           (16, 4, 128, 4096, 4096),  # 8B TP=2 rank: K = 2048
+                                          (16, 16, 96, 3072, 3072),  # Phi-3 TP=2 rank: K = 1536 (3 chunks)
                                           (8, 1, 64, 1024, 1000)])   # a partial last row block
 @pytest.mark.parametrize("add_resid", [True, False])
 def test_qkv_attn_o_role_matches_the_o_gemv(cuda, nh, nkv, D, K, H, add_resid):

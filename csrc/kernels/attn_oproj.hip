@@ -97,10 +97,12 @@ constexpr int kAoRouterMaxE = 8, kAoRouterMaxBlocks = 256;
 // launch's granule tag. The block's 9 values go out as data-tagged granules (no drain, no ticket).
 // Block 0's router wave then merges: it re-polls the granule rows (by quantity, so a wave load
 // reads 64 consecutive blocks' values: a few lines) until every tag is this launch's, sums them in
-// block order and picks the top k. Block 0 waits on the grid's other blocks here: this form runs
-// only for an engine alone on its GPU, where the whole grid (one block per CU) is resident; the
-// wait is bounded (fault 4). (A ticketed last-arriver merge measured 5.1 us on the chain, the
-// top-k as its own launch 4.9: profiles/r6_decode_experiments.md.)
+// block order and picks the top k. Block 0 waits on the grid's other blocks here, none of which
+// ever waits on block 0 (no cycle, whatever the residency: a block not yet resident gets its CU
+// when some kernel's block finishes); for an engine alone on its GPU the whole 256-block grid is
+// resident and the wait ends with the last block's publish. Bounded (fault 4). (A ticketed
+// last-arriver merge measured 5.1 us on the chain, the top-k as its own launch 4.9:
+// profiles/r6_decode_experiments.md.)
 __device__ __forceinline__ void ao_router_tail(const AoRouter& rt, const float* rv, u32x2 rw, u32x2 rg, uint32_t tag,
                                                int blk, int nblk, int H, int lane, int* fault) {
   float p = 0.f;

@@ -313,10 +313,15 @@ def bench_qkv_rope():
         def plain():
             for W in Ws:
                 ops.gemv(x, W, 0, out=out, norm_w=nw)
+
+        def bare():
+            for W in Ws:
+                ops.gemv(x, W, 0, out=out)
         tr = timeit(rope, iters=2, warm=1) / copies
         tp = timeit(plain, iters=2, warm=1) / copies
-        print(f"qkv nh={nh} nkv={nkv} D={D} H={H} (N={N}): rope+kv epilogue {tr:6.2f} us, plain {tp:6.2f} us",
-              flush=True)
+        tb = timeit(bare, iters=2, warm=1) / copies
+        print(f"qkv nh={nh} nkv={nkv} D={D} H={H} (N={N}, {N * H * 2 / 1e6:.1f} MB): rope+kv epilogue {tr:6.2f} us, "
+              f"plain (norm prologue) {tp:6.2f} us, bare (no norm) {tb:6.2f} us", flush=True)
 
 
 def bench_launch():

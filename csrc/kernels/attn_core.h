@@ -231,6 +231,18 @@ __device__ __forceinline__ void st16_sc1(__amdgpu_buffer_rsrc_t rsrc, int byte_o
 __device__ __forceinline__ u32x4 ld16_sc1(__amdgpu_buffer_rsrc_t rsrc, int byte_off) {
   return __builtin_amdgcn_raw_buffer_load_b128(rsrc, byte_off, 0, 16);
 }
+// default-policy 16-B store: the line stays in this XCD's L2 (a same-XCD reader's sc1 load hits it
+// there; a reader on another XCD may see a stale line: only ever an additional copy, see
+// publish_partial's `rsrc_l2`)
+__device__ __forceinline__ void st16_l2(__amdgpu_buffer_rsrc_t rsrc, int byte_off, u32x4 v) {
+  __builtin_amdgcn_raw_buffer_store_b128(v, rsrc, byte_off, 0, 0);
+}
+// this wave's XCD (0-7): for choosing a faster same-XCD path only, never for correctness
+__device__ __forceinline__ uint32_t xcc_id() {
+  uint32_t x;
+  asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID, 0, 4)" : "=s"(x));
+  return x;
+}
 // lambda granule: an 8-B relaxed agent-scope atomic load (global_load_dwordx2 sc1). Being an
 // ordered load it also keeps the compiler from hoisting the O-unit buffer loads out of a re-poll
 // (a loop with no ordered access looks loop-invariant to it).
@@ -240,9 +252,12 @@ __device__ __forceinline__ u32x2 ld8_atomic(const char* base, int byte_off) {
   return u32x2{static_cast<uint32_t>(v), static_cast<uint32_t>(v >> 32)};
 }
 
-template <int G, int D, int NW>
-__device__ __forceinline__ void publish_partial(const float* red, __amdgpu_buffer_rsrc_t rsrc, int c, uint32_t tag,
-                                                int tid) {
+// DUAL: the same granules also into a second slab (`rsrc_l2`) with default-policy stores, whose
+// lines stay in this XCD's L2 — a merger that knows every producer ran on its own XCD reads that
+// copy from L2 instead of the write-through copy from memory (attn_oproj.hip)
+template <int G, int D, int NW, bool DUAL>
+__device__ __forceinline__ void publish_partial_x(const float* red, __amdgpu_buffer_rsrc_t rsrc, int c, uint32_t tag,
+                                                  int tid, __amdgpu_buffer_rsrc_t rsrc_l2) {
   constexpr int HQ = D / 4, RU = HQ + 1;
   for (int p = tid; p < G * HQ; p += NW * 64) {
     const int g = p / HQ, u = p % HQ;
@@ -251,12 +266,26 @@ __device__ __forceinline__ void publish_partial(const float* red, __amdgpu_buffe
     for (int e = 0; e < 4; ++e) merge_waves<G, D, NW>(red, g, 4 * u + e, o[e], m, l);
     const float inv = 1.f / l;
     const int row = (c * G + g) * RU;
-    st16_sc1(rsrc, (row + u) * 16, u32x4{pack_bf16x2(o[0] * inv, o[1] * inv), tag, pack_bf16x2(o[2] * inv, o[3] * inv), tag});
+    const u32x4 ov{pack_bf16x2(o[0] * inv, o[1] * inv), tag, pack_bf16x2(o[2] * inv, o[3] * inv), tag};
+    if constexpr (DUAL) st16_l2(rsrc_l2, (row + u) * 16, ov);
+    st16_sc1(rsrc, (row + u) * 16, ov);
     if (u == 0) {
       const uint32_t lam = __float_as_uint(m + __log2f(l));
+      if constexpr (DUAL) st16_l2(rsrc_l2, (row + HQ) * 16, u32x4{lam, tag, lam, tag});
       st16_sc1(rsrc, (row + HQ) * 16, u32x4{lam, tag, lam, tag});
     }
   }
+}
+
+template <int G, int D, int NW>
+__device__ __forceinline__ void publish_partial(const float* red, __amdgpu_buffer_rsrc_t rsrc, int c, uint32_t tag,
+                                                int tid) {
+  publish_partial_x<G, D, NW, false>(red, rsrc, c, tag, tid, rsrc);
+}
+template <int G, int D, int NW>
+__device__ __forceinline__ void publish_partial_dual(const float* red, __amdgpu_buffer_rsrc_t rsrc,
+                                                     __amdgpu_buffer_rsrc_t rsrc_l2, int c, uint32_t tag, int tid) {
+  publish_partial_x<G, D, NW, true>(red, rsrc, c, tag, tid, rsrc_l2);
 }
 
 // Merge the partial rows [r0, r0 + n) of a granule slab: thread = (output quad, row group), up to
@@ -264,9 +293,13 @@ __device__ __forceinline__ void publish_partial(const float* red, __amdgpu_buffe
 // straggler is a store already issued by a block that has arrived: no wait on any block that is
 // not running), folded with an online log-sum-exp; row groups meet in LDS. On return threads
 // tid < G * D / 4 hold their quad's (M, S) in ms[0..1] and the unnormalised sums in acc.
+// first_polls > 0: the first polls read the copy at (rsrc_first, base_first) instead (a same-XCD
+// L2 copy, publish_partial's DUAL), then the write-through copy
 template <int G, int D, int NT, int BATCH = 8>
 __device__ __forceinline__ void merge_rows(__amdgpu_buffer_rsrc_t rsrc, const char* base, int r0, int n, uint32_t tag,
-                                           f32x4* scratch, int tid, f32x4& ms, f32x4& acc, int* fault) {
+                                           f32x4* scratch, int tid, f32x4& ms, f32x4& acc, int* fault,
+                                           __amdgpu_buffer_rsrc_t rsrc_first, const char* base_first,
+                                           unsigned first_polls) {
   constexpr int HQ = D / 4, RU = HQ + 1, Q = G * HQ;
   static_assert(Q <= NT, "one pass");
   const int ngr = max(1, min(NT / Q, n));
@@ -279,12 +312,15 @@ __device__ __forceinline__ void merge_rows(__amdgpu_buffer_rsrc_t rsrc, const ch
       u32x2 lv[BATCH];
       for (unsigned spins = 0;; ++spins) {
         bool ok = true;
+        const bool first = spins < first_polls;  // wave-uniform
+        const __amdgpu_buffer_rsrc_t rs = first ? rsrc_first : rsrc;
+        const char* bs = first ? base_first : base;
 #pragma unroll
         for (int j = 0; j < BATCH; ++j) {
           const int cc = r0 + min(c0 + j * ngr, n - 1);  // clamped: every load in flight, masked below
           const int row = (cc * G + g) * RU;
-          ov[j] = ld16_sc1(rsrc, (row + u) * 16);
-          lv[j] = ld8_atomic(base, (row + HQ) * 16);
+          ov[j] = ld16_sc1(rs, (row + u) * 16);
+          lv[j] = ld8_atomic(bs, (row + HQ) * 16);
         }
 #pragma unroll
         for (int j = 0; j < BATCH; ++j)
@@ -331,6 +367,12 @@ __device__ __forceinline__ void merge_rows(__amdgpu_buffer_rsrc_t rsrc, const ch
     }
   }
   __syncthreads();  // scratch is reused by the caller's next merge
+}
+
+template <int G, int D, int NT, int BATCH = 8>
+__device__ __forceinline__ void merge_rows(__amdgpu_buffer_rsrc_t rsrc, const char* base, int r0, int n, uint32_t tag,
+                                           f32x4* scratch, int tid, f32x4& ms, f32x4& acc, int* fault) {
+  merge_rows<G, D, NT, BATCH>(rsrc, base, r0, n, tag, scratch, tid, ms, acc, fault, rsrc, base, 0u);
 }
 
 // Publish this chunk's partial and take a ticket in its GROUP (returns true in the block that wrote

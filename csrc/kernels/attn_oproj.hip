@@ -53,6 +53,7 @@ namespace llmc {
 constexpr int kAoThreads = 512, kAoWaves = kAoThreads / kWave;
 constexpr int kAoLine = 16;  // int32 words per counter line (64 B)
 constexpr int kAoMaxKv = 8;  // kv heads (= head groups summed per o_proj row) at most
+constexpr unsigned kAoL2Polls = 16;  // polls of the same-XCD L2 copy of the partials before the write-through one
 
 // Reduce-scatter of N per-lane row sums over the 64 lanes, one stage per lane bit M = 32, 16, ...:
 // lanes with bit M keep the upper half of the live rows, the others the lower half, and add the
@@ -208,7 +209,8 @@ __global__ __launch_bounds__(kAoThreads) void attn_oproj_kernel(
     const bf16_t* __restrict__ w_o, int K_o, bf16_t* __restrict__ h, bf16_t* __restrict__ attn_out,
     float* __restrict__ part, uint32_t* __restrict__ handoff, uint64_t* __restrict__ tile_part, int* __restrict__ ctr,
     int* __restrict__ fault, int nkv, int bs, int nblocks, int chunk, float scale_log2,
-    uint64_t* __restrict__ stamps, int defer, int add_resid, CarArgs ar, int gate, int prio, AoRouter rt) {
+    uint64_t* __restrict__ stamps, int defer, int add_resid, CarArgs ar, int gate, int prio, AoRouter rt,
+    int l2copy) {
   static_assert(G * D == 512, "one 16-B column chunk per lane per row");
   static_assert(RW >= 1 && RW <= 32 && (RW & (RW - 1)) == 0, "rows per wave: power of two <= 32");
   static_assert(SUBS == 1 || (SUBS == 2 && LATE), "two sub-tiles per wave only with late weights (registers)");
@@ -216,11 +218,14 @@ __global__ __launch_bounds__(kAoThreads) void attn_oproj_kernel(
   using ST = SubTile<G, D>;
   constexpr int HQ = D / 4, RU = HQ + 1, Q = G * HQ;  // 16-B units: per head, per partial row, per group
   constexpr int R = 4 * RW;                              // o_proj rows per block (4 o waves)
-  const int c = blockIdx.x, g = blockIdx.y, nc = gridDim.x;
+  // block b = (c, g) with g = b % nkv: under the observed round-robin dispatch the nc blocks of a kv
+  // head share one XCD (b % 8), so the head's merger can read their partials from that XCD's L2
+  // (see step 2; placement only ever changes the speed)
+  const int c = blockIdx.x / nkv, g = blockIdx.x % nkv, nc = gridDim.x / nkv;
   const int tid = threadIdx.x, wave = tid / kWave, lane = tid % kWave;
   uint64_t* stp = stamps != nullptr ? stamps + (static_cast<int64_t>(g) * nc + c) * 8 : nullptr;
   ao_stamp(stp, 0, tid == 0);
-  int* hctr = ctr + g * kAoLine;            // {head ticket, head epoch}
+  int* hctr = ctr + g * kAoLine;            // {-, head epoch, head ticket (u64: count + per-XCD counts)}
   int* tctr = ctr + (nkv + c) * kAoLine;    // {tile ticket}
   int* xctr = ctr + (nkv + nc) * kAoLine;   // {exit count, tile epoch}
   int* gctr = ctr + (nkv + nc + 1) * kAoLine;  // {attention arrivals, weight-gate epoch} (mode bit 3)
@@ -331,13 +336,29 @@ __global__ __launch_bounds__(kAoThreads) void attn_oproj_kernel(
   // ---- ... -> block state -> partial -> head ticket ----
   st.to_lds(red, wave, lane);
   __syncthreads();
+  // Two copies of the partial: write-through granules in `slab` (read by a merger anywhere) and
+  // default-policy ones in `slab_l2` (they stay in this XCD's L2). The head ticket also counts the
+  // arrivals per XCD (6 bits each above an 8-bit total), so the merger knows whether every producer
+  // of its head ran on its own XCD; then it reads the L2 copy (L2 hits, not fabric round trips queued
+  // behind the other blocks' weight stream), else the write-through one. Tags decide either way.
   const int slab_rows = nc;
   float* slab = part + static_cast<int64_t>(g) * slab_rows * G * RU * 4;
+  float* slab_l2 = part + static_cast<int64_t>(nkv + g) * slab_rows * G * RU * 4;
   const __amdgpu_buffer_rsrc_t rsrc = __builtin_amdgcn_make_buffer_rsrc(slab, 0, slab_rows * G * RU * 16, 0x00020000);
-  if (block_keys) publish_partial<G, D, kAoWaves>(red, rsrc, c, tag_h, o_wave ? Q : ct);
+  const __amdgpu_buffer_rsrc_t rsrc_l2 =
+      __builtin_amdgcn_make_buffer_rsrc(slab_l2, 0, slab_rows * G * RU * 16, 0x00020000);
+  if (block_keys) {
+    if (l2copy) publish_partial_dual<G, D, kAoWaves>(red, rsrc, rsrc_l2, c, tag_h, o_wave ? Q : ct);
+    else publish_partial<G, D, kAoWaves>(red, rsrc, c, tag_h, o_wave ? Q : ct);
+  }
   __syncthreads();  // every wave's stores are issued (the merger checks tags)
   if (ct == kTicketThread) {
-    *flag = __hip_atomic_fetch_add(hctr, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == nc - 1;
+    const uint32_t xcc = xcc_id();
+    const uint64_t old = __hip_atomic_fetch_add(reinterpret_cast<uint64_t*>(hctr + 2),
+                                                1ull + (1ull << (8 + 6 * xcc)), __ATOMIC_RELAXED,
+                                                __HIP_MEMORY_SCOPE_AGENT);
+    *flag = static_cast<int>(old & 255) == nc - 1;
+    flag[1] = l2copy && nc <= 63 && static_cast<int>((old >> (8 + 6 * xcc)) & 63) == nc - 1;  // all on my XCD
     // weight gate (mode bit 3): the last block of the whole grid to finish its attention opens it
     if (gate && __hip_atomic_fetch_add(gctr, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == nc * nkv - 1) {
       __hip_atomic_store(gctr, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -381,15 +402,19 @@ __global__ __launch_bounds__(kAoThreads) void attn_oproj_kernel(
     // 16 rows per thread would spill the o waves' weight registers of the other blocks). Merge
     // thread mt < Q ends with output unit mt (dims 4 mt .. 4 mt + 3).
     int mt;
+    const unsigned l2_polls = flag[1] ? kAoL2Polls : 0u;  // block-uniform
     if (merger_defers) {
       mt = tid;
       merge_rows<G, D, kAoThreads>(rsrc, reinterpret_cast<const char*>(slab), 0, nsplit, tag_h,
-                                   reinterpret_cast<f32x4*>(smem), tid, ms, acc, fault);
+                                   reinterpret_cast<f32x4*>(smem), tid, ms, acc, fault, rsrc_l2,
+                                   reinterpret_cast<const char*>(slab_l2), l2_polls);
     } else {
       mt = o_wave ? 256 + tid : ct;
       merge_rows<G, D, 256>(rsrc, reinterpret_cast<const char*>(slab), 0, nsplit, tag_h,
-                            reinterpret_cast<f32x4*>(smem), mt, ms, acc, fault);
+                            reinterpret_cast<f32x4*>(smem), mt, ms, acc, fault, rsrc_l2,
+                            reinterpret_cast<const char*>(slab_l2), l2_polls);
     }
+    if constexpr (FR != 0) ao_stamp(stp, 6, tid == 0);  // whole rows: 6 / 7 = the head merger's merge / publish
     if (mt < Q) {
       const float inv = 1.f / ms[1];
       const uint32_t lo = pack_bf16x2(acc[0] * inv, acc[1] * inv), hi = pack_bf16x2(acc[2] * inv, acc[3] * inv);
@@ -403,9 +428,10 @@ __global__ __launch_bounds__(kAoThreads) void attn_oproj_kernel(
       }
     }
     if (ct == 0) {
-      __hip_atomic_store(hctr, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);                            // re-arm
+      __hip_atomic_store(reinterpret_cast<uint64_t*>(hctr + 2), 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // re-arm
       __hip_atomic_store(hctr + 1, static_cast<int>(tag_h), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // epoch
     }
+    if constexpr (FR != 0) ao_stamp(stp, 7, tid == 0);
   }
 
   // FR: the merger's merge is done (its head output is in LDS): its weights go now, while its
@@ -485,7 +511,7 @@ __global__ __launch_bounds__(kAoThreads) void attn_oproj_kernel(
     if (rt.Wr == nullptr) return;  // block-uniform
     __syncthreads();               // the block's 16 rows are in LDS
     if (wave == kAoRouterWave)
-      ao_router_tail(rt, reinterpret_cast<const float*>(flag + 4), rt_w, rt_g, rt_tag, g * nc + c, nc * gridDim.y, nc * R,
+      ao_router_tail(rt, reinterpret_cast<const float*>(flag + 4), rt_w, rt_g, rt_tag, g * nc + c, nc * nkv, nc * R,
                      lane, fault);
     return;
   }
@@ -637,13 +663,16 @@ extern "C" int llmc_attn_oproj_check(int H, int nh, int nkv, int D, int nc, int 
 // merge; bit 2 (with late weights, 8 kv heads, G = 4, D = 128, 32-row tiles): whole o_proj rows per
 // block (FR, see the kernel); bit 3 (with late weights): the weight gate — no block requests its
 // weights before every block of the grid has streamed its K/V (lone engines); bit 4: the control
-// waves run at a higher issue priority than the o waves (s_setprio).
+// waves run at a higher issue priority than the o waves (s_setprio); bit 5: no same-XCD L2 copy of
+// the attention partials (the head merger always reads the write-through copy).
 // fault codes: 1 a partial never arrived (merge), 2 the head output never arrived, 3 a tile partial,
 // 4 a router granule (rt_*).
 // stamps (nullable, diagnostics): uint64 [nkv][nc][8] s_memrealtime per block: 0 start, 1 o wave 0's
 // attention done, 2 control wave 4's attention done, 3 head ticket taken, 4 head output in LDS,
-// 5 o wave 0's tile partial published, 6 tile ticket taken, 7 tile reduced (reducer only).
-// Workspace (zeroed once): part f32 [nkv][nc][G][D/4 + 1][4]; handoff u32 [nkv][G D / 4][4];
+// 5 o wave 0's tile partial published, 6 tile ticket taken, 7 tile reduced (reducer only); whole
+// rows (mode bit 2): 6 the head merger's merge done, 7 its output stores issued (mergers only).
+// Workspace (zeroed once): part f32 [2 nkv][nc][G][D/4 + 1][4] (write-through copy, then the L2 copy);
+// handoff u32 [nkv][G D / 4][4];
 // tile_part u64 [nc][nkv][H / nc]; ctr int32 [(nkv + nc + 2) * 16].
 // Tensor-parallel ranks (h = this rank's row-parallel partial of the sum over ranks): add_resid = 0
 // writes h = W_o . attention instead of adding (a rank != 0 whose all-reduce follows as its own
@@ -709,7 +738,7 @@ extern "C" int llmc_attn_oproj(const void* q, const void* k_cache, const void* v
                   world <= 1;  // full rows (no tile reducer to run the all-reduce)
   const size_t lds = kAoWaves * 32 * kVRowBytes + static_cast<size_t>(kAoWaves) * G * (D + 2) * sizeof(float) +
                      (fr ? kAoMaxKv : 1) * 64 * 16 + 16 + 16 * sizeof(float);  // + flag, router rows
-  dim3 grid(nc, nkv);
+  dim3 grid(nc * nkv);  // block b = (c = b / nkv, g = b % nkv)
   const float sl2 = scale * 1.4426950408889634f;
 #define LLMC_AO_K(KERN)                                                                                          \
   do {                                                                                                            \
@@ -718,7 +747,7 @@ extern "C" int llmc_attn_oproj(const void* q, const void* k_cache, const void* v
       (const bf16_t*)q, (const bf16_t*)k_cache, (const bf16_t*)v_cache, (const int32_t*)block_table, bt_len,       \
       (const int32_t*)seq_len, (const bf16_t*)w_o, K_o, (bf16_t*)h, (bf16_t*)attn_out, (float*)part,               \
       (uint32_t*)handoff, (uint64_t*)tile_part, (int*)ctr, (int*)fault, nkv, bs, nblocks, chunk, sl2, (uint64_t*)stamps, \
-      (mode >> 1) & 1, add_resid, ar, late ? (mode >> 3) & 1 : 0, (mode >> 4) & 1, rt); \
+      (mode >> 1) & 1, add_resid, ar, late ? (mode >> 3) & 1 : 0, (mode >> 4) & 1, rt, ((mode >> 5) & 1) ^ 1); \
   } while (0)
 #define LLMC_AO(GG, DD, RR)                                                                                      \
   do {                                                                                                            \

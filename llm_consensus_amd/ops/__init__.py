@@ -383,11 +383,12 @@ def attn_oproj_workspace(H: int, nh: int, nkv: int, D: int, nc: int, device):
     kernel re-arms its tickets and advances its epochs): attention partial granules f32 [nkv, nc,
     G, D/4 + 1, 4]; the merged per-head output as {bf16x2, tag} granules int32 [nkv, G D / 4, 4];
     the o_proj tile partials as {f32, tag} int64 [nc, nkv, H / nc]; counters int32 [(nkv + nc + 2)
-    * 16] (head {ticket, epoch}, tile tickets, {exit, tile epoch}, {arrivals, weight-gate epoch}, one
-    64-B line each)."""
+    * 16] (head {-, epoch, ticket as u64: count + per-XCD counts}, tile tickets, {exit, tile epoch},
+    {arrivals, weight-gate epoch}, one 64-B line each). The attention partials come twice ([2 nkv,
+    ...]): write-through, and a copy left in the producing XCD's L2 for a same-XCD merger."""
     G = nh // nkv
     dev = torch.device(device)
-    part = torch.zeros(nkv, nc, G, D // 4 + 1, 4, dtype=torch.float32, device=dev)
+    part = torch.zeros(2 * nkv, nc, G, D // 4 + 1, 4, dtype=torch.float32, device=dev)
     handoff = torch.zeros(nkv, G * D // 4, 4, dtype=torch.int32, device=dev)
     tile_part = torch.zeros(nc, nkv, H // nc, dtype=torch.int64, device=dev)
     counters = torch.zeros((nkv + nc + 2) * 16, dtype=torch.int32, device=dev)

@@ -14,6 +14,7 @@ from llm_consensus_amd import ops  # noqa: E402
 
 BF = torch.bfloat16
 NAMES = ["start", "o-attn", "c-attn", "ticket", "head-out", "o-done", "tile-tkt", "reduced"]
+NAMES_FR = ["start", "o-attn", "c-attn", "ticket", "heads-in", "o-done", "merged", "published"]  # mode bit 2
 
 
 def run(L, nh=32, nkv=8, D=128, H=4096, bs=64, mode=0):
@@ -50,7 +51,7 @@ def run(L, nh=32, nkv=8, D=128, H=4096, bs=64, mode=0):
         t0 = st[:, 0].min()
         print(f"L={L} chunk={chunk} nc={nc} mode={mode} {'cold' if cold else 'warm'} weights: us from the first block's start "
               f"(min / median / max over blocks), fault {int(fault.item())}")
-        for k, n in enumerate(NAMES):
+        for k, n in enumerate(NAMES_FR if (mode & 4) and H // nc == 128 and nkv == 8 else NAMES):
             v = st[:, k]
             v = v[v > 0]
             if v.numel() == 0:

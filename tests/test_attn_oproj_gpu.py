@@ -126,6 +126,7 @@ def test_attn_oproj_vs_oracle_and_two_launches(cuda, nh, nkv, D, H, L, cap):
     # all 7 launches, the tile epoch by those with tile partials (not the default's whole rows)
     whole_rows = bool(ops.ATTN_OPROJ_MODE & 4) and nkv == 8 and nh // nkv == 4 and D == 128 and H // nc == 128
     assert int(c[: nkv + nc, 0].abs().sum()) == 0 and int(c[nkv + nc, 0]) == 0, c[:, :2]
+    assert int(c[:nkv, 2:4].abs().sum()) == 0, c[:nkv, :4]  # the u64 head tickets re-armed
     assert torch.equal(c[:nkv, 1], torch.full((nkv,), 7, dtype=torch.int32))
     assert int(c[nkv + nc, 1]) == (4 if whole_rows else 7)
 
@@ -391,3 +392,32 @@ def test_engine_fused_moe_router_matches_router_launch(cuda):
     b = ee.generate_ids(prompt, 16, temperature=0.8, seed=7, stop_on_eos=False)
     assert a == b
     assert int(ea.attn_fault.item()) == 0
+
+
+@pytest.mark.parametrize("nh,nkv,D,H", [(32, 8, 128, 4096), (8, 2, 128, 1024)])
+@pytest.mark.parametrize("L,cap", [(100, 2048), (2048, 2048), (9000, 16384)])
+def test_attn_oproj_l2_copy_is_timing_only(cuda, nh, nkv, D, H, L, cap):
+    """The same-XCD L2 copy of the attention partials (default) vs mode bit 5 (the merger always
+    reads the write-through copy): the same bits, launch after launch on one workspace."""
+    bs = 64
+    nc = ops.attn_oproj_grid(H, nh, nkv, D)
+    chunk = ops.attn_oproj_chunk(cap, nc)
+    if chunk == 0:
+        pytest.skip("bucket beyond the fused launch")
+    kc, vc, bt, sl, q, w_o, h0 = _case(L, nh, nkv, D, H, bs)
+    scale = 1 / math.sqrt(D)
+    fault = torch.zeros(1, dtype=torch.int32, device="cuda")
+    fr = nkv == 8 and nh // nkv == 4 and D == 128 and H // nc == 128
+    base = 7 if fr else 3
+    ws = ops.attn_oproj_workspace(H, nh, nkv, D, nc, "cuda")
+    outs = []
+    for mode in (base, base | 32, base, base | 32, base):
+        hm = h0.clone()
+        am = torch.zeros(1, nh * D, dtype=BF, device="cuda")
+        ops.attn_oproj(q, kc, vc, bt.cuda(), sl.cuda(), w_o, hm, am, ws, nh, nkv, D, bs, chunk, nc, scale, fault=fault,
+                       mode=mode)
+        outs.append((hm, am))
+    torch.cuda.synchronize()
+    assert int(fault.item()) == 0
+    for o in outs[1:]:
+        assert torch.equal(o[0], outs[0][0]) and torch.equal(o[1], outs[0][1])

@@ -58,6 +58,12 @@ __device__ __forceinline__ uint32_t car_arrive_and_wait(const CarPeers& P, int r
       if (!car_spin(P, rank, world, polls, t0)) break;
     }
     __atomic_thread_fence(__ATOMIC_ACQUIRE);
+    // the fence's buffer_inv completes asynchronously: wait for it HERE, so the barrier below
+    // releases the block's other waves (whose plain loads read the peers' staging) only once the
+    // invalidate is done (MI355X_MICROARCH.md, Consumer recipe). Without it a wave could read a
+    // line of a peer's buffer still cached from two launches earlier: rare wrong values in the
+    // sequence-parallel prefill (tests/test_tp_gpu.py, llama-small sp_min_tokens=16).
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   }
   __syncthreads();
   return epoch;

@@ -147,7 +147,11 @@ def _tp2_vs_tp1(name, ekw):
     assert not isinstance(logits, str), logits
     assert not tmo
     logits = torch.tensor(logits)
-    assert (logits - ref_logits).abs().max().item() < 0.05 * ref_logits.abs().max().item()
+    d = (logits - ref_logits).abs()
+    bad = (d > 0.05 * ref_logits.abs().max()).nonzero().flatten()
+    assert bad.numel() == 0, (f"{bad.numel()} of {d.numel()} logits off (max {d.max().item():.3f}); first "
+                              f"{bad[:8].tolist()} last {bad[-8:].tolist()}; got {logits[bad[:8]].tolist()} "
+                              f"want {ref_logits[bad[:8]].tolist()}")
     # greedy continuation: equal until the first numerical near-tie, which the TP=1 model must
     # confirm (teacher-forced: its logits at the diverging position put the TP token within noise
     # of its own argmax)

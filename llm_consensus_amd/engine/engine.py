@@ -831,11 +831,20 @@ class Engine:
         return out
 
     def full_logits(self, seq: Sequence) -> torch.Tensor:
-        """Full-vocabulary last-token logits of a prefilled sequence (collective under TP)."""
+        """Full-vocabulary last-token logits of a prefilled sequence (collective under TP), safe to
+        use on the caller's stream: the prefill ran on the engine's stream and returned without a
+        sync, so the gather runs there too and the caller's stream then waits for it (reading
+        ``seq.logits`` from another stream raced the prefill's lm_head: a TP=2 test saw a few
+        logits not yet written)."""
         if self.tp.size == 1:
-            return seq.logits
-        self.logits_local[0].copy_(seq.logits)
-        return self._gather_logits(1)[0]
+            out = seq.logits
+        else:
+            with self._on_stream():
+                self.logits_local[0].copy_(seq.logits)
+                out = self._gather_logits(1)[0]
+        if self.stream is not None:
+            torch.cuda.current_stream(self.device).wait_stream(self.stream)
+        return out
 
     def _sample(self, B: int, logits: torch.Tensor) -> None:
         use_topkp = bool(self._use_topkp)

@@ -7,6 +7,8 @@
 // block are picked so the grid fills whole rounds of the 256 CUs (pick_waves). Paired epilogues
 // (SiLU gate/up, RoPE) meet their partner row of the next wave through LDS (PAIR_LDS); shapes
 // that do not tile keep 256 threads x 2 rows/wave.
+#include <cstdlib>
+
 #include "gemv_core.h"
 
 namespace llmc {
@@ -41,9 +43,13 @@ static int pick_waves(int N, bool paired) {
   // blocks with 8 loads per lane spread them over 3-6x the CUs (768x4096: 4.04 vs 5.68 us,
   // profiles/r1_attn_decode_tp_shapes.md)
   if (N < 2048 && (!paired || N % 8 == 0)) return 4;
+  // 10-wave blocks: a 70B TP=4 rank's qkv (2560 rows) is 256 blocks of 10 rows instead of 160 of 16
+  // (96 CUs idle)
+  static const bool no10 = std::getenv("LLMC_GEMV_NO_W10") != nullptr;  // A/B runs only
   int best = 16;
   double best_idle = 2.0;
-  for (int w : {16, 12, 8}) {
+  for (int w : {16, 12, 10, 8}) {
+    if (w == 10 && no10) continue;
     if (paired && N % (2 * w) != 0) continue;
     const long blocks = (N + w - 1) / w;
     const long slots = (blocks + 255) / 256 * 256;
@@ -68,10 +74,13 @@ static int launch_gemv(const void* x, int x_stride, const void* nw, float eps, c
   if constexpr (M <= 2) {
     if (w == 16 && K >= 8192 && N <= 4096)
       return launch_gemv_g<M, 1024, 1, PRO, EPI, 8>(x, x_stride, nw, eps, W, out, out_stride, N, K, rope, s);
+    if (w == 10 && K >= 8192)
+      return launch_gemv_g<M, 640, 1, PRO, EPI, 8>(x, x_stride, nw, eps, W, out, out_stride, N, K, rope, s);
   }
   switch (w) {
     case 16: return launch_gemv_g<M, 1024, 1, PRO, EPI>(x, x_stride, nw, eps, W, out, out_stride, N, K, rope, s);
     case 12: return launch_gemv_g<M, 768, 1, PRO, EPI>(x, x_stride, nw, eps, W, out, out_stride, N, K, rope, s);
+    case 10: return launch_gemv_g<M, 640, 1, PRO, EPI>(x, x_stride, nw, eps, W, out, out_stride, N, K, rope, s);
     case 8: return launch_gemv_g<M, 512, 1, PRO, EPI>(x, x_stride, nw, eps, W, out, out_stride, N, K, rope, s);
     case 4: return launch_gemv_g<M, 256, 1, PRO, EPI, 8>(x, x_stride, nw, eps, W, out, out_stride, N, K, rope, s);
     default:  // paired rows that do not tile by 16-32 rows: pairs inside one wave
@@ -172,9 +181,11 @@ static int gemv_ar_geom(const void* x, int x_stride, const void* W, void* h, int
   // the dense GEMV's geometry rule (pick_waves): same blocks, same accumulation order, same bits
   const int w = pick_waves(N, false);
   if (w == 16 && K >= 8192 && N <= 4096) return launch_gemv_ar<M, 1024, 8>(x, x_stride, W, h, h_stride, N, K, ar, s);
+  if (w == 10 && K >= 8192) return launch_gemv_ar<M, 640, 8>(x, x_stride, W, h, h_stride, N, K, ar, s);
   switch (w) {
     case 16: return launch_gemv_ar<M, 1024, 4>(x, x_stride, W, h, h_stride, N, K, ar, s);
     case 12: return launch_gemv_ar<M, 768, 4>(x, x_stride, W, h, h_stride, N, K, ar, s);
+    case 10: return launch_gemv_ar<M, 640, 4>(x, x_stride, W, h, h_stride, N, K, ar, s);
     case 8: return launch_gemv_ar<M, 512, 4>(x, x_stride, W, h, h_stride, N, K, ar, s);
     case 4: return launch_gemv_ar<M, 256, 8>(x, x_stride, W, h, h_stride, N, K, ar, s);
     default: return -7;
@@ -223,6 +234,7 @@ static int moe_gemv_geom(int npairs, const void* x, int x_stride, const void* nw
   switch (pick_waves(N, EPI == EPI_SILU)) {
     case 16: return launch_moe_gemv<1024, 1, EPI, PRO>(npairs, x, x_stride, nw, eps, W, ids, x_div, out, out_stride, N, K, s);
     case 12: return launch_moe_gemv<768, 1, EPI, PRO>(npairs, x, x_stride, nw, eps, W, ids, x_div, out, out_stride, N, K, s);
+    case 10: return launch_moe_gemv<640, 1, EPI, PRO>(npairs, x, x_stride, nw, eps, W, ids, x_div, out, out_stride, N, K, s);
     case 8: return launch_moe_gemv<512, 1, EPI, PRO>(npairs, x, x_stride, nw, eps, W, ids, x_div, out, out_stride, N, K, s);
     case 4: return launch_moe_gemv<256, 1, EPI, PRO>(npairs, x, x_stride, nw, eps, W, ids, x_div, out, out_stride, N, K, s);
     default: return launch_moe_gemv<256, 2, EPI, PRO>(npairs, x, x_stride, nw, eps, W, ids, x_div, out, out_stride, N, K, s);

@@ -45,11 +45,14 @@ static int pick_waves(int N, bool paired) {
   if (N < 2048 && (!paired || N % 8 == 0)) return 4;
   // 10-wave blocks: a 70B TP=4 rank's qkv (2560 rows) is 256 blocks of 10 rows instead of 160 of 16
   // (96 CUs idle)
+  // 14-wave blocks (paired outputs): a TP=8 / TP=4 rank's gate_up (3584 / 7168 rows) is 256 / 512
+  // blocks instead of 224 / 448
   static const bool no10 = std::getenv("LLMC_GEMV_NO_W10") != nullptr;  // A/B runs only
+  static const bool no14 = std::getenv("LLMC_GEMV_NO_W14") != nullptr;
   int best = 16;
   double best_idle = 2.0;
-  for (int w : {16, 12, 10, 8}) {
-    if (w == 10 && no10) continue;
+  for (int w : {16, 14, 12, 10, 8}) {
+    if ((w == 10 && no10) || (w == 14 && (no14 || !paired))) continue;
     if (paired && N % (2 * w) != 0) continue;
     const long blocks = (N + w - 1) / w;
     const long slots = (blocks + 255) / 256 * 256;
@@ -79,6 +82,7 @@ static int launch_gemv(const void* x, int x_stride, const void* nw, float eps, c
   }
   switch (w) {
     case 16: return launch_gemv_g<M, 1024, 1, PRO, EPI>(x, x_stride, nw, eps, W, out, out_stride, N, K, rope, s);
+    case 14: return launch_gemv_g<M, 896, 1, PRO, EPI>(x, x_stride, nw, eps, W, out, out_stride, N, K, rope, s);
     case 12: return launch_gemv_g<M, 768, 1, PRO, EPI>(x, x_stride, nw, eps, W, out, out_stride, N, K, rope, s);
     case 10: return launch_gemv_g<M, 640, 1, PRO, EPI>(x, x_stride, nw, eps, W, out, out_stride, N, K, rope, s);
     case 8: return launch_gemv_g<M, 512, 1, PRO, EPI>(x, x_stride, nw, eps, W, out, out_stride, N, K, rope, s);
@@ -233,6 +237,7 @@ static int moe_gemv_geom(int npairs, const void* x, int x_stride, const void* nw
   // the rounds, so whole rounds per pair are whole rounds overall
   switch (pick_waves(N, EPI == EPI_SILU)) {
     case 16: return launch_moe_gemv<1024, 1, EPI, PRO>(npairs, x, x_stride, nw, eps, W, ids, x_div, out, out_stride, N, K, s);
+    case 14: return launch_moe_gemv<896, 1, EPI, PRO>(npairs, x, x_stride, nw, eps, W, ids, x_div, out, out_stride, N, K, s);
     case 12: return launch_moe_gemv<768, 1, EPI, PRO>(npairs, x, x_stride, nw, eps, W, ids, x_div, out, out_stride, N, K, s);
     case 10: return launch_moe_gemv<640, 1, EPI, PRO>(npairs, x, x_stride, nw, eps, W, ids, x_div, out, out_stride, N, K, s);
     case 8: return launch_moe_gemv<512, 1, EPI, PRO>(npairs, x, x_stride, nw, eps, W, ids, x_div, out, out_stride, N, K, s);

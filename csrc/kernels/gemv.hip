@@ -75,6 +75,12 @@ static int launch_gemv(const void* x, int x_stride, const void* nw, float eps, c
   // two rows only: with 3-4 rows (the VALU form runs them only when K is off the MFMA form's 128-k
   // tiles) that geometry kept 20-48 B per lane in scratch (tests/test_kernel_plan_cpu.py)
   if constexpr (M <= 2) {
+    // the RoPE epilogue with both rows of a pair in one wave (no LDS pair exchange behind a block
+    // barrier) where that still fills whole rounds: Llama-3-8B / Mixtral qkv (6144 rows) as 256
+    // blocks of 12 waves x 2 rows
+    static const bool rope_rpw1 = std::getenv("LLMC_GEMV_ROPE_RPW1") != nullptr;  // A/B runs only
+    if (EPI == EPI_ROPE && w == 12 && N % (2 * 12 * 256) == 0 && !rope_rpw1)
+      return launch_gemv_g<M, 768, 2, PRO, EPI, 4>(x, x_stride, nw, eps, W, out, out_stride, N, K, rope, s);
     if (w == 16 && K >= 8192 && N <= 4096)
       return launch_gemv_g<M, 1024, 1, PRO, EPI, 8>(x, x_stride, nw, eps, W, out, out_stride, N, K, rope, s);
     if (w == 10 && K >= 8192)
@@ -325,6 +331,11 @@ extern "C" int llmc_gemv_sweep(int variant, const void* x, const void* nw, const
     case 16: return launch_sweep<768, 1, 4>(x, nw, W, out, N, K, s);
     case 17: return launch_sweep<1024, 4, 2>(x, nw, W, out, N, K, s);
     case 18: return launch_sweep<1024, 1, 6>(x, nw, W, out, N, K, s);
+    case 19: return launch_sweep<768, 2, 4>(x, nw, W, out, N, K, s);
+    case 20: return launch_sweep<640, 1, 8>(x, nw, W, out, N, K, s);
+    case 21: return launch_sweep<896, 1, 4>(x, nw, W, out, N, K, s);
+    case 22: return launch_sweep<768, 2, 2>(x, nw, W, out, N, K, s);
+    case 23: return launch_sweep<1024, 2, 2>(x, nw, W, out, N, K, s);
     default: return -2;
   }
 }

@@ -78,6 +78,9 @@ __device__ __forceinline__ void gemv_block(const int bx, const int by, char* sme
                                            const CarArgs& ar) {
   constexpr int WAVES = NT / kWave;
   constexpr bool PAIR_LDS = (EPI == EPI_SILU || EPI == EPI_ROPE) && RPW == 1;  // host: N % (2 * WAVES) == 0
+  // RoPE operands through the scalar cache, early (below): one pair per wave (PAIR_LDS: the even
+  // wave's row and its partner; RPW == 2: the wave's own two rows)
+  constexpr bool ROPE_PRE = EPI == EPI_ROPE && (PAIR_LDS || RPW == 2);
   // EXPERT (MoE decode): by = (token, slot) pair; weights of expert expert_ids[pair],
   // input row pair / x_div, output row pair (M must be 1).
   // EPI_COMBINE (MoE decode down projection fused with the combine; EXPERT, M == RPW == top-k):
@@ -180,7 +183,7 @@ __device__ __forceinline__ void gemv_block(const int bx, const int by, char* sme
   // dependent cos/sin loads after the prologue, when the position has landed.
   int pre_pos[M], pre_slot[M];
   float pre_c[M], pre_s[M];
-  if constexpr (PAIR_LDS && EPI == EPI_ROPE) {
+  if constexpr (ROPE_PRE) {
 #pragma unroll
     for (int m = 0; m < M; ++m) {
       pre_slot[m] = ld_scalar(rope.slots + m);
@@ -295,7 +298,7 @@ __device__ __forceinline__ void gemv_block(const int bx, const int by, char* sme
   }
   __syncthreads();
   if (!PAIR_LDS && EPI != EPI_AR && row0 >= N) return;  // PAIR_LDS / EPI_AR: every wave reaches the barriers
-  if constexpr (PAIR_LDS && EPI == EPI_ROPE) {
+  if constexpr (ROPE_PRE) {
     const int w_u = __builtin_amdgcn_readfirstlane(wave);
     const int r_u = (bx * WAVES + w_u) * RPW;
     const int D = rope.D, half = D / 2;
@@ -511,7 +514,13 @@ __device__ __forceinline__ void gemv_block(const int bx, const int by, char* sme
           if ((r & 1) == 0) {
             float c = 1.f, sn = 0.f;
             int slot = -1;
-            if constexpr (EPI == EPI_ROPE) rope_ops(n, m, c, sn, slot);
+            if constexpr (EPI == EPI_ROPE && RPW == 2) {  // r == 0: the wave's pair, preloaded
+              c = pre_c[m];
+              sn = pre_s[m];
+              slot = pre_slot[m];
+            } else if constexpr (EPI == EPI_ROPE) {
+              rope_ops(n, m, c, sn, slot);
+            }
             pair_epi(n, m, v, acc[r + 1][m], c, sn, slot);
           }
         }

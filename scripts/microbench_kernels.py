@@ -189,7 +189,8 @@ def bench_gemv():
 
 
 SWEEP = ["256x1u8", "256x2u4", "256x4u4", "512x1u8", "512x2u4", "128x1u8", "64x1u8", "1024x1u4", "256x1u4",
-         "256x2u8", "512x4u2", "128x2u4", "1024x1u8", "1024x2u4", "1024x2u2", "1024x1u2", "768x1u4", "1024x4u2", "1024x1u6"]
+         "256x2u8", "512x4u2", "128x2u4", "1024x1u8", "1024x2u4", "1024x2u2", "1024x1u2", "768x1u4", "1024x4u2", "1024x1u6",
+         "768x2u4", "640x1u8", "896x1u4", "768x2u2", "1024x2u2b"]
 
 
 ALL_VARIANTS = os.environ.get("SWEEP_ALL") == "1"
@@ -211,8 +212,12 @@ def bench_gemv_sweep(shapes=None):
         out = torch.zeros(1, N, dtype=BF, device="cuda")
         res = []
         for v, name in enumerate(SWEEP):
-            if not ALL_VARIANTS and name not in ("256x2u4", "512x1u8", "1024x1u4", "1024x1u6", "1024x1u8", "768x1u4",
-                                                 "1024x1u2"):
+            keep = os.environ.get("SWEEP_ONLY")
+            if keep:
+                if name not in keep.split(","):
+                    continue
+            elif not ALL_VARIANTS and name not in ("256x2u4", "512x1u8", "1024x1u4", "1024x1u6", "1024x1u8", "768x1u4",
+                                                   "1024x1u2"):
                 continue
             st = torch.cuda.current_stream().cuda_stream
 

@@ -81,6 +81,15 @@ static int launch_gemv(const void* x, int x_stride, const void* nw, float eps, c
     static const bool rope_rpw1 = std::getenv("LLMC_GEMV_ROPE_RPW1") != nullptr;  // A/B runs only
     if (EPI == EPI_ROPE && w == 12 && N % (2 * 12 * 256) == 0 && !rope_rpw1)
       return launch_gemv_g<M, 768, 2, PRO, EPI, 4>(x, x_stride, nw, eps, W, out, out_stride, N, K, rope, s);
+    // ... and the SiLU gate/up pairs, at the widest block that still fills whole rounds with two rows
+    // per wave (8B gate_up 28672 rows: 14 waves, 1024 blocks; Phi-3 16384: 16 waves, 512)
+    static const bool silu_rpw1 = std::getenv("LLMC_GEMV_SILU_RPW1") != nullptr;  // A/B runs only
+    if (EPI == EPI_SILU && !silu_rpw1 && K < 8192) {
+      if (N % (2 * 16 * 256) == 0)
+        return launch_gemv_g<M, 1024, 2, PRO, EPI, 4>(x, x_stride, nw, eps, W, out, out_stride, N, K, rope, s);
+      if (N % (2 * 14 * 256) == 0)
+        return launch_gemv_g<M, 896, 2, PRO, EPI, 4>(x, x_stride, nw, eps, W, out, out_stride, N, K, rope, s);
+    }
     if (w == 16 && K >= 8192 && N <= 4096)
       return launch_gemv_g<M, 1024, 1, PRO, EPI, 8>(x, x_stride, nw, eps, W, out, out_stride, N, K, rope, s);
     if (w == 10 && K >= 8192)

@@ -249,7 +249,16 @@ template <int EPI, int PRO>
 static int moe_gemv_geom(int npairs, const void* x, int x_stride, const void* nw, float eps, const void* W,
                          const void* ids, int x_div, void* out, int out_stride, int N, int K, hipStream_t s) {
   // same geometry rule as the dense GEMV; the grid's y dimension (token, expert) pairs multiplies
-  // the rounds, so whole rounds per pair are whole rounds overall
+  // the rounds, so whole rounds per pair are whole rounds overall. SiLU pairs in one wave where
+  // that fills whole rounds (Mixtral's expert gate_up, 28672 rows: 14 waves x 2 rows), as the
+  // dense launcher does
+  static const bool silu_rpw1 = std::getenv("LLMC_GEMV_SILU_RPW1") != nullptr;  // A/B runs only
+  if (EPI == EPI_SILU && !silu_rpw1 && K < 8192) {
+    if (N % (2 * 16 * 256) == 0)
+      return launch_moe_gemv<1024, 2, EPI, PRO>(npairs, x, x_stride, nw, eps, W, ids, x_div, out, out_stride, N, K, s);
+    if (N % (2 * 14 * 256) == 0)
+      return launch_moe_gemv<896, 2, EPI, PRO>(npairs, x, x_stride, nw, eps, W, ids, x_div, out, out_stride, N, K, s);
+  }
   switch (pick_waves(N, EPI == EPI_SILU)) {
     case 16: return launch_moe_gemv<1024, 1, EPI, PRO>(npairs, x, x_stride, nw, eps, W, ids, x_div, out, out_stride, N, K, s);
     case 14: return launch_moe_gemv<896, 1, EPI, PRO>(npairs, x, x_stride, nw, eps, W, ids, x_div, out, out_stride, N, K, s);
@@ -265,6 +274,11 @@ static int moe_gemv_geom(int npairs, const void* x, int x_stride, const void* nw
 // MoE decode down projection fused with the combine: h[t] += sum_j w[t, j] * (W_down[ids[t, j]] . act[t*k + j])
 // for top-2 routing (k == 2), one block per 16 output rows per token, each wave streaming its row
 // of both experts. Expert-parallel ranks (ids -1) keep the separate GEMV + combine.
+// MoE decode down projection fused with the combine: h[t] += sum_j w[t, j] * (W_down[ids[t, j]] . act[t*k + j])
+// for top-2 routing (k == 2), one block per 16 output rows per token, each wave streaming its row
+// of both experts. Expert-parallel ranks (ids -1) keep the separate GEMV + combine.
+// (Measured against 512 threads x 4 / 1024 x 2 / 512 x 8 loads per lane: none faster,
+// profiles/r6_decode_experiments.md.)
 extern "C" int llmc_moe_down_combine(int T, const void* act, int act_stride, const void* W, const void* ids,
                                      const void* w, void* h, int h_stride, int N, int K, int k, hipStream_t s) {
   if (k != 2 || K % 8 != 0) return -1;

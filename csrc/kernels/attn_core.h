@@ -112,8 +112,8 @@ struct SubTile {
         s[kt][i] = v;
         mx = fmaxf(mx, v);
       }
-    mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
-    mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+    mx = xor16_max(mx);
+    mx = xor32_max(mx);
     const float m_new = fmaxf(m_run, mx);
     const float alpha = exp2f(m_run - m_new);
     float rs = 0.f;
@@ -125,8 +125,8 @@ struct SubTile {
         s[kt][i] = p;
         rs += p;
       }
-    rs += __shfl_xor(rs, 16, 64);
-    rs += __shfl_xor(rs, 32, 64);
+    rs = xor16_add(rs);
+    rs = xor32_add(rs);
     l_run = l_run * alpha + rs;
     m_run = m_new;
     // P^T fragment: k = 8*g4 + j  <->  key 4*g4 + j (j < 4), 16 + 4*g4 + (j - 4) (j >= 4)

@@ -67,7 +67,7 @@ __device__ __forceinline__ void ao_reduce_scatter(float (&s)[RWt], int lane) {
     for (int i = 0; i < N / 2; ++i) {
       const float send = up ? s[i] : s[i + N / 2];
       const float keep = up ? s[i + N / 2] : s[i];
-      s[i] = keep + __shfl_xor(send, M, 64);
+      s[i] = keep + xor_shfl<M>(send, lane);
     }
     ao_reduce_scatter<N / 2, M / 2, RWt>(s, lane);
   }
@@ -114,11 +114,13 @@ __device__ __forceinline__ void ao_router_tail(const AoRouter& rt, const float* 
 #pragma unroll
     for (int j = 0; j < 4; ++j) p += w[j] * (gm[j] * rv[4 * q4 + j]);
   }
-  p += __shfl_xor(p, 1, 64);
-  p += __shfl_xor(p, 2, 64);
+  p += xor_shfl<1>(p, lane);
+  p += xor_shfl<2>(p, lane);
   float sq = lane < 16 ? rv[lane] * rv[lane] : 0.f;
-#pragma unroll
-  for (int m = 1; m < 16; m <<= 1) sq += __shfl_xor(sq, m, 64);
+  sq += xor_shfl<1>(sq, lane);
+  sq += xor_shfl<2>(sq, lane);
+  sq += xor_shfl<4>(sq, lane);
+  sq += xor_shfl<8>(sq, lane);
   const float pv = __shfl(p, (lane & 7) * 4, 64);  // every lane takes part in both shuffles
   const float sv = __shfl(sq, 0, 64);
   if (lane <= 8) {
@@ -157,9 +159,7 @@ __device__ __forceinline__ void ao_router_tail(const AoRouter& rt, const float* 
 #pragma unroll
       for (int i = 0; i < 9; ++i) acc[i] += __uint_as_float(static_cast<uint32_t>(v[r][i]));
 #pragma unroll
-  for (int m = 32; m >= 1; m >>= 1)
-#pragma unroll
-    for (int i = 0; i < 9; ++i) acc[i] += __shfl_xor(acc[i], m, 64);
+  for (int i = 0; i < 9; ++i) acc[i] = wave_sum(acc[i]);
   if (lane == 0) {
     // softmax over the E logits, top k (lowest index on ties), renormalised: moe_router_kernel's rule
     const float inv = rsqrtf(acc[8] / H + rt.eps);
@@ -498,8 +498,7 @@ __global__ __launch_bounds__(kAoThreads) void attn_oproj_kernel(
       }
       ao_reduce_scatter<RWF, 32>(s, lane);
       constexpr int LPR = 64 / RWF;
-#pragma unroll
-      for (int m = LPR / 2; m >= 1; m >>= 1) s[0] += __shfl_xor(s[0], m, 64);
+      s[0] = xor_tree_sum<LPR / 2>(s[0], lane);
       if ((lane % LPR) == 0) {
         bf16_t* hp = h + (g * nc + c) * (R / FR) + wave * RWF + lane / LPR;
         const bf16_t hv = f32_to_bf16((add_resid ? bf16_to_f32(*hp) : 0.f) + s[0]);
@@ -525,8 +524,7 @@ __global__ __launch_bounds__(kAoThreads) void attn_oproj_kernel(
     for (int j = 0; j < RW; ++j) s[j] = dot8_bf16(wt[j], x, 0.f);
     ao_reduce_scatter<RW, 32>(s, lane);
     constexpr int LPR = 64 / RW;  // lanes sharing one row after the stages (the low log2(LPR) bits)
-#pragma unroll
-    for (int m = LPR / 2; m >= 1; m >>= 1) s[0] += __shfl_xor(s[0], m, 64);
+    s[0] = xor_tree_sum<LPR / 2>(s[0], lane);
     if ((lane % LPR) == 0) {
       const int my_row = wave * RW + lane / LPR;  // row within the tile
       const uint64_t gv = static_cast<uint64_t>(__float_as_uint(s[0])) | (static_cast<uint64_t>(tag_t) << 32);

@@ -19,6 +19,7 @@ typedef uintptr_t ptr;
 extern "C" {
 int llmc_rmsnorm(const void*, const void*, void*, int, int, int, int, float, hipStream_t);
 int llmc_embedding(const void*, const void*, void*, int, int, int, hipStream_t);
+int llmc_lane_exchange_check(const void*, void*, int, hipStream_t);
 int llmc_silu_mul_interleaved(const void*, void*, int, int, hipStream_t);
 int llmc_gemv(int, const void*, int, const void*, float, const void*, void*, int, int, int, int, int, hipStream_t);
 int llmc_gemvm(int, const void*, int, const void*, float, const void*, void*, int, int, int, int, int, hipStream_t);
@@ -111,6 +112,9 @@ PYBIND11_MODULE(_llmc_hip, m) {
   m.doc() = "llm_consensus_amd gfx950 HIP kernels (raw-pointer launchers)";
   m.def("rmsnorm", [](ptr x, ptr w, ptr y, int T, int H, int xs, int ys, float eps, ptr s) {
     check(llmc_rmsnorm(P(x), P(w), P(y), T, H, xs, ys, eps, S(s)), "rmsnorm");
+  });
+  m.def("lane_exchange_check", [](ptr in, ptr out, int nb, ptr s) {
+    check(llmc_lane_exchange_check(P(in), P(out), nb, S(s)), "lane_exchange_check");
   });
   m.def("embedding", [](ptr ids, ptr table, ptr out, int T, int H, int V, ptr s) {
     check(llmc_embedding(P(ids), P(table), P(out), T, H, V, S(s)), "embedding");

@@ -76,23 +76,120 @@ __device__ __forceinline__ T ld_scalar(const T* p) {
   return *reinterpret_cast<const __attribute__((address_space(4))) T*>(reinterpret_cast<uintptr_t>(p));
 }
 
-// Full-wave reductions (xor butterfly over 64 lanes).
+// Cross-lane exchanges without an LDS round trip. __shfl_xor lowers to ds_bpermute (an LDS access and
+// an lgkmcnt wait on every step of a reduction's dependency chain); these run in the VALU:
+//  * lanes (l, l ^ 32) / (l, l ^ 16): v_permlane32_swap / v_permlane16_swap of v with itself leaves
+//    the pair's two values in the two results, in lane-dependent order -> for a commutative op,
+//    op(r0, r1) == op(v, v[l ^ o]) bit for bit;
+//  * lanes (l, l ^ 8) inside a 16-lane row: DPP row_ror:8; (l, l ^ 2) / (l, l ^ 1): DPP quad_perm.
+// IEEE add and max are commutative, so each step below computes exactly the value of the shuffle
+// form it replaces (same association order: the results are bit-identical).
+__device__ __forceinline__ uint32_t fbits(float v) { return __builtin_bit_cast(uint32_t, v); }
+__device__ __forceinline__ float bitsf(uint32_t v) { return __builtin_bit_cast(float, v); }
+__device__ __forceinline__ float fmax_raw(float a, float b) {  // no canonicalising v_max x, x on a and b
+  float r;
+  asm("v_max_f32 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
+  return r;
+}
+// The swap as inline asm with explicit wait states on both sides: the hipcc-scheduled builtin gave
+// intermittently wrong sums in the two-token-group MFMA GEMV (tests/test_kernels_gpu.py
+// test_linear_batched_decode_rows, M = 20 / 32), not in the isolated check
+__device__ __forceinline__ void permlane_swap16(uint32_t& a, uint32_t& b) {
+  asm volatile("s_nop 4\n\tv_permlane16_swap_b32 %0, %1\n\ts_nop 4" : "+v"(a), "+v"(b));
+}
+__device__ __forceinline__ void permlane_swap32(uint32_t& a, uint32_t& b) {
+  asm volatile("s_nop 4\n\tv_permlane32_swap_b32 %0, %1\n\ts_nop 4" : "+v"(a), "+v"(b));
+}
+__device__ __forceinline__ float xor32_add(float v) {
+  uint32_t a = fbits(v), b = fbits(v);
+  permlane_swap32(a, b);
+  return bitsf(a) + bitsf(b);
+}
+__device__ __forceinline__ float xor16_add(float v) {
+  uint32_t a = fbits(v), b = fbits(v);
+  permlane_swap16(a, b);
+  return bitsf(a) + bitsf(b);
+}
+__device__ __forceinline__ float xor32_max(float v) {
+  uint32_t a = fbits(v), b = fbits(v);
+  permlane_swap32(a, b);
+  return fmax_raw(bitsf(a), bitsf(b));
+}
+__device__ __forceinline__ float xor16_max(float v) {
+  uint32_t a = fbits(v), b = fbits(v);
+  permlane_swap16(a, b);
+  return fmax_raw(bitsf(a), bitsf(b));
+}
+template <int CTRL>
+__device__ __forceinline__ float dpp_f(float v) {
+  return bitsf(static_cast<uint32_t>(__builtin_amdgcn_update_dpp(0, static_cast<int>(fbits(v)), CTRL, 0xF, 0xF, true)));
+}
+constexpr int kDppXor1 = 0xB1, kDppXor2 = 0x4E;  // quad_perm [1,0,3,2] / [2,3,0,1]
+constexpr int kDppRor8 = 0x128, kDppRor4 = 0x124;  // row_ror:8 = lane ^ 8 within a 16-lane row
+
+// v of lane ^ M for any lane pattern (the exact __shfl_xor(v, M, 64)), in the VALU. DPP row_ror:n
+// reads lane (l - n) mod 16 of the row (norm.hip lane_exchange_check_kernel: every helper against
+// __shfl_xor, bit for bit, tests/test_kernels_gpu.py).
+template <int M>
+__device__ __forceinline__ float xor_shfl(float v, int lane) {
+  static_assert(M == 1 || M == 2 || M == 4 || M == 8 || M == 16 || M == 32, "lane xor of one bit");
+  if constexpr (M == 32) {
+    uint32_t a = fbits(v), b = fbits(v);
+    permlane_swap32(a, b);
+    return bitsf(lane & 32 ? a : b);
+  } else if constexpr (M == 16) {
+    uint32_t a = fbits(v), b = fbits(v);
+    permlane_swap16(a, b);
+    return bitsf(lane & 16 ? a : b);
+  } else if constexpr (M == 8) {
+    return dpp_f<kDppRor8>(v);
+  } else if constexpr (M == 4) {
+    // both rotations under the full EXEC mask (a select over two DPP reads was lowered to two
+    // EXEC-masked DPP moves, which read 0 from the masked-off source lanes): banks 0 / 2 (lanes
+    // 0-3, 8-11 of each row) take ror:12 (lane + 4), banks 1 / 3 ror:4 (lane - 4), by the DPP bank mask
+    const int lo = __builtin_amdgcn_update_dpp(0, static_cast<int>(fbits(v)), 0x12C, 0xF, 0x5, false);
+    return bitsf(static_cast<uint32_t>(__builtin_amdgcn_update_dpp(lo, static_cast<int>(fbits(v)), kDppRor4, 0xF, 0xA, false)));
+  } else {
+    return dpp_f<M == 2 ? kDppXor2 : kDppXor1>(v);
+  }
+}
+// sum over the lanes l ^ {M, M/2, ..., 1}: the butterfly M, M/2, ..., 1 (every lane of the group
+// ends with the group's sum)
+template <int M>
+__device__ __forceinline__ float xor_tree_sum(float v, int lane) {
+  if constexpr (M >= 1) {
+    v += xor_shfl<M>(v, lane);
+    return xor_tree_sum<M / 2>(v, lane);
+  } else {
+    return v;
+  }
+}
+
+// Full-wave reductions: the xor butterfly 32, 16, 8, 4, 2, 1. After the 32 / 16 / 8 steps every
+// lane's value depends on lane % 8 only, so row_ror:4 (lane -> lane +- 4 in its row) reads the
+// same value as lane ^ 4 would.
 __device__ __forceinline__ float wave_sum(float v) {
-#pragma unroll
-  for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o, 64);
+  v = xor32_add(v);
+  v = xor16_add(v);
+  v += dpp_f<kDppRor8>(v);
+  v += dpp_f<kDppRor4>(v);
+  v += dpp_f<kDppXor2>(v);
+  v += dpp_f<kDppXor1>(v);
   return v;
 }
 __device__ __forceinline__ float wave_max(float v) {
-#pragma unroll
-  for (int o = 32; o >= 1; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
+  v = xor32_max(v);
+  v = xor16_max(v);
+  v = fmax_raw(v, dpp_f<kDppRor8>(v));
+  v = fmax_raw(v, dpp_f<kDppRor4>(v));
+  v = fmax_raw(v, dpp_f<kDppXor2>(v));
+  v = fmax_raw(v, dpp_f<kDppXor1>(v));
   return v;
 }
 // Reduction inside aligned groups of W lanes (W power of two <= 64).
 template <int W>
 __device__ __forceinline__ float group_sum(float v) {
-#pragma unroll
-  for (int o = W / 2; o >= 1; o >>= 1) v += __shfl_xor(v, o, 64);
-  return v;
+  return xor_tree_sum<W / 2>(v, static_cast<int>(threadIdx.x) & 63);
 }
 
 // Block-wide sum for NT threads (NT multiple of 64, <= 1024). `red` needs NT/64 floats.

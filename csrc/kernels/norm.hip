@@ -74,11 +74,52 @@ __global__ __launch_bounds__(256) void silu_mul_interleaved_kernel(const bf16_t*
   reinterpret_cast<u32x2*>(y + static_cast<int64_t>(t) * I)[c] = r;
 }
 
+// Self-test of the cross-lane helpers (common.h): every lane writes each helper's result next to
+// the __shfl_xor form it replaces; the GPU test compares the pairs bit for bit.
+__global__ void lane_exchange_check_kernel(const float* __restrict__ in, float* __restrict__ out) {
+  const int lane = threadIdx.x & 63;
+  const float v = in[blockIdx.x * 64 + lane];
+  float* o = out + (static_cast<int64_t>(blockIdx.x) * 64 + lane) * 20;
+  float w = v;
+  o[0] = xor16_add(v);
+  o[1] = v + __shfl_xor(v, 16, 64);
+  o[2] = xor32_add(v);
+  o[3] = v + __shfl_xor(v, 32, 64);
+  o[4] = xor16_max(v);
+  o[5] = fmaxf(v, __shfl_xor(v, 16, 64));
+  o[6] = xor32_max(v);
+  o[7] = fmaxf(v, __shfl_xor(v, 32, 64));
+  o[8] = wave_sum(v);
+  for (int m = 32; m >= 1; m >>= 1) w += __shfl_xor(w, m, 64);
+  o[9] = w;
+  o[10] = wave_max(v);
+  w = v;
+  for (int m = 32; m >= 1; m >>= 1) w = fmaxf(w, __shfl_xor(w, m, 64));
+  o[11] = w;
+  o[12] = xor_shfl<4>(v, lane);
+  o[13] = __shfl_xor(v, 4, 64);
+  o[14] = xor_shfl<8>(v, lane) + xor_shfl<2>(v, lane) + xor_shfl<1>(v, lane);
+  o[15] = __shfl_xor(v, 8, 64) + __shfl_xor(v, 2, 64) + __shfl_xor(v, 1, 64);
+  o[16] = xor_shfl<16>(v, lane) + xor_shfl<32>(v, lane);
+  o[17] = __shfl_xor(v, 16, 64) + __shfl_xor(v, 32, 64);
+  o[18] = xor_tree_sum<8>(v, lane);
+  w = v;
+  for (int m = 8; m >= 1; m >>= 1) w += __shfl_xor(w, m, 64);
+  o[19] = w;
+}
+
 }  // namespace llmc
 
 using namespace llmc;
 
 extern "C" {
+
+// in: float [nb * 64]; out: float [nb * 64 * 20] (pairs (helper, __shfl_xor form))
+int llmc_lane_exchange_check(const void* in, void* out, int nb, hipStream_t s) {
+  if (nb <= 0) return -1;
+  lane_exchange_check_kernel<<<nb, 64, 0, s>>>((const float*)in, (float*)out);
+  return static_cast<int>(hipGetLastError());
+}
 
 int llmc_rmsnorm(const void* x, const void* w, void* y, int T, int H, int x_stride, int y_stride, float eps,
                  hipStream_t s) {

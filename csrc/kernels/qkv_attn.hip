@@ -133,8 +133,8 @@ __device__ __forceinline__ void qa_attention(int c, int kvh, char* smem, const i
       const int d = g4 * (D / 4) + e;
       s += bf16_to_f32(qh[d]) * bf16_to_f32(kn[d]);
     }
-    s += __shfl_xor(s, 16, 64);
-    s += __shfl_xor(s, 32, 64);
+    s = xor16_add(s);
+    s = xor32_add(s);
     s *= scale_log2;
     const float m_new = fmaxf(st.m_run, s);
     const float alpha = exp2f(st.m_run - m_new), p = exp2f(s - m_new);

@@ -36,6 +36,19 @@ def _bf16(t: torch.Tensor, name: str) -> None:
 
 
 # ---------------------------------------------------------------------------------------------
+def lane_exchange_check(x: torch.Tensor) -> torch.Tensor:
+    """GPU self-test of the kernels' cross-lane helpers (csrc/kernels/common.h: v_permlane*_swap and
+    DPP forms of the wave reductions). ``x``: f32 [nb * 64] on the GPU; returns f32 [nb * 64, 10, 2]:
+    (helper, __shfl_xor form) pairs that must match bit for bit."""
+    if not x.is_cuda:
+        raise RuntimeError("lane_exchange_check: GPU only")
+    x = x.contiguous().float()
+    nb = x.numel() // 64
+    out = torch.empty(nb * 64, 10, 2, dtype=torch.float32, device=x.device)
+    kernels().lane_exchange_check(_p(x), _p(out), nb, _s(x))
+    return out
+
+
 def rmsnorm(x: torch.Tensor, w: torch.Tensor, eps: float, out: Optional[torch.Tensor] = None) -> torch.Tensor:
     if not x.is_cuda:
         r = oracle.rmsnorm(x, w, eps)

@@ -33,6 +33,21 @@ def _normed_exact(x, nw, eps=1e-5):
     return xf * torch.rsqrt(xf.pow(2).mean(-1, keepdim=True) + eps) * nw.cpu().float()
 
 
+def test_lane_exchange_helpers_match_shfl_xor(cuda):
+    """The kernels' wave reductions and lane exchanges (v_permlane16/32_swap, DPP row_ror / quad_perm
+    / bank-masked rotations in csrc/kernels/common.h) against the ds_bpermute (__shfl_xor) forms they
+    replace: the same association order, so every pair is bit-identical — including the +-0 and
+    equal-magnitude cases the random data hits."""
+    torch.manual_seed(5)
+    x = torch.randn(64 * 64, device="cuda") * 50
+    x[:2048:2] = -x[1:2048:2]  # exact cancellations in the first 32 waves
+    x[3::11] = 0.0
+    got = ops.lane_exchange_check(x).cpu()
+    a, b = got[..., 0], got[..., 1]
+    bad = (a.view(torch.int32) != b.view(torch.int32)).nonzero()
+    assert bad.numel() == 0, f"{bad.shape[0]} mismatches, first (lane, check): {bad[:5].tolist()}"
+
+
 def no_worse_than_oracle(got, ref, exact, slack=1e-2):
     """The MFMA decode form (3-16 rows) factorises the fused norm — bf16(x * w), scaled by 1/rms
     in f32 — where the oracle rounds bf16(x / rms * w): each is one bf16 rounding away from the

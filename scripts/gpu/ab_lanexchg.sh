@@ -4,7 +4,6 @@ L=llm_consensus_amd/_lib/_llmc_hip.cpython-310-x86_64-linux-gnu.so
 cp $L abso/new_llmc_hip.so
 run() {
   timeout -k 10 300 python -u scripts/tp_shard_decode.py --tp 1 --ctx 2048,9000 --tokens 256 | sed -u "s/^/$1 /" || return $?
-  timeout -k 10 300 python -u scripts/tp_shard_decode.py --model mixtral-8x7b --tp 1 --ctx 2048 --tokens 256 | sed -u "s/^/$1 /" || return $?
   timeout -k 10 300 python -u scripts/tp_shard_decode.py --model phi-3-mini --tp 1 --ctx 2048 --tokens 256 | sed -u "s/^/$1 /" || return $?
 }
 for v in new old new old; do

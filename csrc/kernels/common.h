@@ -91,14 +91,14 @@ __device__ __forceinline__ float fmax_raw(float a, float b) {  // no canonicalis
   asm("v_max_f32 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
   return r;
 }
-// The swap as inline asm with explicit wait states on both sides: the hipcc-scheduled builtin gave
-// intermittently wrong sums in the two-token-group MFMA GEMV (tests/test_kernels_gpu.py
-// test_linear_batched_decode_rows, M = 20 / 32), not in the isolated check
+// The swap as inline asm, with the 2 wait states the gfx950 hazard rule wants between a VALU write
+// of either operand and the swap inside the string (what hipcc emits for the builtin; the asm keeps
+// the instruction where the source puts it)
 __device__ __forceinline__ void permlane_swap16(uint32_t& a, uint32_t& b) {
-  asm volatile("s_nop 4\n\tv_permlane16_swap_b32 %0, %1\n\ts_nop 4" : "+v"(a), "+v"(b));
+  asm volatile("s_nop 1\n\tv_permlane16_swap_b32 %0, %1" : "+v"(a), "+v"(b));
 }
 __device__ __forceinline__ void permlane_swap32(uint32_t& a, uint32_t& b) {
-  asm volatile("s_nop 4\n\tv_permlane32_swap_b32 %0, %1\n\ts_nop 4" : "+v"(a), "+v"(b));
+  asm volatile("s_nop 1\n\tv_permlane32_swap_b32 %0, %1" : "+v"(a), "+v"(b));
 }
 __device__ __forceinline__ float xor32_add(float v) {
   uint32_t a = fbits(v), b = fbits(v);
